@@ -1,0 +1,282 @@
+/*
+ * amr_oracle.c -- CPU restatement of the reference demodulator hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker (and the timed CPU
+ * baseline, bench.py's cpu_baseline leg).  Only tests/, __graft_entry__.smoke()
+ * and bench.py may load it.  The product path (audio-modem-radio_amd/) never
+ * links or calls it.
+ *
+ * It restates, operation for operation, what the reference computes through
+ * numpy/scipy for one stream:
+ *
+ *   scipy.signal.filtfilt(b, a, x)  (padtype='odd', padlen=3*ntaps)
+ *     used at modem.py:77,88 (BPSK), modem.py:198,204 (QPSK), modem.py:308 (FSK).
+ *     scipy 1.15.3 _signaltools.py filtfilt: odd_ext (_arraytools.py:99-106),
+ *     zi = lfilter_zi * ext[0], forward lfilter, zi * y[-1], reverse lfilter.
+ *     lfilter's direct-form-II-transposed inner loop, in scipy's order
+ *     (no FMA):  y = z0 + b0*x;  z[i] = (z[i+1] + x*b[i+1]) - y*a[i+1];
+ *                z[last] = x*b[last] - y*a[last].
+ *     The odd extension is evaluated in the INPUT's precision (numpy keeps a
+ *     float32 array float32 in `2*x[0] - x[k]`), then promoted to double.
+ *   mixer  filtered * exp(-1j*2*pi*fc*t)   modem.py:80-83, 200-201
+ *     (the LO table comes from the caller, evaluated with numpy's own exp).
+ *   symbol pick baseband[first::sps]        modem.py:92-93 (BPSK first=sps),
+ *                                           modem.py:209   (QPSK first=sps//2)
+ *   differential product s[1:]*conj(s[:-1])  modem.py:100, 214
+ *     numpy 2.2 on AVX-512/FMA3 x86 evaluates complex multiply as
+ *       re = fma(ar, br, -(ai*bi)),  im = fma(ar, bi, ai*br)
+ *     (measured bit for bit in this container);
+ *     restated here with the C99 fma().
+ *   QPSK slicer   modem.py:216-241   atan2, +2pi if negative, 4 sectors
+ *   BPSK slicer   modem.py:102-105   real(diff) < 0 -> 1
+ *   sync + pack   modem.py:111-135 (BPSK), 243-266 (QPSK), 326-341 (FSK)
+ *     first index of "0100011001000010" at any bit offset; pack MSB first
+ *     from there (or from 0 when absent); floor(L/8) bytes.
+ *   FEC decode    fec.py:34-69  parity-XOR triples + CRC32 (zlib polynomial)
+ *
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off; no -ffast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define AMR_DT_F32 0
+#define AMR_DT_F64 1
+#define AMR_DT_I16 2
+
+/* ---- lfilter (DF-II-T) ----------------------------------------------------
+ * scipy/signal lfilter inner loop, real double case.  x and y may alias.   */
+static void df2t(const double *b, const double *a, int nt, double *z,
+                 const double *x, double *y, int64_t n, int64_t step)
+{
+    for (int64_t k = 0; k < n; ++k) {
+        const double xn = x[k * step];
+        const double yn = z[0] + b[0] * xn;
+        for (int i = 0; i < nt - 2; ++i)
+            z[i] = z[i + 1] + xn * b[i + 1] - yn * a[i + 1];
+        z[nt - 2] = xn * b[nt - 1] - yn * a[nt - 1];
+        y[k * step] = yn;
+    }
+}
+
+static double load_x(const void *x, int dtype, int64_t i)
+{
+    if (dtype == AMR_DT_F32) return (double)((const float *)x)[i];
+    if (dtype == AMR_DT_I16) return (double)((const int16_t *)x)[i] / 32768.0;
+    return ((const double *)x)[i];
+}
+
+/* odd extension sample j of the padded sequence (0 <= j < n + 2*pad),
+ * evaluated in the input's own precision as numpy does (_arraytools.py:103). */
+static double ext_sample(const void *x, int dtype, int64_t n, int pad, int64_t j)
+{
+    if (j >= pad && j < pad + n) return load_x(x, dtype, j - pad);
+    if (dtype == AMR_DT_F32) {
+        const float *xf = (const float *)x;
+        if (j < pad) return (double)(2.0f * xf[0] - xf[pad - j]);
+        return (double)(2.0f * xf[n - 1] - xf[n - 2 - (j - pad - n)]);
+    }
+    /* f64 and i16 (decode_wav_file hands the demod float64 = i16/32768) */
+    if (j < pad) return 2.0 * load_x(x, dtype, 0) - load_x(x, dtype, pad - j);
+    return 2.0 * load_x(x, dtype, n - 1) - load_x(x, dtype, n - 2 - (j - pad - n));
+}
+
+/* scipy.signal.filtfilt(b, a, x) with default odd padding, padlen = 3*nt.
+ * work: 2*(n + 2*pad) doubles.  out: n doubles.  Returns -1 if n <= pad. */
+int oracle_filtfilt(const double *b, const double *a, int nt, const double *zi,
+                    const void *x, int dtype, int64_t n, double *out, double *work)
+{
+    const int pad = 3 * nt;
+    if (n <= pad) return -1;
+    const int64_t m = n + 2 * (int64_t)pad;
+    double z[32];
+    double *ext = work;
+    for (int64_t j = 0; j < m; ++j) ext[j] = ext_sample(x, dtype, n, pad, j);
+    for (int i = 0; i < nt - 1; ++i) z[i] = zi[i] * ext[0];
+    df2t(b, a, nt, z, ext, ext, m, 1);                 /* forward, in place */
+    for (int i = 0; i < nt - 1; ++i) z[i] = zi[i] * ext[m - 1];
+    df2t(b, a, nt, z, ext + m - 1, ext + m - 1, m, -1); /* backward over reversed */
+    for (int64_t i = 0; i < n; ++i) out[i] = ext[pad + i];
+    return 0;
+}
+
+/* Same, on a complex sequence given as separate re/im planes (the complex
+ * lfilter with real coefficients is two independent real recurrences). */
+static int filtfilt_complex(const double *b, const double *a, int nt, const double *zi,
+                            double *re, double *im, int64_t n, double *work)
+{
+    int rc = oracle_filtfilt(b, a, nt, zi, re, AMR_DT_F64, n, re, work);
+    if (rc) return rc;
+    return oracle_filtfilt(b, a, nt, zi, im, AMR_DT_F64, n, im, work);
+}
+
+/* ---- sync + pack (modem.py:244-264) -------------------------------------- */
+static const uint8_t SYNC16[16] = {0,1,0,0,0,1,1,0, 0,1,0,0,0,0,1,0};   /* "FB" */
+
+int64_t oracle_find_sync(const uint8_t *bits, int64_t L)
+{
+    for (int64_t p = 0; p + 16 <= L; ++p) {
+        int k = 0;
+        while (k < 16 && bits[p + k] == SYNC16[k]) ++k;
+        if (k == 16) return p;
+    }
+    return -1;
+}
+
+int64_t oracle_pack(const uint8_t *bits, int64_t L, int64_t start, uint8_t *out)
+{
+    int64_t nb = (L - start) / 8;
+    if (nb < 0) nb = 0;
+    for (int64_t j = 0; j < nb; ++j) {
+        uint8_t v = 0;
+        for (int k = 0; k < 8; ++k) v = (uint8_t)((v << 1) | bits[start + 8 * j + k]);
+        out[j] = v;
+    }
+    return nb;
+}
+
+/* ---- DPSK demod (QPSK modem.py:189-266, BPSK modem.py:68-135) ---------------
+ * kind 0 = DQPSK slicer, 1 = DBPSK slicer.  first = index of the first symbol
+ * sample (QPSK sps/2, BPSK sps).  lo: 2*n doubles (re, im interleaved).
+ * out must hold (2*n/sps)/8 + 1 bytes.  Returns the byte count, or
+ * -1 (n <= BP padlen) / -2 (n <= LP padlen).  *sync_out = sync index or -1. */
+int64_t oracle_psk_demod(int kind, const void *x, int dtype, int64_t n,
+                         int64_t sps, int64_t first,
+                         const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                         const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                         const double *lo, uint8_t *out, int64_t *sync_out)
+{
+    *sync_out = -1;
+    int64_t m = n + 2 * 3 * (int64_t)(bp_nt > lp_nt ? bp_nt : lp_nt);
+    double *filt = (double *)malloc(sizeof(double) * n);
+    double *re = (double *)malloc(sizeof(double) * n);
+    double *im = (double *)malloc(sizeof(double) * n);
+    double *work = (double *)malloc(sizeof(double) * 2 * m);
+    int64_t result = 0;
+    uint8_t *bits = NULL;
+    if (oracle_filtfilt(bp_b, bp_a, bp_nt, bp_zi, x, dtype, n, filt, work)) { result = -1; goto done; }
+    for (int64_t i = 0; i < n; ++i) {               /* modem.py:200-201 real*complex */
+        re[i] = filt[i] * lo[2 * i];
+        im[i] = filt[i] * lo[2 * i + 1];
+    }
+    if (filtfilt_complex(lp_b, lp_a, lp_nt, lp_zi, re, im, n, work)) { result = -2; goto done; }
+    {
+        int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
+        if (S < 2) { result = 0; goto done; }        /* modem.py:95-96, 211 */
+        int bps = (kind == 0) ? 2 : 1;
+        int64_t L = (S - 1) * bps;
+        bits = (uint8_t *)malloc((size_t)L + 16);
+        for (int64_t k = 0; k + 1 < S; ++k) {
+            const double ar = re[first + (k + 1) * sps], ai = im[first + (k + 1) * sps];
+            const double br = re[first + k * sps], bi = -im[first + k * sps];   /* conj */
+            const double dr = fma(ar, br, -(ai * bi));
+            if (kind == 1) {
+                bits[k] = (dr < 0) ? 1 : 0;              /* modem.py:103-105 */
+                continue;
+            }
+            const double di = fma(ar, bi, ai * br);
+            double ang = atan2(di, dr);                  /* np.angle, modem.py:219 */
+            if (ang < 0) ang += 2 * M_PI;                /* modem.py:232 */
+            uint8_t h, l;
+            if (ang < M_PI / 4 || ang > 7 * M_PI / 4) { h = 0; l = 0; }
+            else if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) { h = 0; l = 1; }
+            else if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) { h = 1; l = 1; }
+            else { h = 1; l = 0; }
+            bits[2 * k] = h;
+            bits[2 * k + 1] = l;
+        }
+        int64_t s = oracle_find_sync(bits, L);
+        *sync_out = s;
+        result = oracle_pack(bits, L, s < 0 ? 0 : s, out);
+    }
+done:
+    free(filt); free(re); free(im); free(work); free(bits);
+    return result;
+}
+
+/* Batch driver (the CPU baseline): streams are independent; parallelised with
+ * OpenMP across streams when built with -fopenmp. */
+int64_t oracle_psk_demod_batch(int kind, const void *x, int dtype, int64_t n_streams, int64_t n,
+                               int64_t x_stride, int64_t sps, int64_t first,
+                               const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                               const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                               const double *lo, uint8_t *out, int64_t out_stride,
+                               int64_t *out_len, int64_t *sync_idx, int n_threads)
+{
+    const size_t esz = dtype == AMR_DT_F32 ? 4 : dtype == AMR_DT_I16 ? 2 : 8;
+    int64_t worst = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(min:worst)
+#endif
+    for (int64_t s = 0; s < n_streams; ++s) {
+        const void *xs = (const char *)x + (size_t)s * (size_t)x_stride * esz;
+        int64_t r = oracle_psk_demod(kind, xs, dtype, n, sps, first, bp_b, bp_a, bp_nt, bp_zi,
+                                     lp_b, lp_a, lp_nt, lp_zi, lo, out + s * out_stride, &sync_idx[s]);
+        out_len[s] = r;
+        if (r < worst) worst = r;
+    }
+    (void)n_threads;
+    return worst;
+}
+
+/* ---- FSK decision stage (modem.py:315-341) ----------------------------------
+ * Given the two envelopes, reproduce the per-sample compare, the windowed
+ * majority vote and sync+pack.  Returns the byte count. */
+int64_t oracle_fsk_decide(const double *mark_env, const double *space_env, int64_t n,
+                          int64_t sps, uint8_t *out, int64_t *sync_out)
+{
+    int64_t half = sps / 2, q = sps / 4;
+    int64_t nb = 0;
+    uint8_t *dec = (uint8_t *)malloc((size_t)(n / (sps > 0 ? sps : 1) + 2));
+    for (int64_t i = half; i < n; i += sps) {
+        int64_t lo = i - q, hi = i + q < n ? i + q : n;
+        if (hi - lo <= 0) continue;                      /* len(chunk) > 0 */
+        int64_t ones = 0;
+        for (int64_t j = lo; j < hi; ++j) ones += mark_env[j] > space_env[j];
+        dec[nb++] = (2 * ones > hi - lo) ? 1 : 0;        /* np.mean(chunk) > 0.5 */
+    }
+    int64_t s = oracle_find_sync(dec, nb);
+    *sync_out = s;
+    int64_t r = oracle_pack(dec, nb, s < 0 ? 0 : s, out);
+    free(dec);
+    return r;
+}
+
+/* ---- FEC (fec.py:11-69) ------------------------------------------------------ */
+uint32_t oracle_crc32(const uint8_t *p, int64_t n)
+{
+    uint32_t c = 0xFFFFFFFFu;
+    for (int64_t i = 0; i < n; ++i) {
+        c ^= p[i];
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    }
+    return c ^ 0xFFFFFFFFu;
+}
+
+/* Returns decoded length; *crc_ok = 1 when the recomputed CRC32 matches the
+ * trailing little-endian word (the reference only prints on mismatch). */
+int64_t oracle_fec_decode(const uint8_t *in, int64_t n, uint8_t *out, int *crc_ok)
+{
+    if (n < 4) {                                   /* fec.py:36-37: returned as is */
+        memcpy(out, in, (size_t)n);
+        *crc_ok = 1;
+        return n;
+    }
+    const uint32_t want = (uint32_t)in[n - 4] | ((uint32_t)in[n - 3] << 8) |
+                          ((uint32_t)in[n - 2] << 16) | ((uint32_t)in[n - 1] << 24);
+    const int64_t m = n - 4;
+    int64_t o = 0, i = 0;
+    while (i < m) {
+        if (i + 2 < m) {
+            const uint8_t b1 = in[i], b2 = in[i + 1], p = in[i + 2];
+            out[o++] = b1;
+            out[o++] = ((b1 ^ b2) == p) ? b2 : 0x3F;
+            i += 3;
+        } else {
+            out[o++] = in[i++];
+        }
+    }
+    *crc_ok = oracle_crc32(out, o) == want;
+    return o;
+}
