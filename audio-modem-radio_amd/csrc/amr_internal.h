@@ -1,0 +1,63 @@
+// amr_internal.h -- shared between the HIP kernels and the C-ABI runtime.
+//
+// Work decomposition:
+//   * a "group" is 64 consecutive streams; one wave64 owns a group in the
+//     band-pass kernel (lane = stream) and two waves own it in the low-pass
+//     kernels (lane = stream x {re, im}).
+//   * every intermediate lives in HBM TIME-MAJOR inside its group, so the 64
+//     lanes of a wave touch one contiguous 512 B / 1 KiB row per sample step.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace amr {
+
+constexpr int kWave = 64;
+constexpr int kMaxTaps = 16;
+
+enum DType : int { kF32 = 0, kF64 = 1, kI16 = 2 };
+enum PskKind : int { kQpsk = 0, kBpsk = 1 };
+
+// One IIR section as scipy.signal.lfilter sees it (a[0] == 1).
+struct Iir {
+  int nt;                 // taps (order + 1)
+  double b[kMaxTaps];
+  double a[kMaxTaps];
+  double zi[kMaxTaps];    // scipy.signal.lfilter_zi(b, a)
+};
+
+// Everything a PSK launch needs besides the buffers.  Passed by value as a
+// kernel argument, so the coefficients arrive in SGPRs.
+struct PskParams {
+  int64_t n;              // samples per stream
+  int64_t m1;             // n + 2*pad1 (band-pass extended length)
+  int64_t m2;             // n + 2*pad2 (low-pass extended length)
+  int64_t sps;            // samples per symbol
+  int64_t first;          // index of the first symbol sample
+  int64_t n_sym;          // S = len(baseband[first::sps])
+  int64_t n_bits;         // L = (S-1) * bits_per_symbol   (0 when S < 2)
+  int64_t n_words;        // 32-bit words per stream in the bit buffer
+  int pad1, pad2;
+  int kind;               // PskKind
+  int bp_zero_odd;        // 1: b[1], b[3], ... are all +0.0 (band-pass symmetry)
+};
+
+// Pointers of one batch launch (device memory).
+struct PskBuffers {
+  const void* x;          // [B][x_stride] input samples
+  int64_t x_stride;       // elements
+  int dtype;
+  int64_t n_streams;      // B
+  const double* lo;       // [n][4]: (lo_re, lo_im, -(0*lo_im), 0*lo_re)
+  double* s1;             // band-pass forward output  [G][m1p/2][64][2]
+  double* s2;             // mixer output (baseband)   [G][n][64][2]
+  double* s3;             // low-pass forward output   [2G][m2p/2][64][2]
+  uint32_t* words;        // [B][n_words] bit buffer, MSB first
+  int32_t* flags;         // [B] 1 => take the exact complex low-pass path
+  uint8_t* out;           // [B][out_stride] packed bytes
+  int64_t out_stride;
+  int64_t* out_len;       // [B]
+  int64_t* sync_idx;      // [B]
+};
+
+}  // namespace amr

@@ -1,0 +1,590 @@
+// api.cpp -- the C ABI of libamr.so (include/amr.h): plans, HBM scratch,
+// launches, timing and the RCCL gather.  Host code; compiled by hipcc.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/amr.h"
+#include "amr_internal.h"
+
+namespace amr {
+hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_lowpass_fwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_lowpass_bwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_lowpass_exact(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
+                            hipStream_t);
+hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, uint8_t*, int64_t, int64_t*,
+                             int32_t*, const uint32_t*, const uint32_t*, hipStream_t);
+}  // namespace amr
+
+using namespace amr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(e_ == hipErrorOutOfMemory ? AMR_E_NOMEM : AMR_E_HIP,                             \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                             \
+  } while (0)
+
+// CRC32 tables for the FEC kernel (uploaded once per device)
+struct CrcTables {
+  uint32_t table[256];
+  uint32_t x2n[32];
+  CrcTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+      table[i] = c;
+    }
+    auto mul = [](uint32_t a, uint32_t b) {
+      uint32_t m = 1u << 31, p = 0;
+      for (int i = 0; i < 32; ++i) {
+        if (a & m) p ^= b;
+        m >>= 1;
+        b = (b & 1) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+      }
+      return p;
+    };
+    uint32_t p = 1u << 30;  // x^1
+    x2n[0] = p;
+    for (int n = 1; n < 32; ++n) x2n[n] = p = mul(p, p);
+  }
+};
+
+struct DeviceCrc {
+  uint32_t* d = nullptr;  // [256 table][32 x2n]
+};
+std::mutex g_crc_mu;
+DeviceCrc g_crc[64];
+
+int device_crc(int dev, const uint32_t** table, const uint32_t** x2n) {
+  std::lock_guard<std::mutex> lk(g_crc_mu);
+  if (dev < 0 || dev >= 64) return fail(AMR_E_INVALID, "device ordinal out of range");
+  if (!g_crc[dev].d) {
+    static const CrcTables t;
+    uint32_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, sizeof(uint32_t) * 288));
+    HIP_TRY(hipMemcpy(p, t.table, sizeof(t.table), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(p + 256, t.x2n, sizeof(t.x2n), hipMemcpyHostToDevice));
+    g_crc[dev].d = p;
+  }
+  *table = g_crc[dev].d;
+  *x2n = g_crc[dev].d + 256;
+  return AMR_OK;
+}
+
+int64_t dtype_size(int dtype) {
+  switch (dtype) {
+    case AMR_DTYPE_F32: return 4;
+    case AMR_DTYPE_F64: return 8;
+    case AMR_DTYPE_I16: return 2;
+  }
+  return 0;
+}
+
+bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }
+
+}  // namespace
+
+struct amr_psk_plan {
+  std::mutex mu;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  PskParams p{};
+  Iir bp{}, lp{};
+  bool lp_exact_only = false;   // low-pass coefficients outside the separable proof
+  int64_t max_streams = 0, groups = 0;
+  int64_t m1_pairs = 0, m2_pairs = 0;
+  int64_t out_cap = 0;
+  // HBM scratch
+  double* lo = nullptr;
+  double* s1 = nullptr;
+  double* s2 = nullptr;
+  double* s3 = nullptr;
+  uint32_t* words = nullptr;
+  int32_t* flags = nullptr;
+  int64_t scratch_bytes = 0;
+  // staging for the host API (lazily sized)
+  void* d_x = nullptr;
+  int64_t d_x_bytes = 0;
+  uint8_t* d_out = nullptr;
+  int64_t* d_len = nullptr;
+  int64_t* d_sync = nullptr;
+  uint8_t* d_fec = nullptr;   // FEC host API staging
+  int64_t* d_fec_len = nullptr;
+  int32_t* d_crc = nullptr;
+  // timing
+  bool timing = false;
+  hipEvent_t ev[AMR_T_COUNT + 1][2]{};
+  bool ev_used[AMR_T_COUNT]{};
+  int64_t last_exact = 0;
+};
+
+struct amr_comm {
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  int device = 0;
+};
+
+extern "C" {
+
+int amr_abi_version(void) { return AMR_ABI_VERSION; }
+const char* amr_last_error(void) { return g_err.c_str(); }
+
+int amr_device_count(int* count) {
+  if (!count) return fail(AMR_E_INVALID, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(AMR_E_NODEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return AMR_OK;
+}
+
+int amr_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return AMR_OK;
+}
+int amr_malloc(void** dptr, int64_t bytes) {
+  if (!dptr || bytes < 0) return fail(AMR_E_INVALID, "amr_malloc: bad argument");
+  HIP_TRY(hipMalloc(dptr, (size_t)(bytes > 0 ? bytes : 1)));
+  return AMR_OK;
+}
+int amr_free(void* dptr) {
+  HIP_TRY(hipFree(dptr));
+  return AMR_OK;
+}
+int amr_memcpy_h2d(void* dst, const void* src, int64_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+  return AMR_OK;
+}
+int amr_memcpy_d2h(void* dst, const void* src, int64_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+  return AMR_OK;
+}
+int amr_memcpy_d2d(void* dst, const void* src, int64_t bytes) {
+  HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice));
+  return AMR_OK;
+}
+int amr_device_synchronize(void) {
+  HIP_TRY(hipDeviceSynchronize());
+  return AMR_OK;
+}
+
+static void plan_free(amr_psk_plan* pl) {
+  if (!pl) return;
+  (void)hipSetDevice(pl->device);
+  if (pl->stream) (void)hipStreamSynchronize(pl->stream);
+  for (auto* p : {(void*)pl->lo, (void*)pl->s1, (void*)pl->s2, (void*)pl->s3, (void*)pl->words, (void*)pl->flags,
+                  pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
+                  (void*)pl->d_fec_len, (void*)pl->d_crc})
+    if (p) (void)hipFree(p);
+  for (auto& e : pl->ev)
+    for (auto& h : e)
+      if (h) (void)hipEventDestroy(h);
+  if (pl->stream) (void)hipStreamDestroy(pl->stream);
+  delete pl;
+}
+
+int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int64_t sps, int64_t first,
+                        const double* bp_b, const double* bp_a, const double* bp_zi, int bp_nt,
+                        const double* lp_b, const double* lp_a, const double* lp_zi, int lp_nt,
+                        const double* lo4, int64_t max_streams) {
+  if (!out || !bp_b || !bp_a || !bp_zi || !lp_b || !lp_a || !lp_zi || !lo4)
+    return fail(AMR_E_INVALID, "amr_psk_plan_create: NULL argument");
+  *out = nullptr;
+  if (kind != AMR_PSK_QPSK && kind != AMR_PSK_BPSK) return fail(AMR_E_INVALID, "unknown PSK kind");
+  if (sps < 1 || first < 0 || max_streams < 1) return fail(AMR_E_INVALID, "bad sps/first/max_streams");
+  if (bp_nt != 9 && bp_nt != 7) return fail(AMR_E_INVALID, "band-pass must have 7 or 9 taps");
+  if (lp_nt != 5) return fail(AMR_E_INVALID, "low-pass must have 5 taps");
+  if (bp_a[0] != 1.0 || lp_a[0] != 1.0) return fail(AMR_E_INVALID, "a[0] must be 1 (scipy butter form)");
+  if (n <= 3 * bp_nt || n <= 3 * lp_nt)
+    return fail(AMR_E_PADLEN, "The length of the input vector x must be greater than padlen, which is " +
+                                  std::to_string(3 * (n <= 3 * bp_nt ? bp_nt : lp_nt)) + ".");
+  auto* pl = new amr_psk_plan();
+  pl->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    delete pl;
+    return fail(AMR_E_NODEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  }
+  PskParams& p = pl->p;
+  p.n = n;
+  p.pad1 = 3 * bp_nt;
+  p.pad2 = 3 * lp_nt;
+  p.m1 = n + 2 * p.pad1;
+  p.m2 = n + 2 * p.pad2;
+  p.sps = sps;
+  p.first = first;
+  p.kind = kind;
+  p.n_sym = n > first ? (n - first + sps - 1) / sps : 0;
+  const int bps = kind == AMR_PSK_QPSK ? 2 : 1;
+  p.n_bits = p.n_sym >= 2 ? (p.n_sym - 1) * bps : 0;
+  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
+  bool zodd = true;
+  for (int i = 1; i < bp_nt; i += 2) zodd = zodd && is_pos_zero(bp_b[i]);
+  p.bp_zero_odd = zodd ? 1 : 0;
+  pl->bp.nt = bp_nt;
+  pl->lp.nt = lp_nt;
+  for (int i = 0; i < bp_nt; ++i) { pl->bp.b[i] = bp_b[i]; pl->bp.a[i] = bp_a[i]; }
+  for (int i = 0; i < bp_nt - 1; ++i) pl->bp.zi[i] = bp_zi[i];
+  for (int i = 0; i < lp_nt; ++i) { pl->lp.b[i] = lp_b[i]; pl->lp.a[i] = lp_a[i]; }
+  for (int i = 0; i < lp_nt - 1; ++i) pl->lp.zi[i] = lp_zi[i];
+  // separable low-pass proof needs b > 0 normal and zi, a normal non-zero
+  for (int i = 0; i < lp_nt; ++i) {
+    if (!(lp_b[i] > 0.0 && std::isnormal(lp_b[i]) && lp_b[i] >= 0x1p-50)) pl->lp_exact_only = true;
+    if (i > 0 && !std::isnormal(lp_a[i])) pl->lp_exact_only = true;
+  }
+  for (int i = 0; i < lp_nt - 1; ++i)
+    if (!std::isnormal(lp_zi[i])) pl->lp_exact_only = true;
+  // test hook: route every stream through the exact complex low-pass kernel
+  if (const char* f = std::getenv("AMR_FORCE_EXACT_LOWPASS"))
+    if (f[0] == '1') pl->lp_exact_only = true;
+
+  pl->max_streams = max_streams;
+  pl->groups = (max_streams + kWave - 1) / kWave;
+  const int qs1 = p.pad1 & 1, qs2 = p.pad2 & 1;
+  pl->m1_pairs = (p.m1 + qs1 + 1) >> 1;
+  pl->m2_pairs = (p.m2 + qs2 + 1) >> 1;
+  pl->out_cap = p.n_bits / 8 + 1;
+  const int64_t g = pl->groups;
+  struct A { void** ptr; int64_t bytes; };
+  const A allocs[] = {
+      {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
+      {(void**)&pl->s1, g * pl->m1_pairs * kWave * 16},
+      {(void**)&pl->s2, g * n * kWave * 16},
+      {(void**)&pl->s3, 2 * g * pl->m2_pairs * kWave * 16},
+      {(void**)&pl->words, g * kWave * p.n_words * 4},
+      {(void**)&pl->flags, g * kWave * 4},
+  };
+  for (const A& a : allocs) {
+    e = hipMalloc(a.ptr, (size_t)a.bytes);
+    if (e != hipSuccess) {
+      plan_free(pl);
+      return fail(AMR_E_NOMEM, "hipMalloc(" + std::to_string(a.bytes) + " B): " + hipGetErrorString(e));
+    }
+    pl->scratch_bytes += a.bytes;
+  }
+  e = hipMemcpy(pl->lo, lo4, (size_t)(n * 4 * sizeof(double)), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    plan_free(pl);
+    return fail(AMR_E_HIP, std::string("plan setup: ") + hipGetErrorString(e));
+  }
+  *out = pl;
+  return AMR_OK;
+}
+
+int amr_psk_plan_destroy(amr_psk_plan* plan) {
+  plan_free(plan);
+  return AMR_OK;
+}
+int64_t amr_psk_plan_out_capacity(const amr_psk_plan* plan) { return plan ? plan->out_cap : -1; }
+int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) { return plan ? plan->scratch_bytes : -1; }
+
+int amr_psk_plan_synchronize(amr_psk_plan* plan) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  HIP_TRY(hipSetDevice(plan->device));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  return AMR_OK;
+}
+
+int amr_psk_plan_enable_timing(amr_psk_plan* plan, int on) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (on && !plan->ev[0][0]) {
+    for (auto& e : plan->ev)
+      for (auto& h : e) HIP_TRY(hipEventCreate(&h));
+  }
+  plan->timing = on != 0;
+  return AMR_OK;
+}
+
+int amr_psk_plan_timings(amr_psk_plan* plan, float* ms, int count) {
+  if (!plan || !ms) return fail(AMR_E_INVALID, "NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  for (int i = 0; i < count && i < AMR_T_COUNT; ++i) {
+    ms[i] = -1.0f;
+    if (plan->timing && plan->ev_used[i]) HIP_TRY(hipEventElapsedTime(&ms[i], plan->ev[i][0], plan->ev[i][1]));
+  }
+  return AMR_OK;
+}
+
+int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
+  if (!plan || !count) return fail(AMR_E_INVALID, "NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  std::vector<int32_t> fl((size_t)plan->groups * kWave);
+  HIP_TRY(hipMemcpy(fl.data(), plan->flags, fl.size() * 4, hipMemcpyDeviceToHost));
+  int64_t c = 0;
+  for (int64_t i = 0; i < plan->last_exact; ++i) c += fl[(size_t)i] != 0;
+  *count = c;
+  return AMR_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Launch the whole PSK pipeline on plan->stream.  Caller holds plan->mu.
+int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, uint8_t* d_out,
+            int64_t out_stride, int64_t* d_len, int64_t* d_sync, uint8_t* d_fec, int64_t fec_stride,
+            int64_t* d_fec_len, int32_t* d_crc) {
+  if (B < 0 || B > pl->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (dtype_size(dtype) == 0) return fail(AMR_E_INVALID, "unknown dtype");
+  if (x_stride < pl->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < pl->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
+  for (bool& u : pl->ev_used) u = false;
+  pl->last_exact = B;
+  if (B == 0) return AMR_OK;
+  hipStream_t st = pl->stream;
+  PskBuffers b{};
+  b.x = d_x;
+  b.x_stride = x_stride;
+  b.dtype = dtype;
+  b.n_streams = B;
+  b.lo = pl->lo;
+  b.s1 = pl->s1;
+  b.s2 = pl->s2;
+  b.s3 = pl->s3;
+  b.words = pl->words;
+  b.flags = pl->flags;
+  b.out = d_out;
+  b.out_stride = out_stride;
+  b.out_len = d_len;
+  b.sync_idx = d_sync;
+  auto mark = [&](int slot, int which) -> hipError_t {
+    if (!pl->timing) return hipSuccess;
+    pl->ev_used[slot] = true;
+    return hipEventRecord(pl->ev[slot][which], st);
+  };
+  if (pl->p.n_sym < 2) {
+    // modem.py:95-96, 211: fewer than two symbols -> b''
+    HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
+    HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
+  } else {
+    HIP_TRY(mark(AMR_T_BANDPASS, 0));
+    HIP_TRY(launch_psk_bandpass(b, pl->p, pl->bp, st));
+    HIP_TRY(mark(AMR_T_BANDPASS, 1));
+    if (pl->lp_exact_only) {
+      // every stream takes the exact complex path
+      HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)pl->flags, 1, (size_t)B, st));
+    } else {
+      HIP_TRY(mark(AMR_T_LOWPASS_FWD, 0));
+      HIP_TRY(launch_psk_lowpass_fwd(b, pl->p, pl->lp, st));
+      HIP_TRY(mark(AMR_T_LOWPASS_FWD, 1));
+      HIP_TRY(mark(AMR_T_LOWPASS_BWD, 0));
+      HIP_TRY(launch_psk_lowpass_bwd(b, pl->p, pl->lp, st));
+      HIP_TRY(mark(AMR_T_LOWPASS_BWD, 1));
+    }
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 0));
+    HIP_TRY(launch_psk_lowpass_exact(b, pl->p, pl->lp, st));
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
+    HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
+  }
+  if (d_fec) {
+    const uint32_t *tab = nullptr, *x2n = nullptr;
+    int rc = device_crc(pl->device, &tab, &x2n);
+    if (rc) return rc;
+    HIP_TRY(mark(AMR_T_FEC, 0));
+    HIP_TRY(launch_fec_decode(d_out, out_stride, d_len, B, d_fec, fec_stride, d_fec_len, d_crc, tab, x2n, st));
+    HIP_TRY(mark(AMR_T_FEC, 1));
+  }
+  return AMR_OK;
+}
+
+int ensure(void** p, int64_t* have, int64_t need) {
+  if (*have >= need && *p) return AMR_OK;
+  if (*p) HIP_TRY(hipFree(*p));
+  *p = nullptr;
+  HIP_TRY(hipMalloc(p, (size_t)need));
+  *have = need;
+  return AMR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int amr_psk_demod_device(amr_psk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,
+                         uint8_t* d_out, int64_t out_stride, int64_t* d_out_len, int64_t* d_sync_idx) {
+  if (!plan || (!d_x && n_streams) || (!d_out && n_streams) || (!d_out_len && n_streams) ||
+      (!d_sync_idx && n_streams))
+    return fail(AMR_E_INVALID, "amr_psk_demod_device: NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  return run_psk(plan, d_x, dtype, n_streams, x_stride, d_out, out_stride, d_out_len, d_sync_idx, nullptr, 0,
+                 nullptr, nullptr);
+}
+
+int amr_psk_demod_fec_device(amr_psk_plan* plan, const void* d_x, int dtype, int64_t n_streams,
+                             int64_t x_stride, uint8_t* d_out, int64_t out_stride, int64_t* d_out_len,
+                             int64_t* d_sync_idx, uint8_t* d_fec, int64_t fec_stride, int64_t* d_fec_len,
+                             int32_t* d_crc_ok) {
+  if (!plan || !d_fec || !d_fec_len || !d_crc_ok) return fail(AMR_E_INVALID, "NULL argument");
+  if (fec_stride < out_stride) return fail(AMR_E_INVALID, "fec_stride < out_stride");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  return run_psk(plan, d_x, dtype, n_streams, x_stride, d_out, out_stride, d_out_len, d_sync_idx, d_fec,
+                 fec_stride, d_fec_len, d_crc_ok);
+}
+
+int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                       uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+  if (!plan || (B && (!x || !out || !out_len || !sync_idx)))
+    return fail(AMR_E_INVALID, "amr_psk_demod_host: NULL argument");
+  const int64_t es = dtype_size(dtype);
+  if (!es) return fail(AMR_E_INVALID, "unknown dtype");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (B == 0) return AMR_OK;
+  const int64_t n = plan->p.n;
+  const int64_t cap = plan->out_cap;
+  int rc = ensure(&plan->d_x, &plan->d_x_bytes, plan->max_streams * n * 8);
+  if (rc) return rc;
+  if (!plan->d_out) {
+    HIP_TRY(hipMalloc(&plan->d_out, (size_t)(plan->max_streams * cap)));
+    HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
+    HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
+  }
+  HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
+                           hipMemcpyHostToDevice, plan->stream));
+  rc = run_psk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync, nullptr, 0, nullptr,
+               nullptr);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpy2DAsync(out, (size_t)out_stride, plan->d_out, (size_t)cap,
+                           (size_t)(out_stride < cap ? out_stride : cap), (size_t)B, hipMemcpyDeviceToHost,
+                           plan->stream));
+  HIP_TRY(hipMemcpyAsync(out_len, plan->d_len, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  return AMR_OK;
+}
+
+int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_len, int64_t n, uint8_t* out,
+                        int64_t out_stride, int64_t* out_len, int32_t* crc_ok) {
+  if (n < 0 || (n && (!in || !in_len || !out || !out_len || !crc_ok)))
+    return fail(AMR_E_INVALID, "amr_fec_decode_host: NULL argument");
+  if (n == 0) return AMR_OK;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  const uint32_t *tab = nullptr, *x2n = nullptr;
+  int rc = device_crc(dev, &tab, &x2n);
+  if (rc) return rc;
+  int64_t maxlen = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (in_len[i] < 0 || in_len[i] > in_stride || in_len[i] > out_stride)
+      return fail(AMR_E_INVALID, "in_len out of range");
+    maxlen = in_len[i] > maxlen ? in_len[i] : maxlen;
+  }
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  int64_t *d_in_len = nullptr, *d_out_len = nullptr;
+  int32_t* d_crc = nullptr;
+  const int64_t stride = maxlen > 0 ? maxlen : 1;
+  hipError_t e = hipMalloc(&d_in, (size_t)(n * stride));
+  if (e == hipSuccess) e = hipMalloc(&d_out, (size_t)(n * stride));
+  if (e == hipSuccess) e = hipMalloc(&d_in_len, (size_t)n * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_out_len, (size_t)n * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_crc, (size_t)n * 4);
+  if (e == hipSuccess && maxlen > 0)
+    e = hipMemcpy2D(d_in, (size_t)stride, in, (size_t)in_stride, (size_t)maxlen, (size_t)n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_fec_decode(d_in, stride, d_in_len, n, d_out, stride, d_out_len, d_crc, tab, x2n, 0);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && maxlen > 0)
+    e = hipMemcpy2D(out, (size_t)out_stride, d_out, (size_t)stride, (size_t)maxlen, (size_t)n, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out_len, d_out_len, (size_t)n * 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(crc_ok, d_crc, (size_t)n * 4, hipMemcpyDeviceToHost);
+  for (void* p : {(void*)d_in, (void*)d_out, (void*)d_in_len, (void*)d_out_len, (void*)d_crc})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_fec_decode_host: ") + hipGetErrorString(e));
+  return AMR_OK;
+}
+
+// ---- RCCL -------------------------------------------------------------------
+int amr_comm_unique_id(uint8_t* id) {
+  if (!id) return fail(AMR_E_INVALID, "id is NULL");
+  static_assert(sizeof(ncclUniqueId) == AMR_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(id, &u, sizeof(u));
+  return AMR_OK;
+}
+
+int amr_comm_create(amr_comm** comm, const uint8_t* id, int nranks, int rank, int device) {
+  if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(AMR_E_INVALID, "bad comm args");
+  HIP_TRY(hipSetDevice(device));
+  auto* c = new amr_comm();
+  c->device = device;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(AMR_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    ncclCommDestroy(c->comm);
+    delete c;
+    return fail(AMR_E_HIP, "hipStreamCreate failed");
+  }
+  *comm = c;
+  return AMR_OK;
+}
+
+int amr_comm_destroy(amr_comm* comm) {
+  if (!comm) return AMR_OK;
+  (void)hipSetDevice(comm->device);
+  if (comm->stream) (void)hipStreamSynchronize(comm->stream);
+  if (comm->comm) ncclCommDestroy(comm->comm);
+  if (comm->stream) (void)hipStreamDestroy(comm->stream);
+  delete comm;
+  return AMR_OK;
+}
+
+int amr_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_psk_plan* plan) {
+  if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
+  HIP_TRY(hipSetDevice(comm->device));
+  hipStream_t st = plan ? plan->stream : comm->stream;
+  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, st);
+  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  return AMR_OK;
+}
+
+int amr_comm_synchronize(amr_comm* comm) {
+  if (!comm) return fail(AMR_E_INVALID, "comm is NULL");
+  HIP_TRY(hipSetDevice(comm->device));
+  HIP_TRY(hipStreamSynchronize(comm->stream));
+  return AMR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,193 @@
+// util_kernels.hip -- bit-level sync + byte pack, and the parity-XOR/CRC32 FEC
+// decode, for gfx950.  Integer work: one wave per stream, wave-level
+// reductions, no floating point.
+//
+//   k_sync_pack   replaces the tail of every reference demodulator:
+//                 bit_str.find("0100011001000010") + MSB-first byte packing
+//                 (modem.py:111-135 BPSK, 243-266 QPSK, 326-341 FSK)
+//   k_fec_decode  replaces fec.ReedSolomonFEC.decode (fec.py:34-69):
+//                 parity-XOR triples (b1, b2, b1^b2) -> b1, b2 or b1, '?'
+//                 plus a zlib CRC32 over the decoded bytes.
+#include "amr_internal.h"
+
+namespace amr {
+
+constexpr uint32_t kSync16 = 0x4642u;   // "0100011001000010" = "FB"
+
+__device__ __forceinline__ uint32_t word_at(const uint32_t* __restrict__ w, int64_t i, int64_t nw) {
+  return (i >= 0 && i < nw) ? w[i] : 0u;
+}
+
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int64_t o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// One wave per stream.  words: [B][n_words] MSB-first bits, n_bits valid.
+// mode_fsk: FSK packs from idx-or-0 exactly like PSK (modem.py:333), so one
+// kernel serves both.
+__global__ __launch_bounds__(64) void k_sync_pack(const uint32_t* __restrict__ words_all, int64_t n_words,
+                                                  int64_t n_bits, int64_t n_streams,
+                                                  uint8_t* __restrict__ out, int64_t out_stride,
+                                                  int64_t* __restrict__ out_len, int64_t* __restrict__ sync_idx) {
+  const int lane = threadIdx.x;
+  const int64_t s = blockIdx.x;
+  if (s >= n_streams) return;
+  const uint32_t* __restrict__ w = words_all + (size_t)s * n_words;
+  const int64_t L = n_bits;
+  const int64_t nw = (L + 31) >> 5;
+  constexpr int64_t kNone = 0x7fffffffffffffffLL;
+
+  // ---- find the first sync position p (bits p..p+15 == kSync16, p+16 <= L)
+  int64_t found = kNone;
+  for (int64_t base = 0; base < nw && found == kNone; base += kWave) {
+    const int64_t wi = base + lane;
+    int64_t mine = kNone;
+    if (wi < nw) {
+      const uint64_t win = ((uint64_t)word_at(w, wi, nw) << 32) | word_at(w, wi + 1, nw);
+      for (int q = 0; q < 32; ++q) {
+        const int64_t pos = wi * 32 + q;
+        if (pos + 16 > L) break;
+        if ((uint32_t)((win >> (48 - q)) & 0xFFFFu) == kSync16) { mine = pos; break; }
+      }
+    }
+    found = wave_min_i64(mine);
+  }
+  const int64_t start = (found == kNone) ? 0 : found;
+  const int64_t nbytes = (L - start) > 0 ? (L - start) >> 3 : 0;
+  if (lane == 0) {
+    out_len[s] = nbytes;
+    sync_idx[s] = (found == kNone) ? -1 : found;
+  }
+  // ---- pack: lane handles 4 output bytes per step
+  uint8_t* __restrict__ o = out + (size_t)s * out_stride;
+  for (int64_t jb = (int64_t)lane * 4; jb < nbytes; jb += 4 * kWave) {
+    const int64_t bo = start + jb * 8;
+    const int64_t wi = bo >> 5;
+    const int sh = (int)(bo & 31);
+    const uint64_t win = ((uint64_t)word_at(w, wi, nw) << 32) | word_at(w, wi + 1, nw);
+    const uint32_t v = (uint32_t)(win >> (32 - sh));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (jb + k < nbytes) o[jb + k] = (uint8_t)(v >> (24 - 8 * k));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CRC32 (zlib polynomial, reflected).  Per-lane table CRC over a chunk, then a
+// log2(64)-step tree combine with crc(A||B) = mulx8n(crc(A), |B|) ^ crc(B)
+// (zlib crc32_combine: multmodp / x2nmodp).
+constexpr uint32_t kPoly = 0xEDB88320u;
+
+__device__ __forceinline__ uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t m = 1u << 31, p = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (a & m) p ^= b;
+    m >>= 1;
+    b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
+  }
+  return p;
+}
+
+// x^(8*len) mod P using x^(2^k) powers (x2n[k] = x^(2^k) mod P)
+__device__ __forceinline__ uint32_t x8nmodp(int64_t len, const uint32_t* __restrict__ x2n) {
+  uint32_t p = 1u << 31;   // x^0
+  int k = 3;
+  while (len) {
+    if (len & 1) p = multmodp(x2n[k & 31], p);
+    len >>= 1;
+    ++k;
+  }
+  return p;
+}
+
+__global__ __launch_bounds__(64) void k_fec_decode(const uint8_t* __restrict__ in, int64_t in_stride,
+                                                   const int64_t* __restrict__ in_len, int64_t n_streams,
+                                                   uint8_t* __restrict__ out, int64_t out_stride,
+                                                   int64_t* __restrict__ out_len, int32_t* __restrict__ crc_ok,
+                                                   const uint32_t* __restrict__ crc_table,
+                                                   const uint32_t* __restrict__ x2n) {
+  __shared__ uint32_t tab[256];
+  __shared__ uint32_t xp[32];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 256; i += kWave) tab[i] = crc_table[i];
+  if (lane < 32) xp[lane] = x2n[lane];
+  __syncthreads();
+  const int64_t s = blockIdx.x;
+  if (s >= n_streams) return;
+  const uint8_t* __restrict__ src = in + (size_t)s * in_stride;
+  uint8_t* __restrict__ dst = out + (size_t)s * out_stride;
+  const int64_t n = in_len[s];
+  if (n < 4) {                                  // fec.py:36-37: returned unchanged
+    for (int64_t i = lane; i < n; i += kWave) dst[i] = src[i];
+    if (lane == 0) { out_len[s] = n; crc_ok[s] = 1; }
+    return;
+  }
+  const int64_t m = n - 4;
+  const int64_t nt = m / 3, rem = m % 3;        // full triples, copied tail (fec.py:46-62)
+  const int64_t dlen = 2 * nt + rem;
+  for (int64_t t = lane; t < nt; t += kWave) {
+    const uint8_t b1 = src[3 * t], b2 = src[3 * t + 1], p = src[3 * t + 2];
+    dst[2 * t] = b1;
+    dst[2 * t + 1] = ((uint8_t)(b1 ^ b2) == p) ? b2 : (uint8_t)0x3F;
+  }
+  if (lane < rem) dst[2 * nt + lane] = src[3 * nt + lane];
+  // CRC over the decoded bytes, recomputed from src (no read-back of dst):
+  // lane chunk [lo, hi) with c = ceil(dlen/64)
+  const int64_t c = (dlen + kWave - 1) / kWave;
+  const int64_t lo = (int64_t)lane * c;
+  const int64_t hi = lo + c < dlen ? lo + c : dlen;
+  uint32_t crc = 0xFFFFFFFFu;
+  for (int64_t i = lo; i < hi; ++i) {
+    uint8_t v;
+    if (i < 2 * nt) {
+      const int64_t t = i >> 1;
+      const uint8_t b1 = src[3 * t];
+      if ((i & 1) == 0) v = b1;
+      else { const uint8_t b2 = src[3 * t + 1]; v = ((uint8_t)(b1 ^ b2) == src[3 * t + 2]) ? b2 : (uint8_t)0x3F; }
+    } else {
+      v = src[3 * nt + (i - 2 * nt)];
+    }
+    crc = tab[(crc ^ v) & 0xFF] ^ (crc >> 8);
+  }
+  crc ^= 0xFFFFFFFFu;                           // zlib crc32 of this chunk
+  int64_t len = hi > lo ? hi - lo : 0;
+  // tree combine: after step d, lane (multiple of 2d) holds crc of lanes [lane, lane+2d)
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t rc = __shfl_down(crc, d);
+    const int64_t rl = __shfl_down(len, d);
+    if ((lane & (2 * d - 1)) == 0) {
+      crc = multmodp(x8nmodp(rl, xp), crc) ^ rc;
+      len += rl;
+    }
+  }
+  if (lane == 0) {
+    const uint32_t want = (uint32_t)src[n - 4] | ((uint32_t)src[n - 3] << 8) |
+                          ((uint32_t)src[n - 2] << 16) | ((uint32_t)src[n - 1] << 24);
+    out_len[s] = dlen;
+    crc_ok[s] = (crc == want) ? 1 : 0;
+  }
+}
+
+hipError_t launch_sync_pack(const uint32_t* words, int64_t n_words, int64_t n_bits, int64_t n_streams,
+                            uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_sync_pack, dim3((unsigned)n_streams), dim3(kWave), 0, st, words, n_words, n_bits,
+                     n_streams, out, out_stride, out_len, sync_idx);
+  return hipGetLastError();
+}
+
+hipError_t launch_fec_decode(const uint8_t* in, int64_t in_stride, const int64_t* in_len, int64_t n_streams,
+                             uint8_t* out, int64_t out_stride, int64_t* out_len, int32_t* crc_ok,
+                             const uint32_t* crc_table, const uint32_t* x2n, hipStream_t st) {
+  hipLaunchKernelGGL(k_fec_decode, dim3((unsigned)n_streams), dim3(kWave), 0, st, in, in_stride, in_len,
+                     n_streams, out, out_stride, out_len, crc_ok, crc_table, x2n);
+  return hipGetLastError();
+}
+
+}  // namespace amr

@@ -1,0 +1,152 @@
+/*
+ * amr.h -- C ABI of libamr.so, the MI355X (gfx950) batched demodulator core.
+ *
+ * Plain C: pointers, sizes and status codes only.  Host-side callers are the
+ * drop-in Python modules in audio-modem-radio_amd/ (ctypes; INTEGRATION.md
+ * shows the binding) and bench.py.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to szumanski/Audio-Modem-Radio):
+ *
+ *   amr_psk_plan_create     the per-call filter/LO setup inside
+ *                           modem.qpsk_demodulate   modem.py:191-204
+ *                           modem.bpsk_demodulate   modem.py:70-88
+ *                           (the host designs b/a/zi with scipy exactly like
+ *                            the reference and hands them over; the LO table
+ *                            is numpy's exp(-1j*2*pi*fc*t), modem.py:82,201)
+ *   amr_psk_demod_host      modem.qpsk_demodulate(samples, baud, carrier, fs)
+ *                           modem.py:189-266 (also psk8_demodulate modem.py:348,
+ *                           ofdm_demodulate_simple modem.py:375-376, and the
+ *                           decoder dispatch decoder.py:422-434) and
+ *                           modem.bpsk_demodulate modem.py:68-135 -- for a whole
+ *                           batch of equal-length streams per call
+ *   amr_psk_demod_device    the same with the batch already resident in HBM
+ *   amr_psk_demod_fec_device  8PSK alias + fec.ReedSolomonFEC.decode fused
+ *                           (modem.py:348 then fec.py:34-69; BASELINE config 5)
+ *   amr_fec_decode_host     fec.ReedSolomonFEC.decode  fec.py:34-69, batched
+ *   amr_allgather           the gather of decoded bytes across GPUs (RCCL)
+ *
+ * Status: every function returns AMR_OK (0) or a negative AMR_E_* code;
+ * amr_last_error() gives the message of the calling thread's last failure.
+ * Ownership: host buffers are borrowed for the duration of a synchronous
+ * call; device buffers passed to *_device calls must stay valid until the
+ * plan's stream is synchronised (amr_psk_plan_synchronize).  A plan owns its
+ * device scratch; calls on one plan are serialised by a per-plan mutex, so
+ * two host threads may share a plan (the reference decodes from a capture
+ * QThread and the GUI thread, filebeep_advanced_v2.py:324,1112).
+ */
+#ifndef AMR_H
+#define AMR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMR_ABI_VERSION 1
+
+#define AMR_OK 0
+#define AMR_E_INVALID -1      /* bad argument */
+#define AMR_E_PADLEN -2       /* n_samples <= filtfilt padlen (scipy ValueError) */
+#define AMR_E_HIP -3          /* HIP runtime failure (message in amr_last_error) */
+#define AMR_E_NOMEM -4        /* device allocation failed */
+#define AMR_E_NODEVICE -5     /* no usable gfx950 device */
+#define AMR_E_RCCL -6         /* RCCL failure */
+#define AMR_E_CAPACITY -7     /* batch larger than the plan's max_streams */
+
+#define AMR_DTYPE_F32 0       /* float32 samples (live capture path) */
+#define AMR_DTYPE_F64 1       /* float64 samples (decode_wav_file path) */
+#define AMR_DTYPE_I16 2       /* int16 PCM, read as int16/32768.0 (libsndfile default) */
+
+#define AMR_PSK_QPSK 0        /* DQPSK slicer, modem.py:216-241 */
+#define AMR_PSK_BPSK 1        /* DBPSK slicer, modem.py:102-105 */
+
+/* kernel timing slots reported by amr_psk_plan_timings() */
+#define AMR_T_BANDPASS 0
+#define AMR_T_LOWPASS_FWD 1
+#define AMR_T_LOWPASS_BWD 2
+#define AMR_T_LOWPASS_EXACT 3
+#define AMR_T_SYNC_PACK 4
+#define AMR_T_FEC 5
+#define AMR_T_COUNT 6
+
+typedef struct amr_psk_plan amr_psk_plan;
+typedef struct amr_comm amr_comm;
+
+int amr_abi_version(void);
+const char *amr_last_error(void);
+int amr_device_count(int *count);
+
+/* ---- memory helpers (device = the plan's / current device) ---------------- */
+int amr_set_device(int device);
+int amr_malloc(void **dptr, int64_t bytes);
+int amr_free(void *dptr);
+int amr_memcpy_h2d(void *dst, const void *src, int64_t bytes);
+int amr_memcpy_d2h(void *dst, const void *src, int64_t bytes);
+int amr_memcpy_d2d(void *dst, const void *src, int64_t bytes);
+int amr_device_synchronize(void);
+
+/* ---- DPSK demodulation ------------------------------------------------------
+ * kind          AMR_PSK_QPSK | AMR_PSK_BPSK
+ * n_samples     samples per stream (all streams of a call share it)
+ * sps           int(fs / baud)                                 modem.py:70,191
+ * first_symbol  sps // 2 (QPSK, modem.py:209) or sps (BPSK, modem.py:92)
+ * bp_*          band-pass b, a, lfilter_zi (ntaps each; a[0] must be 1)
+ * lp_*          low-pass  b, a, lfilter_zi
+ * lo4           [n_samples][4] doubles: lo_re, lo_im, -(0*lo_im), 0*lo_re
+ *               where lo = numpy.exp(-1j*2*pi*carrier*arange(n)/fs)
+ * max_streams   largest batch this plan will see (sizes the HBM scratch)
+ */
+int amr_psk_plan_create(amr_psk_plan **plan, int device, int kind, int64_t n_samples, int64_t sps,
+                        int64_t first_symbol, const double *bp_b, const double *bp_a, const double *bp_zi,
+                        int bp_ntaps, const double *lp_b, const double *lp_a, const double *lp_zi,
+                        int lp_ntaps, const double *lo4, int64_t max_streams);
+int amr_psk_plan_destroy(amr_psk_plan *plan);
+/* bytes a stream's output can need: floor(bits/8) */
+int64_t amr_psk_plan_out_capacity(const amr_psk_plan *plan);
+/* scratch bytes the plan holds in HBM */
+int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
+int amr_psk_plan_synchronize(amr_psk_plan *plan);
+/* record per-kernel HIP events on the plan's stream (1) or not (0) */
+int amr_psk_plan_enable_timing(amr_psk_plan *plan, int on);
+/* milliseconds of each AMR_T_* kernel in the last call (-1 = not run) */
+int amr_psk_plan_timings(amr_psk_plan *plan, float *ms, int count);
+/* number of streams the exact complex low-pass path re-ran in the last call */
+int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
+
+/* x: [n_streams][x_stride] samples of `dtype`; out: [n_streams][out_stride]
+ * bytes; out_len[s] = bytes written for stream s; sync_idx[s] = bit index of
+ * the "FB" sync or -1.  Synchronous. */
+int amr_psk_demod_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                       uint8_t *out, int64_t out_stride, int64_t *out_len, int64_t *sync_idx);
+/* Same contract, all pointers device pointers; asynchronous on the plan's stream. */
+int amr_psk_demod_device(amr_psk_plan *plan, const void *d_x, int dtype, int64_t n_streams, int64_t x_stride,
+                         uint8_t *d_out, int64_t out_stride, int64_t *d_out_len, int64_t *d_sync_idx);
+/* Demod then FEC decode of each stream's bytes, fused on the device. */
+int amr_psk_demod_fec_device(amr_psk_plan *plan, const void *d_x, int dtype, int64_t n_streams,
+                             int64_t x_stride, uint8_t *d_out, int64_t out_stride, int64_t *d_out_len,
+                             int64_t *d_sync_idx, uint8_t *d_fec, int64_t fec_stride, int64_t *d_fec_len,
+                             int32_t *d_crc_ok);
+
+/* ---- FEC (fec.py:34-69) -----------------------------------------------------
+ * in: [n][in_stride] bytes, in_len[n]; out: [n][out_stride] (>= in_len each);
+ * crc_ok[s] = 1 when the recomputed CRC32 equals the trailing word
+ * (the reference only prints "Aviso: CRC ..." on mismatch). */
+int amr_fec_decode_host(const uint8_t *in, int64_t in_stride, const int64_t *in_len, int64_t n,
+                        uint8_t *out, int64_t out_stride, int64_t *out_len, int32_t *crc_ok);
+
+/* ---- multi-GPU: RCCL over xGMI ----------------------------------------------- */
+#define AMR_UNIQUE_ID_BYTES 128
+int amr_comm_unique_id(uint8_t *id /* AMR_UNIQUE_ID_BYTES */);
+int amr_comm_create(amr_comm **comm, const uint8_t *id, int nranks, int rank, int device);
+int amr_comm_destroy(amr_comm *comm);
+/* ncclAllGather of bytes_per_rank bytes per rank; stream = plan's (or NULL = comm's own) */
+int amr_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
+                  amr_psk_plan *plan);
+int amr_comm_synchronize(amr_comm *comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMR_H */

@@ -101,14 +101,66 @@ int oracle_filtfilt(const double *b, const double *a, int nt, const double *zi,
     return 0;
 }
 
-/* Same, on a complex sequence given as separate re/im planes (the complex
- * lfilter with real coefficients is two independent real recurrences). */
+/* ---- complex filtfilt, exact numpy/scipy semantics --------------------------
+ * filtfilt on a complex128 sequence with real coefficients (modem.py:88, 204).
+ * scipy's complex lfilter inner loop (CDOUBLE_filt) evaluates every tap
+ * product as a complex multiply by (b + 0j) normalised by a0 = 1:
+ *     re = (b*xr - (+0)*xi) / 1,   im = ((+0)*xr + b*xi) / 1
+ * and numpy builds the odd extension (2*x[0] - x[k]) and zi*x[0] with its
+ * complex multiply  re = fma(ar, br, -(ai*bi)), im = fma(ar, bi, ai*br).
+ * The extra terms only ever change the SIGN OF A ZERO, but a signed zero
+ * reaches np.angle in silent (exactly zero) regions, so the oracle keeps them.
+ * Verified bit for bit against scipy.signal.lfilter on signed-zero inputs. */
+static void df2t_cplx(const double *b, const double *a, int nt, double *zr, double *zi,
+                      double *xr, double *xi, int64_t n, int64_t step)
+{
+    for (int64_t k = 0; k < n; ++k) {
+        const double x0 = xr[k * step], x1 = xi[k * step];
+        const double t0x = 0.0 * x1, t1x = 0.0 * x0;
+        const double y0 = zr[0] + (b[0] * x0 - t0x);
+        const double y1 = zi[0] + (t1x + b[0] * x1);
+        const double t0y = 0.0 * y1, t1y = 0.0 * y0;
+        int i = 0;
+        for (; i < nt - 2; ++i) {
+            double r = zr[i + 1] + (b[i + 1] * x0 - t0x);
+            double m = zi[i + 1] + (t1x + b[i + 1] * x1);
+            zr[i] = r - (a[i + 1] * y0 - t0y);
+            zi[i] = m - (t1y + a[i + 1] * y1);
+        }
+        zr[i] = (b[i + 1] * x0 - t0x) - (a[i + 1] * y0 - t0y);
+        zi[i] = (t1x + b[i + 1] * x1) - (t1y + a[i + 1] * y1);
+        xr[k * step] = y0;
+        xi[k * step] = y1;
+    }
+}
+
+/* numpy complex multiply (ar + i ai)*(br + i bi) on AVX-512/FMA3 x86 */
+static inline void cmul_np(double ar, double ai, double br, double bi, double *re, double *im)
+{
+    *re = fma(ar, br, -(ai * bi));
+    *im = fma(ar, bi, ai * br);
+}
+
 static int filtfilt_complex(const double *b, const double *a, int nt, const double *zi,
                             double *re, double *im, int64_t n, double *work)
 {
-    int rc = oracle_filtfilt(b, a, nt, zi, re, AMR_DT_F64, n, re, work);
-    if (rc) return rc;
-    return oracle_filtfilt(b, a, nt, zi, im, AMR_DT_F64, n, im, work);
+    const int pad = 3 * nt;
+    if (n <= pad) return -1;
+    const int64_t m = n + 2 * (int64_t)pad;
+    double *er = work, *ei = work + m;
+    double zr[32], zc[32], tr, ti;
+    /* odd extension: 2*x[0] - x[k] as numpy complex ops (_arraytools.py:103) */
+    cmul_np(2.0, 0.0, re[0], im[0], &tr, &ti);
+    for (int j = 0; j < pad; ++j) { er[j] = tr - re[pad - j]; ei[j] = ti - im[pad - j]; }
+    for (int64_t j = 0; j < n; ++j) { er[pad + j] = re[j]; ei[pad + j] = im[j]; }
+    cmul_np(2.0, 0.0, re[n - 1], im[n - 1], &tr, &ti);
+    for (int j = 0; j < pad; ++j) { er[pad + n + j] = tr - re[n - 2 - j]; ei[pad + n + j] = ti - im[n - 2 - j]; }
+    for (int i = 0; i < nt - 1; ++i) cmul_np(zi[i], 0.0, er[0], ei[0], &zr[i], &zc[i]);
+    df2t_cplx(b, a, nt, zr, zc, er, ei, m, 1);
+    for (int i = 0; i < nt - 1; ++i) cmul_np(zi[i], 0.0, er[m - 1], ei[m - 1], &zr[i], &zc[i]);
+    df2t_cplx(b, a, nt, zr, zc, er + m - 1, ei + m - 1, m, -1);
+    for (int64_t i = 0; i < n; ++i) { re[i] = er[pad + i]; im[i] = ei[pad + i]; }
+    return 0;
 }
 
 /* ---- sync + pack (modem.py:244-264) -------------------------------------- */
@@ -156,10 +208,8 @@ int64_t oracle_psk_demod(int kind, const void *x, int dtype, int64_t n,
     int64_t result = 0;
     uint8_t *bits = NULL;
     if (oracle_filtfilt(bp_b, bp_a, bp_nt, bp_zi, x, dtype, n, filt, work)) { result = -1; goto done; }
-    for (int64_t i = 0; i < n; ++i) {               /* modem.py:200-201 real*complex */
-        re[i] = filt[i] * lo[2 * i];
-        im[i] = filt[i] * lo[2 * i + 1];
-    }
+    for (int64_t i = 0; i < n; ++i)                  /* modem.py:200-201: (f + 0j) * lo */
+        cmul_np(filt[i], 0.0, lo[2 * i], lo[2 * i + 1], &re[i], &im[i]);
     if (filtfilt_complex(lp_b, lp_a, lp_nt, lp_zi, re, im, n, work)) { result = -2; goto done; }
     {
         int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
@@ -170,12 +220,12 @@ int64_t oracle_psk_demod(int kind, const void *x, int dtype, int64_t n,
         for (int64_t k = 0; k + 1 < S; ++k) {
             const double ar = re[first + (k + 1) * sps], ai = im[first + (k + 1) * sps];
             const double br = re[first + k * sps], bi = -im[first + k * sps];   /* conj */
-            const double dr = fma(ar, br, -(ai * bi));
+            double dr, di;
+            cmul_np(ar, ai, br, bi, &dr, &di);
             if (kind == 1) {
                 bits[k] = (dr < 0) ? 1 : 0;              /* modem.py:103-105 */
                 continue;
             }
-            const double di = fma(ar, bi, ai * br);
             double ang = atan2(di, dr);                  /* np.angle, modem.py:219 */
             if (ang < 0) ang += 2 * M_PI;                /* modem.py:232 */
             uint8_t h, l;

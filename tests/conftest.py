@@ -1,0 +1,33 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "audio-modem-radio_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    import numpy as np
+    g = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(g, "manifest.json")) as f:
+        manifest = json.load(f)
+    inputs = np.load(os.path.join(g, "inputs.npz"))
+    return manifest, inputs
+
+
+@pytest.fixture(scope="session")
+def built_lib():
+    """libamr.so, built in-tree if missing (hipcc cross-compiles without a GPU)."""
+    import build
+    return build.build()

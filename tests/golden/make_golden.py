@@ -195,6 +195,42 @@ def main():
         {"baud": 1200, "mark_freq": 2400.0, "space_freq": 4800.0},
         lambda x: _run(modem.fsk_demodulate, x, 1200, 2400.0, 4800.0))
 
+    # --- signed zeros, silence, denormals, non-finite (exact-zero semantics) ----------
+    sig = synth.fit(modem.qpsk_modulate(synth.random_frame(rng, 400), baud=9600), 20000)
+    add("qpsk_negzero", "qpsk_demodulate", np.full(5000, -0.0, np.float32), {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = np.concatenate([sig + noise(20000, 0.05), np.zeros(60000, np.float32)]).astype(np.float32)
+    add("qpsk_tail_silence", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = np.concatenate([np.zeros(40000, np.float32), sig + noise(20000, 0.05)]).astype(np.float32)
+    add("qpsk_head_silence", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = (sig[:8000].astype(np.float64) + rng.normal(0, 0.05, 8000)) * 1e-310
+    add("qpsk_denorm_f64", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = ((sig[:8000] + noise(8000, 0.05)) * np.float32(1e-41)).astype(np.float32)
+    add("qpsk_denorm_f32", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = (sig[:6000] + noise(6000, 0.05)).astype(np.float32)
+    x[3000] = np.nan
+    add("qpsk_nan", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = (sig[:6000] + noise(6000, 0.05)).astype(np.float32)
+    x[100] = np.inf
+    add("qpsk_inf", "qpsk_demodulate", x, {"baud": 9600},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=9600))
+    x = np.zeros(3000, np.float32)
+    x[::7] = -0.0
+    x[1::11] = 0.5
+    add("qpsk_sparse", "qpsk_demodulate", x, {"baud": 2400},
+        lambda x: _run(modem.qpsk_demodulate, x, baud=2400))
+    x = modem.bpsk_modulate(synth.random_frame(rng, 60), baud=2400)
+    x = np.concatenate([x, np.zeros(50000, np.float32)]).astype(np.float32)
+    add("bpsk_tail_silence", "bpsk_demodulate", x, {"baud": 2400},
+        lambda x: _run(modem.bpsk_demodulate, x, baud=2400))
+    add("bpsk_zeros", "bpsk_demodulate", np.zeros(4000, np.float64), {"baud": 1200},
+        lambda x: _run(modem.bpsk_demodulate, x, baud=1200))
+
     # --- FEC parity-XOR + CRC32 decode (fec.py:34-69) ------------------------------------
     rs = fec.ReedSolomonFEC()
     fec_cases = []

@@ -1,0 +1,203 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's own
+outputs (golden fixtures) and against the oracle on seeded inputs up to the
+BASELINE sizes.  Bar: bit-exact bytes (and identical error contracts)."""
+import contextlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+from _util import call_case, expected, outcome
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(built_lib):
+    import _amr
+    if _amr.device_count() < 1:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
+
+
+def test_every_golden_psk_case_bit_exact(golden):
+    import modem
+    manifest, inputs = golden
+    bad = []
+    for case in manifest["cases"]:
+        if case["fn"].startswith("fsk"):
+            continue
+        got = outcome(lambda: call_case(modem, case, inputs[case["id"]]))
+        if got != expected(case):
+            bad.append(case["id"])
+    assert not bad, f"GPU differs from the reference on {bad}"
+
+
+def test_golden_qpsk9600_as_one_batch(golden):
+    import modem
+    manifest, inputs = golden
+    cases = [c for c in manifest["cases"] if c["id"].startswith("qpsk9600_f32_")]
+    x = np.stack([inputs[c["id"]] for c in cases])
+    outs = modem.qpsk_demodulate_batch(x, baud=9600)
+    assert [o.hex() for o in outs] == [c["out"] for c in cases]
+
+
+def test_exact_complex_lowpass_path_matches(golden, monkeypatch):
+    """Force every stream through k_lowpass_exact (scipy's complex lfilter
+    semantics) and check it reproduces the reference too."""
+    import _amr
+    manifest, inputs = golden
+    monkeypatch.setenv("AMR_FORCE_EXACT_LOWPASS", "1")
+    bad = []
+    for case in manifest["cases"]:
+        if case["status"] != "ok" or case["fn"] not in ("qpsk_demodulate", "bpsk_demodulate"):
+            continue
+        x = inputs[case["id"]]
+        kind = "qpsk" if case["fn"] == "qpsk_demodulate" else "bpsk"
+        p = case["params"]
+        plan = _amr.PskPlan(kind, x.size, p["baud"], p.get("carrier", 3000.0), 96000, max_streams=1)
+        outs, _ = plan.demod_host(x[None, :])
+        if outs[0].hex() != case["out"]:
+            bad.append(case["id"])
+    assert not bad, bad
+
+
+def test_silence_cases_take_exact_path(golden):
+    """Exactly-zero regions must be routed to the exact kernel by the detector."""
+    import _amr
+    manifest, inputs = golden
+    x = inputs["qpsk_tail_silence"]
+    plan = _amr.PskPlan("qpsk", x.size, 9600, max_streams=1)
+    outs, _ = plan.demod_host(x[None, :])
+    assert outs[0].hex() == [c for c in manifest["cases"] if c["id"] == "qpsk_tail_silence"][0]["out"]
+    assert plan.exact_streams() == 1
+    xs = inputs["qpsk9600_f32_0"]
+    plan2 = _amr.PskPlan("qpsk", xs.size, 9600, max_streams=1)
+    plan2.demod_host(xs[None, :])
+    assert plan2.exact_streams() == 0
+
+
+def test_int16_pcm_path_equals_float64_reference(golden):
+    """AMR_DTYPE_I16 (PCM read as int16/32768) == the reference on the float64 it would see."""
+    import _amr
+    manifest, inputs = golden
+    x = inputs["qpsk9600_wav"]
+    q = np.round(x * 32768.0).astype(np.int16)
+    assert np.array_equal(q.astype(np.float64) / 32768.0, x)
+    plan = _amr.PskPlan("qpsk", x.size, 9600, max_streams=1)
+    outs, _ = plan.demod_host(q[None, :])
+    assert outs[0].hex() == [c for c in manifest["cases"] if c["id"] == "qpsk9600_wav"][0]["out"]
+
+
+@pytest.mark.parametrize("kind,baud,B,N", [("qpsk", 9600, 4096, 96000), ("qpsk", 19200, 257, 96000),
+                                           ("bpsk", 1200, 130, 48000), ("qpsk", 2400, 65, 30001)])
+def test_batch_vs_oracle(kind, baud, B, N):
+    """Seeded batches up to the BASELINE config-2 size, every stream checked
+    against the oracle (bit-exact bytes and sync index)."""
+    import _amr
+    import synth
+    from oracle import oracle
+    if kind == "qpsk" and baud == 19200:
+        x = synth.dpsk8_batch(B, N, baud, seed=B, distinct=8)
+    else:
+        x = synth.qpsk_batch(B, N, baud, seed=B, distinct=8) if kind == "qpsk" else \
+            np.stack([synth.fit(synth.bpsk_waveform(synth.random_frame(np.random.default_rng(i), 200), baud), N)
+                      + np.random.default_rng(i).normal(0, 0.05, N).astype(np.float32) for i in range(B)])
+    plan = _amr.PskPlan(kind, N, baud, max_streams=B)
+    got, gsync = plan.demod_host(x)
+    want, wsync = oracle.psk_demod_batch(kind, x, baud, n_threads=min(16, os.cpu_count() or 1))
+    mism = [i for i in range(B) if got[i] != want[i]]
+    assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
+    assert np.array_equal(gsync, wsync)
+
+
+def test_ragged_streams():
+    import modem
+    from oracle import oracle
+    rng = np.random.default_rng(5)
+    streams = [rng.normal(0, 0.5, n).astype(np.float32) for n in (28, 100, 5000, 5000, 4999, 60)]
+    got = modem.demodulate_ragged("qpsk", streams, 2400)
+    for s, g in zip(streams, got):
+        assert g == oracle.qpsk_demodulate(s, baud=2400)
+
+
+def test_fec_gpu_matches_reference(golden):
+    import fec
+    manifest, _ = golden
+    rs = fec.ReedSolomonFEC()
+    ins = [bytes.fromhex(f["in"]) for f in manifest["fec"]]
+    outs, oks = rs.decode_batch(ins)
+    for f, o, ok, d in zip(manifest["fec"], outs, oks, ins):
+        assert o.hex() == f["out"]
+        if len(d) >= 4:
+            assert ok == (not f["crc_warn"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        assert rs.decode(ins[-1]).hex() == manifest["fec"][-1]["out"]
+    assert ("Aviso: CRC" in buf.getvalue()) == manifest["fec"][-1]["crc_warn"]
+
+
+def test_fec_fused_after_8psk_demod():
+    """Config 5: 8PSK@19200 demod + FEC decode fused on the device == oracle chain."""
+    import ctypes
+    import _amr
+    import synth
+    from oracle import oracle
+    B, N = 64, 96000
+    x = synth.dpsk8_batch(B, N, 19200, seed=11, distinct=4)
+    plan = _amr.PskPlan("qpsk", N, 19200, max_streams=B)
+    L = _amr.lib()
+    cap = plan.out_cap
+    ptrs = {}
+    for name, nbytes in (("x", x.nbytes), ("out", B * cap), ("len", B * 8), ("sync", B * 8), ("fec", B * cap),
+                         ("flen", B * 8), ("ok", B * 4)):
+        p = ctypes.c_void_p()
+        _amr.check(L.amr_malloc(ctypes.byref(p), nbytes))
+        ptrs[name] = p
+    try:
+        _amr.check(L.amr_memcpy_h2d(ptrs["x"], _amr.ptr(x), x.nbytes))
+        _amr.check(L.amr_psk_demod_fec_device(plan.handle, ptrs["x"], _amr.DTYPE_F32, B, N, ptrs["out"], cap,
+                                              ptrs["len"], ptrs["sync"], ptrs["fec"], cap, ptrs["flen"], ptrs["ok"]))
+        _amr.check(L.amr_psk_plan_synchronize(plan.handle))
+        fec_out = np.empty((B, cap), np.uint8)
+        flen = np.empty(B, np.int64)
+        ok = np.empty(B, np.int32)
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(fec_out), ptrs["fec"], B * cap))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(flen), ptrs["flen"], B * 8))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(ok), ptrs["ok"], B * 4))
+    finally:
+        for p in ptrs.values():
+            L.amr_free(p)
+    dem, _ = oracle.psk_demod_batch("qpsk", x, 19200, n_threads=8)
+    for i in range(B):
+        want, wok = oracle.fec_decode(dem[i])
+        assert fec_out[i, :flen[i]].tobytes() == want
+        assert bool(ok[i]) == wok
+
+
+def test_decode_wav_file_end_to_end(golden, tmp_path, monkeypatch):
+    import decoder
+    manifest, inputs = golden
+    monkeypatch.chdir(tmp_path)
+    for case in manifest["decoder"]:
+        p = tmp_path / (case["id"] + ".wav")
+        p.write_bytes(inputs[case["id"]].tobytes())
+        with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+            saved = decoder.decode_wav_file(str(p), case["mode"], case["symbol_rate"])
+        got = []
+        for s in saved:
+            with open(s, "rb") as f:
+                got.append({"name": os.path.basename(s).split("_", 1)[1], "data": f.read().hex()})
+        assert got == case["files"], case["id"]
+
+
+def test_timing_hooks():
+    import _amr
+    import synth
+    x = synth.qpsk_batch(64, 20000, 9600, seed=1, distinct=2)
+    plan = _amr.PskPlan("qpsk", 20000, 9600, max_streams=64)
+    plan.enable_timing(True)
+    plan.demod_host(x)
+    t = plan.timings()
+    assert set(t) >= {"bandpass", "lowpass_fwd", "lowpass_bwd", "sync_pack"}
+    assert all(v > 0 for v in t.values())
