@@ -48,9 +48,9 @@ struct PskBuffers {
   int64_t x_stride;       // elements
   int dtype;
   int64_t n_streams;      // B
-  const double* lo;       // [n][4]: (lo_re, lo_im, -(0*lo_im), 0*lo_re)
+  const double* lo;       // [n][4]: (lo_re, -(0*lo_im), lo_im, 0*lo_re)
   double* s1;             // band-pass forward output  [G][m1p/2][64][2]
-  double* s2;             // mixer output (baseband)   [G][n][64][2]
+  double* s2;             // band-pass output f        [G][2][n2][32][2]
   double* s3;             // low-pass forward output   [2G][m2p/2][64][2]
   uint32_t* words;        // [B][n_words] bit buffer, MSB first
   int32_t* flags;         // [B] 1 => take the exact complex low-pass path

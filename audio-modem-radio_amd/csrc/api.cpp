@@ -272,7 +272,7 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   const A allocs[] = {
       {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
       {(void**)&pl->s1, g * pl->m1_pairs * kWave * 16},
-      {(void**)&pl->s2, g * n * kWave * 16},
+      {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16},
       {(void**)&pl->s3, 2 * g * pl->m2_pairs * kWave * 16},
       {(void**)&pl->words, g * kWave * p.n_words * 4},
       {(void**)&pl->flags, g * kWave * 4},
@@ -285,7 +285,18 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
     }
     pl->scratch_bytes += a.bytes;
   }
-  e = hipMemcpy(pl->lo, lo4, (size_t)(n * 4 * sizeof(double)), hipMemcpyHostToDevice);
+  {
+    // device LO layout [n][4] = (lo_re, -(0*lo_im), lo_im, 0*lo_re): per sample and
+    // component the (multiplier, addend) pair of numpy's complex multiply
+    std::vector<double> lo_dev((size_t)n * 4);
+    for (int64_t i = 0; i < n; ++i) {
+      lo_dev[4 * i + 0] = lo4[4 * i + 0];
+      lo_dev[4 * i + 1] = lo4[4 * i + 2];
+      lo_dev[4 * i + 2] = lo4[4 * i + 1];
+      lo_dev[4 * i + 3] = lo4[4 * i + 3];
+    }
+    e = hipMemcpy(pl->lo, lo_dev.data(), (size_t)(n * 4 * sizeof(double)), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     plan_free(pl);

@@ -12,15 +12,25 @@
 // The oracle (oracle/amr_oracle.c) states the same arithmetic on the CPU.
 //
 // Pipeline for one batch (one kernel per stage, all streams in flight):
-//   K1 k_bandpass_mix  lane = stream: band-pass filtfilt (forward pass to
-//                      s1, backward pass from s1) fused with the LO mixer -> s2
-//   K2 k_lowpass_fwd   lane = (stream, re|im): low-pass forward pass -> s3
+//   K1 k_bandpass      lane = stream: band-pass filtfilt.  Forward pass reads
+//                      the caller's stream-major samples through a coalesced
+//                      LDS transpose tile and writes s1; the backward pass
+//                      streams s1 back (register prefetch ring) and writes the
+//                      real filtered signal f to s2.
+//   K2 k_lowpass_fwd   lane = (stream, re|im): LO mixer (numpy's complex
+//                      multiply) fused into the low-pass forward pass -> s3
 //   K3 k_lowpass_bwd   lane = (stream, re|im): low-pass backward pass fused
 //                      with symbol pick, differential product, slicer and the
 //                      bit writer -> words
 //   K3x k_lowpass_exact lane = stream: the complex low-pass with scipy's full
 //                      signed-zero semantics, only for streams K2/K3 flagged
 //   (K4 sync + pack lives in util_kernels.hip)
+//
+// Every wave runs alone on its SIMD (the batch of 4096 streams is only
+// 64-128 waves), so each kernel is bound by its per-sample instruction stream;
+// the memory side is arranged so that no load is waited on before it has had
+// a whole chunk of compute to land (tools/fp64_probe.hip measured the
+// register-only band-pass step at 126 cycles/sample).
 #include <math.h>
 
 #include "amr_internal.h"
@@ -68,31 +78,40 @@ __device__ __forceinline__ double df2t_step(double (&z)[NT - 1], const double (&
   return y;
 }
 
+// [group][q/2][64 lanes][2] doubles
 __device__ __forceinline__ size_t pair_index(int64_t group, int64_t m_pairs, int64_t q, int lane) {
-  // [group][q/2][64 lanes][2] doubles
   return ((size_t)(group * m_pairs + (q >> 1)) * kWave + lane) * 2 + (q & 1);
 }
 
-// ---------------------------------------------------------------------------
-// K1: band-pass filtfilt + mixer.  One wave per group of 64 streams, lane = stream.
-//   forward : ext[j] (j < m1)  -> s1      (scipy filtfilt forward lfilter)
-//   backward: s1 reversed      -> y2, trimmed to [pad1, pad1+n)
-//   mixer   : bb[n] = (y2 + 0j) * lo[n]   numpy complex multiply, exact:
-//             re = fma(y2, lo_re, -(0*lo_im)),  im = fma(y2, lo_im, 0*lo_re)
-// s1 is indexed by q = j + (pad1 & 1) so that the main body starts on a pair.
-constexpr int kChunk = 16;
+// s2 (band-pass output f): [group][half][n2][32 streams][2 samples] doubles,
+// so that a low-pass wave (one half-group) streams one 512 B row per 2 samples.
+__device__ __forceinline__ size_t f_index(int64_t g, int64_t n2, int64_t i, int s_in_group) {
+  const int h = s_in_group >> 5, sl = s_in_group & 31;
+  return ((size_t)((g * 2 + h) * n2 + (i >> 1)) * 32 + sl) * 2 + (i & 1);
+}
 
+typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector: SROA-friendly (HIP's uint4 is a struct)
+
+constexpr int kTileBytes = 256;                 // bytes of one stream per input tile
+constexpr int kTilePitch = kTileBytes + 16;     // LDS row pitch: conflict-free ds_read_b128 per lane
+constexpr int kBwdChunk = 32;                   // samples per backward prefetch chunk (16 pairs)
+
+// ---------------------------------------------------------------------------
+// K1: band-pass filtfilt.  One wave per group of 64 streams, lane = stream.
 template <int NT, bool ZODD, typename T>
-__global__ __launch_bounds__(64) void k_bandpass_mix(PskBuffers buf, PskParams p, Iir f) {
+__global__ __launch_bounds__(64) void k_bandpass(PskBuffers buf, PskParams p, Iir f) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[2][kWave][kTilePitch];
+  constexpr int TS = kTileBytes / (int)sizeof(T);          // samples per tile
   const int lane = threadIdx.x;
   const int64_t g = blockIdx.x;
   const int64_t s = g * kWave + lane;
-  const int64_t sc = s < buf.n_streams ? s : buf.n_streams - 1;   // idle lanes shadow a real stream
-  const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + sc * buf.x_stride;
+  const int64_t last = buf.n_streams - 1;
+  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
+  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
   const int64_t n = p.n;
   const int pad = p.pad1;
   const int64_t m1 = p.m1;
-  const int qs = pad & 1;                       // q = j + qs
+  const int qs = pad & 1;                       // s1 index q = j + qs (main body starts on a pair)
   const int64_t m1_pairs = (m1 + qs + 1) >> 1;
   double* __restrict__ s1 = buf.s1;
 
@@ -111,28 +130,47 @@ __global__ __launch_bounds__(64) void k_bandpass_mix(PskBuffers buf, PskParams p
     const double y = df2t_step<NT, ZODD>(z, b, a, In<T>::ext(x0, x[pad - j]));
     s1[pair_index(g, m1_pairs, j + qs, lane)] = y;
   }
-  // main body: chunks of kChunk samples, next chunk prefetched into registers
-  const int64_t n_main = (n / kChunk) * kChunk;
-  {
-    T nxt[kChunk];
+  // main body: tiles of TS samples x 64 streams, loaded row-coalesced
+  // (16 lanes x 16 B per stream row) and transposed through LDS.
+  const int64_t n_tiles = n / TS;
+  const int64_t n_main = n_tiles * TS;
+  if (n_tiles > 0) {
+    const int rsub = lane >> 4, cb = (lane & 15) * 16;
+    const uint8_t* rowp[16];
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) nxt[k] = (n_main > 0) ? x[k] : T(0);
-    for (int64_t c = 0; c < n_main; c += kChunk) {
-      T cur[kChunk];
+    for (int i = 0; i < 16; ++i) {
+      const int64_t rs = g * kWave + 4 * i + rsub;
+      rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * buf.x_stride) + cb;
+    }
+    v4u r[16];
 #pragma unroll
-      for (int k = 0; k < kChunk; ++k) cur[k] = nxt[k];
-      if (c + kChunk < n_main) {
+    for (int i = 0; i < 16; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i]);
 #pragma unroll
-        for (int k = 0; k < kChunk; ++k) nxt[k] = x[c + kChunk + k];
-      }
-      const int64_t q0 = pad + qs + c;          // even
+    for (int i = 0; i < 16; ++i) *reinterpret_cast<v4u*>(&tile[0][4 * i + rsub][cb]) = r[i];
+    for (int64_t t = 0; t < n_tiles; ++t) {
+      const int cur = (int)(t & 1);
+      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;   // unconditional (clamped) prefetch
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + tn * kTileBytes);
+      __builtin_amdgcn_sched_barrier(0);
+      const int64_t q0 = pad + qs + t * TS;                // even
       double2* __restrict__ dst = reinterpret_cast<double2*>(s1) + (size_t)(g * m1_pairs + (q0 >> 1)) * kWave + lane;
+      constexpr int PER = 16 / (int)sizeof(T);             // samples per ds_read_b128
 #pragma unroll
-      for (int k = 0; k < kChunk; k += 2) {
-        const double y0 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(cur[k]));
-        const double y1 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(cur[k + 1]));
-        dst[(k >> 1) * kWave] = make_double2(y0, y1);
+      for (int k = 0; k < TS; k += PER) {
+        const v4u v = *reinterpret_cast<const v4u*>(&tile[cur][lane][k * sizeof(T)]);
+        T xs[PER];
+        __builtin_memcpy(xs, &v, 16);
+#pragma unroll
+        for (int u = 0; u < PER; u += 2) {
+          const double y0 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(xs[u]));
+          const double y1 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(xs[u + 1]));
+          dst[((k + u) >> 1) * kWave] = make_double2(y0, y1);
+        }
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) *reinterpret_cast<v4u*>(&tile[cur ^ 1][4 * i + rsub][cb]) = r[i];
     }
   }
   for (int64_t i = n_main; i < n; ++i) {        // main-body remainder
@@ -148,51 +186,57 @@ __global__ __launch_bounds__(64) void k_bandpass_mix(PskBuffers buf, PskParams p
   // own stores must be visible to own loads below
   __threadfence();
 
-  // ---- backward pass + mixer ----------------------------------------------
+  // ---- backward pass ------------------------------------------------------
 #pragma unroll
   for (int i = 0; i < NT - 1; ++i) z[i] = f.zi[i] * ylast;
   // the right extension region: outputs discarded (trimmed)
   for (int64_t j = m1 - 1; j >= pad + n; --j)
     (void)df2t_step<NT, ZODD>(z, b, a, s1[pair_index(g, m1_pairs, j + qs, lane)]);
 
-  const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);
-  double2* __restrict__ bb = reinterpret_cast<double2*>(buf.s2) + (size_t)g * n * kWave + lane;
-  // top remainder of the main body, one sample at a time (n % kChunk samples)
-  const int64_t n_top = n - n_main;
-  for (int64_t i = n - 1; i >= n - n_top; --i) {
+  const int64_t n2 = (n + 1) >> 1;
+  double* __restrict__ fo = buf.s2;
+  const int64_t nb = n / kBwdChunk;             // full chunks, processed top-down
+  const int64_t n_lo = nb * kBwdChunk;
+  for (int64_t i = n - 1; i >= n_lo; --i) {     // top remainder, one sample at a time
     const double y = df2t_step<NT, ZODD>(z, b, a, s1[pair_index(g, m1_pairs, pad + i + qs, lane)]);
-    const double4 l = lo[i];
-    bb[(size_t)i * kWave] = make_double2(__builtin_fma(y, l.x, l.z), __builtin_fma(y, l.y, l.w));
+    fo[f_index(g, n2, i, lane)] = y;
   }
-  // main body backward in chunks; q of chunk start is even
-  {
+  if (nb > 0) {
     const double2* __restrict__ src = reinterpret_cast<const double2*>(s1) + (size_t)g * m1_pairs * kWave + lane;
-    double2 nxt[kChunk / 2];
-    const int64_t cstart = n_main - kChunk;
-    if (n_main > 0) {
+    double2* __restrict__ dst = reinterpret_cast<double2*>(fo);
+    const size_t fbase = (size_t)((g * 2 + (lane >> 5)) * n2) * 32 + (lane & 31);
+    constexpr int PP = kBwdChunk / 2;
+    double2 ra[PP], rb[PP];
+    auto load = [&](double2 (&r)[PP], int64_t c) {   // chunk c covers i in [c*32, c*32+32)
+      const int64_t cc = c < 0 ? 0 : c;
+      const int64_t qp = (pad + qs + cc * kBwdChunk) >> 1;
 #pragma unroll
-      for (int k = 0; k < kChunk / 2; ++k) nxt[k] = src[(size_t)(((pad + qs + cstart) >> 1) + k) * kWave];
-    }
-    for (int64_t c = cstart; c >= 0; c -= kChunk) {
-      double2 cur[kChunk / 2];
+      for (int k = 0; k < PP; ++k) r[k] = src[(size_t)(qp + k) * kWave];
+    };
+    auto run = [&](const double2 (&r)[PP], int64_t c) {
 #pragma unroll
-      for (int k = 0; k < kChunk / 2; ++k) cur[k] = nxt[k];
-      if (c >= kChunk) {
-        const int64_t qp = (pad + qs + c - kChunk) >> 1;
-#pragma unroll
-        for (int k = 0; k < kChunk / 2; ++k) nxt[k] = src[(size_t)(qp + k) * kWave];
+      for (int k = PP - 1; k >= 0; --k) {
+        const double y1 = df2t_step<NT, ZODD>(z, b, a, r[k].y);
+        const double y0 = df2t_step<NT, ZODD>(z, b, a, r[k].x);
+        dst[fbase + (size_t)(c * PP + k) * 32] = make_double2(y0, y1);
       }
-#pragma unroll
-      for (int k = kChunk / 2 - 1; k >= 0; --k) {
-        const int64_t i1 = c + 2 * k + 1, i0 = c + 2 * k;
-        const double y1 = df2t_step<NT, ZODD>(z, b, a, cur[k].y);
-        const double4 l1 = lo[i1];
-        bb[(size_t)i1 * kWave] = make_double2(__builtin_fma(y1, l1.x, l1.z), __builtin_fma(y1, l1.y, l1.w));
-        const double y0 = df2t_step<NT, ZODD>(z, b, a, cur[k].x);
-        const double4 l0 = lo[i0];
-        bb[(size_t)i0 * kWave] = make_double2(__builtin_fma(y0, l0.x, l0.z), __builtin_fma(y0, l0.y, l0.w));
-      }
+    };
+    // sched_barrier pins each refill right after the chunk that freed its
+    // registers, so every chunk's data was requested a full chunk earlier
+    load(ra, nb - 1);
+    load(rb, nb - 2);
+    int64_t c = nb - 1;
+    for (; c >= 1; c -= 2) {
+      run(ra, c);
+      __builtin_amdgcn_sched_barrier(0);
+      load(ra, c - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      run(rb, c - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(rb, c - 3);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (c == 0) run(ra, 0);
   }
   // (the left extension region of the backward pass produces only trimmed
   //  outputs and no state anyone reads: scipy's final zf is discarded)
@@ -200,8 +244,12 @@ __global__ __launch_bounds__(64) void k_bandpass_mix(PskBuffers buf, PskParams p
 
 // ---------------------------------------------------------------------------
 // Low-pass kernels: lane l of wave w handles stream 32*(w&1) + l/2 of group
-// w/2, component l&1 (0 = re, 1 = im).  s2 row of a half-group is 64
-// contiguous doubles, so lane l simply reads element l of that row.
+// w/2, component l&1 (0 = re, 1 = im).
+//
+// The mixer (modem.py:200-201) is numpy's complex multiply (f + 0j) * lo:
+//   re = fma(f, lo_re, -(0*lo_im)),  im = fma(f, lo_im, 0*lo_re)
+// The plan stores, per sample and component, (lo_c, addend_c) so each lane
+// does exactly one fma: bb = fma(f, lo2[n][c].x, lo2[n][c].y).
 //
 // The complex lfilter with real coefficients is two real recurrences EXCEPT
 // for the sign of zero results (scipy evaluates b*x as b*xr - (+0)*xi, ...).
@@ -219,23 +267,32 @@ __device__ __forceinline__ double df2t_lp(double (&z)[NT - 1], const double (&b)
   return y;
 }
 
+constexpr int kLpChunk = 16;                    // samples per low-pass prefetch chunk
+
 template <int NT>
 __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
   const int64_t w = blockIdx.x;                 // wave index = 2*group + half
-  const int64_t g = w >> 1, h = w & 1;
   const int64_t n = p.n;
+  const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int qs = pad & 1;
   const int64_t m2_pairs = (p.m2 + qs + 1) >> 1;
-  const double* __restrict__ in = buf.s2 + ((size_t)g * n * kWave + h * 32) * 2 + lane;   // + n*128
+  const int comp = lane & 1;
+  // f of this lane's stream: pairs at fsrc[p*32]
+  const double2* __restrict__ fsrc = reinterpret_cast<const double2*>(buf.s2) + (size_t)w * n2 * 32 + (lane >> 1);
+  const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;   // lo2[n][comp] at lo[2n]
   double* __restrict__ s3 = buf.s3;
 
   double b[NT], a[NT], z[NT - 1];
 #pragma unroll
   for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
   bool bad = false;
-  auto X = [&](int64_t i) { return in[(size_t)i * 2 * kWave]; };
+  auto X = [&](int64_t i) {                     // mixer output bb[i] for this lane's component
+    const double2 fp = fsrc[(size_t)(i >> 1) * 32];
+    const double2 l = lo[2 * i];
+    return __builtin_fma((i & 1) ? fp.y : fp.x, l.x, l.y);
+  };
 
   const double x0 = X(0), xl = X(n - 1);
   const double e0 = 2.0 * x0 - X(pad);
@@ -249,32 +306,48 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
     bad |= __builtin_amdgcn_class(y, kClsY);
     s3[pair_index(w, m2_pairs, j + qs, lane)] = y;
   }
-  const int64_t n_main = (n / kChunk) * kChunk;
-  {
-    double nxt[kChunk];
+  const int64_t nc = n / kLpChunk;
+  const int64_t n_main = nc * kLpChunk;
+  if (nc > 0) {
+    constexpr int PP = kLpChunk / 2;
+    double2 fa[PP], fb[PP], la[kLpChunk], lb[kLpChunk];
+    auto load = [&](double2 (&fr)[PP], double2 (&lr)[kLpChunk], int64_t c) {
+      const int64_t cc = c < nc ? c : nc - 1;
 #pragma unroll
-    for (int k = 0; k < kChunk; ++k) nxt[k] = (n_main > 0) ? X(k) : 0.0;
-    for (int64_t c = 0; c < n_main; c += kChunk) {
-      double cur[kChunk];
+      for (int k = 0; k < PP; ++k) fr[k] = fsrc[(size_t)(cc * PP + k) * 32];
 #pragma unroll
-      for (int k = 0; k < kChunk; ++k) cur[k] = nxt[k];
-      if (c + kChunk < n_main) {
-#pragma unroll
-        for (int k = 0; k < kChunk; ++k) nxt[k] = X(c + kChunk + k);
-      }
-      const int64_t q0 = pad + qs + c;
+      for (int k = 0; k < kLpChunk; ++k) lr[k] = lo[2 * (cc * kLpChunk + k)];
+    };
+    auto run = [&](const double2 (&fr)[PP], const double2 (&lr)[kLpChunk], int64_t c) {
+      const int64_t q0 = pad + qs + c * kLpChunk;
       double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (size_t)(w * m2_pairs + (q0 >> 1)) * kWave + lane;
 #pragma unroll
-      for (int k = 0; k < kChunk; k += 2) {
-        bad |= __builtin_amdgcn_class(cur[k], kClsX);
-        const double y0 = df2t_lp<NT>(z, b, a, cur[k]);
+      for (int k = 0; k < PP; ++k) {
+        const double e0 = __builtin_fma(fr[k].x, lr[2 * k].x, lr[2 * k].y);
+        const double e1 = __builtin_fma(fr[k].y, lr[2 * k + 1].x, lr[2 * k + 1].y);
+        bad |= __builtin_amdgcn_class(e0, kClsX);
+        const double y0 = df2t_lp<NT>(z, b, a, e0);
         bad |= __builtin_amdgcn_class(y0, kClsY);
-        bad |= __builtin_amdgcn_class(cur[k + 1], kClsX);
-        const double y1 = df2t_lp<NT>(z, b, a, cur[k + 1]);
+        bad |= __builtin_amdgcn_class(e1, kClsX);
+        const double y1 = df2t_lp<NT>(z, b, a, e1);
         bad |= __builtin_amdgcn_class(y1, kClsY);
-        dst[(k >> 1) * kWave] = make_double2(y0, y1);
+        dst[k * kWave] = make_double2(y0, y1);
       }
+    };
+    load(fa, la, 0);
+    load(fb, lb, 1);
+    int64_t c = 0;
+    for (; c + 1 < nc; c += 2) {
+      run(fa, la, c);
+      __builtin_amdgcn_sched_barrier(0);
+      load(fa, la, c + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      run(fb, lb, c + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(fb, lb, c + 3);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (c < nc) run(fa, la, c);
   }
   for (int64_t i = n_main; i < n; ++i) {
     const double e = X(i);
@@ -293,8 +366,8 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
   // stream flag = re lane | im lane
   const int fl = bad ? 1 : 0;
   const int other = __shfl_xor(fl, 1);
-  const int64_t s = g * kWave + h * 32 + (lane >> 1);
-  if ((lane & 1) == 0 && s < buf.n_streams) buf.flags[s] = fl | other;
+  const int64_t s = (w >> 1) * kWave + (w & 1) * 32 + (lane >> 1);
+  if (comp == 0 && s < buf.n_streams) buf.flags[s] = fl | other;
 }
 
 // Exact sector decision of modem.py:216-241 for diff = (dr, di).
@@ -302,18 +375,22 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
 // the sector is read off the signs; near an edge (or for zeros / NaN / inf)
 // the reference's own steps are replayed: atan2, +2pi if negative, and the
 // same four comparisons against the same double constants.
-__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
-  const double adr = fabs(dr), adi = fabs(di);
-  const double d = adi - adr;
-  const double thr = (adr + adi) * 0x1p-30;
-  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
-  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
+__device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
   double ang = atan2(di, dr);
   if (ang < 0) ang += 2 * M_PI;
   if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
   if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
   if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3u;
   return 2u;
+}
+
+__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
+  const double adr = fabs(dr), adi = fabs(di);
+  const double d = adi - adr;
+  const double thr = (adr + adi) * 0x1p-30;
+  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
+  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
+  return qpsk_dibit_slow(dr, di);
 }
 
 // diff = s_{k+1} * conj(s_k) with numpy's complex multiply (see oracle)
@@ -357,6 +434,7 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   int64_t next_n = p.first + k * p.sps;
   double pr = 0.0, pim = 0.0;
   uint32_t acc = 0;
+  const bool qpsk = p.kind == kQpsk;
 
   auto on_output = [&](int64_t i, double y) {
     bad |= __builtin_amdgcn_class(y, kClsY);
@@ -367,7 +445,7 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
         double dr, di;
         diff_np(pr, pim, cr, ci, dr, di);
         int64_t pos;
-        if (p.kind == kQpsk) {
+        if (qpsk) {
           pos = 2 * k;
           acc |= qpsk_dibit(dr, di) << (30 - (pos & 31));
         } else {
@@ -385,33 +463,47 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
     }
   };
 
-  const int64_t n_main = (n / kChunk) * kChunk;
-  const int64_t n_top = n - n_main;
-  for (int64_t i = n - 1; i >= n - n_top; --i)
+  const int64_t nc = n / kLpChunk;
+  const int64_t n_lo = nc * kLpChunk;
+  for (int64_t i = n - 1; i >= n_lo; --i)
     on_output(i, df2t_lp<NT>(z, b, a, s3[pair_index(w, m2_pairs, pad + i + qs, lane)]));
-  {
+  if (nc > 0) {
     const double2* __restrict__ src = reinterpret_cast<const double2*>(s3) + (size_t)w * m2_pairs * kWave + lane;
-    double2 nxt[kChunk / 2];
-    const int64_t cstart = n_main - kChunk;
-    if (n_main > 0) {
+    constexpr int PP = kLpChunk / 2;
+    double2 ra[PP], rb[PP], rc[PP];
+    auto load = [&](double2 (&r)[PP], int64_t c) {
+      const int64_t cc = c < 0 ? 0 : c;
+      const int64_t qp = (pad + qs + cc * kLpChunk) >> 1;
 #pragma unroll
-      for (int kk = 0; kk < kChunk / 2; ++kk) nxt[kk] = src[(size_t)(((pad + qs + cstart) >> 1) + kk) * kWave];
-    }
-    for (int64_t c = cstart; c >= 0; c -= kChunk) {
-      double2 cur[kChunk / 2];
+      for (int kk = 0; kk < PP; ++kk) r[kk] = src[(size_t)(qp + kk) * kWave];
+    };
+    auto run = [&](const double2 (&r)[PP], int64_t c) {
 #pragma unroll
-      for (int kk = 0; kk < kChunk / 2; ++kk) cur[kk] = nxt[kk];
-      if (c >= kChunk) {
-        const int64_t qp = (pad + qs + c - kChunk) >> 1;
-#pragma unroll
-        for (int kk = 0; kk < kChunk / 2; ++kk) nxt[kk] = src[(size_t)(qp + kk) * kWave];
+      for (int kk = PP - 1; kk >= 0; --kk) {
+        on_output(c * kLpChunk + 2 * kk + 1, df2t_lp<NT>(z, b, a, r[kk].y));
+        on_output(c * kLpChunk + 2 * kk, df2t_lp<NT>(z, b, a, r[kk].x));
       }
-#pragma unroll
-      for (int kk = kChunk / 2 - 1; kk >= 0; --kk) {
-        on_output(c + 2 * kk + 1, df2t_lp<NT>(z, b, a, cur[kk].y));
-        on_output(c + 2 * kk, df2t_lp<NT>(z, b, a, cur[kk].x));
-      }
+    };
+    load(ra, nc - 1);
+    load(rb, nc - 2);
+    load(rc, nc - 3);
+    int64_t c = nc - 1;
+    for (; c >= 2; c -= 3) {
+      run(ra, c);
+      __builtin_amdgcn_sched_barrier(0);
+      load(ra, c - 3);
+      __builtin_amdgcn_sched_barrier(0);
+      run(rb, c - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(rb, c - 4);
+      __builtin_amdgcn_sched_barrier(0);
+      run(rc, c - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      load(rc, c - 5);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (c >= 0) run(ra, c);
+    if (c >= 1) run(rb, c - 1);
   }
   // left-extension outputs are trimmed but still pass through the detector
   for (int j = pad - 1; j >= 0; --j) {
@@ -425,7 +517,7 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
 
 // ---------------------------------------------------------------------------
 // K3x: exact complex low-pass (scipy CDOUBLE_filt semantics) for flagged
-// streams only.  lane = stream; scratch reuses s3 as [group][q][64] double2.
+// streams only.  lane = stream; scratch reuses s3 as [group][j][64] double2.
 template <int NT>
 __device__ __forceinline__ void df2t_cplx_step(double (&zr)[NT - 1], double (&zc)[NT - 1],
                                                const double (&b)[NT], const double (&a)[NT],
@@ -458,9 +550,10 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
   const bool live = s < buf.n_streams && buf.flags[s] != 0;
   if (!__any(live)) return;                     // wave-uniform early exit (the common case)
   const int64_t n = p.n;
+  const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int64_t m2 = p.m2;
-  const double2* __restrict__ bb = reinterpret_cast<const double2*>(buf.s2) + (size_t)g * n * kWave + lane;
+  const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
   double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)g * m2 * kWave + lane;
   uint32_t* __restrict__ words = buf.words + (size_t)(s < buf.n_streams ? s : 0) * p.n_words;
 
@@ -468,15 +561,20 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 #pragma unroll
   for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
 
+  auto bb = [&](int64_t i) -> double2 {         // (f + 0j) * lo[i], numpy's complex multiply
+    const double fv = buf.s2[f_index(g, n2, i, lane)];
+    const double4 l = lo[i];
+    return make_double2(__builtin_fma(fv, l.x, l.y), __builtin_fma(fv, l.z, l.w));
+  };
   // odd extension with numpy complex ops: (2+0j)*x[0] - x[k]
-  const double2 x0 = bb[0], xl = bb[(size_t)(n - 1) * kWave];
+  const double2 x0 = bb(0), xl = bb(n - 1);
   double l2r, l2i, r2r, r2i;
   cmul_np(2.0, 0.0, x0.x, x0.y, l2r, l2i);
   cmul_np(2.0, 0.0, xl.x, xl.y, r2r, r2i);
   auto ext = [&](int64_t j) -> double2 {
-    if (j < pad) { const double2 v = bb[(size_t)(pad - j) * kWave]; return make_double2(l2r - v.x, l2i - v.y); }
-    if (j < pad + n) return bb[(size_t)(j - pad) * kWave];
-    const double2 v = bb[(size_t)(n - 2 - (j - pad - n)) * kWave];
+    if (j < pad) { const double2 v = bb(pad - j); return make_double2(l2r - v.x, l2i - v.y); }
+    if (j < pad + n) return bb(j - pad);
+    const double2 v = bb(n - 2 - (j - pad - n));
     return make_double2(r2r - v.x, r2i - v.y);
   };
   {
@@ -533,10 +631,10 @@ template <typename T>
 static hipError_t launch_bp(int nt, bool zodd, const PskBuffers& b, const PskParams& p, const Iir& f,
                             hipStream_t st, int64_t groups) {
   dim3 grid((unsigned)groups), block(kWave);
-  if (nt == 9 && zodd) { hipLaunchKernelGGL((k_bandpass_mix<9, true, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 9) { hipLaunchKernelGGL((k_bandpass_mix<9, false, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 7 && zodd) { hipLaunchKernelGGL((k_bandpass_mix<7, true, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 7) { hipLaunchKernelGGL((k_bandpass_mix<7, false, T>), grid, block, 0, st, b, p, f); }
+  if (nt == 9 && zodd) { hipLaunchKernelGGL((k_bandpass<9, true, T>), grid, block, 0, st, b, p, f); }
+  else if (nt == 9) { hipLaunchKernelGGL((k_bandpass<9, false, T>), grid, block, 0, st, b, p, f); }
+  else if (nt == 7 && zodd) { hipLaunchKernelGGL((k_bandpass<7, true, T>), grid, block, 0, st, b, p, f); }
+  else if (nt == 7) { hipLaunchKernelGGL((k_bandpass<7, false, T>), grid, block, 0, st, b, p, f); }
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }
