@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -19,6 +20,7 @@ hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, 
 hipError_t launch_psk_lowpass_fwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_lowpass_bwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_lowpass_exact(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_slice(const PskBuffers&, const PskParams&, hipStream_t);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
                             hipStream_t);
 hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, uint8_t*, int64_t, int64_t*,
@@ -271,7 +273,8 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
-      {(void**)&pl->s1, g * pl->m1_pairs * kWave * 16},
+      // s1 doubles as the symbol buffer [2G][S][64] after K1 (sym_index in psk_kernels.hip)
+      {(void**)&pl->s1, std::max(g * pl->m1_pairs * kWave * 16, 2 * g * std::max<int64_t>(p.n_sym, 1) * kWave * 8)},
       {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16},
       {(void**)&pl->s3, 2 * g * pl->m2_pairs * kWave * 16},
       {(void**)&pl->words, g * kWave * p.n_words * 4},
@@ -388,7 +391,20 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   b.out_stride = out_stride;
   b.out_len = d_len;
   b.sync_idx = d_sync;
+  // AMR_SYNC_EACH_KERNEL=1: synchronise after every launch so a fault names its kernel
+  static const bool sync_each = [] {
+    const char* e = std::getenv("AMR_SYNC_EACH_KERNEL");
+    return e && e[0] == '1';
+  }();
   auto mark = [&](int slot, int which) -> hipError_t {
+    if (sync_each && which == 1) {
+      hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) {
+        static const char* names[] = {"bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "slice+sync_pack", "fec"};
+        std::fprintf(stderr, "[amr] kernel slot %s failed: %s\n", names[slot], hipGetErrorString(e));
+        return e;
+      }
+    }
     if (!pl->timing) return hipSuccess;
     pl->ev_used[slot] = true;
     return hipEventRecord(pl->ev[slot][which], st);
@@ -416,6 +432,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(launch_psk_lowpass_exact(b, pl->p, pl->lp, st));
     HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
+    HIP_TRY(launch_psk_slice(b, pl->p, st));
     HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
   }

@@ -19,12 +19,13 @@
 //                      real filtered signal f to s2.
 //   K2 k_lowpass_fwd   lane = (stream, re|im): LO mixer (numpy's complex
 //                      multiply) fused into the low-pass forward pass -> s3
-//   K3 k_lowpass_bwd   lane = (stream, re|im): low-pass backward pass fused
-//                      with symbol pick, differential product, slicer and the
-//                      bit writer -> words
+//   K3 k_lowpass_bwd   lane = (stream, re|im): low-pass backward pass; the
+//                      baseband at each symbol centre goes to the symbol buffer
+//   K4a k_slice        thread = (stream, output word): differential product,
+//                      QPSK/BPSK slicer, bit packing -> words (fully parallel)
 //   K3x k_lowpass_exact lane = stream: the complex low-pass with scipy's full
 //                      signed-zero semantics, only for streams K2/K3 flagged
-//   (K4 sync + pack lives in util_kernels.hip)
+//   (K4b sync + pack lives in util_kernels.hip)
 //
 // Every wave runs alone on its SIMD (the batch of 4096 streams is only
 // 64-128 waves), so each kernel is bound by its per-sample instruction stream;
@@ -370,34 +371,11 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
   if (comp == 0 && s < buf.n_streams) buf.flags[s] = fl | other;
 }
 
-// Exact sector decision of modem.py:216-241 for diff = (dr, di).
-// Far from a sector edge (|di| vs |dr| differ by more than 2^-30 relative)
-// the sector is read off the signs; near an edge (or for zeros / NaN / inf)
-// the reference's own steps are replayed: atan2, +2pi if negative, and the
-// same four comparisons against the same double constants.
-__device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
-  double ang = atan2(di, dr);
-  if (ang < 0) ang += 2 * M_PI;
-  if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
-  if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
-  if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3u;
-  return 2u;
-}
-
-__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
-  const double adr = fabs(dr), adi = fabs(di);
-  const double d = adi - adr;
-  const double thr = (adr + adi) * 0x1p-30;
-  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
-  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
-  return qpsk_dibit_slow(dr, di);
-}
-
-// diff = s_{k+1} * conj(s_k) with numpy's complex multiply (see oracle)
-__device__ __forceinline__ void diff_np(double ar, double ai, double sr, double si, double& dr, double& di) {
-  const double br = sr, bi = -si;
-  dr = __builtin_fma(ar, br, -(ai * bi));
-  di = __builtin_fma(ar, bi, ai * br);
+// Symbol buffer (reuses s1, free after K1): the baseband sample of every
+// symbol, time-major per low-pass wave: sym[w][k][64 lanes] doubles, i.e. as
+// double2 (re, im) at ((w*S + k)*32 + stream-in-half).
+__device__ __forceinline__ size_t sym_index(int64_t w, int64_t n_sym, int64_t k, int lane) {
+  return (size_t)((w * n_sym + k) * kWave + lane);
 }
 
 template <int NT>
@@ -411,10 +389,9 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   const int64_t m2 = p.m2;
   const int64_t m2_pairs = (m2 + qs + 1) >> 1;
   const double* __restrict__ s3 = buf.s3;
+  double* __restrict__ sym = buf.s1;
+  const int64_t S = p.n_sym;
   const int64_t s = g * kWave + h * 32 + (lane >> 1);
-  const bool is_re = (lane & 1) == 0;
-  const bool writer = is_re && s < buf.n_streams;
-  uint32_t* __restrict__ words = buf.words + (size_t)(s < buf.n_streams ? s : 0) * p.n_words;
 
   double b[NT], a[NT], z[NT - 1];
 #pragma unroll
@@ -429,37 +406,15 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
     bad |= __builtin_amdgcn_class(y, kClsY);
   }
 
-  // symbols k = S-1 .. 0 at baseband index first + k*sps
-  int64_t k = p.n_sym - 1;
+  // symbols k = S-1 .. 0 sit at baseband index first + k*sps (modem.py:209 / :93)
+  int64_t k = S - 1;
   int64_t next_n = p.first + k * p.sps;
-  double pr = 0.0, pim = 0.0;
-  uint32_t acc = 0;
-  const bool qpsk = p.kind == kQpsk;
-
   auto on_output = [&](int64_t i, double y) {
     bad |= __builtin_amdgcn_class(y, kClsY);
-    if (i == next_n) {                          // uniform branch
-      const double other = __shfl_xor(y, 1);
-      const double cr = is_re ? y : other, ci = is_re ? other : y;
-      if (k < p.n_sym - 1) {                    // diff index k: s_{k+1} * conj(s_k)
-        double dr, di;
-        diff_np(pr, pim, cr, ci, dr, di);
-        int64_t pos;
-        if (qpsk) {
-          pos = 2 * k;
-          acc |= qpsk_dibit(dr, di) << (30 - (pos & 31));
-        } else {
-          pos = k;
-          acc |= (dr < 0 ? 1u : 0u) << (31 - (pos & 31));
-        }
-        if ((pos & 31) == 0) {
-          if (writer) words[pos >> 5] = acc;
-          acc = 0;
-        }
-      }
-      pr = cr; pim = ci;
+    if (i == next_n) {                          // uniform branch: one store per symbol
+      sym[sym_index(w, S, k, lane)] = y;
       --k;
-      next_n -= p.sps;
+      next_n = k >= 0 ? next_n - p.sps : -1;   // BPSK: first == sps, so index 0 is not a symbol
     }
   };
 
@@ -512,12 +467,13 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   }
   const int fl = bad ? 1 : 0;
   const int other = __shfl_xor(fl, 1);
-  if (writer) buf.flags[s] |= (fl | other);
+  if ((lane & 1) == 0 && s < buf.n_streams) buf.flags[s] |= (fl | other);
 }
 
 // ---------------------------------------------------------------------------
 // K3x: exact complex low-pass (scipy CDOUBLE_filt semantics) for flagged
-// streams only.  lane = stream; scratch reuses s3 as [group][j][64] double2.
+// streams only.  lane = stream; scratch reuses s3 as [group][j][64] double2;
+// writes its symbols into the same sym buffer K3 fills.
 template <int NT>
 __device__ __forceinline__ void df2t_cplx_step(double (&zr)[NT - 1], double (&zc)[NT - 1],
                                                const double (&b)[NT], const double (&a)[NT],
@@ -553,9 +509,12 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
   const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int64_t m2 = p.m2;
+  const int64_t S = p.n_sym;
   const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
   double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)g * m2 * kWave + lane;
-  uint32_t* __restrict__ words = buf.words + (size_t)(s < buf.n_streams ? s : 0) * p.n_words;
+  double2* __restrict__ sym2 = reinterpret_cast<double2*>(buf.s1);
+  const int64_t wq = 2 * g + (lane >> 5);       // the low-pass wave that owns this stream
+  const int sl = lane & 31;
 
   double b[NT], a[NT], zr[NT - 1], zc[NT - 1];
 #pragma unroll
@@ -592,37 +551,80 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 #pragma unroll
   for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, y0, y1, zr[i], zc[i]);
 
-  int64_t k = p.n_sym - 1;
+  int64_t k = S - 1;
   int64_t next_n = p.first + k * p.sps;
-  double pr = 0.0, pim = 0.0;
-  uint32_t acc = 0;
   for (int64_t j = m2 - 1; j >= 0; --j) {
     const double2 e = sc[(size_t)j * kWave];
     double o0, o1;
     df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
-    const int64_t i = j - pad;
-    if (i == next_n && k >= 0) {
-      if (k < p.n_sym - 1) {
-        double dr, di;
-        diff_np(pr, pim, o0, o1, dr, di);
-        int64_t pos;
-        if (p.kind == kQpsk) {
-          pos = 2 * k;
-          acc |= qpsk_dibit(dr, di) << (30 - (pos & 31));
-        } else {
-          pos = k;
-          acc |= (dr < 0 ? 1u : 0u) << (31 - (pos & 31));
-        }
-        if ((pos & 31) == 0) {
-          if (live) words[pos >> 5] = acc;
-          acc = 0;
-        }
-      }
-      pr = o0; pim = o1;
+    if (j - pad == next_n && k >= 0) {
+      if (live) sym2[(size_t)(wq * S + k) * 32 + sl] = make_double2(o0, o1);
       --k;
       next_n -= p.sps;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// K4a: differential product + slicer + bit packing, fully parallel.
+// One thread per (stream, 32-bit output word): word j holds the bits of diff
+// indices [16j, 16j+16) (QPSK, 2 bits each) or [32j, 32j+32) (BPSK).
+//   diff = s[k+1] * conj(s[k])   numpy complex multiply   modem.py:100, 214
+//   QPSK sectors                                          modem.py:216-241
+//   BPSK real(diff) < 0 -> 1                              modem.py:103-105
+// Sector decision: far from a sector edge (|di| vs |dr| differ by more than
+// 2^-30 relative) the sector is read off the signs; near an edge (or for
+// zeros / NaN / inf) the reference's own steps are replayed: atan2, +2pi if
+// negative, the same four comparisons against the same double constants.
+__device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
+  double ang = atan2(di, dr);
+  if (ang < 0) ang += 2 * M_PI;
+  if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
+  if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
+  if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3u;
+  return 2u;
+}
+
+__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
+  const double adr = fabs(dr), adi = fabs(di);
+  const double d = adi - adr;
+  const double thr = (adr + adi) * 0x1p-30;
+  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
+  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
+  return qpsk_dibit_slow(dr, di);
+}
+
+__global__ __launch_bounds__(64) void k_slice(PskBuffers buf, PskParams p) {
+  const int64_t j = blockIdx.x;                 // word index
+  const int64_t s = (int64_t)blockIdx.y * kWave + threadIdx.x;
+  if (s >= buf.n_streams) return;
+  const int64_t S = p.n_sym;
+  const bool qpsk = p.kind == kQpsk;
+  const int per = qpsk ? 16 : 32;
+  const int64_t k0 = j * per;
+  const int64_t nd = S - 1;                     // number of diffs
+  const double2* __restrict__ sym2 = reinterpret_cast<const double2*>(buf.s1);
+  const int64_t wq = s >> 5;
+  const int sl = (int)(s & 31);
+  auto SYM = [&](int64_t k) { return sym2[(size_t)(wq * S + k) * 32 + sl]; };
+  uint32_t word = 0;
+  double2 prev = SYM(k0 < S ? k0 : S - 1);
+  for (int u = 0; u < per; ++u) {
+    const int64_t k = k0 + u;
+    if (k >= nd) break;
+    const double2 nx = SYM(k + 1);
+    // diff_k = s_{k+1} * conj(s_k): numpy fma form (see oracle)
+    const double br = prev.x, bi = -prev.y;
+    const double dr = __builtin_fma(nx.x, br, -(nx.y * bi));
+    if (qpsk) {
+      const double di = __builtin_fma(nx.x, bi, nx.y * br);
+      word |= qpsk_dibit(dr, di) << (30 - 2 * u);
+    } else {
+      word |= (dr < 0 ? 1u : 0u) << (31 - u);
+    }
+    prev = nx;
+  }
+  buf.words[(size_t)s * p.n_words + j] = word;
 }
 
 // ---------------------------------------------------------------------------
@@ -660,6 +662,13 @@ hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_lowpass_bwd<5>), dim3((unsigned)(2 * groups)), dim3(kWave), 0, st, b, p, f);
+  return hipGetLastError();
+}
+
+hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t st) {
+  const int64_t groups = (b.n_streams + kWave - 1) / kWave;
+  if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
+  hipLaunchKernelGGL(k_slice, dim3((unsigned)p.n_words, (unsigned)groups), dim3(kWave), 0, st, b, p);
   return hipGetLastError();
 }
 
