@@ -17,10 +17,11 @@
 //                      LDS transpose tile and writes s1; the backward pass
 //                      streams s1 back (register prefetch ring) and writes the
 //                      real filtered signal f to s2.
-//   K2 k_lowpass_fwd   lane = (stream, re|im): LO mixer (numpy's complex
-//                      multiply) fused into the low-pass forward pass -> s3
-//   K3 k_lowpass_bwd   lane = (stream, re|im): low-pass backward pass; the
-//                      baseband at each symbol centre goes to the symbol buffer
+//   K2 k_lowpass_fwd   lane quad = stream (re/im x 2-lane state split): LO
+//                      mixer (numpy's complex multiply) fused into the
+//                      low-pass forward pass -> s3
+//   K3 k_lowpass_bwd   same lanes: low-pass backward pass; the baseband at
+//                      each symbol centre goes to the symbol buffer
 //   K4a k_slice        thread = (stream, output word): differential product,
 //                      QPSK/BPSK slicer, bit packing -> words (fully parallel)
 //   K3x k_lowpass_exact lane = stream: the complex low-pass with scipy's full
@@ -33,6 +34,7 @@
 // a whole chunk of compute to land (tools/fp64_probe.hip measured the
 // register-only band-pass step at 126 cycles/sample).
 #include <math.h>
+#include <stdlib.h>
 
 #include "amr_internal.h"
 
@@ -244,8 +246,202 @@ __global__ __launch_bounds__(64) void k_bandpass(PskBuffers buf, PskParams p, Ii
 }
 
 // ---------------------------------------------------------------------------
-// Low-pass kernels: lane l of wave w handles stream 32*(w&1) + l/2 of group
-// w/2, component l&1 (0 = re, 1 = im).
+// K1q: the 9-tap band-pass with its 8 states SPLIT ACROSS A LANE QUAD.
+// A lone wave on a SIMD is bound by the length of its per-sample instruction
+// stream, and at the benchmark batch (4096 streams = 64 lane-per-stream waves)
+// three quarters of the chip would sit idle.  Here lane j of quad q owns
+// states z[2j], z[2j+1] of stream q; the wave serves 16 streams, so the
+// batch fills 4x the SIMDs and each wave issues 16 VALU per sample instead of
+// 31.  Arithmetic is unchanged, op for op:
+//   y       = z0 + b0*x                       (lane 0 of the quad, broadcast by DPP)
+//   z[2j]   = (z[2j+1] + x*b[2j+1]) - y*a[2j+1]
+//   z[2j+1] = (z[2j+2] + x*b[2j+2]) - y*a[2j+2]   z[2j+2] = lane j+1's old z[2j]
+// and for the top state (lane 3) the missing z[8] is -0.0, so
+// (-0.0 + x*b8) - y*a8 == x*b8 - y*a8 bit for bit (also for signed zeros).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long u = __builtin_bit_cast(long long, v);
+  // every source lane of a quad_perm is valid, so no "old" value is needed
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffff), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+constexpr int kQuadBcast0 = 0x00;   // quad_perm [0,0,0,0]
+constexpr int kQuadNext = 0xF9;     // quad_perm [1,2,3,3]
+
+struct QuadIir {
+  double b0, cAb, cAa, cBb, cBa;
+  bool top;                         // lane 3 of the quad
+};
+
+__device__ __forceinline__ double quad_step(const QuadIir& c, double& zA, double& zB, double x) {
+  const double t = zA + c.b0 * x;
+  const double y = dpp_f64<kQuadBcast0>(t);
+  double zC = dpp_f64<kQuadNext>(zA);
+  zC = c.top ? -0.0 : zC;
+  const double nA = (zB + x * c.cAb) - y * c.cAa;
+  const double nB = (zC + x * c.cBb) - y * c.cBa;
+  zA = nA;
+  zB = nB;
+  return y;
+}
+
+// s1 for K1q: [g16][q/2][16 streams][2] doubles
+__device__ __forceinline__ size_t pair16_index(int64_t g16, int64_t m_pairs, int64_t q, int sq) {
+  return ((size_t)(g16 * m_pairs + (q >> 1)) * 16 + sq) * 2 + (q & 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_bandpass_quad(PskBuffers buf, PskParams p, Iir f) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[2][16][kTilePitch];
+  constexpr int TS = kTileBytes / (int)sizeof(T);
+  const int lane = threadIdx.x;
+  const int j = lane & 3, sq = lane >> 2;
+  const int64_t g16 = blockIdx.x;
+  const int64_t s = g16 * 16 + sq;
+  const int64_t last = buf.n_streams - 1;
+  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
+  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad1;
+  const int64_t m1 = p.m1;
+  const int qs = pad & 1;
+  const int64_t m1_pairs = (m1 + qs + 1) >> 1;
+  double* __restrict__ s1 = buf.s1;
+
+  QuadIir c;
+  c.b0 = f.b[0];
+  c.cAb = j == 0 ? f.b[1] : j == 1 ? f.b[3] : j == 2 ? f.b[5] : f.b[7];
+  c.cAa = j == 0 ? f.a[1] : j == 1 ? f.a[3] : j == 2 ? f.a[5] : f.a[7];
+  c.cBb = j == 0 ? f.b[2] : j == 1 ? f.b[4] : j == 2 ? f.b[6] : f.b[8];
+  c.cBa = j == 0 ? f.a[2] : j == 1 ? f.a[4] : j == 2 ? f.a[6] : f.a[8];
+  c.top = j == 3;
+  const double ziA = j == 0 ? f.zi[0] : j == 1 ? f.zi[2] : j == 2 ? f.zi[4] : f.zi[6];
+  const double ziB = j == 0 ? f.zi[1] : j == 1 ? f.zi[3] : j == 2 ? f.zi[5] : f.zi[7];
+  double zA, zB;
+
+  // ---- forward pass -------------------------------------------------------
+  const T x0 = x[0], xl = x[n - 1];
+  {
+    const double e0 = In<T>::ext(x0, x[pad]);
+    zA = ziA * e0;
+    zB = ziB * e0;
+  }
+  for (int jj = 0; jj < pad; ++jj) {
+    const double y = quad_step(c, zA, zB, In<T>::ext(x0, x[pad - jj]));
+    s1[pair16_index(g16, m1_pairs, jj + qs, sq)] = y;
+  }
+  const int64_t n_tiles = n / TS;
+  const int64_t n_main = n_tiles * TS;
+  if (n_tiles > 0) {
+    const int rsub = lane >> 4, cb = (lane & 15) * 16;
+    const uint8_t* rowp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t rs = g16 * 16 + 4 * i + rsub;
+      rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * buf.x_stride) + cb;
+    }
+    v4u r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&tile[0][4 * i + rsub][cb]) = r[i];
+    for (int64_t t = 0; t < n_tiles; ++t) {
+      const int cur = (int)(t & 1);
+      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + tn * kTileBytes);
+      __builtin_amdgcn_sched_barrier(0);
+      const int64_t q0 = pad + qs + t * TS;
+      double2* __restrict__ dst = reinterpret_cast<double2*>(s1) + (size_t)(g16 * m1_pairs + (q0 >> 1)) * 16 + sq;
+      constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+      for (int k = 0; k < TS; k += PER) {
+        const v4u v = *reinterpret_cast<const v4u*>(&tile[cur][sq][k * sizeof(T)]);
+        T xs[PER];
+        __builtin_memcpy(xs, &v, 16);
+#pragma unroll
+        for (int u = 0; u < PER; u += 2) {
+          const double y0 = quad_step(c, zA, zB, In<T>::cvt(xs[u]));
+          const double y1 = quad_step(c, zA, zB, In<T>::cvt(xs[u + 1]));
+          dst[((k + u) >> 1) * 16] = make_double2(y0, y1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&tile[cur ^ 1][4 * i + rsub][cb]) = r[i];
+    }
+  }
+  for (int64_t i = n_main; i < n; ++i) {
+    const double y = quad_step(c, zA, zB, In<T>::cvt(x[i]));
+    s1[pair16_index(g16, m1_pairs, pad + i + qs, sq)] = y;
+  }
+  double ylast = 0.0;
+  for (int jj = 0; jj < pad; ++jj) {
+    ylast = quad_step(c, zA, zB, In<T>::ext(xl, x[n - 2 - jj]));
+    s1[pair16_index(g16, m1_pairs, pad + n + jj + qs, sq)] = ylast;
+  }
+  __threadfence();
+
+  // ---- backward pass ------------------------------------------------------
+  zA = ziA * ylast;
+  zB = ziB * ylast;
+  for (int64_t jj = m1 - 1; jj >= pad + n; --jj)
+    (void)quad_step(c, zA, zB, s1[pair16_index(g16, m1_pairs, jj + qs, sq)]);
+
+  const int64_t n2 = (n + 1) >> 1;
+  double* __restrict__ fo = buf.s2;
+  const int64_t sgrp = s >> 6;
+  const int sig = (int)(s & 63);
+  const int64_t nb = n / kBwdChunk;
+  const int64_t n_lo = nb * kBwdChunk;
+  for (int64_t i = n - 1; i >= n_lo; --i) {
+    const double y = quad_step(c, zA, zB, s1[pair16_index(g16, m1_pairs, pad + i + qs, sq)]);
+    fo[f_index(sgrp, n2, i, sig)] = y;
+  }
+  if (nb > 0) {
+    const double2* __restrict__ src = reinterpret_cast<const double2*>(s1) + (size_t)g16 * m1_pairs * 16 + sq;
+    double2* __restrict__ dst = reinterpret_cast<double2*>(fo);
+    const size_t fbase = (size_t)((sgrp * 2 + (sig >> 5)) * n2) * 32 + (sig & 31);
+    constexpr int PP = kBwdChunk / 2;
+    double2 ra[PP], rb[PP];
+    auto load = [&](double2 (&r)[PP], int64_t cc0) {
+      const int64_t cc = cc0 < 0 ? 0 : cc0;
+      const int64_t qp = (pad + qs + cc * kBwdChunk) >> 1;
+#pragma unroll
+      for (int k = 0; k < PP; ++k) r[k] = src[(size_t)(qp + k) * 16];
+    };
+    auto run = [&](const double2 (&r)[PP], int64_t cc) {
+#pragma unroll
+      for (int k = PP - 1; k >= 0; --k) {
+        const double y1 = quad_step(c, zA, zB, r[k].y);
+        const double y0 = quad_step(c, zA, zB, r[k].x);
+        dst[fbase + (size_t)(cc * PP + k) * 32] = make_double2(y0, y1);
+      }
+    };
+    load(ra, nb - 1);
+    load(rb, nb - 2);
+    int64_t cc = nb - 1;
+    for (; cc >= 1; cc -= 2) {
+      run(ra, cc);
+      __builtin_amdgcn_sched_barrier(0);
+      load(ra, cc - 2);
+      __builtin_amdgcn_sched_barrier(0);
+      run(rb, cc - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      load(rb, cc - 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cc == 0) run(ra, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Low-pass kernels K2/K3.  A lane QUAD serves one stream: lanes
+// (re, j=0), (re, j=1), (im, j=0), (im, j=1); lane j of a pair owns states
+// z[2j], z[2j+1] of that component's 5-tap recurrence (the same DPP split
+// as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1, -0.0 above
+// the top state).  A wave serves 16 streams.
 //
 // The mixer (modem.py:200-201) is numpy's complex multiply (f + 0j) * lo:
 //   re = fma(f, lo_re, -(0*lo_im)),  im = fma(f, lo_im, 0*lo_re)
@@ -254,41 +450,80 @@ __global__ __launch_bounds__(64) void k_bandpass(PskBuffers buf, PskParams p, Ii
 //
 // The complex lfilter with real coefficients is two real recurrences EXCEPT
 // for the sign of zero results (scipy evaluates b*x as b*xr - (+0)*xi, ...).
-// K2/K3 run the separable recurrences and flag a stream whenever an operand
-// could make the two differ (kClsX/kClsY above; DESIGN.md §Numerics proves the
-// rule); K3x then recomputes that stream with the full complex semantics.
+// The separable recurrences are exact whenever every tap product is a
+// non-zero finite number, which holds when every input
+// and output magnitude is >= 2^-1022 and nothing is inf/NaN.  K2/K3 track
+// min|x|, min|y| (one v_min_f64 each) and test the final states for
+// finiteness (NaN/inf are sticky in the recurrence); a stream that fails is
+// flagged and K3x recomputes it with the full complex semantics.  The single
+// sample that is +0 by construction (bb_im[0]: lo_im[0] == -0) is judged by
+// its class instead: +0 there is provably harmless.
+constexpr int kLpChunk = 16;                    // samples per low-pass prefetch chunk
+constexpr int kPairBcast = 0xA0;                // quad_perm [0,0,2,2]
+constexpr int kPairNext = 0xF5;                 // quad_perm [1,1,3,3]
+constexpr double kMinNormal = 0x1p-1022;
 
-template <int NT>
-__device__ __forceinline__ double df2t_lp(double (&z)[NT - 1], const double (&b)[NT],
-                                          const double (&a)[NT], double x) {
-  const double y = z[0] + b[0] * x;
-#pragma unroll
-  for (int i = 0; i < NT - 2; ++i) z[i] = (z[i + 1] + x * b[i + 1]) - y * a[i + 1];
-  z[NT - 2] = x * b[NT - 1] - y * a[NT - 1];
+struct PairIir {
+  double b0, cAb, cAa, cBb, cBa;
+  bool top;                                     // j == 1
+};
+
+__device__ __forceinline__ double pair_step(const PairIir& c, double& zA, double& zB, double x) {
+  const double t = zA + c.b0 * x;
+  const double y = dpp_f64<kPairBcast>(t);
+  double zC = dpp_f64<kPairNext>(zA);
+  zC = c.top ? -0.0 : zC;
+  const double nA = (zB + x * c.cAb) - y * c.cAa;
+  const double nB = (zC + x * c.cBb) - y * c.cBa;
+  zA = nA;
+  zB = nB;
   return y;
 }
 
-constexpr int kLpChunk = 16;                    // samples per low-pass prefetch chunk
+__device__ __forceinline__ PairIir pair_coef(const Iir& f, int j, double& ziA, double& ziB) {
+  PairIir c;
+  c.b0 = f.b[0];
+  c.cAb = j ? f.b[3] : f.b[1];
+  c.cAa = j ? f.a[3] : f.a[1];
+  c.cBb = j ? f.b[4] : f.b[2];
+  c.cBa = j ? f.a[4] : f.a[2];
+  c.top = j == 1;
+  ziA = j ? f.zi[2] : f.zi[0];
+  ziB = j ? f.zi[3] : f.zi[1];
+  return c;
+}
 
-template <int NT>
+// s3: [w16][q/2][16 streams][2 comps] double2 (a pair of samples)
+__device__ __forceinline__ size_t s3_index(int64_t w16, int64_t m_pairs, int64_t q, int sq, int comp) {
+  return ((((size_t)(w16 * m_pairs + (q >> 1)) * 16 + sq) * 2 + comp) * 2) + (q & 1);
+}
+
+// Symbol buffer (reuses s1, free after K1): the baseband sample of every
+// symbol: sym[s/32][k][32 streams][re, im] doubles.
+__device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k, int comp) {
+  return ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2 + comp;
+}
+
 __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
-  const int64_t w = blockIdx.x;                 // wave index = 2*group + half
+  const int j = lane & 1, comp = (lane >> 1) & 1, sq = lane >> 2;
+  const int64_t w16 = blockIdx.x;
+  const int64_t s = w16 * 16 + sq;
   const int64_t n = p.n;
   const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int qs = pad & 1;
   const int64_t m2_pairs = (p.m2 + qs + 1) >> 1;
-  const int comp = lane & 1;
-  // f of this lane's stream: pairs at fsrc[p*32]
-  const double2* __restrict__ fsrc = reinterpret_cast<const double2*>(buf.s2) + (size_t)w * n2 * 32 + (lane >> 1);
+  const double2* __restrict__ fsrc =
+      reinterpret_cast<const double2*>(buf.s2) + (size_t)((s >> 6) * 2 + ((s >> 5) & 1)) * n2 * 32 + (s & 31);
   const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;   // lo2[n][comp] at lo[2n]
   double* __restrict__ s3 = buf.s3;
 
-  double b[NT], a[NT], z[NT - 1];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
+  double ziA, ziB;
+  const PairIir c = pair_coef(f, j, ziA, ziB);
+  double zA, zB;
   bool bad = false;
+  double xmin = __builtin_inf(), ymin = __builtin_inf();
   auto X = [&](int64_t i) {                     // mixer output bb[i] for this lane's component
     const double2 fp = fsrc[(size_t)(i >> 1) * 32];
     const double2 l = lo[2 * i];
@@ -296,93 +531,88 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
   };
 
   const double x0 = X(0), xl = X(n - 1);
+  bad |= __builtin_amdgcn_class(x0, kClsX);     // bb[0]: +0 allowed (see above)
   const double e0 = 2.0 * x0 - X(pad);
   bad |= __builtin_amdgcn_class(e0, kClsY);     // zi * ext[0] must not meet a zero
-#pragma unroll
-  for (int i = 0; i < NT - 1; ++i) z[i] = f.zi[i] * e0;
-  for (int j = 0; j < pad; ++j) {
-    const double e = 2.0 * x0 - X(pad - j);
-    bad |= __builtin_amdgcn_class(e, kClsX);
-    const double y = df2t_lp<NT>(z, b, a, e);
-    bad |= __builtin_amdgcn_class(y, kClsY);
-    s3[pair_index(w, m2_pairs, j + qs, lane)] = y;
+  zA = ziA * e0;
+  zB = ziB * e0;
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * x0 - X(pad - jj);
+    xmin = fmin(xmin, fabs(e));
+    const double y = pair_step(c, zA, zB, e);
+    ymin = fmin(ymin, fabs(y));
+    s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)] = y;
   }
   const int64_t nc = n / kLpChunk;
   const int64_t n_main = nc * kLpChunk;
   if (nc > 0) {
     constexpr int PP = kLpChunk / 2;
     double2 fa[PP], fb[PP], la[kLpChunk], lb[kLpChunk];
-    auto load = [&](double2 (&fr)[PP], double2 (&lr)[kLpChunk], int64_t c) {
-      const int64_t cc = c < nc ? c : nc - 1;
+    auto load = [&](double2 (&fr)[PP], double2 (&lr)[kLpChunk], int64_t cc0) {
+      const int64_t cc = cc0 < nc ? cc0 : nc - 1;
 #pragma unroll
       for (int k = 0; k < PP; ++k) fr[k] = fsrc[(size_t)(cc * PP + k) * 32];
 #pragma unroll
       for (int k = 0; k < kLpChunk; ++k) lr[k] = lo[2 * (cc * kLpChunk + k)];
     };
-    auto run = [&](const double2 (&fr)[PP], const double2 (&lr)[kLpChunk], int64_t c) {
-      const int64_t q0 = pad + qs + c * kLpChunk;
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (size_t)(w * m2_pairs + (q0 >> 1)) * kWave + lane;
+    auto run = [&](const double2 (&fr)[PP], const double2 (&lr)[kLpChunk], int64_t cc) {
+      const int64_t q0 = pad + qs + cc * kLpChunk;
+      double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3_index(w16, m2_pairs, q0, sq, comp) >> 1);
 #pragma unroll
       for (int k = 0; k < PP; ++k) {
-        const double e0 = __builtin_fma(fr[k].x, lr[2 * k].x, lr[2 * k].y);
-        const double e1 = __builtin_fma(fr[k].y, lr[2 * k + 1].x, lr[2 * k + 1].y);
-        bad |= __builtin_amdgcn_class(e0, kClsX);
-        const double y0 = df2t_lp<NT>(z, b, a, e0);
-        bad |= __builtin_amdgcn_class(y0, kClsY);
-        bad |= __builtin_amdgcn_class(e1, kClsX);
-        const double y1 = df2t_lp<NT>(z, b, a, e1);
-        bad |= __builtin_amdgcn_class(y1, kClsY);
-        dst[k * kWave] = make_double2(y0, y1);
+        const double e0v = __builtin_fma(fr[k].x, lr[2 * k].x, lr[2 * k].y);
+        const double e1v = __builtin_fma(fr[k].y, lr[2 * k + 1].x, lr[2 * k + 1].y);
+        // bb[0] is judged by its class above, not by magnitude
+        xmin = fmin(xmin, (k == 0 && cc == 0) ? __builtin_inf() : fabs(e0v));
+        const double y0 = pair_step(c, zA, zB, e0v);
+        xmin = fmin(xmin, fabs(e1v));
+        const double y1 = pair_step(c, zA, zB, e1v);
+        ymin = fmin(ymin, fmin(fabs(y0), fabs(y1)));
+        dst[(size_t)k * 32] = make_double2(y0, y1);   // next pair: +16 streams x 2 comps
       }
     };
     load(fa, la, 0);
     load(fb, lb, 1);
-    int64_t c = 0;
-    for (; c + 1 < nc; c += 2) {
-      run(fa, la, c);
+    int64_t cc = 0;
+    for (; cc + 1 < nc; cc += 2) {
+      run(fa, la, cc);
       __builtin_amdgcn_sched_barrier(0);
-      load(fa, la, c + 2);
+      load(fa, la, cc + 2);
       __builtin_amdgcn_sched_barrier(0);
-      run(fb, lb, c + 1);
+      run(fb, lb, cc + 1);
       __builtin_amdgcn_sched_barrier(0);
-      load(fb, lb, c + 3);
+      load(fb, lb, cc + 3);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (c < nc) run(fa, la, c);
+    if (cc < nc) run(fa, la, cc);
   }
   for (int64_t i = n_main; i < n; ++i) {
     const double e = X(i);
-    bad |= __builtin_amdgcn_class(e, kClsX);
-    const double y = df2t_lp<NT>(z, b, a, e);
-    bad |= __builtin_amdgcn_class(y, kClsY);
-    s3[pair_index(w, m2_pairs, pad + i + qs, lane)] = y;
+    if (i != 0) xmin = fmin(xmin, fabs(e));
+    const double y = pair_step(c, zA, zB, e);
+    ymin = fmin(ymin, fabs(y));
+    s3[s3_index(w16, m2_pairs, pad + i + qs, sq, comp)] = y;
   }
-  for (int j = 0; j < pad; ++j) {
-    const double e = 2.0 * xl - X(n - 2 - j);
-    bad |= __builtin_amdgcn_class(e, kClsX);
-    const double y = df2t_lp<NT>(z, b, a, e);
-    bad |= __builtin_amdgcn_class(y, kClsY);
-    s3[pair_index(w, m2_pairs, pad + n + j + qs, lane)] = y;
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * xl - X(n - 2 - jj);
+    xmin = fmin(xmin, fabs(e));
+    const double y = pair_step(c, zA, zB, e);
+    ymin = fmin(ymin, fabs(y));
+    s3[s3_index(w16, m2_pairs, pad + n + jj + qs, sq, comp)] = y;
   }
-  // stream flag = re lane | im lane
-  const int fl = bad ? 1 : 0;
-  const int other = __shfl_xor(fl, 1);
-  const int64_t s = (w >> 1) * kWave + (w & 1) * 32 + (lane >> 1);
-  if (comp == 0 && s < buf.n_streams) buf.flags[s] = fl | other;
+  bad |= !(xmin >= kMinNormal) || !(ymin >= kMinNormal);
+  bad |= !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
+  int fl = bad ? 1 : 0;
+  fl |= __shfl_xor(fl, 1);
+  fl |= __shfl_xor(fl, 2);
+  if ((lane & 3) == 0 && s < buf.n_streams) buf.flags[s] = fl;
 }
 
-// Symbol buffer (reuses s1, free after K1): the baseband sample of every
-// symbol, time-major per low-pass wave: sym[w][k][64 lanes] doubles, i.e. as
-// double2 (re, im) at ((w*S + k)*32 + stream-in-half).
-__device__ __forceinline__ size_t sym_index(int64_t w, int64_t n_sym, int64_t k, int lane) {
-  return (size_t)((w * n_sym + k) * kWave + lane);
-}
-
-template <int NT>
 __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
-  const int64_t w = blockIdx.x;
-  const int64_t g = w >> 1, h = w & 1;
+  const int j = lane & 1, comp = (lane >> 1) & 1, sq = lane >> 2;
+  const int64_t w16 = blockIdx.x;
+  const int64_t s = w16 * 16 + sq;
   const int64_t n = p.n;
   const int pad = p.pad2;
   const int qs = pad & 1;
@@ -391,28 +621,27 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   const double* __restrict__ s3 = buf.s3;
   double* __restrict__ sym = buf.s1;
   const int64_t S = p.n_sym;
-  const int64_t s = g * kWave + h * 32 + (lane >> 1);
 
-  double b[NT], a[NT], z[NT - 1];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
-  bool bad = false;
+  double ziA, ziB;
+  const PairIir c = pair_coef(f, j, ziA, ziB);
+  double zA, zB;
+  double ymin = __builtin_inf();
 
-  const double ylast = s3[pair_index(w, m2_pairs, m2 - 1 + qs, lane)];
-#pragma unroll
-  for (int i = 0; i < NT - 1; ++i) z[i] = f.zi[i] * ylast;
-  for (int64_t j = m2 - 1; j >= pad + n; --j) {
-    const double y = df2t_lp<NT>(z, b, a, s3[pair_index(w, m2_pairs, j + qs, lane)]);
-    bad |= __builtin_amdgcn_class(y, kClsY);
+  const double ylast = s3[s3_index(w16, m2_pairs, m2 - 1 + qs, sq, comp)];
+  zA = ziA * ylast;
+  zB = ziB * ylast;
+  for (int64_t jj = m2 - 1; jj >= pad + n; --jj) {
+    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)]);
+    ymin = fmin(ymin, fabs(y));
   }
 
   // symbols k = S-1 .. 0 sit at baseband index first + k*sps (modem.py:209 / :93)
   int64_t k = S - 1;
   int64_t next_n = p.first + k * p.sps;
+  const size_t sym_base = sym_index(s, S, 0, comp);
   auto on_output = [&](int64_t i, double y) {
-    bad |= __builtin_amdgcn_class(y, kClsY);
     if (i == next_n) {                          // uniform branch: one store per symbol
-      sym[sym_index(w, S, k, lane)] = y;
+      sym[sym_base + (size_t)k * 64] = y;
       --k;
       next_n = k >= 0 ? next_n - p.sps : -1;   // BPSK: first == sps, so index 0 is not a symbol
     }
@@ -420,54 +649,62 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
 
   const int64_t nc = n / kLpChunk;
   const int64_t n_lo = nc * kLpChunk;
-  for (int64_t i = n - 1; i >= n_lo; --i)
-    on_output(i, df2t_lp<NT>(z, b, a, s3[pair_index(w, m2_pairs, pad + i + qs, lane)]));
+  for (int64_t i = n - 1; i >= n_lo; --i) {
+    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, pad + i + qs, sq, comp)]);
+    ymin = fmin(ymin, fabs(y));
+    on_output(i, y);
+  }
   if (nc > 0) {
-    const double2* __restrict__ src = reinterpret_cast<const double2*>(s3) + (size_t)w * m2_pairs * kWave + lane;
+    const double2* __restrict__ src = reinterpret_cast<const double2*>(s3) + ((size_t)w16 * m2_pairs * 16 + sq) * 2 + comp;
     constexpr int PP = kLpChunk / 2;
     double2 ra[PP], rb[PP], rc[PP];
-    auto load = [&](double2 (&r)[PP], int64_t c) {
-      const int64_t cc = c < 0 ? 0 : c;
+    auto load = [&](double2 (&r)[PP], int64_t cc0) {
+      const int64_t cc = cc0 < 0 ? 0 : cc0;
       const int64_t qp = (pad + qs + cc * kLpChunk) >> 1;
 #pragma unroll
-      for (int kk = 0; kk < PP; ++kk) r[kk] = src[(size_t)(qp + kk) * kWave];
+      for (int kk = 0; kk < PP; ++kk) r[kk] = src[(size_t)(qp + kk) * 32];
     };
-    auto run = [&](const double2 (&r)[PP], int64_t c) {
+    auto run = [&](const double2 (&r)[PP], int64_t cc) {
 #pragma unroll
       for (int kk = PP - 1; kk >= 0; --kk) {
-        on_output(c * kLpChunk + 2 * kk + 1, df2t_lp<NT>(z, b, a, r[kk].y));
-        on_output(c * kLpChunk + 2 * kk, df2t_lp<NT>(z, b, a, r[kk].x));
+        const double y1 = pair_step(c, zA, zB, r[kk].y);
+        on_output(cc * kLpChunk + 2 * kk + 1, y1);
+        const double y0 = pair_step(c, zA, zB, r[kk].x);
+        on_output(cc * kLpChunk + 2 * kk, y0);
+        ymin = fmin(ymin, fmin(fabs(y0), fabs(y1)));
       }
     };
     load(ra, nc - 1);
     load(rb, nc - 2);
     load(rc, nc - 3);
-    int64_t c = nc - 1;
-    for (; c >= 2; c -= 3) {
-      run(ra, c);
+    int64_t cc = nc - 1;
+    for (; cc >= 2; cc -= 3) {
+      run(ra, cc);
       __builtin_amdgcn_sched_barrier(0);
-      load(ra, c - 3);
+      load(ra, cc - 3);
       __builtin_amdgcn_sched_barrier(0);
-      run(rb, c - 1);
+      run(rb, cc - 1);
       __builtin_amdgcn_sched_barrier(0);
-      load(rb, c - 4);
+      load(rb, cc - 4);
       __builtin_amdgcn_sched_barrier(0);
-      run(rc, c - 2);
+      run(rc, cc - 2);
       __builtin_amdgcn_sched_barrier(0);
-      load(rc, c - 5);
+      load(rc, cc - 5);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (c >= 0) run(ra, c);
-    if (c >= 1) run(rb, c - 1);
+    if (cc >= 0) run(ra, cc);
+    if (cc >= 1) run(rb, cc - 1);
   }
   // left-extension outputs are trimmed but still pass through the detector
-  for (int j = pad - 1; j >= 0; --j) {
-    const double y = df2t_lp<NT>(z, b, a, s3[pair_index(w, m2_pairs, j + qs, lane)]);
-    bad |= __builtin_amdgcn_class(y, kClsY);
+  for (int jj = pad - 1; jj >= 0; --jj) {
+    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)]);
+    ymin = fmin(ymin, fabs(y));
   }
-  const int fl = bad ? 1 : 0;
-  const int other = __shfl_xor(fl, 1);
-  if ((lane & 1) == 0 && s < buf.n_streams) buf.flags[s] |= (fl | other);
+  bool bad = !(ymin >= kMinNormal) || !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
+  int fl = bad ? 1 : 0;
+  fl |= __shfl_xor(fl, 1);
+  fl |= __shfl_xor(fl, 2);
+  if ((lane & 3) == 0 && s < buf.n_streams) buf.flags[s] |= fl;
 }
 
 // ---------------------------------------------------------------------------
@@ -513,8 +750,6 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
   const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
   double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)g * m2 * kWave + lane;
   double2* __restrict__ sym2 = reinterpret_cast<double2*>(buf.s1);
-  const int64_t wq = 2 * g + (lane >> 5);       // the low-pass wave that owns this stream
-  const int sl = lane & 31;
 
   double b[NT], a[NT], zr[NT - 1], zc[NT - 1];
 #pragma unroll
@@ -558,7 +793,7 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
     double o0, o1;
     df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
     if (j - pad == next_n && k >= 0) {
-      if (live) sym2[(size_t)(wq * S + k) * 32 + sl] = make_double2(o0, o1);
+      if (live) sym2[sym_index(s, S, k, 0) >> 1] = make_double2(o0, o1);
       --k;
       next_n -= p.sps;
     }
@@ -604,9 +839,7 @@ __global__ __launch_bounds__(64) void k_slice(PskBuffers buf, PskParams p) {
   const int64_t k0 = j * per;
   const int64_t nd = S - 1;                     // number of diffs
   const double2* __restrict__ sym2 = reinterpret_cast<const double2*>(buf.s1);
-  const int64_t wq = s >> 5;
-  const int sl = (int)(s & 31);
-  auto SYM = [&](int64_t k) { return sym2[(size_t)(wq * S + k) * 32 + sl]; };
+  auto SYM = [&](int64_t k) { return sym2[sym_index(s, S, k, 0) >> 1]; };
   uint32_t word = 0;
   double2 prev = SYM(k0 < S ? k0 : S - 1);
   for (int u = 0; u < per; ++u) {
@@ -641,7 +874,28 @@ static hipError_t launch_bp(int nt, bool zodd, const PskBuffers& b, const PskPar
   return hipGetLastError();
 }
 
+template <typename T>
+static hipError_t launch_bp_quad(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  const int64_t g16 = (b.n_streams + 15) / 16;
+  hipLaunchKernelGGL((k_bandpass_quad<T>), dim3((unsigned)g16), dim3(kWave), 0, st, b, p, f);
+  return hipGetLastError();
+}
+
+// AMR_BANDPASS_LANE=1 selects the lane-per-stream band-pass (A/B comparisons)
+static bool bandpass_lane_mode() {
+  static const bool v = [] { const char* e = getenv("AMR_BANDPASS_LANE"); return e && e[0] == '1'; }();
+  return v;
+}
+
 hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  if (f.nt == 9 && !bandpass_lane_mode()) {
+    switch (b.dtype) {
+      case kF32: return launch_bp_quad<float>(b, p, f, st);
+      case kF64: return launch_bp_quad<double>(b, p, f, st);
+      case kI16: return launch_bp_quad<int16_t>(b, p, f, st);
+    }
+    return hipErrorInvalidValue;
+  }
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   switch (b.dtype) {
     case kF32: return launch_bp<float>(f.nt, p.bp_zero_odd != 0, b, p, f, st, groups);
@@ -654,14 +908,14 @@ hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Ii
 hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_lowpass_fwd<5>), dim3((unsigned)(2 * groups)), dim3(kWave), 0, st, b, p, f);
+  hipLaunchKernelGGL(k_lowpass_fwd, dim3((unsigned)(4 * groups)), dim3(kWave), 0, st, b, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_lowpass_bwd<5>), dim3((unsigned)(2 * groups)), dim3(kWave), 0, st, b, p, f);
+  hipLaunchKernelGGL(k_lowpass_bwd, dim3((unsigned)(4 * groups)), dim3(kWave), 0, st, b, p, f);
   return hipGetLastError();
 }
 
