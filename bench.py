@@ -128,11 +128,14 @@ def main():
         comm = ctypes.c_void_p()
         _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
         d_gather = dmalloc(world * B * cap)
+        d_gather_len = dmalloc(world * B * 8)
 
     def step():
         _amr.check(L.amr_psk_demod_device(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
         if comm is not None:
+            # the decoded bytes of every rank to every rank (RCCL over xGMI)
             _amr.check(L.amr_allgather(comm, d_out, d_gather, B * cap, plan.handle))
+            _amr.check(L.amr_allgather(comm, d_len, d_gather_len, B * 8, plan.handle))
         _amr.check(L.amr_psk_plan_synchronize(plan.handle))
 
     for _ in range(args.warmup):
@@ -156,16 +159,32 @@ def main():
     # per-kernel averages (HIP events on the plan's stream)
     kavg = {k: v / args.steps for k, v in kt.items() if v > 0}
     dom = max(kavg, key=kavg.get)
-    # algorithmic bytes of the dominant kernel per launch:
-    # band-pass+mixer reads the input (4 B/sample) and writes the baseband
-    # (complex128, 16 B/sample) -- its defined inputs and outputs.
-    alg_bytes = {"bandpass": B * N * (4 + 16), "lowpass_fwd": B * N * (16 + 16), "lowpass_bwd": B * N * 16,
-                 "sync_pack": B * (sym_per_stream * 2 / 8 * 2), "lowpass_exact": 0, "fec": 0}
-    fp64_ops = {"bandpass": B * (N + 54) * 2 * 30 + B * N * 2, "lowpass_fwd": B * (N + 30) * 2 * 17,
+    # Algorithmic bytes per launch: each stage's
+    # compulsory input + output at its minimal width --
+    #   bandpass    : x float32 (4 B/sample) in, filtered f float64 (8 B) out
+    #   lowpass_fwd : f (8 B) in, forward low-pass complex128 (16 B) out
+    #   lowpass_bwd : forward low-pass (16 B) in, symbol samples (16 B/symbol) out
+    #   sync_pack   : symbols (16 B/symbol) in, packed bytes out
+    S_sym = sym_per_stream + 1
+    alg_bytes = {"bandpass": B * N * (4 + 8), "lowpass_fwd": B * N * (8 + 16),
+                 "lowpass_bwd": B * (N * 16 + S_sym * 16), "sync_pack": B * (S_sym * 16 + cap),
+                 "lowpass_exact": 0, "fec": 0}
+    # FP64 operations scipy's arithmetic needs (no FMA): band-pass 30/sample per
+    # pass (9 taps incl. the zero odd taps), low-pass 17/sample per pass per
+    # component, mixer 2/sample
+    fp64_ops = {"bandpass": B * ((N + 54) + (N + 27)) * 30,
+                "lowpass_fwd": B * ((N + 30) * 2 * 17 + N * 2),
                 "lowpass_bwd": B * (N + 30) * 2 * 17}
     achieved = alg_bytes[dom] / (kavg[dom] / 1e3) / 1e9
     pipeline_bytes = B * N * 4 + B * sym_per_stream * 2 / 8
     fp64_achieved = fp64_ops.get(dom, 0) / (kavg[dom] / 1e3) / 1e12
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", "r01_pmc.json")
+    if (B, N, int(baud)) == (4096, 96000, 9600) and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            pk = json.load(f)["kernels"].get("k_" + dom, {})
+        if "hbm_bytes_per_dispatch" in pk:
+            traffic = int(pk["hbm_bytes_per_dispatch"])
 
     # parity spot-check after timing (not timed): GPU bytes vs the oracle
     out = np.empty((B, cap), np.uint8)
@@ -179,7 +198,7 @@ def main():
         cpu = None
         parity = "skipped"
         if not args.no_cpu:
-            n_cpu = args.cpu_streams or max(threads, int(round(10.0 / 0.009)))   # ~10 s of single-core work
+            n_cpu = args.cpu_streams or B          # the whole batch: ~10 s of single-core work on the box
             idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
             val, cdt, couts = cpu_baseline(x[idx], baud, threads)
             cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
@@ -196,7 +215,9 @@ def main():
                                    "(BASELINE configs[1])", "global_batch": world * B, "samples_per_stream": N,
                        "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": "profiles/r01_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
+                         "alg_bytes_per_launch": int(alg_bytes[dom]),
                          "fp64_valu": {"achieved_tops": round(fp64_achieved, 3), "peak_tops": FP64_PEAK_TOPS,
                                        "frac": round(fp64_achieved / FP64_PEAK_TOPS, 4)}},
             "pipeline_hbm_gbs": round(pipeline_bytes / (ms_per_step / 1e3) / 1e9, 2),
@@ -210,6 +231,7 @@ def main():
         L.amr_free(p)
     if comm is not None:
         L.amr_free(d_gather)
+        L.amr_free(d_gather_len)
         L.amr_comm_destroy(comm)
     if dist is not None:
         dist.barrier()
