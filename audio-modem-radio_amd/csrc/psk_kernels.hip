@@ -17,9 +17,9 @@
 //                      LDS transpose tile and writes s1; the backward pass
 //                      streams s1 back (register prefetch ring) and writes the
 //                      real filtered signal f to s2.
-//   K2 k_lowpass_fwd   lane quad = stream (re/im x 2-lane state split): LO
-//                      mixer (numpy's complex multiply) fused into the
-//                      low-pass forward pass -> s3
+//   K2 k_lowpass_fwd   wave = (32 streams, re|im), lane pair = one recurrence
+//                      (2-lane state split): LO mixer (numpy's complex
+//                      multiply) fused into the low-pass forward pass -> s3
 //   K3 k_lowpass_bwd   same lanes: low-pass backward pass; the baseband at
 //                      each symbol centre goes to the symbol buffer
 //   K4a k_slice        thread = (stream, output word): differential product,
@@ -437,11 +437,10 @@ __global__ __launch_bounds__(64) void k_bandpass_quad(PskBuffers buf, PskParams 
 }
 
 // ---------------------------------------------------------------------------
-// Low-pass kernels K2/K3.  A lane QUAD serves one stream: lanes
-// (re, j=0), (re, j=1), (im, j=0), (im, j=1); lane j of a pair owns states
-// z[2j], z[2j+1] of that component's 5-tap recurrence (the same DPP split
-// as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1, -0.0 above
-// the top state).  A wave serves 16 streams.
+// Low-pass kernels K2/K3.  A lane PAIR serves one component of one stream:
+// lane j of the pair owns states z[2j], z[2j+1] of the 5-tap recurrence (the
+// same DPP split as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1,
+// -0.0 above the top state).
 //
 // The mixer (modem.py:200-201) is numpy's complex multiply (f + 0j) * lo:
 //   re = fma(f, lo_re, -(0*lo_im)),  im = fma(f, lo_im, 0*lo_re)
@@ -468,6 +467,21 @@ struct PairIir {
   bool top;                                     // j == 1
 };
 
+// pair_step2 also hands back t: on lane j=0 it IS y, bit for bit, and as an
+// arithmetic result (not a DPP move) the detector's fmin needs no canonicalise.
+__device__ __forceinline__ double pair_step2(const PairIir& c, double& zA, double& zB, double x, double& t_out) {
+  const double t = zA + c.b0 * x;
+  t_out = t;
+  const double y = dpp_f64<kPairBcast>(t);
+  double zC = dpp_f64<kPairNext>(zA);
+  zC = c.top ? -0.0 : zC;
+  const double nA = (zB + x * c.cAb) - y * c.cAa;
+  const double nB = (zC + x * c.cBb) - y * c.cBa;
+  zA = nA;
+  zB = nB;
+  return y;
+}
+
 __device__ __forceinline__ double pair_step(const PairIir& c, double& zA, double& zB, double x) {
   const double t = zA + c.b0 * x;
   const double y = dpp_f64<kPairBcast>(t);
@@ -493,9 +507,14 @@ __device__ __forceinline__ PairIir pair_coef(const Iir& f, int j, double& ziA, d
   return c;
 }
 
-// s3: [w16][q/2][16 streams][2 comps] double2 (a pair of samples)
-__device__ __forceinline__ size_t s3_index(int64_t w16, int64_t m_pairs, int64_t q, int sq, int comp) {
-  return ((((size_t)(w16 * m_pairs + (q >> 1)) * 16 + sq) * 2 + comp) * 2) + (q & 1);
+// Low-pass wave mapping: wave = (half-group hg of 32 streams, component);
+// lane l -> stream hg*32 + l/2, state pair position j = l & 1.  Keeping one
+// component per wave makes the LO uniform across the wave, so it arrives
+// through scalar loads instead of one vector load per lane per sample.
+//
+// s3: [hg][comp][q/2][32 streams][2] doubles (a pair of samples per stream)
+__device__ __forceinline__ size_t s3_index(int64_t hg, int comp, int64_t m_pairs, int64_t q, int sl) {
+  return ((((size_t)((hg * 2 + comp) * m_pairs + (q >> 1))) * 32 + sl) * 2) + (q & 1);
 }
 
 // Symbol buffer (reuses s1, free after K1): the baseband sample of every
@@ -506,17 +525,21 @@ __device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k,
 
 __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
-  const int j = lane & 1, comp = (lane >> 1) & 1, sq = lane >> 2;
-  const int64_t w16 = blockIdx.x;
-  const int64_t s = w16 * 16 + sq;
+  const int j = lane & 1, sl = lane >> 1;
+  const int64_t hg = blockIdx.x >> 1;
+  const int comp = blockIdx.x & 1;
+  const int64_t s = hg * 32 + sl;
   const int64_t n = p.n;
   const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int qs = pad & 1;
   const int64_t m2_pairs = (p.m2 + qs + 1) >> 1;
-  const double2* __restrict__ fsrc =
-      reinterpret_cast<const double2*>(buf.s2) + (size_t)((s >> 6) * 2 + ((s >> 5) & 1)) * n2 * 32 + (s & 31);
-  const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;   // lo2[n][comp] at lo[2n]
+  const double2* __restrict__ fsrc = reinterpret_cast<const double2*>(buf.s2) + (size_t)hg * n2 * 32 + sl;
+  // uniform per wave: lo2[i] = (lo_c, addend_c) at lo[2i] (double2 units).  In
+  // the main body lane k of the wave loads the entry of sample k of a chunk
+  // (one VMEM per chunk instead of one per sample) and v_readlane broadcasts
+  // it into SGPRs when that sample is mixed.
+  const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;
   double* __restrict__ s3 = buf.s3;
 
   double ziA, ziB;
@@ -524,10 +547,14 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
   double zA, zB;
   bool bad = false;
   double xmin = __builtin_inf(), ymin = __builtin_inf();
-  auto X = [&](int64_t i) {                     // mixer output bb[i] for this lane's component
+  // numpy's (f + 0j) * lo for this component: fma(f, lo_c, addend) with an
+  // exactly-zero addend == (f * lo_c) + addend whenever f*lo_c does not
+  // underflow to zero; that case makes |bb| < 2^-1022 and is flagged below.
+  auto MIXL = [&](double fv, double2 l) { return fv * l.x + l.y; };
+  auto MIX = [&](double fv, int64_t i) { return MIXL(fv, lo[2 * i]); };
+  auto X = [&](int64_t i) {
     const double2 fp = fsrc[(size_t)(i >> 1) * 32];
-    const double2 l = lo[2 * i];
-    return __builtin_fma((i & 1) ? fp.y : fp.x, l.x, l.y);
+    return MIX((i & 1) ? fp.y : fp.x, i);
   };
 
   const double x0 = X(0), xl = X(n - 1);
@@ -541,78 +568,94 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
     xmin = fmin(xmin, fabs(e));
     const double y = pair_step(c, zA, zB, e);
     ymin = fmin(ymin, fabs(y));
-    s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)] = y;
+    s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)] = y;
   }
   const int64_t nc = n / kLpChunk;
   const int64_t n_main = nc * kLpChunk;
   if (nc > 0) {
     constexpr int PP = kLpChunk / 2;
-    double2 fa[PP], fb[PP], la[kLpChunk], lb[kLpChunk];
-    auto load = [&](double2 (&fr)[PP], double2 (&lr)[kLpChunk], int64_t cc0) {
+    double2 fa[PP], fb[PP], la, lb;
+    auto load = [&](double2 (&fr)[PP], double2& lr, int64_t cc0) {
       const int64_t cc = cc0 < nc ? cc0 : nc - 1;
 #pragma unroll
       for (int k = 0; k < PP; ++k) fr[k] = fsrc[(size_t)(cc * PP + k) * 32];
-#pragma unroll
-      for (int k = 0; k < kLpChunk; ++k) lr[k] = lo[2 * (cc * kLpChunk + k)];
+      lr = lo[2 * (cc * kLpChunk + (lane & (kLpChunk - 1)))];
     };
-    auto run = [&](const double2 (&fr)[PP], const double2 (&lr)[kLpChunk], int64_t cc) {
+    auto bcast = [&](const double2& lr, int k) {   // lane k's LO entry, as wave-uniform values
+      const long long lx = __builtin_bit_cast(long long, lr.x), ly = __builtin_bit_cast(long long, lr.y);
+      const int a0 = __builtin_amdgcn_readlane((int)(lx & 0xffffffff), k);
+      const int a1 = __builtin_amdgcn_readlane((int)(lx >> 32), k);
+      const int c0 = __builtin_amdgcn_readlane((int)(ly & 0xffffffff), k);
+      const int c1 = __builtin_amdgcn_readlane((int)(ly >> 32), k);
+      return make_double2(__builtin_bit_cast(double, ((long long)a1 << 32) | (unsigned)a0),
+                          __builtin_bit_cast(double, ((long long)c1 << 32) | (unsigned)c0));
+    };
+    auto run = [&](const double2 (&fr)[PP], const double2& lr, int64_t cc, int) {
       const int64_t q0 = pad + qs + cc * kLpChunk;
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3_index(w16, m2_pairs, q0, sq, comp) >> 1);
+      double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3_index(hg, comp, m2_pairs, q0, sl) >> 1);
 #pragma unroll
       for (int k = 0; k < PP; ++k) {
-        const double e0v = __builtin_fma(fr[k].x, lr[2 * k].x, lr[2 * k].y);
-        const double e1v = __builtin_fma(fr[k].y, lr[2 * k + 1].x, lr[2 * k + 1].y);
+        const double e0v = MIXL(fr[k].x, bcast(lr, 2 * k));
+        const double e1v = MIXL(fr[k].y, bcast(lr, 2 * k + 1));
         // bb[0] is judged by its class above, not by magnitude
         xmin = fmin(xmin, (k == 0 && cc == 0) ? __builtin_inf() : fabs(e0v));
-        const double y0 = pair_step(c, zA, zB, e0v);
+        double t0, t1;
+        const double y0 = pair_step2(c, zA, zB, e0v, t0);
         xmin = fmin(xmin, fabs(e1v));
-        const double y1 = pair_step(c, zA, zB, e1v);
-        ymin = fmin(ymin, fmin(fabs(y0), fabs(y1)));
-        dst[(size_t)k * 32] = make_double2(y0, y1);   // next pair: +16 streams x 2 comps
+        const double y1 = pair_step2(c, zA, zB, e1v, t1);
+        ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
+        dst[(size_t)k * 32] = make_double2(y0, y1);
       }
     };
     load(fa, la, 0);
     load(fb, lb, 1);
     int64_t cc = 0;
     for (; cc + 1 < nc; cc += 2) {
-      run(fa, la, cc);
+      run(fa, la, cc, 0);
       __builtin_amdgcn_sched_barrier(0);
       load(fa, la, cc + 2);
       __builtin_amdgcn_sched_barrier(0);
-      run(fb, lb, cc + 1);
+      run(fb, lb, cc + 1, 1);
       __builtin_amdgcn_sched_barrier(0);
       load(fb, lb, cc + 3);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (cc < nc) run(fa, la, cc);
+    if (cc < nc) run(fa, la, cc, 0);
   }
   for (int64_t i = n_main; i < n; ++i) {
     const double e = X(i);
     if (i != 0) xmin = fmin(xmin, fabs(e));
     const double y = pair_step(c, zA, zB, e);
     ymin = fmin(ymin, fabs(y));
-    s3[s3_index(w16, m2_pairs, pad + i + qs, sq, comp)] = y;
+    s3[s3_index(hg, comp, m2_pairs, pad + i + qs, sl)] = y;
   }
   for (int jj = 0; jj < pad; ++jj) {
     const double e = 2.0 * xl - X(n - 2 - jj);
     xmin = fmin(xmin, fabs(e));
     const double y = pair_step(c, zA, zB, e);
     ymin = fmin(ymin, fabs(y));
-    s3[s3_index(w16, m2_pairs, pad + n + jj + qs, sq, comp)] = y;
+    s3[s3_index(hg, comp, m2_pairs, pad + n + jj + qs, sl)] = y;
   }
-  bad |= !(xmin >= kMinNormal) || !(ymin >= kMinNormal);
+  bad |= !(xmin >= kMinNormal) || (j == 0 && !(ymin >= kMinNormal));   // ymin is y only on j == 0
   bad |= !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
   int fl = bad ? 1 : 0;
   fl |= __shfl_xor(fl, 1);
-  fl |= __shfl_xor(fl, 2);
-  if ((lane & 3) == 0 && s < buf.n_streams) buf.flags[s] = fl;
+  if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
 }
 
+// K3.  SPS > 0: a specialisation for sps == SPS and first == SPS/2 (QPSK at
+// the benchmark rates) whose chunk length is a multiple of SPS, so the symbol
+// samples sit at the same static offsets of every chunk: no per-sample branch.
+// SPS == 0: generic, one uniform branch per sample.
+template <int SPS>
 __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int CH = SPS > 0 ? 20 : kLpChunk;  // 20 = lcm-friendly for SPS in {2,4,5,10,20}
+  static_assert(SPS == 0 || CH % SPS == 0, "chunk must be a multiple of SPS");
   const int lane = threadIdx.x;
-  const int j = lane & 1, comp = (lane >> 1) & 1, sq = lane >> 2;
-  const int64_t w16 = blockIdx.x;
-  const int64_t s = w16 * 16 + sq;
+  const int j = lane & 1, sl = lane >> 1;
+  const int64_t hg = blockIdx.x >> 1;
+  const int comp = blockIdx.x & 1;
+  const int64_t s = hg * 32 + sl;
   const int64_t n = p.n;
   const int pad = p.pad2;
   const int qs = pad & 1;
@@ -627,11 +670,11 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   double zA, zB;
   double ymin = __builtin_inf();
 
-  const double ylast = s3[s3_index(w16, m2_pairs, m2 - 1 + qs, sq, comp)];
+  const double ylast = s3[s3_index(hg, comp, m2_pairs, m2 - 1 + qs, sl)];
   zA = ziA * ylast;
   zB = ziB * ylast;
   for (int64_t jj = m2 - 1; jj >= pad + n; --jj) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)]);
+    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)]);
     ymin = fmin(ymin, fabs(y));
   }
 
@@ -647,31 +690,48 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
     }
   };
 
-  const int64_t nc = n / kLpChunk;
-  const int64_t n_lo = nc * kLpChunk;
+  const int64_t nc = n / CH;
+  const int64_t n_lo = nc * CH;
   for (int64_t i = n - 1; i >= n_lo; --i) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, pad + i + qs, sq, comp)]);
+    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, pad + i + qs, sl)]);
     ymin = fmin(ymin, fabs(y));
     on_output(i, y);
   }
   if (nc > 0) {
-    const double2* __restrict__ src = reinterpret_cast<const double2*>(s3) + ((size_t)w16 * m2_pairs * 16 + sq) * 2 + comp;
-    constexpr int PP = kLpChunk / 2;
+    const double2* __restrict__ src =
+        reinterpret_cast<const double2*>(s3) + (size_t)(hg * 2 + comp) * m2_pairs * 32 + sl;
+    constexpr int PP = CH / 2;
     double2 ra[PP], rb[PP], rc[PP];
     auto load = [&](double2 (&r)[PP], int64_t cc0) {
       const int64_t cc = cc0 < 0 ? 0 : cc0;
-      const int64_t qp = (pad + qs + cc * kLpChunk) >> 1;
+      const int64_t qp = (pad + qs + cc * CH) >> 1;
 #pragma unroll
       for (int kk = 0; kk < PP; ++kk) r[kk] = src[(size_t)(qp + kk) * 32];
     };
     auto run = [&](const double2 (&r)[PP], int64_t cc) {
+      if constexpr (SPS > 0) {
+        // chunk covers i in [cc*CH, cc*CH + CH); symbols at offsets SPS/2 + m*SPS
+        // with index k = (cc*CH + SPS/2 - first)/SPS + m = cc*(CH/SPS) + m
+        const size_t kb = sym_base + (size_t)(cc * (CH / SPS)) * 64;
 #pragma unroll
-      for (int kk = PP - 1; kk >= 0; --kk) {
-        const double y1 = pair_step(c, zA, zB, r[kk].y);
-        on_output(cc * kLpChunk + 2 * kk + 1, y1);
-        const double y0 = pair_step(c, zA, zB, r[kk].x);
-        on_output(cc * kLpChunk + 2 * kk, y0);
-        ymin = fmin(ymin, fmin(fabs(y0), fabs(y1)));
+        for (int kk = PP - 1; kk >= 0; --kk) {
+          double t0, t1;
+          const double y1 = pair_step2(c, zA, zB, r[kk].y, t1);
+          const double y0 = pair_step2(c, zA, zB, r[kk].x, t0);
+          ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
+          if ((2 * kk + 1) % SPS == SPS / 2) sym[kb + (size_t)((2 * kk + 1) / SPS) * 64] = y1;
+          if ((2 * kk) % SPS == SPS / 2) sym[kb + (size_t)((2 * kk) / SPS) * 64] = y0;
+        }
+      } else {
+#pragma unroll
+        for (int kk = PP - 1; kk >= 0; --kk) {
+          double t0, t1;
+          const double y1 = pair_step2(c, zA, zB, r[kk].y, t1);
+          on_output(cc * CH + 2 * kk + 1, y1);
+          const double y0 = pair_step2(c, zA, zB, r[kk].x, t0);
+          on_output(cc * CH + 2 * kk, y0);
+          ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
+        }
       }
     };
     load(ra, nc - 1);
@@ -697,14 +757,13 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
   }
   // left-extension outputs are trimmed but still pass through the detector
   for (int jj = pad - 1; jj >= 0; --jj) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(w16, m2_pairs, jj + qs, sq, comp)]);
+    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)]);
     ymin = fmin(ymin, fabs(y));
   }
-  bool bad = !(ymin >= kMinNormal) || !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
+  const bool bad = (j == 0 && !(ymin >= kMinNormal)) || !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
   int fl = bad ? 1 : 0;
   fl |= __shfl_xor(fl, 1);
-  fl |= __shfl_xor(fl, 2);
-  if ((lane & 3) == 0 && s < buf.n_streams) buf.flags[s] |= fl;
+  if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -908,6 +967,8 @@ hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Ii
 hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_lowpass_fwd, dim3((unsigned)(4 * groups)), dim3(kWave), 0, st, b, p, f);
   return hipGetLastError();
 }
@@ -915,7 +976,11 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const
 hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_lowpass_bwd, dim3((unsigned)(4 * groups)), dim3(kWave), 0, st, b, p, f);
+  const dim3 grid((unsigned)(4 * groups)), block(kWave);
+  if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd<10>), grid, block, 0, st, b, p, f);
+  else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd<5>), grid, block, 0, st, b, p, f);
+  else if (p.sps == 20 && p.first == 10) hipLaunchKernelGGL((k_lowpass_bwd<20>), grid, block, 0, st, b, p, f);
+  else hipLaunchKernelGGL((k_lowpass_bwd<0>), grid, block, 0, st, b, p, f);
   return hipGetLastError();
 }
 
