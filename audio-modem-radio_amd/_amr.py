@@ -26,6 +26,8 @@ AMR_E_INVALID, AMR_E_PADLEN, AMR_E_HIP, AMR_E_NOMEM, AMR_E_NODEVICE, AMR_E_RCCL,
 DTYPE_F32, DTYPE_F64, DTYPE_I16 = 0, 1, 2
 PSK_QPSK, PSK_BPSK = 0, 1
 T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec"]
+TF_NAMES = ["bandpass", "fft_fwd", "fft_inv", "decide"]
+DTYPES = {np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64, np.dtype(np.int16): DTYPE_I16}
 
 # every symbol include/amr.h declares (tests/test_abi.py checks the export table)
 EXPORTS = [
@@ -34,6 +36,9 @@ EXPORTS = [
     "amr_psk_plan_create", "amr_psk_plan_destroy", "amr_psk_plan_out_capacity", "amr_psk_plan_scratch_bytes",
     "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
+    "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
+    "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
+    "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
     "amr_comm_synchronize",
 ]
@@ -84,6 +89,19 @@ def lib():
             "amr_psk_demod_host": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_device": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
+            "amr_fsk_plan_create": (I32, [P, I32, I64, I64, P, P, P, P, P, P, I32, I64]),
+            "amr_fsk_plan_destroy": (I32, [P]),
+            "amr_fsk_plan_out_capacity": (I64, [P]),
+            "amr_fsk_plan_scratch_bytes": (I64, [P]),
+            "amr_fsk_plan_fft_length": (I64, [P]),
+            "amr_fsk_plan_synchronize": (I32, [P]),
+            "amr_fsk_plan_enable_timing": (I32, [P, I32]),
+            "amr_fsk_plan_timings": (I32, [P, P, I32]),
+            "amr_fsk_demod_host": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
+            "amr_fsk_demod_device": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
+            "amr_fsk_envelopes_host": (I32, [P, P, I32, I64, I64, P, P]),
+            "amr_fft_c2c_host": (I32, [P, P, I64, I64, I32, I32]),
+            "amr_hilbert_host": (I32, [P, P, I64, I64, I32]),
             "amr_fec_decode_host": (I32, [P, I64, P, I64, P, I64, P, P]),
             "amr_comm_unique_id": (I32, [P]),
             "amr_comm_create": (I32, [P, P, I32, I32, I32]),
@@ -204,7 +222,7 @@ class PskPlan:
     def demod_host(self, x: np.ndarray):
         """x [B][N] float32/float64/int16 (int16 = PCM read as int16/32768). Returns (list[bytes], sync)."""
         x = np.ascontiguousarray(x)
-        dt = {np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64, np.dtype(np.int16): DTYPE_I16}
+        dt = DTYPES
         B = x.shape[0]
         outs, syncs = [], np.empty(B, np.int64)
         cap = max(self.out_cap, 1)
@@ -269,3 +287,21 @@ def fec_decode_host(datas):
     check(lib().amr_set_device(default_device()))
     check(lib().amr_fec_decode_host(ptr(buf), stride, ptr(ln), n, ptr(out), stride, ptr(out_len), ptr(ok)))
     return [out[i, :out_len[i]].tobytes() for i in range(n)], [bool(v) for v in ok]
+
+
+def fft(x: np.ndarray, inverse: bool = False) -> np.ndarray:
+    """numpy.fft.fft / ifft along the last axis of a [batch][n] complex array, on the GPU."""
+    require_gpu()
+    x = np.ascontiguousarray(np.atleast_2d(x), np.complex128)
+    out = np.empty_like(x)
+    check(lib().amr_fft_c2c_host(ptr(x), ptr(out), x.shape[1], x.shape[0], 1 if inverse else 0, default_device()))
+    return out
+
+
+def hilbert(x: np.ndarray) -> np.ndarray:
+    """scipy.signal.hilbert(x) along the last axis of a real [batch][n] array, on the GPU."""
+    require_gpu()
+    x = np.ascontiguousarray(np.atleast_2d(x), np.float64)
+    out = np.empty(x.shape, np.complex128)
+    check(lib().amr_hilbert_host(ptr(x), ptr(out), x.shape[1], x.shape[0], default_device()))
+    return out

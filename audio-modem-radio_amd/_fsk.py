@@ -3,18 +3,25 @@
 fsk_demodulate (modem.py:298-341): per tone butter(3, [(f-baud)/nyq, (f+baud)/nyq],
 'band') WITHOUT clamping -- scipy raises for an edge <= 0 or >= 1, which is the
 reference's behaviour at its own defaults -- then filtfilt,
-|hilbert|, per-sample compare, windowed majority, sync + pack.
+|hilbert|, per-sample compare, windowed majority, sync + pack.  Everything
+after the filter design runs in libamr.so (fsk_kernels.hip, fft_kernels.hip).
 """
 from __future__ import annotations
+
+import ctypes
+import threading
 
 import numpy as np
 
 import _amr
+from _amr import check, lib, ptr
 
 
 def design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
-    """Raise exactly where the reference raises, in the reference's order."""
+    """Return (sps, [(b, a, zi) mark, (b, a, zi) space]); raise exactly where
+    the reference raises, in the reference's order (modem.py:301-320)."""
     from scipy import signal
+    sps = int(samp_rate / baud)            # modem.py:301 (ZeroDivisionError for baud == 0)
     nyq = samp_rate / 2
     out = []
     for f in (mark_freq, space_freq):      # mark envelope is computed first (modem.py:311-312)
@@ -23,7 +30,109 @@ def design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
         if n <= 3 * nt:
             raise ValueError("The length of the input vector x must be greater than padlen, which is %d." % (3 * nt))
         out.append(tuple(np.ascontiguousarray(v, np.float64) for v in (b, a, signal.lfilter_zi(b, a))))
-    return out
+    if sps == 0:
+        raise ValueError("range() arg 3 must not be zero")   # modem.py:320
+    return sps, out
+
+
+class FskPlan:
+    """A device plan: both tones' coefficients, the FFT tables and HBM scratch."""
+
+    def __init__(self, n: int, baud, mark_freq, space_freq, samp_rate=96000, max_streams=64, device=None):
+        self.n = int(n)
+        self.sps, ((mb, ma, mzi), (sb, sa, szi)) = design_fsk(n, baud, mark_freq, space_freq, samp_rate)
+        self.coef = (mb, ma, mzi, sb, sa, szi)
+        _amr.require_gpu()
+        self.device = _amr.default_device() if device is None else device
+        self.max_streams = int(max_streams)
+        self.handle = None
+        self.out_cap = 1
+        self.lock = threading.Lock()
+        if self.sps < 0:
+            return      # range(sps//2, n, sps) with a negative step is empty: b'' for every stream
+        h = ctypes.c_void_p()
+        check(lib().amr_fsk_plan_create(ctypes.byref(h), self.device, self.n, self.sps, ptr(mb), ptr(ma), ptr(mzi),
+                                        ptr(sb), ptr(sa), ptr(szi), len(mb), self.max_streams))
+        self.handle = h
+        self.out_cap = int(lib().amr_fsk_plan_out_capacity(h))
+        self.fft_length = int(lib().amr_fsk_plan_fft_length(h))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and _amr._lib is not None:
+            try:
+                _amr._lib.amr_fsk_plan_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+    def _chunks(self, x):
+        x = np.ascontiguousarray(x)
+        if x.dtype not in _amr.DTYPES:
+            x = np.ascontiguousarray(x, np.float64)
+        for s0 in range(0, x.shape[0], self.max_streams):
+            yield s0, x[s0:s0 + self.max_streams]
+
+    def demod_host(self, x: np.ndarray):
+        """x [B][N] float32/float64/int16. Returns (list[bytes], sync[B])."""
+        B = x.shape[0]
+        if self.handle is None:
+            return [b""] * B, np.full(B, -1, np.int64)
+        outs, syncs = [], np.empty(B, np.int64)
+        cap = max(self.out_cap, 1)
+        for s0, xb in self._chunks(x):
+            nb = xb.shape[0]
+            out = np.empty((nb, cap), np.uint8)
+            ln = np.empty(nb, np.int64)
+            sy = np.empty(nb, np.int64)
+            with self.lock:
+                check(lib().amr_fsk_demod_host(self.handle, ptr(xb), _amr.DTYPES[xb.dtype], nb, xb.shape[1],
+                                               ptr(out), cap, ptr(ln), ptr(sy)))
+            outs += [out[i, :ln[i]].tobytes() for i in range(nb)]
+            syncs[s0:s0 + nb] = sy
+        return outs, syncs
+
+    def envelopes(self, x: np.ndarray):
+        """(mark_env, space_env) [B][N]: |hilbert(filtfilt(.))| per tone (modem.py:308-309)."""
+        if self.handle is None:
+            raise _amr.AmrError(_amr.AMR_E_INVALID, "plan has no decision path (sps < 0)")
+        B = x.shape[0]
+        m = np.empty((B, self.n))
+        s = np.empty((B, self.n))
+        for s0, xb in self._chunks(x):
+            nb = xb.shape[0]
+            with self.lock:
+                check(lib().amr_fsk_envelopes_host(self.handle, ptr(xb), _amr.DTYPES[xb.dtype], nb, xb.shape[1],
+                                                   ptr(m[s0:s0 + nb]), ptr(s[s0:s0 + nb])))
+        return m, s
+
+    def enable_timing(self, on=True):
+        check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
+
+    def timings(self) -> dict:
+        ms = (ctypes.c_float * len(_amr.TF_NAMES))()
+        check(lib().amr_fsk_plan_timings(self.handle, ms, len(_amr.TF_NAMES)))
+        return {k: float(v) for k, v in zip(_amr.TF_NAMES, ms) if v >= 0}
+
+
+_plans: dict = {}
+_plans_lock = threading.Lock()
+MAX_CHUNK = 16384
+
+
+def get_fsk_plan(n, baud, mark_freq, space_freq, samp_rate, batch) -> FskPlan:
+    dev = _amr.default_device()
+    key = (int(n), float(baud), float(mark_freq), float(space_freq), float(samp_rate), dev)
+    with _plans_lock:
+        pl = _plans.get(key)
+        if pl is None or pl.max_streams < min(batch, MAX_CHUNK):
+            # drop the old plan's HBM scratch before sizing a bigger one
+            _plans.pop(key, None)
+            pl = None
+            pl = FskPlan(n, baud, mark_freq, space_freq, samp_rate, max_streams=max(16, min(batch, MAX_CHUNK)),
+                         device=dev)
+            _plans[key] = pl
+        return pl
 
 
 def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate) -> list:
@@ -31,4 +140,6 @@ def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate) 
         raise ValueError("batch input must be a 2-D [streams, samples] array")
     design_fsk(x.shape[1], baud, mark_freq, space_freq, samp_rate)
     _amr.require_gpu()
-    raise _amr.AmrError(_amr.AMR_E_INVALID, "FSK GPU kernels are not built yet")
+    if x.shape[0] == 0:
+        return []
+    return get_fsk_plan(x.shape[1], baud, mark_freq, space_freq, samp_rate, x.shape[0]).demod_host(x)[0]

@@ -60,4 +60,20 @@ struct PskBuffers {
   int64_t* sync_idx;      // [B]
 };
 
+// FSK (fsk_kernels.hip): both tones' band-pass filters, lane = (stream, tone)
+struct FskParams {
+  int64_t n;        // samples per stream
+  int64_t sps;      // int(fs / baud)
+  int64_t n_bits;   // decided bits per stream
+  int64_t n_words;
+  int nt;           // band-pass taps (7)
+  int pad;          // 3 * nt
+};
+
+struct FskIir {            // [tone][tap], tone 0 = mark
+  double b[2][8];
+  double a[2][8];
+  double zi[2][8];
+};
+
 }  // namespace amr

@@ -12,8 +12,8 @@
 #include <string>
 #include <vector>
 
-#include "../../include/amr.h"
 #include "amr_internal.h"
+#include "api_common.h"
 
 namespace amr {
 hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
@@ -30,21 +30,24 @@ hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, u
 using namespace amr;
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+int amr::fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
 
-#define HIP_TRY(expr)                                                                              \
-  do {                                                                                             \
-    hipError_t e_ = (expr);                                                                        \
-    if (e_ != hipSuccess)                                                                          \
-      return fail(e_ == hipErrorOutOfMemory ? AMR_E_NOMEM : AMR_E_HIP,                             \
-                  std::string(#expr) + ": " + hipGetErrorString(e_));                             \
-  } while (0)
+int64_t amr::dtype_size(int dtype) {
+  switch (dtype) {
+    case AMR_DTYPE_F32: return 4;
+    case AMR_DTYPE_F64: return 8;
+    case AMR_DTYPE_I16: return 2;
+  }
+  return 0;
+}
+
+namespace {
 
 // CRC32 tables for the FEC kernel (uploaded once per device)
 struct CrcTables {
@@ -91,15 +94,6 @@ int device_crc(int dev, const uint32_t** table, const uint32_t** x2n) {
   *table = g_crc[dev].d;
   *x2n = g_crc[dev].d + 256;
   return AMR_OK;
-}
-
-int64_t dtype_size(int dtype) {
-  switch (dtype) {
-    case AMR_DTYPE_F32: return 4;
-    case AMR_DTYPE_F64: return 8;
-    case AMR_DTYPE_I16: return 2;
-  }
-  return 0;
 }
 
 bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }

@@ -523,6 +523,9 @@ __device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k,
   return ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2 + comp;
 }
 
+// VAR != 0: timing-only ablations for tools/k2_ablation.py (wrong results):
+//   1 = no main-body stores, 2 = no LO (bb = f), 3 = no detector, 4 = no f loads
+template <int VAR>
 __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
   const int j = lane & 1, sl = lane >> 1;
@@ -550,7 +553,8 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
   // numpy's (f + 0j) * lo for this component: fma(f, lo_c, addend) with an
   // exactly-zero addend == (f * lo_c) + addend whenever f*lo_c does not
   // underflow to zero; that case makes |bb| < 2^-1022 and is flagged below.
-  auto MIXL = [&](double fv, double2 l) { return fv * l.x + l.y; };
+  auto MIXL = [&](double fv, double2 l) { return VAR == 2 ? fv : fv * l.x + l.y; };
+  double sink = 0.0;
   auto MIX = [&](double fv, int64_t i) { return MIXL(fv, lo[2 * i]); };
   auto X = [&](int64_t i) {
     const double2 fp = fsrc[(size_t)(i >> 1) * 32];
@@ -578,7 +582,8 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
     auto load = [&](double2 (&fr)[PP], double2& lr, int64_t cc0) {
       const int64_t cc = cc0 < nc ? cc0 : nc - 1;
 #pragma unroll
-      for (int k = 0; k < PP; ++k) fr[k] = fsrc[(size_t)(cc * PP + k) * 32];
+      for (int k = 0; k < PP; ++k)
+        fr[k] = VAR == 4 ? make_double2(1e-3 * (k + lane) + cc, 2e-3 * k + cc) : fsrc[(size_t)(cc * PP + k) * 32];
       lr = lo[2 * (cc * kLpChunk + (lane & (kLpChunk - 1)))];
     };
     auto bcast = [&](const double2& lr, int k) {   // lane k's LO entry, as wave-uniform values
@@ -598,13 +603,14 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
         const double e0v = MIXL(fr[k].x, bcast(lr, 2 * k));
         const double e1v = MIXL(fr[k].y, bcast(lr, 2 * k + 1));
         // bb[0] is judged by its class above, not by magnitude
-        xmin = fmin(xmin, (k == 0 && cc == 0) ? __builtin_inf() : fabs(e0v));
+        if (VAR != 3) xmin = fmin(xmin, (k == 0 && cc == 0) ? __builtin_inf() : fabs(e0v));
         double t0, t1;
         const double y0 = pair_step2(c, zA, zB, e0v, t0);
-        xmin = fmin(xmin, fabs(e1v));
+        if (VAR != 3) xmin = fmin(xmin, fabs(e1v));
         const double y1 = pair_step2(c, zA, zB, e1v, t1);
-        ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
-        dst[(size_t)k * 32] = make_double2(y0, y1);
+        if (VAR != 3) ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
+        if (VAR == 1) sink += y0 - y1;
+        else dst[(size_t)k * 32] = make_double2(y0, y1);
       }
     };
     load(fa, la, 0);
@@ -636,6 +642,7 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p,
     ymin = fmin(ymin, fabs(y));
     s3[s3_index(hg, comp, m2_pairs, pad + n + jj + qs, sl)] = y;
   }
+  if (VAR == 1 && sink == 1.2345) bad = true;
   bad |= !(xmin >= kMinNormal) || (j == 0 && !(ymin >= kMinNormal));   // ymin is y only on j == 0
   bad |= !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
   int fl = bad ? 1 : 0;
@@ -969,7 +976,16 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const
   if (f.nt != 5) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lowpass_fwd, dim3((unsigned)(4 * groups)), dim3(kWave), 0, st, b, p, f);
+  const char* v = getenv("AMR_K2_VARIANT");
+  const int var = v ? atoi(v) : 0;
+  const dim3 grid((unsigned)(4 * groups)), block(kWave);
+  switch (var) {
+    case 1: hipLaunchKernelGGL(k_lowpass_fwd<1>, grid, block, 0, st, b, p, f); break;
+    case 2: hipLaunchKernelGGL(k_lowpass_fwd<2>, grid, block, 0, st, b, p, f); break;
+    case 3: hipLaunchKernelGGL(k_lowpass_fwd<3>, grid, block, 0, st, b, p, f); break;
+    case 4: hipLaunchKernelGGL(k_lowpass_fwd<4>, grid, block, 0, st, b, p, f); break;
+    default: hipLaunchKernelGGL(k_lowpass_fwd<0>, grid, block, 0, st, b, p, f); break;
+  }
   return hipGetLastError();
 }
 

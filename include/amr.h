@@ -23,6 +23,13 @@
  *   amr_psk_demod_device    the same with the batch already resident in HBM
  *   amr_psk_demod_fec_device  8PSK alias + fec.ReedSolomonFEC.decode fused
  *                           (modem.py:348 then fec.py:34-69; BASELINE config 5)
+ *   amr_fsk_plan_create     the per-call butter/lfilter_zi setup of
+ *                           modem.fsk_demodulate    modem.py:301-307
+ *   amr_fsk_demod_host      modem.fsk_demodulate    modem.py:298-341 (also
+ *                           fsk_high_speed_demodulate modem.py:355-356,
+ *                           ft8_demodulate modem.py:391), batched
+ *   amr_fsk_envelopes_host  the envelopes |hilbert(filtfilt(.))| modem.py:308-309
+ *   amr_hilbert_host        scipy.signal.hilbert as modem.py:309 calls it
  *   amr_fec_decode_host     fec.ReedSolomonFEC.decode  fec.py:34-69, batched
  *   amr_allgather           the gather of decoded bytes across GPUs (RCCL)
  *
@@ -128,6 +135,54 @@ int amr_psk_demod_fec_device(amr_psk_plan *plan, const void *d_x, int dtype, int
                              int64_t x_stride, uint8_t *d_out, int64_t out_stride, int64_t *d_out_len,
                              int64_t *d_sync_idx, uint8_t *d_fec, int64_t fec_stride, int64_t *d_fec_len,
                              int32_t *d_crc_ok);
+
+/* ---- FSK demodulation (modem.py:298-341) ------------------------------------
+ * Replaces modem.fsk_demodulate(samples, baud, mark, space, fs) for a batch of
+ * equal-length streams (also fsk_high_speed_demodulate modem.py:355-356,
+ * ft8_demodulate modem.py:391 and the decoder's FSK dispatch decoder.py:426-432).
+ * n_samples     samples per stream
+ * sps           int(fs / baud)                                  modem.py:301
+ * mark_* space_* butter(3, [(f-baud)/nyq, (f+baud)/nyq], 'band') b, a and
+ *               lfilter_zi (ntaps each, a[0] == 1)              modem.py:307
+ * The envelopes |hilbert(filtfilt(...))| (modem.py:308-309) use a double-precision
+ * FFT of length n_samples (mixed radix 2/3/4/5, Bluestein otherwise).
+ */
+#define AMR_TF_BANDPASS 0     /* both tones' filtfilt */
+#define AMR_TF_FFT_FWD 1      /* forward FFT incl. the -i*sgn(k) multiplier */
+#define AMR_TF_FFT_INV 2      /* inverse FFT incl. both envelopes and the compare */
+#define AMR_TF_DECIDE 3       /* window majority, sync and pack */
+#define AMR_TF_COUNT 4
+
+typedef struct amr_fsk_plan amr_fsk_plan;
+
+int amr_fsk_plan_create(amr_fsk_plan **plan, int device, int64_t n_samples, int64_t sps, const double *mark_b,
+                        const double *mark_a, const double *mark_zi, const double *space_b, const double *space_a,
+                        const double *space_zi, int ntaps, int64_t max_streams);
+int amr_fsk_plan_destroy(amr_fsk_plan *plan);
+int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan *plan);
+int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan *plan);
+/* FFT length actually run: n_samples, or the Bluestein length when n is not 5-smooth */
+int64_t amr_fsk_plan_fft_length(const amr_fsk_plan *plan);
+int amr_fsk_plan_synchronize(amr_fsk_plan *plan);
+int amr_fsk_plan_enable_timing(amr_fsk_plan *plan, int on);
+/* milliseconds of each AMR_TF_* stage in the last call (-1 = not run) */
+int amr_fsk_plan_timings(amr_fsk_plan *plan, float *ms, int count);
+/* Same contracts as amr_psk_demod_host / _device. */
+int amr_fsk_demod_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                       uint8_t *out, int64_t out_stride, int64_t *out_len, int64_t *sync_idx);
+int amr_fsk_demod_device(amr_fsk_plan *plan, const void *d_x, int dtype, int64_t n_streams, int64_t x_stride,
+                         uint8_t *d_out, int64_t out_stride, int64_t *d_out_len, int64_t *d_sync_idx);
+/* mark_env, space_env: [n_streams][n_samples] doubles, |hilbert(filtfilt(.))|
+ * of each tone (modem.py:308-309) -- the intermediate the tolerance tests read. */
+int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                           double *mark_env, double *space_env);
+
+/* ---- FFT / Hilbert (the transforms under scipy.signal.hilbert) --------------
+ * in/out: [batch][n] interleaved complex doubles; inverse scales by 1/n
+ * (numpy.fft.fft / numpy.fft.ifft).  analytic: [batch][n] complex doubles =
+ * scipy.signal.hilbert(x) for real x [batch][n].  Synchronous, on `device`. */
+int amr_fft_c2c_host(const double *in, double *out, int64_t n, int64_t batch, int inverse, int device);
+int amr_hilbert_host(const double *x, double *analytic, int64_t n, int64_t batch, int device);
 
 /* ---- FEC (fec.py:34-69) -----------------------------------------------------
  * in: [n][in_stride] bytes, in_len[n]; out: [n][out_stride] (>= in_len each);

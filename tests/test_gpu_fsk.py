@@ -1,0 +1,152 @@
+"""GPU parity of the FSK path (modem.py:298-341) and its FFT/Hilbert core.
+
+Bars (stated here):
+  * decoded bytes and sync index: bit-exact against the reference's golden
+    outputs and against the oracle (scipy's own hilbert + the C restatement);
+  * FFT / Hilbert intermediates: the GPU's fp64 FFT is not pocketfft, so its
+    rounding differs -- max |err| <= 1e-12 * max |X| (1e-11 for Bluestein
+    lengths) against numpy.fft, and envelopes within 1e-9 relative of the
+    reference's |hilbert(filtfilt(.))| (the tolerance north_star names for
+    intermediate magnitudes).
+"""
+import numpy as np
+import pytest
+
+from _util import call_case, expected, outcome
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(built_lib):
+    import _amr
+    if _amr.device_count() < 1:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
+
+
+@pytest.mark.parametrize("n,batch", [(96000, 3), (51840, 2), (24001, 2), (1000, 5), (7, 4), (409600, 1),
+                                     (97, 3)])
+def test_fft_matches_numpy(n, batch):
+    import _amr
+    rng = np.random.default_rng(n)
+    x = rng.normal(size=(batch, n)) + 1j * rng.normal(size=(batch, n))
+    for inverse, ref in ((False, np.fft.fft), (True, np.fft.ifft)):
+        got = _amr.fft(x, inverse=inverse)
+        want = ref(x, axis=1)
+        err = np.abs(got - want).max() / np.abs(want).max()
+        tol = 1e-12 if n in (96000, 51840, 1000, 409600) else 1e-11
+        assert err <= tol, (n, inverse, err)
+
+
+@pytest.mark.parametrize("n", [96000, 24001, 51840, 22])
+def test_hilbert_matches_scipy(n):
+    import _amr
+    from scipy import signal
+    rng = np.random.default_rng(n + 1)
+    x = rng.normal(size=(3, n))
+    got = _amr.hilbert(x)
+    want = signal.hilbert(x, axis=1)
+    assert np.abs(got - want).max() <= 1e-11 * np.abs(want).max()
+
+
+def test_every_golden_fsk_case(golden):
+    """Bytes (or the ValueError) of every FSK case the reference produced."""
+    import modem
+    manifest, inputs = golden
+    cases = [c for c in manifest["cases"] if c["fn"].startswith("fsk")]
+    assert len(cases) >= 6
+    bad = []
+    for case in cases:
+        got = outcome(lambda: call_case(modem, case, inputs[case["id"]]))
+        if got != expected(case):
+            bad.append((case["id"], got[:2]))
+    assert not bad, f"GPU differs from the reference on {bad}"
+
+
+def test_fsk_bluestein_length_uses_bluestein(golden):
+    import _fsk
+    _, inputs = golden
+    x = inputs["fsk9600_f32_1"]
+    pl = _fsk.FskPlan(x.size, 9600, 12000.0, 24000.0, max_streams=1)
+    assert pl.fft_length != x.size and pl.fft_length >= 2 * x.size - 1
+
+
+@pytest.mark.parametrize("case_id", ["fsk9600_f32_0", "fsk9600_f32_1", "fsk1200_f32"])
+def test_fsk_envelopes_within_tolerance(golden, case_id):
+    import _fsk
+    from oracle import oracle
+    from scipy import signal
+    manifest, inputs = golden
+    case = [c for c in manifest["cases"] if c["id"] == case_id][0]
+    p = case["params"]
+    x = inputs[case_id]
+    pl = _fsk.FskPlan(x.size, p["baud"], p["mark_freq"], p["space_freq"], max_streams=1)
+    m, s = pl.envelopes(x[None, :])
+    nyq = 48000.0
+    for got, f in ((m[0], p["mark_freq"]), (s[0], p["space_freq"])):
+        b, a = signal.butter(3, [(f - p["baud"]) / nyq, (f + p["baud"]) / nyq], btype="band")
+        want = np.abs(signal.hilbert(oracle.filtfilt(b, a, x)))
+        assert np.abs(got - want).max() <= 1e-9 * np.abs(want).max()
+
+
+@pytest.mark.parametrize("B,N,baud,mark,space,dtype", [
+    (64, 96000, 9600, 12000.0, 24000.0, np.float32),
+    (33, 48000, 1200, 2400.0, 4800.0, np.float64),
+    (20, 30011, 4800, 8000.0, 16000.0, np.float32),     # Bluestein length
+    (17, 9600, 19200, 21000.0, 27000.0, np.float32),    # sps 5: windows of 2
+])
+def test_fsk_batch_vs_oracle(B, N, baud, mark, space, dtype):
+    import _fsk
+    import synth
+    from oracle import oracle
+    x = synth.fsk_batch(B, N, baud, mark, space, seed=B, distinct=4, noise=0.3).astype(dtype)
+    pl = _fsk.FskPlan(N, baud, mark, space, max_streams=B)
+    got, _ = pl.demod_host(x)
+    want = [oracle.fsk_demodulate(x[i], baud, mark, space) for i in range(B)]
+    mism = [i for i in range(B) if got[i] != want[i]]
+    assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
+
+
+def test_fsk_int16_pcm_equals_float64():
+    import _fsk
+    import synth
+    x = synth.fsk_batch(8, 24000, 9600, seed=3, distinct=2, noise=0.1)
+    q = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16)
+    pl = _fsk.FskPlan(24000, 9600, 12000.0, 24000.0, max_streams=8)
+    a, _ = pl.demod_host(q)
+    b, _ = pl.demod_host(q.astype(np.float64) / 32768.0)
+    assert a == b
+
+
+def test_fsk_full_batch_round_trip():
+    """BASELINE config 3 size (B=16384, N=96000 float32).  Streams are 16
+    distinct frames plus light noise; every noisy stream must decode exactly
+    like its clean frame (size-independent property), the clean frames must
+    match the oracle, and a sample of noisy streams must too."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    B, N = 16384, 96000
+    x = synth.fsk_batch(B, N, 9600, 12000.0, 24000.0, seed=9, distinct=16, noise=0.05)
+    clean = synth.fsk_batch(16, N, 9600, 12000.0, 24000.0, seed=9, distinct=16, noise=0.0)
+    pl = _fsk.get_fsk_plan(N, 9600, 12000.0, 24000.0, 96000, B)
+    got, sync = pl.demod_host(x)
+    ref, _ = pl.demod_host(clean)
+    for j in range(16):
+        assert ref[j] == oracle.fsk_demodulate(clean[j], 9600, 12000.0, 24000.0)
+    assert (sync >= 0).all()
+    bad = [i for i in range(B) if got[i] != ref[i % 16]]
+    assert not bad, f"{len(bad)} streams differ from their clean frame, first {bad[:5]}"
+    for i in range(0, B, 2047):
+        assert got[i] == oracle.fsk_demodulate(x[i], 9600, 12000.0, 24000.0)
+
+
+def test_fsk_timing_hooks():
+    import _fsk
+    import synth
+    x = synth.fsk_batch(32, 20000, 9600, seed=1, distinct=2)
+    pl = _fsk.FskPlan(20000, 9600, 12000.0, 24000.0, max_streams=32)
+    pl.enable_timing(True)
+    pl.demod_host(x)
+    t = pl.timings()
+    assert set(t) == {"bandpass", "fft_fwd", "fft_inv", "decide"} and all(v > 0 for v in t.values())
