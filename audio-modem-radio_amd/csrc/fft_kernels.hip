@@ -117,8 +117,9 @@ __device__ double2* lds_fft(double2* A, double2* B, const FftLen& f) {
 
 // Pass A: in[b][j] (j = j1 + n1*j2) -> T[b][k2*n1 + j1] = W_n^(j1 k2) * DFT_n2(in[b][j1 + n1*:])[k2]
 // inv: conjugate the input on load (inverse = conj(FFT(conj x))).
+template <bool INV>
 __global__ __launch_bounds__(kFftThreads) void k_fft_pass_a(const double2* __restrict__ in, double2* __restrict__ out,
-                                                           FftDesc d, int64_t batch, int inv) {
+                                                           FftDesc d, int64_t batch) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n1 + kFftTile - 1) / kFftTile;
   const int64_t b = blockIdx.x / tiles;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_pass_a(const double2* __res
     const int t = idx % kFftTile, j2 = idx / kFftTile;
     const int j1 = j1_0 + t;
     double2 v = j1 < d.n1 ? src[(size_t)j1 + (size_t)d.n1 * j2] : make_double2(0.0, 0.0);
-    A[t * L + j2] = inv ? conj2(v) : v;
+    A[t * L + j2] = INV ? conj2(v) : v;
   }
   const double2* R = lds_fft(A, B, d.a);
   double2* dst = out + (size_t)b * d.n;
@@ -154,10 +155,11 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_pass_a(const double2* __res
 //              cmp[b][k] = hypot(f.x, X.x) > hypot(f.y, X.y)        (modem.py:309,315)
 //   kEnvOut    the two envelopes themselves -> dst[b][k] = (|a_mark|, |a_space|)
 //   kMulTab    dst[b][k] = X * tab[k]        (Bluestein: times FFT(chirp))
+template <int MODE>
 __device__ __forceinline__ void fft_epilogue(const FftEpi& e, double2* __restrict__ dst, int64_t b, int64_t k,
                                              double2 v) {
   const size_t o = (size_t)b * e.n + k;
-  switch (e.mode) {
+  switch (MODE) {
     case kHilbert: {
       const int64_t k2 = 2 * k;
       v = (k == 0 || k2 == e.n) ? make_double2(0.0, 0.0) : (k2 < e.n ? mul_mi(v) : make_double2(-v.y, v.x));
@@ -181,9 +183,9 @@ __device__ __forceinline__ void fft_epilogue(const FftEpi& e, double2* __restric
 
 // Pass C: T[b][k2*n1 + j1] -> X[b][k2 + n2*k1] = DFT_n1(T[b][k2*n1 + :])[k1]
 // inv: conjugate and scale by `scale`; then the epilogue.
+template <bool INV, int MODE>
 __global__ __launch_bounds__(kFftThreads) void k_fft_pass_c(const double2* __restrict__ in, double2* __restrict__ out,
-                                                           FftDesc d, int64_t batch, int inv, double scale,
-                                                           FftEpi e) {
+                                                           FftDesc d, int64_t batch, double scale, FftEpi e) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
   const int64_t b = blockIdx.x / tiles;
@@ -204,8 +206,8 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_pass_c(const double2* __res
     const int k2 = k2_0 + t;
     if (k2 < d.n2) {
       double2 v = R[t * L + k1];
-      if (inv) v = make_double2(v.x * scale, -v.y * scale);
-      fft_epilogue(e, out, b, (int64_t)k2 + (int64_t)d.n2 * k1, v);
+      if (INV) v = make_double2(v.x * scale, -v.y * scale);
+      fft_epilogue<MODE>(e, out, b, (int64_t)k2 + (int64_t)d.n2 * k1, v);
     }
   }
 }
@@ -230,6 +232,7 @@ __global__ __launch_bounds__(256) void k_bs_pre(const double2* __restrict__ x, d
   a[i] = v;
 }
 
+template <int MODE>
 __global__ __launch_bounds__(256) void k_bs_post(const double2* __restrict__ y, double2* __restrict__ out,
                                                  const double2* __restrict__ w, int64_t n, int64_t M, int64_t batch,
                                                  int inv, double scale, FftEpi e) {
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(256) void k_bs_post(const double2* __restrict__ y, 
   const int64_t b = i / n, k = i - b * n;
   double2 v = cmul(y[(size_t)b * M + k], conj2(w[k]));
   if (inv) v = make_double2(v.x * scale, -v.y * scale);
-  fft_epilogue(e, out, b, k, v);
+  fft_epilogue<MODE>(e, out, b, k, v);
 }
 
 size_t fft_smem_bytes(const FftDesc& d, bool pass_a) {
@@ -246,17 +249,31 @@ size_t fft_smem_bytes(const FftDesc& d, bool pass_a) {
   return (size_t)2 * kFftTile * L * sizeof(double2);
 }
 
+// The (direction, epilogue) pairs the FSK path and the test entry points use;
+// each is its own kernel so rocprof attributes time per stage.
+#define AMR_FFT_VARIANTS(X) \
+  X(false, kStore) X(true, kStore) X(false, kHilbert) X(true, kEnvelope) X(true, kEnvOut) X(false, kMulTab)
+
 hipError_t launch_fft(const double2* in, double2* tmp, double2* out, const FftDesc& d, int64_t batch, bool inverse,
                       const FftEpi& epi, hipStream_t st) {
   const unsigned ga = (unsigned)(batch * ((d.n1 + kFftTile - 1) / kFftTile));
   const unsigned gc = (unsigned)(batch * ((d.n2 + kFftTile - 1) / kFftTile));
-  hipLaunchKernelGGL(k_fft_pass_a, dim3(ga), dim3(kFftThreads), fft_smem_bytes(d, true), st, in, tmp, d, batch,
-                     inverse ? 1 : 0);
+  const size_t sa = fft_smem_bytes(d, true), sc = fft_smem_bytes(d, false);
+  if (inverse)
+    hipLaunchKernelGGL(k_fft_pass_a<true>, dim3(ga), dim3(kFftThreads), sa, st, in, tmp, d, batch);
+  else
+    hipLaunchKernelGGL(k_fft_pass_a<false>, dim3(ga), dim3(kFftThreads), sa, st, in, tmp, d, batch);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_fft_pass_c, dim3(gc), dim3(kFftThreads), fft_smem_bytes(d, false), st, tmp, out, d, batch,
-                     inverse ? 1 : 0, inverse ? 1.0 / (double)d.n : 1.0, epi);
-  return hipGetLastError();
+  const double scale = inverse ? 1.0 / (double)d.n : 1.0;
+#define AMR_FFT_LAUNCH_C(I, M)                                                                          \
+  if (inverse == I && epi.mode == M) {                                                                  \
+    hipLaunchKernelGGL((k_fft_pass_c<I, M>), dim3(gc), dim3(kFftThreads), sc, st, tmp, out, d, batch, scale, epi); \
+    return hipGetLastError();                                                                           \
+  }
+  AMR_FFT_VARIANTS(AMR_FFT_LAUNCH_C)
+#undef AMR_FFT_LAUNCH_C
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_bs_pre(const double2* x, double2* a, const double2* w, int64_t n, int64_t M, int64_t batch,
@@ -270,17 +287,30 @@ hipError_t launch_bs_pre(const double2* x, double2* a, const double2* w, int64_t
 hipError_t launch_bs_post(const double2* y, double2* out, const double2* w, int64_t n, int64_t M, int64_t batch,
                           bool inverse, const FftEpi& epi, hipStream_t st) {
   const int64_t tot = batch * n;
-  hipLaunchKernelGGL(k_bs_post, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, y, out, w, n, M, batch,
-                     inverse ? 1 : 0, inverse ? 1.0 / (double)n : 1.0, epi);
+  const dim3 g((unsigned)((tot + 255) / 256));
+  const int inv = inverse ? 1 : 0;
+  const double scale = inverse ? 1.0 / (double)n : 1.0;
+  switch (epi.mode) {
+    case kStore: hipLaunchKernelGGL(k_bs_post<kStore>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
+    case kHilbert: hipLaunchKernelGGL(k_bs_post<kHilbert>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
+    case kEnvelope: hipLaunchKernelGGL(k_bs_post<kEnvelope>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
+    case kEnvOut: hipLaunchKernelGGL(k_bs_post<kEnvOut>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 hipError_t fft_configure_smem() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_fft_pass_a, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     2 * kFftTile * kFftMaxL * (int)sizeof(double2));
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)k_fft_pass_c, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             2 * kFftTile * kFftMaxL * (int)sizeof(double2));
+  const int bytes = 2 * kFftTile * kFftMaxL * (int)sizeof(double2);
+  hipError_t e = hipFuncSetAttribute((const void*)k_fft_pass_a<false>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)k_fft_pass_a<true>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+#define AMR_FFT_ATTR_C(I, M)                                                                                 \
+  if (e == hipSuccess)                                                                                       \
+    e = hipFuncSetAttribute((const void*)k_fft_pass_c<I, M>, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  AMR_FFT_VARIANTS(AMR_FFT_ATTR_C)
+#undef AMR_FFT_ATTR_C
+  return e;
 }
 
 }  // namespace amr

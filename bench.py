@@ -35,6 +35,7 @@ import synth  # noqa: E402
 
 FS = 96000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PROFILE_ROUND = "r01"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
 
 
@@ -79,14 +80,33 @@ def cpu_baseline(x_sample: np.ndarray, baud: float, threads: int):
     return x_sample.shape[0] * (S - 1) / dt / 1e6, dt, outs
 
 
+def cpu_baseline_fsk(x_sample: np.ndarray, baud, mark, space, threads: int):
+    """oracle.fsk_demodulate (C filtfilt + scipy's hilbert + C decide) on the host cores."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle
+    oracle.lib()
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        outs = list(ex.map(lambda r: oracle.fsk_demodulate(r, baud, mark, space), x_sample))
+    dt = time.perf_counter() - t0
+    sps = int(FS / baud)
+    nb = (x_sample.shape[1] - sps // 2 + sps - 1) // sps
+    return x_sample.shape[0] * nb / dt / 1e6, dt, outs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--workload", choices=["qpsk9600", "fsk9600"], default="qpsk9600",
+                    help="qpsk9600 = BASELINE configs[1] (the headline metric); fsk9600 = configs[3]")
+    ap.add_argument("--batch", type=int, default=0, help="streams per GPU (0 = the config's: 4096 / 16384)")
     ap.add_argument("--samples", type=int, default=96000)
     ap.add_argument("--baud", type=float, default=9600)
+    ap.add_argument("--mark", type=float, default=12000.0, help="fsk9600: mark tone (SURVEY §6 config 3)")
+    ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
     ap.add_argument("--distinct", type=int, default=64, help="distinct waveforms (noise is per stream)")
     ap.add_argument("--cpu-streams", type=int, default=0, help="cpu_baseline sample size (0 = auto ~10 s CPU)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -94,19 +114,31 @@ def main():
 
     dist, world, rank, local = dist_setup(args.gpus)
     dev = local
-    B, N, baud = args.batch, args.samples, args.baud
+    fsk = args.workload == "fsk9600"
+    B = args.batch or (16384 if fsk else 4096)
+    N, baud = args.samples, args.baud
     L = _amr.lib()
     _amr.check(L.amr_set_device(dev))
 
     t0 = time.perf_counter()
-    x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
+    if fsk:
+        x = synth.fsk_batch(B, N, baud, args.mark, args.space, seed=1000 + rank, distinct=args.distinct)
+    else:
+        x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
     log(f"[rank {rank}] synthesised {B}x{N} float32 in {time.perf_counter() - t0:.1f}s")
 
-    plan = _amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev)
+    if fsk:
+        import _fsk
+        plan = _fsk.FskPlan(N, baud, args.mark, args.space, FS, max_streams=B, device=dev)
+        sym_per_stream = (N - plan.sps // 2 + plan.sps - 1) // plan.sps     # decided bits (modem.py:320)
+        demod, sync_fn, names = L.amr_fsk_demod_device, L.amr_fsk_plan_synchronize, _amr.TF_NAMES
+    else:
+        plan = _amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev)
+        S = (N - plan.first + plan.sps - 1) // plan.sps
+        sym_per_stream = S - 1                       # differential symbols decided per stream
+        demod, sync_fn, names = L.amr_psk_demod_device, L.amr_psk_plan_synchronize, _amr.T_NAMES
     plan.enable_timing(True)
     cap = plan.out_cap
-    S = (N - plan.first + plan.sps - 1) // plan.sps
-    sym_per_stream = S - 1                       # differential symbols decided per stream
 
     def dmalloc(nbytes):
         p = ctypes.c_void_p()
@@ -129,18 +161,24 @@ def main():
         _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
         d_gather = dmalloc(world * B * cap)
         d_gather_len = dmalloc(world * B * 8)
+    # amr_allgather enqueues on a PSK plan's stream (or the comm's own for NULL)
+    gather_stream = None if fsk else plan.handle
 
     def step():
-        _amr.check(L.amr_psk_demod_device(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
+        _amr.check(demod(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
         if comm is not None:
+            if fsk:
+                _amr.check(sync_fn(plan.handle))
             # the decoded bytes of every rank to every rank (RCCL over xGMI)
-            _amr.check(L.amr_allgather(comm, d_out, d_gather, B * cap, plan.handle))
-            _amr.check(L.amr_allgather(comm, d_len, d_gather_len, B * 8, plan.handle))
-        _amr.check(L.amr_psk_plan_synchronize(plan.handle))
+            _amr.check(L.amr_allgather(comm, d_out, d_gather, B * cap, gather_stream))
+            _amr.check(L.amr_allgather(comm, d_len, d_gather_len, B * 8, gather_stream))
+            if fsk:
+                _amr.check(L.amr_comm_synchronize(comm))
+        _amr.check(sync_fn(plan.handle))
 
     for _ in range(args.warmup):
         step()
-    kt = {k: 0.0 for k in _amr.T_NAMES}
+    kt = {k: 0.0 for k in names}
     barrier(dist)
     _amr.check(L.amr_device_synchronize())
     t0 = time.perf_counter()
@@ -160,31 +198,43 @@ def main():
     kavg = {k: v / args.steps for k, v in kt.items() if v > 0}
     dom = max(kavg, key=kavg.get)
     # Algorithmic bytes per launch: each stage's
-    # compulsory input + output at its minimal width --
-    #   bandpass    : x float32 (4 B/sample) in, filtered f float64 (8 B) out
-    #   lowpass_fwd : f (8 B) in, forward low-pass complex128 (16 B) out
-    #   lowpass_bwd : forward low-pass (16 B) in, symbol samples (16 B/symbol) out
-    #   sync_pack   : symbols (16 B/symbol) in, packed bytes out
-    S_sym = sym_per_stream + 1
-    alg_bytes = {"bandpass": B * N * (4 + 8), "lowpass_fwd": B * N * (8 + 16),
-                 "lowpass_bwd": B * (N * 16 + S_sym * 16), "sync_pack": B * (S_sym * 16 + cap),
-                 "lowpass_exact": 0, "fec": 0}
-    # FP64 operations scipy's arithmetic needs (no FMA): band-pass 30/sample per
-    # pass (9 taps incl. the zero odd taps), low-pass 17/sample per pass per
-    # component, mixer 2/sample
-    fp64_ops = {"bandpass": B * ((N + 54) + (N + 27)) * 30,
-                "lowpass_fwd": B * ((N + 30) * 2 * 17 + N * 2),
-                "lowpass_bwd": B * (N + 30) * 2 * 17}
+    # compulsory input + output at its minimal width.
+    if fsk:
+        #   bandpass : x float32 (4 B/sample) in, z = f_mark + i f_space (16 B) out
+        #   fft_fwd  : z (16 B) in, spectrum (16 B) out      (one fused transform)
+        #   fft_inv  : spectrum (16 B) + z (16 B) in, compare byte (1 B) out
+        #   decide   : compare bytes in the windows (sps//2 of every sps) + output bytes
+        q = plan.sps // 4
+        alg_bytes = {"bandpass": B * N * (4 + 16), "fft_fwd": B * N * 32, "fft_inv": B * N * 33,
+                     "decide": B * (sym_per_stream * 2 * q + cap)}
+        # FP64 ops: filtfilt 7 taps = 25 ops/sample/pass/tone; FFT ~ 5 n log2 n per transform
+        fp64_ops = {"bandpass": B * 2 * 2 * (N + 42) * 25,
+                    "fft_fwd": B * 5 * N * np.log2(N), "fft_inv": B * 5 * N * np.log2(N)}
+    else:
+        #   bandpass    : x float32 (4 B/sample) in, filtered f float64 (8 B) out
+        #   lowpass_fwd : f (8 B) in, forward low-pass complex128 (16 B) out
+        #   lowpass_bwd : forward low-pass (16 B) in, symbol samples (16 B/symbol) out
+        #   sync_pack   : symbols (16 B/symbol) in, packed bytes out
+        S_sym = sym_per_stream + 1
+        alg_bytes = {"bandpass": B * N * (4 + 8), "lowpass_fwd": B * N * (8 + 16),
+                     "lowpass_bwd": B * (N * 16 + S_sym * 16), "sync_pack": B * (S_sym * 16 + cap),
+                     "lowpass_exact": 0, "fec": 0}
+        # FP64 operations scipy's arithmetic needs (no FMA): band-pass 30/sample per
+        # pass (9 taps incl. the zero odd taps), low-pass 17/sample per pass per
+        # component, mixer 2/sample
+        fp64_ops = {"bandpass": B * ((N + 54) + (N + 27)) * 30,
+                    "lowpass_fwd": B * ((N + 30) * 2 * 17 + N * 2),
+                    "lowpass_bwd": B * (N + 30) * 2 * 17}
     achieved = alg_bytes[dom] / (kavg[dom] / 1e3) / 1e9
-    pipeline_bytes = B * N * 4 + B * sym_per_stream * 2 / 8
+    pipeline_bytes = B * N * 4 + B * sym_per_stream * (1 if fsk else 2) / 8
     fp64_achieved = fp64_ops.get(dom, 0) / (kavg[dom] / 1e3) / 1e12
     traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", "r01_pmc.json")
-    if (B, N, int(baud)) == (4096, 96000, 9600) and os.path.exists(pmc_file):
+    pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
+    if (B, N, int(baud)) == ((16384 if fsk else 4096), 96000, 9600) and os.path.exists(pmc_file):
         with open(pmc_file) as f:
-            pk = json.load(f)["kernels"].get("k_" + dom, {})
-        if "hbm_bytes_per_dispatch" in pk:
-            traffic = int(pk["hbm_bytes_per_dispatch"])
+            pk = json.load(f).get(args.workload, {}).get("slots", {}).get(dom, {})
+        if "hbm_bytes_per_launch" in pk:
+            traffic = int(pk["hbm_bytes_per_launch"])
 
     # parity spot-check after timing (not timed): GPU bytes vs the oracle
     out = np.empty((B, cap), np.uint8)
@@ -198,34 +248,50 @@ def main():
         cpu = None
         parity = "skipped"
         if not args.no_cpu:
-            n_cpu = args.cpu_streams or B          # the whole batch: ~10 s of single-core work on the box
-            idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
-            val, cdt, couts = cpu_baseline(x[idx], baud, threads)
+            if fsk:
+                # scipy's hilbert dominates; ~30 streams ~ 10-20 s of single-core work
+                n_cpu = args.cpu_streams or 256
+                idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
+                val, cdt, couts = cpu_baseline_fsk(x[idx], baud, args.mark, args.space, threads)
+                how = "oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
+            else:
+                n_cpu = args.cpu_streams or B          # the whole batch: ~10 s of single-core work on the box
+                idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
+                val, cdt, couts = cpu_baseline(x[idx], baud, threads)
+                how = "the C restatement oracle/amr_oracle.c, OpenMP over streams"
             cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
-                   "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through the C "
-                             f"restatement oracle/amr_oracle.c, OpenMP over streams, {cdt:.2f} s wall"}
+                   "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through {how}, "
+                             f"{cdt:.2f} s wall"}
             bad = sum(1 for j, i in enumerate(idx) if out[i, :ln[i]].tobytes() != couts[j])
             parity = f"{len(idx) - bad}/{len(idx)} streams bit-exact vs oracle"
+        if fsk:
+            metric = "FSK demod Msymbols/s (batch), FSK9600 96kHz mark/space 12k/24k"
+            workload = (f"FSK@{int(baud)} 96kHz tones {args.mark:g}/{args.space:g} Hz, batch {B} x {N} float32 "
+                        "streams per GPU (BASELINE configs[3] at SURVEY §6's valid tones)")
+        else:
+            metric = "demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU"
+            workload = f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU (BASELINE configs[1])"
         result = {
-            "metric": "demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU",
+            "metric": metric,
             "value": round(value, 3), "unit": "Msym/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU "
-                                   "(BASELINE configs[1])", "global_batch": world * B, "samples_per_stream": N,
+            "config": {"workload": workload, "global_batch": world * B, "samples_per_stream": N,
                        "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": "profiles/r01_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)",
+                         "traffic_source": f"profiles/{PROFILE_ROUND}_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                           "bytes/launch)",
                          "alg_bytes_per_launch": int(alg_bytes[dom]),
                          "fp64_valu": {"achieved_tops": round(fp64_achieved, 3), "peak_tops": FP64_PEAK_TOPS,
                                        "frac": round(fp64_achieved / FP64_PEAK_TOPS, 4)}},
             "pipeline_hbm_gbs": round(pipeline_bytes / (ms_per_step / 1e3) / 1e9, 2),
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
-            "exact_path_streams": plan.exact_streams(),
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if not fsk:
+            result["exact_path_streams"] = plan.exact_streams()
         print(json.dumps(result), flush=True)
     for p in (d_x, d_out, d_len, d_sync):
         L.amr_free(p)

@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """Fold rocprofv3 CSVs (scripts/profile.sh) into profiles/<tag>_*.
 
+    python scripts/prof_summary.py gpurun_out/prof_<tag>_<workload> <tag> <workload>
+
 Outputs:
-  profiles/<tag>_kernel_stats.csv   rocprofv3 --stats summary, verbatim
-  profiles/<tag>_pmc.json           per kernel: avg duration (trace pass), HBM
-                                    bytes per dispatch from FETCH_SIZE (x2, the
-                                    gfx950 wide-read correction of
-                                    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both KB
-  profiles/<tag>_summary.md         the same as a table
+  profiles/<tag>_<workload>_kernel_stats.csv  rocprofv3 --stats summary, verbatim
+  profiles/<tag>_pmc.json    [workload]["kernels"][kernel]: avg duration (trace
+                             pass), HBM bytes per dispatch from FETCH_SIZE (x2,
+                             the gfx950 wide-read correction of
+                             MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KB);
+                             [workload]["slots"][slot]: the same summed over the
+                             kernels of one bench.py timing slot, per step
+  profiles/<tag>_summary.md  the same as tables, one section per workload
 """
 import csv
 import glob
@@ -27,21 +31,36 @@ def find(d, pat):
     return m[0] if m else None
 
 
+KERNELS = ["k_bandpass_quad", "k_bandpass", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
+           "k_sync_pack", "k_fec_decode", "k_fsk_bandpass", "k_fsk_decide",
+           "k_fft_pass_a<false>", "k_fft_pass_a<true>", "k_fft_pass_c<false, 1>", "k_fft_pass_c<true, 2>",
+           "k_fft_pass_c", "k_bs_pre", "k_bs_post"]
+# bench.py timing slot -> the kernels it brackets (one launch each per step)
+SLOTS = {
+    "qpsk9600": {"bandpass": ["k_bandpass_quad", "k_bandpass"], "lowpass_fwd": ["k_lowpass_fwd"],
+                 "lowpass_bwd": ["k_lowpass_bwd"], "lowpass_exact": ["k_lowpass_exact"],
+                 "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
+    "fsk9600": {"bandpass": ["k_fsk_bandpass"], "fft_fwd": ["k_fft_pass_a<false>", "k_fft_pass_c<false, 1>"],
+                "fft_inv": ["k_fft_pass_a<true>", "k_fft_pass_c<true, 2>"], "decide": ["k_fsk_decide", "k_sync_pack"]},
+}
+
+
 def short(name):
-    for k in ("k_bandpass", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice", "k_sync_pack",
-              "k_fec_decode", "k_fsk"):
-        if k in name:
+    n = name.replace("amr::", "").replace("(amr::FftEpiMode)", "")
+    for k in KERNELS:
+        if k in n:
             return k
     return name[:60]
 
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
+    workload = sys.argv[3] if len(sys.argv) > 3 else "qpsk9600"
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     prof = os.path.join(repo, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
-    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    shutil.copy(stats, os.path.join(prof, f"{tag}_{workload}_kernel_stats.csv"))
     res = {}
     for r in rows(stats):
         res.setdefault(short(r["Name"]), {})["avg_ns"] = float(r["AverageNs"])
@@ -61,15 +80,39 @@ def main():
     for k, v in res.items():
         if "fetch_bytes_per_dispatch" in v or "write_bytes_per_dispatch" in v:
             v["hbm_bytes_per_dispatch"] = v.get("fetch_bytes_per_dispatch", 0) + v.get("write_bytes_per_dispatch", 0)
-    with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
-        json.dump({"source": "rocprofv3 kernel-trace --stats + separate --pmc FETCH_SIZE / WRITE_SIZE passes",
-                   "fetch_correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads)",
-                   "kernels": res}, f, indent=1)
+    slots = {}
+    for slot, ks in SLOTS.get(workload, {}).items():
+        got = [res[k] for k in ks if k in res]
+        if not got:
+            continue
+        d = {"kernels": [k for k in ks if k in res], "avg_ns": sum(g.get("avg_ns", 0) for g in got)}
+        for key in ("fetch_bytes_per_dispatch", "write_bytes_per_dispatch", "hbm_bytes_per_dispatch"):
+            if all(key in g for g in got):
+                d[key.replace("_per_dispatch", "_per_launch")] = sum(g[key] for g in got)
+        slots[slot] = d
+    pmc_path = os.path.join(prof, f"{tag}_pmc.json")
+    allres = {}
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            allres = json.load(f)
+        if "kernels" in allres:       # older single-workload layout
+            allres = {}
+    allres["source"] = "rocprofv3 kernel-trace --stats + separate --pmc FETCH_SIZE / WRITE_SIZE passes"
+    allres["fetch_correction"] = "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads)"
+    allres[workload] = {"kernels": res, "slots": slots}
+    with open(pmc_path, "w") as f:
+        json.dump(allres, f, indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
-        f.write(f"# rocprofv3 summary ({tag})\n\n| kernel | calls | avg ms | HBM read MB/disp (x2 corr.) | HBM write MB/disp |\n|---|---|---|---|---|\n")
-        for k, v in sorted(res.items(), key=lambda kv: -kv[1].get("avg_ns", 0)):
-            f.write(f"| {k} | {v.get('calls', '')} | {v.get('avg_ns', 0) / 1e6:.3f} | "
-                    f"{v.get('fetch_bytes_per_dispatch', 0) / 1e6:.1f} | {v.get('write_bytes_per_dispatch', 0) / 1e6:.1f} |\n")
+        f.write(f"# rocprofv3 summary ({tag})\n")
+        for wl, r in allres.items():
+            if not isinstance(r, dict) or "kernels" not in r:
+                continue
+            f.write(f"\n## {wl}\n\n| kernel | calls | avg ms | HBM read MB/disp (x2 corr.) | HBM write MB/disp |\n"
+                    "|---|---|---|---|---|\n")
+            for k, v in sorted(r["kernels"].items(), key=lambda kv: -kv[1].get("avg_ns", 0)):
+                f.write(f"| {k} | {v.get('calls', '')} | {v.get('avg_ns', 0) / 1e6:.3f} | "
+                        f"{v.get('fetch_bytes_per_dispatch', 0) / 1e6:.1f} | "
+                        f"{v.get('write_bytes_per_dispatch', 0) / 1e6:.1f} |\n")
     print(json.dumps(res, indent=1))
 
 

@@ -7,12 +7,13 @@
 # scripts/prof_summary.py folds them into profiles/<tag>_*.{csv,json,md}.
 set -u
 TAG=${TAG:-r01}
+WORKLOAD=${WORKLOAD:-qpsk9600}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/prof_$TAG
+OUT=$ROOT/gpurun_out/prof_${TAG}_$WORKLOAD
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
-ARGS="--steps ${STEPS:-3} --warmup 1 --no-cpu ${BENCH_ARGS:-}"
+ARGS="--workload $WORKLOAD --steps ${STEPS:-3} --warmup 1 --no-cpu ${BENCH_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
@@ -20,4 +21,4 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-for
 rc=$?; echo "fetch rc=$rc"; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/write_bench.json" 2> "$OUT/write.err"
 rc=$?; echo "write rc=$rc"; [ $rc -ne 0 ] && exit $rc
-cd "$ROOT" && python3 scripts/prof_summary.py "$OUT" "$TAG"
+cd "$ROOT" && python3 scripts/prof_summary.py "$OUT" "$TAG" "$WORKLOAD"
