@@ -26,7 +26,7 @@ AMR_E_INVALID, AMR_E_PADLEN, AMR_E_HIP, AMR_E_NOMEM, AMR_E_NODEVICE, AMR_E_RCCL,
 DTYPE_F32, DTYPE_F64, DTYPE_I16 = 0, 1, 2
 PSK_QPSK, PSK_BPSK = 0, 1
 T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec"]
-TF_NAMES = ["bandpass", "fft_fwd", "fft_inv", "decide"]
+TF_NAMES = ["bandpass", "hilbert", "decide"]
 DTYPES = {np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64, np.dtype(np.int16): DTYPE_I16}
 
 # every symbol include/amr.h declares (tests/test_abi.py checks the export table)

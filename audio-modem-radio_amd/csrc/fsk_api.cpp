@@ -3,9 +3,9 @@
 //
 // Pipeline per call (all on the plan's stream):
 //   F1  k_fsk_bandpass          x -> z = f_mark + i f_space           [B][n] c128
-//   F2  FFT_n(z) * (-i sgn k)   z -> (u) -> v                         [B][n] c128
-//   F3  IFFT_n(v) + envelopes   v -> (u) -> cmp = |a_mark| > |a_space| [B][n] u8
-//   F4  k_fsk_decide + k_sync_pack  cmp -> words -> bytes
+//   F2  H[z] = IFFT_n(-i sgn(k) FFT_n(z)) in three passes z -> u -> v -> cmp,
+//       the last forming both envelopes: cmp = |a_mark| > |a_space|   [B][n] u8
+//   F3  k_fsk_decide + k_sync_pack  cmp -> words -> bytes
 // A length that is not 5-smooth runs each FFT_n as a Bluestein convolution of
 // length M (u, v then hold M-long rows).
 #include <hip/hip_runtime.h>
@@ -23,7 +23,7 @@
 #include "fft.h"
 
 namespace amr {
-hipError_t launch_fsk_bandpass(int, const void*, int64_t, int64_t, double*, double*, const FskParams&,
+hipError_t launch_fsk_bandpass(int, const void*, int64_t, int64_t, double*, double2*, const FskParams&,
                                const FskIir&, hipStream_t);
 hipError_t launch_fsk_decide(const uint8_t*, uint32_t*, int64_t, const FskParams&, hipStream_t);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
@@ -48,16 +48,6 @@ struct FftPlan {
 void fft_plan_free(FftPlan& f) {
   if (f.tables) (void)hipFree(f.tables);
   f.tables = nullptr;
-}
-
-int fill_len(FftLen& fl, int L, const double2* tw) {
-  const std::vector<int> r = radices_for(L);
-  if ((int)r.size() > kFftMaxStages) return fail(AMR_E_INVALID, "FFT factor too long");
-  fl.L = L;
-  fl.nst = (int)r.size();
-  for (int i = 0; i < fl.nst; ++i) fl.r[i] = r[(size_t)i];
-  fl.tw = tw;
-  return AMR_OK;
 }
 
 // Plans FFT_n; needs the plan's stream for the Bluestein kernel FFT.
@@ -115,8 +105,8 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
   f.d.n = M;
   f.d.n1 = n1;
   f.d.n2 = n2;
-  if (int rc = fill_len(f.d.a, n2, t)) return rc;
-  if (int rc = fill_len(f.d.c, n1, t + n2)) return rc;
+  if (!fill_fft_len(f.d.a, n2, t) || !fill_fft_len(f.d.c, n1, t + n2))
+    return fail(AMR_E_INVALID, "FFT factor plan failed for n=" + std::to_string(n));
   f.d.twn = t + n2 + n1;
   if (f.bluestein) {
     f.chirp = t + n2 + n1 + M;
@@ -126,10 +116,7 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
     HIP_TRY(hipMalloc(&a, (size_t)M * sizeof(double2)));
     hipError_t e = hipMalloc(&tmp, (size_t)M * sizeof(double2));
     if (e == hipSuccess) e = hipMemcpyAsync(a, bw.data(), (size_t)M * sizeof(double2), hipMemcpyHostToDevice, st);
-    FftEpi ep{};
-    ep.mode = kStore;
-    ep.n = M;
-    if (e == hipSuccess) e = launch_fft(a, tmp, bh, f.d, 1, false, ep, st);
+    if (e == hipSuccess) e = launch_fft(a, tmp, bh, f.d, 1, false, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(a);
     if (tmp) (void)hipFree(tmp);
@@ -138,24 +125,42 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
   return AMR_OK;
 }
 
-// X = FFT_n(in) (or IFFT_n), then the epilogue `epi` (its n must be the plan's n).
-// u, v: [batch][M] scratch; `in` must not alias u, and `out` may alias v.
-hipError_t fft_run(const FftPlan& f, const double2* in, double2* u, double2* v, double2* out, int64_t batch,
-                   bool inverse, FftEpi epi, hipStream_t st) {
-  epi.n = f.n;
-  if (!f.bluestein) return launch_fft(in, u, out, f.d, batch, inverse, epi, st);
-  const int64_t n = f.n, M = f.M;
-  hipError_t e = launch_bs_pre(in, u, f.chirp, n, M, batch, inverse, st);
-  FftEpi mul{};
-  mul.mode = kMulTab;
-  mul.n = M;
-  mul.tab = f.bhat;
-  if (e == hipSuccess) e = launch_fft(u, v, u, f.d, batch, false, mul, st);
+// out = FFT_n(in) or IFFT_n(in).  u, v: [batch][M] scratch; in != u; out != v.
+hipError_t fft_c2c(const FftPlan& f, const double2* in, double2* u, double2* v, double2* out, int64_t batch,
+                   bool inverse, hipStream_t st) {
+  if (!f.bluestein) return launch_fft(in, u, out, f.d, batch, inverse, st);
   FftEpi store{};
   store.mode = kStore;
-  store.n = M;
-  if (e == hipSuccess) e = launch_fft(u, v, u, f.d, batch, true, store, st);
-  if (e == hipSuccess) e = launch_bs_post(u, out, f.chirp, n, M, batch, inverse, epi, st);
+  store.n = f.n;        // row stride of `out` (launch_fft_filter sets its own)
+  hipError_t e = launch_bs_pre(in, u, f.chirp, f.n, f.M, batch, inverse, st);
+  if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  if (e == hipSuccess) e = launch_bs_post(v, out, f.chirp, f.n, f.M, batch, inverse, store, st);
+  return e;
+}
+
+// epi(IFFT_n(-i*sgn(k) * FFT_n(in))) = epi(H[in]), the Hilbert transform of
+// each row (scipy.signal.hilbert(x).imag for real x).  u, v: [batch][M]
+// scratch, in != u, v; a kStore / kEnvOut result lands in hilbert_out(f, u, v).
+double2* hilbert_out(const FftPlan& f, double2* u, double2* v) { return f.bluestein ? v : u; }
+
+hipError_t fft_hilbert(const FftPlan& f, const double2* in, double2* u, double2* v, int64_t batch, FftEpi epi,
+                       hipStream_t st) {
+  epi.n = f.n;
+  if (!f.bluestein) return launch_fft_filter(in, u, v, u, f.d, batch, kHilbert, nullptr, epi, st);
+  const int64_t n = f.n, M = f.M;
+  FftEpi store{};
+  store.mode = kStore;
+  FftEpi hil{};
+  hil.mode = kHilbert;
+  hil.n = n;
+  // forward: W = -i sgn(k) FFT_n(in) -> u (n-long rows)
+  hipError_t e = launch_bs_pre(in, u, f.chirp, n, M, batch, false, st);
+  if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  if (e == hipSuccess) e = launch_bs_post(v, u, f.chirp, n, M, batch, false, hil, st);
+  // inverse: epi(IFFT_n(W)) -> v / cmp
+  if (e == hipSuccess) e = launch_bs_pre(u, v, f.chirp, n, M, batch, true, st);
+  if (e == hipSuccess) e = launch_fft_filter(v, u, v, u, f.d, batch, kMulTab, f.bhat, store, st);
+  if (e == hipSuccess) e = launch_bs_post(u, v, f.chirp, n, M, batch, true, epi, st);
   return e;
 }
 
@@ -205,7 +210,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   delete pl;
 }
 
-// F1 .. F3: x -> cmp (or -> the two envelopes in v when env_out).  Caller holds mu.
+// F1, F2: x -> cmp (or -> the two envelopes in hilbert_out(u, v) when env_out).  Caller holds mu.
 int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
   hipStream_t st = pl->stream;
   auto mark = [&](int slot, int which) -> hipError_t {
@@ -214,21 +219,16 @@ int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     return hipEventRecord(pl->ev[slot][which], st);
   };
   HIP_TRY(mark(AMR_TF_BANDPASS, 0));
-  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u),
-                              reinterpret_cast<double*>(pl->z), pl->p, pl->f, st));
+  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, pl->p, pl->f, st));
   HIP_TRY(mark(AMR_TF_BANDPASS, 1));
-  FftEpi hil{};
-  hil.mode = kHilbert;
-  HIP_TRY(mark(AMR_TF_FFT_FWD, 0));
-  HIP_TRY(fft_run(pl->fft, pl->z, pl->u, pl->v, pl->v, B, false, hil, st));
-  HIP_TRY(mark(AMR_TF_FFT_FWD, 1));
   FftEpi env{};
   env.mode = env_out ? kEnvOut : kEnvelope;
   env.z = pl->z;
   env.cmp = pl->cmp;
-  HIP_TRY(mark(AMR_TF_FFT_INV, 0));
-  HIP_TRY(fft_run(pl->fft, pl->v, pl->u, pl->v, pl->v, B, true, env, st));
-  HIP_TRY(mark(AMR_TF_FFT_INV, 1));
+  // one timing slot for the whole Hilbert filter (column, middle and final row passes)
+  HIP_TRY(mark(AMR_TF_HILBERT, 0));
+  HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, st));
+  HIP_TRY(mark(AMR_TF_HILBERT, 1));
   return AMR_OK;
 }
 
@@ -320,7 +320,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   }
   const int64_t M = pl->fft.M;
   const int64_t waves = (max_streams + 31) / 32;
-  const int64_t s1_bytes = waves * (n + 2 * p.pad) * 64 * 8;
+  const int64_t s1_bytes = waves * ((n + 2 * p.pad + 2) / 2) * 64 * 16;
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, max_streams * n * 16},
@@ -429,7 +429,8 @@ int amr_fsk_envelopes_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t
   if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
   if (int rc = run_fsk_front(plan, plan->d_x, dtype, B, n, true)) return rc;
   std::vector<double> h((size_t)(B * n * 2));
-  HIP_TRY(hipMemcpyAsync(h.data(), plan->v, h.size() * 8, hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipMemcpyAsync(h.data(), hilbert_out(plan->fft, plan->u, plan->v), h.size() * 8, hipMemcpyDeviceToHost,
+                         plan->stream));
   HIP_TRY(hipStreamSynchronize(plan->stream));
   for (int64_t i = 0; i < B * n; ++i) {
     mark_env[i] = h[(size_t)(2 * i)];
@@ -453,10 +454,8 @@ int amr_fft_c2c_host(const double* in, double* out, int64_t n, int64_t batch, in
     if (e == hipSuccess) e = hipMalloc(&u, (size_t)(batch * f.M * 16));
     if (e == hipSuccess) e = hipMalloc(&v, (size_t)(batch * f.M * 16));
     if (e == hipSuccess) e = hipMemcpyAsync(x, in, (size_t)(batch * n * 16), hipMemcpyHostToDevice, st);
-    FftEpi ep{};
-    ep.mode = kStore;
-    if (e == hipSuccess) e = fft_run(f, x, u, v, v, batch, inverse != 0, ep, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, v, (size_t)(batch * n * 16), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = fft_c2c(f, x, u, v, x, batch, inverse != 0, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, x, (size_t)(batch * n * 16), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
   }
   for (void* p : {(void*)x, (void*)u, (void*)v})
@@ -481,18 +480,15 @@ int amr_hilbert_host(const double* xr, double* analytic, int64_t n, int64_t batc
   std::vector<double> h((size_t)(batch * n * 2), 0.0);
   if (!rc) {
     for (int64_t i = 0; i < batch * n; ++i) h[(size_t)(2 * i)] = xr[i];
-    e = hipMalloc(&x, (size_t)(batch * f.M * 16));   // reused as the inverse's M-long scratch
+    e = hipMalloc(&x, (size_t)(batch * n * 16));
     if (e == hipSuccess) e = hipMalloc(&u, (size_t)(batch * f.M * 16));
     if (e == hipSuccess) e = hipMalloc(&v, (size_t)(batch * f.M * 16));
     if (e == hipSuccess) e = hipMemcpyAsync(x, h.data(), h.size() * 8, hipMemcpyHostToDevice, st);
-    FftEpi hil{};
-    hil.mode = kHilbert;
     FftEpi store{};
     store.mode = kStore;
-    if (e == hipSuccess) e = fft_run(f, x, u, v, v, batch, false, hil, st);
-    // the inverse input v must not alias its u scratch; x is free again
-    if (e == hipSuccess) e = fft_run(f, v, u, x, x, batch, true, store, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), x, h.size() * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = fft_hilbert(f, x, u, v, batch, store, st);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h.data(), hilbert_out(f, u, v), h.size() * 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
   }
   for (void* p : {(void*)x, (void*)u, (void*)v})

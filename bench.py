@@ -201,15 +201,14 @@ def main():
     # compulsory input + output at its minimal width.
     if fsk:
         #   bandpass : x float32 (4 B/sample) in, z = f_mark + i f_space (16 B) out
-        #   fft_fwd  : z (16 B) in, spectrum (16 B) out      (one fused transform)
-        #   fft_inv  : spectrum (16 B) + z (16 B) in, compare byte (1 B) out
+        #   hilbert  : z (16 B) in, compare byte (1 B) out -- the FFT's own passes
+        #              over its intermediates are not algorithmic bytes
         #   decide   : compare bytes in the windows (sps//2 of every sps) + output bytes
         q = plan.sps // 4
-        alg_bytes = {"bandpass": B * N * (4 + 16), "fft_fwd": B * N * 32, "fft_inv": B * N * 33,
+        alg_bytes = {"bandpass": B * N * (4 + 16), "hilbert": B * N * 17,
                      "decide": B * (sym_per_stream * 2 * q + cap)}
         # FP64 ops: filtfilt 7 taps = 25 ops/sample/pass/tone; FFT ~ 5 n log2 n per transform
-        fp64_ops = {"bandpass": B * 2 * 2 * (N + 42) * 25,
-                    "fft_fwd": B * 5 * N * np.log2(N), "fft_inv": B * 5 * N * np.log2(N)}
+        fp64_ops = {"bandpass": B * 2 * 2 * (N + 42) * 25, "hilbert": B * 2 * 5 * N * np.log2(N)}
     else:
         #   bandpass    : x float32 (4 B/sample) in, filtered f float64 (8 B) out
         #   lowpass_fwd : f (8 B) in, forward low-pass complex128 (16 B) out

@@ -148,10 +148,9 @@ int amr_psk_demod_fec_device(amr_psk_plan *plan, const void *d_x, int dtype, int
  * FFT of length n_samples (mixed radix 2/3/4/5, Bluestein otherwise).
  */
 #define AMR_TF_BANDPASS 0     /* both tones' filtfilt */
-#define AMR_TF_FFT_FWD 1      /* forward FFT incl. the -i*sgn(k) multiplier */
-#define AMR_TF_FFT_INV 2      /* inverse FFT incl. both envelopes and the compare */
-#define AMR_TF_DECIDE 3       /* window majority, sync and pack */
-#define AMR_TF_COUNT 4
+#define AMR_TF_HILBERT 1      /* FFT, -i*sgn(k), inverse FFT, both envelopes and the compare */
+#define AMR_TF_DECIDE 2       /* window majority, sync and pack */
+#define AMR_TF_COUNT 3
 
 typedef struct amr_fsk_plan amr_fsk_plan;
 

@@ -33,15 +33,14 @@ def find(d, pat):
 
 KERNELS = ["k_bandpass_quad", "k_bandpass", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
            "k_sync_pack", "k_fec_decode", "k_fsk_bandpass", "k_fsk_decide",
-           "k_fft_pass_a<false>", "k_fft_pass_a<true>", "k_fft_pass_c<false, 1>", "k_fft_pass_c<true, 2>",
-           "k_fft_pass_c", "k_bs_pre", "k_bs_post"]
+           "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
     "qpsk9600": {"bandpass": ["k_bandpass_quad", "k_bandpass"], "lowpass_fwd": ["k_lowpass_fwd"],
                  "lowpass_bwd": ["k_lowpass_bwd"], "lowpass_exact": ["k_lowpass_exact"],
                  "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
-    "fsk9600": {"bandpass": ["k_fsk_bandpass"], "fft_fwd": ["k_fft_pass_a<false>", "k_fft_pass_c<false, 1>"],
-                "fft_inv": ["k_fft_pass_a<true>", "k_fft_pass_c<true, 2>"], "decide": ["k_fsk_decide", "k_sync_pack"]},
+    "fsk9600": {"bandpass": ["k_fsk_bandpass"], "hilbert": ["k_fft_cols", "k_fft_mid", "k_fft_rows"],
+                "decide": ["k_fsk_decide", "k_sync_pack"]},
 }
 
 

@@ -156,4 +156,4 @@ def test_fsk_timing_hooks():
     pl.enable_timing(True)
     pl.demod_host(x)
     t = pl.timings()
-    assert set(t) == {"bandpass", "fft_fwd", "fft_inv", "decide"} and all(v > 0 for v in t.values())
+    assert set(t) == {"bandpass", "hilbert", "decide"} and all(v > 0 for v in t.values())
