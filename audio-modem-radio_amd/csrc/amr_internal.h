@@ -68,6 +68,9 @@ struct FskParams {
   int64_t n_words;
   int nt;           // band-pass taps (7)
   int pad;          // 3 * nt
+  int64_t rn1, rn2; // compare-bit layout (fft.h fft_bits_stride)
+  int64_t bits_stride;
+  float inv_rn1;
 };
 
 struct FskIir {            // [tone][tap], tone 0 = mark

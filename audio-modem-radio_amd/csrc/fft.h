@@ -11,28 +11,37 @@
 
 namespace amr {
 
-constexpr int kFftTile = 8;       // rows (transforms) per workgroup: 8 x 16 B = one 128-B line per column step
-constexpr int kFftThreads = 256;
-constexpr int kFftMaxL = 640;     // longest in-LDS transform: 8 rows x 641 x 16 B = 82 KB of LDS
-constexpr int kFftMaxVals = kFftTile * kFftMaxL / kFftThreads;   // complex values a thread holds per stage
-constexpr int kFftMaxStages = 12;
+constexpr int kFftTile = 8;        // rows (transforms) per workgroup: 8 x 16 B = one 128-B line per column step
+constexpr int kFftThreads = 256;   // four waves: every stage is one butterfly per thread (8 * 25 <= 256)
+constexpr int kFftMaxR = 25;       // largest radix of one stage
+constexpr int kFftMaxL = kFftMaxR * kFftMaxR;   // two stages per row transform
 
-// One radix-r Stockham stage over rows of length L (host-precomputed so the
-// kernels never divide by a runtime value: q = int((i + 0.5f) * inv) is exact
-// for the index ranges used, |i| < 2^20).
-struct FftStage {
-  int r;          // radix 2/3/4/5
-  int ns;         // product of the previous radices
-  int nb;         // L / r butterflies per row
-  int tstep;      // L / (ns * r): W_(ns r)^(k q) = W_L^(k q tstep)
-  float inv_nb, inv_ns;
-};
+// Radices one stage can run as a register-resident DFT: a*b with a, b in 1..5.
+inline bool fft_radix_ok(int r) {
+  switch (r) {
+    case 1: case 2: case 3: case 4: case 5: case 6: case 8: case 9: case 10: case 12: case 15: case 16:
+    case 20: case 25: return true;
+  }
+  return false;
+}
 
+// LDS layout of one row's intermediate Y[j][m] (j < Q, m < P): position
+// j + qp*m with qp = Q rounded up to odd, and the row stride S = 2 (mod 16)
+// 16-B slots, so the 8 rows x 2 columns a 16-lane group touches fall in 16
+// distinct bank slots.
+__host__ __device__ constexpr int fft_block(int Q) { return Q | 1; }
+__host__ __device__ constexpr int fft_row_stride(int P, int Q) {
+  return P * fft_block(Q) + ((2 - P * fft_block(Q)) % 16 + 16) % 16;
+}
+
+// A row transform of length L = r1 * r2 (P = r1, Q = r2) in two register
+// stages: radix P over stride Q, then twiddles W_L^(j m) and radix Q
+// (fft_kernels.hip); r1 >= r2, r2 == 1 for a single stage.
 struct FftLen {
-  int L;
-  int nst;
-  float inv_L;
-  FftStage st[kFftMaxStages];
+  int L, r1, r2;
+  int qp;                         // fft_block(r2)
+  int S;                          // fft_row_stride(r1, r2)
+  float inv_r2;                   // 1/r2 for the row-major thread mapping (exact division, fft_kernels.hip)
   const double2* tw;              // W_L^t, t < L (forward sign)
 };
 
@@ -42,7 +51,8 @@ struct FftDesc {
   int n1, n2;
   FftLen a;                       // length n2: the column pass / the final row pass of a filter
   FftLen c;                       // length n1: the row pass / the middle pass of a filter
-  const double2* twn;             // W_n^t, t < n
+  const double2* tw_lo;           // W_n^t, t < 256
+  const double2* tw_hi;           // W_n^(256 t), t < ceil(n / 256)
 };
 
 // What the last pass does with each output X[b][k] (k < n):
@@ -50,7 +60,8 @@ struct FftDesc {
 //   kHilbert   dst[b][k] = -i*sgn(k) * X     (sgn = +1 for 0 < 2k < n, -1 for
 //              2k > n, 0 at k = 0 and k = n/2: scipy.signal.hilbert's h - 1)
 //   kEnvelope  X = H[z] = H[f_mark] + i*H[f_space];  f = z[b][k]:
-//              cmp[b][k] = hypot(f.x, X.x) > hypot(f.y, X.y)        (modem.py:309,315)
+//              bit k = hypot(f.x, X.x) > hypot(f.y, X.y)             (modem.py:309,315)
+//              packed 8 per byte in the row-pass tile order (fft_bit_byte)
 //   kEnvOut    the two envelopes themselves -> dst[b][k] = (|a_mark|, |a_space|)
 //   kMulTab    dst[b][k] = X * tab[k]        (Bluestein: times FFT(chirp))
 enum FftEpiMode : int { kStore = 0, kHilbert = 1, kEnvelope = 2, kEnvOut = 3, kMulTab = 4 };
@@ -59,7 +70,8 @@ struct FftEpi {
   int mode;
   int64_t n;               // logical length (row stride of z / cmp / dst)
   const double2* z;        // kEnvelope / kEnvOut
-  uint8_t* cmp;            // kEnvelope
+  uint8_t* bits;           // kEnvelope: [b][bits_stride] bytes
+  int64_t bits_stride;
   const double2* tab;      // kMulTab
 };
 
@@ -79,32 +91,38 @@ hipError_t launch_bs_post(const double2* y, double2* out, const double2* w, int6
                           bool inverse, const FftEpi& epi, hipStream_t st);
 hipError_t fft_configure_smem();
 
+// Compare bits of a length-n filter output: sample k = r + rn1*kk (r < rn1,
+// kk < rn2) is bit (r & 7) of byte (r >> 3)*rn2 + kk -- the order in which a
+// final row pass (8 rows r per workgroup, all kk) produces them, so every
+// workgroup writes one contiguous run of bytes.  rn1 = n1, rn2 = n2 for a
+// four-step length; rn1 = n, rn2 = 1 (plain bit order) after Bluestein.
+__host__ __device__ inline int64_t fft_bits_stride(int64_t rn1, int64_t rn2) { return ((rn1 + 7) >> 3) * rn2; }
+
 // ---- host planning -------------------------------------------------------
 
-inline bool smooth5(int64_t m) {
-  for (int p : {2, 3, 5})
-    while (m % p == 0) m /= p;
-  return m == 1;
+// L = r1 * r2 with both radices runnable, r1 >= r2, r2 as large as possible.
+inline bool fft_factor(int L, int& r1, int& r2) {
+  for (int b = kFftMaxR; b >= 1; --b) {
+    if (L % b || !fft_radix_ok(b)) continue;
+    const int a = L / b;
+    if (a >= b && fft_radix_ok(a)) {
+      r1 = a;
+      r2 = b;
+      return true;
+    }
+  }
+  return false;
 }
 
-inline std::vector<int> radices_for(int L) {
-  std::vector<int> r;
-  int m = L;
-  while (m % 4 == 0) { r.push_back(4); m /= 4; }
-  while (m % 2 == 0) { r.push_back(2); m /= 2; }
-  while (m % 3 == 0) { r.push_back(3); m /= 3; }
-  while (m % 5 == 0) { r.push_back(5); m /= 5; }
-  return r;
-}
-
-// n = n1 * n2 with both 5-smooth and <= kFftMaxL, n1 as close to sqrt(n) as possible.
+// n = n1 * n2 with both factorable, n1 as close to sqrt(n) as possible.
 inline bool fft_split(int64_t n, int& n1, int& n2) {
   int best = -1;
   double bestd = 1e300;
   for (int64_t a = 1; a <= kFftMaxL; ++a) {
     if (n % a) continue;
     const int64_t b = n / a;
-    if (b > kFftMaxL || !smooth5(a) || !smooth5(b)) continue;
+    int x, y;
+    if (b > kFftMaxL || !fft_factor((int)a, x, y) || !fft_factor((int)b, x, y)) continue;
     const double dd = std::fabs(std::log((double)a) - std::log((double)b));
     if (dd < bestd) { bestd = dd; best = (int)a; }
   }
@@ -114,40 +132,32 @@ inline bool fft_split(int64_t n, int& n1, int& n2) {
   return true;
 }
 
-// smallest 5-smooth m >= lo that splits (Bluestein length)
+// smallest m >= lo that splits (Bluestein length)
 inline int64_t fft_good_size(int64_t lo) {
-  for (int64_t m = lo;; ++m) {
+  for (int64_t m = lo; m <= (int64_t)kFftMaxL * kFftMaxL; ++m) {
     int a, b;
-    if (smooth5(m) && fft_split(m, a, b)) return m;
+    if (fft_split(m, a, b)) return m;
   }
+  return -1;
 }
 
-// Stage table of a length-L row transform (radices from radices_for).
 inline bool fill_fft_len(FftLen& f, int L, const double2* tw) {
-  const std::vector<int> r = radices_for(L);
-  if ((int)r.size() > kFftMaxStages || L > kFftMaxL) return false;
+  if (!fft_factor(L, f.r1, f.r2)) return false;
   f.L = L;
-  f.nst = (int)r.size();
-  f.inv_L = 1.0f / (float)L;
+  f.qp = fft_block(f.r2);
+  f.S = fft_row_stride(f.r1, f.r2);
+  f.inv_r2 = 1.0f / (float)f.r2;
   f.tw = tw;
-  int ns = 1;
-  for (int i = 0; i < f.nst; ++i) {
-    FftStage& s = f.st[i];
-    s.r = r[(size_t)i];
-    s.ns = ns;
-    s.nb = L / s.r;
-    s.tstep = L / (ns * s.r);
-    s.inv_nb = 1.0f / (float)s.nb;
-    s.inv_ns = 1.0f / (float)s.ns;
-    ns *= s.r;
-  }
   return true;
 }
 
-inline std::vector<double> twiddles(int64_t L) {   // interleaved W_L^t = exp(-2 pi i t / L)
-  std::vector<double> w((size_t)(2 * L));
-  for (int64_t t = 0; t < L; ++t) {
-    const double a = -2.0 * M_PI * (double)t / (double)L;
+inline std::vector<double> twiddles(int64_t L, int64_t count, int64_t step = 1) {
+  // interleaved W_L^(t*step) = exp(-2 pi i t step / L), t < count; the
+  // exponent is reduced mod L in integers so the angle is exact before libm
+  std::vector<double> w((size_t)(2 * count));
+  for (int64_t t = 0; t < count; ++t) {
+    const int64_t e = (t * step) % L;
+    const double a = -2.0 * M_PI * (double)e / (double)L;
     w[2 * t] = std::cos(a);
     w[2 * t + 1] = std::sin(a);
   }

@@ -13,14 +13,15 @@
 // twiddle, and the final row pass conjugates, scales and forms the envelopes.
 // Three passes over HBM instead of four.
 //
-// Every pass: a workgroup owns kFftTile = 8 transforms (rows).  Global
-// accesses move 8 consecutive complex values (one 128-B line) per column
-// step; the transform itself is a mixed-radix (2/3/4/5) Stockham autosort in
-// a single LDS buffer (rows padded by one element, so the 8 rows of a column
-// fall in distinct banks), each stage staged through registers between two
-// barriers.  The inverse transform is conj(FFT(conj(x))).
-// Twiddles come from host tables (W_L^t, t < L, fft.h), one libm cos/sin per
-// entry, so every factor is within an ulp of exact.
+// Every pass: a workgroup of four waves owns kFftTile = 8 transforms (rows) of
+// length L = P * Q <= 625, done as two register-resident stages:
+//   stage 1: radix P (a composite a*b DFT in registers) straight from HBM,
+//            outputs to LDS (one exchange per transform)
+//   stage 2: radix Q from LDS, twiddle W_L^(j m), outputs straight to HBM
+// Column accesses move 8 consecutive complex values (one 128-B line) per
+// step; row accesses are contiguous.  The inverse transform is
+// conj(FFT(conj(x))).  Twiddles come from host tables (fft.h), one libm
+// cos/sin per entry with the exponent reduced in integers.
 #include "fft.h"
 
 namespace amr {
@@ -37,7 +38,7 @@ __device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, 
 // exact floor(i / d) for 0 <= i < 2^20 given inv = 1/d rounded to float (fft.h)
 __device__ __forceinline__ int fdiv(int i, float inv) { return (int)(((float)i + 0.5f) * inv); }
 
-// forward radix-r DFTs (W = exp(-2 pi i / r))
+// forward radix-p DFTs, p <= 5 (W = exp(-2 pi i / p))
 __device__ __forceinline__ void dft2(double2* v) {
   const double2 a = v[0], b = v[1];
   v[0] = cadd(a, b);
@@ -77,66 +78,221 @@ __device__ __forceinline__ void dft5(double2* v) {
   v[3] = csub(m2, n2);
 }
 
-// One Stockham stage (radix R) over kFftTile rows of length L, in place in
-// LDS: every thread reads its butterflies' inputs into registers, the block
-// synchronises, then every thread writes its outputs.
-template <int R>
-__device__ __forceinline__ void stockham_stage(double2* buf, int S, const FftStage& sg,
-                                               const double2* __restrict__ tw) {
-  constexpr int MAXB = (kFftMaxVals + R - 1) / R;
-  const int total = kFftTile * sg.nb;
-  double2 v[MAXB][R];
-  int dst[MAXB];
-#pragma unroll
-  for (int m = 0; m < MAXB; ++m) {
-    const int idx = threadIdx.x + m * kFftThreads;
-    if (idx < total) {
-      const int row = fdiv(idx, sg.inv_nb);
-      const int j = idx - row * sg.nb;
-      const int g = fdiv(j, sg.inv_ns);
-      const int k = j - g * sg.ns;
-      const double2* s = buf + row * S + j;
-#pragma unroll
-      for (int q = 0; q < R; ++q) v[m][q] = s[q * sg.nb];
-      if (sg.ns > 1) {
-#pragma unroll
-        for (int q = 1; q < R; ++q) v[m][q] = cmul(v[m][q], tw[k * q * sg.tstep]);   // k*q*tstep < L
-      }
-      if constexpr (R == 2) dft2(v[m]);
-      if constexpr (R == 3) dft3(v[m]);
-      if constexpr (R == 4) dft4(v[m]);
-      if constexpr (R == 5) dft5(v[m]);
-      dst[m] = row * S + g * sg.ns * R + k;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int m = 0; m < MAXB; ++m) {
-    if ((int)threadIdx.x + m * kFftThreads < total) {
-#pragma unroll
-      for (int q = 0; q < R; ++q) buf[dst[m] + q * sg.ns] = v[m][q];
-    }
-  }
-  __syncthreads();
+template <int P>
+__device__ __forceinline__ void dftp(double2* v) {
+  if constexpr (P == 2) dft2(v);
+  if constexpr (P == 3) dft3(v);
+  if constexpr (P == 4) dft4(v);
+  if constexpr (P == 5) dft5(v);
 }
 
-// Transforms the kFftTile rows in buf (row stride S) in place.  Caller has
-// synchronised after filling buf; returns synchronised.
-__device__ void lds_fft(double2* buf, int S, const FftLen& f) {
-  for (int s = 0; s < f.nst; ++s) {
-    switch (f.st[s].r) {
-      case 2: stockham_stage<2>(buf, S, f.st[s], f.tw); break;
-      case 3: stockham_stage<3>(buf, S, f.st[s], f.tw); break;
-      case 4: stockham_stage<4>(buf, S, f.st[s], f.tw); break;
-      case 5: stockham_stage<5>(buf, S, f.st[s], f.tw); break;
+// R = A * B, A >= B, both <= 5
+template <int R> struct RadixF;
+template <> struct RadixF<1> { static constexpr int A = 1, B = 1; };
+template <> struct RadixF<2> { static constexpr int A = 2, B = 1; };
+template <> struct RadixF<3> { static constexpr int A = 3, B = 1; };
+template <> struct RadixF<4> { static constexpr int A = 4, B = 1; };
+template <> struct RadixF<5> { static constexpr int A = 5, B = 1; };
+template <> struct RadixF<6> { static constexpr int A = 3, B = 2; };
+template <> struct RadixF<8> { static constexpr int A = 4, B = 2; };
+template <> struct RadixF<9> { static constexpr int A = 3, B = 3; };
+template <> struct RadixF<10> { static constexpr int A = 5, B = 2; };
+template <> struct RadixF<12> { static constexpr int A = 4, B = 3; };
+template <> struct RadixF<15> { static constexpr int A = 5, B = 3; };
+template <> struct RadixF<16> { static constexpr int A = 4, B = 4; };
+template <> struct RadixF<20> { static constexpr int A = 5, B = 4; };
+template <> struct RadixF<25> { static constexpr int A = 5, B = 5; };
+
+// Length-R DFT in registers, R = A*B: q = B*q1 + q2, m = m1 + A*m2,
+//   X[m1 + A m2] = sum_q2 W_B^(q2 m2) W_R^(q2 m1) sum_q1 v[B q1 + q2] W_A^(q1 m1)
+// computed in place: on return v[B*m1 + m2] holds X[m1 + A*m2] (bfly_out<R>
+// maps a register slot to its frequency).  W_R^t = tw[t * tstride] (the
+// row's W_L table, tstride = L/R; wave-uniform loads).
+template <int R>
+__host__ __device__ constexpr int bfly_out(int slot) {
+  return slot / RadixF<R>::B + RadixF<R>::A * (slot % RadixF<R>::B);
+}
+
+// inverse of bfly_out: the register slot holding frequency m
+template <int R>
+__host__ __device__ constexpr int bfly_slot(int m) {
+  return RadixF<R>::B * (m % RadixF<R>::A) + m / RadixF<R>::A;
+}
+
+template <int R>
+__device__ __forceinline__ void bfly(double2 (&v)[R], const double2* __restrict__ tw, int tstride) {
+  constexpr int A = RadixF<R>::A, B = RadixF<R>::B;
+  if constexpr (B == 1) {
+    dftp<A>(v);
+  } else {
+#pragma unroll
+    for (int q2 = 0; q2 < B; ++q2) {           // DFT_A down each column q2
+      double2 a[A];
+#pragma unroll
+      for (int q1 = 0; q1 < A; ++q1) a[q1] = v[B * q1 + q2];
+      dftp<A>(a);
+#pragma unroll
+      for (int m1 = 0; m1 < A; ++m1) v[B * m1 + q2] = q2 > 0 && m1 > 0 ? cmul(a[m1], tw[q2 * m1 * tstride]) : a[m1];
+    }
+#pragma unroll
+    for (int m1 = 0; m1 < A; ++m1) {           // DFT_B along each row m1
+      double2 c[B];
+#pragma unroll
+      for (int q2 = 0; q2 < B; ++q2) c[q2] = v[B * m1 + q2];
+      dftp<B>(c);
+#pragma unroll
+      for (int m2 = 0; m2 < B; ++m2) v[B * m1 + m2] = c[m2];
     }
   }
+}
+
+#define AMR_FFT_RADICES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(8) X(9) X(10) X(12) X(15) X(16) X(20) X(25)
+
+// A row of length L = P*Q (fft.h FftLen: P = r1, Q = r2), element c = j + Q*q:
+//   stage 1, per j < Q:  Y[j][m] = sum_q x[j + Q q] W_P^(q m)                  (m < P)
+//   stage 2, per m < P:  X[m + P p] = sum_j W_Q^(j p) (W_L^(j m) Y[j][m])        (p < Q)
+// Y lives in LDS at row t, position j + Qp*m (Qp = Q + pad, odd), so stage 1
+// writes the positions it read (in place without hazards) and stage 2 reads
+// contiguous blocks.  One butterfly per thread (8 * 25 <= kFftThreads).
+//
+// stage 1: ld(t, j, q) -> x[j + Q q];  st(t, j, m, v) stores Y[j][m].
+// ROWFAST maps lanes along a row (contiguous sources), otherwise across the 8
+// rows (column-strided sources, 8 consecutive columns = one 128-B line).
+// twl: the row's W_L table in LDS.  fill_twl: copy it from f.tw after this
+// stage's loads are issued, then a block barrier, so the two latencies overlap.
+// QC: Q as a compile-time constant (0: runtime f.r2).
+template <int P, int QC, bool ROWFAST, class Ld, class St>
+__device__ __forceinline__ void fft_stage1(const FftLen& f, double2* twl, Ld ld, St st, bool fill_twl) {
+  const int Q = QC ? QC : f.r2;
+  const int idx = threadIdx.x;
+  const bool on = idx < kFftTile * Q;
+  int t, j;
+  if (ROWFAST) {
+    t = QC ? idx / QC : fdiv(idx, f.inv_r2);
+    j = idx - t * Q;
+  } else {
+    t = idx & (kFftTile - 1);
+    j = idx / kFftTile;
+  }
+  double2 v[P];
+  if (on) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) v[q] = ld(t, j, q);
+  }
+  if (fill_twl) {
+    for (int i = threadIdx.x; i < f.L; i += kFftThreads) twl[i] = f.tw[i];
+    __syncthreads();
+  }
+  if (on) {
+    bfly<P>(v, twl, Q);
+#pragma unroll
+    for (int i = 0; i < P; ++i) st(t, j, bfly_out<P>(i), v[i]);
+  }
+}
+
+// stage 2: ld(t, j, m) -> Y[j][m];  st(t, m, p, v) stores X[m + P p].
+// Lanes run across the 8 rows so column-strided destinations coalesce.
+// POSTTW: outputs are multiplied by base * step^p, (base, step) = tw(t, m)
+// (the four-step twiddle W_n^(r (m + P p)), by recurrence: no per-output gathers).
+// sync_between: a block barrier between the loads and the stores (stores to
+// positions other threads read).
+// PC: P as a compile-time constant (0: runtime f.r1).
+template <int Q, int PC, bool POSTTW, class Ld, class Tw, class St>
+__device__ __forceinline__ void fft_stage2(const FftLen& f, const double2* twl, Ld ld, Tw tw, St st,
+                                           bool sync_between) {
+  const int P = PC ? PC : f.r1;
+  const int idx = threadIdx.x;
+  const bool on = idx < kFftTile * P;
+  const int t = idx & (kFftTile - 1), m = idx / kFftTile;
+  double2 v[Q];
+  double2 base, step;
+  if (on) {
+    if constexpr (POSTTW) tw(t, m, base, step);
+#pragma unroll
+    for (int j = 0; j < Q; ++j) v[j] = ld(t, j, m);
+#pragma unroll
+    for (int j = 1; j < Q; ++j) v[j] = cmul(v[j], twl[j * m]);   // W_L^(j m), j*m < L
+    bfly<Q>(v, twl, P);
+  }
+  if (sync_between) __syncthreads();
+  if (on) {
+    // frequencies in order p = 0..Q-1 (slot bfly_slot(p)); each value is
+    // twiddled (POSTTW: base * step^p by recurrence) right before its store
+#pragma unroll
+    for (int p = 0; p < Q; ++p) {
+      double2 x = v[bfly_slot<Q>(p)];
+      if constexpr (POSTTW) {
+        x = cmul(x, base);
+        base = cmul(base, step);
+      }
+      st(t, m, p, x);
+    }
+  }
+}
+
+struct NoTw {
+  __device__ void operator()(int, int, double2&, double2&) const {}
+};
+
+// (PC, QC) = (P, Q) of a specialised kernel, or (0, 0): radices from f at run time.
+template <bool ROWFAST, int PC, int QC, class Ld, class St>
+__device__ __forceinline__ void run_stage1(const FftLen& f, double2* twl, Ld ld, St st, bool fill_twl = false) {
+  if constexpr (PC > 0) {
+    fft_stage1<PC, QC, ROWFAST>(f, twl, ld, st, fill_twl);
+  } else {
+    switch (f.r1) {
+#define AMR_S1(R) \
+  case R: fft_stage1<R, 0, ROWFAST>(f, twl, ld, st, fill_twl); break;
+      AMR_FFT_RADICES(AMR_S1)
+#undef AMR_S1
+    }
+  }
+}
+
+template <bool POSTTW, int PC, int QC, class Ld, class St, class Tw = NoTw>
+__device__ __forceinline__ void run_stage2(const FftLen& f, const double2* twl, Ld ld, St st,
+                                           bool sync_between = false, Tw tw = Tw()) {
+  if constexpr (QC > 0) {
+    fft_stage2<QC, PC, POSTTW>(f, twl, ld, tw, st, sync_between);
+  } else {
+    switch (f.r2) {
+#define AMR_S2(R) \
+  case R: fft_stage2<R, 0, POSTTW>(f, twl, ld, tw, st, sync_between); break;
+      AMR_FFT_RADICES(AMR_S2)
+#undef AMR_S2
+    }
+  }
+}
+
+// Logical block of a grid whose size is a multiple of 8: consecutive logical
+// blocks (neighbouring tiles of one stream, whose column-strided 128-B
+// segments share HBM lines) land on the same XCD and L2 (workgroups are
+// dealt to the 8 XCDs round robin; a placement assumption for speed only).
+__device__ __forceinline__ int64_t xcd_block() {
+  return (int64_t)(blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+}
+static inline unsigned grid8(int64_t blocks) { return (unsigned)((blocks + 7) & ~(int64_t)7); }
+
+// LDS home of the row's W_L table (after the kFftTile rows)
+__device__ __forceinline__ double2* twl_of(double2* smem, const FftLen& f) { return smem + kFftTile * f.S; }
+
+// W_n^a = W_n^(256 hi) * W_n^lo  (a < n < 2^31)
+__device__ __forceinline__ double2 twn(const FftDesc& d, unsigned a) {
+  return cmul(d.tw_hi[a >> 8], d.tw_lo[a & 255]);
 }
 
 // -i*sgn(k) * v for a length-n transform (scipy.signal.hilbert's h, minus the identity)
-__device__ __forceinline__ double2 hilbert_mul(double2 v, int64_t k, int64_t n) {
+__device__ __forceinline__ double2 hilbert_mul(double2 v, int64_t k, int64_t n) {   // k < n < 2^31
   const int64_t k2 = 2 * k;
   return (k == 0 || k2 == n) ? make_double2(0.0, 0.0) : (k2 < n ? mul_mi(v) : make_double2(-v.y, v.x));
+}
+
+// |a_mark| > |a_space| with a = f + i X (np.abs = hypot): compared as squares,
+// exact up to the last ulp of the envelopes; hypot where squares could overflow
+__device__ __forceinline__ bool env_gt(double2 f, double2 v) {
+  const double big = fmax(fmax(fabs(f.x), fabs(v.x)), fmax(fabs(f.y), fabs(v.y)));
+  if (big < 1e150) return __builtin_fma(f.x, f.x, v.x * v.x) > __builtin_fma(f.y, f.y, v.y * v.y);
+  return hypot(f.x, v.x) > hypot(f.y, v.y);
 }
 
 template <int MODE>
@@ -145,11 +301,6 @@ __device__ __forceinline__ void fft_epilogue(const FftEpi& e, double2* __restric
   const size_t o = (size_t)b * e.n + k;
   switch (MODE) {
     case kHilbert: dst[o] = hilbert_mul(v, k, e.n); break;
-    case kEnvelope: {
-      const double2 f = e.z[o];
-      e.cmp[o] = hypot(f.x, v.x) > hypot(f.y, v.y) ? 1 : 0;
-      break;
-    }
     case kEnvOut: {
       const double2 f = e.z[o];
       dst[o] = make_double2(hypot(f.x, v.x), hypot(f.y, v.y));
@@ -160,107 +311,144 @@ __device__ __forceinline__ void fft_epilogue(const FftEpi& e, double2* __restric
   }
 }
 
-// Loads rows r0 .. r0+7 (each L contiguous values at src[r*L]) into buf.
-__device__ __forceinline__ void load_rows(double2* buf, int S, const double2* __restrict__ src, int r0, int nrow,
-                                          const FftLen& f, bool conj_in) {
-  const int L = f.L;
-  const int rows = min(kFftTile, nrow - r0);
-  const double2* s = src + (size_t)r0 * L;
-  for (int e = threadIdx.x; e < kFftTile * L; e += kFftThreads) {
-    const int row = fdiv(e, f.inv_L);
-    const int c = e - row * L;
-    const double2 v = row < rows ? s[e] : make_double2(0.0, 0.0);
-    buf[row * S + c] = conj_in ? conj2(v) : v;
-  }
-  __syncthreads();
-}
-
 // ---- column pass: in[b][j1 + n1*j2] -> T[b][k2*n1 + j1] = W_n^(j1 k2) * DFT_n2 ----
-template <bool CONJ_IN>
+template <bool CONJ_IN, int PC, int QC>
 __global__ __launch_bounds__(kFftThreads) void k_fft_cols(const double2* __restrict__ in, double2* __restrict__ out,
                                                          FftDesc d, int64_t batch) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n1 + kFftTile - 1) / kFftTile;
-  const int64_t b = blockIdx.x / tiles;
-  const int j1_0 = (int)(blockIdx.x - b * tiles) * kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int j1_0 = (int)(lb - b * tiles) * kFftTile;
   if (b >= batch) return;
-  const int L = d.n2, S = L + 1;
-  const double2* src = in + (size_t)b * d.n;
-  for (int idx = threadIdx.x; idx < kFftTile * L; idx += kFftThreads) {
-    const int t = idx & (kFftTile - 1), j2 = idx / kFftTile;
-    const int j1 = j1_0 + t;
-    const double2 v = j1 < d.n1 ? src[(size_t)j1 + (size_t)d.n1 * j2] : make_double2(0.0, 0.0);
-    smem[t * S + j2] = CONJ_IN ? conj2(v) : v;
-  }
+  const FftLen& f = d.a;
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
+  const int n1 = d.n1;
+  const double2* __restrict__ src = in + (size_t)b * d.n + j1_0;
+  double2* __restrict__ dst = out + (size_t)b * d.n + j1_0;
+  const int ncol = min(kFftTile, d.n1 - j1_0);
+  double2* twl = twl_of(smem, f);
+  run_stage1<false, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) {
+        const double2 v = t < ncol ? src[(unsigned)(t + n1 * (j + Q * q))] : make_double2(0.0, 0.0);
+        return CONJ_IN ? conj2(v) : v;
+      },
+      [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; }, true);
   __syncthreads();
-  lds_fft(smem, S, d.a);
-  double2* dst = out + (size_t)b * d.n;
-  for (int idx = threadIdx.x; idx < kFftTile * L; idx += kFftThreads) {
-    const int t = idx & (kFftTile - 1), k2 = idx / kFftTile;
-    const int j1 = j1_0 + t;
-    if (j1 < d.n1) dst[(size_t)k2 * d.n1 + j1] = cmul(smem[t * S + k2], d.twn[(int64_t)j1 * k2]);
-  }
+  run_stage2<true, PC, QC>(
+      f, twl, [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; },
+      [&](int t, int m, int p, double2 v) {
+        if (t < ncol) dst[(unsigned)(t + n1 * (m + P * p))] = v;
+      },
+      false,
+      [&](int t, int m, double2& base, double2& step) {   // W_n^(j1 (m + P p))
+        base = twn(d, (unsigned)((j1_0 + t) * m));
+        step = twn(d, (unsigned)((j1_0 + t) * P));
+      });
 }
 
 // ---- middle pass of a filter: rows k2 of T (length n1) -> X[k2 + n2*k1] ->
 // Y = mid(X) -> conj -> DFT_n1 over k1 -> k2', times W_n^(k2 k2') ->
 // T'[k2'*n2 + k2]  (the column pass of FFT(conj Y) with n = n2 * n1) --------
-template <int MID>
+template <int MID, int PC, int QC>
 __global__ __launch_bounds__(kFftThreads) void k_fft_mid(const double2* __restrict__ in, double2* __restrict__ out,
                                                         FftDesc d, int64_t batch, const double2* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
-  const int64_t b = blockIdx.x / tiles;
-  const int r0 = (int)(blockIdx.x - b * tiles) * kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int r0 = (int)(lb - b * tiles) * kFftTile;
   if (b >= batch) return;
-  const int L = d.n1, S = L + 1;
-  load_rows(smem, S, in + (size_t)b * d.n, r0, d.n2, d.c, false);
-  lds_fft(smem, S, d.c);
+  const FftLen& f = d.c;
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2, L = P * Q;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
   const int64_t n = d.n;
-  for (int e = threadIdx.x; e < kFftTile * L; e += kFftThreads) {
-    const int row = fdiv(e, d.c.inv_L);
-    const int k1 = e - row * L;
-    const int64_t k = (int64_t)(r0 + row) + (int64_t)d.n2 * k1;
-    double2 v = smem[row * S + k1];
-    if (MID == kHilbert)
-      v = hilbert_mul(v, k, n);
-    else
-      v = r0 + row < d.n2 ? cmul(v, tab[k]) : make_double2(0.0, 0.0);
-    smem[row * S + k1] = conj2(v);
-  }
+  const int n2 = d.n2;
+  const int nrow = min(kFftTile, d.n2 - r0);
+  const double2* __restrict__ src = in + (size_t)b * n + (size_t)r0 * L;
+  double2* __restrict__ dst = out + (size_t)b * n + r0;
+  auto y_ld = [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; };
+  auto y_st = [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; };
+  double2* twl = twl_of(smem, f);
+  // forward row DFT; its outputs X[k1], k1 = m + P p, stay in registers ...
+  run_stage1<true, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) { return t < nrow ? src[(unsigned)(t * L + j + Q * q)] : make_double2(0.0, 0.0); },
+      y_st, true);
   __syncthreads();
-  lds_fft(smem, S, d.c);
-  double2* dst = out + (size_t)b * n;
-  for (int idx = threadIdx.x; idx < kFftTile * L; idx += kFftThreads) {
-    const int t = idx & (kFftTile - 1), k2p = idx / kFftTile;
-    const int r = r0 + t;
-    if (r < d.n2) dst[(size_t)k2p * d.n2 + r] = cmul(smem[t * S + k2p], d.twn[(int64_t)r * k2p]);
-  }
+  // ... and go back to LDS in natural order (element c = k1 at j = c % Q,
+  // q = c / Q) once every thread has read its stage-2 inputs
+  run_stage2<false, PC, QC>(
+      f, twl, y_ld,
+      [&](int t, int m, int p, double2 v) {
+        const int c = m + P * p;
+        const unsigned k = (unsigned)(r0 + t + n2 * c);
+        if (MID == kHilbert)
+          v = hilbert_mul(v, k, n);
+        else
+          v = t < nrow ? cmul(v, tab[k]) : make_double2(0.0, 0.0);
+        const int qq = QC ? c / QC : fdiv(c, f.inv_r2);
+        smem[t * S + (c - Q * qq) + Qp * qq] = conj2(v);
+      },
+      true);
+  __syncthreads();
+  // forward row DFT of conj(Y) (stage 1 in place), then the twiddle to T'
+  run_stage1<false, PC, QC>(f, twl, y_ld, y_st);
+  __syncthreads();
+  run_stage2<true, PC, QC>(
+      f, twl, y_ld,
+      [&](int t, int m, int p, double2 v) {
+        if (t < nrow) dst[(unsigned)(t + n2 * (m + P * p))] = v;
+      },
+      false,
+      [&](int t, int m, double2& base, double2& step) {   // W_n^(k2 (m + P p))
+        base = twn(d, (unsigned)((r0 + t) * m));
+        step = twn(d, (unsigned)((r0 + t) * P));
+      });
 }
 
 // ---- row pass: rows r of in (length f.L, nrow rows) -> DFT -> out index
 // r + nrow*k; CONJ_OUT conjugates and scales (inverse); then the epilogue --
-template <bool CONJ_OUT, int MODE>
+template <bool CONJ_OUT, int MODE, int PC, int QC>
 __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restrict__ in, double2* __restrict__ out,
-                                                         FftLen f, int nrow, int64_t n, int64_t batch, double scale,
-                                                         FftEpi e) {
+                                                         FftLen f, int nrow_all, int64_t n, int64_t batch,
+                                                         double scale, FftEpi e) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
-  const int tiles = (nrow + kFftTile - 1) / kFftTile;
-  const int64_t b = blockIdx.x / tiles;
-  const int r0 = (int)(blockIdx.x - b * tiles) * kFftTile;
+  const int tiles = (nrow_all + kFftTile - 1) / kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int r0 = (int)(lb - b * tiles) * kFftTile;
   if (b >= batch) return;
-  const int L = f.L, S = L + 1;
-  load_rows(smem, S, in + (size_t)b * n, r0, nrow, f, false);
-  lds_fft(smem, S, f);
-  for (int idx = threadIdx.x; idx < kFftTile * L; idx += kFftThreads) {
-    const int t = idx & (kFftTile - 1), k = idx / kFftTile;
-    const int r = r0 + t;
-    if (r < nrow) {
-      double2 v = smem[t * S + k];
-      if (CONJ_OUT) v = make_double2(v.x * scale, -v.y * scale);
-      fft_epilogue<MODE>(e, out, b, (int64_t)r + (int64_t)nrow * k, v);
-    }
-  }
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2, L = P * Q;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
+  const int nrow = min(kFftTile, nrow_all - r0);
+  const double2* __restrict__ src = in + (size_t)b * n + (size_t)r0 * L;
+  double2* twl = twl_of(smem, f);
+  run_stage1<true, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) { return t < nrow ? src[(unsigned)(t * L + j + Q * q)] : make_double2(0.0, 0.0); },
+      [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; }, true);
+  __syncthreads();
+  run_stage2<false, PC, QC>(
+      f, twl, [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; },
+      [&](int t, int m, int p, double2 v) {
+        const int kk = m + P * p;
+        if constexpr (MODE == kEnvelope) {
+          // 8 lanes (t = 0..7) of one kk -> one byte of compare bits
+          bool gt = false;
+          if (t < nrow) {
+            v = make_double2(v.x * scale, -v.y * scale);
+            gt = env_gt(e.z[(size_t)b * n + (unsigned)(r0 + t + nrow_all * kk)], v);
+          }
+          const uint64_t mask = __ballot(gt);
+          if (t == 0) e.bits[(size_t)b * e.bits_stride + (size_t)(r0 >> 3) * L + kk] = (uint8_t)(mask >> (threadIdx.x & 56));
+        } else if (t < nrow) {
+          if (CONJ_OUT) v = make_double2(v.x * scale, -v.y * scale);
+          fft_epilogue<MODE>(e, out, b, (unsigned)(r0 + t + nrow_all * kk), v);
+        }
+      });
 }
 
 // Bluestein (n not 5-smooth): X_k = conj(w_k) * sum_j (x_j conj(w_j)) w_(k-j),
@@ -295,63 +483,119 @@ __global__ __launch_bounds__(256) void k_bs_post(const double2* __restrict__ y, 
   fft_epilogue<MODE>(e, out, b, k, v);
 }
 
-static size_t fft_smem_bytes(int L) { return (size_t)kFftTile * (L + 1) * sizeof(double2); }
+// Bluestein post + envelope compare, plain bit order: thread = (stream, byte)
+__global__ __launch_bounds__(256) void k_bs_post_env(const double2* __restrict__ y, const double2* __restrict__ w,
+                                                     int64_t n, int64_t M, int64_t batch, double scale, FftEpi e) {
+  const int64_t nbytes = (n + 7) >> 3;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= batch * nbytes) return;
+  const int64_t b = i / nbytes, jb = i - b * nbytes;
+  unsigned byte = 0;
+  for (int u = 0; u < 8; ++u) {
+    const int64_t k = jb * 8 + u;
+    if (k >= n) break;
+    double2 v = cmul(y[(size_t)b * M + k], conj2(w[k]));
+    v = make_double2(v.x * scale, -v.y * scale);
+    byte |= (env_gt(e.z[(size_t)b * n + k], v) ? 1u : 0u) << u;
+  }
+  e.bits[(size_t)b * e.bits_stride + jb] = (uint8_t)byte;
+}
+
+static size_t fft_smem_bytes(const FftLen& f) { return ((size_t)kFftTile * f.S + f.L) * sizeof(double2); }
+
+// Specialised (P, Q) instantiations (compile-time radices: immediate LDS and
+// HBM offsets, fewer live registers) for the lengths of the benchmark
+// streams (96000 = 300 * 320, 300 = 20 * 15, 320 = 20 * 16); everything else
+// runs the generic kernels (radices switched at run time).
+#define AMR_FFT_PQ(f, CALL)                      \
+  do {                                           \
+    if ((f).r1 == 20 && (f).r2 == 16) {          \
+      CALL(20, 16);                              \
+    } else if ((f).r1 == 20 && (f).r2 == 15) {   \
+      CALL(20, 15);                              \
+    } else {                                     \
+      CALL(0, 0);                                \
+    }                                            \
+  } while (0)
 
 hipError_t launch_fft(const double2* in, double2* tmp, double2* out, const FftDesc& d, int64_t batch, bool inverse,
                       hipStream_t st) {
-  const unsigned gcol = (unsigned)(batch * ((d.n1 + kFftTile - 1) / kFftTile));
-  const unsigned grow = (unsigned)(batch * ((d.n2 + kFftTile - 1) / kFftTile));
+  const unsigned gcol = grid8(batch * ((d.n1 + kFftTile - 1) / kFftTile));
+  const unsigned grow = grid8(batch * ((d.n2 + kFftTile - 1) / kFftTile));
   FftEpi e{};
   e.mode = kStore;
   e.n = d.n;
+  const double scale = inverse ? 1.0 / (double)d.n : 1.0;
+#define COLS(P, Q)                                                                                               \
+  hipLaunchKernelGGL((k_fft_cols<true, P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, in, tmp, d, \
+                     batch)
+#define COLSF(P, Q)                                                                                               \
+  hipLaunchKernelGGL((k_fft_cols<false, P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, in, tmp, d, \
+                     batch)
+#define ROWS(P, Q)                                                                                            \
+  hipLaunchKernelGGL((k_fft_rows<true, kStore, P, Q>), dim3(grow), dim3(kFftThreads), fft_smem_bytes(d.c), st, \
+                     tmp, out, d.c, d.n2, d.n, batch, scale, e)
+#define ROWSF(P, Q)                                                                                            \
+  hipLaunchKernelGGL((k_fft_rows<false, kStore, P, Q>), dim3(grow), dim3(kFftThreads), fft_smem_bytes(d.c), st, \
+                     tmp, out, d.c, d.n2, d.n, batch, scale, e)
   if (inverse) {
-    hipLaunchKernelGGL(k_fft_cols<true>, dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.n2), st, in, tmp, d, batch);
-    hipLaunchKernelGGL((k_fft_rows<true, kStore>), dim3(grow), dim3(kFftThreads), fft_smem_bytes(d.n1), st,
-                       tmp, out, d.c, d.n2, d.n, batch, 1.0 / (double)d.n, e);
+    AMR_FFT_PQ(d.a, COLS);
+    AMR_FFT_PQ(d.c, ROWS);
   } else {
-    hipLaunchKernelGGL(k_fft_cols<false>, dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.n2), st, in, tmp, d, batch);
-    hipLaunchKernelGGL((k_fft_rows<false, kStore>), dim3(grow), dim3(kFftThreads), fft_smem_bytes(d.n1), st,
-                       tmp, out, d.c, d.n2, d.n, batch, 1.0, e);
+    AMR_FFT_PQ(d.a, COLSF);
+    AMR_FFT_PQ(d.c, ROWSF);
   }
+#undef COLS
+#undef COLSF
+#undef ROWS
+#undef ROWSF
   return hipGetLastError();
 }
 
 hipError_t launch_fft_filter(const double2* in, double2* t1, double2* t2, double2* out, const FftDesc& d,
                              int64_t batch, int mid, const double2* tab, const FftEpi& epi, hipStream_t st) {
-  const unsigned gcol = (unsigned)(batch * ((d.n1 + kFftTile - 1) / kFftTile));
-  const unsigned gmid = (unsigned)(batch * ((d.n2 + kFftTile - 1) / kFftTile));
-  hipLaunchKernelGGL(k_fft_cols<false>, dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.n2), st, in, t1, d, batch);
-  if (mid == kHilbert)
-    hipLaunchKernelGGL(k_fft_mid<kHilbert>, dim3(gmid), dim3(kFftThreads), fft_smem_bytes(d.n1), st, t1, t2, d,
-                       batch, tab);
-  else if (mid == kMulTab)
-    hipLaunchKernelGGL(k_fft_mid<kMulTab>, dim3(gmid), dim3(kFftThreads), fft_smem_bytes(d.n1), st, t1, t2, d,
-                       batch, tab);
-  else
-    return hipErrorInvalidValue;
+  const unsigned gcol = grid8(batch * ((d.n1 + kFftTile - 1) / kFftTile));
+  const unsigned gmid = grid8(batch * ((d.n2 + kFftTile - 1) / kFftTile));
+  const unsigned gfin = grid8(batch * ((d.n1 + kFftTile - 1) / kFftTile));
+  if (mid != kHilbert && mid != kMulTab) return hipErrorInvalidValue;
+  if (epi.mode != kStore && epi.mode != kEnvelope && epi.mode != kEnvOut) return hipErrorInvalidValue;
+#define COLSF(P, Q)                                                                                              \
+  hipLaunchKernelGGL((k_fft_cols<false, P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, in, t1, d, \
+                     batch)
+  AMR_FFT_PQ(d.a, COLSF);
+#undef COLSF
+#define MIDK(P, Q)                                                                                                  \
+  do {                                                                                                              \
+    if (mid == kHilbert)                                                                                            \
+      hipLaunchKernelGGL((k_fft_mid<kHilbert, P, Q>), dim3(gmid), dim3(kFftThreads), fft_smem_bytes(d.c), st, t1, \
+                         t2, d, batch, tab);                                                                        \
+    else                                                                                                            \
+      hipLaunchKernelGGL((k_fft_mid<kMulTab, P, Q>), dim3(gmid), dim3(kFftThreads), fft_smem_bytes(d.c), st, t1,  \
+                         t2, d, batch, tab);                                                                        \
+  } while (0)
+  AMR_FFT_PQ(d.c, MIDK);
+#undef MIDK
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   // final row pass: the n1 rows k2' of T' (length n2) -> index k2' + n1*k1', conj, 1/n
   FftEpi e = epi;
   e.n = d.n;
-  const unsigned gfin = (unsigned)(batch * ((d.n1 + kFftTile - 1) / kFftTile));
   const double scale = 1.0 / (double)d.n;
-  const size_t sm = fft_smem_bytes(d.n2);
-  switch (epi.mode) {
-    case kStore:
-      hipLaunchKernelGGL((k_fft_rows<true, kStore>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out, d.a,
-                         d.n1, d.n, batch, scale, e);
-      break;
-    case kEnvelope:
-      hipLaunchKernelGGL((k_fft_rows<true, kEnvelope>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out, d.a,
-                         d.n1, d.n, batch, scale, e);
-      break;
-    case kEnvOut:
-      hipLaunchKernelGGL((k_fft_rows<true, kEnvOut>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out, d.a,
-                         d.n1, d.n, batch, scale, e);
-      break;
-    default: return hipErrorInvalidValue;
-  }
+  const size_t sm = fft_smem_bytes(d.a);
+#define FIN(P, Q)                                                                                                  \
+  do {                                                                                                             \
+    if (epi.mode == kStore)                                                                                        \
+      hipLaunchKernelGGL((k_fft_rows<true, kStore, P, Q>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out, d.a,  \
+                         d.n1, d.n, batch, scale, e);                                                              \
+    else if (epi.mode == kEnvelope)                                                                                \
+      hipLaunchKernelGGL((k_fft_rows<true, kEnvelope, P, Q>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out,    \
+                         d.a, d.n1, d.n, batch, scale, e);                                                         \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_fft_rows<true, kEnvOut, P, Q>), dim3(gfin), dim3(kFftThreads), sm, st, t2, out, d.a, \
+                         d.n1, d.n, batch, scale, e);                                                              \
+  } while (0)
+  AMR_FFT_PQ(d.a, FIN);
+#undef FIN
   return hipGetLastError();
 }
 
@@ -372,25 +616,39 @@ hipError_t launch_bs_post(const double2* y, double2* out, const double2* w, int6
   switch (epi.mode) {
     case kStore: hipLaunchKernelGGL(k_bs_post<kStore>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
     case kHilbert: hipLaunchKernelGGL(k_bs_post<kHilbert>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
-    case kEnvelope: hipLaunchKernelGGL(k_bs_post<kEnvelope>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
+    case kEnvelope: {
+      if (!inverse) return hipErrorInvalidValue;
+      const int64_t tb = batch * ((n + 7) >> 3);
+      hipLaunchKernelGGL(k_bs_post_env, dim3((unsigned)((tb + 255) / 256)), dim3(256), 0, st, y, w, n, M, batch,
+                         scale, epi);
+      break;
+    }
     case kEnvOut: hipLaunchKernelGGL(k_bs_post<kEnvOut>, g, dim3(256), 0, st, y, out, w, n, M, batch, inv, scale, epi); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-hipError_t fft_configure_smem() {
-  const int bytes = (int)fft_smem_bytes(kFftMaxL);
+template <int P, int Q>
+static hipError_t fft_set_smem(int bytes) {
   const void* fns[] = {
-      (const void*)k_fft_cols<false>, (const void*)k_fft_cols<true>, (const void*)k_fft_mid<kHilbert>,
-      (const void*)k_fft_mid<kMulTab>, (const void*)k_fft_rows<false, kStore>,
-      (const void*)k_fft_rows<true, kStore>, (const void*)k_fft_rows<true, kEnvelope>,
-      (const void*)k_fft_rows<true, kEnvOut>};
+      (const void*)k_fft_cols<false, P, Q>, (const void*)k_fft_cols<true, P, Q>,
+      (const void*)k_fft_mid<kHilbert, P, Q>, (const void*)k_fft_mid<kMulTab, P, Q>,
+      (const void*)k_fft_rows<false, kStore, P, Q>, (const void*)k_fft_rows<true, kStore, P, Q>,
+      (const void*)k_fft_rows<true, kEnvelope, P, Q>, (const void*)k_fft_rows<true, kEnvOut, P, Q>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t fft_configure_smem() {
+  const int bytes = (kFftTile * fft_row_stride(kFftMaxR, kFftMaxR) + kFftMaxL) * (int)sizeof(double2);
+  hipError_t e = fft_set_smem<0, 0>(bytes);
+  if (e == hipSuccess) e = fft_set_smem<20, 16>(bytes);
+  if (e == hipSuccess) e = fft_set_smem<20, 15>(bytes);
+  return e;
 }
 
 }  // namespace amr

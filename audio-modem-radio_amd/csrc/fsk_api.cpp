@@ -4,8 +4,8 @@
 // Pipeline per call (all on the plan's stream):
 //   F1  k_fsk_bandpass          x -> z = f_mark + i f_space           [B][n] c128
 //   F2  H[z] = IFFT_n(-i sgn(k) FFT_n(z)) in three passes z -> u -> v -> cmp,
-//       the last forming both envelopes: cmp = |a_mark| > |a_space|   [B][n] u8
-//   F3  k_fsk_decide + k_sync_pack  cmp -> words -> bytes
+//       the last forming both envelopes: bit = |a_mark| > |a_space|   [B][n/8] u8
+//   F3  k_fsk_decide + k_sync_pack  cmp bits -> words -> bytes
 // A length that is not 5-smooth runs each FFT_n as a Bluestein convolution of
 // length M (u, v then hold M-long rows).
 #include <hip/hip_runtime.h>
@@ -58,24 +58,27 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
   HIP_TRY(smem_err);
   f.n = n;
   int n1 = 0, n2 = 0;
-  if (smooth5(n) && fft_split(n, n1, n2)) {
+  if (fft_split(n, n1, n2)) {
     f.M = n;
   } else {
     f.bluestein = true;
     f.M = fft_good_size(2 * n - 1);
-    if (!fft_split(f.M, n1, n2)) return fail(AMR_E_INVALID, "FFT length too large");
+    if (f.M < 0 || !fft_split(f.M, n1, n2))
+      return fail(AMR_E_INVALID, "FFT length " + std::to_string(n) + " exceeds the two-pass limit (Bluestein "
+                                 "length <= " + std::to_string((int64_t)kFftMaxL * kFftMaxL) + ")");
   }
-  if (f.M > (int64_t)kFftMaxL * kFftMaxL)
-    return fail(AMR_E_INVALID, "FFT length " + std::to_string(n) + " exceeds the two-pass limit " +
-                                   std::to_string((int64_t)kFftMaxL * kFftMaxL));
   const int64_t M = f.M;
-  const int64_t ntab = n2 + n1 + M + (f.bluestein ? n + M : 0);
+  const int64_t nhi = (M + 255) / 256;
+  // [tw n2][tw n1][W_M^t, t < 256][W_M^(256 t), t < nhi][chirp n][bhat M]
+  const int64_t ntab = n2 + n1 + 256 + nhi + (f.bluestein ? n + M : 0);
   std::vector<double> host;
   host.reserve((size_t)(2 * ntab));
-  for (int64_t L : {(int64_t)n2, (int64_t)n1, M}) {
-    const std::vector<double> w = twiddles(L);
-    host.insert(host.end(), w.begin(), w.end());
-  }
+  auto put = [&](const std::vector<double>& w) { host.insert(host.end(), w.begin(), w.end()); };
+  put(twiddles(n2, n2));
+  put(twiddles(n1, n1));
+  put(twiddles(M, 256));
+  put(twiddles(M, nhi, 256));
+  const int64_t off_chirp = n2 + n1 + 256 + nhi;
   std::vector<double> bw;
   if (f.bluestein) {
     // chirp w_j = exp(i pi j^2 / n); j^2 reduced mod 2n keeps the angle exact
@@ -87,7 +90,7 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
     }
     // convolution kernel bw[m] = w_m, bw[M-m] = w_m (0 < m < n), zero elsewhere
     bw.assign((size_t)(2 * M), 0.0);
-    const double* w = host.data() + 2 * (n2 + n1 + M);
+    const double* w = host.data() + 2 * off_chirp;
     for (int64_t m = 0; m < n; ++m) {
       bw[2 * m] = w[2 * m];
       bw[2 * m + 1] = w[2 * m + 1];
@@ -99,7 +102,7 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
     host.resize((size_t)(2 * ntab), 0.0);
   }
   HIP_TRY(hipMalloc(&f.tables, (size_t)ntab * sizeof(double2)));
-  HIP_TRY(hipMemcpy(f.tables, host.data(), (size_t)(2 * (n2 + n1 + M + (f.bluestein ? n : 0))) * 8,
+  HIP_TRY(hipMemcpy(f.tables, host.data(), (size_t)(2 * (off_chirp + (f.bluestein ? n : 0))) * 8,
                     hipMemcpyHostToDevice));
   const double2* t = f.tables;
   f.d.n = M;
@@ -107,10 +110,11 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
   f.d.n2 = n2;
   if (!fill_fft_len(f.d.a, n2, t) || !fill_fft_len(f.d.c, n1, t + n2))
     return fail(AMR_E_INVALID, "FFT factor plan failed for n=" + std::to_string(n));
-  f.d.twn = t + n2 + n1;
+  f.d.tw_lo = t + n2 + n1;
+  f.d.tw_hi = t + n2 + n1 + 256;
   if (f.bluestein) {
-    f.chirp = t + n2 + n1 + M;
-    double2* bh = f.tables + n2 + n1 + M + n;
+    f.chirp = t + off_chirp;
+    double2* bh = f.tables + off_chirp + n;
     f.bhat = bh;
     double2 *a = nullptr, *tmp = nullptr;
     HIP_TRY(hipMalloc(&a, (size_t)M * sizeof(double2)));
@@ -179,7 +183,7 @@ struct amr_fsk_plan {
   double2* z = nullptr;        // [B][n]
   double2* u = nullptr;        // [B][max(M, n + 2 pad)]  (also F1's forward scratch)
   double2* v = nullptr;        // [B][M]
-  uint8_t* cmp = nullptr;      // [B][n]
+  uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
   int64_t scratch_bytes = 0;
   // staging for the host API
@@ -224,7 +228,8 @@ int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   FftEpi env{};
   env.mode = env_out ? kEnvOut : kEnvelope;
   env.z = pl->z;
-  env.cmp = pl->cmp;
+  env.bits = pl->cmp;
+  env.bits_stride = pl->p.bits_stride;
   // one timing slot for the whole Hilbert filter (column, middle and final row passes)
   HIP_TRY(mark(AMR_TF_HILBERT, 0));
   HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, st));
@@ -319,6 +324,10 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     return rc;
   }
   const int64_t M = pl->fft.M;
+  p.rn1 = pl->fft.bluestein ? n : pl->fft.d.n1;
+  p.rn2 = pl->fft.bluestein ? 1 : pl->fft.d.n2;
+  p.bits_stride = fft_bits_stride(p.rn1, p.rn2);
+  p.inv_rn1 = 1.0f / (float)p.rn1;
   const int64_t waves = (max_streams + 31) / 32;
   const int64_t s1_bytes = waves * ((n + 2 * p.pad + 2) / 2) * 64 * 16;
   struct A { void** ptr; int64_t bytes; };
@@ -326,7 +335,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       {(void**)&pl->z, max_streams * n * 16},
       {(void**)&pl->u, std::max(max_streams * M * 16, s1_bytes)},
       {(void**)&pl->v, max_streams * M * 16},
-      {(void**)&pl->cmp, max_streams * n},
+      {(void**)&pl->cmp, max_streams * p.bits_stride},
       {(void**)&pl->words, max_streams * p.n_words * 4},
   };
   for (const A& a : allocs) {

@@ -19,7 +19,7 @@
 //   F2 (fft_kernels.hip) H[z] = IFFT(-i sgn(k) FFT(z)) = H[f_mark] + i H[f_space]
 //                      (the Hilbert transform is real-linear, so one complex
 //                      transform pair serves both tones); its last pass forms
-//                      both envelopes hypot(f, H f) and writes the compare byte.
+//                      both envelopes hypot(f, H f) and packs the compare bits.
 //   F3 k_fsk_decide    thread = (stream, bit): window majority, ballot-packed
 //                      MSB first into words (then k_sync_pack, util_kernels.hip)
 // Parity: the FFT cannot reproduce pocketfft's rounding; envelopes agree to
@@ -218,21 +218,31 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 }
 
 // F3.  thread = (stream, bit): bit b of the stream is 1 when more than half of
-// cmp[i-q, min(i+q, n)) are 1, i = sps/2 + b*sps  (np.mean(chunk) > 0.5,
-// modem.py:320-323).  A wave covers 64 consecutive bits (64*sps contiguous
-// bytes); a ballot packs them MSB first into two words.
-__global__ __launch_bounds__(64) void k_fsk_decide(const uint8_t* __restrict__ cmp, uint32_t* __restrict__ words,
+// the compare bits of samples [i-q, min(i+q, n)) are 1, i = sps/2 + b*sps
+// (np.mean(chunk) > 0.5, modem.py:320-323).  Compare bits are in the final
+// row pass's tile order (fft.h fft_bits_stride).  A wave covers 64
+// consecutive bits; a ballot packs them MSB first into two words.
+__global__ __launch_bounds__(64) void k_fsk_decide(const uint8_t* __restrict__ bits, uint32_t* __restrict__ words,
                                                    int64_t n_streams, FskParams p) {
   const int64_t s = blockIdx.y;
   const int64_t bi = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const uint8_t* __restrict__ c = cmp + (size_t)s * p.n;
+  const uint8_t* __restrict__ c = bits + (size_t)s * p.bits_stride;
   const int64_t q = p.sps / 4, half = p.sps / 2;
   bool bit = false;
   if (bi < p.n_bits) {
     const int64_t i = half + bi * p.sps;
     const int64_t lo = i - q, hi = (i + q < p.n) ? i + q : p.n;
+    // sample lo = r + rn1*kk
+    int64_t kk = (int64_t)(((float)lo + 0.5f) * p.inv_rn1);
+    int64_t r = lo - kk * p.rn1;
     int64_t ones = 0;
-    for (int64_t k = lo; k < hi; ++k) ones += c[k];
+    for (int64_t k = lo; k < hi; ++k) {
+      ones += (c[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
+      if (++r == p.rn1) {
+        r = 0;
+        ++kk;
+      }
+    }
     bit = 2 * ones > hi - lo;
   }
   const uint64_t mask = __ballot(bit);
