@@ -26,6 +26,7 @@ namespace amr {
 hipError_t launch_fsk_bandpass(int, const void*, int64_t, int64_t, double*, double2*, const FskParams&,
                                const FskIir&, hipStream_t);
 hipError_t launch_fsk_decide(const uint8_t*, uint32_t*, int64_t, const FskParams&, hipStream_t);
+int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
                             hipStream_t);
 }  // namespace amr
@@ -181,7 +182,7 @@ struct amr_fsk_plan {
   int64_t out_cap = 0;
   // HBM scratch
   double2* z = nullptr;        // [B][n]
-  double2* u = nullptr;        // [B][max(M, n + 2 pad)]  (also F1's forward scratch)
+  double2* u = nullptr;        // [B][M]  (also F1's checkpoint scratch)
   double2* v = nullptr;        // [B][M]
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
@@ -328,8 +329,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   p.rn2 = pl->fft.bluestein ? 1 : pl->fft.d.n2;
   p.bits_stride = fft_bits_stride(p.rn1, p.rn2);
   p.inv_rn1 = 1.0f / (float)p.rn1;
-  const int64_t waves = (max_streams + 31) / 32;
-  const int64_t s1_bytes = waves * ((n + 2 * p.pad + 2) / 2) * 64 * 16;
+  const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, max_streams * n * 16},

@@ -59,30 +59,37 @@ __device__ __forceinline__ double fsk_step(double (&z)[6], const double (&b)[7],
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector (HIP's uint4 is a struct)
 
-constexpr int kFskTile = 64;          // samples per input tile
-constexpr int kFskChunk = 32;         // samples per backward chunk (16 pairs)
+constexpr int kFskTile = 64;          // samples per input tile (and per checkpoint)
 
-// s1: [wave][q/2][64 lanes][2] doubles (q = j + (pad & 1), so the body starts on a pair)
-__device__ __forceinline__ size_t fsk_pair_index(int64_t w, int64_t m_pairs, int64_t q, int lane) {
-  return ((size_t)(w * m_pairs + (q >> 1)) * 64 + lane) * 2 + (q & 1);
+// F1 scratch, per wave: checkpoints ck[tile][6 states][64 lanes] doubles, then
+// the forward outputs of the tail (the last n % 64 samples and the right
+// extension) tl[j][64 lanes].
+__host__ __device__ inline int64_t fsk_tail_len(int64_t n, int pad) { return n % kFskTile + pad; }
+__host__ __device__ inline int64_t fsk_scratch_doubles_per_wave(int64_t n, int pad) {
+  return ((n / kFskTile) * 6 + fsk_tail_len(n, pad)) * 64;
 }
 
-// F1.  wave = 32 streams x 2 tones (lane = 2*stream + tone).  Input rows are
-// loaded 16 B per lane (64 samples of 32 streams per tile) and transposed
-// through LDS; the forward output goes to s1 as one 1 KiB row per sample pair;
-// the backward output is staged in LDS and written as 512 B row segments of
-// z (stream-major complex, f_mark + i f_space).
+// F1.  wave = 32 streams x 2 tones (lane = 2*stream + tone), checkpointed
+// filtfilt: the forward pass keeps only each 64-sample tile's starting state
+// (and the short tail's outputs); the backward pass walks the tiles top-down,
+// re-runs the forward recursion of a tile from its checkpoint (bit-identical
+// outputs, kept in LDS), then runs the backward recursion over them.  HBM
+// traffic per sample: x twice and z once, instead of also writing and
+// re-reading the forward outputs.  Input tiles are loaded 16 B
+// per lane and transposed through LDS; outputs are written back into the same
+// LDS slots and stored as 1 KiB rows of z (stream-major f_mark + i f_space).
 template <typename T>
 __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_stride, int64_t n_streams,
-                                                     double* __restrict__ s1, double2* __restrict__ z,
+                                                     double* __restrict__ scratch, double2* __restrict__ z,
                                                      FskParams p, FskIir f) {
   constexpr int RB = kFskTile * (int)sizeof(T);     // bytes per stream row per tile
   constexpr int PITCH = RB + 16;
   constexpr int LPR = RB / 16;                      // lanes per row in a load
   constexpr int RPI = 64 / LPR;                     // rows per load instruction
   constexpr int NI = 32 / RPI;                      // load instructions per tile
+  constexpr int YP = 66;                            // yb pitch (doubles): 16-B slot (33 l + row) % 16
   __shared__ __attribute__((aligned(16))) uint8_t tin[2][32][PITCH];
-  __shared__ __attribute__((aligned(16))) double tout[32][kFskChunk * 2 + 2];   // [stream][i][tone], padded
+  __shared__ __attribute__((aligned(16))) double yb[kFskTile][YP];   // [sample][lane]
   const int lane = threadIdx.x;
   const int tone = lane & 1, sl = lane >> 1;
   const int64_t w = blockIdx.x;
@@ -93,162 +100,163 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   const int64_t n = p.n;
   const int pad = p.pad;
   const int64_t m = n + 2 * (int64_t)pad;
-  const int qs = pad & 1;
-  const int64_t m_pairs = (m + qs + 1) >> 1;
+  const int64_t n_tiles = n / kFskTile;
+  const int64_t n_main = n_tiles * kFskTile;
+  double* __restrict__ ck = scratch + (size_t)w * fsk_scratch_doubles_per_wave(n, pad) + lane;
+  double* __restrict__ tl = ck + (size_t)n_tiles * 6 * 64;
   double b[7], a[7], zs[6];
 #pragma unroll
   for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
 
-  // ---- forward pass -------------------------------------------------------
+  const int rsub = lane / LPR, cb = (lane % LPR) * 16;
+  const uint8_t* rowp[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int64_t rs = w * 32 + RPI * i + rsub;
+    rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * x_stride) + cb;
+  }
+  v4u r[NI];
+  auto fetch = [&](int64_t t) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + t * RB);
+  };
+  auto deposit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[buf][RPI * i + rsub][cb]) = r[i];
+  };
+  // forward steps over tile `buf`; emit(k, y)
+  auto run_tile = [&](int buf, auto emit) {
+    constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int k = 0; k < kFskTile; k += PER) {
+      const v4u v = *reinterpret_cast<const v4u*>(&tin[buf][sl][k * sizeof(T)]);
+      T xs[PER];
+      __builtin_memcpy(xs, &v, 16);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step(zs, b, a, FIn<T>::cvt(xs[u])));
+    }
+  };
+
+  // ---- forward pass: checkpoints only ------------------------------------
   const T x0 = x[0], xl = x[n - 1];
   const double e0 = FIn<T>::ext(x0, x[pad]);
 #pragma unroll
   for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
-  for (int j = 0; j < pad; ++j)
-    s1[fsk_pair_index(w, m_pairs, j + qs, lane)] = fsk_step(zs, b, a, FIn<T>::ext(x0, x[pad - j]));
-  const int64_t n_tiles = n / kFskTile;
-  const int64_t n_main = n_tiles * kFskTile;
+  for (int j = 0; j < pad; ++j) (void)fsk_step(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
   if (n_tiles > 0) {
-    const int rsub = lane / LPR, cb = (lane % LPR) * 16;
-    const uint8_t* rowp[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int64_t rs = w * 32 + RPI * i + rsub;
-      rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * x_stride) + cb;
-    }
-    v4u r[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i]);
-#pragma unroll
-    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][RPI * i + rsub][cb]) = r[i];
+    fetch(0);
+    deposit(0);
     __syncthreads();
     for (int64_t t = 0; t < n_tiles; ++t) {
       const int cur = (int)(t & 1);
-      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;   // unconditional (clamped) prefetch
-#pragma unroll
-      for (int i = 0; i < NI; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + tn * RB);
-      __builtin_amdgcn_sched_barrier(0);
-      const int64_t q0 = pad + qs + t * kFskTile;         // even
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s1) + (size_t)(w * m_pairs + (q0 >> 1)) * 64 + lane;
-      constexpr int PER = 16 / (int)sizeof(T);
-#pragma unroll
-      for (int k = 0; k < kFskTile; k += PER) {
-        const v4u v = *reinterpret_cast<const v4u*>(&tin[cur][sl][k * sizeof(T)]);
-        T xs[PER];
-        __builtin_memcpy(xs, &v, 16);
-#pragma unroll
-        for (int u = 0; u < PER; u += 2) {
-          const double y0 = fsk_step(zs, b, a, FIn<T>::cvt(xs[u]));
-          const double y1 = fsk_step(zs, b, a, FIn<T>::cvt(xs[u + 1]));
-          dst[((k + u) >> 1) * 64] = make_double2(y0, y1);
-        }
-      }
+      fetch(t + 1 < n_tiles ? t + 1 : t);                 // unconditional (clamped) prefetch
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[cur ^ 1][RPI * i + rsub][cb]) = r[i];
+      for (int i = 0; i < 6; ++i) ck[((size_t)t * 6 + i) * 64] = zs[i];
+      run_tile(cur, [](int, double) {});
+      __builtin_amdgcn_sched_barrier(0);
+      deposit(cur ^ 1);
       __syncthreads();
     }
   }
-  for (int64_t i = n_main; i < n; ++i)
-    s1[fsk_pair_index(w, m_pairs, pad + i + qs, lane)] = fsk_step(zs, b, a, FIn<T>::cvt(x[i]));
+  for (int64_t i = n_main; i < n; ++i) tl[(size_t)(i - n_main) * 64] = fsk_step(zs, b, a, FIn<T>::cvt(x[i]));
   double ylast = 0.0;
   for (int j = 0; j < pad; ++j) {
     ylast = fsk_step(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
-    s1[fsk_pair_index(w, m_pairs, pad + n + j + qs, lane)] = ylast;
+    tl[(size_t)(n - n_main + j) * 64] = ylast;
   }
   __threadfence();
 
-  // ---- backward pass ------------------------------------------------------
+  // ---- backward pass --------------------------------------------------------
 #pragma unroll
   for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * ylast;
-  for (int64_t j = m - 1; j >= pad + n; --j) (void)fsk_step(zs, b, a, s1[fsk_pair_index(w, m_pairs, j + qs, lane)]);
-  const int64_t nc = n / kFskChunk;                 // full chunks, processed top-down
-  const int64_t n_lo = nc * kFskChunk;
+  for (int64_t j = n - n_main + pad - 1; j >= n - n_main; --j) (void)fsk_step(zs, b, a, tl[(size_t)j * 64]);
   double* __restrict__ zd = reinterpret_cast<double*>(z);
-  for (int64_t i = n - 1; i >= n_lo; --i) {         // top remainder, one sample at a time
-    const double y = fsk_step(zs, b, a, s1[fsk_pair_index(w, m_pairs, pad + i + qs, lane)]);
+  for (int64_t i = n - 1; i >= n_main; --i) {          // tail outputs, one sample at a time
+    const double y = fsk_step(zs, b, a, tl[(size_t)(i - n_main) * 64]);
     if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
   }
-  if (nc > 0) {
-    const double2* __restrict__ src = reinterpret_cast<const double2*>(s1) + (size_t)w * m_pairs * 64 + lane;
-    constexpr int PP = kFskChunk / 2;
-    double2 ra[PP], rb[PP];
-    auto load = [&](double2 (&r)[PP], int64_t c0) {
-      const int64_t c = c0 < 0 ? 0 : c0;
-      const int64_t qp = (pad + qs + c * kFskChunk) >> 1;
+  if (n_tiles > 0) {
+    double zf[6], zb[6];
+    fetch(n_tiles - 1);
 #pragma unroll
-      for (int k = 0; k < PP; ++k) r[k] = src[(size_t)(qp + k) * 64];
-    };
-    // chunk c -> z[s][32c .. 32c+32): 32 streams x 512 B, two rows per store instruction
-    auto run = [&](const double2 (&r)[PP], int64_t c) {
-#pragma unroll
-      for (int k = PP - 1; k >= 0; --k) {
-        const double y1 = fsk_step(zs, b, a, r[k].y);
-        const double y0 = fsk_step(zs, b, a, r[k].x);
-        tout[sl][(2 * k) * 2 + tone] = y0;
-        tout[sl][(2 * k + 1) * 2 + tone] = y1;
-      }
+    for (int i = 0; i < 6; ++i) zf[i] = ck[((size_t)(n_tiles - 1) * 6 + i) * 64];
+    for (int64_t t = n_tiles - 1; t >= 0; --t) {
+      deposit(0);
       __syncthreads();
-      const int half = lane >> 5, col = lane & 31;
+      const int64_t tp = t > 0 ? t - 1 : 0;
+      fetch(tp);                                            // next (lower) tile, and its checkpoint
+#pragma unroll
+      for (int i = 0; i < 6; ++i) zb[i] = ck[((size_t)tp * 6 + i) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+      // forward recursion of tile t from its checkpoint -> yb
+      double zsave[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) { zsave[i] = zs[i]; zs[i] = zf[i]; }
+      run_tile(0, [&](int k, double y) { yb[k][lane] = y; });
+#pragma unroll
+      for (int i = 0; i < 6; ++i) { zs[i] = zsave[i]; zf[i] = zb[i]; }
+      // backward recursion over it, outputs in place
+#pragma unroll 8
+      for (int k = kFskTile - 1; k >= 0; --k) yb[k][lane] = fsk_step(zs, b, a, yb[k][lane]);
+      __syncthreads();
+      // 32 rows x 64 samples of z, one 1 KiB row per store instruction
+      const int64_t i0 = t * kFskTile;
 #pragma unroll 4
-      for (int rr = 0; rr < 32; rr += 2) {
-        const int row = rr + half;
+      for (int row = 0; row < 32; ++row) {
         const int64_t so = w * 32 + row;
-        if (so < n_streams)
-          z[(size_t)so * n + c * kFskChunk + col] =
-              make_double2(tout[row][2 * col], tout[row][2 * col + 1]);
+        const double2 v = *reinterpret_cast<const double2*>(&yb[lane][2 * row]);
+        if (so < n_streams) z[(size_t)so * n + i0 + lane] = v;
       }
       __syncthreads();
-    };
-    load(ra, nc - 1);
-    load(rb, nc - 2);
-    int64_t c = nc - 1;
-    for (; c >= 1; c -= 2) {
-      run(ra, c);
-      __builtin_amdgcn_sched_barrier(0);
-      load(ra, c - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      run(rb, c - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      load(rb, c - 3);
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (c == 0) run(ra, 0);
   }
 }
 
-// F3.  thread = (stream, bit): bit b of the stream is 1 when more than half of
-// the compare bits of samples [i-q, min(i+q, n)) are 1, i = sps/2 + b*sps
-// (np.mean(chunk) > 0.5, modem.py:320-323).  Compare bits are in the final
-// row pass's tile order (fft.h fft_bits_stride).  A wave covers 64
-// consecutive bits; a ballot packs them MSB first into two words.
-__global__ __launch_bounds__(64) void k_fsk_decide(const uint8_t* __restrict__ bits, uint32_t* __restrict__ words,
-                                                   int64_t n_streams, FskParams p) {
-  const int64_t s = blockIdx.y;
-  const int64_t bi = (int64_t)blockIdx.x * 64 + threadIdx.x;
+// F3.  workgroup = stream: the stream's compare bits (in the final row pass's
+// tile order, fft.h fft_bits_stride; <= 49 KiB) are staged in LDS with
+// coalesced 16-B loads, then thread = output word: bit b is 1 when more than
+// half of the compare bits of samples [i-q, min(i+q, n)) are 1,
+// i = sps/2 + b*sps (np.mean(chunk) > 0.5, modem.py:320-323); bits go MSB first.
+constexpr int kDecideThreads = 256;
+
+__global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __restrict__ bits,
+                                                               uint32_t* __restrict__ words, int64_t n_streams,
+                                                               FskParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t sb[];
+  const int64_t s = blockIdx.x;
   const uint8_t* __restrict__ c = bits + (size_t)s * p.bits_stride;
+  const int nb = (int)p.bits_stride;
+  // bits_stride need not be a multiple of 16 (nor rows 16-B aligned): bytes
+  for (int i = threadIdx.x; i < nb; i += kDecideThreads) sb[i] = c[i];
+  __syncthreads();
   const int64_t q = p.sps / 4, half = p.sps / 2;
-  bool bit = false;
-  if (bi < p.n_bits) {
-    const int64_t i = half + bi * p.sps;
-    const int64_t lo = i - q, hi = (i + q < p.n) ? i + q : p.n;
-    // sample lo = r + rn1*kk
-    int64_t kk = (int64_t)(((float)lo + 0.5f) * p.inv_rn1);
-    int64_t r = lo - kk * p.rn1;
-    int64_t ones = 0;
-    for (int64_t k = lo; k < hi; ++k) {
-      ones += (c[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
-      if (++r == p.rn1) {
-        r = 0;
-        ++kk;
+  for (int64_t w = threadIdx.x; w < p.n_words; w += kDecideThreads) {
+    uint32_t word = 0;
+    for (int u = 0; u < 32; ++u) {
+      const int64_t bi = w * 32 + u;
+      if (bi >= p.n_bits) break;
+      const int64_t i = half + bi * p.sps;
+      const int64_t lo = i - q, hi = (i + q < p.n) ? i + q : p.n;
+      int64_t kk = (int64_t)(((float)lo + 0.5f) * p.inv_rn1);   // sample lo = r + rn1*kk
+      int64_t r = lo - kk * p.rn1;
+      int64_t ones = 0;
+      for (int64_t k = lo; k < hi; ++k) {
+        ones += (sb[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
+        if (++r == p.rn1) {
+          r = 0;
+          ++kk;
+        }
       }
+      word |= (2 * ones > hi - lo ? 1u : 0u) << (31 - u);
     }
-    bit = 2 * ones > hi - lo;
+    words[(size_t)s * p.n_words + w] = word;
   }
-  const uint64_t mask = __ballot(bit);
-  const int64_t w0 = (int64_t)blockIdx.x * 2;
-  if (threadIdx.x == 0 && w0 < p.n_words) words[(size_t)s * p.n_words + w0] = __brev((uint32_t)mask);
-  if (threadIdx.x == 32 && w0 + 1 < p.n_words) words[(size_t)s * p.n_words + w0 + 1] = __brev((uint32_t)(mask >> 32));
+}
+
+int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad) {
+  return ((n_streams + 31) / 32) * fsk_scratch_doubles_per_wave(n, pad) * (int64_t)sizeof(double);
 }
 
 hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
@@ -266,8 +274,8 @@ hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,
                              hipStream_t st) {
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
-  hipLaunchKernelGGL(k_fsk_decide, dim3((unsigned)((p.n_bits + 63) / 64), (unsigned)n_streams), dim3(64), 0, st,
-                     cmp, words, n_streams, p);
+  hipLaunchKernelGGL(k_fsk_decide, dim3((unsigned)n_streams), dim3(kDecideThreads), (size_t)p.bits_stride, st, cmp,
+                     words, n_streams, p);
   return hipGetLastError();
 }
 

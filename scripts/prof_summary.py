@@ -31,8 +31,8 @@ def find(d, pat):
     return m[0] if m else None
 
 
-KERNELS = ["k_bandpass_quad", "k_bandpass", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
-           "k_sync_pack", "k_fec_decode", "k_fsk_bandpass", "k_fsk_decide",
+KERNELS = ["k_fsk_bandpass", "k_fsk_decide", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
+           "k_sync_pack", "k_fec_decode",
            "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
