@@ -248,8 +248,9 @@ def main():
         parity = "skipped"
         if not args.no_cpu:
             if fsk:
-                # scipy's hilbert dominates; ~30 streams ~ 10-20 s of single-core work
-                n_cpu = args.cpu_streams or 256
+                # ~16 ms of single-core work per stream (scipy's hilbert dominates):
+                # 1024 streams ~ 15 s of CPU work spread over the host threads
+                n_cpu = args.cpu_streams or 1024
                 idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
                 val, cdt, couts = cpu_baseline_fsk(x[idx], baud, args.mark, args.space, threads)
                 how = "oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
