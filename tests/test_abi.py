@@ -52,6 +52,25 @@ def test_demod_fails_loudly_without_gpu(built_lib):
         modem.qpsk_demodulate(x, baud=9600)
     with pytest.raises(_amr.AmrError):
         modem.bpsk_demodulate(x, baud=1200)
+    with pytest.raises(_amr.AmrError):
+        modem.fsk_demodulate(x, baud=9600, mark_freq=12000.0, space_freq=24000.0)
+    with pytest.raises(_amr.AmrError):
+        _amr.hilbert(np.zeros((1, 64)))
+
+
+def test_fsk_plan_create_argument_checks(built_lib):
+    import _amr
+    L = _amr.lib()
+    h = ctypes.c_void_p()
+    b = np.zeros(7)
+    a = np.zeros(7); a[0] = 1
+    args = [_amr.ptr(v) for v in (b, a, b, b, a, b)]
+    assert L.amr_fsk_plan_create(ctypes.byref(h), 0, 1000, 10, *args, 9, 1) == _amr.AMR_E_INVALID   # taps
+    assert L.amr_fsk_plan_create(ctypes.byref(h), 0, 1000, 0, *args, 7, 1) == _amr.AMR_E_INVALID    # sps
+    assert L.amr_fsk_plan_create(ctypes.byref(h), 0, 21, 10, *args, 7, 1) == _amr.AMR_E_PADLEN
+    assert b"padlen, which is 21" in L.amr_last_error()
+    args[1] = _amr.ptr(np.zeros(7))
+    assert L.amr_fsk_plan_create(ctypes.byref(h), 0, 1000, 10, *args, 7, 1) == _amr.AMR_E_INVALID   # a[0]
 
 
 def test_plan_create_argument_checks(built_lib):
