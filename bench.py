@@ -100,11 +100,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["qpsk9600", "fsk9600"], default="qpsk9600",
-                    help="qpsk9600 = BASELINE configs[1] (the headline metric); fsk9600 = configs[3]")
-    ap.add_argument("--batch", type=int, default=0, help="streams per GPU (0 = the config's: 4096 / 16384)")
+    ap.add_argument("--workload", choices=["qpsk9600", "fsk9600", "ofdm8", "psk8fec"], default="qpsk9600",
+                    help="qpsk9600 = BASELINE configs[1] (the headline metric); fsk9600 = configs[3]; "
+                         "ofdm8 = configs[4] (QPSK alias, global batch 8192 sharded); psk8fec = configs[5] "
+                         "(8PSK@19200 + fused FEC decode, global batch 8192 sharded)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="streams per GPU (qpsk9600/fsk9600, default 4096/16384) or in total (ofdm8/psk8fec, "
+                         "default 8192)")
     ap.add_argument("--samples", type=int, default=96000)
-    ap.add_argument("--baud", type=float, default=9600)
+    ap.add_argument("--baud", type=float, default=None, help="default 9600 (19200 for psk8fec)")
     ap.add_argument("--mark", type=float, default=12000.0, help="fsk9600: mark tone (SURVEY §6 config 3)")
     ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
     ap.add_argument("--distinct", type=int, default=64, help="distinct waveforms (noise is per stream)")
@@ -115,14 +119,29 @@ def main():
     dist, world, rank, local = dist_setup(args.gpus)
     dev = local
     fsk = args.workload == "fsk9600"
-    B = args.batch or (16384 if fsk else 4096)
-    N, baud = args.samples, args.baud
+    fec_fused = args.workload == "psk8fec"
+    strong = args.workload in ("ofdm8", "psk8fec")       # a fixed global batch sharded over the ranks
+    if strong:
+        from multi import shard_range
+        B_global = args.batch or 8192
+        lo_s, hi_s = shard_range(B_global, rank, world)
+        B = hi_s - lo_s
+        B_slot = -(-B_global // world)                    # all-gather slot (ranks' shards differ by <= 1)
+    else:
+        B = args.batch or (16384 if fsk else 4096)
+        B_global = world * B
+        lo_s = rank * B
+        B_slot = B
+    N = args.samples
+    baud = args.baud or (19200.0 if fec_fused else 9600.0)
     L = _amr.lib()
     _amr.check(L.amr_set_device(dev))
 
     t0 = time.perf_counter()
     if fsk:
         x = synth.fsk_batch(B, N, baud, args.mark, args.space, seed=1000 + rank, distinct=args.distinct)
+    elif fec_fused:
+        x = synth.dpsk8_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
     else:
         x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
     log(f"[rank {rank}] synthesised {B}x{N} float32 in {time.perf_counter() - t0:.1f}s")
@@ -146,7 +165,9 @@ def main():
         return p
 
     d_x = dmalloc(x.nbytes)
-    d_out, d_len, d_sync = dmalloc(B * cap), dmalloc(B * 8), dmalloc(B * 8)
+    d_out, d_len, d_sync = dmalloc(B_slot * cap), dmalloc(B_slot * 8), dmalloc(B_slot * 8)
+    if fec_fused:
+        d_fec, d_flen, d_ok = dmalloc(B_slot * cap), dmalloc(B_slot * 8), dmalloc(B_slot * 4)
     _amr.check(L.amr_memcpy_h2d(d_x, _amr.ptr(x), x.nbytes))
     comm = None
     d_gather = None
@@ -159,19 +180,26 @@ def main():
         uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
         comm = ctypes.c_void_p()
         _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
-        d_gather = dmalloc(world * B * cap)
-        d_gather_len = dmalloc(world * B * 8)
+        d_gather = dmalloc(world * B_slot * cap)
+        d_gather_len = dmalloc(world * B_slot * 8)
     # amr_allgather enqueues on a PSK plan's stream (or the comm's own for NULL)
     gather_stream = None if fsk else plan.handle
 
+    # the bytes every rank hands to the gather: the FEC output for psk8fec
+    g_out, g_len = (d_fec, d_flen) if fec_fused else (d_out, d_len)
+
     def step():
-        _amr.check(demod(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
+        if fec_fused:
+            _amr.check(L.amr_psk_demod_fec_device(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync,
+                                                  d_fec, cap, d_flen, d_ok))
+        else:
+            _amr.check(demod(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
         if comm is not None:
             if fsk:
                 _amr.check(sync_fn(plan.handle))
             # the decoded bytes of every rank to every rank (RCCL over xGMI)
-            _amr.check(L.amr_allgather(comm, d_out, d_gather, B * cap, gather_stream))
-            _amr.check(L.amr_allgather(comm, d_len, d_gather_len, B * 8, gather_stream))
+            _amr.check(L.amr_allgather(comm, g_out, d_gather, B_slot * cap, gather_stream))
+            _amr.check(L.amr_allgather(comm, g_len, d_gather_len, B_slot * 8, gather_stream))
             if fsk:
                 _amr.check(L.amr_comm_synchronize(comm))
         _amr.check(sync_fn(plan.handle))
@@ -191,7 +219,7 @@ def main():
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dist, dt)
     ms_per_step = dt / args.steps * 1e3
-    total_sym = world * B * sym_per_stream
+    total_sym = B_global * sym_per_stream
     value = total_sym / (dt / args.steps) / 1e6
 
     # per-kernel averages (HIP events on the plan's stream)
@@ -217,7 +245,7 @@ def main():
         S_sym = sym_per_stream + 1
         alg_bytes = {"bandpass": B * N * (4 + 8), "lowpass_fwd": B * N * (8 + 16),
                      "lowpass_bwd": B * (N * 16 + S_sym * 16), "sync_pack": B * (S_sym * 16 + cap),
-                     "lowpass_exact": 0, "fec": 0}
+                     "lowpass_exact": 0, "fec": B * 2 * cap}
         # FP64 operations scipy's arithmetic needs (no FMA): band-pass 30/sample per
         # pass (9 taps incl. the zero odd taps), low-pass 17/sample per pass per
         # component, mixer 2/sample
@@ -229,7 +257,8 @@ def main():
     fp64_achieved = fp64_ops.get(dom, 0) / (kavg[dom] / 1e3) / 1e12
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
-    if (B, N, int(baud)) == ((16384 if fsk else 4096), 96000, 9600) and os.path.exists(pmc_file):
+    if (args.workload in ("qpsk9600", "fsk9600") and (B, N, int(baud)) == ((16384 if fsk else 4096), 96000, 9600)
+            and os.path.exists(pmc_file)):
         with open(pmc_file) as f:
             pk = json.load(f).get(args.workload, {}).get("slots", {}).get(dom, {})
         if "hbm_bytes_per_launch" in pk:
@@ -238,8 +267,8 @@ def main():
     # parity spot-check after timing (not timed): GPU bytes vs the oracle
     out = np.empty((B, cap), np.uint8)
     ln = np.empty(B, np.int64)
-    _amr.check(L.amr_memcpy_d2h(_amr.ptr(out), d_out, B * cap))
-    _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), d_len, B * 8))
+    _amr.check(L.amr_memcpy_d2h(_amr.ptr(out), g_out, B * cap))
+    _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
 
     result = None
     if rank == 0:
@@ -259,6 +288,13 @@ def main():
                 idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
                 val, cdt, couts = cpu_baseline(x[idx], baud, threads)
                 how = "the C restatement oracle/amr_oracle.c, OpenMP over streams"
+                if fec_fused:
+                    from oracle import oracle
+                    t1 = time.perf_counter()
+                    couts = [oracle.fec_decode(c)[0] for c in couts]
+                    cdt += time.perf_counter() - t1
+                    val = len(idx) * sym_per_stream / cdt / 1e6
+                    how += " + oracle.fec_decode"
             cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
                    "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through {how}, "
                              f"{cdt:.2f} s wall"}
@@ -268,6 +304,14 @@ def main():
             metric = "FSK demod Msymbols/s (batch), FSK9600 96kHz mark/space 12k/24k"
             workload = (f"FSK@{int(baud)} 96kHz tones {args.mark:g}/{args.space:g} Hz, batch {B} x {N} float32 "
                         "streams per GPU (BASELINE configs[3] at SURVEY §6's valid tones)")
+        elif args.workload == "ofdm8":
+            metric = "OFDM8 (qpsk_demodulate alias) demod Msymbols/s, global batch sharded + RCCL gather"
+            workload = (f"OFDM8 = QPSK@{int(baud)} 96kHz (modem.py:375-376), {B_global} x {N} float32 streams "
+                        f"sharded over {world} GPU(s) (BASELINE configs[4])")
+        elif fec_fused:
+            metric = "8PSK@19200 demod + fused FEC decode Msymbols/s, global batch sharded + RCCL gather"
+            workload = (f"8PSK@{int(baud)} = QPSK path (modem.py:348) + ReedSolomonFEC.decode fused, {B_global} x "
+                        f"{N} float32 streams sharded over {world} GPU(s) (BASELINE configs[5])")
         else:
             metric = "demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU"
             workload = f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU (BASELINE configs[1])"
@@ -275,8 +319,8 @@ def main():
             "metric": metric,
             "value": round(value, 3), "unit": "Msym/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": workload, "global_batch": world * B, "samples_per_stream": N,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload, "global_batch": B_global, "samples_per_stream": N,
                        "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -292,8 +336,10 @@ def main():
         }
         if not fsk:
             result["exact_path_streams"] = plan.exact_streams()
+        if fec_fused:
+            result["parity"] += " (FEC output)"
         print(json.dumps(result), flush=True)
-    for p in (d_x, d_out, d_len, d_sync):
+    for p in (d_x, d_out, d_len, d_sync) + ((d_fec, d_flen, d_ok) if fec_fused else ()):
         L.amr_free(p)
     if comm is not None:
         L.amr_free(d_gather)
