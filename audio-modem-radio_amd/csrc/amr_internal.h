@@ -49,6 +49,7 @@ struct PskBuffers {
   int dtype;
   int64_t n_streams;      // B
   const double* lo;       // [n][4]: (lo_re, -(0*lo_im), lo_im, 0*lo_re)
+  const double* lo2;      // [2][n]: lo_re[n], lo_im[n] (the multipliers alone)
   double* s1;             // band-pass forward output  [G][m1p/2][64][2]
   double* s2;             // band-pass output f        [G][2][n2][32][2]
   double* s3;             // low-pass forward output   [2G][m2p/2][64][2]

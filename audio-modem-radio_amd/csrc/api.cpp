@@ -100,6 +100,10 @@ bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }
 
 }  // namespace
 
+// doubles of slack below s1/s3: the backward passes prefetch up to a few
+// chunks past the start of their block instead of clamping the index
+constexpr int64_t kFrontSlack = 8192;
+
 struct amr_psk_plan {
   std::mutex mu;
   int device = 0;
@@ -112,9 +116,12 @@ struct amr_psk_plan {
   int64_t out_cap = 0;
   // HBM scratch
   double* lo = nullptr;
-  double* s1 = nullptr;
+  double* lo2 = nullptr;
+  double* s1 = nullptr;   // = s1_base + kFrontSlack (backward prefetch may read below)
   double* s2 = nullptr;
-  double* s3 = nullptr;
+  double* s3 = nullptr;   // = s3_base + kFrontSlack
+  double* s1_base = nullptr;
+  double* s3_base = nullptr;
   uint32_t* words = nullptr;
   int32_t* flags = nullptr;
   int64_t scratch_bytes = 0;
@@ -191,7 +198,7 @@ static void plan_free(amr_psk_plan* pl) {
   if (!pl) return;
   (void)hipSetDevice(pl->device);
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
-  for (auto* p : {(void*)pl->lo, (void*)pl->s1, (void*)pl->s2, (void*)pl->s3, (void*)pl->words, (void*)pl->flags,
+  for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
                   pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
     if (p) (void)hipFree(p);
@@ -267,10 +274,13 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
+      // + slack: K2q's prefetch runs up to a few chunks past the end (psk_kernels.hip)
+      {(void**)&pl->lo2, (n * 2 + 1024) * (int64_t)sizeof(double)},
       // s1 doubles as the symbol buffer [2G][S][64] after K1 (sym_index in psk_kernels.hip)
-      {(void**)&pl->s1, std::max(g * pl->m1_pairs * kWave * 16, 2 * g * std::max<int64_t>(p.n_sym, 1) * kWave * 8)},
-      {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16},
-      {(void**)&pl->s3, 2 * g * pl->m2_pairs * kWave * 16},
+      {(void**)&pl->s1_base,
+       kFrontSlack * 8 + std::max(g * pl->m1_pairs * kWave * 16, 2 * g * std::max<int64_t>(p.n_sym, 1) * kWave * 8)},
+      {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
+      {(void**)&pl->s3_base, kFrontSlack * 8 + 2 * g * pl->m2_pairs * kWave * 16},
       {(void**)&pl->words, g * kWave * p.n_words * 4},
       {(void**)&pl->flags, g * kWave * 4},
   };
@@ -282,6 +292,8 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
     }
     pl->scratch_bytes += a.bytes;
   }
+  pl->s1 = pl->s1_base + kFrontSlack;
+  pl->s3 = pl->s3_base + kFrontSlack;
   {
     // device LO layout [n][4] = (lo_re, -(0*lo_im), lo_im, 0*lo_re): per sample and
     // component the (multiplier, addend) pair of numpy's complex multiply
@@ -293,6 +305,12 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
       lo_dev[4 * i + 3] = lo4[4 * i + 3];
     }
     e = hipMemcpy(pl->lo, lo_dev.data(), (size_t)(n * 4 * sizeof(double)), hipMemcpyHostToDevice);
+    // [2][n]: the multipliers alone (K2q's main-body mixer, psk_kernels.hip)
+    for (int64_t i = 0; i < n; ++i) {
+      lo_dev[(size_t)i] = lo4[4 * i + 0];
+      lo_dev[(size_t)(n + i)] = lo4[4 * i + 1];
+    }
+    if (e == hipSuccess) e = hipMemcpy(pl->lo2, lo_dev.data(), (size_t)(n * 2 * sizeof(double)), hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
@@ -376,6 +394,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   b.dtype = dtype;
   b.n_streams = B;
   b.lo = pl->lo;
+  b.lo2 = pl->lo2;
   b.s1 = pl->s1;
   b.s2 = pl->s2;
   b.s3 = pl->s3;

@@ -437,6 +437,204 @@ __global__ __launch_bounds__(64) void k_bandpass_quad(PskBuffers buf, PskParams 
 }
 
 // ---------------------------------------------------------------------------
+// K1r: the 9-tap band-pass with ONE STATE PER LANE of a 16-lane DPP row.
+// A lone wave issues one FP64 instruction every ~4.7 cycles, so what bounds a
+// stream is the length of its per-sample instruction stream.  K1q needed 16
+// (10 FP64 + 6 moves); here lane 8+j of row r owns z[j] of stream 4w+r and a
+// sample costs 9:
+//   t     = z + b0*x                   (lane 8: t IS y)
+//   y     = v_mov_b64 row_newbcast:8   (one 64-bit DPP move)
+//   zC    = row_shl:1 (z)              (z[j+1] from lane 9+j: two 32-bit moves)
+//   z     = (zC + x*b[j+1]) - y*a[j+1]
+// Lane 15 (z[7]) reads beyond its row: its lo word comes back 0 (bound_ctrl)
+// and its hi word is never written, so it keeps 0x80000000 -- zC is exactly
+// -0.0 there and (-0.0 + x*b8) - y*a8 == x*b8 - y*a8 bit for bit.  Lanes 0-7
+// run the same instructions on garbage nobody reads.  At the benchmark batch
+// (4096 streams) the kernel is 1024 waves = one per SIMD
+// (tools/step_probe2.hip: 51.5 vs 76.3 cycles/sample for K1q).
+constexpr int kRowStreams = 4;                  // streams (DPP rows) per wave
+constexpr int kBpRing = 3;                      // K1r backward prefetch ring depth (32-sample chunks)
+
+__device__ __forceinline__ double row_bcast8(double v) {
+  const long u = __builtin_bit_cast(long, v);
+  const long r = __builtin_amdgcn_update_dpp(0L, u, 0x158, 0xF, 0xF, true);   // row_newbcast:8
+  return __builtin_bit_cast(double, r);
+}
+// z[j+1] from the next lane of the row; hk is the hi word's DPP destination,
+// carried across steps so that the out-of-row lane keeps 0x80000000
+__device__ __forceinline__ double row_next(double v, int& hk) {
+  const long long u = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xffffffff), 0x101, 0xF, 0xF, true);   // row_shl:1
+  hk = __builtin_amdgcn_update_dpp(hk, (int)(u >> 32), 0x101, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hk << 32) | (unsigned)lo);
+}
+
+struct RowIir {
+  double b0, cb, ca;
+};
+
+__device__ __forceinline__ double row_step(const RowIir& c, double& z, int& hk, double x) {
+  const double t = z + c.b0 * x;
+  const double y = row_bcast8(t);
+  const double zC = row_next(z, hk);
+  z = (zC + x * c.cb) - y * c.ca;
+  return y;
+}
+
+// s1 for K1r: [w][q/2][4 streams][2] doubles
+__device__ __forceinline__ size_t row_pair_index(int64_t w, int64_t m_pairs, int64_t q, int r) {
+  return ((size_t)(w * m_pairs + (q >> 1)) * kRowStreams + r) * 2 + (q & 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams p, Iir f) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[4][2][kRowStreams][kTilePitch];
+  constexpr int TS = kTileBytes / (int)sizeof(T);
+  const int wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int r = lane >> 4, l = lane & 15;
+  const int j = l & 7;                          // state owned (lanes 8-15; 0-7 mirror them)
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t s = w * kRowStreams + r;
+  const int64_t last = buf.n_streams - 1;
+  if (w * kRowStreams > last) return;           // whole wave past the batch (wave-uniform)
+  auto& tile = tiles[wv];
+  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
+  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad1;
+  const int64_t m1 = p.m1;
+  const int qs = pad & 1;
+  const int64_t m1_pairs = (m1 + qs + 1) >> 1;
+  double* __restrict__ s1 = buf.s1;
+
+  RowIir c;
+  c.b0 = f.b[0];
+  c.cb = f.b[j + 1];
+  c.ca = f.a[j + 1];
+  const double zi = f.zi[j];
+  double z;
+  int hk = (int)0x80000000;
+
+  // ---- forward pass -------------------------------------------------------
+  const T x0 = x[0], xl = x[n - 1];
+  z = zi * In<T>::ext(x0, x[pad]);
+  for (int jj = 0; jj < pad; ++jj) {
+    const double y = row_step(c, z, hk, In<T>::ext(x0, x[pad - jj]));
+    s1[row_pair_index(w, m1_pairs, jj + qs, r)] = y;
+  }
+  const int64_t n_tiles = n / TS;
+  const int64_t n_main = n_tiles * TS;
+  if (n_tiles > 0) {
+    // one tile = 4 stream rows x 256 B: one 16-B load per lane
+    const int cb = l * 16;
+    const uint8_t* rowp = reinterpret_cast<const uint8_t*>(x) + cb;
+    v4u rv = *reinterpret_cast<const v4u*>(rowp);
+    *reinterpret_cast<v4u*>(&tile[0][r][cb]) = rv;
+    for (int64_t t = 0; t < n_tiles; ++t) {
+      const int cur = (int)(t & 1);
+      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
+      rv = *reinterpret_cast<const v4u*>(rowp + tn * kTileBytes);
+      __builtin_amdgcn_sched_barrier(0);
+      const int64_t q0 = pad + qs + t * TS;
+      double2* __restrict__ dst =
+          reinterpret_cast<double2*>(s1) + (size_t)(w * m1_pairs + (q0 >> 1)) * kRowStreams + r;
+      constexpr int PER = 16 / (int)sizeof(T);
+      // the row's whole tile into registers at once: one LDS round trip per
+      // tile instead of one per 16 B (the reads are broadcasts, 4 addresses)
+      v4u xv[TS / PER];
+#pragma unroll
+      for (int k = 0; k < TS / PER; ++k) xv[k] = *reinterpret_cast<const v4u*>(&tile[cur][r][k * 16]);
+#pragma unroll
+      for (int k = 0; k < TS; k += PER) {
+        T xs[PER];
+        __builtin_memcpy(xs, &xv[k / PER], 16);
+#pragma unroll
+        for (int u = 0; u < PER; u += 2) {
+          const double y0 = row_step(c, z, hk, In<T>::cvt(xs[u]));
+          const double y1 = row_step(c, z, hk, In<T>::cvt(xs[u + 1]));
+          dst[((k + u) >> 1) * kRowStreams] = make_double2(y0, y1);   // all 16 lanes: same value
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      *reinterpret_cast<v4u*>(&tile[cur ^ 1][r][cb]) = rv;
+    }
+  }
+  for (int64_t i = n_main; i < n; ++i) {
+    const double y = row_step(c, z, hk, In<T>::cvt(x[i]));
+    s1[row_pair_index(w, m1_pairs, pad + i + qs, r)] = y;
+  }
+  double ylast = 0.0;
+  for (int jj = 0; jj < pad; ++jj) {
+    ylast = row_step(c, z, hk, In<T>::ext(xl, x[n - 2 - jj]));
+    s1[row_pair_index(w, m1_pairs, pad + n + jj + qs, r)] = ylast;
+  }
+  __threadfence();
+
+  // ---- backward pass ------------------------------------------------------
+  z = zi * ylast;
+  hk = (int)0x80000000;
+  for (int64_t jj = m1 - 1; jj >= pad + n; --jj)
+    (void)row_step(c, z, hk, s1[row_pair_index(w, m1_pairs, jj + qs, r)]);
+
+  const int64_t n2 = (n + 1) >> 1;
+  double* __restrict__ fo = buf.s2;
+  const int64_t sgrp = s >> 6;
+  const int sig = (int)(s & 63);
+  const int64_t nb = n / kBwdChunk;
+  const int64_t n_lo = nb * kBwdChunk;
+  for (int64_t i = n - 1; i >= n_lo; --i) {
+    const double y = row_step(c, z, hk, s1[row_pair_index(w, m1_pairs, pad + i + qs, r)]);
+    fo[f_index(sgrp, n2, i, sig)] = y;
+  }
+  if (nb > 0) {
+    // pointers walk down one chunk per run/load (loads may run R chunks below
+    // the block, into the plan's front slack, instead of clamping)
+    constexpr int PP = kBwdChunk / 2;
+    const double2* __restrict__ rnext = reinterpret_cast<const double2*>(s1) +
+                                        ((size_t)w * m1_pairs + ((pad + qs + (nb - 1) * kBwdChunk) >> 1)) * kRowStreams + r;
+    double2* __restrict__ dst = reinterpret_cast<double2*>(fo) + (size_t)((sgrp * 2 + (sig >> 5)) * n2) * 32 +
+                                (sig & 31) + (size_t)((nb - 1) * PP) * 32;
+    constexpr int R = kBpRing;
+    double2 rr_[R][PP];
+    auto load = [&](double2 (&rr)[PP]) {
+#pragma unroll
+      for (int k = 0; k < PP; ++k) rr[k] = rnext[k * kRowStreams];
+      rnext -= PP * kRowStreams;
+    };
+    auto run = [&](const double2 (&rr)[PP]) {
+#pragma unroll
+      for (int k = PP - 1; k >= 0; --k) {
+        const double y1 = row_step(c, z, hk, rr[k].y);
+        const double y0 = row_step(c, z, hk, rr[k].x);
+        dst[k * 32] = make_double2(y0, y1);
+      }
+      dst -= PP * 32;
+    };
+    // ring slot u holds chunk cc-u, refilled R chunks further down right
+    // after it is consumed; slot 0 is issued first (vmcnt retires in order)
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      load(rr_[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int64_t cc = nb - 1;
+    for (; cc >= R - 1; cc -= R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        run(rr_[u]);
+        __builtin_amdgcn_sched_barrier(0);
+        load(rr_[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (cc - u >= 0) run(rr_[u]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Low-pass kernels K2/K3.  A lane PAIR serves one component of one stream:
 // lane j of the pair owns states z[2j], z[2j+1] of the 5-tap recurrence (the
 // same DPP split as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1,
@@ -774,6 +972,325 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
 }
 
 // ---------------------------------------------------------------------------
+// K2q / K3q: the low-pass with ONE STATE PER LANE of a quad (lane j owns z[j]
+// of the 5-tap recurrence); a wave serves 16 streams x one component, so the
+// LO stays wave-uniform.  Per sample 11 VALU instead of the pair split's 16:
+//   t  = z + b0*x ; y = quad_perm[0,0,0,0](t)
+//   zC = quad_perm[1,2,3,3](z) * m      (m = 1, and 0 on the top lane j = 3)
+//   z  = (zC + x*b[j+1]) - y*a[j+1]
+// On the top lane zC*0 is a signed zero, and (+-0 + x*b4) == x*b4 whenever
+// x*b4 != 0, i.e. whenever x != 0 (b4 >= 2^-50, checked at plan time): every
+// input the detector lets through.  So the recurrence is scipy's bit for bit
+// on every stream that is not flagged, and flagged streams are recomputed by
+// K3x as before.
+//
+// Detector (one VALU per sample in K2q, half in K3q): the minimum over
+// |hi word read as float32| of the values that must be >= 2^-1022.  That hi
+// word is >= FLT_MIN exactly when the double's exponent field is >= 8, i.e.
+// |v| >= 2^-1015, so zeros and denormals are always caught (values in
+// [2^-1022, 2^-1015) are flagged too -- conservative, they take the exact
+// path).  Infinities and NaN are sticky and caught by the final-state test.
+// v_min3_f32 runs in inline asm so the compiler adds no NaN canonicalisation.
+constexpr int kQuadShift = 0xF9;                // quad_perm [1,2,3,3]
+constexpr int kLpQChunk = 8;                    // K2q main-body chunk (samples)
+constexpr int kLpQRing = 8;                     // K2q f prefetch ring depth (chunks)
+constexpr int kLpBRing = 5;                     // K3q prefetch ring depth (chunks of 20/16 samples)
+typedef __attribute__((address_space(4))) const double CDouble;   // constant AS: uniform loads -> SMEM
+constexpr float kTinyHi = 0x1p-126f;            // FLT_MIN
+
+struct Quad5 {
+  double b0, cb, ca, cm;
+};
+
+__device__ __forceinline__ Quad5 quad5_coef(const Iir& f, int j, double& zi) {
+  Quad5 c;
+  c.b0 = f.b[0];
+  c.cb = f.b[j + 1];
+  c.ca = f.a[j + 1];
+  c.cm = j == 3 ? 0.0 : 1.0;
+  zi = f.zi[j];
+  return c;
+}
+
+__device__ __forceinline__ double quad5_step(const Quad5& c, double& z, double x) {
+  const double t = z + c.b0 * x;
+  const double y = dpp_f64<kQuadBcast0>(t);
+  const double zC = dpp_f64<kQuadShift>(z) * c.cm;
+  z = (zC + x * c.cb) - y * c.ca;
+  return y;
+}
+
+__device__ __forceinline__ float tiny_min3(float acc, double a, double b) {
+  const float ha = __builtin_bit_cast(float, (unsigned)(__builtin_bit_cast(unsigned long long, a) >> 32));
+  const float hb = __builtin_bit_cast(float, (unsigned)(__builtin_bit_cast(unsigned long long, b) >> 32));
+  float r;
+  asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(acc), "v"(ha), "v"(hb));
+  return r;
+}
+
+// s3 for K2q/K3q: [w16][comp][q/2][16 streams][2] doubles
+__device__ __forceinline__ size_t s3q_index(int64_t w, int comp, int64_t m_pairs, int64_t q, int sq) {
+  return ((((size_t)((w * 2 + comp) * m_pairs + (q >> 1))) * 16 + sq) * 2) + (q & 1);
+}
+
+__device__ __forceinline__ void quad_flag(PskBuffers& buf, int64_t s, int j, bool bad) {
+  int fl = bad ? 1 : 0;
+  fl |= __shfl_xor(fl, 1);
+  fl |= __shfl_xor(fl, 2);
+  if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
+}
+
+// VAR != 0: timing-only ablations (wrong results; AMR_K2_VARIANT):
+//   1 = no main-body stores, 2 = no LO loads, 4 = no f loads
+template <int VAR>
+__global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams p, Iir f) {
+  const int lane = threadIdx.x;
+  const int j = lane & 3, sq = lane >> 2;
+  const int64_t w = blockIdx.x >> 1;
+  const int comp = blockIdx.x & 1;
+  const int64_t s = w * 16 + sq;
+  if (w * 16 >= buf.n_streams) return;          // wave-uniform
+  const int64_t n = p.n;
+  const int64_t n2 = (n + 1) >> 1;
+  const int pad = p.pad2;
+  const int qs = pad & 1;
+  const int64_t m2_pairs = (p.m2 + qs + 1) >> 1;
+  const int64_t g = s >> 6;
+  const double2* __restrict__ fsrc =
+      reinterpret_cast<const double2*>(buf.s2) + (size_t)((g * 2 + ((s >> 5) & 1)) * n2) * 32 + (s & 31);
+  const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;   // (lo_c, addend) at lo[2i]
+  const double* __restrict__ loc = buf.lo2 + comp * n;                               // lo_c alone
+  double* __restrict__ s3 = buf.s3;
+
+  double zi;
+  const Quad5 c = quad5_coef(f, j, zi);
+  bool bad = false;
+  float acc = __builtin_inff();
+  // numpy's (f + 0j) * lo: f*lo_c + addend (addend a signed zero)
+  auto X = [&](int64_t i) {
+    const double2 fp = fsrc[(size_t)(i >> 1) * 32];
+    const double2 l = lo[2 * i];
+    return ((i & 1) ? fp.y : fp.x) * l.x + l.y;
+  };
+
+  const double x0 = X(0), xl = X(n - 1);
+  bad |= __builtin_amdgcn_class(x0, kClsX);     // bb[0]: +0 allowed (judged by class)
+  const double e0 = 2.0 * x0 - X(pad);
+  bad |= __builtin_amdgcn_class(e0, kClsY);
+  double z = zi * e0;
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * x0 - X(pad - jj);
+    const double y = quad5_step(c, z, e);
+    acc = tiny_min3(acc, e, y);
+    s3[s3q_index(w, comp, m2_pairs, jj + qs, sq)] = y;
+  }
+  const int64_t nc = n / kLpQChunk;
+  const int64_t n_main = nc * kLpQChunk;
+  // the first kLpChunk samples hold bb[0] (full complex-multiply form, class-checked above)
+  const int64_t n_gen = n >= kLpChunk ? kLpChunk : n;
+  for (int64_t i = 0; i < n_gen; ++i) {
+    const double e = i == 0 ? x0 : X(i);
+    const double y = quad5_step(c, z, e);
+    acc = tiny_min3(acc, i == 0 ? y : e, y);
+    s3[s3q_index(w, comp, m2_pairs, pad + i + qs, sq)] = y;
+  }
+  constexpr int64_t kC0 = kLpChunk / kLpQChunk;   // chunks covered by the generic loop
+  if (nc > kC0) {
+    // main body: bb = f * lo_c (equal to f*lo_c + addend whenever it is not a
+    // zero, and a zero is flagged).  f and the LO multipliers arrive through
+    // register rings (f R chunks deep, LO R/2).  The LO is wave-uniform, but
+    // scalar loads would not do: SMEM returns out of order, so every use of
+    // one waits for all of them (lgkmcnt(0)), and the table falls out of L2
+    // under the streaming traffic.  Loads run up to R chunks past the
+    // stream's end into the plan's slack (api.cpp) instead of clamping: every
+    // instruction here costs a wave issue slot.
+    constexpr int CH = kLpQChunk, PP = CH / 2, R = VAR >= 10 ? VAR - 10 : kLpQRing, RL = R / 2;
+    static_assert(R % RL == 0, "the LO ring must divide the f ring");
+    double2 fr[R][PP];
+    double2 lr[RL][PP];                         // LO multipliers, wave-uniform (a pair per dwordx4)
+    const double2* __restrict__ fnext = fsrc + (size_t)kC0 * PP * 32;   // next chunk to load
+    const double2* __restrict__ lnext = reinterpret_cast<const double2*>(loc + kC0 * CH);
+    double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3q_index(w, comp, m2_pairs, pad + qs + kC0 * CH, sq) >> 1);
+    auto loadf = [&](double2 (&d)[PP]) {
+#pragma unroll
+      for (int k = 0; k < PP; ++k) d[k] = VAR == 4 ? make_double2(1e-3 * k + (double)(size_t)fnext, 2e-3) : fnext[k * 32];
+      fnext += PP * 32;
+    };
+    auto loadl = [&](double2 (&d)[PP]) {
+#pragma unroll
+      for (int k = 0; k < PP; ++k) d[k] = VAR == 2 ? make_double2(0.5 + 1e-3 * k + (double)(size_t)lnext, 0.25) : lnext[k];
+      lnext += PP;
+    };
+    auto run = [&](const double2 (&fv)[PP], const double2 (&lv)[PP]) {
+#pragma unroll
+      for (int k = 0; k < PP; ++k) {
+        const double e0v = fv[k].x * lv[k].x;
+        const double e1v = fv[k].y * lv[k].y;
+        const double y0 = quad5_step(c, z, e0v);
+        const double y1 = quad5_step(c, z, e1v);
+        acc = tiny_min3(acc, e0v, e1v);
+        acc = tiny_min3(acc, y0, y1);
+        if (VAR == 1) acc = tiny_min3(acc, y0 - y1, y1);
+        else dst[k * 16] = make_double2(y0, y1);
+      }
+      dst += PP * 16;
+    };
+    // ring slot u holds chunk cc+u (LO: slot u % RL); each slot is refilled
+    // right after it is consumed (f R chunks ahead, LO RL chunks ahead), so
+    // no control flow sits inside the loop.  Issue order matters: vmcnt
+    // retires in order, so slot 0 must be the oldest.
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      loadf(fr[u]);
+      if (u < RL) loadl(lr[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int64_t cc = kC0;
+    for (; cc + R <= nc; cc += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        run(fr[u], lr[u % RL]);
+        __builtin_amdgcn_sched_barrier(0);
+        loadf(fr[u]);
+        loadl(lr[u % RL]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (cc + u < nc) {
+        run(fr[u], lr[u % RL]);
+        if (u + RL < R) loadl(lr[u % RL]);     // LO for chunk cc+u+RL (still inside the tail)
+      }
+    }
+  }
+  for (int64_t i = n_main > n_gen ? n_main : n_gen; i < n; ++i) {
+    const double e = X(i);
+    const double y = quad5_step(c, z, e);
+    acc = tiny_min3(acc, e, y);
+    s3[s3q_index(w, comp, m2_pairs, pad + i + qs, sq)] = y;
+  }
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * xl - X(n - 2 - jj);
+    const double y = quad5_step(c, z, e);
+    acc = tiny_min3(acc, e, y);
+    s3[s3q_index(w, comp, m2_pairs, pad + n + jj + qs, sq)] = y;
+  }
+  bad |= !(acc >= kTinyHi) || !__builtin_isfinite(z);
+  quad_flag(buf, s, j, bad);
+}
+
+// K3q: SPS > 0 as K3 (static symbol offsets inside CH-sample chunks)
+template <int SPS>
+__global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int CH = SPS > 0 ? 20 : kLpChunk;
+  static_assert(SPS == 0 || CH % SPS == 0, "chunk must be a multiple of SPS");
+  const int lane = threadIdx.x;
+  const int j = lane & 3, sq = lane >> 2;
+  const int64_t w = blockIdx.x >> 1;
+  const int comp = blockIdx.x & 1;
+  const int64_t s = w * 16 + sq;
+  if (w * 16 >= buf.n_streams) return;
+  const int64_t n = p.n;
+  const int pad = p.pad2;
+  const int qs = pad & 1;
+  const int64_t m2 = p.m2;
+  const int64_t m2_pairs = (m2 + qs + 1) >> 1;
+  const double* __restrict__ s3 = buf.s3;
+  double* __restrict__ sym = buf.s1;
+  const int64_t S = p.n_sym;
+
+  double zi;
+  const Quad5 c = quad5_coef(f, j, zi);
+  float acc = __builtin_inff();
+  const double ylast = s3[s3q_index(w, comp, m2_pairs, m2 - 1 + qs, sq)];
+  double z = zi * ylast;
+  for (int64_t jj = m2 - 1; jj >= pad + n; --jj) {
+    const double y = quad5_step(c, z, s3[s3q_index(w, comp, m2_pairs, jj + qs, sq)]);
+    acc = tiny_min3(acc, y, y);
+  }
+
+  int64_t k = S - 1;
+  int64_t next_n = p.first + k * p.sps;
+  const size_t sym_base = sym_index(s, S, 0, comp);
+  auto on_output = [&](int64_t i, double y) {
+    if (i == next_n) {
+      sym[sym_base + (size_t)k * 64] = y;
+      --k;
+      next_n = k >= 0 ? next_n - p.sps : -1;
+    }
+  };
+  const int64_t nc = n / CH;
+  const int64_t n_lo = nc * CH;
+  for (int64_t i = n - 1; i >= n_lo; --i) {
+    const double y = quad5_step(c, z, s3[s3q_index(w, comp, m2_pairs, pad + i + qs, sq)]);
+    acc = tiny_min3(acc, y, y);
+    on_output(i, y);
+  }
+  if (nc > 0) {
+    // pointers walk down one chunk per run/load; loads run up to R chunks
+    // below the block into the plan's front slack (api.cpp) instead of
+    // clamping -- every instruction costs this wave an issue slot
+    constexpr int PP = CH / 2;
+    const double2* __restrict__ rnext = reinterpret_cast<const double2*>(s3) +
+                                        ((size_t)(w * 2 + comp) * m2_pairs + ((pad + qs + (nc - 1) * CH) >> 1)) * 16 + sq;
+    double* __restrict__ symp = sym + sym_base + (size_t)((nc - 1) * (SPS > 0 ? CH / SPS : 0)) * 64;
+    constexpr int R = kLpBRing;
+    double2 rr_[R][PP];
+    auto load = [&](double2 (&r)[PP]) {
+#pragma unroll
+      for (int kk = 0; kk < PP; ++kk) r[kk] = rnext[kk * 16];
+      rnext -= PP * 16;
+    };
+    auto run = [&](const double2 (&r)[PP], int64_t cc) {
+      if constexpr (SPS > 0) {
+#pragma unroll
+        for (int kk = PP - 1; kk >= 0; --kk) {
+          const double y1 = quad5_step(c, z, r[kk].y);
+          const double y0 = quad5_step(c, z, r[kk].x);
+          acc = tiny_min3(acc, y0, y1);
+          if ((2 * kk + 1) % SPS == SPS / 2) symp[((2 * kk + 1) / SPS) * 64] = y1;
+          if ((2 * kk) % SPS == SPS / 2) symp[((2 * kk) / SPS) * 64] = y0;
+        }
+        symp -= (CH / SPS) * 64;
+      } else {
+#pragma unroll
+        for (int kk = PP - 1; kk >= 0; --kk) {
+          const double y1 = quad5_step(c, z, r[kk].y);
+          on_output(cc * CH + 2 * kk + 1, y1);
+          const double y0 = quad5_step(c, z, r[kk].x);
+          on_output(cc * CH + 2 * kk, y0);
+          acc = tiny_min3(acc, y0, y1);
+        }
+      }
+    };
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      load(rr_[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    int64_t cc = nc - 1;
+    for (; cc >= R - 1; cc -= R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        run(rr_[u], cc - u);
+        __builtin_amdgcn_sched_barrier(0);
+        load(rr_[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (cc - u >= 0) run(rr_[u], cc - u);
+  }
+  for (int jj = pad - 1; jj >= 0; --jj) {
+    const double y = quad5_step(c, z, s3[s3q_index(w, comp, m2_pairs, jj + qs, sq)]);
+    acc = tiny_min3(acc, y, y);
+  }
+  quad_flag(buf, s, j, !(acc >= kTinyHi) || !__builtin_isfinite(z));
+}
+
+// ---------------------------------------------------------------------------
 // K3x: exact complex low-pass (scipy CDOUBLE_filt semantics) for flagged
 // streams only.  lane = stream; scratch reuses s3 as [group][j][64] double2;
 // writes its symbols into the same sym buffer K3 fills.
@@ -947,13 +1464,37 @@ static hipError_t launch_bp_quad(const PskBuffers& b, const PskParams& p, const 
   return hipGetLastError();
 }
 
-// AMR_BANDPASS_LANE=1 selects the lane-per-stream band-pass (A/B comparisons)
-static bool bandpass_lane_mode() {
-  static const bool v = [] { const char* e = getenv("AMR_BANDPASS_LANE"); return e && e[0] == '1'; }();
-  return v;
+template <typename T>
+static hipError_t launch_bp_row(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  const int64_t waves = (b.n_streams + kRowStreams - 1) / kRowStreams;
+  hipLaunchKernelGGL((k_bandpass_row<T>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, b, p, f);
+  return hipGetLastError();
 }
 
+// AMR_PSK_LAYOUT selects older lane layouts for A/B comparisons:
+//   "lane" = lane per stream (K1/K2/K3), "quad" = K1q + pair-split K2/K3;
+//   default = K1r + quad-split K2q/K3q
+static int psk_layout() {
+  static const int v = [] {
+    const char* e = getenv("AMR_PSK_LAYOUT");
+    if (!e) return 2;
+    if (e[0] == 'l') return 0;
+    if (e[0] == 'q') return 1;
+    return 2;
+  }();
+  return v;
+}
+static bool bandpass_lane_mode() { return psk_layout() == 0; }
+
 hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  if (f.nt == 9 && psk_layout() == 2) {
+    switch (b.dtype) {
+      case kF32: return launch_bp_row<float>(b, p, f, st);
+      case kF64: return launch_bp_row<double>(b, p, f, st);
+      case kI16: return launch_bp_row<int16_t>(b, p, f, st);
+    }
+    return hipErrorInvalidValue;
+  }
   if (f.nt == 9 && !bandpass_lane_mode()) {
     switch (b.dtype) {
       case kF32: return launch_bp_quad<float>(b, p, f, st);
@@ -978,6 +1519,19 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const
   if (e != hipSuccess) return e;
   const char* v = getenv("AMR_K2_VARIANT");
   const int var = v ? atoi(v) : 0;
+  if (psk_layout() == 2) {
+    const dim3 gq((unsigned)(2 * ((b.n_streams + 15) / 16))), bq(kWave);
+    switch (var) {
+      case 1: hipLaunchKernelGGL(k_lowpass_fwd_q<1>, gq, bq, 0, st, b, p, f); break;
+      case 2: hipLaunchKernelGGL(k_lowpass_fwd_q<2>, gq, bq, 0, st, b, p, f); break;
+      case 4: hipLaunchKernelGGL(k_lowpass_fwd_q<4>, gq, bq, 0, st, b, p, f); break;
+      case 14: hipLaunchKernelGGL(k_lowpass_fwd_q<14>, gq, bq, 0, st, b, p, f); break;
+      case 18: hipLaunchKernelGGL(k_lowpass_fwd_q<18>, gq, bq, 0, st, b, p, f); break;
+      case 12: hipLaunchKernelGGL(k_lowpass_fwd_q<12>, gq, bq, 0, st, b, p, f); break;
+      default: hipLaunchKernelGGL(k_lowpass_fwd_q<0>, gq, bq, 0, st, b, p, f); break;
+    }
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(4 * groups)), block(kWave);
   switch (var) {
     case 1: hipLaunchKernelGGL(k_lowpass_fwd<1>, grid, block, 0, st, b, p, f); break;
@@ -992,6 +1546,14 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const
 hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
+  if (psk_layout() == 2) {
+    const dim3 gq((unsigned)(2 * ((b.n_streams + 15) / 16))), bq(kWave);
+    if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd_q<10>), gq, bq, 0, st, b, p, f);
+    else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd_q<5>), gq, bq, 0, st, b, p, f);
+    else if (p.sps == 20 && p.first == 10) hipLaunchKernelGGL((k_lowpass_bwd_q<20>), gq, bq, 0, st, b, p, f);
+    else hipLaunchKernelGGL((k_lowpass_bwd_q<0>), gq, bq, 0, st, b, p, f);
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)(4 * groups)), block(kWave);
   if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd<10>), grid, block, 0, st, b, p, f);
   else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd<5>), grid, block, 0, st, b, p, f);
