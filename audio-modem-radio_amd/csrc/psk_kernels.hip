@@ -36,6 +36,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "amr_internal.h"
 
 namespace amr {
@@ -94,6 +96,7 @@ __device__ __forceinline__ size_t f_index(int64_t g, int64_t n2, int64_t i, int 
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector: SROA-friendly (HIP's uint4 is a struct)
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 constexpr int kTileBytes = 256;                 // bytes of one stream per input tile
 constexpr int kTilePitch = kTileBytes + 16;     // LDS row pitch: conflict-free ds_read_b128 per lane
@@ -453,7 +456,61 @@ __global__ __launch_bounds__(64) void k_bandpass_quad(PskBuffers buf, PskParams 
 // (4096 streams) the kernel is 1024 waves = one per SIMD
 // (tools/step_probe2.hip: 51.5 vs 76.3 cycles/sample for K1q).
 constexpr int kRowStreams = 4;                  // streams (DPP rows) per wave
-constexpr int kBpRing = 3;                      // K1r backward prefetch ring depth (32-sample chunks)
+constexpr int kBpRing = 8;                      // K1r backward LDS-DMA ring depth (32-sample chunks)
+
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
+// expcnt[6:4] = 7 and lgkmcnt[11:8] = 15 mean "don't wait")
+// -- as inline asm: the compiler's waitcnt pass does not know what the DMA
+// feeds and would drop a __builtin_amdgcn_s_waitcnt it considers redundant.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(%0)" : : "i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS-DMA (global_load_lds_dwordx4: each lane's 16 B to lds_dst + lane*16)
+// issued as inline asm, so that the compiler does not know a DMA is in
+// flight: it would make every LDS access it cannot prove disjoint from the
+// target wait vmcnt(0) (and always does at loop headers), draining the ring.
+// The caller waits for the data itself (vm_wait, counting every vector-memory
+// instruction issued after the DMA).  M0 is written and restored inside the
+// statement (recipe of cdna_hip_programming.md); "memory" keeps the compiler's
+// LDS accesses on their side of it.
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N-1>)
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for_up(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_up<N, I + 1>(f);
+  }
+}
+// f(integral_constant<int, N-1>), ..., f(integral_constant<int, 0>)
+template <int N, typename F>
+__device__ __forceinline__ void static_for_down(F&& f) {
+  if constexpr (N > 0) {
+    f(std::integral_constant<int, N - 1>{});
+    static_for_down<N - 1>(f);
+  }
+}
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void dma16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+// per-wave LDS of K1r's backward pass (the DMA ring is a separate __shared__
+// object so that the compiler's LDS-DMA tracking can tell the staging
+// accesses do not alias it)
+struct BwdStage {
+  uint8_t stage[1024];                          // output image of one chunk
+  uint8_t junk[2048];                           // writes of the non-writer lanes
+};
 
 __device__ __forceinline__ double row_bcast8(double v) {
   const long u = __builtin_bit_cast(long, v);
@@ -473,6 +530,20 @@ struct RowIir {
   double b0, cb, ca;
 };
 
+// Stores from a lane group that holds one value (a DPP row or quad after the
+// y broadcast) go out from ONE lane: every other lane's buffer offset is out
+// of range, so the hardware drops its write (no exec-mask juggling, no extra
+// VALU).  Letting all lanes write the same 16 B made each store instruction
+// 16 (row) or 4 (quad) duplicate write requests; measured on K1r's backward
+// pass: 5.8 -> 2.8 ms.  A raw buffer resource (stride 0) bounds-checks
+// voffset + the instruction offset against num_records; soffset is added
+// after the check.
+constexpr int kBufFlags = 0x00020000;           // gfx9 raw buffer dword3
+constexpr int kBufDrop = 0x7ff00000;            // offset that is always out of range
+__device__ __forceinline__ void store_lane(__amdgpu_buffer_rsrc_t rs, int voff, int soff, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, voff, soff, 0);
+}
+
 __device__ __forceinline__ double row_step(const RowIir& c, double& z, int& hk, double x) {
   const double t = z + c.b0 * x;
   const double y = row_bcast8(t);
@@ -489,8 +560,10 @@ __device__ __forceinline__ size_t row_pair_index(int64_t w, int64_t m_pairs, int
 template <typename T>
 __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams p, Iir f) {
   __shared__ __attribute__((aligned(16))) uint8_t tiles[4][2][kRowStreams][kTilePitch];
+  __shared__ __attribute__((aligned(16))) uint8_t bwd_ring[4][kBpRing][1024];   // s1 chunks (LDS-DMA)
+  __shared__ __attribute__((aligned(16))) BwdStage bwd_st[4];
   constexpr int TS = kTileBytes / (int)sizeof(T);
-  const int wv = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (buffer rsrc, LDS bases)
   const int lane = threadIdx.x & 63;
   const int r = lane >> 4, l = lane & 15;
   const int j = l & 7;                          // state owned (lanes 8-15; 0-7 mirror them)
@@ -525,37 +598,40 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
   }
   const int64_t n_tiles = n / TS;
   const int64_t n_main = n_tiles * TS;
+  // main-body stores: one writer lane per row (lane 8), see store_lane.  (An
+  // LDS staging image as in the backward pass measured slower here: this pass
+  // has no loads for the stores to compete with.)
+  const __amdgpu_buffer_rsrc_t srs =
+      __builtin_amdgcn_make_buffer_rsrc(s1 + (size_t)w * m1_pairs * kRowStreams * 2, 0, (int)(m1_pairs * 64), kBufFlags);
+  const int svo = l == 8 ? r * 16 : kBufDrop;
   if (n_tiles > 0) {
     // one tile = 4 stream rows x 256 B: one 16-B load per lane
     const int cb = l * 16;
     const uint8_t* rowp = reinterpret_cast<const uint8_t*>(x) + cb;
     v4u rv = *reinterpret_cast<const v4u*>(rowp);
     *reinterpret_cast<v4u*>(&tile[0][r][cb]) = rv;
+    // this lane's 16 B of each flushed image: s1 pair (image base + lane/4), row lane&3
+    uint8_t* sdst = reinterpret_cast<uint8_t*>(s1) + (((size_t)w * m1_pairs + ((pad + qs) >> 1)) * kRowStreams + lane) * 16;
     for (int64_t t = 0; t < n_tiles; ++t) {
       const int cur = (int)(t & 1);
       const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
       rv = *reinterpret_cast<const v4u*>(rowp + tn * kTileBytes);
       __builtin_amdgcn_sched_barrier(0);
-      const int64_t q0 = pad + qs + t * TS;
-      double2* __restrict__ dst =
-          reinterpret_cast<double2*>(s1) + (size_t)(w * m1_pairs + (q0 >> 1)) * kRowStreams + r;
+      const int sso = (int)(((pad + qs + t * TS) >> 1) * 64);
       constexpr int PER = 16 / (int)sizeof(T);
       // the row's whole tile into registers at once: one LDS round trip per
       // tile instead of one per 16 B (the reads are broadcasts, 4 addresses)
       v4u xv[TS / PER];
 #pragma unroll
       for (int k = 0; k < TS / PER; ++k) xv[k] = *reinterpret_cast<const v4u*>(&tile[cur][r][k * 16]);
-#pragma unroll
-      for (int k = 0; k < TS; k += PER) {
+      static_for_up<TS / 2>([&](auto jc) {
+        constexpr int jp = decltype(jc)::value;             // pair of the tile
         T xs[PER];
-        __builtin_memcpy(xs, &xv[k / PER], 16);
-#pragma unroll
-        for (int u = 0; u < PER; u += 2) {
-          const double y0 = row_step(c, z, hk, In<T>::cvt(xs[u]));
-          const double y1 = row_step(c, z, hk, In<T>::cvt(xs[u + 1]));
-          dst[((k + u) >> 1) * kRowStreams] = make_double2(y0, y1);   // all 16 lanes: same value
-        }
-      }
+        __builtin_memcpy(xs, &xv[(2 * jp) / PER], 16);
+        const double y0 = row_step(c, z, hk, In<T>::cvt(xs[(2 * jp) % PER]));
+        const double y1 = row_step(c, z, hk, In<T>::cvt(xs[(2 * jp) % PER + 1]));
+        store_lane(srs, svo + jp * 64, sso, make_double2(y0, y1));
+      });
       __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<v4u*>(&tile[cur ^ 1][r][cb]) = rv;
     }
@@ -588,49 +664,91 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
     fo[f_index(sgrp, n2, i, sig)] = y;
   }
   if (nb > 0) {
-    // pointers walk down one chunk per run/load (loads may run R chunks below
-    // the block, into the plan's front slack, instead of clamping)
+    // Main body, chunks of 32 samples walked downwards.  Every memory
+    // instruction moves 1 KiB of distinct data: the TA spends the same cycles
+    // on a wave instruction whatever its lanes hold, and with one load + one
+    // store per sample pair from all 64 lanes it was busy 93 % of the kernel.
+    //   in : one LDS-DMA (global_load_lds_dwordx4) per chunk = 16 pairs x 4
+    //        rows of s1, into a ring of kBpRing chunks; each pair is then a
+    //        broadcast ds_read_b128 (4 addresses per wave)
+    //   out: each pair's (y0, y1) goes to an LDS staging image from lane 8 of
+    //        its row (the other lanes write a junk area: no exec masking);
+    //        per chunk one ds_read_b128 + one global store of the image
+    // LDS-DMA completion is tracked by vmcnt only, and the compiler adds no
+    // wait between the DMA and the ds_reads of its data: vm_wait() below.
     constexpr int PP = kBwdChunk / 2;
-    const double2* __restrict__ rnext = reinterpret_cast<const double2*>(s1) +
-                                        ((size_t)w * m1_pairs + ((pad + qs + (nb - 1) * kBwdChunk) >> 1)) * kRowStreams + r;
-    double2* __restrict__ dst = reinterpret_cast<double2*>(fo) + (size_t)((sgrp * 2 + (sig >> 5)) * n2) * 32 +
-                                (sig & 31) + (size_t)((nb - 1) * PP) * 32;
+    static_assert(PP * kRowStreams * 16 == 1024, "one DMA wave-instruction per chunk");
     constexpr int R = kBpRing;
-    double2 rr_[R][PP];
-    auto load = [&](double2 (&rr)[PP]) {
-#pragma unroll
-      for (int k = 0; k < PP; ++k) rr[k] = rnext[k * kRowStreams];
-      rnext -= PP * kRowStreams;
+    uint8_t* const ring = bwd_ring[wv][0];
+    uint8_t* const stage = bwd_st[wv].stage;
+    // junk slots chosen so that the 8 lanes of each LDS cycle group write 8
+    // different 16-B bank groups: lane l of row r -> bank group (l + r) mod 8,
+    // the writer (l = 8) included
+    uint8_t* const wr_base = l == 8 ? stage + r * 16 : bwd_st[wv].junk + (lane + r) * 16;
+    // this lane's 16 B of each chunk: s1 pair (chunk base + lane/4), row lane&3
+    const uint8_t* gsrc = reinterpret_cast<const uint8_t*>(s1) +
+                          (((size_t)w * m1_pairs + ((pad + qs + (nb - 1) * kBwdChunk) >> 1)) * kRowStreams + lane) * 16;
+    // ... and of each chunk's output image: f pair (chunk base + lane/4), stream lane&3
+    const int64_t hgrp = (w * kRowStreams) >> 5;
+    uint8_t* fdst = reinterpret_cast<uint8_t*>(fo) +
+                    (((size_t)(hgrp * n2) + (size_t)((nb - 1) * PP) + (lane >> 2)) * 32 +
+                     (size_t)(((w * kRowStreams) & 31) + (lane & 3))) * 16;
+    auto dma = [&](int slot) {
+      dma16(gsrc, lds_addr(ring + slot * 1024));
+      gsrc -= 1024;
     };
-    auto run = [&](const double2 (&rr)[PP]) {
+    auto run = [&](int slot) {
+      const uint8_t* rs = ring + slot * 1024 + r * 16;
+      v4u xv[PP];                               // the whole chunk up front: one LDS round trip
 #pragma unroll
-      for (int k = PP - 1; k >= 0; --k) {
-        const double y1 = row_step(c, z, hk, rr[k].y);
-        const double y0 = row_step(c, z, hk, rr[k].x);
-        dst[k * 32] = make_double2(y0, y1);
+      for (int k = 0; k < PP; ++k) xv[k] = *reinterpret_cast<const v4u*>(rs + k * 64);
+      static_for_down<PP>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const double2 xx = __builtin_bit_cast(double2, xv[k]);
+        const double y1 = row_step(c, z, hk, xx.y);
+        const double y0 = row_step(c, z, hk, xx.x);
+        *reinterpret_cast<v4u*>(wr_base + k * 64) = __builtin_bit_cast(v4u, make_double2(y0, y1));
+      });
+    };
+    // the image is read back right after its chunk and stored one chunk later,
+    // when the read has long returned (LDS keeps the read ahead of the next
+    // chunk's writes)
+    v4u img;
+    auto flush = [&](auto storec) {
+      if constexpr (decltype(storec)::value) {
+        *reinterpret_cast<v4u*>(fdst) = img;
+        fdst -= (size_t)PP * 32 * 16;
       }
-      dst -= PP * 32;
+      img = *reinterpret_cast<const v4u*>(stage + lane * 16);
     };
-    // ring slot u holds chunk cc-u, refilled R chunks further down right
-    // after it is consumed; slot 0 is issued first (vmcnt retires in order)
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
-      load(rr_[u]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    for (int u = 0; u < R; ++u) dma(u);
     int64_t cc = nb - 1;
-    for (; cc >= R - 1; cc -= R) {
+    // first R chunks: fewer ops are younger than their DMA (no stores yet);
+    // the very first chunk has no image to store yet
+    static_for_up<R>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (cc - u < 0) return;
+      vm_wait<R - 1>();
+      run(u);
+      dma(u);
+      flush(std::integral_constant<bool, (u > 0)>{});
+    });
+    cc -= R;
+    // steady state: each DMA has 2R-1 younger vector-memory ops when its
+    // chunk comes up (R-1 DMAs + R stores)
+    for (; cc >= 0; cc -= R) {
 #pragma unroll
       for (int u = 0; u < R; ++u) {
-        run(rr_[u]);
-        __builtin_amdgcn_sched_barrier(0);
-        load(rr_[u]);
-        __builtin_amdgcn_sched_barrier(0);
+        if (cc - u < 0) break;
+        vm_wait<2 * R - 1>();
+        run(u);
+        dma(u);
+        flush(std::true_type{});
       }
     }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (cc - u >= 0) run(rr_[u]);
+    *reinterpret_cast<v4u*>(fdst) = img;        // the last chunk's image
+    vm_wait<0>();                               // no DMA may land after the wave ends
   }
 }
 
@@ -993,7 +1111,7 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p,
 // v_min3_f32 runs in inline asm so the compiler adds no NaN canonicalisation.
 constexpr int kQuadShift = 0xF9;                // quad_perm [1,2,3,3]
 constexpr int kLpQChunk = 8;                    // K2q main-body chunk (samples)
-constexpr int kLpQRing = 8;                     // K2q f prefetch ring depth (chunks)
+constexpr int kLpQRing = 8;                     // K2q f prefetch ring depth (8-sample chunks)
 constexpr int kLpBRing = 5;                     // K3q prefetch ring depth (chunks of 20/16 samples)
 typedef __attribute__((address_space(4))) const double CDouble;   // constant AS: uniform loads -> SMEM
 constexpr float kTinyHi = 0x1p-126f;            // FLT_MIN
@@ -1040,14 +1158,15 @@ __device__ __forceinline__ void quad_flag(PskBuffers& buf, int64_t s, int j, boo
   if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
 }
 
-// VAR != 0: timing-only ablations (wrong results; AMR_K2_VARIANT):
-//   1 = no main-body stores, 2 = no LO loads, 4 = no f loads
-template <int VAR>
 __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
   const int j = lane & 3, sq = lane >> 2;
-  const int64_t w = blockIdx.x >> 1;
-  const int comp = blockIdx.x & 1;
+  // blocks b and b+8 land on the same XCD (blocks are dealt to the 8 XCDs
+  // round-robin) and run the re and im waves of the same 16 streams, so the
+  // second read of their f rows is an L2 hit instead of a second HBM read
+  const int64_t bx = blockIdx.x, kx = bx >> 3;
+  const int64_t w = (kx >> 1) * 8 + (bx & 7);
+  const int comp = (int)(kx & 1);
   const int64_t s = w * 16 + sq;
   if (w * 16 >= buf.n_streams) return;          // wave-uniform
   const int64_t n = p.n;
@@ -1103,22 +1222,27 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
     // one waits for all of them (lgkmcnt(0)), and the table falls out of L2
     // under the streaming traffic.  Loads run up to R chunks past the
     // stream's end into the plan's slack (api.cpp) instead of clamping: every
-    // instruction here costs a wave issue slot.
-    constexpr int CH = kLpQChunk, PP = CH / 2, R = VAR >= 10 ? VAR - 10 : kLpQRing, RL = R / 2;
+    // instruction here costs a wave issue slot.  (An LDS-DMA ring as in K1r's
+    // backward pass measured slower here: 4.4 vs 3.5 ms.)
+    constexpr int CH = kLpQChunk, PP = CH / 2, R = kLpQRing, RL = R / 2;
     static_assert(R % RL == 0, "the LO ring must divide the f ring");
     double2 fr[R][PP];
     double2 lr[RL][PP];                         // LO multipliers, wave-uniform (a pair per dwordx4)
     const double2* __restrict__ fnext = fsrc + (size_t)kC0 * PP * 32;   // next chunk to load
     const double2* __restrict__ lnext = reinterpret_cast<const double2*>(loc + kC0 * CH);
-    double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3q_index(w, comp, m2_pairs, pad + qs + kC0 * CH, sq) >> 1);
+    // stores: one writer lane per quad (j == 0), see store_lane
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        s3 + (size_t)(w * 2 + comp) * m2_pairs * 32, 0, (int)(m2_pairs * 256), kBufFlags);
+    const int dvo = j == 0 ? sq * 16 : kBufDrop;
+    int dso = (int)(((pad + qs + kC0 * CH) >> 1) * 256);
     auto loadf = [&](double2 (&d)[PP]) {
 #pragma unroll
-      for (int k = 0; k < PP; ++k) d[k] = VAR == 4 ? make_double2(1e-3 * k + (double)(size_t)fnext, 2e-3) : fnext[k * 32];
+      for (int k = 0; k < PP; ++k) d[k] = fnext[k * 32];
       fnext += PP * 32;
     };
     auto loadl = [&](double2 (&d)[PP]) {
 #pragma unroll
-      for (int k = 0; k < PP; ++k) d[k] = VAR == 2 ? make_double2(0.5 + 1e-3 * k + (double)(size_t)lnext, 0.25) : lnext[k];
+      for (int k = 0; k < PP; ++k) d[k] = lnext[k];
       lnext += PP;
     };
     auto run = [&](const double2 (&fv)[PP], const double2 (&lv)[PP]) {
@@ -1130,10 +1254,9 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
         const double y1 = quad5_step(c, z, e1v);
         acc = tiny_min3(acc, e0v, e1v);
         acc = tiny_min3(acc, y0, y1);
-        if (VAR == 1) acc = tiny_min3(acc, y0 - y1, y1);
-        else dst[k * 16] = make_double2(y0, y1);
+        store_lane(drs, dvo + k * 256, dso, make_double2(y0, y1));
       }
-      dst += PP * 16;
+      dso += PP * 256;
     };
     // ring slot u holds chunk cc+u (LO: slot u % RL); each slot is refilled
     // right after it is consumed (f R chunks ahead, LO RL chunks ahead), so
@@ -1234,7 +1357,11 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams 
     constexpr int PP = CH / 2;
     const double2* __restrict__ rnext = reinterpret_cast<const double2*>(s3) +
                                         ((size_t)(w * 2 + comp) * m2_pairs + ((pad + qs + (nc - 1) * CH) >> 1)) * 16 + sq;
-    double* __restrict__ symp = sym + sym_base + (size_t)((nc - 1) * (SPS > 0 ? CH / SPS : 0)) * 64;
+    // symbol stores: one writer lane per quad (j == 0), see store_lane
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        sym + (size_t)(w >> 1) * S * 64, 0, (int)(S * 512), kBufFlags);   // (s >> 5 == w >> 1, uniform)
+    const int yvo = j == 0 ? (int)(((s & 31) * 2 + comp) * 8) : kBufDrop;
+    int yso = (int)((nc - 1) * (SPS > 0 ? CH / SPS : 0) * 512);
     constexpr int R = kLpBRing;
     double2 rr_[R][PP];
     auto load = [&](double2 (&r)[PP]) {
@@ -1249,10 +1376,12 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams 
           const double y1 = quad5_step(c, z, r[kk].y);
           const double y0 = quad5_step(c, z, r[kk].x);
           acc = tiny_min3(acc, y0, y1);
-          if ((2 * kk + 1) % SPS == SPS / 2) symp[((2 * kk + 1) / SPS) * 64] = y1;
-          if ((2 * kk) % SPS == SPS / 2) symp[((2 * kk) / SPS) * 64] = y0;
+          if ((2 * kk + 1) % SPS == SPS / 2)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y1), yrs, yvo + ((2 * kk + 1) / SPS) * 512, yso, 0);
+          if ((2 * kk) % SPS == SPS / 2)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y0), yrs, yvo + ((2 * kk) / SPS) * 512, yso, 0);
         }
-        symp -= (CH / SPS) * 64;
+        yso -= (CH / SPS) * 512;
       } else {
 #pragma unroll
         for (int kk = PP - 1; kk >= 0; --kk) {
@@ -1520,16 +1649,9 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const
   const char* v = getenv("AMR_K2_VARIANT");
   const int var = v ? atoi(v) : 0;
   if (psk_layout() == 2) {
-    const dim3 gq((unsigned)(2 * ((b.n_streams + 15) / 16))), bq(kWave);
-    switch (var) {
-      case 1: hipLaunchKernelGGL(k_lowpass_fwd_q<1>, gq, bq, 0, st, b, p, f); break;
-      case 2: hipLaunchKernelGGL(k_lowpass_fwd_q<2>, gq, bq, 0, st, b, p, f); break;
-      case 4: hipLaunchKernelGGL(k_lowpass_fwd_q<4>, gq, bq, 0, st, b, p, f); break;
-      case 14: hipLaunchKernelGGL(k_lowpass_fwd_q<14>, gq, bq, 0, st, b, p, f); break;
-      case 18: hipLaunchKernelGGL(k_lowpass_fwd_q<18>, gq, bq, 0, st, b, p, f); break;
-      case 12: hipLaunchKernelGGL(k_lowpass_fwd_q<12>, gq, bq, 0, st, b, p, f); break;
-      default: hipLaunchKernelGGL(k_lowpass_fwd_q<0>, gq, bq, 0, st, b, p, f); break;
-    }
+    // a multiple of 16 blocks: the XCD pairing in k_lowpass_fwd_q is a bijection
+    const dim3 gq((unsigned)((2 * ((b.n_streams + 15) / 16) + 15) / 16 * 16)), bq(kWave);
+    hipLaunchKernelGGL(k_lowpass_fwd_q, gq, bq, 0, st, b, p, f);
     return hipGetLastError();
   }
   const dim3 grid((unsigned)(4 * groups)), block(kWave);
