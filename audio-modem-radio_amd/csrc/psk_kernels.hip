@@ -598,26 +598,27 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
   }
   const int64_t n_tiles = n / TS;
   const int64_t n_main = n_tiles * TS;
-  // main-body stores: one writer lane per row (lane 8), see store_lane.  (An
-  // LDS staging image as in the backward pass measured slower here: this pass
-  // has no loads for the stores to compete with.)
-  const __amdgpu_buffer_rsrc_t srs =
-      __builtin_amdgcn_make_buffer_rsrc(s1 + (size_t)w * m1_pairs * kRowStreams * 2, 0, (int)(m1_pairs * 64), kBufFlags);
-  const int svo = l == 8 ? r * 16 : kBufDrop;
+  // main-body stores as in the backward pass: each pair's (y0, y1) into the
+  // wave's LDS staging image from lane 8 of its row (conflict-free junk slots
+  // for the others), read back every 16 pairs and stored as one 1-KiB
+  // instruction 16 pairs later
+  uint8_t* const stage = bwd_st[wv].stage;
+  uint8_t* const wr_base = l == 8 ? stage + r * 16 : bwd_st[wv].junk + (lane + r) * 16;
   if (n_tiles > 0) {
     // one tile = 4 stream rows x 256 B: one 16-B load per lane
     const int cb = l * 16;
     const uint8_t* rowp = reinterpret_cast<const uint8_t*>(x) + cb;
     v4u rv = *reinterpret_cast<const v4u*>(rowp);
     *reinterpret_cast<v4u*>(&tile[0][r][cb]) = rv;
-    // this lane's 16 B of each flushed image: s1 pair (image base + lane/4), row lane&3
+    // this lane's 16 B of each image: s1 pair (image base + lane/4), row lane&3
     uint8_t* sdst = reinterpret_cast<uint8_t*>(s1) + (((size_t)w * m1_pairs + ((pad + qs) >> 1)) * kRowStreams + lane) * 16;
-    for (int64_t t = 0; t < n_tiles; ++t) {
+    v4u img;
+    auto tile_body = [&](int64_t t, auto firstc) {
+      constexpr bool FIRST = decltype(firstc)::value;
       const int cur = (int)(t & 1);
       const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
       rv = *reinterpret_cast<const v4u*>(rowp + tn * kTileBytes);
       __builtin_amdgcn_sched_barrier(0);
-      const int sso = (int)(((pad + qs + t * TS) >> 1) * 64);
       constexpr int PER = 16 / (int)sizeof(T);
       // the row's whole tile into registers at once: one LDS round trip per
       // tile instead of one per 16 B (the reads are broadcasts, 4 addresses)
@@ -630,11 +631,22 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
         __builtin_memcpy(xs, &xv[(2 * jp) / PER], 16);
         const double y0 = row_step(c, z, hk, In<T>::cvt(xs[(2 * jp) % PER]));
         const double y1 = row_step(c, z, hk, In<T>::cvt(xs[(2 * jp) % PER + 1]));
-        store_lane(srs, svo + jp * 64, sso, make_double2(y0, y1));
+        *reinterpret_cast<v4u*>(wr_base + (jp % 16) * 64) = __builtin_bit_cast(v4u, make_double2(y0, y1));
+        if constexpr (jp % 16 == 15) {
+          if constexpr (!(FIRST && jp == 15)) {
+            *reinterpret_cast<v4u*>(sdst) = img;
+            sdst += 1024;
+          }
+          img = *reinterpret_cast<const v4u*>(stage + lane * 16);
+        }
       });
       __builtin_amdgcn_sched_barrier(0);
       *reinterpret_cast<v4u*>(&tile[cur ^ 1][r][cb]) = rv;
-    }
+    };
+    static_assert(TS / 2 % 16 == 0, "a tile holds whole staging images");
+    tile_body(0, std::true_type{});
+    for (int64_t t = 1; t < n_tiles; ++t) tile_body(t, std::false_type{});
+    *reinterpret_cast<v4u*>(sdst) = img;        // the last image
   }
   for (int64_t i = n_main; i < n; ++i) {
     const double y = row_step(c, z, hk, In<T>::cvt(x[i]));
