@@ -530,19 +530,6 @@ struct RowIir {
   double b0, cb, ca;
 };
 
-// Stores from a lane group that holds one value (a DPP row or quad after the
-// y broadcast) go out from ONE lane: every other lane's buffer offset is out
-// of range, so the hardware drops its write (no exec-mask juggling, no extra
-// VALU).  Letting all lanes write the same 16 B made each store instruction
-// 16 (row) or 4 (quad) duplicate write requests; measured on K1r's backward
-// pass: 5.8 -> 2.8 ms.  A raw buffer resource (stride 0) bounds-checks
-// voffset + the instruction offset against num_records; soffset is added
-// after the check.
-constexpr int kBufFlags = 0x00020000;           // gfx9 raw buffer dword3
-constexpr int kBufDrop = 0x7ff00000;            // offset that is always out of range
-__device__ __forceinline__ void store_lane(__amdgpu_buffer_rsrc_t rs, int voff, int soff, double2 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, voff, soff, 0);
-}
 
 __device__ __forceinline__ double row_step(const RowIir& c, double& z, int& hk, double x) {
   const double t = z + c.b0 * x;
@@ -1242,11 +1229,7 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
     double2 lr[RL][PP];                         // LO multipliers, wave-uniform (a pair per dwordx4)
     const double2* __restrict__ fnext = fsrc + (size_t)kC0 * PP * 32;   // next chunk to load
     const double2* __restrict__ lnext = reinterpret_cast<const double2*>(loc + kC0 * CH);
-    // stores: one writer lane per quad (j == 0), see store_lane
-    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-        s3 + (size_t)(w * 2 + comp) * m2_pairs * 32, 0, (int)(m2_pairs * 256), kBufFlags);
-    const int dvo = j == 0 ? sq * 16 : kBufDrop;
-    int dso = (int)(((pad + qs + kC0 * CH) >> 1) * 256);
+    double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3q_index(w, comp, m2_pairs, pad + qs + kC0 * CH, sq) >> 1);
     auto loadf = [&](double2 (&d)[PP]) {
 #pragma unroll
       for (int k = 0; k < PP; ++k) d[k] = fnext[k * 32];
@@ -1266,9 +1249,9 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
         const double y1 = quad5_step(c, z, e1v);
         acc = tiny_min3(acc, e0v, e1v);
         acc = tiny_min3(acc, y0, y1);
-        store_lane(drs, dvo + k * 256, dso, make_double2(y0, y1));
+        dst[k * 16] = make_double2(y0, y1);     // all 4 lanes of the quad: the same 16 B
       }
-      dso += PP * 256;
+      dst += PP * 16;
     };
     // ring slot u holds chunk cc+u (LO: slot u % RL); each slot is refilled
     // right after it is consumed (f R chunks ahead, LO RL chunks ahead), so
@@ -1369,11 +1352,7 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams 
     constexpr int PP = CH / 2;
     const double2* __restrict__ rnext = reinterpret_cast<const double2*>(s3) +
                                         ((size_t)(w * 2 + comp) * m2_pairs + ((pad + qs + (nc - 1) * CH) >> 1)) * 16 + sq;
-    // symbol stores: one writer lane per quad (j == 0), see store_lane
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        sym + (size_t)(w >> 1) * S * 64, 0, (int)(S * 512), kBufFlags);   // (s >> 5 == w >> 1, uniform)
-    const int yvo = j == 0 ? (int)(((s & 31) * 2 + comp) * 8) : kBufDrop;
-    int yso = (int)((nc - 1) * (SPS > 0 ? CH / SPS : 0) * 512);
+    double* __restrict__ symp = sym + sym_base + (size_t)((nc - 1) * (SPS > 0 ? CH / SPS : 0)) * 64;
     constexpr int R = kLpBRing;
     double2 rr_[R][PP];
     auto load = [&](double2 (&r)[PP]) {
@@ -1388,12 +1367,10 @@ __global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams 
           const double y1 = quad5_step(c, z, r[kk].y);
           const double y0 = quad5_step(c, z, r[kk].x);
           acc = tiny_min3(acc, y0, y1);
-          if ((2 * kk + 1) % SPS == SPS / 2)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y1), yrs, yvo + ((2 * kk + 1) / SPS) * 512, yso, 0);
-          if ((2 * kk) % SPS == SPS / 2)
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, y0), yrs, yvo + ((2 * kk) / SPS) * 512, yso, 0);
+          if ((2 * kk + 1) % SPS == SPS / 2) symp[((2 * kk + 1) / SPS) * 64] = y1;
+          if ((2 * kk) % SPS == SPS / 2) symp[((2 * kk) / SPS) * 64] = y0;
         }
-        yso -= (CH / SPS) * 512;
+        symp -= (CH / SPS) * 64;
       } else {
 #pragma unroll
         for (int kk = PP - 1; kk >= 0; --kk) {
@@ -1628,7 +1605,8 @@ static int psk_layout() {
 static bool bandpass_lane_mode() { return psk_layout() == 0; }
 
 hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  if (f.nt == 9 && psk_layout() == 2) {
+  static const bool bp_quad = [] { const char* e = getenv("AMR_BP_QUAD"); return e && e[0] == '1'; }();
+  if (f.nt == 9 && psk_layout() == 2 && !bp_quad) {
     switch (b.dtype) {
       case kF32: return launch_bp_row<float>(b, p, f, st);
       case kF64: return launch_bp_row<double>(b, p, f, st);

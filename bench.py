@@ -298,7 +298,10 @@ def main():
             cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
                    "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through {how}, "
                              f"{cdt:.2f} s wall"}
-            bad = sum(1 for j, i in enumerate(idx) if out[i, :ln[i]].tobytes() != couts[j])
+            bad_idx = [int(i) for j, i in enumerate(idx) if out[i, :ln[i]].tobytes() != couts[j]]
+            bad = len(bad_idx)
+            if bad:
+                log(f"[rank {rank}] streams differing from the oracle: {bad_idx[:32]}{' ...' if bad > 32 else ''}")
             parity = f"{len(idx) - bad}/{len(idx)} streams bit-exact vs oracle"
         if fsk:
             metric = "FSK demod Msymbols/s (batch), FSK9600 96kHz mark/space 12k/24k"

@@ -89,11 +89,13 @@ def test_int16_pcm_path_equals_float64_reference(golden):
     assert outs[0].hex() == [c for c in manifest["cases"] if c["id"] == "qpsk9600_wav"][0]["out"]
 
 
-@pytest.mark.parametrize("kind,baud,B,N", [("qpsk", 9600, 4096, 96000), ("qpsk", 19200, 257, 96000),
+@pytest.mark.parametrize("kind,baud,B,N", [("qpsk", 9600, 4096, 96000), ("qpsk", 9600, 8192, 96000),
+                                           ("qpsk", 19200, 257, 96000),
                                            ("bpsk", 1200, 130, 48000), ("qpsk", 2400, 65, 30001)])
 def test_batch_vs_oracle(kind, baud, B, N):
-    """Seeded batches up to the BASELINE config-2 size, every stream checked
-    against the oracle (bit-exact bytes and sync index)."""
+    """Seeded batches up to the BASELINE config-2 size (and the 8192-stream
+    single launch of configs 4/5 on one GPU), every stream checked against the
+    oracle (bit-exact bytes and sync index)."""
     import _amr
     import synth
     from oracle import oracle
