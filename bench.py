@@ -257,8 +257,9 @@ def main():
     fp64_achieved = fp64_ops.get(dom, 0) / (kavg[dom] / 1e3) / 1e12
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
-    if (args.workload in ("qpsk9600", "fsk9600") and (B, N, int(baud)) == ((16384 if fsk else 4096), 96000, 9600)
-            and os.path.exists(pmc_file)):
+    # the PMC file was recorded at each workload's default size on one GPU
+    pmc_cfg = {"qpsk9600": (4096, 9600), "fsk9600": (16384, 9600), "ofdm8": (8192, 9600), "psk8fec": (8192, 19200)}
+    if ((B, int(baud)) == pmc_cfg[args.workload] and N == 96000 and world == 1 and os.path.exists(pmc_file)):
         with open(pmc_file) as f:
             pk = json.load(f).get(args.workload, {}).get("slots", {}).get(dom, {})
         if "hbm_bytes_per_launch" in pk:
