@@ -12,27 +12,31 @@
 // The oracle (oracle/amr_oracle.c) states the same arithmetic on the CPU.
 //
 // Pipeline for one batch (one kernel per stage, all streams in flight):
-//   K1 k_bandpass      lane = stream: band-pass filtfilt.  Forward pass reads
-//                      the caller's stream-major samples through a coalesced
-//                      LDS transpose tile and writes s1; the backward pass
-//                      streams s1 back (register prefetch ring) and writes the
-//                      real filtered signal f to s2.
-//   K2 k_lowpass_fwd   wave = (32 streams, re|im), lane pair = one recurrence
-//                      (2-lane state split): LO mixer (numpy's complex
-//                      multiply) fused into the low-pass forward pass -> s3
-//   K3 k_lowpass_bwd   same lanes: low-pass backward pass; the baseband at
-//                      each symbol centre goes to the symbol buffer
-//   K4a k_slice        thread = (stream, output word): differential product,
-//                      QPSK/BPSK slicer, bit packing -> words (fully parallel)
-//   K3x k_lowpass_exact lane = stream: the complex low-pass with scipy's full
-//                      signed-zero semantics, only for streams K2/K3 flagged
+//   K1r k_bandpass_row   16-lane DPP row = stream (lane 8+j owns state j):
+//                        band-pass filtfilt.  Forward pass reads the caller's
+//                        stream-major samples through an LDS tile and writes
+//                        s1 through an LDS staging image; the backward pass
+//                        streams s1 back through an LDS-DMA ring and writes
+//                        the real filtered signal f to s2 the same way.
+//   K2q k_lowpass_fwd_q  lane quad = one component of one stream (lane j owns
+//                        state j), wave = 16 streams x (re|im): LO mixer
+//                        (numpy's complex multiply) fused into the low-pass
+//                        forward pass -> s3
+//   K3q k_lowpass_bwd_q  same lanes: low-pass backward pass; the baseband at
+//                        each symbol centre goes to the symbol buffer
+//   K4a k_slice          thread = (stream, output word): differential product,
+//                        QPSK/BPSK slicer, bit packing -> words (fully parallel)
+//   K3x k_lowpass_exact  lane = stream: the complex low-pass with scipy's full
+//                        signed-zero semantics, only for streams K2q/K3q flagged
 //   (K4b sync + pack lives in util_kernels.hip)
+// The older layouts (K1q quad / K1 lane per stream band-pass, K2/K3 pair
+// low-pass) stay selectable with AMR_PSK_LAYOUT=quad|lane for A/B runs.
 //
-// Every wave runs alone on its SIMD (the batch of 4096 streams is only
-// 64-128 waves), so each kernel is bound by its per-sample instruction stream;
+// At the benchmark batch (4096 streams) every wave runs alone on its SIMD, so
+// each kernel is bound by its per-sample instruction stream;
 // the memory side is arranged so that no load is waited on before it has had
-// a whole chunk of compute to land (tools/fp64_probe.hip measured the
-// register-only band-pass step at 126 cycles/sample).
+// many chunks of compute to land and every memory instruction carries as much
+// distinct data as the layout allows.
 #include <math.h>
 #include <stdlib.h>
 
