@@ -27,6 +27,12 @@ DTYPE_F32, DTYPE_F64, DTYPE_I16 = 0, 1, 2
 PSK_QPSK, PSK_BPSK = 0, 1
 T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec"]
 TF_NAMES = ["bandpass", "hilbert", "decide"]
+# amr_frame_rec (include/amr.h), 64 bytes
+FRAME_SHORT, FRAME_NONAME, FRAME_NOMETA, FRAME_BADLEN, FRAME_INCOMPLETE, FRAME_CRC_BAD, FRAME_OK = range(7)
+FRAME_REC = np.dtype([("start", "<i8"), ("name_start", "<i8"), ("payload_start", "<i8"), ("status", "<i4"),
+                      ("name_len", "<i4"), ("part", "<u4"), ("total", "<u4"), ("fsize", "<u4"), ("fcrc", "<u4"),
+                      ("dlen", "<u4"), ("pcrc", "<u4"), ("calc_crc", "<u4"), ("reserved", "<u4")])
+assert FRAME_REC.itemsize == 64
 DTYPES = {np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64, np.dtype(np.int16): DTYPE_I16}
 
 # every symbol include/amr.h declares (tests/test_abi.py checks the export table)
@@ -39,9 +45,28 @@ EXPORTS = [
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
-    "amr_fec_decode_host", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
+    "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
     "amr_comm_synchronize",
 ]
+
+
+def frame_parse(raws, max_cands: int = 64):
+    """Batched decoder.parse_fbp_stream_enhanced scan (decoder.py:142-208) on
+    the GPU: for each bytes object, (n_candidates, records[:min(n, max_cands)])
+    with the reference's per-candidate verdict (FRAME_*) and header fields."""
+    require_gpu()
+    n = len(raws)
+    if n == 0:
+        return []
+    lens = np.array([len(r) for r in raws], np.int64)
+    stride = max(1, int(lens.max()))
+    buf = np.zeros((n, stride), np.uint8)
+    for i, r in enumerate(raws):
+        buf[i, :len(r)] = np.frombuffer(r, np.uint8)
+    cnt = np.zeros(n, np.int32)
+    recs = np.zeros((n, max_cands), FRAME_REC)
+    check(lib().amr_frame_parse_host(ptr(buf), stride, ptr(lens), n, max_cands, ptr(cnt), recs.ctypes.data))
+    return [(int(cnt[i]), recs[i, :min(int(cnt[i]), max_cands)]) for i in range(n)]
 
 
 class AmrError(RuntimeError):
@@ -103,6 +128,8 @@ def lib():
             "amr_fft_c2c_host": (I32, [P, P, I64, I64, I32, I32]),
             "amr_hilbert_host": (I32, [P, P, I64, I64, I32]),
             "amr_fec_decode_host": (I32, [P, I64, P, I64, P, I64, P, P]),
+            "amr_frame_parse_host": (I32, [P, I64, P, I64, I64, P, P]),
+            "amr_frame_parse_device": (I32, [P, P, I64, P, I64, I64, P, P]),
             "amr_comm_unique_id": (I32, [P]),
             "amr_comm_create": (I32, [P, P, I32, I32, I32]),
             "amr_comm_destroy": (I32, [P]),

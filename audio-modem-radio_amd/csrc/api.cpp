@@ -25,6 +25,8 @@ hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*
                             hipStream_t);
 hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, uint8_t*, int64_t, int64_t*,
                              int32_t*, const uint32_t*, const uint32_t*, hipStream_t);
+hipError_t launch_frame_parse(const uint8_t*, int64_t, const int64_t*, int64_t, int64_t, int32_t*, amr_frame_rec*,
+                              const uint32_t*, const uint32_t*, hipStream_t);
 }  // namespace amr
 
 using namespace amr;
@@ -566,6 +568,66 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
   for (void* p : {(void*)d_in, (void*)d_out, (void*)d_in_len, (void*)d_out_len, (void*)d_crc})
     if (p) (void)hipFree(p);
   if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_fec_decode_host: ") + hipGetErrorString(e));
+  return AMR_OK;
+}
+
+// ---- FBP frame parse (decoder.py:142-208) ------------------------------------
+int amr_frame_parse_device(amr_psk_plan* plan, const uint8_t* d_in, int64_t in_stride, const int64_t* d_in_len,
+                           int64_t n, int64_t max_cands, int32_t* d_n_cands, amr_frame_rec* d_recs) {
+  if (n < 0 || max_cands < 1 || in_stride < 0 || (n && (!d_in || !d_in_len || !d_n_cands || !d_recs)))
+    return fail(AMR_E_INVALID, "amr_frame_parse_device: bad argument");
+  if (n == 0) return AMR_OK;
+  int dev = 0;
+  hipStream_t st = nullptr;
+  if (plan) {
+    dev = plan->device;
+    st = plan->stream;
+    HIP_TRY(hipSetDevice(dev));
+  } else {
+    HIP_TRY(hipGetDevice(&dev));
+  }
+  const uint32_t *tab = nullptr, *x2n = nullptr;
+  int rc = device_crc(dev, &tab, &x2n);
+  if (rc) return rc;
+  HIP_TRY(launch_frame_parse(d_in, in_stride, d_in_len, n, max_cands, d_n_cands, d_recs, tab, x2n, st));
+  return AMR_OK;
+}
+
+int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in_len, int64_t n, int64_t max_cands,
+                         int32_t* n_cands, amr_frame_rec* recs) {
+  if (n < 0 || max_cands < 1 || (n && (!in || !in_len || !n_cands || !recs)))
+    return fail(AMR_E_INVALID, "amr_frame_parse_host: bad argument");
+  if (n == 0) return AMR_OK;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  const uint32_t *tab = nullptr, *x2n = nullptr;
+  int rc = device_crc(dev, &tab, &x2n);
+  if (rc) return rc;
+  int64_t maxlen = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (in_len[i] < 0 || in_len[i] > in_stride) return fail(AMR_E_INVALID, "in_len out of range");
+    maxlen = in_len[i] > maxlen ? in_len[i] : maxlen;
+  }
+  uint8_t* d_in = nullptr;
+  int64_t* d_in_len = nullptr;
+  int32_t* d_cnt = nullptr;
+  amr_frame_rec* d_recs = nullptr;
+  const int64_t stride = maxlen > 0 ? maxlen : 1;
+  hipError_t e = hipMalloc(&d_in, (size_t)(n * stride));
+  if (e == hipSuccess) e = hipMalloc(&d_in_len, (size_t)n * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_cnt, (size_t)n * 4);
+  if (e == hipSuccess) e = hipMalloc(&d_recs, (size_t)(n * max_cands) * sizeof(amr_frame_rec));
+  if (e == hipSuccess && maxlen > 0)
+    e = hipMemcpy2D(d_in, (size_t)stride, in, (size_t)in_stride, (size_t)maxlen, (size_t)n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_frame_parse(d_in, stride, d_in_len, n, max_cands, d_cnt, d_recs, tab, x2n, 0);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(n_cands, d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess)
+    e = hipMemcpy(recs, d_recs, (size_t)(n * max_cands) * sizeof(amr_frame_rec), hipMemcpyDeviceToHost);
+  for (void* p : {(void*)d_in, (void*)d_in_len, (void*)d_cnt, (void*)d_recs})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_frame_parse_host: ") + hipGetErrorString(e));
   return AMR_OK;
 }
 

@@ -7,7 +7,8 @@ error behaviour; the demodulation itself runs on the MI355X via modem.py.
 
   decode_wav_file            decoder.py:380-389
   decode_from_buffer         decoder.py:417-464   (+ decode_from_buffer_batch)
-  parse_fbp_stream_enhanced  decoder.py:142-208
+  parse_fbp_stream_enhanced  decoder.py:142-208   (+ parse_fbp_stream_enhanced_batch:
+                             the scan and payload CRCs on the GPU, k_frame_parse)
   smart_decompress           decoder.py:210-243
   find_frame_start           decoder.py:470-478
   get_assembly_status / get_reception_stats / clear_reception_stats
@@ -93,6 +94,37 @@ def parse_fbp_stream_enhanced(raw: bytes) -> list:
     return parsed_files
 
 
+def parse_fbp_stream_enhanced_batch(raws, max_cands: int = 64) -> list:
+    """parse_fbp_stream_enhanced over a batch of decoded streams, the scan on
+    the GPU (k_frame_parse: magic search, the reference's checks, payload
+    CRC32); the same frames and log lines per stream as the host version.  A
+    stream with more than max_cands magics is parsed on the host instead."""
+    import _amr
+    out = []
+    for raw, (n, recs) in zip(raws, _amr.frame_parse(raws, max_cands)):
+        if n > max_cands:
+            out.append(parse_fbp_stream_enhanced(raw))
+            continue
+        print(f"Encontrados {n} candidatos a cabeçalho.")
+        parsed = []
+        for r in recs:
+            st = int(r["status"])
+            if st < _amr.FRAME_INCOMPLETE:       # short / no name / no meta / bad length: silent
+                continue
+            ns, nl = int(r["name_start"]), int(r["name_len"])
+            fname = raw[ns: ns + nl].decode('utf-8', 'ignore')
+            if st == _amr.FRAME_INCOMPLETE:
+                print(f"Dados incompletos para {fname}")
+            elif st == _amr.FRAME_OK:
+                ps = int(r["payload_start"])
+                print(f"✅ CRC VÁLIDO: {fname} (Parte {int(r['part']) + 1}/{int(r['total'])})")
+                parsed.append({'name': fname, 'data': raw[ps: ps + int(r["dlen"])], 'final_crc': int(r["fcrc"])})
+            else:
+                print(f"❌ Erro de CRC para {fname}")
+        out.append(parsed)
+    return out
+
+
 def smart_decompress(compressed_data: bytes) -> bytes:
     """decoder.py:210-243."""
     import lzma
@@ -165,8 +197,9 @@ def _demod_bytes(data, mode: str, symbol_rate):
         return modem.qpsk_demodulate(data, baud=symbol_rate)
 
 
-def _save_frames(raw_bytes: bytes) -> list:
-    frames = parse_fbp_stream_enhanced(raw_bytes)
+def _save_frames(raw_bytes: bytes, frames=None) -> list:
+    if frames is None:
+        frames = parse_fbp_stream_enhanced(raw_bytes)
     saved = []
     for frame in frames:
         try:
@@ -211,7 +244,13 @@ def decode_from_buffer_batch(data: np.ndarray, mode: str, symbol_rate: int) -> l
         print(f"Erro crítico na demodulação: {e}")
         traceback.print_exc()
         return [[] for _ in range(len(data))]
-    return [_save_frames(r) for r in raws]
+    try:
+        framesets = parse_fbp_stream_enhanced_batch(raws)
+    except Exception as e:
+        print(f"Erro crítico na demodulação: {e}")
+        traceback.print_exc()
+        return [[] for _ in range(len(data))]
+    return [_save_frames(r, fr) for r, fr in zip(raws, framesets)]
 
 
 def get_assembly_status():

@@ -31,6 +31,8 @@
  *   amr_fsk_envelopes_host  the envelopes |hilbert(filtfilt(.))| modem.py:308-309
  *   amr_hilbert_host        scipy.signal.hilbert as modem.py:309 calls it
  *   amr_fec_decode_host     fec.ReedSolomonFEC.decode  fec.py:34-69, batched
+ *   amr_frame_parse_host    decoder.parse_fbp_stream_enhanced  decoder.py:142-208,
+ *                           batched (magic search, checks, payload CRC32)
  *   amr_allgather           the gather of decoded bytes across GPUs (RCCL)
  *
  * Status: every function returns AMR_OK (0) or a negative AMR_E_* code;
@@ -189,6 +191,38 @@ int amr_hilbert_host(const double *x, double *analytic, int64_t n, int64_t batch
  * (the reference only prints "Aviso: CRC ..." on mismatch). */
 int amr_fec_decode_host(const uint8_t *in, int64_t in_stride, const int64_t *in_len, int64_t n,
                         uint8_t *out, int64_t out_stride, int64_t *out_len, int32_t *crc_ok);
+
+/* ---- FBP frame parse (decoder.py:142-208, parse_fbp_stream_enhanced) --------
+ * For every stream's decoded bytes (in: [n][in_stride], in_len[n]): every
+ * b'FBPC' occurrence in increasing order, run through the reference's checks
+ * in its order, and the CRC32 (binascii.crc32) of the payload of those that
+ * pass them.  n_cands[s] = occurrences found (may exceed max_cands: records
+ * are kept for the first min(n_cands, max_cands, 256); a caller seeing more
+ * parses that stream itself).  recs: [n][max_cands].  The host turns records
+ * into the reference's list of {'name', 'data', 'final_crc'} and log lines. */
+#define AMR_FRAME_SHORT 0          /* start + 30 > len(raw)            decoder.py:165 */
+#define AMR_FRAME_NONAME 1         /* name_len == 0                     decoder.py:169 */
+#define AMR_FRAME_NOMETA 2         /* meta_start + 24 > len(raw)        decoder.py:177 */
+#define AMR_FRAME_BADLEN 3         /* dlen > 50_000_000 or dlen == 0    decoder.py:182 */
+#define AMR_FRAME_INCOMPLETE 4     /* payload past the end: "Dados incompletos"  :185-187 */
+#define AMR_FRAME_CRC_BAD 5        /* "Erro de CRC"                     decoder.py:197-198 */
+#define AMR_FRAME_OK 6             /* CRC valid: appended               decoder.py:190-196 */
+#define AMR_FRAME_PENDING_CRC 7    /* internal */
+typedef struct amr_frame_rec {
+  int64_t start;                   /* index of the magic */
+  int64_t name_start;              /* start + 5 */
+  int64_t payload_start;           /* meta_start + 24 */
+  int32_t status;                  /* AMR_FRAME_* */
+  int32_t name_len;                /* raw[start + 4] */
+  uint32_t part, total, fsize, fcrc, dlen, pcrc;   /* '<IIIIII' at meta_start */
+  uint32_t calc_crc;               /* crc32(payload) when computed */
+  uint32_t reserved;
+} amr_frame_rec;                   /* 64 bytes */
+int amr_frame_parse_host(const uint8_t *in, int64_t in_stride, const int64_t *in_len, int64_t n,
+                         int64_t max_cands, int32_t *n_cands, amr_frame_rec *recs);
+/* device pointers, enqueued on the plan's stream (plan may be NULL: the null stream) */
+int amr_frame_parse_device(amr_psk_plan *plan, const uint8_t *d_in, int64_t in_stride, const int64_t *d_in_len,
+                           int64_t n, int64_t max_cands, int32_t *d_n_cands, amr_frame_rec *d_recs);
 
 /* ---- multi-GPU: RCCL over xGMI ----------------------------------------------- */
 #define AMR_UNIQUE_ID_BYTES 128

@@ -111,3 +111,19 @@ def test_fsk_error_contract(built_lib, golden):
             with pytest.raises(ValueError) as ei:
                 call_case(modem, case, inputs[case["id"]])
             assert str(ei.value) == case["emsg"], case["id"]
+
+
+def test_frame_parse_argument_checks(built_lib):
+    """Bad arguments are refused before any device work (amr_frame_parse_*)."""
+    import _amr
+    L = _amr.lib()
+    cnt = np.zeros(2, np.int32)
+    lens = np.array([4, 4], np.int64)
+    buf = np.zeros((2, 4), np.uint8)
+    recs = np.zeros((2, 4), _amr.FRAME_REC)
+    assert L.amr_frame_parse_host(None, 4, _amr.ptr(lens), 2, 4, _amr.ptr(cnt), recs.ctypes.data) == _amr.AMR_E_INVALID
+    assert L.amr_frame_parse_host(_amr.ptr(buf), 4, _amr.ptr(lens), 2, 0, _amr.ptr(cnt), recs.ctypes.data) == _amr.AMR_E_INVALID
+    assert L.amr_frame_parse_device(None, None, 4, None, 2, 4, None, None) == _amr.AMR_E_INVALID
+    assert L.amr_frame_parse_host(None, 0, None, 0, 1, None, None) == _amr.AMR_OK          # empty batch
+    with pytest.raises(_amr.AmrError):
+        _amr.frame_parse([b"FBPC"])                                                         # no GPU here
