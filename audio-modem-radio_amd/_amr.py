@@ -46,8 +46,51 @@ EXPORTS = [
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
-    "amr_comm_synchronize",
+    "amr_comm_synchronize", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
 ]
+
+TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
+TX_MODES = {"bpsk": TX_BPSK, "qpsk": TX_QPSK, "fsk": TX_FSK}
+
+
+def tx_samples(mode: int, n_bytes: int, baud, samp_rate) -> int:
+    """len() of the reference modulator's output for an n_bytes payload."""
+    n = lib().amr_tx_samples(mode, n_bytes, float(baud), float(samp_rate))
+    if n < 0:
+        _raise_tx(int(n))
+    return int(n)
+
+
+def _raise_tx(rc: int):
+    msg = lib().amr_last_error().decode("utf-8", "replace")
+    if msg.startswith("could not broadcast"):
+        raise ValueError(msg)                      # numpy's error, modem.py:58-61 / 181-183
+    if msg == "float division by zero":
+        raise ZeroDivisionError(msg)
+    raise AmrError(rc, msg)
+
+
+def modulate(mode: int, datas, baud, f0, f1=0.0, samp_rate=96000, n_out=None, pcm=False):
+    """Batched transmit side on the GPU (amr_modulate_host): the reference
+    modulator's float32 waveform of every payload in `datas` (modem.py:28-65,
+    138-186, 270-295), cut / zero-padded to n_out samples (default: the
+    longest natural length).  pcm=True also returns wav_from_array's int16."""
+    require_gpu()
+    n = len(datas)
+    lens = np.array([len(d) for d in datas], np.int64)
+    if n_out is None:
+        n_out = max((tx_samples(mode, int(x), baud, samp_rate) for x in lens), default=0)
+    stride = max(1, int(lens.max()) if n else 1)
+    buf = np.zeros((max(n, 1), stride), np.uint8)
+    for i, d in enumerate(datas):
+        buf[i, :len(d)] = np.frombuffer(bytes(d), np.uint8)
+    out = np.zeros((n, n_out), np.float32)
+    pc = np.zeros((n, n_out), np.int16) if pcm else None
+    rc = lib().amr_modulate_host(mode, float(baud), float(f0), float(f1), float(samp_rate), ptr(buf), stride,
+                                 ptr(lens), n, ptr(out), n_out, n_out, ptr(pc) if pcm else None, n_out)
+    if rc != AMR_OK:
+        _raise_tx(rc)
+    return (out, pc) if pcm else out
 
 
 def frame_parse(raws, max_cands: int = 64):
@@ -135,6 +178,10 @@ def lib():
             "amr_comm_destroy": (I32, [P]),
             "amr_allgather": (I32, [P, P, P, I64, P]),
             "amr_comm_synchronize": (I32, [P]),
+            "amr_tx_samples": (I64, [I32, I64, D, D]),
+            "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
+            "amr_modulate_host": (I32, [I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64]),
+            "amr_modulate_device": (I32, [P, I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64, P, I64]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -18,7 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libamr.so")
-SOURCES = ["psk_kernels.hip", "util_kernels.hip", "fft_kernels.hip", "fsk_kernels.hip", "frame_kernels.hip", "api.cpp",
+SOURCES = ["psk_kernels.hip", "util_kernels.hip", "fft_kernels.hip", "fsk_kernels.hip", "frame_kernels.hip", "tx_kernels.hip",
+           "api.cpp", "tx_api.cpp",
            "fsk_api.cpp"]
 HEADERS = ["amr_internal.h", "fft.h", "api_common.h", os.path.join(INCLUDE, "amr.h")]
 ARCH = os.environ.get("AMR_OFFLOAD_ARCH", "gfx950")

@@ -80,4 +80,16 @@ struct FskIir {            // [tone][tap], tone 0 = mark
   double zi[2][8];
 };
 
+// Transmit side (tx_kernels.hip / tx_api.cpp): scalars of one modulate call.
+struct TxParams {
+  int mode;              // AMR_TX_*
+  int64_t sps;           // samples per symbol (per bit for FSK)
+  int64_t ramp;          // int(sps * 0.1)          (PSK envelope)
+  int64_t n_out;         // samples written per stream
+  int64_t sym_stride;    // phases kept per stream = ceil(n_out / sps)
+  double c0, c1;         // 2*pi*f0, 2*pi*f1
+  double fs;             // sample rate
+  double inc0, inc1;     // CPFSK phase increments (bit 1 = f0 = mark, bit 0 = f1 = space)
+};
+
 }  // namespace amr

@@ -149,6 +149,20 @@ struct amr_comm {
   int device = 0;
 };
 
+namespace amr {
+int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
+  *st = nullptr;
+  if (plan) {
+    *dev = plan->device;
+    *st = plan->stream;
+    HIP_TRY(hipSetDevice(*dev));
+  } else {
+    HIP_TRY(hipGetDevice(dev));
+  }
+  return AMR_OK;
+}
+}  // namespace amr
+
 extern "C" {
 
 int amr_abi_version(void) { return AMR_ABI_VERSION; }

@@ -10,6 +10,8 @@
 namespace amr {
 int fail(int code, const std::string& msg);   // sets amr_last_error(), returns code
 int64_t dtype_size(int dtype);                // bytes per sample, 0 = unknown
+// device + stream a *_device call on `plan` runs on (plan NULL: current device, null stream)
+int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st);
 }  // namespace amr
 
 #define HIP_TRY(expr)                                                                              \

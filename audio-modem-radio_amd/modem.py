@@ -13,8 +13,11 @@ Receive side (the hot path, bit-exact with the reference):
 plus batched forms (*_demodulate_batch) that take a [B, N] array and return
 one bytes object per stream -- the form the GPU is built for.
 
-Transmit side (SURVEY §8f "next", host numpy, not bit-exact-claimed):
-  qpsk_modulate / bpsk_modulate / fsk_modulate / wav_from_array and aliases.
+Transmit side (on the GPU: tx_kernels.hip):
+  qpsk_modulate modem.py:138-186   bpsk_modulate modem.py:28-65
+  fsk_modulate  modem.py:270-295   (+ aliases) and modulate_batch; the float32
+  samples equal the reference's up to the last-ulp sin difference the tests bound.
+  wav_from_array modem.py:360-368 (host WAV writer).
 """
 from __future__ import annotations
 
@@ -182,27 +185,36 @@ def feld_hell_demodulate(s, b, c, sr=96000):
 
 
 # ---------------------------------------------------------------------------
-# transmit side (host numpy; SURVEY §8f "next")
-def _check_ramp(baud, samp_rate):
-    sps = int(samp_rate / baud)
-    if int(sps * 0.1) == 0:
-        # the reference's envelope[-0:] = linspace(1, 0, 0) broadcast failure (modem.py:61,183)
-        raise ValueError(f"could not broadcast input array from shape (0,) into shape ({sps},)")
-
-
+# transmit side on the GPU (tx_kernels.hip): the same float32
+# samples as the reference's modulators; wav_from_array stays a host WAV writer.
 def bpsk_modulate(data_bytes: bytes, baud=1200, carrier=3000.0, samp_rate=96000) -> np.ndarray:
-    _check_ramp(baud, samp_rate)
-    return synth.bpsk_waveform(data_bytes, baud, carrier, samp_rate)
+    """modem.py:28-65 (DBPSK)."""
+    return _amr.modulate(_amr.TX_BPSK, [bytes(data_bytes)], baud, carrier, 0.0, samp_rate)[0]
 
 
 def qpsk_modulate(data_bytes: bytes, baud=1200, carrier=3000.0, samp_rate=96000) -> np.ndarray:
-    _check_ramp(baud, samp_rate)
-    return synth.qpsk_waveform(data_bytes, baud, carrier, samp_rate)
+    """modem.py:138-186 (DQPSK)."""
+    return _amr.modulate(_amr.TX_QPSK, [bytes(data_bytes)], baud, carrier, 0.0, samp_rate)[0]
 
 
 def fsk_modulate(data_bytes: bytes, baud=1200, mark_freq=1200.0, space_freq=2200.0, samp_rate=96000) -> np.ndarray:
-    return synth.fsk_waveform(data_bytes, baud, mark_freq, space_freq, samp_rate)
+    """modem.py:270-295 (CPFSK)."""
+    return _amr.modulate(_amr.TX_FSK, [bytes(data_bytes)], baud, mark_freq, space_freq, samp_rate)[0]
+
+
+def modulate_batch(kind: str, datas, baud=1200, f0=None, f1=None, samp_rate=96000, n_out=None, pcm=False):
+    """Batched modulators: [B, n_out] float32 (each row == <kind>_modulate(datas[b])
+    cut / zero-padded to n_out; default the longest), plus wav_from_array's
+    int16 samples when pcm=True.  kind: 'bpsk' | 'qpsk' (f0 = carrier) or
+    'fsk' (f0 = mark_freq, f1 = space_freq)."""
+    mode = _amr.TX_MODES[kind]
+    if f0 is None:
+        f0 = 1200.0 if kind == "fsk" else 3000.0
+    if f1 is None:
+        f1 = 2200.0 if kind == "fsk" else 0.0
+    return _amr.modulate(mode, [bytes(d) for d in datas], baud, f0, f1, samp_rate, n_out, pcm)
 
 
 def wav_from_array(arr, sr=96000):
+    """modem.py:360-368: 16-bit mono WAV of int16(arr * 32767)."""
     return synth.wav_bytes(arr, sr)

@@ -33,6 +33,9 @@
  *   amr_fec_decode_host     fec.ReedSolomonFEC.decode  fec.py:34-69, batched
  *   amr_frame_parse_host    decoder.parse_fbp_stream_enhanced  decoder.py:142-208,
  *                           batched (magic search, checks, payload CRC32)
+ *   amr_modulate_host       modem.bpsk_modulate / qpsk_modulate / fsk_modulate
+ *                           (modem.py:28-65, 138-186, 270-295) + the int16 of
+ *                           wav_from_array (modem.py:360-368), batched
  *   amr_allgather           the gather of decoded bytes across GPUs (RCCL)
  *
  * Status: every function returns AMR_OK (0) or a negative AMR_E_* code;
@@ -223,6 +226,32 @@ int amr_frame_parse_host(const uint8_t *in, int64_t in_stride, const int64_t *in
 /* device pointers, enqueued on the plan's stream (plan may be NULL: the null stream) */
 int amr_frame_parse_device(amr_psk_plan *plan, const uint8_t *d_in, int64_t in_stride, const int64_t *d_in_len,
                            int64_t n, int64_t max_cands, int32_t *d_n_cands, amr_frame_rec *d_recs);
+
+/* ---- transmit side (modem.py:28-65, 138-186, 270-295, 360-368) ------------
+ * The reference's modulators for a batch of payloads: data [n][data_stride]
+ * bytes, n_bytes[n].  out [n][out_stride] float32: each stream's waveform
+ * (bpsk_modulate / qpsk_modulate / fsk_modulate, sample for sample) cut or
+ * zero-padded to n_out samples; pcm (optional, may be NULL) the same samples
+ * as modem.wav_from_array writes them, int16(out * 32767).
+ * f0 = carrier (PSK) or mark_freq (FSK); f1 = space_freq (FSK only).
+ * A PSK symbol of 1..9 samples is the reference's numpy broadcast ValueError
+ * (its 10 % ramp is empty, modem.py:58-61 / 181-183): AMR_E_INVALID with the
+ * reference's message in amr_last_error(). */
+#define AMR_TX_BPSK 0              /* bpsk_modulate  modem.py:28-65   */
+#define AMR_TX_QPSK 1              /* qpsk_modulate  modem.py:138-186 */
+#define AMR_TX_FSK 2               /* fsk_modulate   modem.py:270-295 */
+/* natural waveform length of an n_bytes payload (the reference's len(out)), or < 0 */
+int64_t amr_tx_samples(int mode, int64_t n_bytes, double baud, double sample_rate);
+/* device scratch bytes amr_modulate_device needs for this shape */
+int64_t amr_tx_work_bytes(int mode, double baud, double sample_rate, int64_t n_streams, int64_t n_out);
+int amr_modulate_host(int mode, double baud, double f0, double f1, double sample_rate, const uint8_t *data,
+                      int64_t data_stride, const int64_t *n_bytes, int64_t n, float *out, int64_t out_stride,
+                      int64_t n_out, int16_t *pcm, int64_t pcm_stride);
+/* device pointers, enqueued on the plan's stream (plan may be NULL: the null stream) */
+int amr_modulate_device(amr_psk_plan *plan, int mode, double baud, double f0, double f1, double sample_rate,
+                        const uint8_t *d_data, int64_t data_stride, const int64_t *d_n_bytes, int64_t n,
+                        float *d_out, int64_t out_stride, int64_t n_out, int16_t *d_pcm, int64_t pcm_stride,
+                        void *d_work, int64_t work_bytes);
 
 /* ---- multi-GPU: RCCL over xGMI ----------------------------------------------- */
 #define AMR_UNIQUE_ID_BYTES 128

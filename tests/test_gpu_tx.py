@@ -1,0 +1,119 @@
+"""GPU transmit side (tx_kernels.hip) against the reference's
+own modulator outputs (tests/golden/tx.npz) and the oracle's restatement.
+
+Tolerance: every phase, table and envelope value is the reference's IEEE
+double op in its order, so the only difference left is sin() itself (ocml
+on the GPU, libm on the host; both within 1 ulp in float64).  That reaches
+the float32 output only when the double lands within ~1 ulp64 of a float32
+rounding boundary (p ~ 2^-28 per sample).  The bound asserted: at most 1 ulp
+(float32) per sample, on at most 1e-6 of the samples (+1), and the int16 WAV
+samples within 1 where the float32 differs, equal elsewhere."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(built_lib):
+    import _amr
+    if _amr.device_count() < 1:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
+
+
+@pytest.fixture(scope="module")
+def tx():
+    with open(os.path.join(G, "tx_manifest.json")) as f:
+        return json.load(f)["cases"], np.load(os.path.join(G, "tx.npz"))
+
+
+def ulps(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    def ordered(x):
+        i = x.astype(np.float32).view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7FFFFFFF), i)
+    return np.abs(ordered(a) - ordered(b))
+
+
+def assert_close(got, want, pcm_got=None, pcm_want=None, what=""):
+    assert got.shape == want.shape and got.dtype == np.float32, what
+    u = ulps(got, want)
+    bad = np.count_nonzero(u)
+    assert u.max(initial=0) <= 1, f"{what}: {u.max()} ulp"
+    assert bad <= 1 + got.size * 1e-6, f"{what}: {bad} of {got.size} samples differ"
+    if pcm_got is not None:
+        dp = np.abs(pcm_got.astype(np.int32) - pcm_want.astype(np.int32))
+        assert dp.max(initial=0) <= 1 and np.all(dp[u == 0] == 0), what
+    return bad
+
+
+def test_modulators_match_reference_fixtures(tx):
+    import modem
+    cases, d = tx
+    total_bad = 0
+    for c in cases:
+        fn = getattr(modem, c["fn"])
+        data = d[c["id"] + ".in"].tobytes()
+        if c["status"] == "err":
+            with pytest.raises(ValueError) as e:
+                fn(data, **c["params"])
+            assert str(e.value) == c["emsg"], c["id"]
+            continue
+        y = fn(data, **c["params"])
+        r = d[c["id"] + ".out"]
+        total_bad += assert_close(y, r, what=c["id"])
+        assert modem.wav_from_array(y)[:44] == d[c["id"] + ".wav"].tobytes()[:44]
+    print(f"float32 samples differing from the reference: {total_bad}")
+
+
+def test_batch_pcm_and_padding(tx):
+    """One ragged batch per mode: rows == the single-stream outputs, cut or
+    zero-padded to n_out, and the int16 PCM == wav_from_array's samples."""
+    import modem
+    cases, d = tx
+    for kind, fn in (("qpsk", "qpsk_modulate"), ("bpsk", "bpsk_modulate"), ("fsk", "fsk_modulate")):
+        sel = [c for c in cases if c["fn"] == fn and c["status"] == "ok"
+               and c["params"].get("samp_rate", 96000) == 96000
+               and c["params"].get("baud", 1200) == 1200 and "carrier" not in c["params"]
+               and "mark_freq" not in c["params"]]
+        assert sel, kind
+        datas = [d[c["id"] + ".in"].tobytes() for c in sel] + [b"", b"\x00" * 7]
+        n_out = max(c["n"] for c in sel) - 1001                 # cuts the longest, pads the rest
+        out, pcm = modem.modulate_batch(kind, datas, baud=1200, n_out=n_out, pcm=True)
+        assert out.shape == (len(datas), n_out) and pcm.dtype == np.int16
+        for i, data in enumerate(datas):
+            ref = getattr(oracle, fn)(data)
+            want = np.zeros(n_out, np.float32)
+            m = min(n_out, ref.size)
+            want[:m] = ref[:m]
+            assert_close(out[i], want, pcm[i], oracle.wav_pcm(want), what=f"{kind}[{i}]")
+            assert np.array_equal(pcm[i], oracle.wav_pcm(out[i]))
+
+
+@pytest.mark.parametrize("kind,baud,f0,f1", [("qpsk", 9600, 3000.0, 0.0), ("bpsk", 9600, 3000.0, 0.0),
+                                             ("fsk", 9600, 12000.0, 24000.0)])
+def test_large_batch_against_oracle(kind, baud, f0, f1):
+    """256 distinct 1-second streams of the benchmark shapes (96 000 samples)."""
+    import modem
+    import synth
+    rng = np.random.default_rng(5)
+    n_bytes = {"qpsk": 2390, "bpsk": 1190, "fsk": 1196}[kind]
+    datas = [synth.random_frame(rng, n_bytes - 40 - 8 * (i % 3), name=f"s{i}.bin") for i in range(256)]
+    out = modem.modulate_batch(kind, datas, baud=baud, f0=f0, f1=f1, n_out=96000)
+    bad = 0
+    for i in range(0, 256, 17):           # the per-symbol oracle is slow: every 17th stream
+        ref = {"qpsk": lambda x: oracle.qpsk_modulate(x, baud, f0), "bpsk": lambda x: oracle.bpsk_modulate(x, baud, f0),
+               "fsk": lambda x: oracle.fsk_modulate(x, baud, f0, f1)}[kind](datas[i])
+        want = np.zeros(96000, np.float32)
+        want[:min(96000, ref.size)] = ref[:96000]
+        bad += assert_close(out[i], want, what=f"{kind}[{i}]")
+    # every stream against the vectorised host synthesiser (itself pinned to tx.npz)
+    wave = {"qpsk": lambda x: synth.qpsk_waveform(x, baud, f0), "bpsk": lambda x: synth.bpsk_waveform(x, baud, f0),
+            "fsk": lambda x: synth.fsk_waveform(x, baud, f0, f1)}[kind]
+    want = np.stack([synth.fit(wave(x), 96000) for x in datas])
+    assert_close(out, want, what=kind)
