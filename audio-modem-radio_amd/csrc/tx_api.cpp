@@ -65,7 +65,7 @@ int tx_setup(int mode, double baud, double f0, double f1, double fs, int64_t n_o
       return fail(AMR_E_INVALID, "could not broadcast input array from shape (0,) into shape (" +
                                      std::to_string(p->sps) + ",)");
   }
-  p->sym_stride = p->sps > 0 ? (n_out + p->sps - 1) / p->sps : 0;
+  p->sym_stride = p->sps > 0 ? (((n_out + p->sps - 1) / p->sps) + 1) & ~(int64_t)1 : 0;   // even: 16-B pairs
   return AMR_OK;
 }
 

@@ -117,3 +117,14 @@ def test_large_batch_against_oracle(kind, baud, f0, f1):
             "fsk": lambda x: synth.fsk_waveform(x, baud, f0, f1)}[kind]
     want = np.stack([synth.fit(wave(x), 96000) for x in datas])
     assert_close(out, want, what=kind)
+
+
+@pytest.mark.parametrize("fn,kw", [("qpsk_modulate", {"baud": 50}), ("bpsk_modulate", {"baud": 75, "carrier": 1000.0}),
+                                   ("fsk_modulate", {"baud": 50, "mark_freq": 1000.0, "space_freq": 1050.0}),
+                                   ("qpsk_modulate", {"baud": 90, "samp_rate": 96000})])
+def test_long_symbols(fn, kw):
+    """sps > 1024 (the generic synthesis kernel) and sps just under it."""
+    import modem
+    data = bytes(range(7, 12))
+    y = getattr(modem, fn)(data, **kw)
+    assert_close(y, getattr(oracle, fn)(data, **kw), what=f"{fn}{kw}")
