@@ -47,6 +47,7 @@ EXPORTS = [
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
     "amr_comm_synchronize", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
+    "amr_resample_host",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -179,6 +180,7 @@ def lib():
             "amr_allgather": (I32, [P, P, P, I64, P]),
             "amr_comm_synchronize": (I32, [P]),
             "amr_tx_samples": (I64, [I32, I64, D, D]),
+            "amr_resample_host": (I32, [P, I64, I64, I64, P, I32]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
             "amr_modulate_host": (I32, [I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64]),
             "amr_modulate_device": (I32, [P, I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64, P, I64]),
@@ -379,3 +381,19 @@ def hilbert(x: np.ndarray) -> np.ndarray:
     out = np.empty(x.shape, np.complex128)
     check(lib().amr_hilbert_host(ptr(x), ptr(out), x.shape[1], x.shape[0], default_device()))
     return out
+
+
+def resample(x: np.ndarray, num: int) -> np.ndarray:
+    """scipy.signal.resample(x, num) for real float64 input (1-D, or rows of a
+    2-D array resampled along the last axis) on the GPU -- the resample of
+    decoder.decode_wav_file (decoder.py:385-387)."""
+    require_gpu()
+    a = np.asarray(x)
+    if a.dtype != np.float64:
+        raise TypeError("resample: float64 input only (decode_wav_file's soundfile data)")
+    rows = np.ascontiguousarray(np.atleast_2d(a))
+    if rows.ndim != 2 or num < 1 or rows.shape[1] < 1:
+        raise ValueError("resample: need 1-D / 2-D input with at least one sample and num >= 1")
+    out = np.empty((rows.shape[0], int(num)), np.float64)
+    check(lib().amr_resample_host(ptr(rows), rows.shape[1], int(num), rows.shape[0], ptr(out), default_device()))
+    return out[0] if a.ndim == 1 else out

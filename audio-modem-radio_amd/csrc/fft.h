@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -90,6 +91,13 @@ hipError_t launch_bs_pre(const double2* x, double2* a, const double2* w, int64_t
 hipError_t launch_bs_post(const double2* y, double2* out, const double2* w, int64_t n, int64_t M, int64_t batch,
                           bool inverse, const FftEpi& epi, hipStream_t st);
 hipError_t fft_configure_smem();
+// six-step transpose (+ twiddle W_M^(r c) from tw_lo/tw_hi, conjugated when inverse)
+hipError_t launch_transpose(const double2* in, double2* out, int64_t R, int64_t C, int64_t batch,
+                            const double2* tw_lo, const double2* tw_hi, bool inverse, hipStream_t st);
+// scipy.signal.resample's spectrum surgery and final scaling (fsk_api.cpp amr_resample_host)
+hipError_t launch_resample_spec(const double2* X, double2* Yf, int64_t nx, int64_t num, int64_t batch,
+                                hipStream_t st);
+hipError_t launch_real_scale(const double2* Y, double* y, int64_t tot, double scale, hipStream_t st);
 
 // Compare bits of a length-n filter output: sample k = r + rn1*kk (r < rn1,
 // kk < rn2) is bit (r & 7) of byte (r >> 3)*rn2 + kk -- the order in which a
@@ -132,12 +140,45 @@ inline bool fft_split(int64_t n, int& n1, int& n2) {
   return true;
 }
 
-// smallest m >= lo that splits (Bluestein length)
-inline int64_t fft_good_size(int64_t lo) {
-  for (int64_t m = lo; m <= (int64_t)kFftMaxL * kFftMaxL; ++m) {
-    int a, b;
-    if (fft_split(m, a, b)) return m;
+// M = L1 * L2 with both two-pass lengths (the six-step plan past the two-pass
+// limit): L1 <= L2, L1 as large as possible.
+inline bool fft_six_split(int64_t M, int64_t& L1, int64_t& L2) {
+  const int64_t lim = (int64_t)kFftMaxL * kFftMaxL;
+  for (int64_t a = (int64_t)std::sqrt((double)M) + 1; a >= 2; --a) {
+    if (M % a) continue;
+    const int64_t b = M / a;
+    if (a > b || b > lim) continue;
+    int x, y;
+    if (fft_split(a, x, y) && fft_split(b, x, y)) {
+      L1 = a;
+      L2 = b;
+      return true;
+    }
   }
+  return false;
+}
+
+inline bool fft_plannable(int64_t m) {
+  int a, b;
+  int64_t c, d;
+  return fft_split(m, a, b) || fft_six_split(m, c, d);
+}
+
+// Bluestein length: the smallest two-pass length >= lo, else the smallest
+// six-step one (only 5-smooth lengths run at all)
+inline int64_t fft_good_size(int64_t lo) {
+  const int64_t hi = (int64_t)kFftMaxL * kFftMaxL * kFftMaxL * kFftMaxL;
+  std::vector<int64_t> cand;
+  for (int64_t p2 = 1; p2 <= 2 * lo && p2 <= hi; p2 *= 2)
+    for (int64_t p3 = p2; p3 <= 2 * lo && p3 <= hi; p3 *= 3)
+      for (int64_t p5 = p3; p5 <= 2 * lo && p5 <= hi; p5 *= 5)
+        if (p5 >= lo) cand.push_back(p5);
+  std::sort(cand.begin(), cand.end());
+  int a, b;
+  for (int64_t m : cand)                       // a two-pass length when one exists (fewer passes)
+    if (m <= (int64_t)kFftMaxL * kFftMaxL && fft_split(m, a, b)) return m;
+  for (int64_t m : cand)
+    if (fft_plannable(m)) return m;
   return -1;
 }
 

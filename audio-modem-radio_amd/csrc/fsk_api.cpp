@@ -35,97 +35,199 @@ using namespace amr;
 
 namespace {
 
-// Device FFT of one logical length n.
+// Device FFT of one logical length n, run as one of
+//   two-pass   M = n = n1 * n2 (launch_fft / launch_fft_filter: the fused paths)
+//   six-step   M = n = L1 * L2 past the two-pass limit: transpose, L2-point
+//              row FFTs, twiddle-transpose, L1-point row FFTs, transpose
+//   Bluestein  n not plannable: a length-M circular convolution, M >= 2n-1,
+//              itself two-pass or six-step
+// Plain-order epilogues after a six-step / Bluestein transform go through the
+// Bluestein post kernel with a unit chirp.
 struct FftPlan {
   int64_t n = 0;
   int64_t M = 0;                 // transform length run: n, or the Bluestein length
   bool bluestein = false;
-  FftDesc d{};                   // length M
-  double2* tables = nullptr;     // [tw n2][tw n1][tw M][chirp n][bhat M]
-  const double2* chirp = nullptr;
-  const double2* bhat = nullptr;
+  bool six = false;              // M runs six-step
+  FftDesc d{};                   // length M (two-pass)
+  FftDesc d1{}, d2{};            // lengths L1, L2 (six-step)
+  int64_t L1 = 0, L2 = 0;
+  const double2* tw6_lo = nullptr;   // W_M^t, t < 256
+  const double2* tw6_hi = nullptr;   // W_M^(256 t)
+  const double2* chirp = nullptr;    // Bluestein chirp, or all ones (six-step, plain epilogues)
+  const double2* bhat = nullptr;     // FFT_M(bw) (two-pass Bluestein filter table)
+  const double2* bhat_c = nullptr;   // conj(FFT_M(bw)) (six-step Bluestein: applied by the post kernel)
+  double2* s1 = nullptr;             // six-step scratch [max_batch][M] x 2
+  double2* s2 = nullptr;
+  int64_t max_batch = 0;
+  std::vector<void*> allocs;
 };
 
 void fft_plan_free(FftPlan& f) {
-  if (f.tables) (void)hipFree(f.tables);
-  f.tables = nullptr;
+  for (void* p : f.allocs)
+    if (p) (void)hipFree(p);
+  f.allocs.clear();
+  f.s1 = f.s2 = nullptr;
 }
 
-// Plans FFT_n; needs the plan's stream for the Bluestein kernel FFT.
-int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
+// device copy of interleaved host values
+hipError_t upload(FftPlan& f, const std::vector<double>& h, const double2** out) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, h.size() * 8 + 16);
+  if (e != hipSuccess) return e;
+  f.allocs.push_back(p);
+  e = hipMemcpy(p, h.data(), h.size() * 8, hipMemcpyHostToDevice);
+  *out = static_cast<const double2*>(p);
+  return e;
+}
+
+// two-pass descriptor of length L (fft_split must succeed)
+int desc_init(FftPlan& f, FftDesc& d, int64_t L) {
+  int n1 = 0, n2 = 0;
+  if (!fft_split(L, n1, n2)) return fail(AMR_E_INVALID, "FFT length " + std::to_string(L) + " does not split");
+  const int64_t nhi = (L + 255) / 256;
+  std::vector<double> host;
+  auto put = [&](const std::vector<double>& w) { host.insert(host.end(), w.begin(), w.end()); };
+  put(twiddles(n2, n2));
+  put(twiddles(n1, n1));
+  put(twiddles(L, 256));
+  put(twiddles(L, nhi, 256));
+  const double2* t = nullptr;
+  HIP_TRY(upload(f, host, &t));
+  d.n = L;
+  d.n1 = n1;
+  d.n2 = n2;
+  if (!fill_fft_len(d.a, n2, t) || !fill_fft_len(d.c, n1, t + n2))
+    return fail(AMR_E_INVALID, "FFT factor plan failed for n=" + std::to_string(L));
+  d.tw_lo = t + n2 + n1;
+  d.tw_hi = t + n2 + n1 + 256;
+  return AMR_OK;
+}
+
+// X = FFT_M(in) (or the true inverse) by six steps; out may alias in; s1, s2 scratch.
+hipError_t six_fft(const FftPlan& f, const double2* in, double2* out, int64_t batch, bool inverse, hipStream_t st) {
+  if (batch > f.max_batch) return hipErrorInvalidValue;
+  const int64_t L1 = f.L1, L2 = f.L2;
+  // in[j1 + L1 j2] = [j2][j1] -> s1[j1][j2]
+  hipError_t e = launch_transpose(in, f.s1, L2, L1, batch, nullptr, nullptr, false, st);
+  // L2-point transforms of every row j1 -> s1[j1][k2]
+  if (e == hipSuccess) e = launch_fft(f.s1, f.s2, f.s1, f.d2, batch * L1, inverse, st);
+  // times W_M^(j1 k2), -> s2[k2][j1]
+  if (e == hipSuccess) e = launch_transpose(f.s1, f.s2, L1, L2, batch, f.tw6_lo, f.tw6_hi, inverse, st);
+  // L1-point transforms of every row k2 -> s2[k2][k1]
+  if (e == hipSuccess) e = launch_fft(f.s2, f.s1, f.s2, f.d1, batch * L2, inverse, st);
+  // X[k2 + L2 k1] = out[k1][k2]
+  if (e == hipSuccess) e = launch_transpose(f.s2, out, L2, L1, batch, nullptr, nullptr, false, st);
+  return e;
+}
+
+// IFFT_M(FFT_M(a) * FFT_M(bw)) in place in a (Bluestein's convolution), six-step
+hipError_t six_conv(const FftPlan& f, double2* a, double2* tmp, int64_t batch, hipStream_t st) {
+  FftEpi store{};
+  store.mode = kStore;
+  store.n = f.M;
+  hipError_t e = six_fft(f, a, a, batch, false, st);
+  if (e == hipSuccess) e = launch_bs_post(a, a, f.bhat_c, f.M, f.M, batch, false, store, st);   // * FFT(bw)
+  if (e == hipSuccess) e = six_fft(f, a, tmp, batch, true, st);
+  return e;
+}
+
+// Plans FFT_n for up to max_batch rows; needs the stream for the Bluestein kernel FFT.
+int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st, int64_t max_batch) {
   static std::once_flag smem_once;
   static hipError_t smem_err = hipSuccess;
   std::call_once(smem_once, [] { smem_err = fft_configure_smem(); });
   HIP_TRY(smem_err);
   f.n = n;
-  int n1 = 0, n2 = 0;
-  if (fft_split(n, n1, n2)) {
+  f.max_batch = max_batch;
+  int a = 0, b = 0;
+  int64_t L1 = 0, L2 = 0;
+  if (fft_split(n, a, b)) {
     f.M = n;
+  } else if (fft_six_split(n, L1, L2)) {
+    f.M = n;
+    f.six = true;
   } else {
     f.bluestein = true;
     f.M = fft_good_size(2 * n - 1);
-    if (f.M < 0 || !fft_split(f.M, n1, n2))
-      return fail(AMR_E_INVALID, "FFT length " + std::to_string(n) + " exceeds the two-pass limit (Bluestein "
-                                 "length <= " + std::to_string((int64_t)kFftMaxL * kFftMaxL) + ")");
+    if (f.M < 0) return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
+    if (!fft_split(f.M, a, b)) {
+      if (!fft_six_split(f.M, L1, L2)) return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
+      f.six = true;
+    }
   }
   const int64_t M = f.M;
-  const int64_t nhi = (M + 255) / 256;
-  // [tw n2][tw n1][W_M^t, t < 256][W_M^(256 t), t < nhi][chirp n][bhat M]
-  const int64_t ntab = n2 + n1 + 256 + nhi + (f.bluestein ? n + M : 0);
-  std::vector<double> host;
-  host.reserve((size_t)(2 * ntab));
-  auto put = [&](const std::vector<double>& w) { host.insert(host.end(), w.begin(), w.end()); };
-  put(twiddles(n2, n2));
-  put(twiddles(n1, n1));
-  put(twiddles(M, 256));
-  put(twiddles(M, nhi, 256));
-  const int64_t off_chirp = n2 + n1 + 256 + nhi;
-  std::vector<double> bw;
+  if (f.six) {
+    f.L1 = L1;
+    f.L2 = L2;
+    if (int rc = desc_init(f, f.d1, L1)) return rc;
+    if (int rc = desc_init(f, f.d2, L2)) return rc;
+    const int64_t nhi = (M + 255) / 256;
+    std::vector<double> host = twiddles(M, 256);
+    const std::vector<double> hi = twiddles(M, nhi, 256);
+    host.insert(host.end(), hi.begin(), hi.end());
+    const double2* t = nullptr;
+    HIP_TRY(upload(f, host, &t));
+    f.tw6_lo = t;
+    f.tw6_hi = t + 256;
+    void* p = nullptr;
+    HIP_TRY(hipMalloc(&p, (size_t)(max_batch * M * 16)));
+    f.allocs.push_back(p);
+    f.s1 = static_cast<double2*>(p);
+    HIP_TRY(hipMalloc(&p, (size_t)(max_batch * M * 16)));
+    f.allocs.push_back(p);
+    f.s2 = static_cast<double2*>(p);
+  } else {
+    if (int rc = desc_init(f, f.d, M)) return rc;
+  }
+  if (!f.bluestein && !f.six) return AMR_OK;
+  std::vector<double> w((size_t)(2 * n));
   if (f.bluestein) {
     // chirp w_j = exp(i pi j^2 / n); j^2 reduced mod 2n keeps the angle exact
     for (int64_t j = 0; j < n; ++j) {
       const int64_t r = (j * j) % (2 * n);
-      const double a = M_PI * (double)r / (double)n;
-      host.push_back(std::cos(a));
-      host.push_back(std::sin(a));
+      const double ang = M_PI * (double)r / (double)n;
+      w[(size_t)(2 * j)] = std::cos(ang);
+      w[(size_t)(2 * j + 1)] = std::sin(ang);
     }
-    // convolution kernel bw[m] = w_m, bw[M-m] = w_m (0 < m < n), zero elsewhere
-    bw.assign((size_t)(2 * M), 0.0);
-    const double* w = host.data() + 2 * off_chirp;
-    for (int64_t m = 0; m < n; ++m) {
-      bw[2 * m] = w[2 * m];
-      bw[2 * m + 1] = w[2 * m + 1];
-      if (m > 0) {
-        bw[2 * (M - m)] = w[2 * m];
-        bw[2 * (M - m) + 1] = w[2 * m + 1];
-      }
-    }
-    host.resize((size_t)(2 * ntab), 0.0);
+  } else {
+    for (int64_t j = 0; j < n; ++j) w[(size_t)(2 * j)] = 1.0;   // unit chirp: plain epilogues
   }
-  HIP_TRY(hipMalloc(&f.tables, (size_t)ntab * sizeof(double2)));
-  HIP_TRY(hipMemcpy(f.tables, host.data(), (size_t)(2 * (off_chirp + (f.bluestein ? n : 0))) * 8,
-                    hipMemcpyHostToDevice));
-  const double2* t = f.tables;
-  f.d.n = M;
-  f.d.n1 = n1;
-  f.d.n2 = n2;
-  if (!fill_fft_len(f.d.a, n2, t) || !fill_fft_len(f.d.c, n1, t + n2))
-    return fail(AMR_E_INVALID, "FFT factor plan failed for n=" + std::to_string(n));
-  f.d.tw_lo = t + n2 + n1;
-  f.d.tw_hi = t + n2 + n1 + 256;
-  if (f.bluestein) {
-    f.chirp = t + off_chirp;
-    double2* bh = f.tables + off_chirp + n;
-    f.bhat = bh;
-    double2 *a = nullptr, *tmp = nullptr;
-    HIP_TRY(hipMalloc(&a, (size_t)M * sizeof(double2)));
-    hipError_t e = hipMalloc(&tmp, (size_t)M * sizeof(double2));
-    if (e == hipSuccess) e = hipMemcpyAsync(a, bw.data(), (size_t)M * sizeof(double2), hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = launch_fft(a, tmp, bh, f.d, 1, false, st);
+  HIP_TRY(upload(f, w, &f.chirp));
+  if (!f.bluestein) return AMR_OK;
+  // convolution kernel bw[m] = w_m, bw[M-m] = w_m (0 < m < n), zero elsewhere; bhat = FFT_M(bw)
+  std::vector<double> bw((size_t)(2 * M), 0.0);
+  for (int64_t m = 0; m < n; ++m) {
+    bw[(size_t)(2 * m)] = w[(size_t)(2 * m)];
+    bw[(size_t)(2 * m + 1)] = w[(size_t)(2 * m + 1)];
+    if (m > 0) {
+      bw[(size_t)(2 * (M - m))] = w[(size_t)(2 * m)];
+      bw[(size_t)(2 * (M - m) + 1)] = w[(size_t)(2 * m + 1)];
+    }
+  }
+  const double2* bwd = nullptr;
+  HIP_TRY(upload(f, bw, &bwd));
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, (size_t)M * sizeof(double2)));
+  f.allocs.push_back(p);
+  double2* bh = static_cast<double2*>(p);
+  if (!f.six) {
+    double2* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, (size_t)M * sizeof(double2)));
+    hipError_t e = launch_fft(bwd, tmp, bh, f.d, 1, false, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(a);
-    if (tmp) (void)hipFree(tmp);
+    (void)hipFree(tmp);
     HIP_TRY(e);
+    f.bhat = bh;
+  } else {
+    // conj(FFT_M(bw)) by six steps (the post kernel multiplies by conj(w))
+    hipError_t e = six_fft(f, bwd, bh, 1, false, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    HIP_TRY(e);
+    std::vector<double> hb((size_t)(2 * M));
+    HIP_TRY(hipMemcpy(hb.data(), bh, (size_t)M * 16, hipMemcpyDeviceToHost));
+    for (int64_t m = 0; m < M; ++m) hb[(size_t)(2 * m + 1)] = -hb[(size_t)(2 * m + 1)];
+    HIP_TRY(hipMemcpy(bh, hb.data(), (size_t)M * 16, hipMemcpyHostToDevice));
+    f.bhat_c = bh;
   }
   return AMR_OK;
 }
@@ -133,12 +235,19 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st) {
 // out = FFT_n(in) or IFFT_n(in).  u, v: [batch][M] scratch; in != u; out != v.
 hipError_t fft_c2c(const FftPlan& f, const double2* in, double2* u, double2* v, double2* out, int64_t batch,
                    bool inverse, hipStream_t st) {
-  if (!f.bluestein) return launch_fft(in, u, out, f.d, batch, inverse, st);
+  if (!f.bluestein) {
+    if (f.six) return six_fft(f, in, out, batch, inverse, st);
+    return launch_fft(in, u, out, f.d, batch, inverse, st);
+  }
   FftEpi store{};
   store.mode = kStore;
   store.n = f.n;        // row stride of `out` (launch_fft_filter sets its own)
   hipError_t e = launch_bs_pre(in, u, f.chirp, f.n, f.M, batch, inverse, st);
-  if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  if (f.six) {
+    if (e == hipSuccess) e = six_conv(f, u, v, batch, st);
+  } else {
+    if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  }
   if (e == hipSuccess) e = launch_bs_post(v, out, f.chirp, f.n, f.M, batch, inverse, store, st);
   return e;
 }
@@ -146,25 +255,43 @@ hipError_t fft_c2c(const FftPlan& f, const double2* in, double2* u, double2* v, 
 // epi(IFFT_n(-i*sgn(k) * FFT_n(in))) = epi(H[in]), the Hilbert transform of
 // each row (scipy.signal.hilbert(x).imag for real x).  u, v: [batch][M]
 // scratch, in != u, v; a kStore / kEnvOut result lands in hilbert_out(f, u, v).
-double2* hilbert_out(const FftPlan& f, double2* u, double2* v) { return f.bluestein ? v : u; }
+double2* hilbert_out(const FftPlan& f, double2* u, double2* v) { return (f.bluestein || f.six) ? v : u; }
 
 hipError_t fft_hilbert(const FftPlan& f, const double2* in, double2* u, double2* v, int64_t batch, FftEpi epi,
                        hipStream_t st) {
   epi.n = f.n;
-  if (!f.bluestein) return launch_fft_filter(in, u, v, u, f.d, batch, kHilbert, nullptr, epi, st);
+  if (!f.bluestein && !f.six) return launch_fft_filter(in, u, v, u, f.d, batch, kHilbert, nullptr, epi, st);
   const int64_t n = f.n, M = f.M;
   FftEpi store{};
   store.mode = kStore;
   FftEpi hil{};
   hil.mode = kHilbert;
   hil.n = n;
+  hipError_t e = hipSuccess;
+  if (!f.bluestein) {
+    // six-step, M = n: W = -i sgn(k) FFT(in) -> v; IFFT via conj: FFT(conj W) -> v, post conj/scale + epi
+    e = six_fft(f, in, u, batch, false, st);
+    if (e == hipSuccess) e = launch_bs_post(u, v, f.chirp, n, n, batch, false, hil, st);
+    if (e == hipSuccess) e = launch_bs_pre(v, u, f.chirp, n, n, batch, true, st);
+    if (e == hipSuccess) e = six_fft(f, u, v, batch, false, st);
+    if (e == hipSuccess) e = launch_bs_post(v, v, f.chirp, n, n, batch, true, epi, st);
+    return e;
+  }
   // forward: W = -i sgn(k) FFT_n(in) -> u (n-long rows)
-  hipError_t e = launch_bs_pre(in, u, f.chirp, n, M, batch, false, st);
-  if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  e = launch_bs_pre(in, u, f.chirp, n, M, batch, false, st);
+  if (f.six) {
+    if (e == hipSuccess) e = six_conv(f, u, v, batch, st);
+  } else {
+    if (e == hipSuccess) e = launch_fft_filter(u, v, u, v, f.d, batch, kMulTab, f.bhat, store, st);
+  }
   if (e == hipSuccess) e = launch_bs_post(v, u, f.chirp, n, M, batch, false, hil, st);
   // inverse: epi(IFFT_n(W)) -> v / cmp
   if (e == hipSuccess) e = launch_bs_pre(u, v, f.chirp, n, M, batch, true, st);
-  if (e == hipSuccess) e = launch_fft_filter(v, u, v, u, f.d, batch, kMulTab, f.bhat, store, st);
+  if (f.six) {
+    if (e == hipSuccess) e = six_conv(f, v, u, batch, st);
+  } else {
+    if (e == hipSuccess) e = launch_fft_filter(v, u, v, u, f.d, batch, kMulTab, f.bhat, store, st);
+  }
   if (e == hipSuccess) e = launch_bs_post(u, v, f.chirp, n, M, batch, true, epi, st);
   return e;
 }
@@ -320,13 +447,15 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     fsk_plan_free(pl);
     return fail(AMR_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
   }
-  if (int rc = fft_plan_init(pl->fft, n, pl->stream)) {
+  if (int rc = fft_plan_init(pl->fft, n, pl->stream, max_streams)) {
     fsk_plan_free(pl);
     return rc;
   }
   const int64_t M = pl->fft.M;
-  p.rn1 = pl->fft.bluestein ? n : pl->fft.d.n1;
-  p.rn2 = pl->fft.bluestein ? 1 : pl->fft.d.n2;
+  const bool plain = pl->fft.bluestein || pl->fft.six;   // epilogue in natural order (post kernel)
+  p.rn1 = plain ? n : pl->fft.d.n1;
+  p.rn2 = plain ? 1 : pl->fft.d.n2;
+  if (pl->fft.six) pl->scratch_bytes += 2 * max_streams * M * 16;
   p.bits_stride = fft_bits_stride(p.rn1, p.rn2);
   p.inv_rn1 = 1.0f / (float)p.rn1;
   const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
@@ -455,7 +584,7 @@ int amr_fft_c2c_host(const double* in, double* out, int64_t n, int64_t batch, in
   hipStream_t st = nullptr;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   FftPlan f{};
-  int rc = fft_plan_init(f, n, st);
+  int rc = fft_plan_init(f, n, st, batch);
   double2 *x = nullptr, *u = nullptr, *v = nullptr;
   hipError_t e = hipSuccess;
   if (!rc) {
@@ -483,7 +612,7 @@ int amr_hilbert_host(const double* xr, double* analytic, int64_t n, int64_t batc
   hipStream_t st = nullptr;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   FftPlan f{};
-  int rc = fft_plan_init(f, n, st);
+  int rc = fft_plan_init(f, n, st, batch);
   double2 *x = nullptr, *u = nullptr, *v = nullptr;
   hipError_t e = hipSuccess;
   std::vector<double> h((size_t)(batch * n * 2), 0.0);
@@ -510,6 +639,47 @@ int amr_hilbert_host(const double* xr, double* analytic, int64_t n, int64_t batc
     analytic[2 * i] = xr[i];
     analytic[2 * i + 1] = h[(size_t)(2 * i)];
   }
+  return AMR_OK;
+}
+
+int amr_resample_host(const double* x, int64_t nx, int64_t num, int64_t batch, double* y, int device) {
+  if (!x || !y || nx < 1 || num < 1 || batch < 0) return fail(AMR_E_INVALID, "amr_resample_host: bad argument");
+  if (batch == 0) return AMR_OK;
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  FftPlan fx{}, fy{};
+  int rc = fft_plan_init(fx, nx, st, batch);
+  if (!rc) rc = fft_plan_init(fy, num, st, batch);
+  double2 *X = nullptr, *Y = nullptr, *u = nullptr, *v = nullptr;
+  double* yd = nullptr;
+  hipError_t e = hipSuccess;
+  if (!rc) {
+    const int64_t mu = std::max(fx.M, fy.M);
+    std::vector<double> h((size_t)(batch * nx * 2), 0.0);
+    for (int64_t i = 0; i < batch * nx; ++i) h[(size_t)(2 * i)] = x[i];
+    e = hipMalloc(&X, (size_t)(batch * nx * 16));
+    if (e == hipSuccess) e = hipMalloc(&Y, (size_t)(batch * num * 16));
+    if (e == hipSuccess) e = hipMalloc(&u, (size_t)(batch * mu * 16));
+    if (e == hipSuccess) e = hipMalloc(&v, (size_t)(batch * mu * 16));
+    if (e == hipSuccess) e = hipMalloc(&yd, (size_t)(batch * num * 8));
+    if (e == hipSuccess) e = hipMemcpyAsync(X, h.data(), h.size() * 8, hipMemcpyHostToDevice, st);
+    // X = rfft(x) (the full spectrum; the kernel reads bins 0..nx/2)
+    if (e == hipSuccess) e = fft_c2c(fx, X, u, v, X, batch, false, st);
+    if (e == hipSuccess) e = launch_resample_spec(X, Y, nx, num, batch, st);
+    // y = irfft(Y, num) = Re(IFFT_num(Hermitian Y)), then y *= num / nx
+    if (e == hipSuccess) e = fft_c2c(fy, Y, u, v, Y, batch, true, st);
+    if (e == hipSuccess) e = launch_real_scale(Y, yd, batch * num, (double)num / (double)nx, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(y, yd, (size_t)(batch * num * 8), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+  }
+  for (void* p : {(void*)X, (void*)Y, (void*)u, (void*)v, (void*)yd})
+    if (p) (void)hipFree(p);
+  fft_plan_free(fx);
+  fft_plan_free(fy);
+  (void)hipStreamDestroy(st);
+  if (rc) return rc;
+  HIP_TRY(e);
   return AMR_OK;
 }
 

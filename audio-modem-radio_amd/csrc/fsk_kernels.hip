@@ -99,7 +99,6 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   const T* __restrict__ x = xall + (s < last ? s : last) * x_stride;
   const int64_t n = p.n;
   const int pad = p.pad;
-  const int64_t m = n + 2 * (int64_t)pad;
   const int64_t n_tiles = n / kFskTile;
   const int64_t n_main = n_tiles * kFskTile;
   double* __restrict__ ck = scratch + (size_t)w * fsk_scratch_doubles_per_wave(n, pad) + lane;

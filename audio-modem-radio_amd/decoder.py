@@ -31,6 +31,7 @@ from typing import Dict
 
 import numpy as np
 
+import _amr
 import modem
 from compression import intelligent_decompress, delta_decompress
 
@@ -169,14 +170,13 @@ def _read_wav(path: str):
 
 
 def decode_wav_file(path: str, mode: str, symbol_rate: int) -> list:
-    """decoder.py:380-389: read, channel 0, FFT-resample to 96 kHz, decode."""
+    """decoder.py:380-389: read, channel 0, FFT-resample to 96 kHz (GPU), decode."""
     data, sr = _read_wav(path)
     if len(data.shape) > 1:
         data = data[:, 0]
     if sr != SAMPLE_RATE:
-        from scipy import signal
         number_of_samples = int(round(len(data) * float(SAMPLE_RATE) / sr))
-        data = signal.resample(data, number_of_samples)
+        data = _amr.resample(np.asarray(data, np.float64), number_of_samples)   # scipy.signal.resample, on the GPU
     return decode_from_buffer(data, mode, symbol_rate)
 
 

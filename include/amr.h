@@ -30,6 +30,7 @@
  *                           ft8_demodulate modem.py:391), batched
  *   amr_fsk_envelopes_host  the envelopes |hilbert(filtfilt(.))| modem.py:308-309
  *   amr_hilbert_host        scipy.signal.hilbert as modem.py:309 calls it
+ *   amr_resample_host       scipy.signal.resample in decode_wav_file decoder.py:385-387
  *   amr_fec_decode_host     fec.ReedSolomonFEC.decode  fec.py:34-69, batched
  *   amr_frame_parse_host    decoder.parse_fbp_stream_enhanced  decoder.py:142-208,
  *                           batched (magic search, checks, payload CRC32)
@@ -187,6 +188,11 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
  * scipy.signal.hilbert(x) for real x [batch][n].  Synchronous, on `device`. */
 int amr_fft_c2c_host(const double *in, double *out, int64_t n, int64_t batch, int inverse, int device);
 int amr_hilbert_host(const double *x, double *analytic, int64_t n, int64_t batch, int device);
+/* scipy.signal.resample(x, num) of each real row (x: [batch][nx] -> y: [batch][num]),
+ * as decoder.decode_wav_file calls it (decoder.py:385-387): FFT, the
+ * reference's spectrum truncation / zero-padding with its Nyquist-bin rule,
+ * inverse FFT, times num/nx.  Lengths past the two-pass FFT limit run six-step. */
+int amr_resample_host(const double *x, int64_t nx, int64_t num, int64_t batch, double *y, int device);
 
 /* ---- FEC (fec.py:34-69) -----------------------------------------------------
  * in: [n][in_stride] bytes, in_len[n]; out: [n][out_stride] (>= in_len each);

@@ -25,7 +25,9 @@ def gpu(built_lib):
 
 
 @pytest.mark.parametrize("n,batch", [(96000, 3), (51840, 2), (24001, 2), (1000, 5), (7, 4), (390625, 1), (150001, 1),
-                                     (97, 3)])
+                                     (97, 3),
+                                     (960000, 2),      # past the two-pass limit: six-step
+                                     (400001, 1)])     # Bluestein with a six-step convolution length
 def test_fft_matches_numpy(n, batch):
     import _amr
     rng = np.random.default_rng(n)
@@ -38,7 +40,7 @@ def test_fft_matches_numpy(n, batch):
         assert err <= tol, (n, inverse, err)
 
 
-@pytest.mark.parametrize("n", [96000, 24001, 51840, 22])
+@pytest.mark.parametrize("n", [96000, 24001, 51840, 22, 500000, 400001])
 def test_hilbert_matches_scipy(n):
     import _amr
     from scipy import signal
@@ -157,3 +159,34 @@ def test_fsk_timing_hooks():
     pl.demod_host(x)
     t = pl.timings()
     assert set(t) == {"bandpass", "hilbert", "decide"} and all(v > 0 for v in t.values())
+
+
+@pytest.mark.parametrize("nx,num,batch", [(1000, 2177, 2), (2177, 1000, 2), (999, 1500, 1), (1500, 999, 1),
+                                          (1001, 1001, 1), (4410, 9600, 3), (48000, 96000, 1),
+                                          (441000, 960000, 1)])   # decode_wav_file: 10 s at 44.1 kHz
+def test_resample_matches_scipy(nx, num, batch):
+    """_amr.resample == scipy.signal.resample (decoder.py:385-387): up / down,
+    even / odd lengths (the Nyquist-bin rule), Bluestein and six-step lengths."""
+    import _amr
+    from scipy import signal
+    rng = np.random.default_rng(nx + num)
+    x = rng.normal(size=(batch, nx))
+    got = _amr.resample(x, num)
+    want = signal.resample(x, num, axis=1)
+    err = np.abs(got - want).max() / np.abs(want).max()
+    assert err <= 1e-11, err
+    assert np.array_equal(_amr.resample(x[0], num), got[0])
+
+
+def test_fsk_long_stream_vs_oracle():
+    """A 10-s stream (960 000 samples: six-step FFT) and a 4.2-s stream of a
+    non-5-smooth length (Bluestein over a six-step length): decisions == oracle."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    for N in (960000, 400001):
+        x = synth.fsk_batch(2, N, 9600, 12000.0, 24000.0, seed=N, distinct=2, noise=0.3)
+        pl = _fsk.FskPlan(N, 9600, 12000.0, 24000.0, max_streams=2)
+        got, _ = pl.demod_host(x)
+        want = [oracle.fsk_demodulate(x[i], 9600, 12000.0, 24000.0) for i in range(2)]
+        assert got == want, N

@@ -203,3 +203,37 @@ def test_timing_hooks():
     t = plan.timings()
     assert set(t) >= {"bandpass", "lowpass_fwd", "lowpass_bwd", "sync_pack"}
     assert all(v > 0 for v in t.values())
+
+
+def test_decode_wav_file_44k_qpsk_through_gpu_resample(tmp_path, monkeypatch):
+    """A 44.1 kHz QPSK@1000 WAV: decode_wav_file (GPU resample + GPU demod) ==
+    scipy.signal.resample + the oracle demod + the host frame parse, i.e. the
+    reference's decode_wav_file pipeline (decoder.py:380-389) restated on the CPU.
+    The resample itself is within 1e-11 of scipy's (test_gpu_fsk.py); the
+    decoded bytes are compared exactly ("parity unpinned" at the float64 ulp:
+    no reference fixture holds a resampled 44.1 kHz PSK decode)."""
+    import decoder
+    import synth
+    from oracle import oracle
+    from scipy import signal
+    rng = np.random.default_rng(44)
+    fr = synth.random_frame(rng, 300, name="wav44.bin")
+    x = synth.qpsk_waveform(fr, 1000)                          # 96 kHz, as the reference transmits
+    x = np.concatenate([np.zeros(4000, np.float32), x, np.zeros(6000, np.float32)])
+    x = signal.resample(x.astype(np.float64), int(round(x.size * 44100 / 96000)))   # a 44.1 kHz recording
+    x = 0.8 * x + rng.normal(0, 0.02, x.size)
+    p = tmp_path / "q44.wav"
+    p.write_bytes(synth.wav_bytes(np.clip(x, -1, 1), 44100))
+    monkeypatch.chdir(tmp_path)
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        saved = decoder.decode_wav_file(str(p), "QPSK", 1000)
+    data, sr = decoder._read_wav(str(p))
+    y = signal.resample(data, int(round(len(data) * 96000.0 / sr)))
+    raw = oracle.qpsk_demodulate(y, baud=1000)
+    with contextlib.redirect_stdout(io.StringIO()):
+        frames = decoder.parse_fbp_stream_enhanced(raw)
+    assert [os.path.basename(s).split("_", 1)[1] for s in saved] == [f["name"] for f in frames]
+    assert [f["name"] for f in frames] == ["wav44.bin"]
+    import compression
+    with open(saved[0], "rb") as f:
+        assert f.read() == compression.intelligent_decompress(frames[0]["data"])

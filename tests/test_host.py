@@ -95,8 +95,9 @@ def test_decoder_swallows_errors_like_reference(tmp_path, monkeypatch):
     assert "Erro crítico na demodulação: filter critical frequencies must be greater than 0" in buf.getvalue()
 
 
+@pytest.mark.gpu
 def test_decode_wav_file_config1_plumbing(golden, tmp_path, monkeypatch):
-    """BASELINE config 1: 10 s 44.1 kHz FSK1200 WAV -> resample -> [] (reference's own result)."""
+    """BASELINE config 1: 10 s 44.1 kHz FSK1200 WAV -> GPU resample -> [] (reference's own result)."""
     import decoder
     manifest, inputs = golden
     case = [d for d in manifest["decoder"] if d["id"] == "dec_FSK1200_44k"][0]
