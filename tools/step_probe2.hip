@@ -6,6 +6,10 @@
 //   2  pair 5-tap (current K2/K3)
 //   3  quad 5-tap (lane j owns z[j]; top-lane zero by a multiply)
 //   4  row16 5-tap (lane 12+j owns z[j])
+//   5  row16 9-tap, z0 replicated in every lane (lane 8+j owns z[j+1]): y is
+//      computed by every lane, so the recurrence chain is add -> mul -> sub
+//      with the two DPP moves (z1 broadcast, z[j+2] shift) off the chain
+//   6  quad 5-tap, z0 replicated (lane j owns z[j+1])
 // hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/step_probe2.hip -o tools/step_probe2
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -50,7 +54,10 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* cyc, i
   else if (MODE == 1) { const int jj = j16 >= 8 ? j16 - 8 : 0; cAb = co[jj + 1]; cAa = co[10 + jj]; cBb = cBa = 0; }
   else if (MODE == 2) { cAb = co[2 * j2 + 1]; cAa = co[9 + 2 * j2 + 1]; cBb = co[2 * j2 + 2]; cBa = co[9 + 2 * j2 + 2]; }
   else if (MODE == 3) { cAb = co[j4 + 1]; cAa = co[10 + j4]; cBb = cBa = 0; cm = j4 == 3 ? 0.0 : 1.0; }
-  else { const int jj = j16 >= 12 ? j16 - 12 : 0; cAb = co[jj + 1]; cAa = co[10 + jj]; cBb = cBa = 0; }
+  else if (MODE == 4) { const int jj = j16 >= 12 ? j16 - 12 : 0; cAb = co[jj + 1]; cAa = co[10 + jj]; cBb = cBa = 0; }
+  else if (MODE == 5) { const int jj = j16 >= 8 ? j16 - 8 : 0; cAb = co[jj + 2]; cAa = co[11 + jj]; cBb = co[1]; cBa = co[10]; }
+  else { cAb = co[j4 + 2]; cAa = co[11 + j4]; cBb = co[1]; cBa = co[10]; cm = j4 == 3 ? 0.0 : 1.0; }
+  double z0r = 0.05;
   const bool top4 = j4 == 3, top2 = j2 == 1;
   unsigned long long t0 = now();
   for (int it = 0; it < iters; ++it) {
@@ -80,17 +87,29 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* cyc, i
         y = MODE == 1 ? bcast16<8>(t) : bcast16<12>(t);
         const double zC = shl1(zA, hik);
         zA = (zC + x * cAb) - y * cAa;
-      } else {
+      } else if (MODE == 3) {
         const double t = zA + b0 * x;
         y = dpp_f64<0x00>(t);
         const double zC = dpp_f64<0xF9>(zA) * cm;
+        zA = (zC + x * cAb) - y * cAa;
+      } else if (MODE == 5) {
+        y = z0r + b0 * x;
+        const double z1b = bcast16<8>(zA);
+        const double zC = shl1(zA, hik);
+        z0r = (z1b + x * cBb) - y * cBa;
+        zA = (zC + x * cAb) - y * cAa;
+      } else {
+        y = z0r + b0 * x;
+        const double z1b = dpp_f64<0x00>(zA);
+        const double zC = dpp_f64<0xF9>(zA) * cm;
+        z0r = (z1b + x * cBb) - y * cBa;
         zA = (zC + x * cAb) - y * cAa;
       }
       acc += y;
     }
   }
   unsigned long long t1 = now();
-  out[blockIdx.x * 256 + threadIdx.x] = acc + zA + zB;
+  out[blockIdx.x * 256 + threadIdx.x] = acc + zA + zB + z0r;
   if (lane == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
 }
 
@@ -104,10 +123,11 @@ int main() {
   (void)hipMemcpy(co, h, sizeof(h), hipMemcpyHostToDevice);
   static unsigned long long c[8192];
   const int iters = 1000;
-  const char* names[] = {"quad 9-tap (K1q)", "row16 9-tap", "pair 5-tap (K2/K3)", "quad 5-tap", "row16 5-tap"};
-  void (*ks[])(double*, unsigned long long*, int, const double*) = {k<0>, k<1>, k<2>, k<3>, k<4>};
-  for (int m = 0; m < 5; ++m)
-    for (int waves : {256, 512, 1024, 2048}) {
+  const char* names[] = {"quad 9-tap (K1q)", "row16 9-tap", "pair 5-tap (K2/K3)", "quad 5-tap", "row16 5-tap",
+                         "row16 9-tap z0-rep", "quad 5-tap z0-rep"};
+  void (*ks[])(double*, unsigned long long*, int, const double*) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>};
+  for (int m = 0; m < 7; ++m)
+    for (int waves : {512, 1024, 2048}) {
       const int blocks = waves / 4;
       hipEvent_t e0, e1;
       (void)hipEventCreate(&e0);
