@@ -25,6 +25,9 @@
 // Parity: the FFT cannot reproduce pocketfft's rounding; envelopes agree to
 // ~1e-15 relative and decisions are compared bit for bit with the reference
 // (tests/test_gpu_parity.py), with the envelope tolerance stated there.
+#include <algorithm>
+#include <cstdlib>
+
 #include "amr_internal.h"
 
 namespace amr {
@@ -213,6 +216,201 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   }
 }
 
+// F1, role-split form (the default).  Workgroup = two waves over the same 32
+// streams x 2 tones: wave 0 runs every forward recursion, wave 1 every
+// backward one, so the checkpointed filtfilt's second half overlaps:
+//   phase 1  wave 0: forward pass keeping each 32-sample tile's starting
+//            state (global scratch) and the tail's forward outputs (LDS)
+//   phase 1b wave 1: backward recursion over the right extension and the
+//            tail (outputs of the last n % 32 samples straight to z)
+//   phase 2  iteration i: wave 0 stores tile T+1-i (1 KiB rows of z from
+//            yb[i & 1], run backward by wave 1 in iteration i-1), then re-runs
+//            tile T-1-i forward from its checkpoint into yb[i & 1], while wave 1
+//            runs tile T-i backward in yb[(i-1) & 1]; one block barrier per
+//            iteration
+// 1024 waves fill the 1024 SIMDs at B = 16384 (the one-wave form: 512), and
+// phase 2 costs one recursion per sample instead of two.  Arithmetic and
+// order per recursion are those of k_fsk_bandpass (same outputs).
+constexpr int kFsk2Tile = 64;
+__host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
+
+template <typename T>
+__global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
+                                                       double* __restrict__ scratch, double2* __restrict__ z,
+                                                       FskParams p, FskIir f) {
+  constexpr int TL = kFsk2Tile;
+  constexpr int RB = TL * (int)sizeof(T);           // bytes per stream row per tile
+  constexpr int PITCH = RB + 16;
+  constexpr int LPR = RB / 16;                      // lanes per row in a load
+  constexpr int RPI = 64 / LPR;                     // rows per load instruction
+  constexpr int NI = 32 / RPI;                      // load instructions per tile
+  constexpr int YP = 66;                            // yb pitch (doubles)
+  __shared__ __attribute__((aligned(16))) uint8_t tin[1][32][PITCH];
+  __shared__ __attribute__((aligned(16))) double yb[2 * TL][YP];   // two tile buffers, or the tail (<= 2*TL rows)
+  __shared__ double ylast_sh[64];
+  const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int tone = lane & 1, sl = lane >> 1;
+  const int64_t w = blockIdx.x;
+  const int64_t s = w * 32 + sl;
+  const int64_t last = n_streams - 1;
+  const T* __restrict__ xall = reinterpret_cast<const T*>(xv);
+  const T* __restrict__ x = xall + (s < last ? s : last) * x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad;
+  const int64_t n_tiles = n / TL;
+  const int64_t n_main = n_tiles * TL;
+  const int64_t ntail = n - n_main + pad;            // <= TL - 1 + 21 < 2 * TL
+  double* __restrict__ ck = scratch + (size_t)w * fsk2_scratch_doubles_per_group(n) + lane;
+  double b[7], a[7], zs[6];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
+  double* __restrict__ zd = reinterpret_cast<double*>(z);
+
+  // wave 0's input path: 16 B per lane per row segment, two register sets so
+  // every load has two tiles of work to land behind (tin is this wave's own)
+  const int rsub = lane / LPR, cb = (lane % LPR) * 16;
+  const uint8_t* rowp[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int64_t rs = w * 32 + RPI * i + rsub;
+    rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * x_stride) + cb;
+  }
+  v4u r0[NI], r1[NI];
+  auto fetch = [&](v4u (&r)[NI], int64_t t) {
+    t = t < 0 ? 0 : (t >= n_tiles ? n_tiles - 1 : t);   // clamped: unconditional loads
+#pragma unroll
+    for (int i = 0; i < NI; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + t * RB);
+  };
+  auto deposit = [&](const v4u (&r)[NI]) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][RPI * i + rsub][cb]) = r[i];
+  };
+  auto run_tile = [&](auto emit) {
+    constexpr int PER = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int k = 0; k < TL; k += PER) {
+      const v4u v = *reinterpret_cast<const v4u*>(&tin[0][sl][k * sizeof(T)]);
+      T xs[PER];
+      __builtin_memcpy(xs, &v, 16);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step(zs, b, a, FIn<T>::cvt(xs[u])));
+    }
+  };
+  if (role == 0) {
+    // ---- phase 1: forward pass, checkpoints only
+    const T x0 = x[0], xl = x[n - 1];
+    const double e0 = FIn<T>::ext(x0, x[pad]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
+    for (int j = 0; j < pad; ++j) (void)fsk_step(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
+    if (n_tiles > 0) {
+      fetch(r0, 0);
+      fetch(r1, 1);
+      auto fwd = [&](v4u (&r)[NI], int64_t t) {
+        deposit(r);
+        fetch(r, t + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) ck[((size_t)t * 6 + i) * 64] = zs[i];
+        run_tile([](int, double) {});
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      int64_t t = 0;
+      for (; t + 1 < n_tiles; t += 2) {
+        fwd(r0, t);
+        fwd(r1, t + 1);
+      }
+      if (t < n_tiles) fwd(r0, t);
+    }
+    // the tail's forward outputs -> yb rows 0..ntail-1 (flat), the last -> ylast
+    for (int64_t i = n_main; i < n; ++i) (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step(zs, b, a, FIn<T>::cvt(x[i]));
+    double yl = 0.0;
+    for (int j = 0; j < pad; ++j) {
+      yl = fsk_step(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
+      (&yb[0][0])[(size_t)(n - n_main + j) * YP + lane] = yl;
+    }
+    ylast_sh[lane] = yl;
+  }
+  __syncthreads();                                     // phase 1 -> 1b
+  if (role == 1) {
+    // ---- phase 1b: backward over the right extension and the tail
+    const double yl = ylast_sh[lane];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * yl;
+    const double* tb = &yb[0][0];
+    for (int64_t j = ntail - 1; j >= n - n_main; --j) (void)fsk_step(zs, b, a, tb[(size_t)j * YP + lane]);
+    for (int64_t i = n - 1; i >= n_main; --i) {
+      const double y = fsk_step(zs, b, a, tb[(size_t)(i - n_main) * YP + lane]);
+      if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
+    }
+  }
+  __syncthreads();                                     // the tail rows of yb are free again
+  // ---- phase 2: wave 0 re-forwards tile T-1-i while wave 1 runs tile T-i backward
+  if (role == 0) {
+    // tiles top-down; inputs and checkpoints two tiles ahead
+    double c0[6], c1[6];
+    auto ldck = [&](double (&c)[6], int64_t t) {
+      t = t < 0 ? 0 : t;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) c[i] = ck[((size_t)t * 6 + i) * 64];
+    };
+    if (n_tiles > 0) {
+      fetch(r0, n_tiles - 1);
+      ldck(c0, n_tiles - 1);
+      fetch(r1, n_tiles - 2);
+      ldck(c1, n_tiles - 2);
+    }
+    // tile tz's 32 rows of z from yb buffer bb, after wave 1 has run it backward:
+    // RPS rows per 1-KiB store instruction, lane -> (row, sample)
+    auto store_tile = [&](int bb, int64_t tz) {
+      constexpr int RPS = 64 / TL;
+      const double (*buf)[YP] = &yb[bb * TL];
+      const int64_t i0 = tz * TL;
+      const int sub = lane / TL, k = lane % TL;
+#pragma unroll 4
+      for (int row = 0; row < 32; row += RPS) {
+        const int rr = row + sub;
+        const int64_t so = w * 32 + rr;
+        const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
+        if (so < n_streams) z[(size_t)so * n + i0 + k] = v;
+      }
+    };
+    auto refwd = [&](v4u (&r)[NI], double (&c)[6], int64_t it) {
+      const int64_t t = n_tiles - 1 - it;
+      if (it >= 2) store_tile((int)(it & 1), t + 2);     // done by wave 1 in iteration it-1
+      if (t >= 0) {
+        deposit(r);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) zs[i] = c[i];
+        fetch(r, t - 2);
+        ldck(c, t - 2);
+        __builtin_amdgcn_sched_barrier(0);
+        double (*dst)[YP] = &yb[(it & 1) * TL];
+        run_tile([&](int k, double y) { dst[k][lane] = y; });
+      }
+      __syncthreads();
+    };
+    int64_t it = 0;
+    for (; it + 1 <= n_tiles; it += 2) {
+      refwd(r0, c0, it);
+      refwd(r1, c1, it + 1);
+    }
+    if (it <= n_tiles) refwd(r0, c0, it);
+    if (n_tiles >= 1) store_tile((int)((n_tiles - 1) & 1), 0);   // wave 1's last tile
+  } else {
+    for (int64_t it = 0; it <= n_tiles; ++it) {
+      const int64_t t = n_tiles - it;                    // tile written in the previous iteration
+      if (it >= 1) {
+        double (*buf)[YP] = &yb[((it - 1) & 1) * TL];
+#pragma unroll 8
+        for (int k = TL - 1; k >= 0; --k) buf[k][lane] = fsk_step(zs, b, a, buf[k][lane]);
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // F3.  workgroup = stream: the stream's compare bits (in the final row pass's
 // tile order, fft.h fft_bits_stride; <= 49 KiB) are staged in LDS with
 // coalesced 16-B loads, then thread = output word: bit b is 1 when more than
@@ -255,12 +453,27 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
 }
 
 int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad) {
-  return ((n_streams + 31) / 32) * fsk_scratch_doubles_per_wave(n, pad) * (int64_t)sizeof(double);
+  const int64_t per = std::max(fsk_scratch_doubles_per_wave(n, pad), fsk2_scratch_doubles_per_group(n));
+  return ((n_streams + 31) / 32) * per * (int64_t)sizeof(double);
+}
+
+static bool fsk_one_wave() {
+  static const bool v = [] { const char* e = getenv("AMR_FSK_BP1"); return e && e[0] == '1'; }();
+  return v;
 }
 
 hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
                                const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
+  if (!fsk_one_wave()) {
+    switch (dtype) {
+      case kF32: hipLaunchKernelGGL(k_fsk_bandpass2<float>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF64: hipLaunchKernelGGL(k_fsk_bandpass2<double>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kI16: hipLaunchKernelGGL(k_fsk_bandpass2<int16_t>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (dtype) {
     case kF32: hipLaunchKernelGGL(k_fsk_bandpass<float>, dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
     case kF64: hipLaunchKernelGGL(k_fsk_bandpass<double>, dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;

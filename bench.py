@@ -299,6 +299,12 @@ def main():
             cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
                    "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through {how}, "
                              f"{cdt:.2f} s wall"}
+            if not fsk and not fec_fused:
+                # the same restatement on one core (1 core and all host cores)
+                idx1 = idx[:64]
+                v1, d1, _ = cpu_baseline(x[idx1], baud, 1)
+                cpu["value_1core"] = round(v1, 3)
+                cpu["sample_1core"] = f"{len(idx1)} streams, 1 thread, {d1:.2f} s wall"
             bad_idx = [int(i) for j, i in enumerate(idx) if out[i, :ln[i]].tobytes() != couts[j]]
             bad = len(bad_idx)
             if bad:
