@@ -426,6 +426,20 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
   const int nrow = min(kFftTile, nrow_all - r0);
   const double2* __restrict__ src = in + (size_t)b * n + (size_t)r0 * L;
   double2* twl = twl_of(smem, f);
+  // kEnvelope with compile-time radices: the z values the epilogue compares
+  // against are loaded first, so their latency overlaps the row loads'
+  // instead of following the whole transform (thread (t, m) of stage 2
+  // produces kk = m + P*p, p < Q)
+  constexpr bool kPre = MODE == kEnvelope && QC > 0;
+  double2 zp[kPre ? QC : 1];
+  if constexpr (kPre) {
+    const int t = threadIdx.x & (kFftTile - 1), m = threadIdx.x / kFftTile;
+    if (threadIdx.x < kFftTile * PC && t < nrow) {
+      const double2* __restrict__ zr = e.z + (size_t)b * n + (unsigned)(r0 + t);
+#pragma unroll
+      for (int p = 0; p < QC; ++p) zp[p] = zr[(unsigned)(nrow_all * (m + PC * p))];
+    }
+  }
   run_stage1<true, PC, QC>(
       f, twl,
       [&](int t, int j, int q) { return t < nrow ? src[(unsigned)(t * L + j + Q * q)] : make_double2(0.0, 0.0); },
@@ -440,7 +454,8 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
           bool gt = false;
           if (t < nrow) {
             v = make_double2(v.x * scale, -v.y * scale);
-            gt = env_gt(e.z[(size_t)b * n + (unsigned)(r0 + t + nrow_all * kk)], v);
+            if constexpr (kPre) gt = env_gt(zp[p], v);
+            else gt = env_gt(e.z[(size_t)b * n + (unsigned)(r0 + t + nrow_all * kk)], v);
           }
           const uint64_t mask = __ballot(gt);
           if (t == 0) e.bits[(size_t)b * e.bits_stride + (size_t)(r0 >> 3) * L + kk] = (uint8_t)(mask >> (threadIdx.x & 56));
