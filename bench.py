@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--distinct", type=int, default=64, help="distinct waveforms (noise is per stream)")
     ap.add_argument("--cpu-streams", type=int, default=0, help="cpu_baseline sample size (0 = auto ~10 s CPU)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight on separate HIP streams / plans (0 = 2 for the PSK workloads, 1 for "
+                         "fsk9600): batch k+1's band-pass overlaps batch k's low-pass passes")
     args = ap.parse_args()
 
     dist, world, rank, local = dist_setup(args.gpus)
@@ -146,17 +149,21 @@ def main():
         x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
     log(f"[rank {rank}] synthesised {B}x{N} float32 in {time.perf_counter() - t0:.1f}s")
 
+    inflight = args.inflight or (1 if fsk else 2)
     if fsk:
         import _fsk
-        plan = _fsk.FskPlan(N, baud, args.mark, args.space, FS, max_streams=B, device=dev)
+        plans = [_fsk.FskPlan(N, baud, args.mark, args.space, FS, max_streams=B, device=dev) for _ in range(inflight)]
+        plan = plans[0]
         sym_per_stream = (N - plan.sps // 2 + plan.sps - 1) // plan.sps     # decided bits (modem.py:320)
         demod, sync_fn, names = L.amr_fsk_demod_device, L.amr_fsk_plan_synchronize, _amr.TF_NAMES
     else:
-        plan = _amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev)
+        plans = [_amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev) for _ in range(inflight)]
+        plan = plans[0]
         S = (N - plan.first + plan.sps - 1) // plan.sps
         sym_per_stream = S - 1                       # differential symbols decided per stream
         demod, sync_fn, names = L.amr_psk_demod_device, L.amr_psk_plan_synchronize, _amr.T_NAMES
-    plan.enable_timing(True)
+    for pl in plans:
+        pl.enable_timing(True)
     cap = plan.out_cap
 
     def dmalloc(nbytes):
@@ -165,12 +172,15 @@ def main():
         return p
 
     d_x = dmalloc(x.nbytes)
-    d_out, d_len, d_sync = dmalloc(B_slot * cap), dmalloc(B_slot * 8), dmalloc(B_slot * 8)
-    if fec_fused:
-        d_fec, d_flen, d_ok = dmalloc(B_slot * cap), dmalloc(B_slot * 8), dmalloc(B_slot * 4)
     _amr.check(L.amr_memcpy_h2d(d_x, _amr.ptr(x), x.nbytes))
+    # per batch in flight: its plan (stream + scratch) and its output / gather buffers
+    ctx = []
+    for pl in plans:
+        c = {"plan": pl, "out": dmalloc(B_slot * cap), "len": dmalloc(B_slot * 8), "sync": dmalloc(B_slot * 8)}
+        if fec_fused:
+            c.update(fec=dmalloc(B_slot * cap), flen=dmalloc(B_slot * 8), ok=dmalloc(B_slot * 4))
+        ctx.append(c)
     comm = None
-    d_gather = None
     if world > 1:
         uid = (ctypes.c_uint8 * 128)()
         if rank == 0:
@@ -180,40 +190,63 @@ def main():
         uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
         comm = ctypes.c_void_p()
         _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
-        d_gather = dmalloc(world * B_slot * cap)
-        d_gather_len = dmalloc(world * B_slot * 8)
-    # amr_allgather enqueues on a PSK plan's stream (or the comm's own for NULL)
-    gather_stream = None if fsk else plan.handle
+        for c in ctx:
+            c["gather"], c["gather_len"] = dmalloc(world * B_slot * cap), dmalloc(world * B_slot * 8)
 
-    # the bytes every rank hands to the gather: the FEC output for psk8fec
-    g_out, g_len = (d_fec, d_flen) if fec_fused else (d_out, d_len)
-
-    def step():
+    def step(c):
+        pl = c["plan"]
         if fec_fused:
-            _amr.check(L.amr_psk_demod_fec_device(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync,
-                                                  d_fec, cap, d_flen, d_ok))
+            _amr.check(L.amr_psk_demod_fec_device(pl.handle, d_x, _amr.DTYPE_F32, B, N, c["out"], cap, c["len"],
+                                                  c["sync"], c["fec"], cap, c["flen"], c["ok"]))
         else:
-            _amr.check(demod(plan.handle, d_x, _amr.DTYPE_F32, B, N, d_out, cap, d_len, d_sync))
+            _amr.check(demod(pl.handle, d_x, _amr.DTYPE_F32, B, N, c["out"], cap, c["len"], c["sync"]))
         if comm is not None:
+            # the bytes every rank hands to the gather (the FEC output for psk8fec),
+            # to every rank (RCCL over xGMI), on the plan's stream (FSK: the comm's)
+            g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
+            gs = None if fsk else pl.handle
             if fsk:
-                _amr.check(sync_fn(plan.handle))
-            # the decoded bytes of every rank to every rank (RCCL over xGMI)
-            _amr.check(L.amr_allgather(comm, g_out, d_gather, B_slot * cap, gather_stream))
-            _amr.check(L.amr_allgather(comm, g_len, d_gather_len, B_slot * 8, gather_stream))
+                _amr.check(sync_fn(pl.handle))
+            _amr.check(L.amr_allgather(comm, g_out, c["gather"], B_slot * cap, gs))
+            _amr.check(L.amr_allgather(comm, g_len, c["gather_len"], B_slot * 8, gs))
             if fsk:
                 _amr.check(L.amr_comm_synchronize(comm))
-        _amr.check(sync_fn(plan.handle))
 
-    for _ in range(args.warmup):
-        step()
     kt = {k: 0.0 for k in names}
+    nt = [0]
+
+    def collect(c):
+        _amr.check(sync_fn(c["plan"].handle))
+        for k, v in c["plan"].timings().items():
+            kt[k] += v
+        nt[0] += 1
+
+    # warmup: one batch at a time (also the kernels' solo durations), then with the batches in flight
+    for i in range(args.warmup):
+        step(ctx[i % inflight])
+        if i == 0 and args.warmup > 1:             # the first launch is cold: not counted
+            _amr.check(sync_fn(ctx[0]["plan"].handle))
+            continue
+        collect(ctx[i % inflight])
+    solo = {k: v / max(1, nt[0]) for k, v in kt.items() if v > 0}
+    for i in range(min(args.warmup, inflight)):
+        step(ctx[i])
+    _amr.check(L.amr_device_synchronize())
+    kt = {k: 0.0 for k in names}
+    nt = [0]
     barrier(dist)
     _amr.check(L.amr_device_synchronize())
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        for k, v in plan.timings().items():
-            kt[k] += v
+    # step k runs on ctx[k % inflight]; before a context is reused its previous
+    # batch is waited for (the other batches keep running) and its kernel
+    # timings are read
+    for k in range(args.steps):
+        c = ctx[k % inflight]
+        if k >= inflight:
+            collect(c)
+        step(c)
+    for k in range(max(0, args.steps - inflight), args.steps):
+        collect(ctx[k % inflight])
     _amr.check(L.amr_device_synchronize())
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -223,7 +256,7 @@ def main():
     value = total_sym / (dt / args.steps) / 1e6
 
     # per-kernel averages (HIP events on the plan's stream)
-    kavg = {k: v / args.steps for k, v in kt.items() if v > 0}
+    kavg = {k: v / max(1, nt[0]) for k, v in kt.items() if v > 0}
     dom = max(kavg, key=kavg.get)
     # Algorithmic bytes per launch: each stage's
     # compulsory input + output at its minimal width.
@@ -268,6 +301,7 @@ def main():
     # parity spot-check after timing (not timed): GPU bytes vs the oracle
     out = np.empty((B, cap), np.uint8)
     ln = np.empty(B, np.int64)
+    g_out, g_len = (ctx[0]["fec"], ctx[0]["flen"]) if fec_fused else (ctx[0]["out"], ctx[0]["len"])
     _amr.check(L.amr_memcpy_d2h(_amr.ptr(out), g_out, B * cap))
     _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
 
@@ -331,7 +365,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload, "global_batch": B_global, "samples_per_stream": N,
-                       "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)"},
+                       "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)",
+                       "batches_in_flight": inflight},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": f"profiles/{PROFILE_ROUND}_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
@@ -341,19 +376,21 @@ def main():
                                        "frac": round(fp64_achieved / FP64_PEAK_TOPS, 4)}},
             "pipeline_hbm_gbs": round(pipeline_bytes / (ms_per_step / 1e3) / 1e9, 2),
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
+            "kernel_ms_solo": {k: round(v, 4) for k, v in solo.items()},
             "cpu_baseline": cpu,
             "parity": parity,
         }
         if not fsk:
-            result["exact_path_streams"] = plan.exact_streams()
+            result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
         if fec_fused:
             result["parity"] += " (FEC output)"
         print(json.dumps(result), flush=True)
-    for p in (d_x, d_out, d_len, d_sync) + ((d_fec, d_flen, d_ok) if fec_fused else ()):
-        L.amr_free(p)
+    L.amr_free(d_x)
+    for c in ctx:
+        for key in ("out", "len", "sync", "fec", "flen", "ok", "gather", "gather_len"):
+            if key in c:
+                L.amr_free(c[key])
     if comm is not None:
-        L.amr_free(d_gather)
-        L.amr_free(d_gather_len)
         L.amr_comm_destroy(comm)
     if dist is not None:
         dist.barrier()
