@@ -688,12 +688,37 @@ int amr_comm_destroy(amr_comm* comm) {
   return AMR_OK;
 }
 
+// Every collective of a communicator runs on the communicator's own stream, in
+// call order, so that several plans (batches in flight on several streams)
+// can share one communicator without two ranks ever entering its collectives
+// in different orders.  With a plan, the gather waits for the work already on
+// the plan's stream (event), and the plan's later work waits for the gather
+// (it reads the plan's output buffer).
 int amr_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_psk_plan* plan) {
   if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
   HIP_TRY(hipSetDevice(comm->device));
-  hipStream_t st = plan ? plan->stream : comm->stream;
-  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, st);
+  hipEvent_t before = nullptr, after = nullptr;
+  if (plan) {
+    HIP_TRY(hipEventCreateWithFlags(&before, hipEventDisableTiming));
+    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(before, plan->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comm->stream, before, 0);
+    if (e != hipSuccess) {
+      (void)hipEventDestroy(before);
+      if (after) (void)hipEventDestroy(after);
+      return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
+    }
+  }
+  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, comm->stream);
+  hipError_t e = hipSuccess;
+  if (plan) {
+    if (r == ncclSuccess) e = hipEventRecord(after, comm->stream);
+    if (r == ncclSuccess && e == hipSuccess) e = hipStreamWaitEvent(plan->stream, after, 0);
+    (void)hipEventDestroy(before);                 // released once the waits are done
+    (void)hipEventDestroy(after);
+  }
   if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
   return AMR_OK;
 }
 

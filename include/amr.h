@@ -264,7 +264,9 @@ int amr_modulate_device(amr_psk_plan *plan, int mode, double baud, double f0, do
 int amr_comm_unique_id(uint8_t *id /* AMR_UNIQUE_ID_BYTES */);
 int amr_comm_create(amr_comm **comm, const uint8_t *id, int nranks, int rank, int device);
 int amr_comm_destroy(amr_comm *comm);
-/* ncclAllGather of bytes_per_rank bytes per rank; stream = plan's (or NULL = comm's own) */
+/* ncclAllGather of bytes_per_rank bytes per rank, on the comm's own stream in
+ * call order (safe with several plans in flight); with a plan it is ordered
+ * after the plan's queued work and before the plan's later work. */
 int amr_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
                   amr_psk_plan *plan);
 int amr_comm_synchronize(amr_comm *comm);
