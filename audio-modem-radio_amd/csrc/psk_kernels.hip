@@ -756,6 +756,237 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
 }
 
 // ---------------------------------------------------------------------------
+// K1g: the 9-tap band-pass with one state per lane of an 8-lane GROUP, 8
+// streams per wave (K1r keeps 4: its row's lanes 0-7 only mirror lanes 8-15).
+// Half the waves for the same streams: at B = 4096 the band-pass is 512 waves
+// and leaves half the SIMDs to the other batch in flight (bench.py), at
+// ~1.75x K1r's streams per issue slot (tools/step_probe2.hip "group8").
+//   t  = z + b0*x                            (lane j = 0: t IS y)
+//   y  = v_mov_b64 row_newbcast:0 (banks 0-1) then row_newbcast:8 (banks 2-3)
+//   zC = row_shl:1 (z), and exactly -0.0 on the group's top lane j = 7
+//        (two v_cndmask: lane 7 would read the next group's z0)
+//   z  = (zC + x*b[j+1]) - y*a[j+1]
+// Memory as K1r: forward input tiles of 8 streams x 128 B (one 16-B load per
+// lane) through LDS; outputs through a 1-KiB LDS staging image (8 pairs x 8
+// streams) stored with one instruction; backward input by LDS-DMA, 1 KiB =
+// 8 pairs x 8 streams of s1 per chunk.
+constexpr int kG8Streams = 8;                   // streams (8-lane groups) per wave
+constexpr int kG8TileBytes = 128;               // bytes of one stream per forward input tile
+constexpr int kG8Pitch = kG8TileBytes + 16;
+constexpr int kG8Chunk = 16;                    // samples per backward DMA chunk (8 pairs)
+constexpr int kG8Ring = 8;                      // backward DMA ring depth (chunks)
+
+struct G8Stage {
+  uint8_t stage[1024];                          // output image: [pair k][stream g] 16 B
+  uint8_t junk[256];                            // writes of the non-writer lanes
+};
+
+// s1 for K1g: [w][q/2][8 streams][2] doubles
+__device__ __forceinline__ size_t g8_pair_index(int64_t w, int64_t m_pairs, int64_t q, int g) {
+  return ((size_t)(w * m_pairs + (q >> 1)) * kG8Streams + g) * 2 + (q & 1);
+}
+
+__device__ __forceinline__ double g8_step(const RowIir& c, double& z, bool top, double x) {
+  const double t = z + c.b0 * x;
+  const long u = __builtin_bit_cast(long, t);
+  const long r1 = __builtin_amdgcn_update_dpp(0L, u, 0x150, 0xF, 0x3, false);    // row_newbcast:0 -> lanes 0-7
+  const long r2 = __builtin_amdgcn_update_dpp(r1, u, 0x158, 0xF, 0xC, false);    // row_newbcast:8 -> lanes 8-15
+  const double y = __builtin_bit_cast(double, r2);
+  const long long zu = __builtin_bit_cast(long long, z);
+  int lo = __builtin_amdgcn_update_dpp(0, (int)(zu & 0xffffffff), 0x101, 0xF, 0xF, true);   // row_shl:1
+  int hi = __builtin_amdgcn_update_dpp(0, (int)(zu >> 32), 0x101, 0xF, 0xF, true);
+  lo = top ? 0 : lo;
+  hi = top ? (int)0x80000000 : hi;
+  const double zC = __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+  z = (zC + x * c.cb) - y * c.ca;
+  return y;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p, Iir f) {
+  __shared__ __attribute__((aligned(16))) uint8_t tiles[4][2][kG8Streams][kG8Pitch];
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[4][kG8Ring][1024];   // s1 chunks (LDS-DMA)
+  __shared__ __attribute__((aligned(1024))) G8Stage st8[4];
+  constexpr int TS = kG8TileBytes / (int)sizeof(T);    // samples per input tile
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 3, j = lane & 7;
+  const bool top = j == 7;
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t s = w * kG8Streams + g;
+  const int64_t last = buf.n_streams - 1;
+  if (w * kG8Streams > last) return;            // whole wave past the batch (wave-uniform)
+  auto& tile = tiles[wv];
+  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
+  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad1;
+  const int64_t m1 = p.m1;
+  const int qs = pad & 1;
+  const int64_t m1_pairs = (m1 + qs + 1) >> 1;
+  double* __restrict__ s1 = buf.s1;
+
+  RowIir c;
+  c.b0 = f.b[0];
+  c.cb = f.b[j + 1];
+  c.ca = f.a[j + 1];
+  const double zi = f.zi[j];
+  double z;
+
+  // writer lane j = 0 of group g -> image slot (k, g); the 7 others -> junk
+  // slots whose 16-B bank groups avoid the writer's ((8k + g) mod 16) and each
+  // other within the 8-lane LDS cycle group (= this group)
+  uint8_t* const stage = st8[wv].stage;
+  uint8_t* const jb0 = st8[wv].junk + ((g + j) & 15) * 16;          // k even
+  uint8_t* const jb1 = st8[wv].junk + ((g + j + 8) & 15) * 16;      // k odd
+  auto wr_addr = [&](int k) -> uint8_t* {
+    return j == 0 ? stage + (k * kG8Streams + g) * 16 : ((k & 1) ? jb1 : jb0);
+  };
+
+  // ---- forward pass -------------------------------------------------------
+  const T x0 = x[0], xl = x[n - 1];
+  z = zi * In<T>::ext(x0, x[pad]);
+  for (int jj = 0; jj < pad; ++jj) {
+    const double y = g8_step(c, z, top, In<T>::ext(x0, x[pad - jj]));
+    s1[g8_pair_index(w, m1_pairs, jj + qs, g)] = y;
+  }
+  const int64_t n_tiles = n / TS;
+  const int64_t n_main = n_tiles * TS;
+  if (n_tiles > 0) {
+    // one tile = 8 stream rows x 128 B: one 16-B load per lane
+    const int tr = lane >> 3, cb = (lane & 7) * 16;
+    const T* __restrict__ xr = xall + ((w * kG8Streams + tr) < last ? (w * kG8Streams + tr) : last) * buf.x_stride;
+    const uint8_t* rowp = reinterpret_cast<const uint8_t*>(xr) + cb;
+    v4u rv = *reinterpret_cast<const v4u*>(rowp);
+    *reinterpret_cast<v4u*>(&tile[0][tr][cb]) = rv;
+    uint8_t* sdst = reinterpret_cast<uint8_t*>(s1) +
+                    (((size_t)w * m1_pairs + ((pad + qs) >> 1)) * kG8Streams) * 16 + lane * 16;
+    v4u img;
+    auto tile_body = [&](int64_t t, auto firstc) {
+      constexpr bool FIRST = decltype(firstc)::value;
+      const int cur = (int)(t & 1);
+      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
+      rv = *reinterpret_cast<const v4u*>(rowp + tn * kG8TileBytes);
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int PER = 16 / (int)sizeof(T);
+      v4u xv[TS / PER];
+#pragma unroll
+      for (int k = 0; k < TS / PER; ++k) xv[k] = *reinterpret_cast<const v4u*>(&tile[cur][g][k * 16]);
+      static_for_up<TS / 2>([&](auto jc) {
+        constexpr int jp = decltype(jc)::value;             // pair of the tile
+        T xs[PER];
+        __builtin_memcpy(xs, &xv[(2 * jp) / PER], 16);
+        const double y0 = g8_step(c, z, top, In<T>::cvt(xs[(2 * jp) % PER]));
+        const double y1 = g8_step(c, z, top, In<T>::cvt(xs[(2 * jp) % PER + 1]));
+        *reinterpret_cast<v4u*>(wr_addr(jp % 8)) = __builtin_bit_cast(v4u, make_double2(y0, y1));
+        if constexpr (jp % 8 == 7) {
+          if constexpr (!(FIRST && jp == 7)) {
+            *reinterpret_cast<v4u*>(sdst) = img;
+            sdst += 1024;
+          }
+          img = *reinterpret_cast<const v4u*>(stage + lane * 16);
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      *reinterpret_cast<v4u*>(&tile[cur ^ 1][tr][cb]) = rv;
+    };
+    static_assert(TS / 2 % 8 == 0, "a tile holds whole staging images");
+    tile_body(0, std::true_type{});
+    for (int64_t t = 1; t < n_tiles; ++t) tile_body(t, std::false_type{});
+    *reinterpret_cast<v4u*>(sdst) = img;        // the last image
+  }
+  for (int64_t i = n_main; i < n; ++i) {
+    const double y = g8_step(c, z, top, In<T>::cvt(x[i]));
+    s1[g8_pair_index(w, m1_pairs, pad + i + qs, g)] = y;
+  }
+  double ylast = 0.0;
+  for (int jj = 0; jj < pad; ++jj) {
+    ylast = g8_step(c, z, top, In<T>::ext(xl, x[n - 2 - jj]));
+    s1[g8_pair_index(w, m1_pairs, pad + n + jj + qs, g)] = ylast;
+  }
+  __threadfence();
+
+  // ---- backward pass ------------------------------------------------------
+  z = zi * ylast;
+  for (int64_t jj = m1 - 1; jj >= pad + n; --jj)
+    (void)g8_step(c, z, top, s1[g8_pair_index(w, m1_pairs, jj + qs, g)]);
+
+  const int64_t n2 = (n + 1) >> 1;
+  double* __restrict__ fo = buf.s2;
+  const int64_t sgrp = s >> 6;
+  const int sig = (int)(s & 63);
+  const int64_t nb = n / kG8Chunk;
+  const int64_t n_lo = nb * kG8Chunk;
+  for (int64_t i = n - 1; i >= n_lo; --i) {
+    const double y = g8_step(c, z, top, s1[g8_pair_index(w, m1_pairs, pad + i + qs, g)]);
+    fo[f_index(sgrp, n2, i, sig)] = y;
+  }
+  if (nb > 0) {
+    constexpr int PP = kG8Chunk / 2;
+    static_assert(PP * kG8Streams * 16 == 1024, "one DMA wave-instruction per chunk");
+    constexpr int R = kG8Ring;
+    uint8_t* const rg = ring[wv][0];
+    // this lane's 16 B of each chunk: s1 pair (chunk base + lane/8), stream lane&7
+    const uint8_t* gsrc = reinterpret_cast<const uint8_t*>(s1) +
+                          (((size_t)w * m1_pairs + ((pad + qs + (nb - 1) * kG8Chunk) >> 1)) * kG8Streams + lane) * 16;
+    // ... and of each chunk's output image: f pair (chunk base + lane/8), stream lane&7
+    const int64_t s0 = w * kG8Streams;
+    uint8_t* fdst = reinterpret_cast<uint8_t*>(fo) +
+                    ((((size_t)((s0 >> 6) * 2 + ((s0 >> 5) & 1)) * n2) + (size_t)((nb - 1) * PP) + (lane >> 3)) * 32 +
+                     (size_t)((s0 & 31) + (lane & 7))) * 16;
+    auto dma = [&](int slot) {
+      dma16(gsrc, lds_addr(rg + slot * 1024));
+      gsrc -= 1024;
+    };
+    auto run = [&](int slot) {
+      const uint8_t* rs = rg + slot * 1024 + g * 16;
+      v4u xv[PP];                               // the whole chunk up front: one LDS round trip
+#pragma unroll
+      for (int k = 0; k < PP; ++k) xv[k] = *reinterpret_cast<const v4u*>(rs + k * 128);
+      static_for_down<PP>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        const double2 xx = __builtin_bit_cast(double2, xv[k]);
+        const double y1 = g8_step(c, z, top, xx.y);
+        const double y0 = g8_step(c, z, top, xx.x);
+        *reinterpret_cast<v4u*>(wr_addr(k)) = __builtin_bit_cast(v4u, make_double2(y0, y1));
+      });
+    };
+    v4u img;
+    auto flush = [&](auto storec) {
+      if constexpr (decltype(storec)::value) {
+        *reinterpret_cast<v4u*>(fdst) = img;
+        fdst -= (size_t)PP * 32 * 16;
+      }
+      img = *reinterpret_cast<const v4u*>(stage + lane * 16);
+    };
+#pragma unroll
+    for (int u = 0; u < R; ++u) dma(u);
+    int64_t cc = nb - 1;
+    static_for_up<R>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      if (cc - u < 0) return;
+      vm_wait<R - 1>();
+      run(u);
+      dma(u);
+      flush(std::integral_constant<bool, (u > 0)>{});
+    });
+    cc -= R;
+    for (; cc >= 0; cc -= R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (cc - u < 0) break;
+        vm_wait<2 * R - 1>();
+        run(u);
+        dma(u);
+        flush(std::true_type{});
+      }
+    }
+    *reinterpret_cast<v4u*>(fdst) = img;        // the last chunk's image
+    vm_wait<0>();                               // no DMA may land after the wave ends
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Low-pass kernels K2/K3.  A lane PAIR serves one component of one stream:
 // lane j of the pair owns states z[2j], z[2j+1] of the 5-tap recurrence (the
 // same DPP split as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1,
@@ -1588,6 +1819,25 @@ static hipError_t launch_bp_quad(const PskBuffers& b, const PskParams& p, const 
 
 template <typename T>
 static hipError_t launch_bp_row(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  // K1g once K1r would need more than one wave per SIMD (B > 4 x SIMDs: 4096
+  // on an MI355X); K1r below (fewer instructions per wave, solo-faster).
+  // AMR_BP_G8=0/1 forces either.
+  static const int force = [] { const char* e = getenv("AMR_BP_G8"); return e ? (e[0] == '1' ? 1 : 0) : -1; }();
+  static int simds[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev >= 0 && dev < 64 && simds[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    simds[dev] = 4 * cus;
+  }
+  const int64_t nsimd = (dev >= 0 && dev < 64) ? simds[dev] : 1024;
+  const bool g8 = force >= 0 ? force == 1 : b.n_streams > (int64_t)kRowStreams * nsimd;
+  if (g8) {
+    const int64_t waves = (b.n_streams + kG8Streams - 1) / kG8Streams;
+    hipLaunchKernelGGL((k_bandpass_g8<T>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, b, p, f);
+    return hipGetLastError();
+  }
   const int64_t waves = (b.n_streams + kRowStreams - 1) / kRowStreams;
   hipLaunchKernelGGL((k_bandpass_row<T>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, b, p, f);
   return hipGetLastError();

@@ -31,13 +31,13 @@ def find(d, pat):
     return m[0] if m else None
 
 
-KERNELS = ["k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
+KERNELS = ["k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
            "k_lowpass_bwd_q", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
            "k_sync_pack", "k_fec_decode",
            "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
-    "qpsk9600": {"bandpass": ["k_bandpass_row", "k_bandpass_quad", "k_bandpass"],
+    "qpsk9600": {"bandpass": ["k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass"],
                  "lowpass_fwd": ["k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
                  "lowpass_exact": ["k_lowpass_exact"], "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
     "ofdm8": None, "psk8fec": None,

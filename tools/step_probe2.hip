@@ -10,6 +10,9 @@
 //      computed by every lane, so the recurrence chain is add -> mul -> sub
 //      with the two DPP moves (z1 broadcast, z[j+2] shift) off the chain
 //   6  quad 5-tap, z0 replicated (lane j owns z[j+1])
+//   7  8-lane group 9-tap (8 streams per wave): y by two v_mov_b64 row_newbcast
+//      (:0 into banks 0-1, :8 into banks 2-3), z[j+1] by row_shl:1 times a 0/1
+//      factor (the group's top lane)
 // hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/step_probe2.hip -o tools/step_probe2
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -56,7 +59,8 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* cyc, i
   else if (MODE == 3) { cAb = co[j4 + 1]; cAa = co[10 + j4]; cBb = cBa = 0; cm = j4 == 3 ? 0.0 : 1.0; }
   else if (MODE == 4) { const int jj = j16 >= 12 ? j16 - 12 : 0; cAb = co[jj + 1]; cAa = co[10 + jj]; cBb = cBa = 0; }
   else if (MODE == 5) { const int jj = j16 >= 8 ? j16 - 8 : 0; cAb = co[jj + 2]; cAa = co[11 + jj]; cBb = co[1]; cBa = co[10]; }
-  else { cAb = co[j4 + 2]; cAa = co[11 + j4]; cBb = co[1]; cBa = co[10]; cm = j4 == 3 ? 0.0 : 1.0; }
+  else if (MODE == 6) { cAb = co[j4 + 2]; cAa = co[11 + j4]; cBb = co[1]; cBa = co[10]; cm = j4 == 3 ? 0.0 : 1.0; }
+  else { const int j8 = lane & 7; cAb = co[j8 + 1]; cAa = co[10 + j8]; cBb = cBa = 0; cm = j8 == 7 ? 0.0 : 1.0; }
   double z0r = 0.05;
   const bool top4 = j4 == 3, top2 = j2 == 1;
   unsigned long long t0 = now();
@@ -98,6 +102,14 @@ __global__ __launch_bounds__(256) void k(double* out, unsigned long long* cyc, i
         const double zC = shl1(zA, hik);
         z0r = (z1b + x * cBb) - y * cBa;
         zA = (zC + x * cAb) - y * cAa;
+      } else if (MODE == 7) {
+        const double t = zA + b0 * x;
+        const long u = __builtin_bit_cast(long, t);
+        long r = __builtin_amdgcn_update_dpp(0L, u, 0x150, 0xF, 0x3, false);   // row_newbcast:0, banks 0-1
+        r = __builtin_amdgcn_update_dpp(r, u, 0x158, 0xF, 0xC, false);          // row_newbcast:8, banks 2-3
+        y = __builtin_bit_cast(double, r);
+        const double zC = shl1(zA, hik) * cm;
+        zA = (zC + x * cAb) - y * cAa;
       } else {
         y = z0r + b0 * x;
         const double z1b = dpp_f64<0x00>(zA);
@@ -124,10 +136,10 @@ int main() {
   static unsigned long long c[8192];
   const int iters = 1000;
   const char* names[] = {"quad 9-tap (K1q)", "row16 9-tap", "pair 5-tap (K2/K3)", "quad 5-tap", "row16 5-tap",
-                         "row16 9-tap z0-rep", "quad 5-tap z0-rep"};
-  void (*ks[])(double*, unsigned long long*, int, const double*) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>};
-  for (int m = 0; m < 7; ++m)
-    for (int waves : {512, 1024, 2048}) {
+                         "row16 9-tap z0-rep", "quad 5-tap z0-rep", "group8 9-tap"};
+  void (*ks[])(double*, unsigned long long*, int, const double*) = {k<0>, k<1>, k<2>, k<3>, k<4>, k<5>, k<6>, k<7>};
+  for (int m = 0; m < 8; ++m)
+    for (int waves : {512, 1024, 2048, 3072}) {
       const int blocks = waves / 4;
       hipEvent_t e0, e1;
       (void)hipEventCreate(&e0);
