@@ -29,8 +29,8 @@
 //   K3x k_lowpass_exact  lane = stream: the complex low-pass with scipy's full
 //                        signed-zero semantics, only for streams K2q/K3q flagged
 //   (K4b sync + pack lives in util_kernels.hip)
-// The older layouts (K1q quad / K1 lane per stream band-pass, K2/K3 pair
-// low-pass) stay selectable with AMR_PSK_LAYOUT=quad|lane for A/B runs.
+// (The layouts they replaced -- lane per stream, K1q quads, K2/K3 lane pairs
+// -- are in DESIGN.md §4's progression and the git history.)
 //
 // At the benchmark batch (4096 streams) every wave runs alone on its SIMD, so
 // each kernel is bound by its per-sample instruction stream;
@@ -68,30 +68,6 @@ template <> struct In<int16_t> {   // decode_wav_file: float64 = int16 / 32768 (
 constexpr int kClsX = 0x2B7;   // low-pass INPUT not provably safe: NaN, inf, denormal, -0
 constexpr int kClsY = 0x2F7;   // low-pass OUTPUT not provably safe: the above and +0
 
-// ---------------------------------------------------------------------------
-// One step of scipy's real lfilter (DF-II-T), exact op order:
-//   y = z0 + b0*x ; z[i] = (z[i+1] + x*b[i+1]) - y*a[i+1] ; z[last] = x*b[last] - y*a[last]
-// ZODD: b[1], b[3], ... are +0.0 (Butterworth band-pass); x*(+0.0) is then one
-// product shared by those taps -- the same value scipy computes for each.
-template <int NT, bool ZODD>
-__device__ __forceinline__ double df2t_step(double (&z)[NT - 1], const double (&b)[NT],
-                                            const double (&a)[NT], double x) {
-  const double y = z[0] + b[0] * x;
-  const double xz = x * b[1];
-#pragma unroll
-  for (int i = 0; i < NT - 2; ++i) {
-    const double xb = (ZODD && ((i + 1) & 1)) ? xz : x * b[i + 1];
-    z[i] = (z[i + 1] + xb) - y * a[i + 1];
-  }
-  z[NT - 2] = x * b[NT - 1] - y * a[NT - 1];
-  return y;
-}
-
-// [group][q/2][64 lanes][2] doubles
-__device__ __forceinline__ size_t pair_index(int64_t group, int64_t m_pairs, int64_t q, int lane) {
-  return ((size_t)(group * m_pairs + (q >> 1)) * kWave + lane) * 2 + (q & 1);
-}
-
 // s2 (band-pass output f): [group][half][n2][32 streams][2 samples] doubles,
 // so that a low-pass wave (one half-group) streams one 512 B row per 2 samples.
 __device__ __forceinline__ size_t f_index(int64_t g, int64_t n2, int64_t i, int s_in_group) {
@@ -107,164 +83,8 @@ constexpr int kTilePitch = kTileBytes + 16;     // LDS row pitch: conflict-free 
 constexpr int kBwdChunk = 32;                   // samples per backward prefetch chunk (16 pairs)
 
 // ---------------------------------------------------------------------------
-// K1: band-pass filtfilt.  One wave per group of 64 streams, lane = stream.
-template <int NT, bool ZODD, typename T>
-__global__ __launch_bounds__(64) void k_bandpass(PskBuffers buf, PskParams p, Iir f) {
-  __shared__ __attribute__((aligned(16))) uint8_t tile[2][kWave][kTilePitch];
-  constexpr int TS = kTileBytes / (int)sizeof(T);          // samples per tile
-  const int lane = threadIdx.x;
-  const int64_t g = blockIdx.x;
-  const int64_t s = g * kWave + lane;
-  const int64_t last = buf.n_streams - 1;
-  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
-  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
-  const int64_t n = p.n;
-  const int pad = p.pad1;
-  const int64_t m1 = p.m1;
-  const int qs = pad & 1;                       // s1 index q = j + qs (main body starts on a pair)
-  const int64_t m1_pairs = (m1 + qs + 1) >> 1;
-  double* __restrict__ s1 = buf.s1;
-
-  double b[NT], a[NT], z[NT - 1];
-#pragma unroll
-  for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
-
-  // ---- forward pass -------------------------------------------------------
-  const T x0 = x[0], xl = x[n - 1];
-  {
-    const double e0 = In<T>::ext(x0, x[pad]);
-#pragma unroll
-    for (int i = 0; i < NT - 1; ++i) z[i] = f.zi[i] * e0;
-  }
-  for (int j = 0; j < pad; ++j) {               // left odd extension
-    const double y = df2t_step<NT, ZODD>(z, b, a, In<T>::ext(x0, x[pad - j]));
-    s1[pair_index(g, m1_pairs, j + qs, lane)] = y;
-  }
-  // main body: tiles of TS samples x 64 streams, loaded row-coalesced
-  // (16 lanes x 16 B per stream row) and transposed through LDS.
-  const int64_t n_tiles = n / TS;
-  const int64_t n_main = n_tiles * TS;
-  if (n_tiles > 0) {
-    const int rsub = lane >> 4, cb = (lane & 15) * 16;
-    const uint8_t* rowp[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t rs = g * kWave + 4 * i + rsub;
-      rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * buf.x_stride) + cb;
-    }
-    v4u r[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i]);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) *reinterpret_cast<v4u*>(&tile[0][4 * i + rsub][cb]) = r[i];
-    for (int64_t t = 0; t < n_tiles; ++t) {
-      const int cur = (int)(t & 1);
-      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;   // unconditional (clamped) prefetch
-#pragma unroll
-      for (int i = 0; i < 16; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + tn * kTileBytes);
-      __builtin_amdgcn_sched_barrier(0);
-      const int64_t q0 = pad + qs + t * TS;                // even
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s1) + (size_t)(g * m1_pairs + (q0 >> 1)) * kWave + lane;
-      constexpr int PER = 16 / (int)sizeof(T);             // samples per ds_read_b128
-#pragma unroll
-      for (int k = 0; k < TS; k += PER) {
-        const v4u v = *reinterpret_cast<const v4u*>(&tile[cur][lane][k * sizeof(T)]);
-        T xs[PER];
-        __builtin_memcpy(xs, &v, 16);
-#pragma unroll
-        for (int u = 0; u < PER; u += 2) {
-          const double y0 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(xs[u]));
-          const double y1 = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(xs[u + 1]));
-          dst[((k + u) >> 1) * kWave] = make_double2(y0, y1);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) *reinterpret_cast<v4u*>(&tile[cur ^ 1][4 * i + rsub][cb]) = r[i];
-    }
-  }
-  for (int64_t i = n_main; i < n; ++i) {        // main-body remainder
-    const double y = df2t_step<NT, ZODD>(z, b, a, In<T>::cvt(x[i]));
-    s1[pair_index(g, m1_pairs, pad + i + qs, lane)] = y;
-  }
-  double ylast = 0.0;
-  for (int j = 0; j < pad; ++j) {               // right odd extension
-    ylast = df2t_step<NT, ZODD>(z, b, a, In<T>::ext(xl, x[n - 2 - j]));
-    s1[pair_index(g, m1_pairs, pad + n + j + qs, lane)] = ylast;
-  }
-
-  // own stores must be visible to own loads below
-  __threadfence();
-
-  // ---- backward pass ------------------------------------------------------
-#pragma unroll
-  for (int i = 0; i < NT - 1; ++i) z[i] = f.zi[i] * ylast;
-  // the right extension region: outputs discarded (trimmed)
-  for (int64_t j = m1 - 1; j >= pad + n; --j)
-    (void)df2t_step<NT, ZODD>(z, b, a, s1[pair_index(g, m1_pairs, j + qs, lane)]);
-
-  const int64_t n2 = (n + 1) >> 1;
-  double* __restrict__ fo = buf.s2;
-  const int64_t nb = n / kBwdChunk;             // full chunks, processed top-down
-  const int64_t n_lo = nb * kBwdChunk;
-  for (int64_t i = n - 1; i >= n_lo; --i) {     // top remainder, one sample at a time
-    const double y = df2t_step<NT, ZODD>(z, b, a, s1[pair_index(g, m1_pairs, pad + i + qs, lane)]);
-    fo[f_index(g, n2, i, lane)] = y;
-  }
-  if (nb > 0) {
-    const double2* __restrict__ src = reinterpret_cast<const double2*>(s1) + (size_t)g * m1_pairs * kWave + lane;
-    double2* __restrict__ dst = reinterpret_cast<double2*>(fo);
-    const size_t fbase = (size_t)((g * 2 + (lane >> 5)) * n2) * 32 + (lane & 31);
-    constexpr int PP = kBwdChunk / 2;
-    double2 ra[PP], rb[PP];
-    auto load = [&](double2 (&r)[PP], int64_t c) {   // chunk c covers i in [c*32, c*32+32)
-      const int64_t cc = c < 0 ? 0 : c;
-      const int64_t qp = (pad + qs + cc * kBwdChunk) >> 1;
-#pragma unroll
-      for (int k = 0; k < PP; ++k) r[k] = src[(size_t)(qp + k) * kWave];
-    };
-    auto run = [&](const double2 (&r)[PP], int64_t c) {
-#pragma unroll
-      for (int k = PP - 1; k >= 0; --k) {
-        const double y1 = df2t_step<NT, ZODD>(z, b, a, r[k].y);
-        const double y0 = df2t_step<NT, ZODD>(z, b, a, r[k].x);
-        dst[fbase + (size_t)(c * PP + k) * 32] = make_double2(y0, y1);
-      }
-    };
-    // sched_barrier pins each refill right after the chunk that freed its
-    // registers, so every chunk's data was requested a full chunk earlier
-    load(ra, nb - 1);
-    load(rb, nb - 2);
-    int64_t c = nb - 1;
-    for (; c >= 1; c -= 2) {
-      run(ra, c);
-      __builtin_amdgcn_sched_barrier(0);
-      load(ra, c - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      run(rb, c - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      load(rb, c - 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (c == 0) run(ra, 0);
-  }
-  // (the left extension region of the backward pass produces only trimmed
-  //  outputs and no state anyone reads: scipy's final zf is discarded)
-}
-
-// ---------------------------------------------------------------------------
-// K1q: the 9-tap band-pass with its 8 states SPLIT ACROSS A LANE QUAD.
-// A lone wave on a SIMD is bound by the length of its per-sample instruction
-// stream, and at the benchmark batch (4096 streams = 64 lane-per-stream waves)
-// three quarters of the chip would sit idle.  Here lane j of quad q owns
-// states z[2j], z[2j+1] of stream q; the wave serves 16 streams, so the
-// batch fills 4x the SIMDs and each wave issues 16 VALU per sample instead of
-// 31.  Arithmetic is unchanged, op for op:
-//   y       = z0 + b0*x                       (lane 0 of the quad, broadcast by DPP)
-//   z[2j]   = (z[2j+1] + x*b[2j+1]) - y*a[2j+1]
-//   z[2j+1] = (z[2j+2] + x*b[2j+2]) - y*a[2j+2]   z[2j+2] = lane j+1's old z[2j]
-// and for the top state (lane 3) the missing z[8] is -0.0, so
-// (-0.0 + x*b8) - y*a8 == x*b8 - y*a8 bit for bit (also for signed zeros).
+// 64-bit DPP move within quads (two 32-bit moves; every quad_perm source lane
+// is valid, so no "old" value is needed)
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
   const long long u = __builtin_bit_cast(long long, v);
@@ -274,174 +94,6 @@ __device__ __forceinline__ double dpp_f64(double v) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 constexpr int kQuadBcast0 = 0x00;   // quad_perm [0,0,0,0]
-constexpr int kQuadNext = 0xF9;     // quad_perm [1,2,3,3]
-
-struct QuadIir {
-  double b0, cAb, cAa, cBb, cBa;
-  bool top;                         // lane 3 of the quad
-};
-
-__device__ __forceinline__ double quad_step(const QuadIir& c, double& zA, double& zB, double x) {
-  const double t = zA + c.b0 * x;
-  const double y = dpp_f64<kQuadBcast0>(t);
-  double zC = dpp_f64<kQuadNext>(zA);
-  zC = c.top ? -0.0 : zC;
-  const double nA = (zB + x * c.cAb) - y * c.cAa;
-  const double nB = (zC + x * c.cBb) - y * c.cBa;
-  zA = nA;
-  zB = nB;
-  return y;
-}
-
-// s1 for K1q: [g16][q/2][16 streams][2] doubles
-__device__ __forceinline__ size_t pair16_index(int64_t g16, int64_t m_pairs, int64_t q, int sq) {
-  return ((size_t)(g16 * m_pairs + (q >> 1)) * 16 + sq) * 2 + (q & 1);
-}
-
-template <typename T>
-__global__ __launch_bounds__(64) void k_bandpass_quad(PskBuffers buf, PskParams p, Iir f) {
-  __shared__ __attribute__((aligned(16))) uint8_t tile[2][16][kTilePitch];
-  constexpr int TS = kTileBytes / (int)sizeof(T);
-  const int lane = threadIdx.x;
-  const int j = lane & 3, sq = lane >> 2;
-  const int64_t g16 = blockIdx.x;
-  const int64_t s = g16 * 16 + sq;
-  const int64_t last = buf.n_streams - 1;
-  const T* __restrict__ xall = reinterpret_cast<const T*>(buf.x);
-  const T* __restrict__ x = xall + (s < last ? s : last) * buf.x_stride;
-  const int64_t n = p.n;
-  const int pad = p.pad1;
-  const int64_t m1 = p.m1;
-  const int qs = pad & 1;
-  const int64_t m1_pairs = (m1 + qs + 1) >> 1;
-  double* __restrict__ s1 = buf.s1;
-
-  QuadIir c;
-  c.b0 = f.b[0];
-  c.cAb = j == 0 ? f.b[1] : j == 1 ? f.b[3] : j == 2 ? f.b[5] : f.b[7];
-  c.cAa = j == 0 ? f.a[1] : j == 1 ? f.a[3] : j == 2 ? f.a[5] : f.a[7];
-  c.cBb = j == 0 ? f.b[2] : j == 1 ? f.b[4] : j == 2 ? f.b[6] : f.b[8];
-  c.cBa = j == 0 ? f.a[2] : j == 1 ? f.a[4] : j == 2 ? f.a[6] : f.a[8];
-  c.top = j == 3;
-  const double ziA = j == 0 ? f.zi[0] : j == 1 ? f.zi[2] : j == 2 ? f.zi[4] : f.zi[6];
-  const double ziB = j == 0 ? f.zi[1] : j == 1 ? f.zi[3] : j == 2 ? f.zi[5] : f.zi[7];
-  double zA, zB;
-
-  // ---- forward pass -------------------------------------------------------
-  const T x0 = x[0], xl = x[n - 1];
-  {
-    const double e0 = In<T>::ext(x0, x[pad]);
-    zA = ziA * e0;
-    zB = ziB * e0;
-  }
-  for (int jj = 0; jj < pad; ++jj) {
-    const double y = quad_step(c, zA, zB, In<T>::ext(x0, x[pad - jj]));
-    s1[pair16_index(g16, m1_pairs, jj + qs, sq)] = y;
-  }
-  const int64_t n_tiles = n / TS;
-  const int64_t n_main = n_tiles * TS;
-  if (n_tiles > 0) {
-    const int rsub = lane >> 4, cb = (lane & 15) * 16;
-    const uint8_t* rowp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t rs = g16 * 16 + 4 * i + rsub;
-      rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * buf.x_stride) + cb;
-    }
-    v4u r[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&tile[0][4 * i + rsub][cb]) = r[i];
-    for (int64_t t = 0; t < n_tiles; ++t) {
-      const int cur = (int)(t & 1);
-      const int64_t tn = (t + 1 < n_tiles) ? t + 1 : t;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) r[i] = *reinterpret_cast<const v4u*>(rowp[i] + tn * kTileBytes);
-      __builtin_amdgcn_sched_barrier(0);
-      const int64_t q0 = pad + qs + t * TS;
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s1) + (size_t)(g16 * m1_pairs + (q0 >> 1)) * 16 + sq;
-      constexpr int PER = 16 / (int)sizeof(T);
-#pragma unroll
-      for (int k = 0; k < TS; k += PER) {
-        const v4u v = *reinterpret_cast<const v4u*>(&tile[cur][sq][k * sizeof(T)]);
-        T xs[PER];
-        __builtin_memcpy(xs, &v, 16);
-#pragma unroll
-        for (int u = 0; u < PER; u += 2) {
-          const double y0 = quad_step(c, zA, zB, In<T>::cvt(xs[u]));
-          const double y1 = quad_step(c, zA, zB, In<T>::cvt(xs[u + 1]));
-          dst[((k + u) >> 1) * 16] = make_double2(y0, y1);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&tile[cur ^ 1][4 * i + rsub][cb]) = r[i];
-    }
-  }
-  for (int64_t i = n_main; i < n; ++i) {
-    const double y = quad_step(c, zA, zB, In<T>::cvt(x[i]));
-    s1[pair16_index(g16, m1_pairs, pad + i + qs, sq)] = y;
-  }
-  double ylast = 0.0;
-  for (int jj = 0; jj < pad; ++jj) {
-    ylast = quad_step(c, zA, zB, In<T>::ext(xl, x[n - 2 - jj]));
-    s1[pair16_index(g16, m1_pairs, pad + n + jj + qs, sq)] = ylast;
-  }
-  __threadfence();
-
-  // ---- backward pass ------------------------------------------------------
-  zA = ziA * ylast;
-  zB = ziB * ylast;
-  for (int64_t jj = m1 - 1; jj >= pad + n; --jj)
-    (void)quad_step(c, zA, zB, s1[pair16_index(g16, m1_pairs, jj + qs, sq)]);
-
-  const int64_t n2 = (n + 1) >> 1;
-  double* __restrict__ fo = buf.s2;
-  const int64_t sgrp = s >> 6;
-  const int sig = (int)(s & 63);
-  const int64_t nb = n / kBwdChunk;
-  const int64_t n_lo = nb * kBwdChunk;
-  for (int64_t i = n - 1; i >= n_lo; --i) {
-    const double y = quad_step(c, zA, zB, s1[pair16_index(g16, m1_pairs, pad + i + qs, sq)]);
-    fo[f_index(sgrp, n2, i, sig)] = y;
-  }
-  if (nb > 0) {
-    const double2* __restrict__ src = reinterpret_cast<const double2*>(s1) + (size_t)g16 * m1_pairs * 16 + sq;
-    double2* __restrict__ dst = reinterpret_cast<double2*>(fo);
-    const size_t fbase = (size_t)((sgrp * 2 + (sig >> 5)) * n2) * 32 + (sig & 31);
-    constexpr int PP = kBwdChunk / 2;
-    double2 ra[PP], rb[PP];
-    auto load = [&](double2 (&r)[PP], int64_t cc0) {
-      const int64_t cc = cc0 < 0 ? 0 : cc0;
-      const int64_t qp = (pad + qs + cc * kBwdChunk) >> 1;
-#pragma unroll
-      for (int k = 0; k < PP; ++k) r[k] = src[(size_t)(qp + k) * 16];
-    };
-    auto run = [&](const double2 (&r)[PP], int64_t cc) {
-#pragma unroll
-      for (int k = PP - 1; k >= 0; --k) {
-        const double y1 = quad_step(c, zA, zB, r[k].y);
-        const double y0 = quad_step(c, zA, zB, r[k].x);
-        dst[fbase + (size_t)(cc * PP + k) * 32] = make_double2(y0, y1);
-      }
-    };
-    load(ra, nb - 1);
-    load(rb, nb - 2);
-    int64_t cc = nb - 1;
-    for (; cc >= 1; cc -= 2) {
-      run(ra, cc);
-      __builtin_amdgcn_sched_barrier(0);
-      load(ra, cc - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      run(rb, cc - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      load(rb, cc - 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (cc == 0) run(ra, 0);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // K1r: the 9-tap band-pass with ONE STATE PER LANE of a 16-lane DPP row.
@@ -987,340 +639,24 @@ __global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p
 }
 
 // ---------------------------------------------------------------------------
-// Low-pass kernels K2/K3.  A lane PAIR serves one component of one stream:
-// lane j of the pair owns states z[2j], z[2j+1] of the 5-tap recurrence (the
-// same DPP split as K1q: y broadcast from j=0, z[2j+2] shifted down from j+1,
-// -0.0 above the top state).
-//
-// The mixer (modem.py:200-201) is numpy's complex multiply (f + 0j) * lo:
-//   re = fma(f, lo_re, -(0*lo_im)),  im = fma(f, lo_im, 0*lo_re)
-// The plan stores, per sample and component, (lo_c, addend_c) so each lane
-// does exactly one fma: bb = fma(f, lo2[n][c].x, lo2[n][c].y).
+// Low-pass: the mixer (modem.py:200-201) is numpy's complex multiply
+// (f + 0j) * lo:  re = fma(f, lo_re, -(0*lo_im)),  im = fma(f, lo_im, 0*lo_re);
+// the plan stores, per sample and component, (lo_c, addend_c).
 //
 // The complex lfilter with real coefficients is two real recurrences EXCEPT
 // for the sign of zero results (scipy evaluates b*x as b*xr - (+0)*xi, ...).
 // The separable recurrences are exact whenever every tap product is a
 // non-zero finite number, which holds when every input
-// and output magnitude is >= 2^-1022 and nothing is inf/NaN.  K2/K3 track
-// min|x|, min|y| (one v_min_f64 each) and test the final states for
-// finiteness (NaN/inf are sticky in the recurrence); a stream that fails is
-// flagged and K3x recomputes it with the full complex semantics.  The single
-// sample that is +0 by construction (bb_im[0]: lo_im[0] == -0) is judged by
-// its class instead: +0 there is provably harmless.
+// and output magnitude is >= 2^-1022 and nothing is inf/NaN.  K2q/K3q track
+// that (the detector below) and flag a stream that fails it; K3x recomputes
+// it with the full complex semantics.  The single sample that is +0 by
+// construction (bb_im[0]: lo_im[0] == -0) is judged by its class instead: +0
+// there is provably harmless.
 constexpr int kLpChunk = 16;                    // samples per low-pass prefetch chunk
-constexpr int kPairBcast = 0xA0;                // quad_perm [0,0,2,2]
-constexpr int kPairNext = 0xF5;                 // quad_perm [1,1,3,3]
-constexpr double kMinNormal = 0x1p-1022;
 
-struct PairIir {
-  double b0, cAb, cAa, cBb, cBa;
-  bool top;                                     // j == 1
-};
-
-// pair_step2 also hands back t: on lane j=0 it IS y, bit for bit, and as an
-// arithmetic result (not a DPP move) the detector's fmin needs no canonicalise.
-__device__ __forceinline__ double pair_step2(const PairIir& c, double& zA, double& zB, double x, double& t_out) {
-  const double t = zA + c.b0 * x;
-  t_out = t;
-  const double y = dpp_f64<kPairBcast>(t);
-  double zC = dpp_f64<kPairNext>(zA);
-  zC = c.top ? -0.0 : zC;
-  const double nA = (zB + x * c.cAb) - y * c.cAa;
-  const double nB = (zC + x * c.cBb) - y * c.cBa;
-  zA = nA;
-  zB = nB;
-  return y;
-}
-
-__device__ __forceinline__ double pair_step(const PairIir& c, double& zA, double& zB, double x) {
-  const double t = zA + c.b0 * x;
-  const double y = dpp_f64<kPairBcast>(t);
-  double zC = dpp_f64<kPairNext>(zA);
-  zC = c.top ? -0.0 : zC;
-  const double nA = (zB + x * c.cAb) - y * c.cAa;
-  const double nB = (zC + x * c.cBb) - y * c.cBa;
-  zA = nA;
-  zB = nB;
-  return y;
-}
-
-__device__ __forceinline__ PairIir pair_coef(const Iir& f, int j, double& ziA, double& ziB) {
-  PairIir c;
-  c.b0 = f.b[0];
-  c.cAb = j ? f.b[3] : f.b[1];
-  c.cAa = j ? f.a[3] : f.a[1];
-  c.cBb = j ? f.b[4] : f.b[2];
-  c.cBa = j ? f.a[4] : f.a[2];
-  c.top = j == 1;
-  ziA = j ? f.zi[2] : f.zi[0];
-  ziB = j ? f.zi[3] : f.zi[1];
-  return c;
-}
-
-// Low-pass wave mapping: wave = (half-group hg of 32 streams, component);
-// lane l -> stream hg*32 + l/2, state pair position j = l & 1.  Keeping one
-// component per wave makes the LO uniform across the wave, so it arrives
-// through scalar loads instead of one vector load per lane per sample.
-//
-// s3: [hg][comp][q/2][32 streams][2] doubles (a pair of samples per stream)
-__device__ __forceinline__ size_t s3_index(int64_t hg, int comp, int64_t m_pairs, int64_t q, int sl) {
-  return ((((size_t)((hg * 2 + comp) * m_pairs + (q >> 1))) * 32 + sl) * 2) + (q & 1);
-}
-
-// Symbol buffer (reuses s1, free after K1): the baseband sample of every
-// symbol: sym[s/32][k][32 streams][re, im] doubles.
+// symbol buffer: [stream][symbol][re, im] doubles
 __device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k, int comp) {
   return ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2 + comp;
-}
-
-// VAR != 0: timing-only ablations for tools/k2_ablation.py (wrong results):
-//   1 = no main-body stores, 2 = no LO (bb = f), 3 = no detector, 4 = no f loads
-template <int VAR>
-__global__ __launch_bounds__(64) void k_lowpass_fwd(PskBuffers buf, PskParams p, Iir f) {
-  const int lane = threadIdx.x;
-  const int j = lane & 1, sl = lane >> 1;
-  const int64_t hg = blockIdx.x >> 1;
-  const int comp = blockIdx.x & 1;
-  const int64_t s = hg * 32 + sl;
-  const int64_t n = p.n;
-  const int64_t n2 = (n + 1) >> 1;
-  const int pad = p.pad2;
-  const int qs = pad & 1;
-  const int64_t m2_pairs = (p.m2 + qs + 1) >> 1;
-  const double2* __restrict__ fsrc = reinterpret_cast<const double2*>(buf.s2) + (size_t)hg * n2 * 32 + sl;
-  // uniform per wave: lo2[i] = (lo_c, addend_c) at lo[2i] (double2 units).  In
-  // the main body lane k of the wave loads the entry of sample k of a chunk
-  // (one VMEM per chunk instead of one per sample) and v_readlane broadcasts
-  // it into SGPRs when that sample is mixed.
-  const double2* __restrict__ lo = reinterpret_cast<const double2*>(buf.lo) + comp;
-  double* __restrict__ s3 = buf.s3;
-
-  double ziA, ziB;
-  const PairIir c = pair_coef(f, j, ziA, ziB);
-  double zA, zB;
-  bool bad = false;
-  double xmin = __builtin_inf(), ymin = __builtin_inf();
-  // numpy's (f + 0j) * lo for this component: fma(f, lo_c, addend) with an
-  // exactly-zero addend == (f * lo_c) + addend whenever f*lo_c does not
-  // underflow to zero; that case makes |bb| < 2^-1022 and is flagged below.
-  auto MIXL = [&](double fv, double2 l) { return VAR == 2 ? fv : fv * l.x + l.y; };
-  double sink = 0.0;
-  auto MIX = [&](double fv, int64_t i) { return MIXL(fv, lo[2 * i]); };
-  auto X = [&](int64_t i) {
-    const double2 fp = fsrc[(size_t)(i >> 1) * 32];
-    return MIX((i & 1) ? fp.y : fp.x, i);
-  };
-
-  const double x0 = X(0), xl = X(n - 1);
-  bad |= __builtin_amdgcn_class(x0, kClsX);     // bb[0]: +0 allowed (see above)
-  const double e0 = 2.0 * x0 - X(pad);
-  bad |= __builtin_amdgcn_class(e0, kClsY);     // zi * ext[0] must not meet a zero
-  zA = ziA * e0;
-  zB = ziB * e0;
-  for (int jj = 0; jj < pad; ++jj) {
-    const double e = 2.0 * x0 - X(pad - jj);
-    xmin = fmin(xmin, fabs(e));
-    const double y = pair_step(c, zA, zB, e);
-    ymin = fmin(ymin, fabs(y));
-    s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)] = y;
-  }
-  const int64_t nc = n / kLpChunk;
-  const int64_t n_main = nc * kLpChunk;
-  if (nc > 0) {
-    constexpr int PP = kLpChunk / 2;
-    double2 fa[PP], fb[PP], la, lb;
-    auto load = [&](double2 (&fr)[PP], double2& lr, int64_t cc0) {
-      const int64_t cc = cc0 < nc ? cc0 : nc - 1;
-#pragma unroll
-      for (int k = 0; k < PP; ++k)
-        fr[k] = VAR == 4 ? make_double2(1e-3 * (k + lane) + cc, 2e-3 * k + cc) : fsrc[(size_t)(cc * PP + k) * 32];
-      lr = lo[2 * (cc * kLpChunk + (lane & (kLpChunk - 1)))];
-    };
-    auto bcast = [&](const double2& lr, int k) {   // lane k's LO entry, as wave-uniform values
-      const long long lx = __builtin_bit_cast(long long, lr.x), ly = __builtin_bit_cast(long long, lr.y);
-      const int a0 = __builtin_amdgcn_readlane((int)(lx & 0xffffffff), k);
-      const int a1 = __builtin_amdgcn_readlane((int)(lx >> 32), k);
-      const int c0 = __builtin_amdgcn_readlane((int)(ly & 0xffffffff), k);
-      const int c1 = __builtin_amdgcn_readlane((int)(ly >> 32), k);
-      return make_double2(__builtin_bit_cast(double, ((long long)a1 << 32) | (unsigned)a0),
-                          __builtin_bit_cast(double, ((long long)c1 << 32) | (unsigned)c0));
-    };
-    auto run = [&](const double2 (&fr)[PP], const double2& lr, int64_t cc, int) {
-      const int64_t q0 = pad + qs + cc * kLpChunk;
-      double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3_index(hg, comp, m2_pairs, q0, sl) >> 1);
-#pragma unroll
-      for (int k = 0; k < PP; ++k) {
-        const double e0v = MIXL(fr[k].x, bcast(lr, 2 * k));
-        const double e1v = MIXL(fr[k].y, bcast(lr, 2 * k + 1));
-        // bb[0] is judged by its class above, not by magnitude
-        if (VAR != 3) xmin = fmin(xmin, (k == 0 && cc == 0) ? __builtin_inf() : fabs(e0v));
-        double t0, t1;
-        const double y0 = pair_step2(c, zA, zB, e0v, t0);
-        if (VAR != 3) xmin = fmin(xmin, fabs(e1v));
-        const double y1 = pair_step2(c, zA, zB, e1v, t1);
-        if (VAR != 3) ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
-        if (VAR == 1) sink += y0 - y1;
-        else dst[(size_t)k * 32] = make_double2(y0, y1);
-      }
-    };
-    load(fa, la, 0);
-    load(fb, lb, 1);
-    int64_t cc = 0;
-    for (; cc + 1 < nc; cc += 2) {
-      run(fa, la, cc, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      load(fa, la, cc + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      run(fb, lb, cc + 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      load(fb, lb, cc + 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (cc < nc) run(fa, la, cc, 0);
-  }
-  for (int64_t i = n_main; i < n; ++i) {
-    const double e = X(i);
-    if (i != 0) xmin = fmin(xmin, fabs(e));
-    const double y = pair_step(c, zA, zB, e);
-    ymin = fmin(ymin, fabs(y));
-    s3[s3_index(hg, comp, m2_pairs, pad + i + qs, sl)] = y;
-  }
-  for (int jj = 0; jj < pad; ++jj) {
-    const double e = 2.0 * xl - X(n - 2 - jj);
-    xmin = fmin(xmin, fabs(e));
-    const double y = pair_step(c, zA, zB, e);
-    ymin = fmin(ymin, fabs(y));
-    s3[s3_index(hg, comp, m2_pairs, pad + n + jj + qs, sl)] = y;
-  }
-  if (VAR == 1 && sink == 1.2345) bad = true;
-  bad |= !(xmin >= kMinNormal) || (j == 0 && !(ymin >= kMinNormal));   // ymin is y only on j == 0
-  bad |= !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
-  int fl = bad ? 1 : 0;
-  fl |= __shfl_xor(fl, 1);
-  if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
-}
-
-// K3.  SPS > 0: a specialisation for sps == SPS and first == SPS/2 (QPSK at
-// the benchmark rates) whose chunk length is a multiple of SPS, so the symbol
-// samples sit at the same static offsets of every chunk: no per-sample branch.
-// SPS == 0: generic, one uniform branch per sample.
-template <int SPS>
-__global__ __launch_bounds__(64) void k_lowpass_bwd(PskBuffers buf, PskParams p, Iir f) {
-  constexpr int CH = SPS > 0 ? 20 : kLpChunk;  // 20 = lcm-friendly for SPS in {2,4,5,10,20}
-  static_assert(SPS == 0 || CH % SPS == 0, "chunk must be a multiple of SPS");
-  const int lane = threadIdx.x;
-  const int j = lane & 1, sl = lane >> 1;
-  const int64_t hg = blockIdx.x >> 1;
-  const int comp = blockIdx.x & 1;
-  const int64_t s = hg * 32 + sl;
-  const int64_t n = p.n;
-  const int pad = p.pad2;
-  const int qs = pad & 1;
-  const int64_t m2 = p.m2;
-  const int64_t m2_pairs = (m2 + qs + 1) >> 1;
-  const double* __restrict__ s3 = buf.s3;
-  double* __restrict__ sym = buf.s1;
-  const int64_t S = p.n_sym;
-
-  double ziA, ziB;
-  const PairIir c = pair_coef(f, j, ziA, ziB);
-  double zA, zB;
-  double ymin = __builtin_inf();
-
-  const double ylast = s3[s3_index(hg, comp, m2_pairs, m2 - 1 + qs, sl)];
-  zA = ziA * ylast;
-  zB = ziB * ylast;
-  for (int64_t jj = m2 - 1; jj >= pad + n; --jj) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)]);
-    ymin = fmin(ymin, fabs(y));
-  }
-
-  // symbols k = S-1 .. 0 sit at baseband index first + k*sps (modem.py:209 / :93)
-  int64_t k = S - 1;
-  int64_t next_n = p.first + k * p.sps;
-  const size_t sym_base = sym_index(s, S, 0, comp);
-  auto on_output = [&](int64_t i, double y) {
-    if (i == next_n) {                          // uniform branch: one store per symbol
-      sym[sym_base + (size_t)k * 64] = y;
-      --k;
-      next_n = k >= 0 ? next_n - p.sps : -1;   // BPSK: first == sps, so index 0 is not a symbol
-    }
-  };
-
-  const int64_t nc = n / CH;
-  const int64_t n_lo = nc * CH;
-  for (int64_t i = n - 1; i >= n_lo; --i) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, pad + i + qs, sl)]);
-    ymin = fmin(ymin, fabs(y));
-    on_output(i, y);
-  }
-  if (nc > 0) {
-    const double2* __restrict__ src =
-        reinterpret_cast<const double2*>(s3) + (size_t)(hg * 2 + comp) * m2_pairs * 32 + sl;
-    constexpr int PP = CH / 2;
-    double2 ra[PP], rb[PP], rc[PP];
-    auto load = [&](double2 (&r)[PP], int64_t cc0) {
-      const int64_t cc = cc0 < 0 ? 0 : cc0;
-      const int64_t qp = (pad + qs + cc * CH) >> 1;
-#pragma unroll
-      for (int kk = 0; kk < PP; ++kk) r[kk] = src[(size_t)(qp + kk) * 32];
-    };
-    auto run = [&](const double2 (&r)[PP], int64_t cc) {
-      if constexpr (SPS > 0) {
-        // chunk covers i in [cc*CH, cc*CH + CH); symbols at offsets SPS/2 + m*SPS
-        // with index k = (cc*CH + SPS/2 - first)/SPS + m = cc*(CH/SPS) + m
-        const size_t kb = sym_base + (size_t)(cc * (CH / SPS)) * 64;
-#pragma unroll
-        for (int kk = PP - 1; kk >= 0; --kk) {
-          double t0, t1;
-          const double y1 = pair_step2(c, zA, zB, r[kk].y, t1);
-          const double y0 = pair_step2(c, zA, zB, r[kk].x, t0);
-          ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
-          if ((2 * kk + 1) % SPS == SPS / 2) sym[kb + (size_t)((2 * kk + 1) / SPS) * 64] = y1;
-          if ((2 * kk) % SPS == SPS / 2) sym[kb + (size_t)((2 * kk) / SPS) * 64] = y0;
-        }
-      } else {
-#pragma unroll
-        for (int kk = PP - 1; kk >= 0; --kk) {
-          double t0, t1;
-          const double y1 = pair_step2(c, zA, zB, r[kk].y, t1);
-          on_output(cc * CH + 2 * kk + 1, y1);
-          const double y0 = pair_step2(c, zA, zB, r[kk].x, t0);
-          on_output(cc * CH + 2 * kk, y0);
-          ymin = fmin(ymin, fmin(fabs(t0), fabs(t1)));   // t == y on lane j=0
-        }
-      }
-    };
-    load(ra, nc - 1);
-    load(rb, nc - 2);
-    load(rc, nc - 3);
-    int64_t cc = nc - 1;
-    for (; cc >= 2; cc -= 3) {
-      run(ra, cc);
-      __builtin_amdgcn_sched_barrier(0);
-      load(ra, cc - 3);
-      __builtin_amdgcn_sched_barrier(0);
-      run(rb, cc - 1);
-      __builtin_amdgcn_sched_barrier(0);
-      load(rb, cc - 4);
-      __builtin_amdgcn_sched_barrier(0);
-      run(rc, cc - 2);
-      __builtin_amdgcn_sched_barrier(0);
-      load(rc, cc - 5);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (cc >= 0) run(ra, cc);
-    if (cc >= 1) run(rb, cc - 1);
-  }
-  // left-extension outputs are trimmed but still pass through the detector
-  for (int jj = pad - 1; jj >= 0; --jj) {
-    const double y = pair_step(c, zA, zB, s3[s3_index(hg, comp, m2_pairs, jj + qs, sl)]);
-    ymin = fmin(ymin, fabs(y));
-  }
-  const bool bad = (j == 0 && !(ymin >= kMinNormal)) || !__builtin_isfinite(zA) || !__builtin_isfinite(zB);
-  int fl = bad ? 1 : 0;
-  fl |= __shfl_xor(fl, 1);
-  if (j == 0 && s < buf.n_streams && fl) atomicOr(&buf.flags[s], 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -1799,25 +1135,6 @@ __global__ __launch_bounds__(64) void k_slice(PskBuffers buf, PskParams p) {
 // ---------------------------------------------------------------------------
 // host-side launchers (called from api.cpp)
 template <typename T>
-static hipError_t launch_bp(int nt, bool zodd, const PskBuffers& b, const PskParams& p, const Iir& f,
-                            hipStream_t st, int64_t groups) {
-  dim3 grid((unsigned)groups), block(kWave);
-  if (nt == 9 && zodd) { hipLaunchKernelGGL((k_bandpass<9, true, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 9) { hipLaunchKernelGGL((k_bandpass<9, false, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 7 && zodd) { hipLaunchKernelGGL((k_bandpass<7, true, T>), grid, block, 0, st, b, p, f); }
-  else if (nt == 7) { hipLaunchKernelGGL((k_bandpass<7, false, T>), grid, block, 0, st, b, p, f); }
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-template <typename T>
-static hipError_t launch_bp_quad(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  const int64_t g16 = (b.n_streams + 15) / 16;
-  hipLaunchKernelGGL((k_bandpass_quad<T>), dim3((unsigned)g16), dim3(kWave), 0, st, b, p, f);
-  return hipGetLastError();
-}
-
-template <typename T>
 static hipError_t launch_bp_row(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   // K1g once K1r would need more than one wave per SIMD (B > 4 x SIMDs: 4096
   // on an MI355X); K1r below (fewer instructions per wave, solo-faster).
@@ -1843,88 +1160,33 @@ static hipError_t launch_bp_row(const PskBuffers& b, const PskParams& p, const I
   return hipGetLastError();
 }
 
-// AMR_PSK_LAYOUT selects older lane layouts for A/B comparisons:
-//   "lane" = lane per stream (K1/K2/K3), "quad" = K1q + pair-split K2/K3;
-//   default = K1r + quad-split K2q/K3q
-static int psk_layout() {
-  static const int v = [] {
-    const char* e = getenv("AMR_PSK_LAYOUT");
-    if (!e) return 2;
-    if (e[0] == 'l') return 0;
-    if (e[0] == 'q') return 1;
-    return 2;
-  }();
-  return v;
-}
-static bool bandpass_lane_mode() { return psk_layout() == 0; }
-
 hipError_t launch_psk_bandpass(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  static const bool bp_quad = [] { const char* e = getenv("AMR_BP_QUAD"); return e && e[0] == '1'; }();
-  if (f.nt == 9 && psk_layout() == 2 && !bp_quad) {
-    switch (b.dtype) {
-      case kF32: return launch_bp_row<float>(b, p, f, st);
-      case kF64: return launch_bp_row<double>(b, p, f, st);
-      case kI16: return launch_bp_row<int16_t>(b, p, f, st);
-    }
-    return hipErrorInvalidValue;
-  }
-  if (f.nt == 9 && !bandpass_lane_mode()) {
-    switch (b.dtype) {
-      case kF32: return launch_bp_quad<float>(b, p, f, st);
-      case kF64: return launch_bp_quad<double>(b, p, f, st);
-      case kI16: return launch_bp_quad<int16_t>(b, p, f, st);
-    }
-    return hipErrorInvalidValue;
-  }
-  const int64_t groups = (b.n_streams + kWave - 1) / kWave;
+  if (f.nt != 9) return hipErrorInvalidValue;   // butter(4, band): the plan checks
   switch (b.dtype) {
-    case kF32: return launch_bp<float>(f.nt, p.bp_zero_odd != 0, b, p, f, st, groups);
-    case kF64: return launch_bp<double>(f.nt, p.bp_zero_odd != 0, b, p, f, st, groups);
-    case kI16: return launch_bp<int16_t>(f.nt, p.bp_zero_odd != 0, b, p, f, st, groups);
+    case kF32: return launch_bp_row<float>(b, p, f, st);
+    case kF64: return launch_bp_row<double>(b, p, f, st);
+    case kI16: return launch_bp_row<int16_t>(b, p, f, st);
   }
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_psk_lowpass_fwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
   if (e != hipSuccess) return e;
-  const char* v = getenv("AMR_K2_VARIANT");
-  const int var = v ? atoi(v) : 0;
-  if (psk_layout() == 2) {
-    // a multiple of 16 blocks: the XCD pairing in k_lowpass_fwd_q is a bijection
-    const dim3 gq((unsigned)((2 * ((b.n_streams + 15) / 16) + 15) / 16 * 16)), bq(kWave);
-    hipLaunchKernelGGL(k_lowpass_fwd_q, gq, bq, 0, st, b, p, f);
-    return hipGetLastError();
-  }
-  const dim3 grid((unsigned)(4 * groups)), block(kWave);
-  switch (var) {
-    case 1: hipLaunchKernelGGL(k_lowpass_fwd<1>, grid, block, 0, st, b, p, f); break;
-    case 2: hipLaunchKernelGGL(k_lowpass_fwd<2>, grid, block, 0, st, b, p, f); break;
-    case 3: hipLaunchKernelGGL(k_lowpass_fwd<3>, grid, block, 0, st, b, p, f); break;
-    case 4: hipLaunchKernelGGL(k_lowpass_fwd<4>, grid, block, 0, st, b, p, f); break;
-    default: hipLaunchKernelGGL(k_lowpass_fwd<0>, grid, block, 0, st, b, p, f); break;
-  }
+  // a multiple of 16 blocks: the XCD pairing in k_lowpass_fwd_q is a bijection
+  const dim3 gq((unsigned)((2 * ((b.n_streams + 15) / 16) + 15) / 16 * 16)), bq(kWave);
+  hipLaunchKernelGGL(k_lowpass_fwd_q, gq, bq, 0, st, b, p, f);
   return hipGetLastError();
 }
 
 hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  if (psk_layout() == 2) {
-    const dim3 gq((unsigned)(2 * ((b.n_streams + 15) / 16))), bq(kWave);
-    if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd_q<10>), gq, bq, 0, st, b, p, f);
-    else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd_q<5>), gq, bq, 0, st, b, p, f);
-    else if (p.sps == 20 && p.first == 10) hipLaunchKernelGGL((k_lowpass_bwd_q<20>), gq, bq, 0, st, b, p, f);
-    else hipLaunchKernelGGL((k_lowpass_bwd_q<0>), gq, bq, 0, st, b, p, f);
-    return hipGetLastError();
-  }
-  const dim3 grid((unsigned)(4 * groups)), block(kWave);
-  if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd<10>), grid, block, 0, st, b, p, f);
-  else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd<5>), grid, block, 0, st, b, p, f);
-  else if (p.sps == 20 && p.first == 10) hipLaunchKernelGGL((k_lowpass_bwd<20>), grid, block, 0, st, b, p, f);
-  else hipLaunchKernelGGL((k_lowpass_bwd<0>), grid, block, 0, st, b, p, f);
+  const dim3 gq((unsigned)(2 * ((b.n_streams + 15) / 16))), bq(kWave);
+  if (p.sps == 10 && p.first == 5) hipLaunchKernelGGL((k_lowpass_bwd_q<10>), gq, bq, 0, st, b, p, f);
+  else if (p.sps == 5 && p.first == 2) hipLaunchKernelGGL((k_lowpass_bwd_q<5>), gq, bq, 0, st, b, p, f);
+  else if (p.sps == 20 && p.first == 10) hipLaunchKernelGGL((k_lowpass_bwd_q<20>), gq, bq, 0, st, b, p, f);
+  else hipLaunchKernelGGL((k_lowpass_bwd_q<0>), gq, bq, 0, st, b, p, f);
   return hipGetLastError();
 }
 
