@@ -786,32 +786,48 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
   constexpr int64_t kC0 = kLpChunk / kLpQChunk;   // chunks covered by the generic loop
   if (nc > kC0) {
     // main body: bb = f * lo_c (equal to f*lo_c + addend whenever it is not a
-    // zero, and a zero is flagged).  f and the LO multipliers arrive through
-    // register rings (f R chunks deep, LO R/2).  The LO is wave-uniform, but
-    // scalar loads would not do: SMEM returns out of order, so every use of
-    // one waits for all of them (lgkmcnt(0)), and the table falls out of L2
-    // under the streaming traffic.  Loads run up to R chunks past the
-    // stream's end into the plan's slack (api.cpp) instead of clamping: every
-    // instruction here costs a wave issue slot.  (An LDS-DMA ring as in K1r's
-    // backward pass measured slower here: 4.4 vs 3.5 ms.)
-    constexpr int CH = kLpQChunk, PP = CH / 2, R = kLpQRing, RL = R / 2;
-    static_assert(R % RL == 0, "the LO ring must divide the f ring");
+    // zero, and a zero is flagged).  At 2+ waves per CU this kernel is bound
+    // by the texture addresser (TA), which spends the same cycles on a 64-lane
+    // memory instruction whatever it holds: the f loads move
+    // 256 B of distinct data each (a quad shares its stream's 16 B), and the
+    // old wave-uniform LO loads and quad-shared stores 16 B and 256 B.  So:
+    //   * LO: one 16-B load per lane brings 128 samples (1 KiB) into an LDS
+    //     ring of 4 blocks, two blocks ahead; the register ring then reads
+    //     it by broadcast ds_read_b128 (no TA);
+    //   * stores: each pair goes into an LDS staging image (every lane writes
+    //     its own 16 B: contiguous, conflict-free), read back once per chunk
+    //     as this lane's 16 B of the chunk's 1 KiB of s3 and stored one chunk
+    //     later -- one store instruction per 8 samples instead of four.
+    // f keeps its register ring (R chunks deep).  Loads run up to R chunks
+    // (LO: 3 blocks) past the stream's end into the plan's slack (api.cpp)
+    // instead of clamping: every instruction here costs a wave issue slot.
+    constexpr int CH = kLpQChunk, PP = CH / 2, R = kLpQRing, RL = 2;
+    constexpr int LB = 128;                     // LO samples per LDS block (16 B per lane)
+    constexpr int CPB = LB / CH;                // chunks per LO block = one loop iteration
+    static_assert(CPB == 2 * R && R % RL == 0, "loop iteration = one LO block = two f rings");
+    __shared__ __attribute__((aligned(16))) double2 lo_ring[4][LB / 2];
+    __shared__ __attribute__((aligned(16))) double2 stage[2][PP][16][4];   // [buf][pair][stream][quad lane]
     double2 fr[R][PP];
-    double2 lr[RL][PP];                         // LO multipliers, wave-uniform (a pair per dwordx4)
-    const double2* __restrict__ fnext = fsrc + (size_t)kC0 * PP * 32;   // next chunk to load
-    const double2* __restrict__ lnext = reinterpret_cast<const double2*>(loc + kC0 * CH);
-    double2* __restrict__ dst = reinterpret_cast<double2*>(s3) + (s3q_index(w, comp, m2_pairs, pad + qs + kC0 * CH, sq) >> 1);
+    double2 lr[RL][PP];                         // LO multipliers (wave-uniform, a pair per ds_read_b128)
+    const double2* __restrict__ fnext = fsrc + (size_t)kC0 * PP * 32;   // next f chunk to load
+    const double2* __restrict__ lblk = reinterpret_cast<const double2*>(loc + kC0 * CH) + lane;
+    double2* __restrict__ dstc = reinterpret_cast<double2*>(s3) + (s3q_index(w, comp, m2_pairs, pad + qs + kC0 * CH, 0) >> 1) + lane;
+    // the first chunk has no predecessor: its "previous image" goes to the
+    // plan's front slack below s3 (api.cpp kFrontSlack), never read as data
+    double2* __restrict__ pdst = reinterpret_cast<double2*>(s3) - 64 + lane;
+    double2 img = make_double2(0.0, 0.0);
+    double2* const swr = &stage[0][0][0][0] + lane;                       // this lane's slot of pair 0
+    const double2* const srd = &stage[0][lane >> 4][lane & 15][((lane & 15) >> 1) & 3];
     auto loadf = [&](double2 (&d)[PP]) {
 #pragma unroll
       for (int k = 0; k < PP; ++k) d[k] = fnext[k * 32];
       fnext += PP * 32;
     };
-    auto loadl = [&](double2 (&d)[PP]) {
+    auto loadl = [&](double2 (&d)[PP], const double2* src) {
 #pragma unroll
-      for (int k = 0; k < PP; ++k) d[k] = lnext[k];
-      lnext += PP;
+      for (int k = 0; k < PP; ++k) d[k] = src[k];
     };
-    auto run = [&](const double2 (&fv)[PP], const double2 (&lv)[PP]) {
+    auto run = [&](const double2 (&fv)[PP], const double2 (&lv)[PP], int sb) {
 #pragma unroll
       for (int k = 0; k < PP; ++k) {
         const double e0v = fv[k].x * lv[k].x;
@@ -820,38 +836,57 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
         const double y1 = quad5_step(c, z, e1v);
         acc = tiny_min3(acc, e0v, e1v);
         acc = tiny_min3(acc, y0, y1);
-        dst[k * 16] = make_double2(y0, y1);     // all 4 lanes of the quad: the same 16 B
+        swr[(sb * PP + k) * 64] = make_double2(y0, y1);
       }
-      dst += PP * 16;
+      *pdst = img;                              // the previous chunk's 16 B (read back a chunk ago)
+      img = srd[sb * PP * 64];                  // this chunk's (LDS keeps a wave's accesses in order)
+      pdst = dstc;
+      dstc += PP * 16;
     };
-    // ring slot u holds chunk cc+u (LO: slot u % RL); each slot is refilled
-    // right after it is consumed (f R chunks ahead, LO RL chunks ahead), so
-    // no control flow sits inside the loop.  Issue order matters: vmcnt
-    // retires in order, so slot 0 must be the oldest.
+    // prologue: LO blocks 0 and 1, then the rings
+    lo_ring[0][lane] = lblk[0];
+    lo_ring[1][lane] = lblk[LB / 2];
+    lblk += LB;
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       loadf(fr[u]);
-      if (u < RL) loadl(lr[u]);
+      if (u < RL) loadl(lr[u], &lo_ring[0][u * PP]);
       __builtin_amdgcn_sched_barrier(0);
     }
+    // iteration ib covers LO block ib (chunks kC0 + 16 ib ...): it loads
+    // block ib+2 at its start and writes it to the ring half way, where slot
+    // (ib+2)&3 last held block ib-2, long consumed
     int64_t cc = kC0;
-    for (; cc + R <= nc; cc += R) {
+    int ib = 0;
+    for (; cc + CPB <= nc; cc += CPB, ++ib) {
+      const double2* const l0 = &lo_ring[ib & 3][0];
+      const double2* const l1 = &lo_ring[(ib + 1) & 3][0];
+      double2* const lw = &lo_ring[(ib + 2) & 3][lane];
+      double2 lpend;
 #pragma unroll
-      for (int u = 0; u < R; ++u) {
-        run(fr[u], lr[u % RL]);
+      for (int u = 0; u < CPB; ++u) {
+        if (u == 0) { lpend = *lblk; lblk += LB / 2; }
+        if (u == R) *lw = lpend;
+        run(fr[u % R], lr[u % RL], u & 1);
         __builtin_amdgcn_sched_barrier(0);
-        loadf(fr[u]);
-        loadl(lr[u % RL]);
+        loadf(fr[u % R]);
+        loadl(lr[u % RL], u + RL < CPB ? l0 + (u + RL) * PP : l1 + (u + RL - CPB) * PP);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    {
+      // tail (< 16 chunks of block ib, written one iteration ago)
+      const double2* const l0 = &lo_ring[ib & 3][0];
 #pragma unroll
-    for (int u = 0; u < R; ++u) {
-      if (cc + u < nc) {
-        run(fr[u], lr[u % RL]);
-        if (u + RL < R) loadl(lr[u % RL]);     // LO for chunk cc+u+RL (still inside the tail)
+      for (int u = 0; u < CPB; ++u) {
+        if (cc + u < nc) {
+          run(fr[u % R], lr[u % RL], u & 1);
+          if (u < R) loadf(fr[u]);
+          if (u + RL < CPB) loadl(lr[u % RL], l0 + (u + RL) * PP);
+        }
       }
     }
+    *pdst = img;
   }
   for (int64_t i = n_main > n_gen ? n_main : n_gen; i < n; ++i) {
     const double e = X(i);
