@@ -40,7 +40,7 @@ EXPORTS = [
     "amr_abi_version", "amr_last_error", "amr_device_count", "amr_set_device", "amr_malloc", "amr_free",
     "amr_memcpy_h2d", "amr_memcpy_d2h", "amr_memcpy_d2d", "amr_device_synchronize",
     "amr_psk_plan_create", "amr_psk_plan_destroy", "amr_psk_plan_out_capacity", "amr_psk_plan_scratch_bytes",
-    "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings",
+    "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings", "amr_psk_plan_set_inflight",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
@@ -153,6 +153,7 @@ def lib():
             "amr_psk_plan_scratch_bytes": (I64, [P]),
             "amr_psk_plan_synchronize": (I32, [P]),
             "amr_psk_plan_enable_timing": (I32, [P, I32]),
+            "amr_psk_plan_set_inflight": (I32, [P, I32]),
             "amr_psk_plan_timings": (I32, [P, P, I32]),
             "amr_psk_plan_exact_streams": (I32, [P, P]),
             "amr_psk_demod_host": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
@@ -317,6 +318,10 @@ class PskPlan:
 
     def enable_timing(self, on=True):
         check(lib().amr_psk_plan_enable_timing(self.handle, 1 if on else 0))
+
+    def set_inflight(self, batches: int):
+        """Hint: `batches` batches are kept in flight at once, each on its own plan."""
+        check(lib().amr_psk_plan_set_inflight(self.handle, int(batches)))
 
     def timings(self) -> dict:
         ms = (ctypes.c_float * len(T_NAMES))()

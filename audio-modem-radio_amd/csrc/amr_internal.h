@@ -48,6 +48,7 @@ struct PskBuffers {
   int64_t x_stride;       // elements
   int dtype;
   int64_t n_streams;      // B
+  int inflight;           // batches the caller keeps in flight (amr_psk_plan_set_inflight), >= 1
   const double* lo;       // [n][4]: (lo_re, -(0*lo_im), lo_im, 0*lo_re)
   const double* lo2;      // [2][n]: lo_re[n], lo_im[n] (the multipliers alone)
   double* s1;             // band-pass forward output  [G][m1p/2][64][2]

@@ -138,6 +138,7 @@ struct amr_psk_plan {
   int32_t* d_crc = nullptr;
   // timing
   bool timing = false;
+  int inflight = 1;             // amr_psk_plan_set_inflight hint
   hipEvent_t ev[AMR_T_COUNT + 1][2]{};
   bool ev_used[AMR_T_COUNT]{};
   int64_t last_exact = 0;
@@ -363,6 +364,14 @@ int amr_psk_plan_enable_timing(amr_psk_plan* plan, int on) {
   return AMR_OK;
 }
 
+int amr_psk_plan_set_inflight(amr_psk_plan* plan, int batches) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  if (batches < 1) return fail(AMR_E_INVALID, "batches in flight must be >= 1");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  plan->inflight = batches;
+  return AMR_OK;
+}
+
 int amr_psk_plan_timings(amr_psk_plan* plan, float* ms, int count) {
   if (!plan || !ms) return fail(AMR_E_INVALID, "NULL argument");
   std::lock_guard<std::mutex> lk(plan->mu);
@@ -409,6 +418,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   b.x_stride = x_stride;
   b.dtype = dtype;
   b.n_streams = B;
+  b.inflight = pl->inflight;
   b.lo = pl->lo;
   b.lo2 = pl->lo2;
   b.s1 = pl->s1;

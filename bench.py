@@ -115,7 +115,7 @@ def main():
     ap.add_argument("--cpu-streams", type=int, default=0, help="cpu_baseline sample size (0 = auto ~10 s CPU)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight on separate HIP streams / plans (0 = 2 for the PSK workloads, 1 for "
+                    help="batches in flight on separate HIP streams / plans (0 = 3 for the PSK workloads, 1 for "
                          "fsk9600): batch k+1's band-pass overlaps batch k's low-pass passes")
     args = ap.parse_args()
 
@@ -149,7 +149,7 @@ def main():
         x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
     log(f"[rank {rank}] synthesised {B}x{N} float32 in {time.perf_counter() - t0:.1f}s")
 
-    inflight = args.inflight or (1 if fsk else 2)
+    inflight = args.inflight or (1 if fsk else 3)
     if fsk:
         import _fsk
         plans = [_fsk.FskPlan(N, baud, args.mark, args.space, FS, max_streams=B, device=dev) for _ in range(inflight)]
@@ -164,6 +164,8 @@ def main():
         demod, sync_fn, names = L.amr_psk_demod_device, L.amr_psk_plan_synchronize, _amr.T_NAMES
     for pl in plans:
         pl.enable_timing(True)
+        if not fsk:
+            pl.set_inflight(inflight)
     cap = plan.out_cap
 
     def dmalloc(nbytes):

@@ -123,6 +123,12 @@ int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
 int amr_psk_plan_synchronize(amr_psk_plan *plan);
 /* record per-kernel HIP events on the plan's stream (1) or not (0) */
 int amr_psk_plan_enable_timing(amr_psk_plan *plan, int on);
+/* hint: the caller keeps `batches` batches in flight at once, each on its own
+ * plan (stream); the band-pass layout is then chosen for n_streams x batches
+ * concurrent streams.  Default 1.  No reference counterpart:
+ * a batching knob of this build (the reference decodes one stream per call,
+ * decoder.py:417-464). */
+int amr_psk_plan_set_inflight(amr_psk_plan *plan, int batches);
 /* milliseconds of each AMR_T_* kernel in the last call (-1 = not run) */
 int amr_psk_plan_timings(amr_psk_plan *plan, float *ms, int count);
 /* number of streams the exact complex low-pass path re-ran in the last call */

@@ -127,3 +127,10 @@ def test_frame_parse_argument_checks(built_lib):
     assert L.amr_frame_parse_host(None, 0, None, 0, 1, None, None) == _amr.AMR_OK          # empty batch
     with pytest.raises(_amr.AmrError):
         _amr.frame_parse([b"FBPC"])                                                         # no GPU here
+
+
+def test_set_inflight_argument_checks(built_lib):
+    import _amr
+    L = _amr.lib()
+    assert L.amr_psk_plan_set_inflight(None, 2) == _amr.AMR_E_INVALID
+    assert b"plan is NULL" in L.amr_last_error()
