@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=64, help="distinct waveforms (noise is per stream)")
     ap.add_argument("--cpu-streams", type=int, default=0, help="cpu_baseline sample size (0 = auto ~10 s CPU)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight on separate HIP streams / plans (0 = 3 for the PSK workloads, 1 for "
                          "fsk9600): batch k+1's band-pass overlaps batch k's low-pass passes")
@@ -311,6 +312,30 @@ def main():
     _amr.check(L.amr_memcpy_d2h(_amr.ptr(out), g_out, B * cap))
     _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
 
+    # PCIe-inclusive rate (never `value`): the host API on the
+    # same batch from pageable host memory -- H2D of the float32 samples, the
+    # demod, D2H of the bytes -- one batch at a time; the first call is warmup
+    host_path = None
+    if rank == 0 and world == 1 and not fec_fused and not args.no_host_path:
+        host_fn = L.amr_fsk_demod_host if fsk else L.amr_psk_demod_host
+        h_out = np.empty((B, cap), np.uint8)
+        h_len = np.empty(B, np.int64)
+        h_sync = np.empty(B, np.int64)
+        hts = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            _amr.check(host_fn(plan.handle, _amr.ptr(x), _amr.DTYPE_F32, B, N, _amr.ptr(h_out), cap,
+                               _amr.ptr(h_len), _amr.ptr(h_sync)))
+            hts.append(time.perf_counter() - t1)
+        ht = min(hts[1:])
+        same = bool(np.array_equal(h_len, ln) and all(h_out[i, :ln[i]].tobytes() == out[i, :ln[i]].tobytes()
+                                                      for i in range(B)))
+        host_path = {"ms_per_batch": round(ht * 1e3, 2), "value": round(B * sym_per_stream / ht / 1e6, 3),
+                     "unit": "Msym/s", "input_gb": round(x.nbytes / 1e9, 3),
+                     "what": "amr_%s_demod_host from pageable host float32, one batch at a time (H2D + demod + D2H)"
+                             % ("fsk" if fsk else "psk"),
+                     "bytes_equal_device_path": same}
+
     result = None
     if rank == 0:
         threads = max(1, min(16, os.cpu_count() or 1))
@@ -387,6 +412,7 @@ def main():
             "kernel_ms_solo": {k: round(v, 4) for k, v in solo.items()},
             "cpu_baseline": cpu,
             "parity": parity,
+            "host_path_pcie_inclusive": host_path,
         }
         if not fsk:
             result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
