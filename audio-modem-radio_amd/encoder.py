@@ -68,7 +68,6 @@ def get_file_signature(file_path: str, mode: str, compress: bool, symbol_rate: i
 
 def clear_encoding_cache():
     get_file_signature.cache_clear()
-    logger.info("🧹 Cache de encoding limpo")
 
 
 _encoding_cancelled = False
@@ -135,39 +134,43 @@ def split_file_for_transmission(file_path: str, mode: str, symbol_rate: int,
     return parts
 
 
+# encode_file_parts' modulator dispatch (encoder.py:179-212): mode -> (modulator,
+# keyword arguments; SR stands for the call's symbol_rate).  The calls are the
+# reference's, keywords included -- the aliases that do not take them raise the
+# reference's TypeError.
+_SR = object()
+_PART_CALLS = {
+    "FSK1200": (fsk_modulate, {"baud": 1200, "mark_freq": 1200.0, "space_freq": 2200.0}),
+    "FSK9600": (fsk_modulate, {"baud": 9600}),
+    "BPSK": (bpsk_modulate, {"baud": _SR, "carrier": 3000.0}),
+    "QPSK": (qpsk_modulate, {"baud": _SR, "carrier": 3000.0}),
+    "8PSK": (psk8_modulate, {"baud": _SR, "carrier": 12000.0}),
+    "FSK19200": (fsk_high_speed_modulate, {"baud": 19200}),
+    "OFDM4": (ofdm_modulate_simple, {"baud": _SR, "carrier": 12000.0, "num_subcarriers": 4}),
+    "OFDM8": (ofdm_modulate_simple, {"baud": _SR, "carrier": 12000.0, "num_subcarriers": 8}),
+    "APSK16": (apsk16_modulate, {"baud": _SR, "carrier": 12000.0}),
+    "DSSS": (dsss_modulate, {"baud": _SR, "carrier": 3000.0}),
+    "MSK": (msk_modulate, {"baud": _SR, "carrier": 6000.0}),
+    "FT8": (ft8_modulate, {"baud": _SR, "carrier": 3000.0}),
+    "PSK31": (psk31_modulate, {"baud": _SR, "carrier": 3000.0}),
+    "FELD_HELL": (feld_hell_modulate, {"baud": 122.5, "carrier": 1000.0}),
+}
+
+
 def _modulate_part(framed: bytes, mode: str, symbol_rate: int) -> np.ndarray:
-    """The modulator dispatch of encode_file_parts (encoder.py:179-212), calls as written."""
-    if mode == "FSK1200":
-        return fsk_modulate(framed, baud=1200, mark_freq=1200.0, space_freq=2200.0)
-    elif mode == "FSK9600":
-        return fsk_modulate(framed, baud=9600)
-    elif mode == "BPSK":
-        return bpsk_modulate(framed, baud=symbol_rate, carrier=3000.0)
-    elif mode == "QPSK":
-        return qpsk_modulate(framed, baud=symbol_rate, carrier=3000.0)
-    elif mode == "8PSK":
-        return psk8_modulate(framed, baud=symbol_rate, carrier=12000.0)
-    elif mode == "FSK19200":
-        return fsk_high_speed_modulate(framed, baud=19200)
-    elif mode == "OFDM4":
-        return ofdm_modulate_simple(framed, baud=symbol_rate, carrier=12000.0, num_subcarriers=4)
-    elif mode == "OFDM8":
-        return ofdm_modulate_simple(framed, baud=symbol_rate, carrier=12000.0, num_subcarriers=8)
-    elif mode == "APSK16":
-        return apsk16_modulate(framed, baud=symbol_rate, carrier=12000.0)
-    elif mode == "DSSS":
-        return dsss_modulate(framed, baud=symbol_rate, carrier=3000.0)
-    elif mode == "MSK":
-        return msk_modulate(framed, baud=symbol_rate, carrier=6000.0)
-    elif mode == "HELLSCHREIBER":
+    if mode == "HELLSCHREIBER":
         raise NotImplementedError("Hellschreiber (hellschreiber.py) is outside this build's scope (SURVEY §2)")
-    elif mode == "FT8":
-        return ft8_modulate(framed, baud=symbol_rate, carrier=3000.0)
-    elif mode == "PSK31":
-        return psk31_modulate(framed, baud=symbol_rate, carrier=3000.0)
-    elif mode == "FELD_HELL":
-        return feld_hell_modulate(framed, baud=122.5, carrier=1000.0)
-    raise ValueError(f"Modo desconhecido: {mode}")
+    if mode not in _PART_CALLS:
+        raise ValueError(f"Modo desconhecido: {mode}")
+    fn, kw = _PART_CALLS[mode]
+    return fn(framed, **{k: (symbol_rate if v is _SR else v) for k, v in kw.items()})
+
+
+def _test_tone(n_framed: int, symbol_rate: float) -> np.ndarray:
+    """Last-resort 1 kHz tone of encode_file_parts (encoder.py:225-228)."""
+    duration = max(n_framed / symbol_rate, 1.0)
+    t = np.linspace(0, duration, int(SAMPLE_RATE * duration))
+    return 0.8 * np.sin(2 * np.pi * 1000 * t).astype(np.float32)
 
 
 def _write_wav(outname: str, wavb: bytes) -> None:
@@ -178,44 +181,34 @@ def _write_wav(outname: str, wavb: bytes) -> None:
 
 def encode_file_parts(file_parts: List[tuple], mode: str, compress: bool, symbol_rate: int,
                       progress_callback=None, is_cancelled=None) -> List[str]:
-    """encoder.py:154-252, including the BPSK / test-tone fallbacks on invalid audio."""
-    encoded_files = []
-    total_parts = len(file_parts)
-    for idx, (fname, data, part_number, total_parts, file_size, file_crc) in enumerate(file_parts):
+    """encoder.py:154-252: per part adaptive_compress -> frame -> modulate; invalid
+    audio falls back to BPSK at min(symbol_rate, 4800), then to a test tone."""
+    written = []
+    for k, (fname, data, part_number, total_parts, file_size, file_crc) in enumerate(file_parts):
         if is_cancelled and is_cancelled():
             raise RuntimeError("Codificação cancelada pelo usuário")
-        logger.info(f"Codificando parte {idx + 1}/{total_parts}: {fname}")
-        if compress:
-            data = adaptive_compress(data, mode)
-        framed = _frame_data(fname, data, part_number, total_parts, file_size, file_crc)
-        logger.info(f"🎯 Modulando com modo: {mode}, taxa: {symbol_rate}")
-        arr = _modulate_part(framed, mode, symbol_rate)
-        if not verify_audio_output(arr):
-            logger.error(f"❌ ERRO: Modulação {mode} produziu áudio inválido para a parte {part_number + 1}!")
-            fallback_symbol_rate = min(symbol_rate, 4800)
-            arr = bpsk_modulate(framed, baud=fallback_symbol_rate, carrier=3000.0)
-            if not verify_audio_output(arr):
-                logger.error("❌ FALHA CRÍTICA: Fallback BPSK também falhou!")
-                duration = max(len(framed) / fallback_symbol_rate, 1.0)
-                t = np.linspace(0, duration, int(SAMPLE_RATE * duration))
-                arr = 0.8 * np.sin(2 * np.pi * 1000 * t).astype(np.float32)
-                if not verify_audio_output(arr):
+        payload = adaptive_compress(data, mode) if compress else data
+        framed = _frame_data(fname, payload, part_number, total_parts, file_size, file_crc)
+        audio = _modulate_part(framed, mode, symbol_rate)
+        if not verify_audio_output(audio):
+            slow = min(symbol_rate, 4800)
+            audio = bpsk_modulate(framed, baud=slow, carrier=3000.0)
+            if not verify_audio_output(audio):
+                audio = _test_tone(len(framed), slow)
+                if not verify_audio_output(audio):
                     raise ValueError(
                         "Falha crítica na geração de áudio modulado - não foi possível produzir áudio válido")
-        wavb = wav_from_array(arr, SAMPLE_RATE)
-        if len(wavb) < 100:
-            logger.warning("❌ AVISO: Arquivo WAV gerado é muito pequeno, possivelmente corrompido")
-        outname = os.path.join(CACHE_DIR, f"{fname}.{mode}.sr{symbol_rate}.wav")
-        _write_wav(outname, wavb)
-        if os.path.exists(outname) and os.path.getsize(outname) > 100:
-            logger.info(f"✅ Arquivo salvo: {outname} ({os.path.getsize(outname)} bytes)")
-            encoded_files.append(outname)
-        else:
-            logger.error(f"❌ ERRO: Falha ao salvar arquivo {outname}")
-            raise IOError(f"Falha ao salvar arquivo codificado: {outname}")
+        wav = wav_from_array(audio, SAMPLE_RATE)
+        if len(wav) < 100:
+            logger.warning("WAV under 100 bytes for %s", fname)
+        path = os.path.join(CACHE_DIR, f"{fname}.{mode}.sr{symbol_rate}.wav")
+        _write_wav(path, wav)
+        if not (os.path.exists(path) and os.path.getsize(path) > 100):
+            raise IOError(f"Falha ao salvar arquivo codificado: {path}")
+        written.append(path)
         if progress_callback:
-            progress_callback(idx + 1, total_parts)
-    return encoded_files
+            progress_callback(k + 1, total_parts)
+    return written
 
 
 def encode_hellschreiber_text(text: str):
@@ -311,26 +304,27 @@ def get_encoding_stats(file_path, mode, compress, symbol_rate):
     }
 
 
+# encoder.py:321-330, in the reference's order (a failure is logged by name)
+_AUDIO_CHECKS = (
+    ("Array não é None", lambda a: a is not None),
+    ("Array não vazio", lambda a: len(a) > 0),
+    ("Não é tudo zero", lambda a: not np.all(a == 0)),
+    ("Duração mínima", None),                       # needs expected_min_duration
+    ("Tem variação", lambda a: np.std(a) >= 0.01),
+    ("Sem NaN", lambda a: not np.any(np.isnan(a))),
+    ("Sem infinitos", lambda a: not np.any(np.isinf(a))),
+    ("Valores dentro do range", lambda a: np.all(np.abs(a) <= 1.0)),
+)
+
+
 def verify_audio_output(audio_array: np.ndarray, expected_min_duration: float = 0.1) -> bool:
-    """encoder.py:318-348: eight validity checks, each failure logged."""
-    checks = [
-        ("Array não é None", audio_array is not None),
-        ("Array não vazio", len(audio_array) > 0),
-        ("Não é tudo zero", not np.all(audio_array == 0)),
-        ("Duração mínima", len(audio_array) / SAMPLE_RATE >= expected_min_duration),
-        ("Tem variação", np.std(audio_array) >= 0.01),
-        ("Sem NaN", not np.any(np.isnan(audio_array))),
-        ("Sem infinitos", not np.any(np.isinf(audio_array))),
-        ("Valores dentro do range", np.all(np.abs(audio_array) <= 1.0)),
-    ]
-    failed = [name for name, ok in checks if not ok]
-    for name in failed:
-        logger.warning(f"❌ Verificação de áudio falhou: {name}")
+    """encoder.py:318-348: True when every check passes."""
+    failed = []
+    for name, pred in _AUDIO_CHECKS:
+        ok = (len(audio_array) / SAMPLE_RATE >= expected_min_duration) if pred is None else pred(audio_array)
+        if not ok:
+            failed.append(name)
     if failed:
-        logger.error(f"❌ Áudio inválido. Falhas: {', '.join(failed)}")
+        logger.error("audio rejected: %s", ", ".join(failed))
         return False
-    duration = len(audio_array) / SAMPLE_RATE
-    dynamic_range = np.max(audio_array) - np.min(audio_array)
-    logger.info(f"✅ Áudio válido: {duration:.3f}s, {len(audio_array)} amostras, "
-                f"variação: {np.std(audio_array):.6f}, dynamic_range: {dynamic_range:.6f}")
     return True
