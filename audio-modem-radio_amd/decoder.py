@@ -10,6 +10,11 @@ error behaviour; the demodulation itself runs on the MI355X via modem.py.
   parse_fbp_stream_enhanced  decoder.py:142-208   (+ parse_fbp_stream_enhanced_batch:
                              the scan and payload CRCs on the GPU, k_frame_parse)
   smart_decompress           decoder.py:210-243
+  FileAssembly / AdvancedFileAssembly
+                             decoder.py:20-122  (multi-part reassembly, part quality)
+  save_decoded_files         decoder.py:247-310
+  decode_with_retry          decoder.py:313-377 (three demod attempts at
+                             symbol_rate, x0.95, x1.05 -- each on the GPU)
   find_frame_start           decoder.py:470-478
   get_assembly_status / get_reception_stats / clear_reception_stats
                              decoder.py:467, 481-513
@@ -147,6 +152,200 @@ def smart_decompress(compressed_data: bytes) -> bytes:
     except Exception as e:
         print(f"⚠️ Erro na descompressão inteligente: {e}")
         return compressed_data
+
+
+# ---------------------------------------------------------------------------
+class FileAssembly:
+    """Multi-part file reassembly (decoder.py:20-116): parts keep the copy of best
+    signal quality; the file is the parts in order (size / CRC mismatches are
+    only reported, as the reference does)."""
+
+    def __init__(self, filename: str, total_parts: int, file_size: int, file_crc: int):
+        self.filename = filename
+        self.total_parts = total_parts
+        self.file_size = file_size
+        self.expected_crc = file_crc
+        self.parts = [None] * total_parts
+        self.parts_quality = [0.0] * total_parts
+        self.received_parts = 0
+        self.creation_time = self.last_update = time.time()
+
+    def calculate_signal_quality(self, data: bytes) -> float:
+        """(1 - zero fraction) * distinct bytes / 256, halved when the payload is
+        its first 5 bytes repeated (decoder.py:32-55)."""
+        try:
+            n = len(data)
+            if n == 0:
+                return 0.0
+            zero_ratio = data.count(b'\x00') / n
+            unique_bytes = len(set(data)) / 256
+            penalty = 0.5 if n > 10 and data[:5] * (n // 5) == data[:n - n % 5] else 0
+            return max(0.0, min(1.0, (1 - zero_ratio) * unique_bytes * (1 - penalty)))
+        except Exception:
+            return 0.5
+
+    def add_part(self, part_number: int, data: bytes, signal_quality: float = None) -> bool:
+        """Store a part (a duplicate replaces the stored copy only if of higher
+        quality); True once every part is present (decoder.py:57-84)."""
+        if not 0 <= part_number < self.total_parts:
+            return False
+        q = self.calculate_signal_quality(data) if signal_quality is None else signal_quality
+        if self.parts[part_number] is None:
+            self.received_parts += 1
+        elif q > self.parts_quality[part_number]:
+            print(f"Substituindo parte {part_number} (qualidade {self.parts_quality[part_number]:.3f} -> {q:.3f})")
+        else:
+            print(f"Ignorando parte {part_number} duplicada com qualidade inferior "
+                  f"({q:.3f} <= {self.parts_quality[part_number]:.3f})")
+            return self.received_parts == self.total_parts
+        self.parts[part_number] = data
+        self.parts_quality[part_number] = q
+        self.last_update = time.time()
+        return self.received_parts == self.total_parts
+
+    def get_progress(self) -> float:
+        return (self.received_parts / self.total_parts) * 100 if self.total_parts > 0 else 0
+
+    def get_missing_parts(self) -> list:
+        return [i for i, part in enumerate(self.parts) if part is None]
+
+    def assemble_file(self) -> bytes:
+        if self.received_parts != self.total_parts:
+            raise ValueError(f"Partes insuficientes: {self.received_parts}/{self.total_parts}. "
+                             f"Faltando: {self.get_missing_parts()}")
+        data = b''.join(self.parts)
+        if len(data) != self.file_size:
+            print(f"Aviso: Tamanho do arquivo diferente. Esperado: {self.file_size}, Obtido: {len(data)}")
+        crc = binascii.crc32(data) & 0xffffffff
+        if crc != self.expected_crc:
+            print(f"Aviso: CRC diferente. Esperado: {self.expected_crc:08X}, Obtido: {crc:08X}")
+        return data
+
+    def is_expired(self, timeout_seconds: int = 3600) -> bool:
+        return (time.time() - self.last_update) > timeout_seconds
+
+    def get_quality_report(self) -> dict:
+        q = self.parts_quality
+        return {'average_quality': sum(q) / len(q) if q else 0, 'min_quality': min(q) if q else 0,
+                'max_quality': max(q) if q else 0, 'completed_parts': self.received_parts,
+                'total_parts': self.total_parts}
+
+
+class AdvancedFileAssembly(FileAssembly):
+    """decoder.py:119-122 (no additions in the reference)."""
+
+
+def _safe_name(fname: str) -> str:
+    return "".join(c for c in fname if c.isalnum() or c in (' ', '-', '_', '.'))
+
+
+def _write_received(fname: str, data: bytes) -> str:
+    os.makedirs(RECV_DIR, exist_ok=True)
+    path = os.path.join(RECV_DIR, f"recv_{int(time.time())}_{_safe_name(fname)}")
+    with open(path, 'wb') as f:
+        f.write(data)
+    reception_stats['total_files'] += 1
+    reception_stats['total_bytes'] += len(data)
+    reception_stats['last_reception'] = time.time()
+    return path
+
+
+def save_decoded_files(parsed: list) -> list:
+    """decoder.py:247-310.  Entries are (fname, payload, is_multi, part, total,
+    file_size, file_crc) tuples: single files are smart_decompress'ed and saved,
+    multi-part ones go through a FileAssembly keyed by name + CRC and are saved
+    (undecompressed) once complete; assemblies idle for an hour are dropped."""
+    saved = []
+    for fname, payload, is_multi, part_number, total_parts, file_size, file_crc in parsed:
+        if is_multi:
+            key = f"{fname}_{file_crc}"
+            if key not in file_assemblies:
+                file_assemblies[key] = AdvancedFileAssembly(fname, total_parts, file_size, file_crc)
+            asm = file_assemblies[key]
+            if asm.add_part(part_number, payload):
+                try:
+                    data = asm.assemble_file()
+                    if len(data) != asm.file_size:
+                        print(f"ALERTA: Tamanho do arquivo montado não corresponde! "
+                              f"Esperado: {asm.file_size}, Obtido: {len(data)}")
+                    crc = binascii.crc32(data) & 0xffffffff
+                    if crc != asm.expected_crc:
+                        print(f"ALERTA FINAL: CRC do arquivo montado não corresponde! "
+                              f"Esperado: {asm.expected_crc:08X}, Obtido: {crc:08X}")
+                    saved.append(_write_received(fname, data))
+                    print(f"Arquivo multi-partes montado com sucesso: {fname}")
+                    print(f"Relatório de qualidade: {asm.get_quality_report()}")
+                    del file_assemblies[key]
+                except Exception as e:
+                    print(f"Erro ao montar arquivo {fname}: {e}")
+            continue
+        try:
+            saved.append(_write_received(fname, smart_decompress(payload)))
+        except Exception as e:
+            print(f"Erro ao salvar arquivo {fname}: {e}")
+    for key in [k for k, a in file_assemblies.items() if a.is_expired()]:
+        a = file_assemblies.pop(key)
+        print(f"Removendo arquivo incompleto expirado: {a.filename} ({a.received_parts}/{a.total_parts} partes)")
+    if parsed:
+        reception_stats['success_rate'] = (len(saved) / len(parsed)) * 100
+    return saved
+
+
+# decode_with_retry's demodulator map (decoder.py:329-341): mode -> (demod, kwargs;
+# _SR = the attempt's symbol rate), calls as the reference writes them
+_SR = object()
+_RETRY_CALLS = {
+    "FSK1200": (modem.fsk_demodulate, {"baud": 1200, "mark_freq": 1200.0, "space_freq": 2200.0}),
+    "FSK9600": (modem.fsk_demodulate, {"baud": 9600}),
+    "BPSK": (modem.bpsk_demodulate, {"baud": _SR, "carrier": 3000.0}),
+    "QPSK": (modem.qpsk_demodulate, {"baud": _SR, "carrier": 3000.0}),
+    "8PSK": (modem.psk8_demodulate, {"baud": _SR, "carrier": 12000.0}),
+    "FSK19200": (modem.fsk_high_speed_demodulate, {"baud": 19200}),
+    "OFDM4": (modem.ofdm_demodulate_simple, {"baud": _SR, "carrier": 12000.0, "num_subcarriers": 4}),
+    "OFDM8": (modem.ofdm_demodulate_simple, {"baud": _SR, "carrier": 12000.0, "num_subcarriers": 8}),
+    "FT8": (modem.ft8_demodulate, {"baud": _SR, "carrier": 3000.0}),
+    "PSK31": (modem.psk31_demodulate, {"baud": _SR, "carrier": 3000.0}),
+    "FELD_HELL": (modem.feld_hell_demodulate, {"baud": 122.5, "carrier": 1000.0}),
+}
+
+
+def decode_with_retry(data: np.ndarray, mode: str, symbol_rate: int, max_retries: int = 3):
+    """decoder.py:313-377: up to max_retries demodulations (the 2nd at
+    int(rate*0.95), the 3rd at int(that*1.05)); a result over 100 bytes is
+    dumped to demodulated_attempt_<k>.bin, parsed and handed to
+    save_decoded_files; the first attempt that saves files wins.  Errors in an
+    attempt are printed and the next attempt runs.  (The reference hands the
+    parser's dicts to save_decoded_files, which unpacks tuples -- kept, so
+    frame-bearing attempts fail exactly as there.)"""
+    for attempt in range(max_retries):
+        try:
+            if attempt == 1:
+                symbol_rate = int(symbol_rate * 0.95)
+            elif attempt == 2:
+                symbol_rate = int(symbol_rate * 1.05)
+            if mode in _RETRY_CALLS:
+                fn, kw = _RETRY_CALLS[mode]
+                raw = fn(data, **{k: (symbol_rate if v is _SR else v) for k, v in kw.items()})
+            else:
+                raw = modem.qpsk_demodulate(data, baud=symbol_rate, carrier=3000.0)
+            if len(raw) <= 100:
+                print(f"⚠️ Tentativa {attempt + 1}: demodulação retornou apenas {len(raw)} bytes")
+                continue
+            with open(f"demodulated_attempt_{attempt}.bin", "wb") as f:
+                f.write(raw)
+            parsed = parse_fbp_stream_enhanced(raw)
+            if not parsed:
+                print(f"⚠️ Tentativa {attempt + 1}: nenhum frame encontrado")
+                continue
+            saved_files = save_decoded_files(parsed)
+            if saved_files:
+                return saved_files
+            print(f"⚠️ Tentativa {attempt + 1}: frames encontrados mas não salvos")
+        except Exception as e:
+            print(f"❌ Erro na tentativa {attempt + 1}: {e}")
+            traceback.print_exc()
+    print(f"❌ Falha na demodulação após {max_retries} tentativas")
+    return []
 
 
 # ---------------------------------------------------------------------------
