@@ -52,10 +52,19 @@ template <> struct FIn<int16_t> {
 // whose rounding differs from pocketfft's, so this stage is held to the
 // envelope tolerance (1e-9 relative, tests/test_gpu_fsk.py), not op order;
 // fused multiply-adds halve its FP64 instruction count.
+// ZO: the plan's b1 = b3 = b5 = 0 exactly for both tones (always so for
+// butter(3, band): b is k * poly([1,1,1,-1,-1,-1]) = k * [1,0,-3,0,3,0,-1]);
+// then fma(x, 0, z) == z for every z != 0 and those three FMAs are dropped
+// (10 FP64 instructions per sample instead of 13; only the sign of an exact
+// zero state can differ, which the envelope tolerance does not see).
+template <bool ZO>
 __device__ __forceinline__ double fsk_step(double (&z)[6], const double (&b)[7], const double (&a)[7], double x) {
   const double y = __builtin_fma(b[0], x, z[0]);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) z[i] = __builtin_fma(-y, a[i + 1], __builtin_fma(x, b[i + 1], z[i + 1]));
+  for (int i = 0; i < 5; ++i) {
+    const double zin = (ZO && (i & 1) == 0) ? z[i + 1] : __builtin_fma(x, b[i + 1], z[i + 1]);
+    z[i] = __builtin_fma(-y, a[i + 1], zin);
+  }
   z[5] = __builtin_fma(-y, a[6], x * b[6]);
   return y;
 }
@@ -81,7 +90,7 @@ __host__ __device__ inline int64_t fsk_scratch_doubles_per_wave(int64_t n, int p
 // re-reading the forward outputs.  Input tiles are loaded 16 B
 // per lane and transposed through LDS; outputs are written back into the same
 // LDS slots and stored as 1 KiB rows of z (stream-major f_mark + i f_space).
-template <typename T>
+template <typename T, bool ZO>
 __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_stride, int64_t n_streams,
                                                      double* __restrict__ scratch, double2* __restrict__ z,
                                                      FskParams p, FskIir f) {
@@ -135,7 +144,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
-      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step(zs, b, a, FIn<T>::cvt(xs[u])));
+      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step<ZO>(zs, b, a, FIn<T>::cvt(xs[u])));
     }
   };
 
@@ -144,7 +153,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   const double e0 = FIn<T>::ext(x0, x[pad]);
 #pragma unroll
   for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
-  for (int j = 0; j < pad; ++j) (void)fsk_step(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
+  for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
   if (n_tiles > 0) {
     fetch(0);
     deposit(0);
@@ -161,10 +170,10 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       __syncthreads();
     }
   }
-  for (int64_t i = n_main; i < n; ++i) tl[(size_t)(i - n_main) * 64] = fsk_step(zs, b, a, FIn<T>::cvt(x[i]));
+  for (int64_t i = n_main; i < n; ++i) tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
   double ylast = 0.0;
   for (int j = 0; j < pad; ++j) {
-    ylast = fsk_step(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
+    ylast = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
     tl[(size_t)(n - n_main + j) * 64] = ylast;
   }
   __threadfence();
@@ -172,10 +181,10 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   // ---- backward pass --------------------------------------------------------
 #pragma unroll
   for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * ylast;
-  for (int64_t j = n - n_main + pad - 1; j >= n - n_main; --j) (void)fsk_step(zs, b, a, tl[(size_t)j * 64]);
+  for (int64_t j = n - n_main + pad - 1; j >= n - n_main; --j) (void)fsk_step<ZO>(zs, b, a, tl[(size_t)j * 64]);
   double* __restrict__ zd = reinterpret_cast<double*>(z);
   for (int64_t i = n - 1; i >= n_main; --i) {          // tail outputs, one sample at a time
-    const double y = fsk_step(zs, b, a, tl[(size_t)(i - n_main) * 64]);
+    const double y = fsk_step<ZO>(zs, b, a, tl[(size_t)(i - n_main) * 64]);
     if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
   }
   if (n_tiles > 0) {
@@ -200,7 +209,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       for (int i = 0; i < 6; ++i) { zs[i] = zsave[i]; zf[i] = zb[i]; }
       // backward recursion over it, outputs in place
 #pragma unroll 8
-      for (int k = kFskTile - 1; k >= 0; --k) yb[k][lane] = fsk_step(zs, b, a, yb[k][lane]);
+      for (int k = kFskTile - 1; k >= 0; --k) yb[k][lane] = fsk_step<ZO>(zs, b, a, yb[k][lane]);
       __syncthreads();
       // 32 rows x 64 samples of z, one 1 KiB row per store instruction
       const int64_t i0 = t * kFskTile;
@@ -234,7 +243,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-template <typename T>
+template <typename T, bool ZO>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -294,7 +303,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
-      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step(zs, b, a, FIn<T>::cvt(xs[u])));
+      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step<ZO>(zs, b, a, FIn<T>::cvt(xs[u])));
     }
   };
   if (role == 0) {
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     const double e0 = FIn<T>::ext(x0, x[pad]);
 #pragma unroll
     for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
-    for (int j = 0; j < pad; ++j) (void)fsk_step(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
+    for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
     if (n_tiles > 0) {
       fetch(r0, 0);
       fetch(r1, 1);
@@ -324,10 +333,10 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       if (t < n_tiles) fwd(r0, t);
     }
     // the tail's forward outputs -> yb rows 0..ntail-1 (flat), the last -> ylast
-    for (int64_t i = n_main; i < n; ++i) (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step(zs, b, a, FIn<T>::cvt(x[i]));
+    for (int64_t i = n_main; i < n; ++i) (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
     double yl = 0.0;
     for (int j = 0; j < pad; ++j) {
-      yl = fsk_step(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
+      yl = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
       (&yb[0][0])[(size_t)(n - n_main + j) * YP + lane] = yl;
     }
     ylast_sh[lane] = yl;
@@ -339,9 +348,9 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 #pragma unroll
     for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * yl;
     const double* tb = &yb[0][0];
-    for (int64_t j = ntail - 1; j >= n - n_main; --j) (void)fsk_step(zs, b, a, tb[(size_t)j * YP + lane]);
+    for (int64_t j = ntail - 1; j >= n - n_main; --j) (void)fsk_step<ZO>(zs, b, a, tb[(size_t)j * YP + lane]);
     for (int64_t i = n - 1; i >= n_main; --i) {
-      const double y = fsk_step(zs, b, a, tb[(size_t)(i - n_main) * YP + lane]);
+      const double y = fsk_step<ZO>(zs, b, a, tb[(size_t)(i - n_main) * YP + lane]);
       if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
     }
   }
@@ -404,7 +413,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       if (it >= 1) {
         double (*buf)[YP] = &yb[((it - 1) & 1) * TL];
 #pragma unroll 8
-        for (int k = TL - 1; k >= 0; --k) buf[k][lane] = fsk_step(zs, b, a, buf[k][lane]);
+        for (int k = TL - 1; k >= 0; --k) buf[k][lane] = fsk_step<ZO>(zs, b, a, buf[k][lane]);
       }
       __syncthreads();
     }
@@ -462,25 +471,40 @@ static bool fsk_one_wave() {
   return v;
 }
 
-hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
-                               const FskParams& p, const FskIir& f, hipStream_t st) {
+static bool fsk_zero_odd_taps(const FskIir& f) {
+  static const bool off = [] { const char* e = getenv("AMR_FSK_ZO"); return e && e[0] == '0'; }();
+  if (off) return false;
+  for (int t = 0; t < 2; ++t)
+    if (f.b[t][1] != 0.0 || f.b[t][3] != 0.0 || f.b[t][5] != 0.0) return false;
+  return true;
+}
+
+template <bool ZO>
+static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1,
+                                        double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
   if (!fsk_one_wave()) {
     switch (dtype) {
-      case kF32: hipLaunchKernelGGL(k_fsk_bandpass2<float>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kF64: hipLaunchKernelGGL(k_fsk_bandpass2<double>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kI16: hipLaunchKernelGGL(k_fsk_bandpass2<int16_t>, dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF32: hipLaunchKernelGGL((k_fsk_bandpass2<float, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF64: hipLaunchKernelGGL((k_fsk_bandpass2<double, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kI16: hipLaunchKernelGGL((k_fsk_bandpass2<int16_t, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (dtype) {
-    case kF32: hipLaunchKernelGGL(k_fsk_bandpass<float>, dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kF64: hipLaunchKernelGGL(k_fsk_bandpass<double>, dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kI16: hipLaunchKernelGGL(k_fsk_bandpass<int16_t>, dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kF32: hipLaunchKernelGGL((k_fsk_bandpass<float, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kF64: hipLaunchKernelGGL((k_fsk_bandpass<double, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kI16: hipLaunchKernelGGL((k_fsk_bandpass<int16_t, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
+                               const FskParams& p, const FskIir& f, hipStream_t st) {
+  return fsk_zero_odd_taps(f) ? launch_fsk_bandpass_t<true>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
+                              : launch_fsk_bandpass_t<false>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
 }
 
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,
