@@ -98,7 +98,9 @@ def cpu_baseline_fsk(x_sample: np.ndarray, baud, mark, space, threads: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    # 20 batches: with 3 in flight the timed region starts and ends with a
+    # part-full pipeline; 5 steps measured 8.4-9.3 ms/step, 24 steps 8.1-8.7
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["qpsk9600", "fsk9600", "ofdm8", "psk8fec"], default="qpsk9600",
                     help="qpsk9600 = BASELINE configs[1] (the headline metric); fsk9600 = configs[3]; "
