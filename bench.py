@@ -298,6 +298,7 @@ def main():
     # VALU-roofline view of the pipeline
     fp64_pipeline = sum(fp64_ops.values()) / (ms_per_step / 1e3) / 1e12
     traffic = None
+    pipeline_traffic = None
     pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
     # the PMC file was recorded at each workload's default size on one GPU
     pmc_cfg = {"qpsk9600": (4096, 9600), "fsk9600": (16384, 9600), "ofdm8": (8192, 9600), "psk8fec": (8192, 19200)}
@@ -306,6 +307,16 @@ def main():
             pk = json.load(f).get(args.workload, {}).get("slots", {}).get(dom, {})
         if "hbm_bytes_per_launch" in pk:
             traffic = int(pk["hbm_bytes_per_launch"])
+        with open(pmc_file) as f:
+            wk = json.load(f).get(args.workload, {}).get("kernels", {})
+        step_bytes = sum(v.get("hbm_bytes_per_dispatch", 0) for v in wk.values())
+        if step_bytes > 0:
+            # every kernel of one step, intermediates included (PMC, not algorithmic)
+            pipeline_traffic = {"bytes_per_step": int(step_bytes),
+                                "gbs": round(step_bytes / (ms_per_step / 1e3) / 1e9, 1),
+                                "frac_of_peak": round(step_bytes / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                                "source": f"profiles/{PROFILE_ROUND}_pmc.json: FETCH_SIZE x2 + WRITE_SIZE summed "
+                                          "over the step's kernels, over this run's step time"}
 
     # parity spot-check after timing (not timed): GPU bytes vs the oracle
     out = np.empty((B, cap), np.uint8)
@@ -408,6 +419,7 @@ def main():
                          "fp64_valu": {"achieved_tops": round(fp64_achieved, 3), "peak_tops": FP64_PEAK_TOPS,
                                        "frac": round(fp64_achieved / FP64_PEAK_TOPS, 4)}},
             "pipeline_hbm_gbs": round(pipeline_bytes / (ms_per_step / 1e3) / 1e9, 2),
+            "pipeline_hbm_traffic": pipeline_traffic,
             "pipeline_fp64": {"achieved_tops": round(fp64_pipeline, 3), "peak_tops": FP64_PEAK_TOPS,
                               "frac": round(fp64_pipeline / FP64_PEAK_TOPS, 4)},
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
