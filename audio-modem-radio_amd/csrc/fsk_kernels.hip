@@ -409,8 +409,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     if (n_tiles >= 1) store_tile((int)((n_tiles - 1) & 1), 0);   // wave 1's last tile
   } else {
     for (int64_t it = 0; it <= n_tiles; ++it) {
-      const int64_t t = n_tiles - it;                    // tile written in the previous iteration
-      if (it >= 1) {
+      if (it >= 1) {                                     // tile n_tiles - it, re-run forward by wave 0
         double (*buf)[YP] = &yb[((it - 1) & 1) * TL];
 #pragma unroll 8
         for (int k = TL - 1; k >= 0; --k) buf[k][lane] = fsk_step<ZO>(zs, b, a, buf[k][lane]);
