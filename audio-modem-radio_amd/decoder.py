@@ -349,7 +349,25 @@ def decode_with_retry(data: np.ndarray, mode: str, symbol_rate: int, max_retries
 
 
 # ---------------------------------------------------------------------------
+class _Pcm16:
+    """A 16-bit WAV channel as read from the file: samples = pcm / 32768, the
+    float64 libsndfile hands the reference.  The demodulators take it as int16
+    (a quarter of the float64 bytes over PCIe, converted exactly on the GPU)."""
+
+    def __init__(self, pcm: np.ndarray):
+        self.pcm = np.ascontiguousarray(pcm, np.int16)
+
+    def __len__(self):
+        return len(self.pcm)
+
+    def as_float(self) -> np.ndarray:
+        return self.pcm.astype(np.float64) / 32768.0
+
+
 def _read_wav(path: str):
+    """(data, sr): soundfile.read's float64 [n] or [n, channels] when soundfile
+    is installed; else the raw int16 samples of a 16-bit PCM file, which
+    decode_wav_file scales by 1/32768 or hands to the GPU as int16."""
     try:
         import soundfile as sf  # the reference's reader (decoder.py:381)
         return sf.read(path)
@@ -362,10 +380,10 @@ def _read_wav(path: str):
         raw = w.readframes(w.getnframes())
     if width != 2:
         raise ValueError(f"only 16-bit PCM WAV is supported without soundfile (got {8 * width}-bit)")
-    data = np.frombuffer(raw, dtype='<i2').astype(np.float64) / 32768.0
+    pcm = np.frombuffer(raw, dtype='<i2')
     if nch > 1:
-        data = data.reshape(-1, nch)
-    return data, sr
+        pcm = pcm.reshape(-1, nch)
+    return pcm, sr
 
 
 def decode_wav_file(path: str, mode: str, symbol_rate: int) -> list:
@@ -373,14 +391,20 @@ def decode_wav_file(path: str, mode: str, symbol_rate: int) -> list:
     data, sr = _read_wav(path)
     if len(data.shape) > 1:
         data = data[:, 0]
+    pcm = data.dtype == np.int16                    # read without soundfile: int16 PCM
     if sr != SAMPLE_RATE:
         number_of_samples = int(round(len(data) * float(SAMPLE_RATE) / sr))
-        data = _amr.resample(np.asarray(data, np.float64), number_of_samples)   # scipy.signal.resample, on the GPU
+        x = data.astype(np.float64) / 32768.0 if pcm else np.asarray(data, np.float64)
+        data = _amr.resample(x, number_of_samples)   # scipy.signal.resample, on the GPU
+    elif pcm:
+        data = _Pcm16(data)
     return decode_from_buffer(data, mode, symbol_rate)
 
 
 def _demod_bytes(data, mode: str, symbol_rate):
     """The reference's mode dispatch (decoder.py:421-434)."""
+    if isinstance(data, _Pcm16):
+        return _demod_pcm16(data.pcm, mode, symbol_rate)
     if mode == "BPSK":
         return modem.bpsk_demodulate(data, baud=symbol_rate)
     elif mode == "QPSK" or mode == "8PSK":
@@ -394,6 +418,16 @@ def _demod_bytes(data, mode: str, symbol_rate):
         return modem.fsk_demodulate(data, baud=baud)
     else:
         return modem.qpsk_demodulate(data, baud=symbol_rate)
+
+
+def _demod_pcm16(pcm: np.ndarray, mode: str, symbol_rate):
+    """_demod_bytes for int16 WAV samples (same dispatch, same defaults)."""
+    if mode == "BPSK":
+        return modem._pcm16_psk("bpsk", pcm, symbol_rate)
+    elif mode.startswith("FSK"):
+        baud = 9600 if "9600" in mode else 19200 if "19200" in mode else 1200
+        return modem._pcm16_fsk(pcm, baud)
+    return modem._pcm16_psk("qpsk", pcm, symbol_rate)      # QPSK, 8PSK and every other mode
 
 
 def _save_frames(raw_bytes: bytes, frames=None) -> list:

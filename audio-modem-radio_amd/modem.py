@@ -66,6 +66,22 @@ def _psk_batch(kind: str, x2d: np.ndarray, baud, carrier, samp_rate):
     return outs
 
 
+# 16-bit WAV samples straight from the file (decoder.decode_wav_file): the
+# plans take int16 as pcm / 32768 -- exactly the float64 libsndfile gives the
+# reference -- so a quarter of the float64 bytes cross PCIe.  Internal: the
+# public functions treat integer input as raw values, as the reference does.
+def _pcm16_psk(kind: str, pcm: np.ndarray, baud, carrier=3000.0, samp_rate=96000) -> bytes:
+    x = np.ascontiguousarray(pcm, np.int16)[None, :]
+    plan = _amr.get_psk_plan(kind, x.shape[1], baud, carrier, samp_rate, 1)
+    return plan.demod_host(x)[0][0]
+
+
+def _pcm16_fsk(pcm: np.ndarray, baud, mark_freq=1200.0, space_freq=2200.0, samp_rate=96000) -> bytes:
+    import _fsk
+    return _fsk.fsk_demodulate_batch(np.ascontiguousarray(pcm, np.int16)[None, :], baud, mark_freq, space_freq,
+                                     samp_rate)[0]
+
+
 # ---------------------------------------------------------------------------
 # PSK receive side
 def qpsk_demodulate(samples: np.ndarray, baud=1200, carrier=3000.0, samp_rate=96000) -> bytes:

@@ -281,3 +281,23 @@ sys.exit(1 if bad else 0)
     env = dict(os.environ, AMR_BP_G8="1")
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=250)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_pcm16_wav_path_equals_float64_path():
+    """decode_wav_file hands 16-bit 96 kHz WAV samples to the GPU as int16
+    (pcm / 32768 converted on the device): the bytes equal the float64 path's
+    (the reference's libsndfile reading) for PSK, BPSK and FSK."""
+    import modem
+    import synth
+    rng = np.random.default_rng(77)
+    for kind, baud in (("qpsk", 9600), ("qpsk", 1000), ("bpsk", 1200)):
+        wave_ = synth.qpsk_batch(3, 30001, baud, seed=baud) if kind == "qpsk" else \
+            np.stack([synth.fit(synth.bpsk_waveform(synth.random_frame(rng, 60), baud), 30001) for _ in range(3)])
+        for x in wave_:
+            pcm = np.clip(x * 32767 + rng.normal(0, 30, x.size), -32768, 32767).astype(np.int16)
+            want = (modem.qpsk_demodulate if kind == "qpsk" else modem.bpsk_demodulate)(pcm / 32768.0, baud)
+            assert modem._pcm16_psk(kind, pcm, baud) == want, (kind, baud)
+    for x in synth.fsk_batch(3, 24000, 9600, seed=5):
+        pcm = (x * 20000).astype(np.int16)
+        want = modem.fsk_demodulate(pcm / 32768.0, 9600, 12000.0, 24000.0)
+        assert modem._pcm16_fsk(pcm, 9600, 12000.0, 24000.0) == want
