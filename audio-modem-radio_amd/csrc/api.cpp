@@ -40,6 +40,32 @@ int amr::fail(int code, const std::string& msg) {
   return code;
 }
 
+int amr::copy_batch_h2d(void* dst, const void* src, int64_t row_bytes, int64_t src_pitch, int64_t B,
+                        hipStream_t st) {
+  HIP_TRY(hipStreamSynchronize(st));
+  if (src_pitch == row_bytes)
+    HIP_TRY(hipMemcpy(dst, src, (size_t)(row_bytes * B), hipMemcpyHostToDevice));
+  else
+    HIP_TRY(hipMemcpy2D(dst, (size_t)row_bytes, src, (size_t)src_pitch, (size_t)row_bytes, (size_t)B,
+                        hipMemcpyHostToDevice));
+  return AMR_OK;
+}
+
+int amr::copy_batch_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes,
+                        int64_t B, hipStream_t st) {
+  HIP_TRY(hipStreamSynchronize(st));
+  if (B <= 0 || row_bytes <= 0) return AMR_OK;
+  if (dst_pitch == src_pitch) {
+    HIP_TRY(hipMemcpy(dst, src, (size_t)(src_pitch * (B - 1) + row_bytes), hipMemcpyDeviceToHost));
+    return AMR_OK;
+  }
+  std::vector<uint8_t> h((size_t)(src_pitch * (B - 1) + row_bytes));
+  HIP_TRY(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost));
+  for (int64_t r = 0; r < B; ++r)
+    std::memcpy(static_cast<uint8_t*>(dst) + r * dst_pitch, h.data() + r * src_pitch, (size_t)row_bytes);
+  return AMR_OK;
+}
+
 int64_t amr::dtype_size(int dtype) {
   switch (dtype) {
     case AMR_DTYPE_F32: return 4;
@@ -541,14 +567,13 @@ int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, 
     HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
     HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
   }
-  HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
-                           hipMemcpyHostToDevice, plan->stream));
+  rc = copy_batch_h2d(plan->d_x, x, n * es, x_stride * es, B, plan->stream);
+  if (rc) return rc;
   rc = run_psk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync, nullptr, 0, nullptr,
                nullptr);
   if (rc) return rc;
-  HIP_TRY(hipMemcpy2DAsync(out, (size_t)out_stride, plan->d_out, (size_t)cap,
-                           (size_t)(out_stride < cap ? out_stride : cap), (size_t)B, hipMemcpyDeviceToHost,
-                           plan->stream));
+  rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B, plan->stream);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out_len, plan->d_len, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipStreamSynchronize(plan->stream));

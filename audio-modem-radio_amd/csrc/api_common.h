@@ -12,6 +12,18 @@ int fail(int code, const std::string& msg);   // sets amr_last_error(), returns 
 int64_t dtype_size(int dtype);                // bytes per sample, 0 = unknown
 // device + stream a *_device call on `plan` runs on (plan NULL: current device, null stream)
 int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st);
+// Copy a host batch [B rows of `row_bytes`, `src_pitch` apart] into dense
+// device rows, for the *_host entry points.  Waits for `st` first (its earlier
+// work may still read dst), then copies synchronously: a dense source as one
+// 1-D copy (pageable 1-D copies ran at 56 GB/s on the MI355X box where the
+// pitched async copy of the same 6.3 GB ran at ~24, tools/host_path_probe.py).
+int copy_batch_h2d(void* dst, const void* src, int64_t row_bytes, int64_t src_pitch, int64_t B, hipStream_t st);
+// The output side: B rows of `row_bytes` from device rows `src_pitch` apart to
+// host rows `dst_pitch` apart, after the work queued on `st`.  One 1-D copy
+// (then a host-side scatter when the pitches differ): a pitched D2H copy into
+// pageable memory ran as one transfer per row -- 16384 rows took 215 ms.
+int copy_batch_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes, int64_t B,
+                   hipStream_t st);
 }  // namespace amr
 
 #define HIP_TRY(expr)                                                                              \

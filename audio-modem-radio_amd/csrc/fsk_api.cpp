@@ -395,9 +395,7 @@ int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x
   const int64_t es = dtype_size(dtype);
   const int64_t n = pl->p.n;
   if (!pl->d_x) HIP_TRY(hipMalloc(&pl->d_x, (size_t)(pl->max_streams * n * 8)));
-  HIP_TRY(hipMemcpy2DAsync(pl->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
-                           hipMemcpyHostToDevice, pl->stream));
-  return AMR_OK;
+  return copy_batch_h2d(pl->d_x, x, n * es, x_stride * es, B, pl->stream);
 }
 
 }  // namespace
@@ -545,9 +543,9 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
     HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
   }
   if (int rc = run_fsk(plan, plan->d_x, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
-  HIP_TRY(hipMemcpy2DAsync(out, (size_t)out_stride, plan->d_out, (size_t)cap,
-                           (size_t)(out_stride < cap ? out_stride : cap), (size_t)B, hipMemcpyDeviceToHost,
-                           plan->stream));
+  if (int rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B,
+                              plan->stream))
+    return rc;
   HIP_TRY(hipMemcpyAsync(out_len, plan->d_len, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipStreamSynchronize(plan->stream));
