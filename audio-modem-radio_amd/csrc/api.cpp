@@ -40,29 +40,43 @@ int amr::fail(int code, const std::string& msg) {
   return code;
 }
 
+hipError_t amr::memcpy_rows(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes,
+                            int64_t B, hipMemcpyKind kind) {
+  if (B <= 0 || row_bytes <= 0) return hipSuccess;
+  const size_t span_src = (size_t)(src_pitch * (B - 1) + row_bytes);
+  const size_t span_dst = (size_t)(dst_pitch * (B - 1) + row_bytes);
+  // equal pitches: one copy (a D2H one only when the rows are dense, so the
+  // caller's bytes between rows are never overwritten)
+  if (dst_pitch == src_pitch && (row_bytes == dst_pitch || kind == hipMemcpyHostToDevice))
+    return hipMemcpy(dst, src, span_src, kind);
+  if (kind == hipMemcpyHostToDevice && dst_pitch == row_bytes) {   // pack on the host, one copy
+    std::vector<uint8_t> h(span_dst);
+    for (int64_t r = 0; r < B; ++r)
+      std::memcpy(h.data() + r * dst_pitch, static_cast<const uint8_t*>(src) + r * src_pitch, (size_t)row_bytes);
+    return hipMemcpy(dst, h.data(), span_dst, kind);
+  }
+  if (kind == hipMemcpyDeviceToHost) {                              // one copy, scatter on the host
+    std::vector<uint8_t> h(span_src);
+    hipError_t e = hipMemcpy(h.data(), src, span_src, kind);
+    if (e != hipSuccess) return e;
+    for (int64_t r = 0; r < B; ++r)
+      std::memcpy(static_cast<uint8_t*>(dst) + r * dst_pitch, h.data() + r * src_pitch, (size_t)row_bytes);
+    return hipSuccess;
+  }
+  return hipMemcpy2D(dst, (size_t)dst_pitch, src, (size_t)src_pitch, (size_t)row_bytes, (size_t)B, kind);
+}
+
 int amr::copy_batch_h2d(void* dst, const void* src, int64_t row_bytes, int64_t src_pitch, int64_t B,
                         hipStream_t st) {
   HIP_TRY(hipStreamSynchronize(st));
-  if (src_pitch == row_bytes)
-    HIP_TRY(hipMemcpy(dst, src, (size_t)(row_bytes * B), hipMemcpyHostToDevice));
-  else
-    HIP_TRY(hipMemcpy2D(dst, (size_t)row_bytes, src, (size_t)src_pitch, (size_t)row_bytes, (size_t)B,
-                        hipMemcpyHostToDevice));
+  HIP_TRY(memcpy_rows(dst, row_bytes, src, src_pitch, row_bytes, B, hipMemcpyHostToDevice));
   return AMR_OK;
 }
 
 int amr::copy_batch_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes,
                         int64_t B, hipStream_t st) {
   HIP_TRY(hipStreamSynchronize(st));
-  if (B <= 0 || row_bytes <= 0) return AMR_OK;
-  if (dst_pitch == src_pitch) {
-    HIP_TRY(hipMemcpy(dst, src, (size_t)(src_pitch * (B - 1) + row_bytes), hipMemcpyDeviceToHost));
-    return AMR_OK;
-  }
-  std::vector<uint8_t> h((size_t)(src_pitch * (B - 1) + row_bytes));
-  HIP_TRY(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost));
-  for (int64_t r = 0; r < B; ++r)
-    std::memcpy(static_cast<uint8_t*>(dst) + r * dst_pitch, h.data() + r * src_pitch, (size_t)row_bytes);
+  HIP_TRY(memcpy_rows(dst, dst_pitch, src, src_pitch, row_bytes, B, hipMemcpyDeviceToHost));
   return AMR_OK;
 }
 
@@ -606,12 +620,12 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
   if (e == hipSuccess) e = hipMalloc(&d_out_len, (size_t)n * 8);
   if (e == hipSuccess) e = hipMalloc(&d_crc, (size_t)n * 4);
   if (e == hipSuccess && maxlen > 0)
-    e = hipMemcpy2D(d_in, (size_t)stride, in, (size_t)in_stride, (size_t)maxlen, (size_t)n, hipMemcpyHostToDevice);
+    e = memcpy_rows(d_in, stride, in, in_stride, maxlen, n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = launch_fec_decode(d_in, stride, d_in_len, n, d_out, stride, d_out_len, d_crc, tab, x2n, 0);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e == hipSuccess && maxlen > 0)
-    e = hipMemcpy2D(out, (size_t)out_stride, d_out, (size_t)stride, (size_t)maxlen, (size_t)n, hipMemcpyDeviceToHost);
+    e = memcpy_rows(out, out_stride, d_out, stride, maxlen, n, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(out_len, d_out_len, (size_t)n * 8, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(crc_ok, d_crc, (size_t)n * 4, hipMemcpyDeviceToHost);
   for (void* p : {(void*)d_in, (void*)d_out, (void*)d_in_len, (void*)d_out_len, (void*)d_crc})
@@ -667,7 +681,7 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
   if (e == hipSuccess) e = hipMalloc(&d_cnt, (size_t)n * 4);
   if (e == hipSuccess) e = hipMalloc(&d_recs, (size_t)(n * max_cands) * sizeof(amr_frame_rec));
   if (e == hipSuccess && maxlen > 0)
-    e = hipMemcpy2D(d_in, (size_t)stride, in, (size_t)in_stride, (size_t)maxlen, (size_t)n, hipMemcpyHostToDevice);
+    e = memcpy_rows(d_in, stride, in, in_stride, maxlen, n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = launch_frame_parse(d_in, stride, d_in_len, n, max_cands, d_cnt, d_recs, tab, x2n, 0);
   if (e == hipSuccess) e = hipDeviceSynchronize();

@@ -12,6 +12,11 @@ int fail(int code, const std::string& msg);   // sets amr_last_error(), returns 
 int64_t dtype_size(int dtype);                // bytes per sample, 0 = unknown
 // device + stream a *_device call on `plan` runs on (plan NULL: current device, null stream)
 int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st);
+// B rows of `row_bytes` between pitched buffers without one DMA per row:
+// equal pitches -> one copy; otherwise packed / scattered on the host around
+// one copy (hipMemcpy2D only for a pitched device destination).
+hipError_t memcpy_rows(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes,
+                       int64_t B, hipMemcpyKind kind);
 // Copy a host batch [B rows of `row_bytes`, `src_pitch` apart] into dense
 // device rows, for the *_host entry points.  Waits for `st` first (its earlier
 // work may still read dst), then copies synchronously: a dense source as one

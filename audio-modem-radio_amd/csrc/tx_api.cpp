@@ -149,8 +149,7 @@ int amr_modulate_host(int mode, double baud, double f0, double f1, double sample
   if (e == hipSuccess && pcm) e = hipMalloc(&d_pcm, (size_t)(n * n_out) * 2);
   if (e == hipSuccess) e = hipMalloc(&d_work, (size_t)wb);
   if (e == hipSuccess && maxlen > 0)
-    e = hipMemcpy2D(d_data, (size_t)stride, data, (size_t)data_stride, (size_t)maxlen, (size_t)n,
-                    hipMemcpyHostToDevice);
+    e = memcpy_rows(d_data, stride, data, data_stride, maxlen, n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_nb, n_bytes, (size_t)n * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     rc = amr_modulate_device(nullptr, mode, baud, f0, f1, sample_rate, d_data, stride, d_nb, n, d_out, n_out, n_out,
@@ -158,11 +157,9 @@ int amr_modulate_host(int mode, double baud, double f0, double f1, double sample
     if (rc == AMR_OK) e = hipDeviceSynchronize();
   }
   if (e == hipSuccess && rc == AMR_OK)
-    e = hipMemcpy2D(out, (size_t)out_stride * 4, d_out, (size_t)n_out * 4, (size_t)n_out * 4, (size_t)n,
-                    hipMemcpyDeviceToHost);
+    e = memcpy_rows(out, out_stride * 4, d_out, n_out * 4, n_out * 4, n, hipMemcpyDeviceToHost);
   if (e == hipSuccess && rc == AMR_OK && pcm)
-    e = hipMemcpy2D(pcm, (size_t)pcm_stride * 2, d_pcm, (size_t)n_out * 2, (size_t)n_out * 2, (size_t)n,
-                    hipMemcpyDeviceToHost);
+    e = memcpy_rows(pcm, pcm_stride * 2, d_pcm, n_out * 2, n_out * 2, n, hipMemcpyDeviceToHost);
   for (void* q : {(void*)d_data, (void*)d_nb, (void*)d_out, (void*)d_pcm, d_work})
     if (q) (void)hipFree(q);
   if (rc) return rc;
