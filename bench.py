@@ -428,6 +428,15 @@ def main():
             "parity": parity,
             "host_path_pcie_inclusive": host_path,
         }
+        # the reference's own numpy/scipy code is not on the GPU box; its rate as
+        # measured in the build container is the north-star basis
+        ref_py = {"qpsk9600": (0.292, 1.66), "ofdm8": (0.292, 1.66), "psk8fec": (0.310, 2.43),
+                  "fsk9600": (0.180, 1.15)}[args.workload]
+        result["vs_reference_python"] = {
+            "reference_1core_msym_s": ref_py[0], "reference_8proc_msym_s": ref_py[1],
+            "ratio_1core": round(value / ref_py[0], 1), "ratio_8proc": round(value / ref_py[1], 1),
+            "source": "BASELINE.md §2: the reference's modem.py on numpy 2.2.6 / scipy 1.15.3, measured in the "
+                      "build container (8 cores), not on the GPU box"}
         if not fsk:
             result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
         if fec_fused:
