@@ -37,11 +37,12 @@ DTYPES = {np.dtype(np.float32): DTYPE_F32, np.dtype(np.float64): DTYPE_F64, np.d
 
 # every symbol include/amr.h declares (tests/test_abi.py checks the export table)
 EXPORTS = [
-    "amr_abi_version", "amr_last_error", "amr_device_count", "amr_set_device", "amr_malloc", "amr_free",
+    "amr_abi_version", "amr_build_id", "amr_last_error", "amr_device_count", "amr_set_device", "amr_malloc", "amr_free",
     "amr_memcpy_h2d", "amr_memcpy_d2h", "amr_memcpy_d2d", "amr_device_synchronize",
     "amr_psk_plan_create", "amr_psk_plan_destroy", "amr_psk_plan_out_capacity", "amr_psk_plan_scratch_bytes",
     "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings", "amr_psk_plan_set_inflight",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
+    "amr_psk_slice_host",
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
@@ -94,6 +95,20 @@ def modulate(mode: int, datas, baud, f0, f1=0.0, samp_rate=96000, n_out=None, pc
     return (out, pc) if pcm else out
 
 
+def psk_slice(kind: str, sym: np.ndarray) -> np.ndarray:
+    """The slicer stage alone on the GPU (K4a): sym [B][S] complex128 -> the
+    decided bits [B][bits] as uint8 (modem.py:214-241 QPSK, :100-105 BPSK)."""
+    require_gpu()
+    sym = np.ascontiguousarray(np.atleast_2d(sym), np.complex128)
+    B, S = sym.shape
+    nbits = max(0, (S - 1) * (2 if kind == "qpsk" else 1))
+    nw = max(1, (nbits + 31) // 32)
+    words = np.zeros((B, nw), np.uint32)
+    check(lib().amr_psk_slice_host(PSK_QPSK if kind == "qpsk" else PSK_BPSK, ptr(sym), B, S, ptr(words)))
+    bits = np.unpackbits(words.astype(">u4").view(np.uint8).reshape(B, -1), axis=1)
+    return bits[:, :nbits]
+
+
 def frame_parse(raws, max_cands: int = 64):
     """Batched decoder.parse_fbp_stream_enhanced scan (decoder.py:142-208) on
     the GPU: for each bytes object, (n_candidates, records[:min(n, max_cands)])
@@ -138,6 +153,7 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         sig = {
             "amr_abi_version": (I32, []),
+            "amr_build_id": (ctypes.c_char_p, []),
             "amr_last_error": (ctypes.c_char_p, []),
             "amr_device_count": (I32, [P]),
             "amr_set_device": (I32, [I32]),
@@ -159,6 +175,7 @@ def lib():
             "amr_psk_demod_host": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_device": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
+            "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
             "amr_fsk_plan_create": (I32, [P, I32, I64, I64, P, P, P, P, P, P, I32, I64]),
             "amr_fsk_plan_destroy": (I32, [P]),
             "amr_fsk_plan_out_capacity": (I64, [P]),
@@ -316,6 +333,10 @@ class PskPlan:
             syncs[s0:s0 + nb] = sy
         return outs, syncs
 
+    def scratch_bytes(self) -> int:
+        """Device bytes this plan holds (scratch + host-API staging)."""
+        return int(lib().amr_psk_plan_scratch_bytes(self.handle)) if self.handle else 0
+
     def enable_timing(self, on=True):
         check(lib().amr_psk_plan_enable_timing(self.handle, 1 if on else 0))
 
@@ -334,20 +355,84 @@ class PskPlan:
         return c.value
 
 
-_plans: dict = {}
-_plans_lock = threading.Lock()
+class PlanCache:
+    """LRU of device plans bounded by the HBM they hold.
+
+    The reference keeps no state between calls; a long-running receiver
+    decoding captures of ever-different lengths (the live-capture path,
+    filebeep_advanced_v2.py:324) must not accumulate one plan per length.
+    Plans are kept while their summed device bytes (scratch_bytes(), incl.
+    host-API staging) stay within `budget` and there are at most
+    `max_entries` of them; the least recently used are dropped first (their
+    HBM is released when the last caller holding one lets go of it)."""
+
+    def __init__(self, budget_bytes: int, max_entries: int = 32):
+        import collections
+        self.budget = int(budget_bytes)
+        self.max_entries = int(max_entries)
+        self._d = collections.OrderedDict()
+        self.lock = threading.Lock()
+
+    def get(self, key, need: int, make):
+        """The cached plan for key if it holds >= need streams, else make(need)."""
+        with self.lock:
+            pl = self._d.get(key)
+            if pl is not None and pl.max_streams >= need:
+                self._d.move_to_end(key)
+                return pl
+            if pl is not None:
+                del self._d[key]                    # too small: its scratch goes before the new one's
+                pl = None
+            self._evict(reserve=0)
+            pl = make(need)
+            self._d[key] = pl
+            self._evict(reserve=0, keep=key)
+            return pl
+
+    def total_bytes(self) -> int:
+        with self.lock:
+            return sum(p.scratch_bytes() for p in self._d.values())
+
+    def __len__(self):
+        return len(self._d)
+
+    def clear(self):
+        with self.lock:
+            self._d.clear()
+
+    def _evict(self, reserve: int, keep=None):
+        total = sum(p.scratch_bytes() for p in self._d.values())
+        while self._d and (total + reserve > self.budget or len(self._d) > self.max_entries):
+            k = next(iter(self._d))
+            if k == keep:
+                if len(self._d) == 1:
+                    break
+                self._d.move_to_end(k)
+                k = next(iter(self._d))
+            total -= self._d.pop(k).scratch_bytes()
+
+
+def _cache_budget() -> int:
+    return int(float(os.environ.get("AMR_PLAN_CACHE_BYTES", 24e9)))
+
+
+def stream_bucket(batch: int, cap: int) -> int:
+    """Plan size for a batch: the next power of two (a single-stream call gets
+    a one-stream plan), capped at `cap` streams per launch."""
+    b = max(1, min(int(batch), int(cap)))
+    return 1 << (b - 1).bit_length()
+
+
+_psk_cache = PlanCache(_cache_budget())
+PSK_MAX_CHUNK = 4096
 
 
 def get_psk_plan(kind: str, n: int, baud, carrier, samp_rate, batch: int) -> PskPlan:
     """Plan cache keyed by the reference call's parameters (and device)."""
     dev = default_device()
     key = (kind, int(n), float(baud), float(carrier), float(samp_rate), dev)
-    with _plans_lock:
-        pl = _plans.get(key)
-        if pl is None or pl.max_streams < min(batch, 4096):
-            pl = PskPlan(kind, n, baud, carrier, samp_rate, max_streams=max(64, min(batch, 4096)), device=dev)
-            _plans[key] = pl
-        return pl
+    need = stream_bucket(batch, PSK_MAX_CHUNK)
+    return _psk_cache.get(key, need, lambda m: PskPlan(kind, n, baud, carrier, samp_rate, max_streams=m, device=dev))
 
 
 def fec_decode_host(datas):

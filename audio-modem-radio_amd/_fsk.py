@@ -106,6 +106,10 @@ class FskPlan:
                                                    ptr(m[s0:s0 + nb]), ptr(s[s0:s0 + nb])))
         return m, s
 
+    def scratch_bytes(self) -> int:
+        """Device bytes this plan holds (scratch + host-API staging)."""
+        return int(lib().amr_fsk_plan_scratch_bytes(self.handle)) if self.handle else 0
+
     def enable_timing(self, on=True):
         check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
 
@@ -115,24 +119,16 @@ class FskPlan:
         return {k: float(v) for k, v in zip(_amr.TF_NAMES, ms) if v >= 0}
 
 
-_plans: dict = {}
-_plans_lock = threading.Lock()
 MAX_CHUNK = 16384
+_fsk_cache = _amr.PlanCache(_amr._cache_budget())
 
 
 def get_fsk_plan(n, baud, mark_freq, space_freq, samp_rate, batch) -> FskPlan:
     dev = _amr.default_device()
     key = (int(n), float(baud), float(mark_freq), float(space_freq), float(samp_rate), dev)
-    with _plans_lock:
-        pl = _plans.get(key)
-        if pl is None or pl.max_streams < min(batch, MAX_CHUNK):
-            # drop the old plan's HBM scratch before sizing a bigger one
-            _plans.pop(key, None)
-            pl = None
-            pl = FskPlan(n, baud, mark_freq, space_freq, samp_rate, max_streams=max(16, min(batch, MAX_CHUNK)),
-                         device=dev)
-            _plans[key] = pl
-        return pl
+    need = max(16, _amr.stream_bucket(batch, MAX_CHUNK))   # the FFT passes tile 8+ rows
+    return _fsk_cache.get(key, need, lambda m: FskPlan(n, baud, mark_freq, space_freq, samp_rate, max_streams=m,
+                                                       device=dev))
 
 
 def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate) -> list:

@@ -10,6 +10,7 @@ Compile flags that matter for parity:
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,28 +29,63 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f
           "-I", CSRC, "-I", INCLUDE, "-Wall", "-Wno-unused-function"]
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(paths, extra: str = "") -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    h.update(extra.encode())
+    return h.hexdigest()[:16]
+
+
+def _headers():
+    return [x if os.path.isabs(x) else os.path.join(CSRC, x) for x in HEADERS]
+
+
+def source_hash() -> str:
+    """sha256 prefix over every source, header, this script and the flags:
+    the build id libamr.so reports (amr_build_id), which ties a loaded
+    library to the sources of the tree it runs in."""
+    return _digest([os.path.join(CSRC, s) for s in SOURCES] + _headers() + [os.path.abspath(__file__)],
+                   " ".join(CFLAGS))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Rebuild what changed BY CONTENT (each object records the digest of its
+    source + headers + flags next to it), never by modification time alone."""
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
-    hdrs = [h if os.path.isabs(h) else os.path.join(CSRC, h) for h in HEADERS]
+    hdrs = _headers()
+    bid = source_hash()
     objs = []
+    jobs = []
+    relink = force or not os.path.exists(LIB)
     for src in SOURCES:
         sp = os.path.join(CSRC, src)
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
-        if force or _stale(obj, [sp, *hdrs, __file__]):
-            cmd = [HIPCC, *CFLAGS, "-c", sp, "-o", obj]
-            if verbose:
-                print(" ".join(cmd))
-            subprocess.run(cmd, check=True)
-    if force or _stale(LIB, objs):
+        defs = [f'-DAMR_BUILD_ID="{bid}"'] if src == "api.cpp" else []
+        dig = _digest([sp, *hdrs, os.path.abspath(__file__)], " ".join(CFLAGS + defs))
+        stamp = obj + ".sha"
+        have = open(stamp).read().strip() if os.path.exists(stamp) and os.path.exists(obj) else ""
+        if force or have != dig:
+            jobs.append(([HIPCC, *CFLAGS, *defs, "-c", sp, "-o", obj], stamp, dig))
+
+    def compile_one(job):
+        cmd, stamp, dig = job
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        with open(stamp, "w") as f:
+            f.write(dig + "\n")
+
+    if jobs:
+        from concurrent.futures import ThreadPoolExecutor
+        workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0")) or min(8, os.cpu_count() or 1)))
+        with ThreadPoolExecutor(workers) as ex:
+            list(ex.map(compile_one, jobs))
+        relink = True
+    if relink:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
                "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:

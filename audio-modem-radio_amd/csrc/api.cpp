@@ -207,6 +207,10 @@ int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
 extern "C" {
 
 int amr_abi_version(void) { return AMR_ABI_VERSION; }
+#ifndef AMR_BUILD_ID
+#define AMR_BUILD_ID "unknown"
+#endif
+const char* amr_build_id(void) { return AMR_BUILD_ID; }
 const char* amr_last_error(void) { return g_err.c_str(); }
 
 int amr_device_count(int* count) {
@@ -383,7 +387,12 @@ int amr_psk_plan_destroy(amr_psk_plan* plan) {
   return AMR_OK;
 }
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan* plan) { return plan ? plan->out_cap : -1; }
-int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) { return plan ? plan->scratch_bytes : -1; }
+int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) {
+  if (!plan) return -1;
+  // scratch + whatever host-API staging the plan has allocated so far
+  return plan->scratch_bytes + (plan->d_x ? plan->d_x_bytes : 0) +
+         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
+}
 
 int amr_psk_plan_synchronize(amr_psk_plan* plan) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
@@ -571,6 +580,11 @@ int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, 
   std::lock_guard<std::mutex> lk(plan->mu);
   HIP_TRY(hipSetDevice(plan->device));
   if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  // the same argument contract as the device entry point (run_psk), checked
+  // before any copy: a short out_stride would cut rows while out_len still
+  // reports their full length
+  if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < plan->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
   if (B == 0) return AMR_OK;
   const int64_t n = plan->p.n;
   const int64_t cap = plan->out_cap;
@@ -634,11 +648,53 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
   return AMR_OK;
 }
 
+// ---- the slicer stage alone (modem.py:214-241 / 100-105) ---------------------
+int amr_psk_slice_host(int kind, const double* sym, int64_t n_streams, int64_t n_sym, uint32_t* words) {
+  if (kind != AMR_PSK_QPSK && kind != AMR_PSK_BPSK) return fail(AMR_E_INVALID, "unknown PSK kind");
+  if (n_streams < 0 || n_sym < 0 || (n_streams && n_sym && (!sym || !words)))
+    return fail(AMR_E_INVALID, "amr_psk_slice_host: bad argument");
+  PskParams p{};
+  p.kind = kind;
+  p.n_sym = n_sym;
+  p.n_bits = n_sym >= 2 ? (n_sym - 1) * (kind == AMR_PSK_QPSK ? 2 : 1) : 0;
+  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
+  if (n_streams == 0 || p.n_bits == 0) return AMR_OK;
+  // the symbol buffer layout K3q/K3x write: [B/32][S][32][re, im] (sym_index)
+  const int64_t g32 = (n_streams + 31) / 32;
+  std::vector<double> h((size_t)(g32 * n_sym * 64), 0.0);
+  for (int64_t s = 0; s < n_streams; ++s)
+    for (int64_t k = 0; k < n_sym; ++k) {
+      const size_t d = ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2;
+      h[d] = sym[(s * n_sym + k) * 2];
+      h[d + 1] = sym[(s * n_sym + k) * 2 + 1];
+    }
+  double* d_sym = nullptr;
+  uint32_t* d_words = nullptr;
+  hipError_t e = hipMalloc(&d_sym, h.size() * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_words, (size_t)(n_streams * p.n_words) * 4);
+  if (e == hipSuccess) e = hipMemcpy(d_sym, h.data(), h.size() * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    PskBuffers b{};
+    b.n_streams = n_streams;
+    b.s1 = d_sym;
+    b.words = d_words;
+    e = launch_psk_slice(b, p, nullptr);
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(words, d_words, (size_t)(n_streams * p.n_words) * 4, hipMemcpyDeviceToHost);
+  if (d_sym) (void)hipFree(d_sym);
+  if (d_words) (void)hipFree(d_words);
+  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_psk_slice_host: ") + hipGetErrorString(e));
+  return AMR_OK;
+}
+
 // ---- FBP frame parse (decoder.py:142-208) ------------------------------------
 int amr_frame_parse_device(amr_psk_plan* plan, const uint8_t* d_in, int64_t in_stride, const int64_t* d_in_len,
                            int64_t n, int64_t max_cands, int32_t* d_n_cands, amr_frame_rec* d_recs) {
   if (n < 0 || max_cands < 1 || in_stride < 0 || (n && (!d_in || !d_in_len || !d_n_cands || !d_recs)))
     return fail(AMR_E_INVALID, "amr_frame_parse_device: bad argument");
+  if (max_cands > AMR_FRAME_MAX_CANDS)
+    return fail(AMR_E_INVALID, "max_cands > AMR_FRAME_MAX_CANDS (the kernel keeps at most that many records)");
   if (n == 0) return AMR_OK;
   int dev = 0;
   hipStream_t st = nullptr;
@@ -660,6 +716,8 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
                          int32_t* n_cands, amr_frame_rec* recs) {
   if (n < 0 || max_cands < 1 || (n && (!in || !in_len || !n_cands || !recs)))
     return fail(AMR_E_INVALID, "amr_frame_parse_host: bad argument");
+  if (max_cands > AMR_FRAME_MAX_CANDS)
+    return fail(AMR_E_INVALID, "max_cands > AMR_FRAME_MAX_CANDS (the kernel keeps at most that many records)");
   if (n == 0) return AMR_OK;
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));

@@ -482,7 +482,12 @@ int amr_fsk_plan_destroy(amr_fsk_plan* plan) {
   return AMR_OK;
 }
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan->out_cap : -1; }
-int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) { return plan ? plan->scratch_bytes : -1; }
+int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
+  if (!plan) return -1;
+  // scratch + whatever host-API staging the plan has allocated so far
+  return plan->scratch_bytes + (plan->d_x ? plan->max_streams * plan->p.n * 8 : 0) +
+         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
+}
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 
 int amr_fsk_plan_synchronize(amr_fsk_plan* plan) {
@@ -534,6 +539,7 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   HIP_TRY(hipSetDevice(plan->device));
   if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
   if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < plan->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
   if (B == 0) return AMR_OK;
   const int64_t cap = plan->out_cap;
   if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;

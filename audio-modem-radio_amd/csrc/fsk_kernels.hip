@@ -420,22 +420,31 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 }
 
 // F3.  workgroup = stream: the stream's compare bits (in the final row pass's
-// tile order, fft.h fft_bits_stride; <= 49 KiB) are staged in LDS with
-// coalesced 16-B loads, then thread = output word: bit b is 1 when more than
-// half of the compare bits of samples [i-q, min(i+q, n)) are 1,
+// tile order, fft.h fft_bits_stride; 12 KB for a 1-s stream) are staged in
+// LDS with coalesced loads, then thread = output word: bit b is 1 when more
+// than half of the compare bits of samples [i-q, min(i+q, n)) are 1,
 // i = sps/2 + b*sps (np.mean(chunk) > 0.5, modem.py:320-323); bits go MSB first.
+// A stream whose bits exceed kDecideLdsMax (about 4.2 s at 96 kHz, or any
+// longer capture) reads them straight from global memory (L1/L2-served:
+// neighbouring words read neighbouring bytes) instead -- no LDS limit on n.
 constexpr int kDecideThreads = 256;
+constexpr int64_t kDecideLdsMax = 48 * 1024;
 
+template <bool LDS>
 __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __restrict__ bits,
                                                                uint32_t* __restrict__ words, int64_t n_streams,
                                                                FskParams p) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t sb[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_bits[];
   const int64_t s = blockIdx.x;
   const uint8_t* __restrict__ c = bits + (size_t)s * p.bits_stride;
-  const int nb = (int)p.bits_stride;
-  // bits_stride need not be a multiple of 16 (nor rows 16-B aligned): bytes
-  for (int i = threadIdx.x; i < nb; i += kDecideThreads) sb[i] = c[i];
-  __syncthreads();
+  const uint8_t* __restrict__ sb = c;
+  if constexpr (LDS) {
+    const int nb = (int)p.bits_stride;
+    // bits_stride need not be a multiple of 16 (nor rows 16-B aligned): bytes
+    for (int i = threadIdx.x; i < nb; i += kDecideThreads) lds_bits[i] = c[i];
+    __syncthreads();
+    sb = lds_bits;
+  }
   const int64_t q = p.sps / 4, half = p.sps / 2;
   for (int64_t w = threadIdx.x; w < p.n_words; w += kDecideThreads) {
     uint32_t word = 0;
@@ -509,8 +518,14 @@ hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,
                              hipStream_t st) {
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
-  hipLaunchKernelGGL(k_fsk_decide, dim3((unsigned)n_streams), dim3(kDecideThreads), (size_t)p.bits_stride, st, cmp,
-                     words, n_streams, p);
+  // AMR_FSK_DECIDE_GLOBAL=1: the global-memory form at every length (tests)
+  static const bool force_global = [] { const char* e = getenv("AMR_FSK_DECIDE_GLOBAL"); return e && e[0] == '1'; }();
+  if (p.bits_stride <= kDecideLdsMax && !force_global)
+    hipLaunchKernelGGL(k_fsk_decide<true>, dim3((unsigned)n_streams), dim3(kDecideThreads), (size_t)p.bits_stride,
+                       st, cmp, words, n_streams, p);
+  else
+    hipLaunchKernelGGL(k_fsk_decide<false>, dim3((unsigned)n_streams), dim3(kDecideThreads), 0, st, cmp, words,
+                       n_streams, p);
   return hipGetLastError();
 }
 

@@ -88,6 +88,9 @@ typedef struct amr_psk_plan amr_psk_plan;
 typedef struct amr_comm amr_comm;
 
 int amr_abi_version(void);
+/* sha256 prefix of the sources this library was built from (build.py
+ * source_hash): ties a loaded binary to the tree's sources */
+const char *amr_build_id(void);
 const char *amr_last_error(void);
 int amr_device_count(int *count);
 
@@ -118,7 +121,7 @@ int amr_psk_plan_create(amr_psk_plan **plan, int device, int kind, int64_t n_sam
 int amr_psk_plan_destroy(amr_psk_plan *plan);
 /* bytes a stream's output can need: floor(bits/8) */
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan *plan);
-/* scratch bytes the plan holds in HBM */
+/* device bytes the plan holds in HBM (scratch + host-API staging allocated so far) */
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
 int amr_psk_plan_synchronize(amr_psk_plan *plan);
 /* record per-kernel HIP events on the plan's stream (1) or not (0) */
@@ -147,6 +150,14 @@ int amr_psk_demod_fec_device(amr_psk_plan *plan, const void *d_x, int dtype, int
                              int64_t x_stride, uint8_t *d_out, int64_t out_stride, int64_t *d_out_len,
                              int64_t *d_sync_idx, uint8_t *d_fec, int64_t fec_stride, int64_t *d_fec_len,
                              int32_t *d_crc_ok);
+
+/* The slicer stage alone (K4a): differential product s[k+1]*conj(s[k])
+ * (modem.py:214 / 100) and the QPSK sector / BPSK sign decision
+ * (modem.py:216-241 / 102-105) of sym [n_streams][n_sym] complex doubles
+ * (re, im interleaved) -> words [n_streams][ceil(bits/32)], bits MSB first,
+ * bits = (n_sym-1)*2 (QPSK) or n_sym-1 (BPSK).  Synchronous, current device.
+ * For testing the decision at sector edges directly. */
+int amr_psk_slice_host(int kind, const double *sym, int64_t n_streams, int64_t n_sym, uint32_t *words);
 
 /* ---- FSK demodulation (modem.py:298-341) ------------------------------------
  * Replaces modem.fsk_demodulate(samples, baud, mark, space, fs) for a batch of
@@ -213,8 +224,10 @@ int amr_fec_decode_host(const uint8_t *in, int64_t in_stride, const int64_t *in_
  * in its order, and the CRC32 (binascii.crc32) of the payload of those that
  * pass them.  n_cands[s] = occurrences found (may exceed max_cands: records
  * are kept for the first min(n_cands, max_cands, 256); a caller seeing more
- * parses that stream itself).  recs: [n][max_cands].  The host turns records
+ * parses that stream itself).  recs: [n][max_cands], 1 <= max_cands <=
+ * AMR_FRAME_MAX_CANDS (larger is AMR_E_INVALID).  The host turns records
  * into the reference's list of {'name', 'data', 'final_crc'} and log lines. */
+#define AMR_FRAME_MAX_CANDS 256     /* records kept per stream (LDS list of k_frame_parse) */
 #define AMR_FRAME_SHORT 0          /* start + 30 > len(raw)            decoder.py:165 */
 #define AMR_FRAME_NONAME 1         /* name_len == 0                     decoder.py:169 */
 #define AMR_FRAME_NOMETA 2         /* meta_start + 24 > len(raw)        decoder.py:177 */

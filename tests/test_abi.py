@@ -134,3 +134,26 @@ def test_set_inflight_argument_checks(built_lib):
     L = _amr.lib()
     assert L.amr_psk_plan_set_inflight(None, 2) == _amr.AMR_E_INVALID
     assert b"plan is NULL" in L.amr_last_error()
+
+
+def test_build_id_matches_sources(built_lib):
+    """amr_build_id() is the content hash of the sources the library was built
+    from; it must equal the hash of this tree's sources (no stale binary)."""
+    import _amr
+    import build
+    assert _amr.lib().amr_build_id().decode() == build.source_hash()
+
+
+def test_frame_parse_max_cands_bound(built_lib):
+    """The kernel keeps at most AMR_FRAME_MAX_CANDS (256) records per stream:
+    a larger max_cands is refused instead of leaving records unwritten."""
+    import _amr
+    L = _amr.lib()
+    cnt = np.zeros(1, np.int32)
+    lens = np.array([4], np.int64)
+    buf = np.zeros((1, 4), np.uint8)
+    recs = np.zeros((1, 257), _amr.FRAME_REC)
+    assert L.amr_frame_parse_host(_amr.ptr(buf), 4, _amr.ptr(lens), 1, 257, _amr.ptr(cnt),
+                                  recs.ctypes.data) == _amr.AMR_E_INVALID
+    assert b"AMR_FRAME_MAX_CANDS" in L.amr_last_error()
+    assert L.amr_frame_parse_device(None, None, 4, None, 1, 257, None, None) == _amr.AMR_E_INVALID

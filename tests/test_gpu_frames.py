@@ -1,11 +1,10 @@
-"""GPU frame parse (k_frame_parse) against the host restatement of
-the reference's decoder.parse_fbp_stream_enhanced (decoder.py:142-208): the
+"""GPU frame parse (k_frame_parse) against the REFERENCE's own
+decoder.parse_fbp_stream_enhanced (decoder.py:142-208) output on the same
+streams (tests/golden/frames.json, written by make_frames_golden.py): the
 same frames (name, payload, final_crc) and the same log lines, stream by
 stream, over every branch of the reference's candidate checks."""
-import binascii
 import contextlib
 import io
-import struct
 
 import numpy as np
 import pytest
@@ -20,36 +19,14 @@ def gpu(built_lib):
         pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
 
 
-def frame(name: bytes, payload: bytes, part=0, total=1, fsize=None, fcrc=0x1234, pcrc=None, dlen=None) -> bytes:
-    meta = struct.pack('<IIIIII', part, total, len(payload) if fsize is None else fsize, fcrc,
-                       len(payload) if dlen is None else dlen,
-                       (binascii.crc32(payload) & 0xFFFFFFFF) if pcrc is None else pcrc)
-    return b'FBPC' + bytes([len(name)]) + name + meta + payload
+from frame_streams import streams  # noqa: E402  (shared with tests/golden/make_frames_golden.py)
 
 
-def streams():
-    rng = np.random.default_rng(11)
-    rnd = lambda n: rng.integers(0, 256, n, dtype=np.uint8).tobytes()   # noqa: E731
-    ok1 = frame(b"a.txt", b"RAW" + rnd(300), part=2, total=5)
-    ok2 = frame("ção.bin".encode(), rnd(1000))
-    return [
-        b"",                                                   # nothing
-        rnd(2000),                                             # noise
-        ok1,                                                   # one valid frame
-        rnd(37) + ok1 + rnd(5) + ok2 + rnd(11),                # two frames, unaligned
-        frame(b"x", rnd(64), pcrc=0xDEADBEEF),                 # CRC error
-        frame(b"y", rnd(64))[:-10],                            # payload past the end
-        b"FBPC" + bytes([0]) + rnd(40),                        # name_len == 0
-        frame(b"z", rnd(8), dlen=0) + rnd(8),                  # dlen == 0
-        frame(b"z", rnd(8), dlen=60_000_000) + rnd(8),         # absurd dlen
-        rnd(10) + b"FBPC" + rnd(20),                           # start + 30 > len
-        b"FBPC" + bytes([200]) + rnd(60),                      # meta past the end
-        b"FBPCFBPC" + ok1,                                     # overlapping magics
-        ok1 + b"FBPC",                                         # magic in the last 4 bytes
-        b"FBPC" * 100 + ok2,                                   # more magics than max_cands
-        rnd(5000) + ok2 + rnd(3000) + ok1,                     # long stream
-        frame(b"\xff\xfe", rnd(17)),                           # undecodable name bytes
-    ]
+def golden_frames():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "frames.json")) as f:
+        return json.load(f)["cases"]
 
 
 def host_parse(raw):
@@ -60,18 +37,27 @@ def host_parse(raw):
     return res, buf.getvalue()
 
 
-def test_batch_parse_matches_host_parse():
+@pytest.mark.parametrize("max_cands", [64, 256])
+def test_batch_parse_matches_reference_fixtures(max_cands):
+    """The GPU batch parse == the reference's frames and log lines, per stream
+    (streams with more magics than max_cands take the host restatement)."""
     import decoder
-    raws = streams()
+    cases = golden_frames()
+    raws = [bytes.fromhex(c["raw"]) for c in cases]
+    assert raws == streams()
+    for raw, c in zip(raws, cases):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            got = decoder.parse_fbp_stream_enhanced_batch([raw], max_cands=max_cands)[0]
+        assert [{"name": f["name"], "data": bytes(f["data"]).hex(), "final_crc": int(f["final_crc"])}
+                for f in got] == c["frames"], c["id"]
+        assert buf.getvalue() == c["log"], c["id"]
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        got = decoder.parse_fbp_stream_enhanced_batch(raws, max_cands=64)
-    want_log = []
-    for raw, g in zip(raws, got):
-        w, log = host_parse(raw)
-        assert g == w
-        want_log.append(log)
-    assert buf.getvalue() == "".join(want_log)
+        allg = decoder.parse_fbp_stream_enhanced_batch(raws, max_cands=max_cands)   # one launch, all streams
+    assert [[{"name": f["name"], "data": bytes(f["data"]).hex(), "final_crc": int(f["final_crc"])} for f in g]
+            for g in allg] == [c["frames"] for c in cases]
+    assert buf.getvalue() == "".join(c["log"] for c in cases)
 
 
 def test_records_follow_the_reference_checks():

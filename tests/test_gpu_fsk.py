@@ -190,3 +190,18 @@ def test_fsk_long_stream_vs_oracle():
         got, _ = pl.demod_host(x)
         want = [oracle.fsk_demodulate(x[i], 9600, 12000.0, 24000.0) for i in range(2)]
         assert got == want, N
+
+
+def test_fsk_20s_stream_vs_oracle():
+    """A 20-s FSK1200 capture (1 920 000 samples; tones 2400/4800 Hz round-trip,
+    SURVEY §4): its compare bits (~240 KB) exceed the decide kernel's LDS
+    staging, so the decisions are read from global memory -- still == oracle."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    N = 1_920_000
+    x = synth.fsk_batch(1, N, 1200, 2400.0, 4800.0, seed=20, distinct=1, noise=0.3)
+    pl = _fsk.FskPlan(N, 1200, 2400.0, 4800.0, max_streams=1)
+    got, _ = pl.demod_host(x)
+    assert got[0] == oracle.fsk_demodulate(x[0], 1200, 2400.0, 4800.0)
+    assert len(got[0]) > 1000

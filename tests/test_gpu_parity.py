@@ -139,14 +139,17 @@ def test_fec_gpu_matches_reference(golden):
     assert ("Aviso: CRC" in buf.getvalue()) == manifest["fec"][-1]["crc_warn"]
 
 
-def test_fec_fused_after_8psk_demod():
-    """Config 5: 8PSK@19200 demod + FEC decode fused on the device == oracle chain."""
+@pytest.mark.parametrize("B", [64, 8192])
+def test_fec_fused_after_8psk_demod(B):
+    """Config 5: 8PSK@19200 demod + FEC decode fused on the device == oracle
+    chain (psk_demod_batch then fec_decode, fec.py:34-69), every stream -- at
+    B=64 and at BASELINE configs[5]'s full batch of 8192 (one launch: K1g)."""
     import ctypes
     import _amr
     import synth
     from oracle import oracle
-    B, N = 64, 96000
-    x = synth.dpsk8_batch(B, N, 19200, seed=11, distinct=4)
+    N = 96000
+    x = synth.dpsk8_batch(B, N, 19200, seed=11, distinct=4 if B < 256 else 64)
     plan = _amr.PskPlan("qpsk", N, 19200, max_streams=B)
     L = _amr.lib()
     cap = plan.out_cap
@@ -170,11 +173,13 @@ def test_fec_fused_after_8psk_demod():
     finally:
         for p in ptrs.values():
             L.amr_free(p)
-    dem, _ = oracle.psk_demod_batch("qpsk", x, 19200, n_threads=8)
+    dem, _ = oracle.psk_demod_batch("qpsk", x, 19200, n_threads=min(16, os.cpu_count() or 1))
+    bad = []
     for i in range(B):
         want, wok = oracle.fec_decode(dem[i])
-        assert fec_out[i, :flen[i]].tobytes() == want
-        assert bool(ok[i]) == wok
+        if fec_out[i, :flen[i]].tobytes() != want or bool(ok[i]) != wok:
+            bad.append(i)
+    assert not bad, f"{len(bad)} of {B} streams differ, first {bad[:5]}"
 
 
 def test_decode_wav_file_end_to_end(golden, tmp_path, monkeypatch):
@@ -301,3 +306,31 @@ def test_pcm16_wav_path_equals_float64_path():
         pcm = (x * 20000).astype(np.int16)
         want = modem.fsk_demodulate(pcm / 32768.0, 9600, 12000.0, 24000.0)
         assert modem._pcm16_fsk(pcm, 9600, 12000.0, 24000.0) == want
+
+
+def test_fsk_decide_global_form_forced(tmp_path):
+    """The FSK decide kernel's global-memory form (taken for streams whose
+    compare bits exceed its LDS staging, e.g. 20-s captures) forced at every
+    length: seeded batches == oracle.  One subprocess (the switch is read once)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    script = tmp_path / "fg.py"
+    script.write_text(f'''
+import sys
+sys.path[:0] = [{os.path.join(root, "audio-modem-radio_amd")!r}, {root!r}, {here!r}]
+import numpy as np
+import _fsk, synth
+from oracle import oracle
+bad = []
+for (B, N, baud, m, s) in ((24, 96000, 9600, 12000.0, 24000.0), (5, 30011, 4800, 8000.0, 16000.0)):
+    x = synth.fsk_batch(B, N, baud, m, s, seed=B, distinct=4, noise=0.3)
+    got, _ = _fsk.FskPlan(N, baud, m, s, max_streams=B).demod_host(x)
+    bad += [(N, i) for i in range(B) if got[i] != oracle.fsk_demodulate(x[i], baud, m, s)]
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+''')
+    env = dict(os.environ, AMR_FSK_DECIDE_GLOBAL="1")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=250)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
