@@ -42,11 +42,11 @@ EXPORTS = [
     "amr_psk_plan_create", "amr_psk_plan_destroy", "amr_psk_plan_out_capacity", "amr_psk_plan_scratch_bytes",
     "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings", "amr_psk_plan_set_inflight",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
-    "amr_psk_slice_host",
+    "amr_psk_slice_host", "amr_psk_plan_last_layout", "amr_synth_tile_noise",
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
-    "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather",
+    "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather", "amr_fsk_allgather",
     "amr_comm_synchronize", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
     "amr_resample_host",
 ]
@@ -176,6 +176,8 @@ def lib():
             "amr_psk_demod_device": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
             "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
+            "amr_psk_plan_last_layout": (I32, [P]),
+            "amr_synth_tile_noise": (I32, [P, I64, I64, P, I64, I64, F, ctypes.c_uint64]),
             "amr_fsk_plan_create": (I32, [P, I32, I64, I64, P, P, P, P, P, P, I32, I64]),
             "amr_fsk_plan_destroy": (I32, [P]),
             "amr_fsk_plan_out_capacity": (I64, [P]),
@@ -196,6 +198,7 @@ def lib():
             "amr_comm_create": (I32, [P, P, I32, I32, I32]),
             "amr_comm_destroy": (I32, [P]),
             "amr_allgather": (I32, [P, P, P, I64, P]),
+            "amr_fsk_allgather": (I32, [P, P, P, I64, P]),
             "amr_comm_synchronize": (I32, [P]),
             "amr_tx_samples": (I64, [I32, I64, D, D]),
             "amr_resample_host": (I32, [P, I64, I64, I64, P, I32]),
@@ -348,6 +351,10 @@ class PskPlan:
         ms = (ctypes.c_float * len(T_NAMES))()
         check(lib().amr_psk_plan_timings(self.handle, ms, len(T_NAMES)))
         return {k: float(v) for k, v in zip(T_NAMES, ms) if v >= 0}
+
+    def last_layout(self) -> str:
+        """'row' (state-per-lane kernels) or 'lane' (one stream per lane) for the last call."""
+        return {0: "row", 1: "lane"}.get(int(lib().amr_psk_plan_last_layout(self.handle)), "?")
 
     def exact_streams(self) -> int:
         c = ctypes.c_int64(0)

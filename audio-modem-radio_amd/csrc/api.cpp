@@ -10,6 +10,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "amr_internal.h"
@@ -21,6 +22,13 @@ hipError_t launch_psk_lowpass_fwd(const PskBuffers&, const PskParams&, const Iir
 hipError_t launch_psk_lowpass_bwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_lowpass_exact(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_slice(const PskBuffers&, const PskParams&, hipStream_t);
+hipError_t launch_psk_bandpass_lane(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_lowpass_lane(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+int64_t psk_lane_bp_scratch_doubles(int64_t n_streams, int64_t n, int pad);
+int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad);
+int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2);
+hipError_t launch_synth_tile_noise(const float*, int64_t, int64_t, float*, int64_t, int64_t, float, uint64_t,
+                                   hipStream_t);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
                             hipStream_t);
 hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, uint8_t*, int64_t, int64_t*,
@@ -145,6 +153,9 @@ bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }
 // doubles of slack below s1/s3: the backward passes prefetch up to a few
 // chunks past the start of their block instead of clamping the index
 constexpr int64_t kFrontSlack = 8192;
+// streams in flight (batch x amr_psk_plan_set_inflight) from which the
+// lane-per-stream layout runs
+constexpr int64_t kLaneMinLiveStreams = 16384;
 
 struct amr_psk_plan {
   std::mutex mu;
@@ -164,6 +175,7 @@ struct amr_psk_plan {
   double* s3 = nullptr;   // = s3_base + kFrontSlack
   double* s1_base = nullptr;
   double* s3_base = nullptr;
+  int64_t s1_bytes = 0, s3_bytes = 0;   // allocated (the row layout grows them on first use)
   uint32_t* words = nullptr;
   int32_t* flags = nullptr;
   int64_t scratch_bytes = 0;
@@ -179,6 +191,7 @@ struct amr_psk_plan {
   // timing
   bool timing = false;
   int inflight = 1;             // amr_psk_plan_set_inflight hint
+  int last_layout = 0;          // AMR_LAYOUT_* of the last call
   hipEvent_t ev[AMR_T_COUNT + 1][2]{};
   bool ev_used[AMR_T_COUNT]{};
   int64_t last_exact = 0;
@@ -189,6 +202,46 @@ struct amr_comm {
   hipStream_t stream = nullptr;
   int device = 0;
 };
+
+namespace {
+// bytes of s1 / s3 each layout needs (psk_kernels.hip / psk_lane_kernels.hip)
+int64_t lane_s1_bytes(const amr_psk_plan* pl) {
+  const int64_t g = pl->groups;
+  return std::max(2 * g * std::max<int64_t>(pl->p.n_sym, 1) * kWave * 8,
+                  psk_lane_bp_scratch_doubles(pl->max_streams, pl->p.n, pl->p.pad1) * 8);
+}
+int64_t lane_s3_bytes(const amr_psk_plan* pl) {
+  return std::max(psk_lane_lp_scratch_doubles(pl->max_streams, pl->p.n, pl->p.pad2) * 8,
+                  psk_exact_scratch_bytes(pl->max_streams, pl->p.m2));
+}
+int64_t row_s1_bytes(const amr_psk_plan* pl) {
+  return std::max(pl->groups * pl->m1_pairs * kWave * 16, lane_s1_bytes(pl));
+}
+int64_t row_s3_bytes(const amr_psk_plan* pl) {
+  return std::max(2 * pl->groups * pl->m2_pairs * kWave * 16, lane_s3_bytes(pl));
+}
+// grow s1 / s3 to the row layout's sizes (its forward outputs are full length)
+int ensure_row_buffers(amr_psk_plan* pl) {
+  const int64_t b1 = kFrontSlack * 8 + row_s1_bytes(pl), b3 = kFrontSlack * 8 + row_s3_bytes(pl);
+  for (auto [base, have, want] : {std::tuple<double**, int64_t*, int64_t>{&pl->s1_base, &pl->s1_bytes, b1},
+                                  std::tuple<double**, int64_t*, int64_t>{&pl->s3_base, &pl->s3_bytes, b3}}) {
+    if (*have >= want) continue;
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    HIP_TRY(hipFree(*base));
+    *base = nullptr;
+    hipError_t e = hipMalloc(base, (size_t)want);
+    if (e != hipSuccess) {
+      *have = 0;
+      return fail(AMR_E_NOMEM, "hipMalloc(" + std::to_string(want) + " B): " + hipGetErrorString(e));
+    }
+    pl->scratch_bytes += want - *have;
+    *have = want;
+  }
+  pl->s1 = pl->s1_base + kFrontSlack;
+  pl->s3 = pl->s3_base + kFrontSlack;
+  return AMR_OK;
+}
+}  // namespace
 
 namespace amr {
 int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
@@ -338,10 +391,12 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
       // + slack: K2q's prefetch runs up to a few chunks past the end (psk_kernels.hip)
       {(void**)&pl->lo2, (n * 2 + 1024) * (int64_t)sizeof(double)},
       // s1 doubles as the symbol buffer [2G][S][64] after K1 (sym_index in psk_kernels.hip)
-      {(void**)&pl->s1_base,
-       kFrontSlack * 8 + std::max(g * pl->m1_pairs * kWave * 16, 2 * g * std::max<int64_t>(p.n_sym, 1) * kWave * 8)},
+      // s1 / s3 sized for the lane layout (checkpoints, symbols, K3x's slots);
+      // the row layout's full-length intermediates are allocated on its first
+      // call (ensure_row_buffers)
+      {(void**)&pl->s1_base, kFrontSlack * 8 + lane_s1_bytes(pl)},
       {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
-      {(void**)&pl->s3_base, kFrontSlack * 8 + 2 * g * pl->m2_pairs * kWave * 16},
+      {(void**)&pl->s3_base, kFrontSlack * 8 + lane_s3_bytes(pl)},
       {(void**)&pl->words, g * kWave * p.n_words * 4},
       {(void**)&pl->flags, g * kWave * 4},
   };
@@ -355,6 +410,8 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   }
   pl->s1 = pl->s1_base + kFrontSlack;
   pl->s3 = pl->s3_base + kFrontSlack;
+  pl->s1_bytes = kFrontSlack * 8 + lane_s1_bytes(pl);
+  pl->s3_bytes = kFrontSlack * 8 + lane_s3_bytes(pl);
   {
     // device LO layout [n][4] = (lo_re, -(0*lo_im), lo_im, 0*lo_re): per sample and
     // component the (multiplier, addend) pair of numpy's complex multiply
@@ -389,9 +446,8 @@ int amr_psk_plan_destroy(amr_psk_plan* plan) {
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) {
   if (!plan) return -1;
-  // scratch + whatever host-API staging the plan has allocated so far
-  return plan->scratch_bytes + (plan->d_x ? plan->d_x_bytes : 0) +
-         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
+  // scratch + the host-API staging (allocated on the first amr_psk_demod_host)
+  return plan->scratch_bytes + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
 }
 
 int amr_psk_plan_synchronize(amr_psk_plan* plan) {
@@ -433,6 +489,8 @@ int amr_psk_plan_timings(amr_psk_plan* plan, float* ms, int count) {
   return AMR_OK;
 }
 
+int amr_psk_plan_last_layout(const amr_psk_plan* plan) { return plan ? plan->last_layout : -1; }
+
 int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
   if (!plan || !count) return fail(AMR_E_INVALID, "NULL argument");
   std::lock_guard<std::mutex> lk(plan->mu);
@@ -462,6 +520,19 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   pl->last_exact = B;
   if (B == 0) return AMR_OK;
   hipStream_t st = pl->stream;
+  // Layout: one stream per lane (psk_lane_kernels.hip) once
+  // enough streams are in flight on the device to give it waves -- it does
+  // a third of the arithmetic per stream -- else the state-per-lane kernels
+  // (more waves per stream, lower latency).  AMR_PSK_LANE=0/1 forces either.
+  static const int lane_force = [] {
+    const char* e = std::getenv("AMR_PSK_LANE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  const int64_t live = B * (pl->inflight > 1 ? pl->inflight : 1);
+  const bool lane = pl->bp.nt == 9 && (lane_force >= 0 ? lane_force == 1 : live >= kLaneMinLiveStreams);
+  pl->last_layout = lane ? AMR_LAYOUT_LANE : AMR_LAYOUT_ROW;
+  if (!lane && pl->p.n_sym >= 2)
+    if (int rc = ensure_row_buffers(pl)) return rc;
   PskBuffers b{};
   b.x = d_x;
   b.x_stride = x_stride;
@@ -501,6 +572,25 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     // modem.py:95-96, 211: fewer than two symbols -> b''
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
+  } else if (lane) {
+    HIP_TRY(mark(AMR_T_BANDPASS, 0));
+    HIP_TRY(launch_psk_bandpass_lane(b, pl->p, pl->bp, st));
+    HIP_TRY(mark(AMR_T_BANDPASS, 1));
+    if (pl->lp_exact_only) {
+      HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)pl->flags, 1, (size_t)B, st));
+    } else {
+      // forward + backward low-pass in one kernel: timed in the lowpass_fwd slot
+      HIP_TRY(mark(AMR_T_LOWPASS_FWD, 0));
+      HIP_TRY(launch_psk_lowpass_lane(b, pl->p, pl->lp, st));
+      HIP_TRY(mark(AMR_T_LOWPASS_FWD, 1));
+    }
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 0));
+    HIP_TRY(launch_psk_lowpass_exact(b, pl->p, pl->lp, st));
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
+    HIP_TRY(launch_psk_slice(b, pl->p, st));
+    HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
   } else {
     HIP_TRY(mark(AMR_T_BANDPASS, 0));
     HIP_TRY(launch_psk_bandpass(b, pl->p, pl->bp, st));
@@ -648,6 +738,17 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
   return AMR_OK;
 }
 
+// ---- benchmark / test input generator --------------------------------------
+int amr_synth_tile_noise(const float* d_base, int64_t n_base, int64_t n_samples, float* d_out, int64_t n_streams,
+                         int64_t row_offset, float sigma, uint64_t seed) {
+  if (n_streams < 0 || n_samples < 0 || (n_streams && (!d_base || !d_out || n_base < 1)))
+    return fail(AMR_E_INVALID, "amr_synth_tile_noise: bad argument");
+  HIP_TRY(launch_synth_tile_noise(d_base, n_base, n_samples, d_out, n_streams, row_offset < 0 ? 0 : row_offset, sigma,
+                                  seed, nullptr));
+  HIP_TRY(hipDeviceSynchronize());
+  return AMR_OK;
+}
+
 // ---- the slicer stage alone (modem.py:214-241 / 100-105) ---------------------
 int amr_psk_slice_host(int kind, const double* sym, int64_t n_streams, int64_t n_sym, uint32_t* words) {
   if (kind != AMR_PSK_QPSK && kind != AMR_PSK_BPSK) return fail(AMR_E_INVALID, "unknown PSK kind");
@@ -752,6 +853,47 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
   return AMR_OK;
 }
 
+}  // extern "C"
+
+namespace amr {
+// The gather on the communicator's own stream, in call order (so several
+// plans -- batches in flight on several streams -- can share one
+// communicator without two ranks ever entering its collectives in different
+// orders).  With a producer stream, the gather waits for the work already
+// queued there (event) and the producer's later work waits for the gather
+// (it may reuse the send buffer).
+int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
+                    bool ordered) {
+  if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
+  HIP_TRY(hipSetDevice(comm->device));
+  hipEvent_t before = nullptr, after = nullptr;
+  if (ordered) {
+    HIP_TRY(hipEventCreateWithFlags(&before, hipEventDisableTiming));
+    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(before, producer);
+    if (e == hipSuccess) e = hipStreamWaitEvent(comm->stream, before, 0);
+    if (e != hipSuccess) {
+      (void)hipEventDestroy(before);
+      if (after) (void)hipEventDestroy(after);
+      return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
+    }
+  }
+  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, comm->stream);
+  hipError_t e = hipSuccess;
+  if (ordered) {
+    if (r == ncclSuccess) e = hipEventRecord(after, comm->stream);
+    if (r == ncclSuccess && e == hipSuccess) e = hipStreamWaitEvent(producer, after, 0);
+    (void)hipEventDestroy(before);                 // released once the waits are done
+    (void)hipEventDestroy(after);
+  }
+  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
+  return AMR_OK;
+}
+}  // namespace amr
+
+extern "C" {
+
 // ---- RCCL -------------------------------------------------------------------
 int amr_comm_unique_id(uint8_t* id) {
   if (!id) return fail(AMR_E_INVALID, "id is NULL");
@@ -802,31 +944,7 @@ int amr_comm_destroy(amr_comm* comm) {
 // the plan's stream (event), and the plan's later work waits for the gather
 // (it reads the plan's output buffer).
 int amr_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_psk_plan* plan) {
-  if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
-  HIP_TRY(hipSetDevice(comm->device));
-  hipEvent_t before = nullptr, after = nullptr;
-  if (plan) {
-    HIP_TRY(hipEventCreateWithFlags(&before, hipEventDisableTiming));
-    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(before, plan->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(comm->stream, before, 0);
-    if (e != hipSuccess) {
-      (void)hipEventDestroy(before);
-      if (after) (void)hipEventDestroy(after);
-      return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
-    }
-  }
-  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, comm->stream);
-  hipError_t e = hipSuccess;
-  if (plan) {
-    if (r == ncclSuccess) e = hipEventRecord(after, comm->stream);
-    if (r == ncclSuccess && e == hipSuccess) e = hipStreamWaitEvent(plan->stream, after, 0);
-    (void)hipEventDestroy(before);                 // released once the waits are done
-    (void)hipEventDestroy(after);
-  }
-  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
-  return AMR_OK;
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan ? plan->stream : nullptr, plan != nullptr);
 }
 
 int amr_comm_synchronize(amr_comm* comm) {

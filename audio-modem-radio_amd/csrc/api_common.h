@@ -29,6 +29,9 @@ int copy_batch_h2d(void* dst, const void* src, int64_t row_bytes, int64_t src_pi
 // pageable memory ran as one transfer per row -- 16384 rows took 215 ms.
 int copy_batch_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes, int64_t B,
                    hipStream_t st);
+// the RCCL all-gather of amr_allgather / amr_fsk_allgather (api.cpp)
+int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
+                    bool ordered);
 }  // namespace amr
 
 #define HIP_TRY(expr)                                                                              \

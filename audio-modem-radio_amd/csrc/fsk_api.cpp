@@ -484,9 +484,8 @@ int amr_fsk_plan_destroy(amr_fsk_plan* plan) {
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
-  // scratch + whatever host-API staging the plan has allocated so far
-  return plan->scratch_bytes + (plan->d_x ? plan->max_streams * plan->p.n * 8 : 0) +
-         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
+  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host)
+  return plan->scratch_bytes + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 
@@ -519,6 +518,10 @@ int amr_fsk_plan_timings(amr_fsk_plan* plan, float* ms, int count) {
     if (plan->timing && plan->ev_used[i]) HIP_TRY(hipEventElapsedTime(&ms[i], plan->ev[i][0], plan->ev[i][1]));
   }
   return AMR_OK;
+}
+
+int amr_fsk_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_fsk_plan* plan) {
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan ? plan->stream : nullptr, plan != nullptr);
 }
 
 int amr_fsk_demod_device(amr_fsk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,

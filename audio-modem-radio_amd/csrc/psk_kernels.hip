@@ -43,40 +43,9 @@
 #include <type_traits>
 
 #include "amr_internal.h"
+#include "psk_common.h"
 
 namespace amr {
-
-// ---------------------------------------------------------------------------
-// input conversion + odd extension in the INPUT's precision
-// (scipy _arraytools.odd_ext: 2*x[0] - x[k] on the caller's dtype)
-template <typename T> struct In;
-template <> struct In<float> {
-  static __device__ __forceinline__ double cvt(float v) { return (double)v; }
-  static __device__ __forceinline__ double ext(float e, float v) { return (double)(2.0f * e - v); }
-};
-template <> struct In<double> {
-  static __device__ __forceinline__ double cvt(double v) { return v; }
-  static __device__ __forceinline__ double ext(double e, double v) { return 2.0 * e - v; }
-};
-template <> struct In<int16_t> {   // decode_wav_file: float64 = int16 / 32768 (exact)
-  static __device__ __forceinline__ double cvt(int16_t v) { return (double)v / 32768.0; }
-  static __device__ __forceinline__ double ext(int16_t e, int16_t v) { return 2.0 * cvt(e) - cvt(v); }
-};
-
-// class masks for __builtin_amdgcn_class (v_cmp_class_f64)
-// bit: 0 sNaN 1 qNaN 2 -inf 3 -norm 4 -denorm 5 -0 6 +0 7 +denorm 8 +norm 9 +inf
-constexpr int kClsX = 0x2B7;   // low-pass INPUT not provably safe: NaN, inf, denormal, -0
-constexpr int kClsY = 0x2F7;   // low-pass OUTPUT not provably safe: the above and +0
-
-// s2 (band-pass output f): [group][half][n2][32 streams][2 samples] doubles,
-// so that a low-pass wave (one half-group) streams one 512 B row per 2 samples.
-__device__ __forceinline__ size_t f_index(int64_t g, int64_t n2, int64_t i, int s_in_group) {
-  const int h = s_in_group >> 5, sl = s_in_group & 31;
-  return ((size_t)((g * 2 + h) * n2 + (i >> 1)) * 32 + sl) * 2 + (i & 1);
-}
-
-typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector: SROA-friendly (HIP's uint4 is a struct)
-typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 constexpr int kTileBytes = 256;                 // bytes of one stream per input tile
 constexpr int kTilePitch = kTileBytes + 16;     // LDS row pitch: conflict-free ds_read_b128 per lane
@@ -654,11 +623,6 @@ __global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p
 // there is provably harmless.
 constexpr int kLpChunk = 16;                    // samples per low-pass prefetch chunk
 
-// symbol buffer: [stream][symbol][re, im] doubles
-__device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k, int comp) {
-  return ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2 + comp;
-}
-
 // ---------------------------------------------------------------------------
 // K2q / K3q: the low-pass with ONE STATE PER LANE of a quad (lane j owns z[j]
 // of the 5-tap recurrence); a wave serves 16 streams x one component, so the
@@ -683,9 +647,6 @@ constexpr int kQuadShift = 0xF9;                // quad_perm [1,2,3,3]
 constexpr int kLpQChunk = 8;                    // K2q main-body chunk (samples)
 constexpr int kLpQRing = 8;                     // K2q f prefetch ring depth (8-sample chunks)
 constexpr int kLpBRing = 5;                     // K3q prefetch ring depth (chunks of 20/16 samples)
-typedef __attribute__((address_space(4))) const double CDouble;   // constant AS: uniform loads -> SMEM
-constexpr float kTinyHi = 0x1p-126f;            // FLT_MIN
-
 struct Quad5 {
   double b0, cb, ca, cm;
 };
@@ -706,14 +667,6 @@ __device__ __forceinline__ double quad5_step(const Quad5& c, double& z, double x
   const double zC = dpp_f64<kQuadShift>(z) * c.cm;
   z = (zC + x * c.cb) - y * c.ca;
   return y;
-}
-
-__device__ __forceinline__ float tiny_min3(float acc, double a, double b) {
-  const float ha = __builtin_bit_cast(float, (unsigned)(__builtin_bit_cast(unsigned long long, a) >> 32));
-  const float hb = __builtin_bit_cast(float, (unsigned)(__builtin_bit_cast(unsigned long long, b) >> 32));
-  float r;
-  asm("v_min3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(acc), "v"(ha), "v"(hb));
-  return r;
 }
 
 // s3 for K2q/K3q: [w16][comp][q/2][16 streams][2] doubles
@@ -1042,68 +995,80 @@ __device__ __forceinline__ void cmul_np(double ar, double ai, double br, double 
   im = __builtin_fma(ar, bi, ai * br);
 }
 
+// K3x scratch: kExactSlots waves, each owning one [m2][64] double2 slot and
+// walking the groups g = slot, slot + kExactSlots, ... (flagged streams are
+// rare: silence, NaN/inf captures), so the scratch does not scale with B.
+constexpr int kExactSlots = 8;
+int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2) {
+  const int64_t g = (n_streams + kWave - 1) / kWave;
+  return (g < kExactSlots ? g : kExactSlots) * m2 * kWave * 16;
+}
+
 template <int NT>
 __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams p, Iir f) {
   const int lane = threadIdx.x;
-  const int64_t g = blockIdx.x;
-  const int64_t s = g * kWave + lane;
-  const bool live = s < buf.n_streams && buf.flags[s] != 0;
-  if (!__any(live)) return;                     // wave-uniform early exit (the common case)
+  const int64_t n_groups = (buf.n_streams + kWave - 1) / kWave;
   const int64_t n = p.n;
   const int64_t n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int64_t m2 = p.m2;
   const int64_t S = p.n_sym;
   const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
-  double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)g * m2 * kWave + lane;
+  double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)blockIdx.x * m2 * kWave + lane;
   double2* __restrict__ sym2 = reinterpret_cast<double2*>(buf.s1);
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+    const int64_t s = g * kWave + lane;
+    const bool live = s < buf.n_streams && buf.flags[s] != 0;
+    if (!__any(live)) continue;                 // wave-uniform skip (the common case)
 
-  double b[NT], a[NT], zr[NT - 1], zc[NT - 1];
+    double b[NT], a[NT], zr[NT - 1], zc[NT - 1];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
+    for (int i = 0; i < NT; ++i) { b[i] = f.b[i]; a[i] = f.a[i]; }
 
-  auto bb = [&](int64_t i) -> double2 {         // (f + 0j) * lo[i], numpy's complex multiply
-    const double fv = buf.s2[f_index(g, n2, i, lane)];
-    const double4 l = lo[i];
-    return make_double2(__builtin_fma(fv, l.x, l.y), __builtin_fma(fv, l.z, l.w));
-  };
-  // odd extension with numpy complex ops: (2+0j)*x[0] - x[k]
-  const double2 x0 = bb(0), xl = bb(n - 1);
-  double l2r, l2i, r2r, r2i;
-  cmul_np(2.0, 0.0, x0.x, x0.y, l2r, l2i);
-  cmul_np(2.0, 0.0, xl.x, xl.y, r2r, r2i);
-  auto ext = [&](int64_t j) -> double2 {
-    if (j < pad) { const double2 v = bb(pad - j); return make_double2(l2r - v.x, l2i - v.y); }
-    if (j < pad + n) return bb(j - pad);
-    const double2 v = bb(n - 2 - (j - pad - n));
-    return make_double2(r2r - v.x, r2i - v.y);
-  };
-  {
-    const double2 e0 = ext(0);
+    auto bb = [&](int64_t i) -> double2 {       // (f + 0j) * lo[i], numpy's complex multiply
+      const double fv = buf.s2[f_index(g, n2, i, lane)];
+      const double4 l = lo[i];
+      return make_double2(__builtin_fma(fv, l.x, l.y), __builtin_fma(fv, l.z, l.w));
+    };
+    // odd extension with numpy complex ops: (2+0j)*x[0] - x[k]
+    const double2 x0 = bb(0), xl = bb(n - 1);
+    double l2r, l2i, r2r, r2i;
+    cmul_np(2.0, 0.0, x0.x, x0.y, l2r, l2i);
+    cmul_np(2.0, 0.0, xl.x, xl.y, r2r, r2i);
+    auto ext = [&](int64_t j) -> double2 {
+      if (j < pad) { const double2 v = bb(pad - j); return make_double2(l2r - v.x, l2i - v.y); }
+      if (j < pad + n) return bb(j - pad);
+      const double2 v = bb(n - 2 - (j - pad - n));
+      return make_double2(r2r - v.x, r2i - v.y);
+    };
+    {
+      const double2 e0 = ext(0);
 #pragma unroll
-    for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, e0.x, e0.y, zr[i], zc[i]);
-  }
-  double y0 = 0, y1 = 0;
-  for (int64_t j = 0; j < m2; ++j) {
-    const double2 e = ext(j);
-    df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, y0, y1);
-    sc[(size_t)j * kWave] = make_double2(y0, y1);
-  }
-  __threadfence();
-#pragma unroll
-  for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, y0, y1, zr[i], zc[i]);
-
-  int64_t k = S - 1;
-  int64_t next_n = p.first + k * p.sps;
-  for (int64_t j = m2 - 1; j >= 0; --j) {
-    const double2 e = sc[(size_t)j * kWave];
-    double o0, o1;
-    df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
-    if (j - pad == next_n && k >= 0) {
-      if (live) sym2[sym_index(s, S, k, 0) >> 1] = make_double2(o0, o1);
-      --k;
-      next_n -= p.sps;
+      for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, e0.x, e0.y, zr[i], zc[i]);
     }
+    double y0 = 0, y1 = 0;
+    for (int64_t j = 0; j < m2; ++j) {
+      const double2 e = ext(j);
+      df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, y0, y1);
+      sc[(size_t)j * kWave] = make_double2(y0, y1);
+    }
+    __threadfence();
+#pragma unroll
+    for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, y0, y1, zr[i], zc[i]);
+
+    int64_t k = S - 1;
+    int64_t next_n = p.first + k * p.sps;
+    for (int64_t j = m2 - 1; j >= 0; --j) {
+      const double2 e = sc[(size_t)j * kWave];
+      double o0, o1;
+      df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
+      if (j - pad == next_n && k >= 0) {
+        if (live) sym2[sym_index(s, S, k, 0) >> 1] = make_double2(o0, o1);
+        --k;
+        next_n -= p.sps;
+      }
+    }
+    __threadfence();                            // the slot's scratch is rewritten for the next group
   }
 }
 
@@ -1118,8 +1083,32 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 // 2^-30 relative) the sector is read off the signs; near an edge (or for
 // zeros / NaN / inf) the reference's own steps are replayed: atan2, +2pi if
 // negative, the same four comparisons against the same double constants.
+// np.angle near a sector edge.  numpy evaluates arctan2 with its AVX-512
+// (SVML) kernel on the hosts the reference ran on (the golden fixtures' host;
+// numpy._core.__cpu_features__['AVX512_SKX']), which is not correctly rounded
+// and differs from ocml's atan2 by an ulp on ~6 % of near-tie inputs -- the
+// ones where an ulp decides the sector.  Within |t| < 2^-29 of the diagonal
+// and for components of magnitude 2^-996 .. 2^963, its result is, bit for
+// bit (tests/test_gpu_slicer.py; probed on 1.2 M near-tie pairs here):
+//   t  = (|y| - |x|) / (|y| + |x|)
+//   x > 0:  pi4 + (t + pi4_lo)                 x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
+// negated for y < 0, with pi4 / pi split into double hi + lo.  Outside that
+// domain (denormal or huge components, zeros, inf, NaN) ocml's atan2 is used.
+__device__ __forceinline__ bool numpy_atan2_near_diag(double y, double x, double& ang) {
+  const double ay = fabs(y), ax = fabs(x);
+  if (!(ax >= 0x1p-996 && ax <= 0x1p963 && ay >= 0x1p-996 && ay <= 0x1p963)) return false;
+  const double t = (ay - ax) / (ay + ax);
+  if (!(fabs(t) < 0x1p-29)) return false;
+  const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;
+  const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53;
+  const double a = x > 0 ? pi4 + (t + pi4_lo) : pi - (pi4 - (pi_lo - (t + pi4_lo)));
+  ang = y < 0 ? -a : a;
+  return true;
+}
+
 __device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
-  double ang = atan2(di, dr);
+  double ang;
+  if (!numpy_atan2_near_diag(di, dr, ang)) ang = atan2(di, dr);
   if (ang < 0) ang += 2 * M_PI;
   if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
   if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
@@ -1242,7 +1231,8 @@ hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t
 hipError_t launch_psk_lowpass_exact(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_lowpass_exact<5>), dim3((unsigned)groups), dim3(kWave), 0, st, b, p, f);
+  const int64_t slots = groups < kExactSlots ? groups : kExactSlots;
+  hipLaunchKernelGGL((k_lowpass_exact<5>), dim3((unsigned)slots), dim3(kWave), 0, st, b, p, f);
   return hipGetLastError();
 }
 

@@ -1,0 +1,384 @@
+// psk_lane_kernels.hip -- the PSK filtfilt passes with ONE STREAM PER LANE
+// (the throughput layout), for gfx950.
+//
+// Same reference arithmetic as psk_kernels.hip (K1r/K1g band-pass, K2q/K3q
+// low-pass; modem.py:194-204 -> scipy filtfilt/lfilter in DF-II-T order, no
+// contraction), the same buffers downstream (f in s2 for the low-pass and
+// K3x, symbols in s1 for K4a) and the same low-pass zero/denormal detector,
+// so every stream's bytes are identical whichever layout ran.
+//
+// Why a second layout.  The state-per-lane kernels spread one stream over
+// 4-16 lanes to keep ~1000 waves busy at B = 4096, but half of their
+// instructions move states between lanes (DPP, selects), and their lanes do
+// 8-16x the arithmetic one lane needs: measured register-only
+// (tools/step_probe3.hip, one wave per SIMD) a lane-per-stream band-pass
+// step issues 34 FP64 instructions for 64 streams and sustains 921
+// stream-samples/ns against 303 for the 8-lane groups of K1g; the low-pass
+// per component 1452 against 592 (quads).  The FP64 pipe is saturated at one
+// wave per SIMD.  The price is parallelism: B = 4096 is only 64 band-pass
+// waves, so this layout is picked when enough streams are in flight on the
+// device (api.cpp) -- several batches at once, or big batches.
+//
+// Intermediates not written to HBM (checkpoint + recompute):
+//   * band-pass (k_bp_lane): the forward pass keeps the filter state at the
+//     start of every kBpT-sample tile (8 doubles); the backward pass re-runs
+//     each tile forward from its checkpoint into registers and filters it
+//     backward from there -- the forward output s1 (2 x 8 B/sample of HBM
+//     traffic in the round-1 kernels) becomes 4 B/sample of re-read input
+//     plus 4 B/sample of checkpoints.
+//   * low-pass (k_lp_lane): the same over f with kLpT-sample tiles (4
+//     doubles per component) -- the complex forward output s3 (2 x 16
+//     B/sample) becomes a second read of f (8 B/sample, mostly L2: the re and
+//     im waves of the same streams run on one XCD) plus 2 B/sample of
+//     checkpoints.  Symbols are written straight from the backward pass.
+// A re-run tile executes exactly the operations the forward pass executed,
+// from exactly the same state, so it reproduces its outputs bit for bit.
+#include <math.h>
+
+#include "amr_internal.h"
+#include "psk_common.h"
+
+namespace amr {
+
+constexpr int kBpT = 32;     // band-pass checkpoint tile (samples)
+constexpr int kLpT = 40;     // low-pass checkpoint tile: a multiple of sps 5 / 10 / 20 (static symbol slots)
+
+// scipy lfilter's DF-II-T step with all states of one stream in one lane:
+//   y = z0 + b0*x ;  z[j] = (z[j+1] + x*b[j+1]) - y*a[j+1] ;  z[last] = x*b[last] - y*a[last]
+// (z[last] of the row kernels is (-0.0 + x*b) - y*a: -0.0 is the additive
+// identity for every double, NaN included, so the forms agree bit for bit)
+template <int NS>
+__device__ __forceinline__ double df2t_step(double (&z)[NS], const Iir& f, double x) {
+  const double y = z[0] + f.b[0] * x;
+#pragma unroll
+  for (int j = 0; j < NS - 1; ++j) z[j] = (z[j + 1] + x * f.b[j + 1]) - y * f.a[j + 1];
+  z[NS - 1] = x * f.b[NS] - y * f.a[NS];
+  return y;
+}
+
+// checkpoint + edge scratch inside the plan's s1 (band-pass) / s3 (low-pass)
+__host__ __device__ inline int64_t bp_lane_edge_cap(int pad) { return kBpT + pad; }
+__host__ __device__ inline int64_t lp_lane_edge_cap(int pad) { return 2 * (kLpT + pad); }
+int64_t psk_lane_bp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
+  const int64_t g = (n_streams + 63) / 64;
+  return g * ((n / kBpT) * 8 + bp_lane_edge_cap(pad)) * 64;
+}
+int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
+  const int64_t g = (n_streams + 63) / 64;
+  return 2 * g * ((n / kLpT) * 4 + lp_lane_edge_cap(pad)) * 64;
+}
+
+// ---------------------------------------------------------------------------
+// band-pass: lane = stream, wave = 64 streams.  Coefficients are wave-uniform
+// (kernel arguments in SGPRs).  s1 = [G][nt][8][64] checkpoints, then
+// [G][edge][64] tail outputs.
+template <typename T>
+__global__ __launch_bounds__(64) void k_bp_lane(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int TB = kBpT;
+  constexpr int PER = 16 / (int)sizeof(T);      // samples per 16-B load
+  constexpr int NL = TB / PER;                  // 16-B loads per tile
+  static_assert(TB % PER == 0 && TB % 2 == 0, "tile = whole loads and whole pairs");
+  const int lane = threadIdx.x;
+  const int64_t w = blockIdx.x;
+  if (w * 64 >= buf.n_streams) return;          // wave-uniform
+  const int64_t last = buf.n_streams - 1;
+  const int64_t s = w * 64 + lane;
+  const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
+  const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
+  const int64_t n = p.n, n2 = (n + 1) >> 1;
+  const int pad = p.pad1;
+  const int64_t nt = n / TB;
+  const int64_t G = (buf.n_streams + 63) / 64;
+  const int64_t ecap = bp_lane_edge_cap(pad);
+  double* __restrict__ ck = buf.s1 + (size_t)w * nt * 8 * 64 + lane;
+  double* __restrict__ eb = buf.s1 + (size_t)G * nt * 8 * 64 + (size_t)w * ecap * 64 + lane;
+  // f = s2 in f_index layout: this lane's pair m at fo + m*64
+  double* __restrict__ fo = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+
+  auto load_tile = [&](int64_t t, v4u (&r)[NL]) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) r[k] = *reinterpret_cast<const v4u*>(xb + (size_t)t * TB * sizeof(T) + k * 16);
+  };
+  auto tile_x = [&](const v4u (&r)[NL], int k) -> double {
+    T v[PER];
+    __builtin_memcpy(v, &r[k / PER], 16);
+    return In<T>::cvt(v[k % PER]);
+  };
+
+  // ---- forward pass: pads + tiles (checkpoints only) + tail (edge) --------
+  double z[8];
+  const T x0 = x[0], xl = x[n - 1];
+  {
+    const double e0 = In<T>::ext(x0, x[pad]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
+  }
+  for (int jj = 0; jj < pad; ++jj) (void)df2t_step<8>(z, f, In<T>::ext(x0, x[pad - jj]));
+  v4u xr[NL];
+  if (nt > 0) load_tile(0, xr);
+  for (int64_t t = 0; t < nt; ++t) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ck[(t * 8 + j) * 64] = z[j];
+    v4u cur[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) cur[k] = xr[k];
+    load_tile(t + 1 < nt ? t + 1 : t, xr);      // next tile in flight during this one
+#pragma unroll
+    for (int k = 0; k < TB; ++k) (void)df2t_step<8>(z, f, tile_x(cur, k));
+  }
+  const int64_t i_tail = nt * TB;
+  int ne = 0;
+  for (int64_t i = i_tail; i < n; ++i) eb[(ne++) * 64] = df2t_step<8>(z, f, In<T>::cvt(x[i]));
+  double ylast = 0.0;
+  for (int jj = 0; jj < pad; ++jj) {
+    ylast = df2t_step<8>(z, f, In<T>::ext(xl, x[n - 2 - jj]));
+    eb[(ne++) * 64] = ylast;
+  }
+  __threadfence();                              // checkpoints / edge re-read below
+
+  // ---- backward pass ------------------------------------------------------
+  double zb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) zb[j] = f.zi[j] * ylast;
+  for (int e = ne - 1; e >= 0; --e) {
+    const double y = df2t_step<8>(zb, f, eb[e * 64]);
+    const int64_t i = i_tail + e;
+    if (i < n) fo[(i >> 1) * 64 + (i & 1)] = y;
+  }
+  if (nt > 0) {
+    load_tile(nt - 1, xr);
+    double cn[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cn[j] = ck[((nt - 1) * 8 + j) * 64];
+    for (int64_t t = nt - 1; t >= 0; --t) {
+      double zf[8];
+      v4u cur[NL];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zf[j] = cn[j];
+#pragma unroll
+      for (int k = 0; k < NL; ++k) cur[k] = xr[k];
+      const int64_t tp = t > 0 ? t - 1 : 0;     // the next (lower) tile's input and checkpoint in flight
+      load_tile(tp, xr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cn[j] = ck[(tp * 8 + j) * 64];
+      double yt[TB];
+#pragma unroll
+      for (int k = 0; k < TB; ++k) yt[k] = df2t_step<8>(zf, f, tile_x(cur, k));
+      double* const fp = fo + (size_t)(t * (TB / 2)) * 64;
+#pragma unroll
+      for (int k = TB - 1; k >= 1; k -= 2) {
+        const double y1 = df2t_step<8>(zb, f, yt[k]);
+        const double y0 = df2t_step<8>(zb, f, yt[k - 1]);
+        *reinterpret_cast<double2*>(fp + (k >> 1) * 64) = make_double2(y0, y1);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// low-pass: lane = stream, wave = 64 streams x ONE component (so the LO
+// multiplier is wave-uniform: scalar loads); blocks b and b+8 are the re and
+// im waves of the same streams and land on the same XCD (blocks are dealt to
+// the 8 XCDs round-robin), so the second read of f is an L2 hit.
+// Mixer and detector exactly as K2q/K3q (psk_kernels.hip): bb[0] in numpy's
+// full complex-multiply form, every other sample f*lo_c (equal whenever it
+// is not a zero, and a zero is flagged); min over |hi words| of every input
+// and output (forward) and every output (backward), final states finite.
+// s3 = [2G][nt][4][64] checkpoints, then [2G][edge][64]: the head (pre-pad
+// + tile 0) and tail (last partial tile + post-pad) forward outputs.
+// SPS > 0: symbols at tile offsets FM + k*SPS (kLpT % SPS == 0, first % SPS
+// == FM); SPS == 0: any sps (run-time symbol test per sample).
+template <int SPS, int FM>
+__global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int TL = kLpT;
+  constexpr int CH = 8;                         // samples per LO scalar block / f chunk
+  static_assert(TL % CH == 0 && TL % 2 == 0, "tile = whole chunks and pairs");
+  static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
+  const int lane = threadIdx.x;
+  const int64_t bx = blockIdx.x, kx = bx >> 3;
+  const int64_t w = (kx >> 1) * 8 + (bx & 7);
+  const int comp = (int)(kx & 1);
+  if (w * 64 >= buf.n_streams) return;          // wave-uniform
+  const int64_t s = w * 64 + lane;
+  const int64_t n = p.n, n2 = (n + 1) >> 1;
+  const int pad = p.pad2;
+  const int64_t nt = n / TL;
+  const int64_t G = (buf.n_streams + 63) / 64;
+  const int64_t wc = w * 2 + comp;
+  const int64_t ecap = lp_lane_edge_cap(pad);
+  double* __restrict__ ck = buf.s3 + (size_t)wc * nt * 4 * 64 + lane;
+  double* __restrict__ eh = buf.s3 + (size_t)2 * G * nt * 4 * 64 + (size_t)wc * ecap * 64 + lane;
+  double* __restrict__ et = eh + (size_t)(pad + TL) * 64;
+  const double* __restrict__ fl = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+  CDouble* const loc = (CDouble*)(buf.lo2 + (size_t)comp * n);          // multiplier lo_c[i]
+  CDouble* const lo4 = (CDouble*)(buf.lo) + 2 * comp;                  // (mult, addend) at [4i]
+  auto F = [&](int64_t i) { return fl[(i >> 1) * 64 + (i & 1)]; };
+  auto Xm = [&](int64_t i) { return F(i) * loc[i]; };
+
+  // one tile's mixer inputs e[k] = f[t*TL + k] * lo_c[t*TL + k]
+  auto tile_e = [&](int64_t t, double (&e)[TL]) {
+    const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2)) * 64);
+#pragma unroll
+    for (int c = 0; c < TL / CH; ++c) {
+      double2 fv[CH / 2];
+#pragma unroll
+      for (int k = 0; k < CH / 2; ++k) fv[k] = fp[(c * (CH / 2) + k) * 32];
+#pragma unroll
+      for (int k = 0; k < CH / 2; ++k) {
+        e[c * CH + 2 * k] = fv[k].x * loc[t * TL + c * CH + 2 * k];
+        e[c * CH + 2 * k + 1] = fv[k].y * loc[t * TL + c * CH + 2 * k + 1];
+      }
+    }
+  };
+
+  // ---- forward pass ---------------------------------------------------------
+  double z[4];
+  float acc = __builtin_inff();
+  bool bad = false;
+  const double x0 = F(0) * lo4[0] + lo4[1];      // bb[0]: numpy's (f + 0j) * lo, +0 allowed (class-checked)
+  const double xl = Xm(n - 1);
+  bad |= __builtin_amdgcn_class(x0, kClsX);
+  const double e0 = 2.0 * x0 - Xm(pad);
+  bad |= __builtin_amdgcn_class(e0, kClsY);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) z[j] = f.zi[j] * e0;
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * x0 - Xm(pad - jj);
+    const double y = df2t_step<4>(z, f, e);
+    acc = tiny_min3(acc, e, y);
+    eh[jj * 64] = y;
+  }
+  const int64_t nh = n < TL ? n : TL;           // tile 0 (holds bb[0]): edge buffer, not recomputed
+  for (int64_t i = 0; i < nh; ++i) {
+    const double e = i == 0 ? x0 : Xm(i);
+    const double y = df2t_step<4>(z, f, e);
+    acc = tiny_min3(acc, i == 0 ? y : e, y);
+    eh[(pad + i) * 64] = y;
+  }
+  for (int64_t t = 1; t < nt; ++t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ck[(t * 4 + j) * 64] = z[j];
+    double e[TL];
+    tile_e(t, e);
+#pragma unroll
+    for (int k = 0; k < TL; k += 2) {
+      const double y0 = df2t_step<4>(z, f, e[k]);
+      const double y1 = df2t_step<4>(z, f, e[k + 1]);
+      acc = tiny_min3(acc, e[k], e[k + 1]);
+      acc = tiny_min3(acc, y0, y1);
+    }
+  }
+  const int64_t i_tail = nt >= 1 ? nt * TL : nh;
+  int ne = 0;
+  for (int64_t i = i_tail; i < n; ++i) {
+    const double e = Xm(i);
+    const double y = df2t_step<4>(z, f, e);
+    acc = tiny_min3(acc, e, y);
+    et[(ne++) * 64] = y;
+  }
+  double ylast = 0.0;
+  for (int jj = 0; jj < pad; ++jj) {
+    const double e = 2.0 * xl - Xm(n - 2 - jj);
+    ylast = df2t_step<4>(z, f, e);
+    acc = tiny_min3(acc, e, ylast);
+    et[(ne++) * 64] = ylast;
+  }
+  bad |= !(acc >= kTinyHi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(z[j]);
+  __threadfence();                              // checkpoints / edges re-read below
+
+  // ---- backward pass ----------------------------------------------------------
+  const int64_t S = p.n_sym, first = p.first, sps = p.sps;
+  double* __restrict__ symp = buf.s1 + sym_index(s, S, 0, comp);   // symbol k at symp[k*64]
+  auto sym_out = [&](int64_t i, double y) {     // generic: a symbol sample at i?
+    if (i >= first && (i - first) % sps == 0) symp[((i - first) / sps) * 64] = y;
+  };
+  float accb = __builtin_inff();
+  double zb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) zb[j] = f.zi[j] * ylast;
+  for (int e = ne - 1; e >= 0; --e) {
+    const double y = df2t_step<4>(zb, f, et[e * 64]);
+    accb = tiny_min3(accb, y, y);
+    const int64_t i = i_tail + e;
+    if (i < n) sym_out(i, y);
+  }
+  if (nt > 1) {
+    const int64_t q0 = SPS > 0 ? first / SPS : 0;
+    double cn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cn[j] = ck[((nt - 1) * 4 + j) * 64];
+    for (int64_t t = nt - 1; t >= 1; --t) {
+      double zf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zf[j] = cn[j];
+      const int64_t tp = t > 1 ? t - 1 : 1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cn[j] = ck[(tp * 4 + j) * 64];
+      double e[TL];
+      tile_e(t, e);
+      double yt[TL];
+#pragma unroll
+      for (int k = 0; k < TL; ++k) yt[k] = df2t_step<4>(zf, f, e[k]);
+#pragma unroll
+      for (int k = TL - 1; k >= 1; k -= 2) {
+        const double y1 = df2t_step<4>(zb, f, yt[k]);
+        const double y0 = df2t_step<4>(zb, f, yt[k - 1]);
+        accb = tiny_min3(accb, y1, y0);
+        if constexpr (SPS > 0) {
+          if (k % SPS == FM) symp[(t * (TL / SPS) + (k - FM) / SPS - q0) * 64] = y1;
+          if ((k - 1) % SPS == FM) symp[(t * (TL / SPS) + (k - 1 - FM) / SPS - q0) * 64] = y0;
+        } else {
+          sym_out(t * TL + k, y1);
+          sym_out(t * TL + k - 1, y0);
+        }
+      }
+    }
+  }
+  for (int e = pad + (int)nh - 1; e >= 0; --e) {
+    const double y = df2t_step<4>(zb, f, eh[e * 64]);
+    accb = tiny_min3(accb, y, y);
+    const int64_t i = e - pad;
+    if (i >= 0) sym_out(i, y);
+  }
+  bad |= !(accb >= kTinyHi);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(zb[j]);
+  if (bad && s < buf.n_streams) atomicOr(&buf.flags[s], 1);
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (api.cpp)
+hipError_t launch_psk_bandpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  if (f.nt != 9) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((b.n_streams + 63) / 64)), block(64);
+  switch (b.dtype) {
+    case kF32: hipLaunchKernelGGL(k_bp_lane<float>, grid, block, 0, st, b, p, f); break;
+    case kF64: hipLaunchKernelGGL(k_bp_lane<double>, grid, block, 0, st, b, p, f); break;
+    case kI16: hipLaunchKernelGGL(k_bp_lane<int16_t>, grid, block, 0, st, b, p, f); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  if (f.nt != 5) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
+  if (e != hipSuccess) return e;
+  // a multiple of 16 blocks: the re/im XCD pairing is a bijection
+  const dim3 grid((unsigned)((2 * ((b.n_streams + 63) / 64) + 15) / 16 * 16)), block(64);
+  const int fm = (int)(p.first % (p.sps > 0 ? p.sps : 1));
+#define AMR_LP_LANE(S_, F_) hipLaunchKernelGGL((k_lp_lane<S_, F_>), grid, block, 0, st, b, p, f)
+  if (p.sps == 10 && fm == 5) AMR_LP_LANE(10, 5);
+  else if (p.sps == 5 && fm == 2) AMR_LP_LANE(5, 2);
+  else if (p.sps == 20 && fm == 10) AMR_LP_LANE(20, 10);
+  else if (p.sps == 10 && fm == 0) AMR_LP_LANE(10, 0);
+  else if (p.sps == 5 && fm == 0) AMR_LP_LANE(5, 0);
+  else if (p.sps == 20 && fm == 0) AMR_LP_LANE(20, 0);
+  else AMR_LP_LANE(0, 0);
+#undef AMR_LP_LANE
+  return hipGetLastError();
+}
+
+}  // namespace amr

@@ -190,4 +190,41 @@ hipError_t launch_fec_decode(const uint8_t* in, int64_t in_stride, const int64_t
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Benchmark / test input generator (no reference counterpart: the reference's
+// samples come from a sound card).  out[s][i] = base[(s + row_offset) % n_base][i]
+// + sigma * N(0, 1), the normal deviate by Box-Muller from a counter hash of
+// (seed, s, i): every in-flight batch of bench.py gets its own noise draw
+// over the same clean frames, written straight into HBM.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth_tile_noise(const float* __restrict__ base, int64_t n_base, int64_t n,
+                                                          float* __restrict__ out, int64_t n_streams,
+                                                          int64_t row_offset, float sigma, uint64_t seed) {
+  const int64_t s = blockIdx.y;
+  const float* __restrict__ src = base + ((s + row_offset) % n_base) * n;
+  float* __restrict__ dst = out + s * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = splitmix64(seed ^ splitmix64(((uint64_t)s << 32) ^ (uint64_t)i));
+    const float u1 = ((float)(h >> 40) + 1.0f) * 0x1p-24f;          // (0, 1]
+    const float u2 = (float)((h >> 16) & 0xFFFFFF) * 0x1p-24f;       // [0, 1)
+    const float g = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
+    dst[i] = src[i] + sigma * g;
+  }
+}
+
+hipError_t launch_synth_tile_noise(const float* base, int64_t n_base, int64_t n, float* out, int64_t n_streams,
+                                   int64_t row_offset, float sigma, uint64_t seed, hipStream_t st) {
+  if (n_streams <= 0 || n <= 0) return hipSuccess;
+  const unsigned gx = (unsigned)((n + 255) / 256 < 64 ? (n + 255) / 256 : 64);
+  hipLaunchKernelGGL(k_synth_tile_noise, dim3(gx, (unsigned)n_streams), dim3(256), 0, st, base, n_base, n, out,
+                     n_streams, row_offset, sigma, seed);
+  return hipGetLastError();
+}
+
 }  // namespace amr

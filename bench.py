@@ -1,30 +1,49 @@
 #!/usr/bin/env python3
-"""bench.py -- BASELINE.json's headline metric on MI355X.
+"""bench.py -- BASELINE.json's headline metric on MI355X, plus BASELINE's other
+GPU configurations as sub-objects of the same JSON line.
 
 metric : demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz
 workload (N=1): BASELINE configs[1] -- QPSK @ 9600 sym/s, 96 kHz, batch 4096
           synthetic 1-s streams (N = 96000 float32 samples each), inputs
           resident in HBM before the timed region.
-step   : one pass of the whole demod path over the batch:
-          band-pass filtfilt + mixer -> low-pass filtfilt + slicer ->
-          [exact-path fixups] -> sync + pack  (and, for N>1 GPUs, the RCCL
-          all-gather of the decoded bytes).
-scaling: weak -- every rank demodulates its own 4096 streams; value is the
-          whole-job symbols/s = (ranks * 4096 * 9599) / max-over-ranks time.
+step   : one pass of the whole demod path over ONE batch: band-pass filtfilt
+          + mixer -> low-pass filtfilt -> [exact-path fixups] -> slicer + sync
+          + pack (and, for N>1 GPUs, the RCCL all-gather of the decoded bytes).
+          K steps = K distinct batches (each in-flight slot has its own input
+          buffer and noise draw), at most P of them in flight at once on P
+          plans / HIP streams (P = --inflight, default min(16, K // 2): two or
+          more pipeline rounds inside the timed region).
+scaling: weak for qpsk9600 / fsk9600 (every rank its own batch), strong for
+          ofdm8 / psk8fec (a global batch of 8192 sharded over the ranks).
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+Also reported: the one-batch-at-a-time latency, per-kernel HIP-event times
+(in flight and solo), the roofline (contract form + solo + pipeline + FP64),
+the CPU baseline (the C oracle on the host cores), bit-exact parity of
+sampled streams of in-flight slots against the oracle, and for N>1 a check
+that the gathered buffer equals every rank's own output.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--inflight P]
         multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
 
-import argparse
-import ctypes
-import json
 import os
 import sys
-import time
 
-import numpy as np
+# HIP reads GPU_MAX_HW_QUEUES when it initialises (the first HIP call, below).
+# One hardware queue per in-flight batch lets their kernels run side by side
+# (the lane-per-stream kernels need ~16 batches resident to fill the chip).
+_q = sys.argv[sys.argv.index("--hw-queues") + 1] if "--hw-queues" in sys.argv else "32"
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, int(_q)))
+
+import argparse  # noqa: E402
+import ctypes  # noqa: E402
+import gc  # noqa: E402
+import hashlib  # noqa: E402
+import json  # noqa: E402
+import time  # noqa: E402
+
+import numpy as np  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "audio-modem-radio_amd"))
@@ -35,15 +54,30 @@ import synth  # noqa: E402
 
 FS = 96000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_ROUND = "r01"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
+PROFILE_ROUND = "r02"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
+
+# BASELINE.json configs[1..4] (configs[0] is the reference's CPU plumbing case)
+WORKLOADS = {
+    "qpsk9600": dict(baud=9600.0, batch=4096, strong=False, fsk=False, fec=False,
+                     metric="demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU"),
+    "fsk9600": dict(baud=9600.0, batch=16384, strong=False, fsk=True, fec=False,
+                    metric="FSK demod Msymbols/s (batch), FSK9600 96kHz mark/space 12k/24k"),
+    "ofdm8": dict(baud=9600.0, batch=8192, strong=True, fsk=False, fec=False,
+                  metric="OFDM8 (qpsk_demodulate alias) demod Msymbols/s, global batch sharded + RCCL gather"),
+    "psk8fec": dict(baud=19200.0, batch=8192, strong=True, fsk=False, fec=True,
+                    metric="8PSK@19200 demod + fused FEC decode Msymbols/s, global batch sharded + RCCL gather"),
+}
+# the reference's own numpy/scipy code (measured in the build
+# container, 8 cores): not on the GPU box; the north-star basis
+REF_PY = {"qpsk9600": (0.292, 1.66), "ofdm8": (0.292, 1.66), "psk8fec": (0.310, 2.43), "fsk9600": (0.180, 1.15)}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup(n_gpus):
+def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -68,154 +102,124 @@ def max_over_ranks(dist, v: float) -> float:
     return float(t.item())
 
 
-def cpu_baseline(x_sample: np.ndarray, baud: float, threads: int):
-    """The oracle (C restatement of the reference path) on the host cores."""
-    from oracle import oracle
-    oracle.lib()
-    t0 = time.perf_counter()
-    outs, _ = oracle.psk_demod_batch("qpsk", x_sample, baud, n_threads=threads)
-    dt = time.perf_counter() - t0
-    sps = int(FS / baud)
-    S = (x_sample.shape[1] - sps // 2 + sps - 1) // sps
-    return x_sample.shape[0] * (S - 1) / dt / 1e6, dt, outs
+def row_digest(rows: np.ndarray, lens: np.ndarray) -> list:
+    """Per-stream digest of decoded bytes and length (the N>1 gather check)."""
+    return [hashlib.blake2b(rows[i, :max(0, int(lens[i]))].tobytes() + int(lens[i]).to_bytes(8, "little", signed=True),
+                            digest_size=8).hexdigest() for i in range(rows.shape[0])]
 
 
-def cpu_baseline_fsk(x_sample: np.ndarray, baud, mark, space, threads: int):
-    """oracle.fsk_demodulate (C filtfilt + scipy's hilbert + C decide) on the host cores."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    from oracle import oracle
-    oracle.lib()
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        outs = list(ex.map(lambda r: oracle.fsk_demodulate(r, baud, mark, space), x_sample))
-    dt = time.perf_counter() - t0
-    sps = int(FS / baud)
-    nb = (x_sample.shape[1] - sps // 2 + sps - 1) // sps
-    return x_sample.shape[0] * nb / dt / 1e6, dt, outs
+def gather_verdict(gathered_digests, own_digests, shard_sizes):
+    """Slice r of the gathered buffer (as rank 0 holds it) must equal rank r's
+    own output, stream for stream (only the rank's real streams; the slot
+    padding of strong-scaling shards is not compared)."""
+    bad = [r for r, n in enumerate(shard_sizes) if gathered_digests[r][:n] != own_digests[r][:n]]
+    return bad
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    # 20 batches: with 3 in flight the timed region starts and ends with a
-    # part-full pipeline; 5 steps measured 8.4-9.3 ms/step, 24 steps 8.1-8.7
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["qpsk9600", "fsk9600", "ofdm8", "psk8fec"], default="qpsk9600",
-                    help="qpsk9600 = BASELINE configs[1] (the headline metric); fsk9600 = configs[3]; "
-                         "ofdm8 = configs[4] (QPSK alias, global batch 8192 sharded); psk8fec = configs[5] "
-                         "(8PSK@19200 + fused FEC decode, global batch 8192 sharded)")
-    ap.add_argument("--batch", type=int, default=0,
-                    help="streams per GPU (qpsk9600/fsk9600, default 4096/16384) or in total (ofdm8/psk8fec, "
-                         "default 8192)")
-    ap.add_argument("--samples", type=int, default=96000)
-    ap.add_argument("--baud", type=float, default=None, help="default 9600 (19200 for psk8fec)")
-    ap.add_argument("--mark", type=float, default=12000.0, help="fsk9600: mark tone (SURVEY §6 config 3)")
-    ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
-    ap.add_argument("--distinct", type=int, default=64, help="distinct waveforms (noise is per stream)")
-    ap.add_argument("--cpu-streams", type=int, default=0, help="cpu_baseline sample size (0 = auto ~10 s CPU)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
-    ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight on separate HIP streams / plans (0 = 3 for the PSK workloads, 2 for "
-                         "fsk9600): batch k+1's band-pass overlaps batch k's low-pass passes")
-    args = ap.parse_args()
+class Dev:
+    """Device buffers through the C ABI (freed at close)."""
 
-    dist, world, rank, local = dist_setup(args.gpus)
-    dev = local
-    fsk = args.workload == "fsk9600"
-    fec_fused = args.workload == "psk8fec"
-    strong = args.workload in ("ofdm8", "psk8fec")       # a fixed global batch sharded over the ranks
-    if strong:
-        from multi import shard_range
-        B_global = args.batch or 8192
+    def __init__(self, L):
+        self.L, self.ptrs = L, []
+
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _amr.check(self.L.amr_malloc(ctypes.byref(p), int(max(1, nbytes))))
+        self.ptrs.append(p)
+        return p
+
+    def close(self):
+        for p in self.ptrs:
+            self.L.amr_free(p)
+        self.ptrs = []
+
+
+def workload_sizes(name, batch_arg, world, rank):
+    """(B local, B global, first global stream, gather slot) for a rank."""
+    from multi import shard_range
+    W = WORKLOADS[name]
+    if W["strong"]:
+        B_global = batch_arg or W["batch"]
         lo_s, hi_s = shard_range(B_global, rank, world)
-        B = hi_s - lo_s
-        B_slot = -(-B_global // world)                    # all-gather slot (ranks' shards differ by <= 1)
-    else:
-        B = args.batch or (16384 if fsk else 4096)
-        B_global = world * B
-        lo_s = rank * B
-        B_slot = B
-    N = args.samples
-    baud = args.baud or (19200.0 if fec_fused else 9600.0)
+        return hi_s - lo_s, B_global, lo_s, -(-B_global // world)
+    B = batch_arg or W["batch"]
+    return B, world * B, rank * B, B
+
+
+def run_workload(name, args, dist, world, rank, dev, comm, headline):
+    W = WORKLOADS[name]
     L = _amr.lib()
-    _amr.check(L.amr_set_device(dev))
+    fsk, fec_fused, strong = W["fsk"], W["fec"], W["strong"]
+    from multi import shard_range
+    B, B_global, lo_s, B_slot = workload_sizes(name, args.batch, world, rank)
+    N = args.samples
+    baud = W["baud"]
+    mark, space = args.mark, args.space
+    K = args.steps
+    P = args.inflight or (min(2, max(1, K // 2)) if fsk else min(16, max(1, K // 2)))
 
+    # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
     t0 = time.perf_counter()
+    D = min(args.distinct, B)
     if fsk:
-        x = synth.fsk_batch(B, N, baud, args.mark, args.space, seed=1000 + rank, distinct=args.distinct)
+        base = synth.fsk_batch(D, N, baud, mark, space, seed=1000 + rank, noise=0.0)
     elif fec_fused:
-        x = synth.dpsk8_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
+        base = synth.dpsk8_batch(D, N, baud, seed=1000 + rank, noise=0.0)
     else:
-        x = synth.qpsk_batch(B, N, baud, seed=1000 + rank, distinct=args.distinct)
-    log(f"[rank {rank}] synthesised {B}x{N} float32 in {time.perf_counter() - t0:.1f}s")
+        base = synth.qpsk_batch(D, N, baud, seed=1000 + rank, noise=0.0)
+    mem = Dev(L)
+    d_base = mem.alloc(base.nbytes)
+    _amr.check(L.amr_memcpy_h2d(d_base, _amr.ptr(base), base.nbytes))
+    d_x = []
+    for k in range(P):
+        d = mem.alloc(B * N * 4)
+        seed = int.from_bytes(hashlib.blake2b(f"{name}/{rank}/{k}".encode(), digest_size=8).digest(), "little")
+        _amr.check(L.amr_synth_tile_noise(d_base, D, N, d, B, lo_s + 17 * k, ctypes.c_float(0.05), seed))
+        d_x.append(d)
+    log(f"[rank {rank}] {name}: {P} distinct {B}x{N} float32 batches in HBM in {time.perf_counter() - t0:.1f}s")
 
-    inflight = args.inflight or (2 if fsk else 3)         # same-box fsk9600: 1 -> 40.3, 2 -> 39.15 ms
+    # ---- plans: one per in-flight batch (own HIP stream + scratch) ----
     if fsk:
         import _fsk
-        plans = [_fsk.FskPlan(N, baud, args.mark, args.space, FS, max_streams=B, device=dev) for _ in range(inflight)]
-        plan = plans[0]
-        sym_per_stream = (N - plan.sps // 2 + plan.sps - 1) // plan.sps     # decided bits (modem.py:320)
+        plans = [_fsk.FskPlan(N, baud, mark, space, FS, max_streams=B, device=dev) for _ in range(P)]
+        sym_per_stream = (N - plans[0].sps // 2 + plans[0].sps - 1) // plans[0].sps   # decided bits (modem.py:320)
         demod, sync_fn, names = L.amr_fsk_demod_device, L.amr_fsk_plan_synchronize, _amr.TF_NAMES
+        gather_fn = L.amr_fsk_allgather
     else:
-        plans = [_amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev) for _ in range(inflight)]
-        plan = plans[0]
-        S = (N - plan.first + plan.sps - 1) // plan.sps
-        sym_per_stream = S - 1                       # differential symbols decided per stream
+        plans = [_amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev) for _ in range(P)]
+        S = (N - plans[0].first + plans[0].sps - 1) // plans[0].sps
+        sym_per_stream = S - 1                          # differential symbols decided per stream
         demod, sync_fn, names = L.amr_psk_demod_device, L.amr_psk_plan_synchronize, _amr.T_NAMES
+        gather_fn = L.amr_allgather
     for pl in plans:
         pl.enable_timing(True)
         if not fsk:
-            pl.set_inflight(inflight)
-    cap = plan.out_cap
-
-    def dmalloc(nbytes):
-        p = ctypes.c_void_p()
-        _amr.check(L.amr_malloc(ctypes.byref(p), int(nbytes)))
-        return p
-
-    d_x = dmalloc(x.nbytes)
-    _amr.check(L.amr_memcpy_h2d(d_x, _amr.ptr(x), x.nbytes))
-    # per batch in flight: its plan (stream + scratch) and its output / gather buffers
+            pl.set_inflight(P)
+    cap = plans[0].out_cap
     ctx = []
-    for pl in plans:
-        c = {"plan": pl, "out": dmalloc(B_slot * cap), "len": dmalloc(B_slot * 8), "sync": dmalloc(B_slot * 8)}
+    for k, pl in enumerate(plans):
+        c = {"plan": pl, "x": d_x[k], "out": mem.alloc(B_slot * cap), "len": mem.alloc(B_slot * 8),
+             "sync": mem.alloc(B_slot * 8)}
         if fec_fused:
-            c.update(fec=dmalloc(B_slot * cap), flen=dmalloc(B_slot * 8), ok=dmalloc(B_slot * 4))
+            c.update(fec=mem.alloc(B_slot * cap), flen=mem.alloc(B_slot * 8), ok=mem.alloc(B_slot * 4))
+        if comm is not None:
+            c["gather"], c["gather_len"] = mem.alloc(world * B_slot * cap), mem.alloc(world * B_slot * 8)
         ctx.append(c)
-    comm = None
-    if world > 1:
-        uid = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            _amr.check(L.amr_comm_unique_id(uid))
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
-        comm = ctypes.c_void_p()
-        _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
-        for c in ctx:
-            c["gather"], c["gather_len"] = dmalloc(world * B_slot * cap), dmalloc(world * B_slot * 8)
 
     def step(c):
         pl = c["plan"]
         if fec_fused:
-            _amr.check(L.amr_psk_demod_fec_device(pl.handle, d_x, _amr.DTYPE_F32, B, N, c["out"], cap, c["len"],
+            _amr.check(L.amr_psk_demod_fec_device(pl.handle, c["x"], _amr.DTYPE_F32, B, N, c["out"], cap, c["len"],
                                                   c["sync"], c["fec"], cap, c["flen"], c["ok"]))
         else:
-            _amr.check(demod(pl.handle, d_x, _amr.DTYPE_F32, B, N, c["out"], cap, c["len"], c["sync"]))
+            _amr.check(demod(pl.handle, c["x"], _amr.DTYPE_F32, B, N, c["out"], cap, c["len"], c["sync"]))
         if comm is not None:
-            # the bytes every rank hands to the gather (the FEC output for psk8fec),
-            # to every rank (RCCL over xGMI), on the plan's stream (FSK: the comm's)
+            # the bytes every rank hands to the gather (the FEC output for
+            # psk8fec), to every rank (RCCL over xGMI), ordered after this
+            # plan's queued demod and before its next batch
             g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
-            gs = None if fsk else pl.handle
-            if fsk:
-                _amr.check(sync_fn(pl.handle))
-            _amr.check(L.amr_allgather(comm, g_out, c["gather"], B_slot * cap, gs))
-            _amr.check(L.amr_allgather(comm, g_len, c["gather_len"], B_slot * 8, gs))
-            if fsk:
-                _amr.check(L.amr_comm_synchronize(comm))
+            _amr.check(gather_fn(comm, g_out, c["gather"], B_slot * cap, pl.handle))
+            _amr.check(gather_fn(comm, g_len, c["gather_len"], B_slot * 8, pl.handle))
 
     kt = {k: 0.0 for k in names}
     nt = [0]
@@ -226,227 +230,304 @@ def main():
             kt[k] += v
         nt[0] += 1
 
-    # warmup: one batch at a time (also the kernels' solo durations), then with the batches in flight
-    for i in range(args.warmup):
-        step(ctx[i % inflight])
-        if i == 0 and args.warmup > 1:             # the first launch is cold: not counted
-            _amr.check(sync_fn(ctx[0]["plan"].handle))
+    # ---- warmup: one batch at a time (solo kernel times + latency) ----------
+    lat = []
+    for i in range(max(1, args.warmup)):
+        c = ctx[i % P]
+        t1 = time.perf_counter()
+        step(c)
+        _amr.check(sync_fn(c["plan"].handle))
+        if comm is not None:
+            _amr.check(L.amr_comm_synchronize(comm))
+        if i == 0 and args.warmup > 1:                  # the first launch is cold: not counted
             continue
-        collect(ctx[i % inflight])
+        lat.append(time.perf_counter() - t1)
+        collect(c)
     solo = {k: v / max(1, nt[0]) for k, v in kt.items() if v > 0}
-    for i in range(min(args.warmup, inflight)):
-        step(ctx[i])
+    latency_layout = ctx[0]["plan"].last_layout() if not fsk else "fsk"
+    for c in ctx:                                       # every plan / stream once before timing
+        step(c)
     _amr.check(L.amr_device_synchronize())
     kt = {k: 0.0 for k in names}
     nt = [0]
+
+    # ---- timed region: exactly K batches, at most P in flight ----------------
     barrier(dist)
     _amr.check(L.amr_device_synchronize())
     t0 = time.perf_counter()
-    # step k runs on ctx[k % inflight]; before a context is reused its previous
-    # batch is waited for (the other batches keep running) and its kernel
-    # timings are read
-    for k in range(args.steps):
-        c = ctx[k % inflight]
-        if k >= inflight:
-            collect(c)
+    for k in range(K):
+        c = ctx[k % P]
+        if k >= P:
+            collect(c)                                  # that context's previous batch (the others keep running)
         step(c)
-    for k in range(max(0, args.steps - inflight), args.steps):
-        collect(ctx[k % inflight])
+    for k in range(max(0, K - P), K):
+        collect(ctx[k % P])
     _amr.check(L.amr_device_synchronize())
     barrier(dist)
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dist, dt)
-    ms_per_step = dt / args.steps * 1e3
-    total_sym = B_global * sym_per_stream
-    value = total_sym / (dt / args.steps) / 1e6
-
-    # per-kernel averages (HIP events on the plan's stream)
+    layout = ctx[0]["plan"].last_layout() if not fsk else "fsk"
+    ms_per_step = dt / K * 1e3
+    value = B_global * sym_per_stream / (dt / K) / 1e6
     kavg = {k: v / max(1, nt[0]) for k, v in kt.items() if v > 0}
-    dom = max(kavg, key=kavg.get)
-    # Algorithmic bytes per launch: each stage's
-    # compulsory input + output at its minimal width.
-    if fsk:
-        #   bandpass : x float32 (4 B/sample) in, z = f_mark + i f_space (16 B) out
-        #   hilbert  : z (16 B) in, compare byte (1 B) out -- the FFT's own passes
-        #              over its intermediates are not algorithmic bytes
-        #   decide   : compare bytes in the windows (sps//2 of every sps) + output bytes
-        q = plan.sps // 4
-        alg_bytes = {"bandpass": B * N * (4 + 16), "hilbert": B * N * 17,
-                     "decide": B * (sym_per_stream * 2 * q + cap)}
-        # FP64 ops: filtfilt 7 taps = 25 ops/sample/pass/tone; FFT ~ 5 n log2 n per transform
-        fp64_ops = {"bandpass": B * 2 * 2 * (N + 42) * 25, "hilbert": B * 2 * 5 * N * np.log2(N)}
-    else:
-        #   bandpass    : x float32 (4 B/sample) in, filtered f float64 (8 B) out
-        #   lowpass_fwd : f (8 B) in, forward low-pass complex128 (16 B) out
-        #   lowpass_bwd : forward low-pass (16 B) in, symbol samples (16 B/symbol) out
-        #   sync_pack   : symbols (16 B/symbol) in, packed bytes out
-        S_sym = sym_per_stream + 1
-        alg_bytes = {"bandpass": B * N * (4 + 8), "lowpass_fwd": B * N * (8 + 16),
-                     "lowpass_bwd": B * (N * 16 + S_sym * 16), "sync_pack": B * (S_sym * 16 + cap),
-                     "lowpass_exact": 0, "fec": B * 2 * cap}
-        # FP64 operations scipy's arithmetic needs (no FMA): band-pass 30/sample per
-        # pass (9 taps incl. the zero odd taps), low-pass 17/sample per pass per
-        # component, mixer 2/sample
-        fp64_ops = {"bandpass": B * 2 * (N + 54) * 30,
-                    "lowpass_fwd": B * ((N + 30) * 2 * 17 + N * 2),
-                    "lowpass_bwd": B * (N + 30) * 2 * 17}
-    achieved = alg_bytes[dom] / (kavg[dom] / 1e3) / 1e9
-    pipeline_bytes = B * N * 4 + B * sym_per_stream * (1 if fsk else 2) / 8
-    fp64_achieved = fp64_ops.get(dom, 0) / (kavg[dom] / 1e3) / 1e12
-    # the whole step's FP64 work over the step time: with batches in flight the
-    # kernels share the SIMDs, so this (not the per-launch figure) is the
-    # VALU-roofline view of the pipeline
-    fp64_pipeline = sum(fp64_ops.values()) / (ms_per_step / 1e3) / 1e12
-    traffic = None
-    pipeline_traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
-    # the PMC file was recorded at each workload's default size on one GPU
-    pmc_cfg = {"qpsk9600": (4096, 9600), "fsk9600": (16384, 9600), "ofdm8": (8192, 9600), "psk8fec": (8192, 19200)}
-    if ((B, int(baud)) == pmc_cfg[args.workload] and N == 96000 and world == 1 and os.path.exists(pmc_file)):
-        with open(pmc_file) as f:
-            pk = json.load(f).get(args.workload, {}).get("slots", {}).get(dom, {})
-        if "hbm_bytes_per_launch" in pk:
-            traffic = int(pk["hbm_bytes_per_launch"])
-        with open(pmc_file) as f:
-            wk = json.load(f).get(args.workload, {}).get("kernels", {})
-        step_bytes = sum(v.get("hbm_bytes_per_dispatch", 0) for v in wk.values())
-        if step_bytes > 0:
-            # every kernel of one step, intermediates included (PMC, not algorithmic)
-            pipeline_traffic = {"bytes_per_step": int(step_bytes),
-                                "gbs": round(step_bytes / (ms_per_step / 1e3) / 1e9, 1),
-                                "frac_of_peak": round(step_bytes / (ms_per_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                                "source": f"profiles/{PROFILE_ROUND}_pmc.json: FETCH_SIZE x2 + WRITE_SIZE summed "
-                                          "over the step's kernels, over this run's step time"}
 
-    # parity spot-check after timing (not timed): GPU bytes vs the oracle
-    out = np.empty((B, cap), np.uint8)
-    ln = np.empty(B, np.int64)
-    g_out, g_len = (ctx[0]["fec"], ctx[0]["flen"]) if fec_fused else (ctx[0]["out"], ctx[0]["len"])
-    _amr.check(L.amr_memcpy_d2h(_amr.ptr(out), g_out, B * cap))
-    _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
+    # ---- outputs of every slot (after timing) --------------------------------
+    outs = []
+    for c in ctx:
+        o = np.empty((B, cap), np.uint8)
+        ln = np.empty(B, np.int64)
+        g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(o), g_out, B * cap))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
+        outs.append((o, ln))
 
-    # PCIe-inclusive rate (never `value`): the host API on the
-    # same batch from pageable host memory -- H2D of the float32 samples, the
-    # demod, D2H of the bytes -- one batch at a time; the first call is warmup
-    host_path = None
-    if rank == 0 and world == 1 and not fec_fused and not args.no_host_path:
-        host_fn = L.amr_fsk_demod_host if fsk else L.amr_psk_demod_host
-        h_out = np.empty((B, cap), np.uint8)
-        h_len = np.empty(B, np.int64)
-        h_sync = np.empty(B, np.int64)
-        hts = []
-        for _ in range(3):
-            t1 = time.perf_counter()
-            _amr.check(host_fn(plan.handle, _amr.ptr(x), _amr.DTYPE_F32, B, N, _amr.ptr(h_out), cap,
-                               _amr.ptr(h_len), _amr.ptr(h_sync)))
-            hts.append(time.perf_counter() - t1)
-        ht = min(hts[1:])
-        same = bool(np.array_equal(h_len, ln) and all(h_out[i, :ln[i]].tobytes() == out[i, :ln[i]].tobytes()
-                                                      for i in range(B)))
-        host_path = {"ms_per_batch": round(ht * 1e3, 2), "value": round(B * sym_per_stream / ht / 1e6, 3),
-                     "unit": "Msym/s", "input_gb": round(x.nbytes / 1e9, 3),
-                     "what": "amr_%s_demod_host from pageable host float32, one batch at a time (H2D + demod + D2H)"
-                             % ("fsk" if fsk else "psk"),
-                     "bytes_equal_device_path": same}
+    # ---- N>1: the gathered buffer must equal every rank's own output ----------
+    gather_check = None
+    if comm is not None:
+        last = (K - 1) % P
+        o, ln = outs[last]
+        gp = np.empty((world, B_slot, cap), np.uint8)
+        gl = np.empty((world, B_slot), np.int64)
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(gp), ctx[last]["gather"], gp.nbytes))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(gl), ctx[last]["gather_len"], gl.nbytes))
+        own = [None] * world
+        dist.all_gather_object(own, row_digest(o, ln))
+        sizes = [workload_sizes(name, args.batch, world, r)[0] for r in range(world)]
+        bad = gather_verdict([row_digest(gp[r], gl[r]) for r in range(world)], own, sizes)
+        flags = [None] * world
+        dist.all_gather_object(flags, bad)
+        bad_any = sorted({b for f in flags for b in f})
+        gather_check = (f"ok: every rank's gathered [{world}][{B_slot}][{cap}] buffer == each rank's own bytes and "
+                        "lengths" if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
 
+    # ---- parity: sampled streams of in-flight slots vs the oracle; CPU baseline
     result = None
-    if rank == 0:
+    if rank == 0 and args.no_cpu:
+        log(f"[rank 0] {name}: {ms_per_step:.3f} ms/step, {value:.1f} Msym/s, kernels {kavg} (no parity: --no-cpu)")
+    if rank == 0 and not args.no_cpu:
+        from oracle import oracle
         threads = max(1, min(16, os.cpu_count() or 1))
+        xh = np.empty((B, N), np.float32)
+        checked, n_slots, bad_total = 0, 0, []
         cpu = None
-        parity = "skipped"
-        if not args.no_cpu:
-            if fsk:
-                # ~16 ms of single-core work per stream (scipy's hilbert dominates):
-                # 1024 streams ~ 15 s of CPU work spread over the host threads
-                n_cpu = args.cpu_streams or 1024
-                idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
-                val, cdt, couts = cpu_baseline_fsk(x[idx], baud, args.mark, args.space, threads)
-                how = "oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
+        slots = range(P) if args.parity_all_slots else sorted({0, 1 % P, P - 1})
+        for k in slots:
+            if headline and k == 0 and not fsk:
+                idx = np.arange(B)                                  # the whole batch of slot 0
             else:
-                n_cpu = args.cpu_streams or B          # the whole batch: ~10 s of single-core work on the box
-                idx = np.linspace(0, B - 1, num=min(n_cpu, B)).astype(int)
-                val, cdt, couts = cpu_baseline(x[idx], baud, threads)
-                how = "the C restatement oracle/amr_oracle.c, OpenMP over streams"
+                idx = np.linspace(0, B - 1, num=min(B, 256 if k == 0 else 16)).astype(int)
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[k]["x"], xh.nbytes))
+            xs = xh[idx]
+            t1 = time.perf_counter()
+            if fsk:
+                from concurrent.futures import ThreadPoolExecutor
+                with ThreadPoolExecutor(threads) as ex:
+                    want = list(ex.map(lambda r: oracle.fsk_demodulate(r, baud, mark, space), xs))
+            else:
+                want, _ = oracle.psk_demod_batch("qpsk", xs, baud, n_threads=threads)
                 if fec_fused:
-                    from oracle import oracle
-                    t1 = time.perf_counter()
-                    couts = [oracle.fec_decode(c)[0] for c in couts]
-                    cdt += time.perf_counter() - t1
-                    val = len(idx) * sym_per_stream / cdt / 1e6
-                    how += " + oracle.fec_decode"
-            cpu = {"value": round(val, 3), "unit": "Msym/s", "cores": threads, "kind": "port",
-                   "sample": f"{len(idx)} of the {B} benchmark streams ({N} samples each) through {how}, "
-                             f"{cdt:.2f} s wall"}
-            if not fsk and not fec_fused:
-                # the same restatement on one core (1 core and all host cores)
-                idx1 = idx[:64]
-                v1, d1, _ = cpu_baseline(x[idx1], baud, 1)
-                cpu["value_1core"] = round(v1, 3)
-                cpu["sample_1core"] = f"{len(idx1)} streams, 1 thread, {d1:.2f} s wall"
-            bad_idx = [int(i) for j, i in enumerate(idx) if out[i, :ln[i]].tobytes() != couts[j]]
-            bad = len(bad_idx)
-            if bad:
-                log(f"[rank {rank}] streams differing from the oracle: {bad_idx[:32]}{' ...' if bad > 32 else ''}")
-            parity = f"{len(idx) - bad}/{len(idx)} streams bit-exact vs oracle"
+                    want = [oracle.fec_decode(w)[0] for w in want]
+            cdt = time.perf_counter() - t1
+            if k == 0:
+                how = ("oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
+                       if fsk else "the C restatement oracle/amr_oracle.c, OpenMP over streams" +
+                       (" + oracle.fec_decode" if fec_fused else ""))
+                cpu = {"value": round(len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s", "cores": threads,
+                       "kind": "port", "sample": f"{len(idx)} of the {B} streams of benchmark batch 0 ({N} samples "
+                                                 f"each) through {how}, {cdt:.2f} s wall"}
+            o, ln = outs[k]
+            bad_total += [(k, int(i)) for j, i in enumerate(idx) if o[i, :ln[i]].tobytes() != want[j]]
+            checked += len(idx)
+            n_slots += 1
+        if bad_total:
+            log(f"[rank {rank}] {name}: streams differing from the oracle (slot, stream): {bad_total[:16]}")
+        parity = (f"{checked - len(bad_total)}/{checked} streams bit-exact vs oracle (sampled from {n_slots} of the "
+                  f"{P} in-flight batches)" + (" (FEC output)" if fec_fused else ""))
+        if headline and not fsk and cpu is not None:
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[0]["x"], xh.nbytes))
+            t1 = time.perf_counter()
+            oracle.psk_demod_batch("qpsk", xh[:64], baud, n_threads=1)
+            d1 = time.perf_counter() - t1
+            cpu["value_1core"] = round(64 * sym_per_stream / d1 / 1e6, 3)
+            cpu["sample_1core"] = f"64 streams, 1 thread, {d1:.2f} s wall"
+
+        # ---- roofline ----
+        # algorithmic bytes per launch: the path's compulsory input + output,
+        # float32 samples in + the decided bits out (40.25 B/symbol at sps 10)
+        out_bytes = sym_per_stream * (1 if fsk else 2) / 8
+        alg_bytes = B * (N * 4 + out_bytes)
+        dom = max(kavg, key=kavg.get)
+        # FP64 ops the reference arithmetic needs per sample (scipy's DF-II-T,
+        # no FMA): band-pass 33/pass (9 taps), low-pass 17/pass/component,
+        # mixer 1/component (PSK); FSK filtfilt 25/pass/tone + FFT ~5 n log2 n
         if fsk:
-            metric = "FSK demod Msymbols/s (batch), FSK9600 96kHz mark/space 12k/24k"
-            workload = (f"FSK@{int(baud)} 96kHz tones {args.mark:g}/{args.space:g} Hz, batch {B} x {N} float32 "
-                        "streams per GPU (BASELINE configs[3] at SURVEY §6's valid tones)")
-        elif args.workload == "ofdm8":
-            metric = "OFDM8 (qpsk_demodulate alias) demod Msymbols/s, global batch sharded + RCCL gather"
-            workload = (f"OFDM8 = QPSK@{int(baud)} 96kHz (modem.py:375-376), {B_global} x {N} float32 streams "
-                        f"sharded over {world} GPU(s) (BASELINE configs[4])")
-        elif fec_fused:
-            metric = "8PSK@19200 demod + fused FEC decode Msymbols/s, global batch sharded + RCCL gather"
-            workload = (f"8PSK@{int(baud)} = QPSK path (modem.py:348) + ReedSolomonFEC.decode fused, {B_global} x "
-                        f"{N} float32 streams sharded over {world} GPU(s) (BASELINE configs[5])")
+            fp64 = B * (2 * 2 * (N + 42) * 25 + 2 * 2 * 5 * N * np.log2(N))
         else:
-            metric = "demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU"
+            fp64 = B * (2 * (N + 54) * 33 + 2 * (N + 30) * 2 * 17 + 2 * N)
+        traffic, step_traffic = None, None
+        pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
+        if os.path.exists(pmc_file) and world == 1 and N == 96000 and not args.batch:
+            with open(pmc_file) as f:
+                pm = json.load(f).get(name, {})
+            if pm.get("inflight") == P and pm.get("layout", layout) == layout:
+                traffic = pm.get("slots", {}).get(dom, {}).get("hbm_bytes_per_launch")
+                step_traffic = sum(v.get("hbm_bytes_per_dispatch", 0) for v in pm.get("kernels", {}).values()) or None
+        ach = alg_bytes / (kavg[dom] / 1e3) / 1e9
+        roofline = {
+            "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": int(traffic) if traffic else None,
+            "traffic_ratio": round(traffic / alg_bytes, 2) if traffic else None,
+            "alg_bytes_per_launch": int(alg_bytes),
+            "alg_bytes_def": "SURVEY 8(d): per stream N x 4 B float32 samples in + decided bits / 8 out "
+                             f"({(N * 4 + out_bytes) / sym_per_stream:.2f} B/symbol here)",
+            "kernel_ms_used": round(kavg[dom], 4),
+            "kernel_ms_note": "the dominant kernel's average HIP-event duration over the timed region (its batches "
+                              "share the GPU with the other in-flight batches), as rocprofv3 reports it",
+            "solo": {"kernel_ms": round(solo[dom], 4) if dom in solo else None,
+                     "achieved": round(alg_bytes / (solo[dom] / 1e3) / 1e9, 2) if dom in solo else None,
+                     "frac": round(alg_bytes / (solo[dom] / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if dom in solo else None,
+                     "layout": latency_layout},
+            "pipeline": {"ms_per_step": round(ms_per_step, 4), "achieved": round(alg_bytes / ms_per_step / 1e6, 2),
+                         "frac": round(alg_bytes / ms_per_step / 1e6 / HBM_PEAK_GBS, 5),
+                         "hbm_traffic_per_step": int(step_traffic) if step_traffic else None,
+                         "hbm_traffic_gbs": round(step_traffic / ms_per_step / 1e6, 1) if step_traffic else None},
+            "fp64_valu": {"ops_per_step": float(fp64), "achieved_tops": round(fp64 / ms_per_step / 1e9, 3),
+                          "peak_tops": FP64_PEAK_TOPS, "frac": round(fp64 / ms_per_step / 1e9 / FP64_PEAK_TOPS, 4),
+                          "note": "the binding roof of the bit-exact path (SURVEY §0.7): FP64 ops the reference's "
+                                  "arithmetic needs per step over the step time"},
+        }
+        if fsk:
+            workload = (f"FSK@{int(baud)} 96kHz tones {mark:g}/{space:g} Hz, batch {B} x {N} float32 streams per GPU "
+                        "(BASELINE configs[3] at SURVEY §6's valid tones: the reference's defaults raise)")
+        elif name == "ofdm8":
+            workload = (f"OFDM8 = QPSK@{int(baud)} 96kHz (modem.py:375-376), global batch {B_global} x {N} float32 "
+                        f"streams sharded over {world} GPU(s) (BASELINE configs[4])")
+        elif fec_fused:
+            workload = (f"8PSK@{int(baud)} = QPSK path (modem.py:348) + ReedSolomonFEC.decode fused, global batch "
+                        f"{B_global} x {N} float32 streams sharded over {world} GPU(s) (BASELINE configs[5])")
+        else:
             workload = f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU (BASELINE configs[1])"
         result = {
-            "metric": metric,
-            "value": round(value, 3), "unit": "Msym/s", "n_gpus": world, "steps": args.steps,
+            "metric": W["metric"], "value": round(value, 3), "unit": "Msym/s", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload, "global_batch": B_global, "samples_per_stream": N,
                        "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)",
-                       "batches_in_flight": inflight},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": f"profiles/{PROFILE_ROUND}_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                                           "bytes/launch)",
-                         "alg_bytes_per_launch": int(alg_bytes[dom]),
-                         "fp64_valu": {"achieved_tops": round(fp64_achieved, 3), "peak_tops": FP64_PEAK_TOPS,
-                                       "frac": round(fp64_achieved / FP64_PEAK_TOPS, 4)}},
-            "pipeline_hbm_gbs": round(pipeline_bytes / (ms_per_step / 1e3) / 1e9, 2),
-            "pipeline_hbm_traffic": pipeline_traffic,
-            "pipeline_fp64": {"achieved_tops": round(fp64_pipeline, 3), "peak_tops": FP64_PEAK_TOPS,
-                              "frac": round(fp64_pipeline / FP64_PEAK_TOPS, 4)},
+                       "batches_in_flight": P, "kernel_layout": layout,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "inputs": f"{P} distinct device batches per rank: {D} clean frames + per-slot N(0, 0.05^2) "
+                                 "noise (amr_synth_tile_noise)"},
+            "latency_ms_one_batch": round(float(np.median(lat)) * 1e3, 3) if lat else None,
+            "latency_layout": latency_layout,
+            "roofline": roofline,
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "kernel_ms_solo": {k: round(v, 4) for k, v in solo.items()},
             "cpu_baseline": cpu,
             "parity": parity,
-            "host_path_pcie_inclusive": host_path,
+            "vs_reference_python": {
+                "reference_1core_msym_s": REF_PY[name][0], "reference_8proc_msym_s": REF_PY[name][1],
+                "ratio_1core": round(value / REF_PY[name][0], 1), "ratio_8proc": round(value / REF_PY[name][1], 1),
+                "source": "BASELINE.md §2: the reference's modem.py on numpy 2.2.6 / scipy 1.15.3, measured in the "
+                          "build container (8 cores), not on the GPU box"},
         }
-        # the reference's own numpy/scipy code is not on the GPU box; its rate as
-        # measured in the build container is the north-star basis
-        ref_py = {"qpsk9600": (0.292, 1.66), "ofdm8": (0.292, 1.66), "psk8fec": (0.310, 2.43),
-                  "fsk9600": (0.180, 1.15)}[args.workload]
-        result["vs_reference_python"] = {
-            "reference_1core_msym_s": ref_py[0], "reference_8proc_msym_s": ref_py[1],
-            "ratio_1core": round(value / ref_py[0], 1), "ratio_8proc": round(value / ref_py[1], 1),
-            "source": "BASELINE.md §2: the reference's modem.py on numpy 2.2.6 / scipy 1.15.3, measured in the "
-                      "build container (8 cores), not on the GPU box"}
+        if gather_check is not None:
+            result["gather_check"] = gather_check
         if not fsk:
             result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
-        if fec_fused:
-            result["parity"] += " (FEC output)"
-        print(json.dumps(result), flush=True)
-    L.amr_free(d_x)
+
+        # PCIe-inclusive rate (never `value`): the host API on the
+        # same batch from host memory, H2D + demod + D2H, one batch at a time
+        if headline and world == 1 and not fec_fused and not args.no_host_path:
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[0]["x"], xh.nbytes))
+            o0, ln0 = outs[0]
+            result["host_path_pcie_inclusive"] = host_path(L, fsk, plans[0], xh, B, N, cap, sym_per_stream, o0, ln0)
+    elif gather_check is not None and "MISMATCH" in gather_check:
+        log(f"[rank {rank}] {name}: {gather_check}")
     for c in ctx:
-        for key in ("out", "len", "sync", "fec", "flen", "ok", "gather", "gather_len"):
-            if key in c:
-                L.amr_free(c[key])
+        c.clear()
+    del plans, ctx
+    gc.collect()
+    mem.close()
+    return result
+
+
+def host_path(L, fsk, plan, xh, B, N, cap, sym_per_stream, out_dev, len_dev):
+    host_fn = L.amr_fsk_demod_host if fsk else L.amr_psk_demod_host
+    h_out = np.empty((B, cap), np.uint8)
+    h_len = np.empty(B, np.int64)
+    h_sync = np.empty(B, np.int64)
+    hts = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        _amr.check(host_fn(plan.handle, _amr.ptr(xh), _amr.DTYPE_F32, B, N, _amr.ptr(h_out), cap, _amr.ptr(h_len),
+                           _amr.ptr(h_sync)))
+        hts.append(time.perf_counter() - t1)
+    ht = min(hts[1:])
+    same = bool(np.array_equal(h_len, len_dev) and all(h_out[i, :h_len[i]].tobytes() == out_dev[i, :h_len[i]].tobytes()
+                                                       for i in range(B)))
+    return {"ms_per_batch": round(ht * 1e3, 2), "value": round(B * sym_per_stream / ht / 1e6, 3), "unit": "Msym/s",
+            "input_gb": round(xh.nbytes / 1e9, 3),
+            "what": "amr_%s_demod_host from pageable host float32, one batch at a time (H2D + demod + D2H)"
+                    % ("fsk" if fsk else "psk"),
+            "bytes_equal_device_path": same}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=list(WORKLOADS), default="qpsk9600",
+                    help="the headline; qpsk9600 (BASELINE configs[1]) also reports the other configs as sub-objects")
+    ap.add_argument("--no-sub", action="store_true", help="skip the sub-workloads of the default run")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="streams per GPU (qpsk9600/fsk9600, default 4096/16384) or in total (ofdm8/psk8fec, 8192)")
+    ap.add_argument("--samples", type=int, default=96000)
+    ap.add_argument("--mark", type=float, default=12000.0, help="fsk9600: mark tone (SURVEY §6 config 3)")
+    ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
+    ap.add_argument("--distinct", type=int, default=64, help="clean frames per rank (noise is per stream and slot)")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
+    ap.add_argument("--parity-all-slots", action="store_true", help="check sampled streams of every in-flight slot")
+    ap.add_argument("--hw-queues", type=int, default=32, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight on separate plans / HIP streams (0 = min(16, steps // 2); fsk9600 2)")
+    args = ap.parse_args()
+
+    dist, world, rank, local = dist_setup()
+    dev = local
+    L = _amr.lib()
+    _amr.check(L.amr_set_device(dev))
+    comm = None
+    if world > 1:
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            _amr.check(L.amr_comm_unique_id(uid))
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        comm = ctypes.c_void_p()
+        _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
+
+    result = run_workload(args.workload, args, dist, world, rank, dev, comm, headline=True)
+    if args.workload == "qpsk9600" and not args.no_sub and not args.batch:
+        subs = {}
+        for name in ("fsk9600", "ofdm8", "psk8fec"):
+            r = run_workload(name, args, dist, world, rank, dev, comm, headline=False)
+            if rank == 0 and r is not None:
+                subs[name] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "parity",
+                                                "latency_ms_one_batch", "kernel_ms", "kernel_ms_solo", "cpu_baseline",
+                                                "config")}
+                subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "solo", "pipeline",
+                                                                          "fp64_valu")}
+                for k in ("gather_check", "exact_path_streams"):
+                    if k in r:
+                        subs[name][k] = r[k]
+        if rank == 0 and result is not None:
+            result["workloads"] = subs
+    if rank == 0 and result is not None:
+        result["build_id"] = L.amr_build_id().decode()
+        print(json.dumps(result), flush=True)
     if comm is not None:
         L.amr_comm_destroy(comm)
     if dist is not None:

@@ -121,7 +121,8 @@ int amr_psk_plan_create(amr_psk_plan **plan, int device, int kind, int64_t n_sam
 int amr_psk_plan_destroy(amr_psk_plan *plan);
 /* bytes a stream's output can need: floor(bits/8) */
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan *plan);
-/* device bytes the plan holds in HBM (scratch + host-API staging allocated so far) */
+/* device bytes the plan holds in HBM: scratch + the host-API staging
+ * (allocated on the first amr_psk_demod_host call) */
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
 int amr_psk_plan_synchronize(amr_psk_plan *plan);
 /* record per-kernel HIP events on the plan's stream (1) or not (0) */
@@ -134,6 +135,12 @@ int amr_psk_plan_enable_timing(amr_psk_plan *plan, int on);
 int amr_psk_plan_set_inflight(amr_psk_plan *plan, int batches);
 /* milliseconds of each AMR_T_* kernel in the last call (-1 = not run) */
 int amr_psk_plan_timings(amr_psk_plan *plan, float *ms, int count);
+/* kernel layout of the last call: AMR_LAYOUT_ROW = states spread over lanes
+ * (psk_kernels.hip), AMR_LAYOUT_LANE = one stream per lane
+ * (psk_lane_kernels.hip); picked by streams in flight */
+#define AMR_LAYOUT_ROW 0
+#define AMR_LAYOUT_LANE 1
+int amr_psk_plan_last_layout(const amr_psk_plan *plan);
 /* number of streams the exact complex low-pass path re-ran in the last call */
 int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
 
@@ -278,6 +285,13 @@ int amr_modulate_device(amr_psk_plan *plan, int mode, double baud, double f0, do
                         float *d_out, int64_t out_stride, int64_t n_out, int16_t *d_pcm, int64_t pcm_stride,
                         void *d_work, int64_t work_bytes);
 
+/* ---- benchmark / test input generator (no reference counterpart) ----------
+ * d_out[s][i] = d_base[(s + row_offset) % n_base][i] + sigma * N(0,1), float32,
+ * the deviate hashed from (seed, s, i): distinct noisy batches over the same
+ * clean frames, generated in HBM (bench.py's in-flight batches).  Synchronous. */
+int amr_synth_tile_noise(const float *d_base, int64_t n_base, int64_t n_samples, float *d_out, int64_t n_streams,
+                         int64_t row_offset, float sigma, uint64_t seed);
+
 /* ---- multi-GPU: RCCL over xGMI ----------------------------------------------- */
 #define AMR_UNIQUE_ID_BYTES 128
 int amr_comm_unique_id(uint8_t *id /* AMR_UNIQUE_ID_BYTES */);
@@ -288,6 +302,9 @@ int amr_comm_destroy(amr_comm *comm);
  * after the plan's queued work and before the plan's later work. */
 int amr_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
                   amr_psk_plan *plan);
+/* the same, ordered after / before the FSK plan's queued work */
+int amr_fsk_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
+                      amr_fsk_plan *plan);
 int amr_comm_synchronize(amr_comm *comm);
 
 #ifdef __cplusplus
