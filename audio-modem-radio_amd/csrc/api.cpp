@@ -446,8 +446,12 @@ int amr_psk_plan_destroy(amr_psk_plan* plan) {
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) {
   if (!plan) return -1;
-  // scratch + the host-API staging (allocated on the first amr_psk_demod_host)
-  return plan->scratch_bytes + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
+  // the most the plan can hold: scratch with s1 / s3 at the row layout's size
+  // (they grow on its first call) + the host-API staging (allocated on the
+  // first amr_psk_demod_host)
+  const int64_t grow = std::max<int64_t>(0, kFrontSlack * 8 + row_s1_bytes(plan) - plan->s1_bytes) +
+                       std::max<int64_t>(0, kFrontSlack * 8 + row_s3_bytes(plan) - plan->s3_bytes);
+  return plan->scratch_bytes + grow + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
 }
 
 int amr_psk_plan_synchronize(amr_psk_plan* plan) {

@@ -1088,15 +1088,16 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 // numpy._core.__cpu_features__['AVX512_SKX']), which is not correctly rounded
 // and differs from ocml's atan2 by an ulp on ~6 % of near-tie inputs -- the
 // ones where an ulp decides the sector.  Within |t| < 2^-29 of the diagonal
-// and for components of magnitude 2^-996 .. 2^963, its result is, bit for
-// bit (tests/test_gpu_slicer.py; probed on 1.2 M near-tie pairs here):
+// and for components of magnitude 2^-1015 .. 2^985 (~1e-306 .. 1e297), its
+// result is, bit for bit (tests/test_gpu_slicer.py; probed on 1.5 M near-tie
+// pairs in the build container, 1 in ~10^5 off by an ulp in the pi-side form):
 //   t  = (|y| - |x|) / (|y| + |x|)
 //   x > 0:  pi4 + (t + pi4_lo)                 x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
 // negated for y < 0, with pi4 / pi split into double hi + lo.  Outside that
 // domain (denormal or huge components, zeros, inf, NaN) ocml's atan2 is used.
 __device__ __forceinline__ bool numpy_atan2_near_diag(double y, double x, double& ang) {
   const double ay = fabs(y), ax = fabs(x);
-  if (!(ax >= 0x1p-996 && ax <= 0x1p963 && ay >= 0x1p-996 && ay <= 0x1p963)) return false;
+  if (!(ax >= 0x1p-1015 && ax <= 0x1p985 && ay >= 0x1p-1015 && ay <= 0x1p985)) return false;
   const double t = (ay - ax) / (ay + ax);
   if (!(fabs(t) < 0x1p-29)) return false;
   const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;

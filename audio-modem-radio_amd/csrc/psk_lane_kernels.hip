@@ -34,6 +34,7 @@
 // A re-run tile executes exactly the operations the forward pass executed,
 // from exactly the same state, so it reproduces its outputs bit for bit.
 #include <math.h>
+#include <stdlib.h>
 
 #include "amr_internal.h"
 #include "psk_common.h"
@@ -42,6 +43,7 @@ namespace amr {
 
 constexpr int kBpT = 32;     // band-pass checkpoint tile (samples)
 constexpr int kLpT = 40;     // low-pass checkpoint tile: a multiple of sps 5 / 10 / 20 (static symbol slots)
+constexpr int kLpT2 = 20;    // the same for the role-split low-pass (LDS: 2 components x 2 buffers x tile)
 
 // scipy lfilter's DF-II-T step with all states of one stream in one lane:
 //   y = z0 + b0*x ;  z[j] = (z[j+1] + x*b[j+1]) - y*a[j+1] ;  z[last] = x*b[last] - y*a[last]
@@ -65,21 +67,21 @@ int64_t psk_lane_bp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
 }
 int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
   const int64_t g = (n_streams + 63) / 64;
-  return 2 * g * ((n / kLpT) * 4 + lp_lane_edge_cap(pad)) * 64;
+  return 2 * g * ((n / kLpT2) * 4 + 2 * (kLpT + pad)) * 64;   // the smaller tile's checkpoints, the larger edges
 }
 
 // ---------------------------------------------------------------------------
 // band-pass: lane = stream, wave = 64 streams.  Coefficients are wave-uniform
 // (kernel arguments in SGPRs).  s1 = [G][nt][8][64] checkpoints, then
 // [G][edge][64] tail outputs.
-template <typename T>
-__global__ __launch_bounds__(64) void k_bp_lane(PskBuffers buf, PskParams p, Iir f) {
+template <typename T, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);      // samples per 16-B load
   constexpr int NL = TB / PER;                  // 16-B loads per tile
   static_assert(TB % PER == 0 && TB % 2 == 0, "tile = whole loads and whole pairs");
-  const int lane = threadIdx.x;
-  const int64_t w = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w * 64 >= buf.n_streams) return;          // wave-uniform
   const int64_t last = buf.n_streams - 1;
   const int64_t s = w * 64 + lane;
@@ -176,10 +178,150 @@ __global__ __launch_bounds__(64) void k_bp_lane(PskBuffers buf, PskParams p, Iir
 }
 
 // ---------------------------------------------------------------------------
+// band-pass, role-split: two waves per group of 64 streams (GPB groups per
+// workgroup).  Wave 0 runs the forward pass (checkpoints + tail edge) while
+// wave 1 waits; then, tile by tile from the end, wave 0 re-runs tile t-1
+// forward from its checkpoint into one LDS buffer while wave 1 filters tile t
+// backward out of the other buffer and stores f -- the backward pass and the
+// re-run overlap, so the kernel takes two passes of latency instead of three
+// and a batch has twice the waves.  One workgroup barrier per tile.
+template <typename T, int GPB>
+__global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int TB = kBpT;
+  constexpr int PER = 16 / (int)sizeof(T);
+  constexpr int NL = TB / PER;
+  static_assert(TB % PER == 0 && TB % 2 == 0, "tile = whole loads and whole pairs");
+  __shared__ __attribute__((aligned(16))) double2 yb[GPB][2][TB / 2][64];   // forward outputs of a tile, by pairs
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int gi = wv >> 1, role = wv & 1;
+  const int64_t w = (int64_t)blockIdx.x * GPB + gi;
+  const bool active = w * 64 < buf.n_streams;   // inactive groups still meet every barrier
+  const int64_t last = buf.n_streams - 1;
+  const int64_t s = w * 64 + lane;
+  const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
+  const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
+  const int64_t n = p.n, n2 = (n + 1) >> 1;
+  const int pad = p.pad1;
+  const int64_t nt = n / TB;
+  const int64_t G = (buf.n_streams + 63) / 64;
+  const int64_t ecap = bp_lane_edge_cap(pad);
+  const int64_t i_tail = nt * TB;
+  const int ne = (int)(n - i_tail) + pad;
+  double* __restrict__ ck = buf.s1 + (size_t)w * nt * 8 * 64 + lane;
+  double* __restrict__ eb = buf.s1 + (size_t)G * nt * 8 * 64 + (size_t)w * ecap * 64 + lane;
+  double* __restrict__ fo = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+
+  auto load_tile = [&](int64_t t, v4u (&r)[NL]) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) r[k] = *reinterpret_cast<const v4u*>(xb + (size_t)t * TB * sizeof(T) + k * 16);
+  };
+  auto tile_x = [&](const v4u (&r)[NL], int k) -> double {
+    T v[PER];
+    __builtin_memcpy(v, &r[k / PER], 16);
+    return In<T>::cvt(v[k % PER]);
+  };
+
+  if (role == 0 && active) {
+    // ---- forward pass: pads + tiles (checkpoints only) + tail (edge) ------
+    double z[8];
+    const T x0 = x[0], xl = x[n - 1];
+    {
+      const double e0 = In<T>::ext(x0, x[pad]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
+    }
+    for (int jj = 0; jj < pad; ++jj) (void)df2t_step<8>(z, f, In<T>::ext(x0, x[pad - jj]));
+    v4u xr[NL];
+    if (nt > 0) load_tile(0, xr);
+    for (int64_t t = 0; t < nt; ++t) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ck[(t * 8 + j) * 64] = z[j];
+      v4u cur[NL];
+#pragma unroll
+      for (int k = 0; k < NL; ++k) cur[k] = xr[k];
+      load_tile(t + 1 < nt ? t + 1 : t, xr);
+#pragma unroll
+      for (int k = 0; k < TB; ++k) (void)df2t_step<8>(z, f, tile_x(cur, k));
+    }
+    int e = 0;
+    for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = df2t_step<8>(z, f, In<T>::cvt(x[i]));
+    for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = df2t_step<8>(z, f, In<T>::ext(xl, x[n - 2 - jj]));
+    __threadfence();                            // checkpoints + edge: read by this wave and the backward wave
+  }
+  __syncthreads();
+
+  if (role == 0) {
+    // ---- re-run tiles nt-1, nt-2, ... 0 forward into LDS --------------------
+    v4u xr[NL];
+    double cn[8];
+    if (active && nt > 0) {
+      load_tile(nt - 1, xr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cn[j] = ck[((nt - 1) * 8 + j) * 64];
+    }
+    for (int64_t it = 0; it <= nt; ++it) {
+      const int64_t t = nt - 1 - it;
+      if (active && t >= 0) {
+        double zf[8];
+        v4u cur[NL];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zf[j] = cn[j];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) cur[k] = xr[k];
+        const int64_t tp = t > 0 ? t - 1 : 0;
+        load_tile(tp, xr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cn[j] = ck[(tp * 8 + j) * 64];
+        double2 (*ybuf)[64] = yb[gi][it & 1];
+#pragma unroll
+        for (int k = 0; k < TB; k += 2) {
+          const double y0 = df2t_step<8>(zf, f, tile_x(cur, k));
+          const double y1 = df2t_step<8>(zf, f, tile_x(cur, k + 1));
+          ybuf[k >> 1][lane] = make_double2(y0, y1);
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---- backward pass: the tail edge, then the tiles out of LDS -------------
+    double zb[8];
+    if (active) {
+      const double ylast = eb[(ne - 1) * 64];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zb[j] = f.zi[j] * ylast;
+      for (int e = ne - 1; e >= 0; --e) {
+        const double y = df2t_step<8>(zb, f, eb[e * 64]);
+        const int64_t i = i_tail + e;
+        if (i < n) fo[(i >> 1) * 64 + (i & 1)] = y;
+      }
+    }
+    __syncthreads();                            // tile nt-1 is in buffer 0
+    for (int64_t it = 1; it <= nt; ++it) {
+      const int64_t t = nt - it;
+      if (active) {
+        const double2 (*ybuf)[64] = yb[gi][(it - 1) & 1];
+        double* const fp = fo + (size_t)(t * (TB / 2)) * 64;
+#pragma unroll
+        for (int k = TB / 2 - 1; k >= 0; --k) {
+          const double2 yy = ybuf[k][lane];
+          const double y1 = df2t_step<8>(zb, f, yy.y);
+          const double y0 = df2t_step<8>(zb, f, yy.x);
+          *reinterpret_cast<double2*>(fp + k * 64) = make_double2(y0, y1);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // low-pass: lane = stream, wave = 64 streams x ONE component (so the LO
-// multiplier is wave-uniform: scalar loads); blocks b and b+8 are the re and
-// im waves of the same streams and land on the same XCD (blocks are dealt to
-// the 8 XCDs round-robin), so the second read of f is an L2 hit.
+// multiplier is wave-uniform).  WPB == 1: blocks b and b+8 are the re and im
+// waves of the same streams and land on the same XCD (blocks are dealt to the
+// 8 XCDs round-robin); WPB >= 2: waves (2i, 2i+1) of a block are the re and
+// im waves of one stream group, on one CU -- either way the second read of f
+// is a cache hit (PMC: f is read from HBM once per pass).
 // Mixer and detector exactly as K2q/K3q (psk_kernels.hip): bb[0] in numpy's
 // full complex-multiply form, every other sample f*lo_c (equal whenever it
 // is not a zero, and a zero is flagged); min over |hi words| of every input
@@ -188,16 +330,31 @@ __global__ __launch_bounds__(64) void k_bp_lane(PskBuffers buf, PskParams p, Iir
 // + tile 0) and tail (last partial tile + post-pad) forward outputs.
 // SPS > 0: symbols at tile offsets FM + k*SPS (kLpT % SPS == 0, first % SPS
 // == FM); SPS == 0: any sps (run-time symbol test per sample).
-template <int SPS, int FM>
-__global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
+// Memory: f streams through a ring of NCH chunk slots (the next tile's chunk
+// c is loaded as soon as this tile's chunk c is consumed: a tile of compute
+// to arrive); the tile's LO multipliers arrive by one 8-B load per lane a tile
+// ahead and are parked in a per-wave LDS double buffer, read back by
+// broadcast ds_read_b128.
+template <int SPS, int FM, int WPB>
+__global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TL = kLpT;
-  constexpr int CH = 8;                         // samples per LO scalar block / f chunk
-  static_assert(TL % CH == 0 && TL % 2 == 0, "tile = whole chunks and pairs");
+  constexpr int CH = 8;                         // samples per f chunk (4 x 16 B per lane)
+  constexpr int NCH = TL / CH, HC = CH / 2;
+  static_assert(TL % CH == 0 && TL <= 64, "tile = whole chunks; one LO value per lane");
   static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
-  const int lane = threadIdx.x;
-  const int64_t bx = blockIdx.x, kx = bx >> 3;
-  const int64_t w = (kx >> 1) * 8 + (bx & 7);
-  const int comp = (int)(kx & 1);
+  __shared__ __attribute__((aligned(16))) double lo_lds[WPB][2][TL];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int64_t w;
+  int comp;
+  if constexpr (WPB == 1) {
+    const int64_t bx = blockIdx.x, kx = bx >> 3;
+    w = (kx >> 1) * 8 + (bx & 7);
+    comp = (int)(kx & 1);
+  } else {
+    w = (int64_t)blockIdx.x * (WPB / 2) + (wv >> 1);
+    comp = wv & 1;
+  }
   if (w * 64 >= buf.n_streams) return;          // wave-uniform
   const int64_t s = w * 64 + lane;
   const int64_t n = p.n, n2 = (n + 1) >> 1;
@@ -210,24 +367,29 @@ __global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir
   double* __restrict__ eh = buf.s3 + (size_t)2 * G * nt * 4 * 64 + (size_t)wc * ecap * 64 + lane;
   double* __restrict__ et = eh + (size_t)(pad + TL) * 64;
   const double* __restrict__ fl = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
-  CDouble* const loc = (CDouble*)(buf.lo2 + (size_t)comp * n);          // multiplier lo_c[i]
-  CDouble* const lo4 = (CDouble*)(buf.lo) + 2 * comp;                  // (mult, addend) at [4i]
+  const double* __restrict__ lov = buf.lo2 + (size_t)comp * n;                   // lo_c[i], vector loads
+  CDouble* const loc = (CDouble*)(buf.lo2 + (size_t)comp * n);                   // the same, scalar loads
+  CDouble* const lo4 = (CDouble*)(buf.lo) + 2 * comp;                            // (mult, addend) at [4i]
   auto F = [&](int64_t i) { return fl[(i >> 1) * 64 + (i & 1)]; };
   auto Xm = [&](int64_t i) { return F(i) * loc[i]; };
-
-  // one tile's mixer inputs e[k] = f[t*TL + k] * lo_c[t*TL + k]
-  auto tile_e = [&](int64_t t, double (&e)[TL]) {
-    const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2)) * 64);
+  // f pairs of tile t, chunk c: this lane's 16 B at fl + (t*TL/2 + c*HC + k) * 64
+  auto load_chunk = [&](int64_t t, int c, double2 (&r)[HC]) {
+    const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2) + c * HC) * 64);
 #pragma unroll
-    for (int c = 0; c < TL / CH; ++c) {
-      double2 fv[CH / 2];
+    for (int k = 0; k < HC; ++k) r[k] = fp[k * 32];
+  };
+  auto load_lo = [&](int64_t t) -> double { return lov[t * TL + (lane < TL ? lane : 0)]; };
+  auto put_lo = [&](int64_t t, double v) {
+    if (lane < TL) lo_lds[wv][t & 1][lane] = v;
+  };
+  // mixer inputs of chunk c from the chunk's f pairs and the tile's LDS multipliers
+  auto chunk_e = [&](int64_t t, int c, const double2 (&fv)[HC], double (&e)[CH]) {
+    const double2* lp = reinterpret_cast<const double2*>(&lo_lds[wv][t & 1][c * CH]);
 #pragma unroll
-      for (int k = 0; k < CH / 2; ++k) fv[k] = fp[(c * (CH / 2) + k) * 32];
-#pragma unroll
-      for (int k = 0; k < CH / 2; ++k) {
-        e[c * CH + 2 * k] = fv[k].x * loc[t * TL + c * CH + 2 * k];
-        e[c * CH + 2 * k + 1] = fv[k].y * loc[t * TL + c * CH + 2 * k + 1];
-      }
+    for (int k = 0; k < HC; ++k) {
+      const double2 l = lp[k];
+      e[2 * k] = fv[k].x * l.x;
+      e[2 * k + 1] = fv[k].y * l.y;
     }
   };
 
@@ -255,18 +417,34 @@ __global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir
     acc = tiny_min3(acc, i == 0 ? y : e, y);
     eh[(pad + i) * 64] = y;
   }
+  double2 ring[NCH][HC];
+  if (nt > 1) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) load_chunk(1, c, ring[c]);
+    put_lo(1, load_lo(1));
+  }
   for (int64_t t = 1; t < nt; ++t) {
+    const int64_t tn = t + 1 < nt ? t + 1 : t;
+    const double lon = load_lo(tn);
 #pragma unroll
     for (int j = 0; j < 4; ++j) ck[(t * 4 + j) * 64] = z[j];
-    double e[TL];
-    tile_e(t, e);
 #pragma unroll
-    for (int k = 0; k < TL; k += 2) {
-      const double y0 = df2t_step<4>(z, f, e[k]);
-      const double y1 = df2t_step<4>(z, f, e[k + 1]);
-      acc = tiny_min3(acc, e[k], e[k + 1]);
-      acc = tiny_min3(acc, y0, y1);
+    for (int c = 0; c < NCH; ++c) {
+      double2 fv[HC];
+#pragma unroll
+      for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
+      load_chunk(tn, c, ring[c]);
+      double e[CH];
+      chunk_e(t, c, fv, e);
+#pragma unroll
+      for (int k = 0; k < CH; k += 2) {
+        const double y0 = df2t_step<4>(z, f, e[k]);
+        const double y1 = df2t_step<4>(z, f, e[k + 1]);
+        acc = tiny_min3(acc, e[k], e[k + 1]);
+        acc = tiny_min3(acc, y0, y1);
+      }
     }
+    put_lo(tn, lon);
   }
   const int64_t i_tail = nt >= 1 ? nt * TL : nh;
   int ne = 0;
@@ -309,18 +487,29 @@ __global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir
     double cn[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) cn[j] = ck[((nt - 1) * 4 + j) * 64];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) load_chunk(nt - 1, c, ring[c]);
+    put_lo(nt - 1, load_lo(nt - 1));
     for (int64_t t = nt - 1; t >= 1; --t) {
       double zf[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) zf[j] = cn[j];
-      const int64_t tp = t > 1 ? t - 1 : 1;
+      const int64_t tp = t > 1 ? t - 1 : 1;     // the next (lower) tile's input and checkpoint in flight
 #pragma unroll
       for (int j = 0; j < 4; ++j) cn[j] = ck[(tp * 4 + j) * 64];
-      double e[TL];
-      tile_e(t, e);
+      const double lop = load_lo(tp);
       double yt[TL];
 #pragma unroll
-      for (int k = 0; k < TL; ++k) yt[k] = df2t_step<4>(zf, f, e[k]);
+      for (int c = 0; c < NCH; ++c) {
+        double2 fv[HC];
+#pragma unroll
+        for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
+        load_chunk(tp, c, ring[c]);
+        double e[CH];
+        chunk_e(t, c, fv, e);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) yt[c * CH + k] = df2t_step<4>(zf, f, e[k]);
+      }
 #pragma unroll
       for (int k = TL - 1; k >= 1; k -= 2) {
         const double y1 = df2t_step<4>(zb, f, yt[k]);
@@ -334,6 +523,7 @@ __global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir
           sym_out(t * TL + k - 1, y0);
         }
       }
+      put_lo(tp, lop);
     }
   }
   for (int e = pad + (int)nh - 1; e >= 0; --e) {
@@ -349,35 +539,316 @@ __global__ __launch_bounds__(64) void k_lp_lane(PskBuffers buf, PskParams p, Iir
 }
 
 // ---------------------------------------------------------------------------
+// low-pass, role-split: four waves per group of 64 streams -- (re, im) x
+// (forward / re-run, backward).  The forward waves run the forward pass
+// (checkpoints every TL2 samples, head / tail edges, the input/output zero
+// detector) while the backward waves wait; then tile by tile from the end the
+// forward waves re-run tile t-1 into an LDS buffer while the backward waves
+// filter tile t out of the other one and write the symbol samples.  Two
+// passes of latency instead of three.  Same arithmetic and detector as
+// k_lp_lane; TL2 = 20 keeps the LDS of a group at 40 KB.
+template <int SPS, int FM, int TL2>
+__global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, Iir f) {
+  constexpr int TL = TL2;
+  constexpr int CH = TL % 8 == 0 ? 8 : 4;       // samples per f chunk
+  constexpr int NCH = TL / CH, HC = CH / 2;
+  static_assert(TL % CH == 0 && TL <= 64, "tile = whole chunks; one LO value per lane");
+  static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
+  __shared__ __attribute__((aligned(16))) double lo_lds[2][2][TL];              // [comp][buf]
+  __shared__ __attribute__((aligned(16))) double2 yb[2][2][TL / 2][64];        // [comp][buf][pair][lane]
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int comp = wv & 1, role = wv >> 1;
+  const int64_t w = blockIdx.x;
+  if (w * 64 >= buf.n_streams) return;          // block-uniform: no barrier is skipped by part of a block
+  const int64_t s = w * 64 + lane;
+  const int64_t n = p.n, n2 = (n + 1) >> 1;
+  const int pad = p.pad2;
+  const int64_t nt = n / TL;
+  const int64_t G = (buf.n_streams + 63) / 64;
+  const int64_t wc = w * 2 + comp;
+  const int64_t ecap = 2 * (TL + pad);
+  double* __restrict__ ck = buf.s3 + (size_t)wc * nt * 4 * 64 + lane;
+  double* __restrict__ eh = buf.s3 + (size_t)2 * G * nt * 4 * 64 + (size_t)wc * ecap * 64 + lane;
+  double* __restrict__ et = eh + (size_t)(pad + TL) * 64;
+  const double* __restrict__ fl = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+  const double* __restrict__ lov = buf.lo2 + (size_t)comp * n;
+  CDouble* const loc = (CDouble*)(buf.lo2 + (size_t)comp * n);
+  CDouble* const lo4 = (CDouble*)(buf.lo) + 2 * comp;
+  auto F = [&](int64_t i) { return fl[(i >> 1) * 64 + (i & 1)]; };
+  auto Xm = [&](int64_t i) { return F(i) * loc[i]; };
+  auto load_chunk = [&](int64_t t, int c, double2 (&r)[HC]) {
+    const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2) + c * HC) * 64);
+#pragma unroll
+    for (int k = 0; k < HC; ++k) r[k] = fp[k * 32];
+  };
+  auto load_lo = [&](int64_t t) -> double { return lov[t * TL + (lane < TL ? lane : 0)]; };
+  auto put_lo = [&](int64_t t, double v) {
+    if (lane < TL) lo_lds[comp][t & 1][lane] = v;
+  };
+  auto chunk_e = [&](int64_t t, int c, const double2 (&fv)[HC], double (&e)[CH]) {
+    const double2* lp = reinterpret_cast<const double2*>(&lo_lds[comp][t & 1][c * CH]);
+#pragma unroll
+    for (int k = 0; k < HC; ++k) {
+      const double2 l = lp[k];
+      e[2 * k] = fv[k].x * l.x;
+      e[2 * k + 1] = fv[k].y * l.y;
+    }
+  };
+  const int64_t nh = n < TL ? n : TL;
+  const int64_t i_tail = nt >= 1 ? nt * TL : nh;
+  const int ne = (int)(n - i_tail) + pad;
+
+  if (role == 0) {
+    // ---- forward pass (as k_lp_lane) ----------------------------------------
+    double z[4];
+    float acc = __builtin_inff();
+    bool bad = false;
+    const double x0 = F(0) * lo4[0] + lo4[1];
+    const double xl = Xm(n - 1);
+    bad |= __builtin_amdgcn_class(x0, kClsX);
+    const double e0 = 2.0 * x0 - Xm(pad);
+    bad |= __builtin_amdgcn_class(e0, kClsY);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) z[j] = f.zi[j] * e0;
+    for (int jj = 0; jj < pad; ++jj) {
+      const double e = 2.0 * x0 - Xm(pad - jj);
+      const double y = df2t_step<4>(z, f, e);
+      acc = tiny_min3(acc, e, y);
+      eh[jj * 64] = y;
+    }
+    for (int64_t i = 0; i < nh; ++i) {
+      const double e = i == 0 ? x0 : Xm(i);
+      const double y = df2t_step<4>(z, f, e);
+      acc = tiny_min3(acc, i == 0 ? y : e, y);
+      eh[(pad + i) * 64] = y;
+    }
+    double2 ring[NCH][HC];
+    if (nt > 1) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) load_chunk(1, c, ring[c]);
+      put_lo(1, load_lo(1));
+    }
+    for (int64_t t = 1; t < nt; ++t) {
+      const int64_t tn = t + 1 < nt ? t + 1 : t;
+      const double lon = load_lo(tn);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ck[(t * 4 + j) * 64] = z[j];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        double2 fv[HC];
+#pragma unroll
+        for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
+        load_chunk(tn, c, ring[c]);
+        double e[CH];
+        chunk_e(t, c, fv, e);
+#pragma unroll
+        for (int k = 0; k < CH; k += 2) {
+          const double y0 = df2t_step<4>(z, f, e[k]);
+          const double y1 = df2t_step<4>(z, f, e[k + 1]);
+          acc = tiny_min3(acc, e[k], e[k + 1]);
+          acc = tiny_min3(acc, y0, y1);
+        }
+      }
+      put_lo(tn, lon);
+    }
+    int ee = 0;
+    for (int64_t i = i_tail; i < n; ++i) {
+      const double e = Xm(i);
+      const double y = df2t_step<4>(z, f, e);
+      acc = tiny_min3(acc, e, y);
+      et[(ee++) * 64] = y;
+    }
+    for (int jj = 0; jj < pad; ++jj) {
+      const double e = 2.0 * xl - Xm(n - 2 - jj);
+      const double y = df2t_step<4>(z, f, e);
+      acc = tiny_min3(acc, e, y);
+      et[(ee++) * 64] = y;
+    }
+    bad |= !(acc >= kTinyHi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(z[j]);
+    if (bad && s < buf.n_streams) atomicOr(&buf.flags[s], 1);
+    __threadfence();                            // checkpoints + edges: read by both roles
+    __syncthreads();
+
+    // ---- re-run tiles nt-1 .. 1 forward into LDS -----------------------------
+    double cn[4];
+    if (nt > 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cn[j] = ck[((nt - 1) * 4 + j) * 64];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) load_chunk(nt - 1, c, ring[c]);
+      put_lo(nt - 1, load_lo(nt - 1));
+    }
+    for (int64_t it = 0; it < nt; ++it) {       // it = nt-1 is the backward waves' last tile: barrier only
+      const int64_t t = nt - 1 - it;
+      if (t >= 1) {
+        double zf[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zf[j] = cn[j];
+        const int64_t tp = t > 1 ? t - 1 : 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cn[j] = ck[(tp * 4 + j) * 64];
+        const double lop = load_lo(tp);
+        double2 (*ybuf)[64] = yb[comp][it & 1];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          double2 fv[HC];
+#pragma unroll
+          for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
+          load_chunk(tp, c, ring[c]);
+          double e[CH];
+          chunk_e(t, c, fv, e);
+#pragma unroll
+          for (int k = 0; k < CH; k += 2) {
+            const double y0 = df2t_step<4>(zf, f, e[k]);
+            const double y1 = df2t_step<4>(zf, f, e[k + 1]);
+            ybuf[(c * CH + k) >> 1][lane] = make_double2(y0, y1);
+          }
+        }
+        put_lo(tp, lop);
+      }
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();                            // the forward pass is done
+    const int64_t S = p.n_sym, first = p.first, sps = p.sps;
+    double* __restrict__ symp = buf.s1 + sym_index(s, S, 0, comp);
+    auto sym_out = [&](int64_t i, double y) {
+      if (i >= first && (i - first) % sps == 0) symp[((i - first) / sps) * 64] = y;
+    };
+    float accb = __builtin_inff();
+    double zb[4];
+    const double ylast = et[(ne - 1) * 64];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zb[j] = f.zi[j] * ylast;
+    for (int e = ne - 1; e >= 0; --e) {
+      const double y = df2t_step<4>(zb, f, et[e * 64]);
+      accb = tiny_min3(accb, y, y);
+      const int64_t i = i_tail + e;
+      if (i < n) sym_out(i, y);
+    }
+    // the forward waves meet nt barriers in their re-run loop: tile nt-1 is in
+    // buffer 0 after the first (none at all when nt == 0)
+    if (nt >= 1) __syncthreads();
+    const int64_t q0 = SPS > 0 ? first / SPS : 0;
+    for (int64_t it = 1; it < nt; ++it) {
+      const int64_t t = nt - it;
+      const double2 (*ybuf)[64] = yb[comp][(it - 1) & 1];
+#pragma unroll
+      for (int k = TL - 1; k >= 1; k -= 2) {
+        const double2 yy = ybuf[k >> 1][lane];
+        const double y1 = df2t_step<4>(zb, f, yy.y);
+        const double y0 = df2t_step<4>(zb, f, yy.x);
+        accb = tiny_min3(accb, y1, y0);
+        if constexpr (SPS > 0) {
+          if (k % SPS == FM) symp[(t * (TL / SPS) + (k - FM) / SPS - q0) * 64] = y1;
+          if ((k - 1) % SPS == FM) symp[(t * (TL / SPS) + (k - 1 - FM) / SPS - q0) * 64] = y0;
+        } else {
+          sym_out(t * TL + k, y1);
+          sym_out(t * TL + k - 1, y0);
+        }
+      }
+      __syncthreads();
+    }
+    for (int e = pad + (int)nh - 1; e >= 0; --e) {
+      const double y = df2t_step<4>(zb, f, eh[e * 64]);
+      accb = tiny_min3(accb, y, y);
+      const int64_t i = e - pad;
+      if (i >= 0) sym_out(i, y);
+    }
+    bool bad = !(accb >= kTinyHi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(zb[j]);
+    if (bad && s < buf.n_streams) atomicOr(&buf.flags[s], 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers (api.cpp)
+static int lane_wpb() {
+  // waves per workgroup of the lane kernels: AMR_LANE_WPB=1/2/4 (default 4:
+  // with 16 batches in flight, 4-wave workgroups ran 4.85 ms/step against
+  // 5.82 for one-wave workgroups -- the dispatcher spreads them better)
+  static const int v = [] {
+    const char* e = getenv("AMR_LANE_WPB");
+    const int k = e ? atoi(e) : 4;
+    return k == 1 || k == 2 ? k : 4;
+  }();
+  return v;
+}
+
+static int bp_split() {
+  // role-split band-pass (k_bp_lane2): AMR_BP_SPLIT=0 turns it off
+  static const int v = [] { const char* e = getenv("AMR_BP_SPLIT"); return e && e[0] == '0' ? 0 : 1; }();
+  return v;
+}
+
+template <typename T>
+static void launch_bp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  const int64_t g = (b.n_streams + 63) / 64;
+  if (bp_split()) {
+    if (lane_wpb() >= 2)
+      hipLaunchKernelGGL((k_bp_lane2<T, 2>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
+    else
+      hipLaunchKernelGGL((k_bp_lane2<T, 1>), dim3((unsigned)g), dim3(128), 0, st, b, p, f);
+    return;
+  }
+  switch (lane_wpb()) {
+    case 4: hipLaunchKernelGGL((k_bp_lane<T, 4>), dim3((unsigned)((g + 3) / 4)), dim3(256), 0, st, b, p, f); break;
+    case 2: hipLaunchKernelGGL((k_bp_lane<T, 2>), dim3((unsigned)((g + 1) / 2)), dim3(128), 0, st, b, p, f); break;
+    default: hipLaunchKernelGGL((k_bp_lane<T, 1>), dim3((unsigned)g), dim3(64), 0, st, b, p, f);
+  }
+}
+
 hipError_t launch_psk_bandpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   if (f.nt != 9) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((b.n_streams + 63) / 64)), block(64);
   switch (b.dtype) {
-    case kF32: hipLaunchKernelGGL(k_bp_lane<float>, grid, block, 0, st, b, p, f); break;
-    case kF64: hipLaunchKernelGGL(k_bp_lane<double>, grid, block, 0, st, b, p, f); break;
-    case kI16: hipLaunchKernelGGL(k_bp_lane<int16_t>, grid, block, 0, st, b, p, f); break;
+    case kF32: launch_bp<float>(b, p, f, st); break;
+    case kF64: launch_bp<double>(b, p, f, st); break;
+    case kI16: launch_bp<int16_t>(b, p, f, st); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+static int lp_split() {
+  // role-split low-pass (k_lp_lane2): AMR_LP_SPLIT=1 turns it on (off by
+  // default: its 20-sample tiles double the checkpoint traffic and leave its
+  // loads less time; 4.54 vs 4.29 ms/step at 16 in flight, same solo time)
+  static const int v = [] { const char* e = getenv("AMR_LP_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
+  return v;
+}
+
+template <int S_, int F_>
+static void launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  const int64_t g = (b.n_streams + 63) / 64;
+  if (lp_split()) {
+    hipLaunchKernelGGL((k_lp_lane2<S_, F_, kLpT2>), dim3((unsigned)g), dim3(256), 0, st, b, p, f);
+    return;
+  }
+  switch (lane_wpb()) {
+    case 4: hipLaunchKernelGGL((k_lp_lane<S_, F_, 4>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f); break;
+    case 2: hipLaunchKernelGGL((k_lp_lane<S_, F_, 2>), dim3((unsigned)g), dim3(128), 0, st, b, p, f); break;
+    default:
+      // a multiple of 16 blocks: the re/im XCD pairing is a bijection
+      hipLaunchKernelGGL((k_lp_lane<S_, F_, 1>), dim3((unsigned)((2 * g + 15) / 16 * 16)), dim3(64), 0, st, b, p, f);
+  }
 }
 
 hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   if (f.nt != 5) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
   if (e != hipSuccess) return e;
-  // a multiple of 16 blocks: the re/im XCD pairing is a bijection
-  const dim3 grid((unsigned)((2 * ((b.n_streams + 63) / 64) + 15) / 16 * 16)), block(64);
   const int fm = (int)(p.first % (p.sps > 0 ? p.sps : 1));
-#define AMR_LP_LANE(S_, F_) hipLaunchKernelGGL((k_lp_lane<S_, F_>), grid, block, 0, st, b, p, f)
-  if (p.sps == 10 && fm == 5) AMR_LP_LANE(10, 5);
-  else if (p.sps == 5 && fm == 2) AMR_LP_LANE(5, 2);
-  else if (p.sps == 20 && fm == 10) AMR_LP_LANE(20, 10);
-  else if (p.sps == 10 && fm == 0) AMR_LP_LANE(10, 0);
-  else if (p.sps == 5 && fm == 0) AMR_LP_LANE(5, 0);
-  else if (p.sps == 20 && fm == 0) AMR_LP_LANE(20, 0);
-  else AMR_LP_LANE(0, 0);
-#undef AMR_LP_LANE
+  if (p.sps == 10 && fm == 5) launch_lp<10, 5>(b, p, f, st);
+  else if (p.sps == 5 && fm == 2) launch_lp<5, 2>(b, p, f, st);
+  else if (p.sps == 20 && fm == 10) launch_lp<20, 10>(b, p, f, st);
+  else if (p.sps == 10 && fm == 0) launch_lp<10, 0>(b, p, f, st);
+  else if (p.sps == 5 && fm == 0) launch_lp<5, 0>(b, p, f, st);
+  else if (p.sps == 20 && fm == 0) launch_lp<20, 0>(b, p, f, st);
+  else launch_lp<0, 0>(b, p, f, st);
   return hipGetLastError();
 }
 

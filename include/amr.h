@@ -121,8 +121,9 @@ int amr_psk_plan_create(amr_psk_plan **plan, int device, int kind, int64_t n_sam
 int amr_psk_plan_destroy(amr_psk_plan *plan);
 /* bytes a stream's output can need: floor(bits/8) */
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan *plan);
-/* device bytes the plan holds in HBM: scratch + the host-API staging
- * (allocated on the first amr_psk_demod_host call) */
+/* the most device memory the plan can hold: scratch (its row-layout buffers
+ * are allocated on the first call that runs that layout) + the host-API
+ * staging (allocated on the first amr_psk_demod_host call) */
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
 int amr_psk_plan_synchronize(amr_psk_plan *plan);
 /* record per-kernel HIP events on the plan's stream (1) or not (0) */

@@ -31,14 +31,14 @@ def find(d, pat):
     return m[0] if m else None
 
 
-KERNELS = ["k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
+KERNELS = ["k_bp_lane", "k_lp_lane", "k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
            "k_lowpass_bwd_q", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
            "k_sync_pack", "k_fec_decode",
            "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
-    "qpsk9600": {"bandpass": ["k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass"],
-                 "lowpass_fwd": ["k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
+    "qpsk9600": {"bandpass": ["k_bp_lane", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass"],
+                 "lowpass_fwd": ["k_lp_lane", "k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
                  "lowpass_exact": ["k_lowpass_exact"], "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
     "ofdm8": None, "psk8fec": None,
     "fsk9600": {"bandpass": ["k_fsk_bandpass"], "hilbert": ["k_fft_cols", "k_fft_mid", "k_fft_rows"],
@@ -74,11 +74,13 @@ def main():
     trace = find(os.path.join(out, "trace"), "*kernel_trace.csv")
     bj = os.path.join(out, "trace_bench.json")
     steps = None
+    cfg = {}
     if os.path.exists(bj):
         with open(bj) as f:
             for line in f:
                 if line.startswith("{"):
                     steps = json.loads(line).get("steps")
+                    cfg = json.loads(line).get("config", {})
     if trace and steps:
         per = {}
         for r in rows(trace):
@@ -122,7 +124,8 @@ def main():
             allres = {}
     allres["source"] = "rocprofv3 kernel-trace --stats + separate --pmc FETCH_SIZE / WRITE_SIZE passes"
     allres["fetch_correction"] = "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads)"
-    allres[workload] = {"kernels": res, "slots": slots}
+    allres[workload] = {"kernels": res, "slots": slots, "inflight": cfg.get("batches_in_flight"),
+                        "layout": cfg.get("kernel_layout")}
     with open(pmc_path, "w") as f:
         json.dump(allres, f, indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:

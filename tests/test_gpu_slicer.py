@@ -11,7 +11,8 @@ within ulps: the band where K4a replays numpy's arctan2), at magnitudes
 1e-300 .. 1e289, plus the axes at magnitudes from the smallest denormal to
 1e300, signed zeros, infinities and NaN.
 
-Ulp ties of np.angle with denormal or > 2^963 components are not covered:
+Ulp ties of np.angle with components below 2^-1015 or above 2^985 are not
+covered:
 numpy's AVX-512 arctan2 takes internal paths there that K4a does not model
 (it uses ocml's atan2), so a decision exactly at an edge may differ; such a
 diff is 2^-30-rare among near-ties of real signals, themselves ~2^-30-rare
@@ -62,7 +63,7 @@ def edge_diffs():
                 base_r, base_i = sr * m, si * m
                 # |dr| vs |di| within 3 ulp of equal: the pi/4 + k*pi/2 edges, where
                 # an ulp of np.angle decides -- inside the domain of K4a's model of
-                # numpy's arctan2 (component magnitudes 2^-996 .. 2^963)
+                # numpy's arctan2 (component magnitudes 2^-1015 .. 2^985)
                 for k in (range(-3, 4) if 1e-300 <= m <= 1e289 else ()):
                     r = base_r
                     for _ in range(abs(k)):

@@ -64,3 +64,62 @@ def test_gloo_world2_equals_single_process(tmp_path, world):
     got = list(np.load(out))
     want = [w.hex() for w in oracle.psk_demod_batch("qpsk", x, 9600)[0]]
     assert got == want
+
+
+def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_file):
+    """bench.py's N>1 bookkeeping end to end on gloo: each rank takes its
+    shard of the strong-scaling global batch (bench.workload_sizes), decodes
+    it (the oracle stands in for the GPU), packs it into its [B_slot][cap]
+    slot, the slots are all-gathered (gloo stands in for RCCL), and the
+    gathered buffer is checked against every rank's own output exactly as
+    bench.py does it (row_digest + gather_verdict)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
+    import torch
+    import torch.distributed as dist
+    import bench
+    import synth
+    from oracle import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B, Bg, lo, B_slot = bench.workload_sizes("ofdm8", B_global, world, rank)
+    allx = synth.qpsk_batch(B_global, 4000, 9600, seed=5, distinct=B_global)
+    outs, _ = oracle.psk_demod_batch("qpsk", allx[lo:lo + B], 9600)
+    own = np.zeros((B_slot, cap), np.uint8)
+    lens = np.zeros(B_slot, np.int64)
+    for i, o in enumerate(outs):
+        own[i, :len(o)] = np.frombuffer(o, np.uint8)
+        lens[i] = len(o)
+    slots = [torch.empty((B_slot, cap), dtype=torch.uint8) for _ in range(world)]
+    lslots = [torch.empty(B_slot, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(slots, torch.from_numpy(own))
+    dist.all_gather(lslots, torch.from_numpy(lens))
+    gp = np.stack([t.numpy() for t in slots])
+    gl = np.stack([t.numpy() for t in lslots])
+    if rank == 0 and corrupt_rank is not None:
+        gp[corrupt_rank, 0, 0] ^= 0xFF                    # a wrong byte in that rank's slice
+    own_digests = [None] * world
+    dist.all_gather_object(own_digests, bench.row_digest(own[:B], lens[:B]))
+    sizes = [bench.workload_sizes("ofdm8", B_global, world, r)[0] for r in range(world)]
+    bad = bench.gather_verdict([bench.row_digest(gp[r], gl[r]) for r in range(world)], own_digests, sizes)
+    if rank == 0:
+        # the gathered rows in rank order are the single-process batch's output
+        want, _ = oracle.psk_demod_batch("qpsk", allx, 9600)
+        got = [gp[r, i, :gl[r, i]].tobytes() for r in range(world) for i in range(sizes[r])]
+        if corrupt_rank is not None:
+            got = want                                    # the corruption is the verdict's to find
+        np.save(result_file, np.array([str(bad), str(got == want)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,B_global,corrupt", [(2, 7, None), (3, 8, None), (3, 8, 2)])
+def test_bench_gather_bookkeeping_gloo(tmp_path, world, B_global, corrupt):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "res.npy")
+    cap = 2 * 4000 // 10 // 8 + 8
+    mp.spawn(_bench_gather_worker, args=(world, _free_port(), B_global, cap, corrupt, out), nprocs=world, join=True)
+    bad, same = list(np.load(out))
+    assert same == "True"
+    assert bad == ("[]" if corrupt is None else f"[{corrupt}]")
