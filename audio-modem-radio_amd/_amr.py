@@ -43,6 +43,8 @@ EXPORTS = [
     "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings", "amr_psk_plan_set_inflight",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
     "amr_psk_slice_host", "amr_psk_plan_last_layout", "amr_synth_tile_noise",
+    "amr_psk_demod_host_async", "amr_fsk_demod_host_async", "amr_host_register", "amr_host_unregister",
+    "amr_host_alloc", "amr_host_free",
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
@@ -128,6 +130,30 @@ def frame_parse(raws, max_cands: int = 64):
     return [(int(cnt[i]), recs[i, :min(int(cnt[i]), max_cands)]) for i in range(n)]
 
 
+class PinnedArray:
+    """A numpy array over page-locked host memory (amr_host_alloc): the buffer
+    a capture loop fills and hands to the *_demod_host_async entries."""
+
+    def __init__(self, shape, dtype):
+        self.nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        self._p = ctypes.c_void_p()
+        check(lib().amr_host_alloc(ctypes.byref(self._p), max(1, self.nbytes)))
+        buf = (ctypes.c_uint8 * max(1, self.nbytes)).from_address(self._p.value)
+        self.array = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if self._p:
+            self.array = None
+            lib().amr_host_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class AmrError(RuntimeError):
     """A libamr.so call failed (message from amr_last_error)."""
 
@@ -177,6 +203,12 @@ def lib():
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
             "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
             "amr_psk_plan_last_layout": (I32, [P]),
+            "amr_psk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
+            "amr_fsk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
+            "amr_host_register": (I32, [P, I64]),
+            "amr_host_alloc": (I32, [P, I64]),
+            "amr_host_free": (I32, [P]),
+            "amr_host_unregister": (I32, [P]),
             "amr_synth_tile_noise": (I32, [P, I64, I64, P, I64, I64, F, ctypes.c_uint64]),
             "amr_fsk_plan_create": (I32, [P, I32, I64, I64, P, P, P, P, P, P, I32, I64]),
             "amr_fsk_plan_destroy": (I32, [P]),

@@ -56,6 +56,7 @@ struct PskBuffers {
   double* s3;             // low-pass forward output   [2G][m2p/2][64][2]
   uint32_t* words;        // [B][n_words] bit buffer, MSB first
   int32_t* flags;         // [B] 1 => take the exact complex low-pass path
+  int32_t* bp_flags;      // [B] 1 => the band-pass skipped its zero taps where that is not exact (lane kernels)
   uint8_t* out;           // [B][out_stride] packed bytes
   int64_t out_stride;
   int64_t* out_len;       // [B]

@@ -148,6 +148,34 @@ int device_crc(int dev, const uint32_t** table, const uint32_t** x2n) {
 
 bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }
 
+// Per-device staging of the synchronous host entries that take no plan
+// (amr_fec_decode_host, amr_frame_parse_host): grow-only buffers kept for the
+// process instead of hipMalloc/hipFree on every call; one call per device at a
+// time (the lock is held for the whole call).
+struct HostStaging {
+  std::mutex mu;
+  void* buf[6] = {};
+  int64_t bytes[6] = {};
+};
+HostStaging g_staging[64];
+
+hipError_t staging_get(HostStaging& hs, int slot, int64_t need, void** out) {
+  if (hs.bytes[slot] < need || !hs.buf[slot]) {
+    if (hs.buf[slot]) {
+      hipError_t e = hipFree(hs.buf[slot]);
+      if (e != hipSuccess) return e;
+    }
+    hs.buf[slot] = nullptr;
+    hs.bytes[slot] = 0;
+    const int64_t grow = std::max<int64_t>(need, hs.bytes[slot] * 2);
+    hipError_t e = hipMalloc(&hs.buf[slot], (size_t)std::max<int64_t>(grow, 256));
+    if (e != hipSuccess) return e;
+    hs.bytes[slot] = std::max<int64_t>(grow, 256);
+  }
+  *out = hs.buf[slot];
+  return hipSuccess;
+}
+
 }  // namespace
 
 // doubles of slack below s1/s3: the backward passes prefetch up to a few
@@ -398,7 +426,7 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
       {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
       {(void**)&pl->s3_base, kFrontSlack * 8 + lane_s3_bytes(pl)},
       {(void**)&pl->words, g * kWave * p.n_words * 4},
-      {(void**)&pl->flags, g * kWave * 4},
+      {(void**)&pl->flags, 2 * g * kWave * 4},   // low-pass flags, then band-pass flags
   };
   for (const A& a : allocs) {
     e = hipMalloc(a.ptr, (size_t)a.bytes);
@@ -550,6 +578,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   b.s3 = pl->s3;
   b.words = pl->words;
   b.flags = pl->flags;
+  b.bp_flags = pl->flags + pl->groups * kWave;
   b.out = d_out;
   b.out_stride = out_stride;
   b.out_len = d_len;
@@ -702,6 +731,77 @@ int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, 
   return AMR_OK;
 }
 
+// Queued host entry: upload, demod and download on the plan's stream, no
+// wait.  With two or more plans used in turn, batch k+1's upload (PCIe) runs
+// while batch k demodulates -- the PCIe-inclusive rate of a stream of
+// batches is then the link's, not link + demod.  Host buffers
+// must stay untouched until amr_psk_plan_synchronize; page-locked buffers
+// (amr_host_register) make the copies truly asynchronous.
+int amr_psk_demod_host_async(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                             uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+  if (!plan || (B && (!x || !out || !out_len || !sync_idx)))
+    return fail(AMR_E_INVALID, "amr_psk_demod_host_async: NULL argument");
+  const int64_t es = dtype_size(dtype);
+  if (!es) return fail(AMR_E_INVALID, "unknown dtype");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < plan->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
+  if (B == 0) return AMR_OK;
+  const int64_t n = plan->p.n;
+  const int64_t cap = plan->out_cap;
+  if (!plan->d_x || plan->d_x_bytes < plan->max_streams * n * 8) {
+    HIP_TRY(hipStreamSynchronize(plan->stream));          // a previous staging buffer may still be read
+    if (int rc = ensure(&plan->d_x, &plan->d_x_bytes, plan->max_streams * n * 8)) return rc;
+  }
+  if (!plan->d_out) {
+    HIP_TRY(hipMalloc(&plan->d_out, (size_t)(plan->max_streams * cap)));
+    HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
+    HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
+  }
+  hipStream_t st = plan->stream;
+  if (x_stride == n)
+    HIP_TRY(hipMemcpyAsync(plan->d_x, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
+  else
+    HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
+                             hipMemcpyHostToDevice, st));
+  if (int rc = run_psk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync, nullptr, 0,
+                       nullptr, nullptr))
+    return rc;
+  if (out_stride == cap)
+    HIP_TRY(hipMemcpyAsync(out, plan->d_out, (size_t)(B * cap), hipMemcpyDeviceToHost, st));
+  else
+    HIP_TRY(hipMemcpy2DAsync(out, (size_t)out_stride, plan->d_out, (size_t)cap, (size_t)std::min(out_stride, cap),
+                             (size_t)B, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out_len, plan->d_len, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+  return AMR_OK;
+}
+
+int amr_host_alloc(void** p, int64_t bytes) {
+  if (!p || bytes <= 0) return fail(AMR_E_INVALID, "amr_host_alloc: bad argument");
+  HIP_TRY(hipHostMalloc(p, (size_t)bytes, hipHostMallocDefault));
+  return AMR_OK;
+}
+
+int amr_host_free(void* p) {
+  if (p) HIP_TRY(hipHostFree(p));
+  return AMR_OK;
+}
+
+int amr_host_register(void* p, int64_t bytes) {
+  if (!p || bytes <= 0) return fail(AMR_E_INVALID, "amr_host_register: bad argument");
+  HIP_TRY(hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault));
+  return AMR_OK;
+}
+
+int amr_host_unregister(void* p) {
+  if (!p) return fail(AMR_E_INVALID, "amr_host_unregister: NULL");
+  HIP_TRY(hipHostUnregister(p));
+  return AMR_OK;
+}
+
 int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_len, int64_t n, uint8_t* out,
                         int64_t out_stride, int64_t* out_len, int32_t* crc_ok) {
   if (n < 0 || (n && (!in || !in_len || !out || !out_len || !crc_ok)))
@@ -718,15 +818,18 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
       return fail(AMR_E_INVALID, "in_len out of range");
     maxlen = in_len[i] > maxlen ? in_len[i] : maxlen;
   }
+  if (dev < 0 || dev >= 64) return fail(AMR_E_INVALID, "device ordinal out of range");
+  HostStaging& hs = g_staging[dev];
+  std::lock_guard<std::mutex> lk(hs.mu);
   uint8_t *d_in = nullptr, *d_out = nullptr;
   int64_t *d_in_len = nullptr, *d_out_len = nullptr;
   int32_t* d_crc = nullptr;
   const int64_t stride = maxlen > 0 ? maxlen : 1;
-  hipError_t e = hipMalloc(&d_in, (size_t)(n * stride));
-  if (e == hipSuccess) e = hipMalloc(&d_out, (size_t)(n * stride));
-  if (e == hipSuccess) e = hipMalloc(&d_in_len, (size_t)n * 8);
-  if (e == hipSuccess) e = hipMalloc(&d_out_len, (size_t)n * 8);
-  if (e == hipSuccess) e = hipMalloc(&d_crc, (size_t)n * 4);
+  hipError_t e = staging_get(hs, 0, n * stride, (void**)&d_in);
+  if (e == hipSuccess) e = staging_get(hs, 1, n * stride, (void**)&d_out);
+  if (e == hipSuccess) e = staging_get(hs, 2, n * 8, (void**)&d_in_len);
+  if (e == hipSuccess) e = staging_get(hs, 3, n * 8, (void**)&d_out_len);
+  if (e == hipSuccess) e = staging_get(hs, 4, n * 4, (void**)&d_crc);
   if (e == hipSuccess && maxlen > 0)
     e = memcpy_rows(d_in, stride, in, in_stride, maxlen, n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
@@ -736,8 +839,6 @@ int amr_fec_decode_host(const uint8_t* in, int64_t in_stride, const int64_t* in_
     e = memcpy_rows(out, out_stride, d_out, stride, maxlen, n, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(out_len, d_out_len, (size_t)n * 8, hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(crc_ok, d_crc, (size_t)n * 4, hipMemcpyDeviceToHost);
-  for (void* p : {(void*)d_in, (void*)d_out, (void*)d_in_len, (void*)d_out_len, (void*)d_crc})
-    if (p) (void)hipFree(p);
   if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_fec_decode_host: ") + hipGetErrorString(e));
   return AMR_OK;
 }
@@ -834,15 +935,18 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
     if (in_len[i] < 0 || in_len[i] > in_stride) return fail(AMR_E_INVALID, "in_len out of range");
     maxlen = in_len[i] > maxlen ? in_len[i] : maxlen;
   }
+  if (dev < 0 || dev >= 64) return fail(AMR_E_INVALID, "device ordinal out of range");
+  HostStaging& hs = g_staging[dev];
+  std::lock_guard<std::mutex> lk(hs.mu);
   uint8_t* d_in = nullptr;
   int64_t* d_in_len = nullptr;
   int32_t* d_cnt = nullptr;
   amr_frame_rec* d_recs = nullptr;
   const int64_t stride = maxlen > 0 ? maxlen : 1;
-  hipError_t e = hipMalloc(&d_in, (size_t)(n * stride));
-  if (e == hipSuccess) e = hipMalloc(&d_in_len, (size_t)n * 8);
-  if (e == hipSuccess) e = hipMalloc(&d_cnt, (size_t)n * 4);
-  if (e == hipSuccess) e = hipMalloc(&d_recs, (size_t)(n * max_cands) * sizeof(amr_frame_rec));
+  hipError_t e = staging_get(hs, 0, n * stride, (void**)&d_in);
+  if (e == hipSuccess) e = staging_get(hs, 2, n * 8, (void**)&d_in_len);
+  if (e == hipSuccess) e = staging_get(hs, 4, n * 4, (void**)&d_cnt);
+  if (e == hipSuccess) e = staging_get(hs, 5, n * max_cands * (int64_t)sizeof(amr_frame_rec), (void**)&d_recs);
   if (e == hipSuccess && maxlen > 0)
     e = memcpy_rows(d_in, stride, in, in_stride, maxlen, n, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(d_in_len, in_len, (size_t)n * 8, hipMemcpyHostToDevice);
@@ -851,8 +955,6 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
   if (e == hipSuccess) e = hipMemcpy(n_cands, d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost);
   if (e == hipSuccess)
     e = hipMemcpy(recs, d_recs, (size_t)(n * max_cands) * sizeof(amr_frame_rec), hipMemcpyDeviceToHost);
-  for (void* p : {(void*)d_in, (void*)d_in_len, (void*)d_cnt, (void*)d_recs})
-    if (p) (void)hipFree(p);
   if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_frame_parse_host: ") + hipGetErrorString(e));
   return AMR_OK;
 }

@@ -561,6 +561,45 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   return AMR_OK;
 }
 
+// Queued host entry (as amr_psk_demod_host_async): upload, demod, download on
+// the plan's stream, no wait; host buffers untouched until amr_fsk_plan_synchronize.
+int amr_fsk_demod_host_async(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                             uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+  if (!plan || (B && (!x || !out || !out_len || !sync_idx)))
+    return fail(AMR_E_INVALID, "amr_fsk_demod_host_async: NULL argument");
+  const int64_t es = dtype_size(dtype);
+  if (!es) return fail(AMR_E_INVALID, "unknown dtype");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < plan->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
+  if (B == 0) return AMR_OK;
+  const int64_t n = plan->p.n;
+  const int64_t cap = plan->out_cap;
+  if (!plan->d_x) HIP_TRY(hipMalloc(&plan->d_x, (size_t)(plan->max_streams * n * 8)));
+  if (!plan->d_out) {
+    HIP_TRY(hipMalloc(&plan->d_out, (size_t)(plan->max_streams * cap)));
+    HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
+    HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
+  }
+  hipStream_t st = plan->stream;
+  if (x_stride == n)
+    HIP_TRY(hipMemcpyAsync(plan->d_x, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
+  else
+    HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
+                             hipMemcpyHostToDevice, st));
+  if (int rc = run_fsk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+  if (out_stride == cap)
+    HIP_TRY(hipMemcpyAsync(out, plan->d_out, (size_t)(B * cap), hipMemcpyDeviceToHost, st));
+  else
+    HIP_TRY(hipMemcpy2DAsync(out, (size_t)out_stride, plan->d_out, (size_t)cap, (size_t)std::min(out_stride, cap),
+                             (size_t)B, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(out_len, plan->d_len, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+  return AMR_OK;
+}
+
 int amr_fsk_envelopes_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
                            double* mark_env, double* space_env) {
   if (!plan || (B && (!x || !mark_env || !space_env))) return fail(AMR_E_INVALID, "NULL argument");

@@ -58,6 +58,45 @@ __device__ __forceinline__ double df2t_step(double (&z)[NS], const Iir& f, doubl
   return y;
 }
 
+// The band-pass's odd taps b1, b3, b5, b7 are exactly +0.0 (butter(4, band);
+// the plan checks, PskParams::bp_zero_odd).  The step without them --
+// z[i] = z[i+1] - y*a[i+1] for even i -- is scipy's bit for bit whenever
+// z[i+1] + x*(+0.0) == z[i+1], i.e. unless z[i+1] is -0.0 (or x is inf / NaN,
+// which makes the final states non-finite).  The detector keeps the minimum
+// |hi word| (as float) of z1, z3, z5, z7 before every step: >= FLT_MIN means
+// |z| >= 2^-1015, never a zero; a stream that fails, or ends non-finite, is
+// flagged and its group re-run with every tap (k_bp_lane in exact mode).
+// 26 instead of 34 FP64 per step, + 2 v_min3_f32.
+__device__ __forceinline__ double df2t_step_zo(double (&z)[8], const Iir& f, double x, float& acc) {
+  acc = tiny_min3(acc, z[1], z[3]);
+  acc = tiny_min3(acc, z[5], z[7]);
+  const double y = z[0] + f.b[0] * x;
+  z[0] = z[1] - y * f.a[1];
+  z[1] = (z[2] + x * f.b[2]) - y * f.a[2];
+  z[2] = z[3] - y * f.a[3];
+  z[3] = (z[4] + x * f.b[4]) - y * f.a[4];
+  z[4] = z[5] - y * f.a[5];
+  z[5] = (z[6] + x * f.b[6]) - y * f.a[6];
+  z[6] = z[7] - y * f.a[7];
+  z[7] = x * f.b[8] - y * f.a[8];
+  return y;
+}
+
+template <bool ZO>
+__device__ __forceinline__ double bp_step(double (&z)[8], const Iir& f, double x, float& acc) {
+  if constexpr (ZO) return df2t_step_zo(z, f, x, acc);
+  else return df2t_step<8>(z, f, x);
+}
+
+template <bool ZO>
+__device__ __forceinline__ bool bp_bad(float acc, const double (&z)[8]) {
+  if constexpr (!ZO) return false;
+  bool bad = !(acc >= kTinyHi);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bad |= !__builtin_isfinite(z[j]);
+  return bad;
+}
+
 // checkpoint + edge scratch inside the plan's s1 (band-pass) / s3 (low-pass)
 __host__ __device__ inline int64_t bp_lane_edge_cap(int pad) { return kBpT + pad; }
 __host__ __device__ inline int64_t lp_lane_edge_cap(int pad) { return 2 * (kLpT + pad); }
@@ -74,7 +113,9 @@ int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
 // band-pass: lane = stream, wave = 64 streams.  Coefficients are wave-uniform
 // (kernel arguments in SGPRs).  s1 = [G][nt][8][64] checkpoints, then
 // [G][edge][64] tail outputs.
-template <typename T, int WPB>
+// FIXUP: re-run (every tap) only the groups the zero-tap kernel flagged;
+// the others exit at once.
+template <typename T, int WPB, bool FIXUP = false>
 __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);      // samples per 16-B load
@@ -85,6 +126,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
   if (w * 64 >= buf.n_streams) return;          // wave-uniform
   const int64_t last = buf.n_streams - 1;
   const int64_t s = w * 64 + lane;
+  if constexpr (FIXUP) {
+    if (!__any(s <= last && buf.bp_flags[s] != 0)) return;   // wave-uniform: nothing to redo here
+  }
   const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
   const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
   const int64_t n = p.n, n2 = (n + 1) >> 1;
@@ -185,7 +229,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
 // backward out of the other buffer and stores f -- the backward pass and the
 // re-run overlap, so the kernel takes two passes of latency instead of three
 // and a batch has twice the waves.  One workgroup barrier per tile.
-template <typename T, int GPB>
+template <typename T, int GPB, bool ZO>
 __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);
@@ -225,13 +269,14 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
   if (role == 0 && active) {
     // ---- forward pass: pads + tiles (checkpoints only) + tail (edge) ------
     double z[8];
+    float acc = __builtin_inff();
     const T x0 = x[0], xl = x[n - 1];
     {
       const double e0 = In<T>::ext(x0, x[pad]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
     }
-    for (int jj = 0; jj < pad; ++jj) (void)df2t_step<8>(z, f, In<T>::ext(x0, x[pad - jj]));
+    for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, In<T>::ext(x0, x[pad - jj]), acc);
     v4u xr[NL];
     if (nt > 0) load_tile(0, xr);
     for (int64_t t = 0; t < nt; ++t) {
@@ -242,11 +287,12 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
       for (int k = 0; k < NL; ++k) cur[k] = xr[k];
       load_tile(t + 1 < nt ? t + 1 : t, xr);
 #pragma unroll
-      for (int k = 0; k < TB; ++k) (void)df2t_step<8>(z, f, tile_x(cur, k));
+      for (int k = 0; k < TB; ++k) (void)bp_step<ZO>(z, f, tile_x(cur, k), acc);
     }
     int e = 0;
-    for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = df2t_step<8>(z, f, In<T>::cvt(x[i]));
-    for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = df2t_step<8>(z, f, In<T>::ext(xl, x[n - 2 - jj]));
+    for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::cvt(x[i]), acc);
+    for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::ext(xl, x[n - 2 - jj]), acc);
+    if (bp_bad<ZO>(acc, z) && s <= last) atomicOr(&buf.bp_flags[s], 1);
     __threadfence();                            // checkpoints + edge: read by this wave and the backward wave
   }
   __syncthreads();
@@ -274,10 +320,11 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 #pragma unroll
         for (int j = 0; j < 8; ++j) cn[j] = ck[(tp * 8 + j) * 64];
         double2 (*ybuf)[64] = yb[gi][it & 1];
+        float dummy = 0.0f;                     // the re-run repeats checked steps: no detector
 #pragma unroll
         for (int k = 0; k < TB; k += 2) {
-          const double y0 = df2t_step<8>(zf, f, tile_x(cur, k));
-          const double y1 = df2t_step<8>(zf, f, tile_x(cur, k + 1));
+          const double y0 = bp_step<ZO>(zf, f, tile_x(cur, k), dummy);
+          const double y1 = bp_step<ZO>(zf, f, tile_x(cur, k + 1), dummy);
           ybuf[k >> 1][lane] = make_double2(y0, y1);
         }
       }
@@ -286,12 +333,13 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
   } else {
     // ---- backward pass: the tail edge, then the tiles out of LDS -------------
     double zb[8];
+    float acc = __builtin_inff();
     if (active) {
       const double ylast = eb[(ne - 1) * 64];
 #pragma unroll
       for (int j = 0; j < 8; ++j) zb[j] = f.zi[j] * ylast;
       for (int e = ne - 1; e >= 0; --e) {
-        const double y = df2t_step<8>(zb, f, eb[e * 64]);
+        const double y = bp_step<ZO>(zb, f, eb[e * 64], acc);
         const int64_t i = i_tail + e;
         if (i < n) fo[(i >> 1) * 64 + (i & 1)] = y;
       }
@@ -305,13 +353,14 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 #pragma unroll
         for (int k = TB / 2 - 1; k >= 0; --k) {
           const double2 yy = ybuf[k][lane];
-          const double y1 = df2t_step<8>(zb, f, yy.y);
-          const double y0 = df2t_step<8>(zb, f, yy.x);
+          const double y1 = bp_step<ZO>(zb, f, yy.y, acc);
+          const double y0 = bp_step<ZO>(zb, f, yy.x, acc);
           *reinterpret_cast<double2*>(fp + k * 64) = make_double2(y0, y1);
         }
       }
       __syncthreads();
     }
+    if (active && bp_bad<ZO>(acc, zb) && s <= last) atomicOr(&buf.bp_flags[s], 1);
   }
 }
 
@@ -785,32 +834,50 @@ static int bp_split() {
   return v;
 }
 
+static int bp_zero_taps(const PskParams& p) {
+  // skip the band-pass's +0.0 odd taps (detector + exact re-run of flagged
+  // groups): AMR_BP_ZO=0 computes every tap instead
+  static const int v = [] { const char* e = getenv("AMR_BP_ZO"); return e && e[0] == '0' ? 0 : 1; }();
+  return v && p.bp_zero_odd;
+}
+
 template <typename T>
-static void launch_bp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+static hipError_t launch_bp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t g = (b.n_streams + 63) / 64;
   if (bp_split()) {
-    if (lane_wpb() >= 2)
-      hipLaunchKernelGGL((k_bp_lane2<T, 2>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
-    else
-      hipLaunchKernelGGL((k_bp_lane2<T, 1>), dim3((unsigned)g), dim3(128), 0, st, b, p, f);
-    return;
+    const bool zo = bp_zero_taps(p);
+    if (zo) {
+      hipError_t e = hipMemsetAsync(b.bp_flags, 0, (size_t)b.n_streams * 4, st);
+      if (e != hipSuccess) return e;
+    }
+    const dim3 grid((unsigned)(lane_wpb() >= 2 ? (g + 1) / 2 : g)), block(lane_wpb() >= 2 ? 256 : 128);
+    if (lane_wpb() >= 2) {
+      if (zo) hipLaunchKernelGGL((k_bp_lane2<T, 2, true>), grid, block, 0, st, b, p, f);
+      else hipLaunchKernelGGL((k_bp_lane2<T, 2, false>), grid, block, 0, st, b, p, f);
+    } else {
+      if (zo) hipLaunchKernelGGL((k_bp_lane2<T, 1, true>), grid, block, 0, st, b, p, f);
+      else hipLaunchKernelGGL((k_bp_lane2<T, 1, false>), grid, block, 0, st, b, p, f);
+    }
+    if (zo)   // every tap for the groups holding a flagged stream (the others exit at once)
+      hipLaunchKernelGGL((k_bp_lane<T, 4, true>), dim3((unsigned)((g + 3) / 4)), dim3(256), 0, st, b, p, f);
+    return hipGetLastError();
   }
   switch (lane_wpb()) {
     case 4: hipLaunchKernelGGL((k_bp_lane<T, 4>), dim3((unsigned)((g + 3) / 4)), dim3(256), 0, st, b, p, f); break;
     case 2: hipLaunchKernelGGL((k_bp_lane<T, 2>), dim3((unsigned)((g + 1) / 2)), dim3(128), 0, st, b, p, f); break;
     default: hipLaunchKernelGGL((k_bp_lane<T, 1>), dim3((unsigned)g), dim3(64), 0, st, b, p, f);
   }
+  return hipGetLastError();
 }
 
 hipError_t launch_psk_bandpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   if (f.nt != 9) return hipErrorInvalidValue;
   switch (b.dtype) {
-    case kF32: launch_bp<float>(b, p, f, st); break;
-    case kF64: launch_bp<double>(b, p, f, st); break;
-    case kI16: launch_bp<int16_t>(b, p, f, st); break;
+    case kF32: return launch_bp<float>(b, p, f, st);
+    case kF64: return launch_bp<double>(b, p, f, st);
+    case kI16: return launch_bp<int16_t>(b, p, f, st);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 static int lp_split() {

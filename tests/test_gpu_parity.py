@@ -342,7 +342,8 @@ def test_lane_layout_forced_on_every_case(tmp_path):
     for every call: every golden PSK case (incl. silence / -0.0 / denormal /
     NaN / inf streams through the detector and K3x), f64 and int16 inputs,
     BPSK, sps 5 / 10 / 20 and a generic sps, streams shorter than one tile,
-    a ragged batch (B not a multiple of 64) and the full 4096 x 96000 batch,
+    a ragged batch (B not a multiple of 64), streams that trip the band-pass
+    zero-tap detector among ordinary ones, and the full 4096 x 96000 batch,
     against the reference / the oracle.  One subprocess (AMR_PSK_LANE is read
     once per process)."""
     import subprocess
@@ -379,6 +380,16 @@ bad += check("qpsk", synth.dpsk8_batch(65, 24000, 19200, seed=7, distinct=5), 19
 bad += check("qpsk", synth.qpsk_batch(33, 30001, 4800, seed=8, distinct=5), 4800, "sps20")
 bad += check("qpsk", synth.qpsk_batch(17, 30001, 2400, seed=9, distinct=5), 2400, "sps40")
 bad += check("qpsk", synth.qpsk_batch(5, 39, 9600, seed=10, distinct=5), 9600, "n39")
+# band-pass zero-tap detector: leading silence, -0.0 runs, a late inf and a
+# NaN inside groups of ordinary streams (their groups re-run with every tap)
+x = synth.qpsk_batch(130, 20000, 9600, seed=11, distinct=9)
+x[3, :5000] = 0.0
+x[64, :777] = -0.0
+x[65, 19999] = np.inf
+x[129, 12345] = np.nan
+x[100, 4000:4100] = 0.0
+x[101] = 0.0
+bad += check("qpsk", x, 9600, "bpzo")
 bad += check("qpsk", synth.qpsk_batch(4096, 96000, 9600, seed=4096, distinct=8), 9600, "b4096")
 print("BAD", bad[:20], len(bad))
 sys.exit(1 if bad else 0)
@@ -386,3 +397,46 @@ sys.exit(1 if bad else 0)
     env = dict(os.environ, AMR_PSK_LANE="1")
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_async_host_entry_stream_of_batches():
+    """amr_psk_demod_host_async / amr_fsk_demod_host_async on two plans in
+    turn (uploads of one batch overlapping the other's demod), page-locked
+    and pageable inputs, a pitched output: every batch == the oracle."""
+    import _amr
+    import _fsk
+    import synth
+    from oracle import oracle
+    L = _amr.lib()
+    B, N = 48, 24000
+    xs = [synth.qpsk_batch(B, N, 9600, seed=40 + k, distinct=6) for k in range(4)]
+    plans = [_amr.PskPlan("qpsk", N, 9600, max_streams=B) for _ in range(2)]
+    cap = plans[0].out_cap
+    outs = [(np.zeros((B, cap + 3), np.uint8), np.zeros(B, np.int64), np.zeros(B, np.int64)) for _ in range(4)]
+    _amr.check(L.amr_host_register(_amr.ptr(xs[0]), xs[0].nbytes))
+    try:
+        for k in range(4):
+            pl = plans[k % 2]
+            if k >= 2:
+                _amr.check(L.amr_psk_plan_synchronize(pl.handle))
+            o, ln, sy = outs[k]
+            _amr.check(L.amr_psk_demod_host_async(pl.handle, _amr.ptr(xs[k]), _amr.DTYPE_F32, B, N, _amr.ptr(o),
+                                                  cap + 3, _amr.ptr(ln), _amr.ptr(sy)))
+        for pl in plans:
+            _amr.check(L.amr_psk_plan_synchronize(pl.handle))
+    finally:
+        L.amr_host_unregister(_amr.ptr(xs[0]))
+    for k in range(4):
+        want, wsync = oracle.psk_demod_batch("qpsk", xs[k], 9600)
+        o, ln, sy = outs[k]
+        assert [o[i, :ln[i]].tobytes() for i in range(B)] == want
+        assert np.array_equal(sy, wsync)
+    xf = synth.fsk_batch(8, N, 9600, 12000.0, 24000.0, seed=3, distinct=4, noise=0.2)
+    pf = _fsk.FskPlan(N, 9600, 12000.0, 24000.0, max_streams=8)
+    o = np.zeros((8, pf.out_cap), np.uint8)
+    ln = np.zeros(8, np.int64)
+    sy = np.zeros(8, np.int64)
+    _amr.check(L.amr_fsk_demod_host_async(pf.handle, _amr.ptr(xf), _amr.DTYPE_F32, 8, N, _amr.ptr(o), pf.out_cap,
+                                          _amr.ptr(ln), _amr.ptr(sy)))
+    _amr.check(L.amr_fsk_plan_synchronize(pf.handle))
+    assert [o[i, :ln[i]].tobytes() for i in range(8)] == [oracle.fsk_demodulate(r, 9600, 12000.0, 24000.0) for r in xf]
