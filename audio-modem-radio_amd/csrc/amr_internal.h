@@ -40,6 +40,8 @@ struct PskParams {
   int pad1, pad2;
   int kind;               // PskKind
   int bp_zero_odd;        // 1: b[1], b[3], ... are all +0.0 (band-pass symmetry)
+  int bp_sym;             // 1: 9 taps with b[8] == b[0] and b[6] == b[2] bit for bit
+  int lp_sym;             // 1: 5 taps with b[4] == b[0] and b[3] == b[1] bit for bit
 };
 
 // Pointers of one batch launch (device memory).

@@ -147,6 +147,12 @@ int device_crc(int dev, const uint32_t** table, const uint32_t** x2n) {
 }
 
 bool is_pos_zero(double v) { return v == 0.0 && !std::signbit(v); }
+static bool same_bits(double a, double b) {
+  uint64_t u, v;
+  std::memcpy(&u, &a, 8);
+  std::memcpy(&v, &b, 8);
+  return u == v;
+}
 
 // Per-device staging of the synchronous host entries that take no plan
 // (amr_fec_decode_host, amr_frame_parse_host): grow-only buffers kept for the
@@ -389,6 +395,10 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   bool zodd = true;
   for (int i = 1; i < bp_nt; i += 2) zodd = zodd && is_pos_zero(bp_b[i]);
   p.bp_zero_odd = zodd ? 1 : 0;
+  // butter()'s numerators are k * poly(zeros at +-1): palindromic, and the
+  // kernels then form each distinct product x * b[i] once (psk_lane_kernels.hip)
+  p.bp_sym = bp_nt == 9 && same_bits(bp_b[8], bp_b[0]) && same_bits(bp_b[6], bp_b[2]) ? 1 : 0;
+  p.lp_sym = lp_nt == 5 && same_bits(lp_b[4], lp_b[0]) && same_bits(lp_b[3], lp_b[1]) ? 1 : 0;
   pl->bp.nt = bp_nt;
   pl->lp.nt = lp_nt;
   for (int i = 0; i < bp_nt; ++i) { pl->bp.b[i] = bp_b[i]; pl->bp.a[i] = bp_a[i]; }
@@ -561,7 +571,10 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
   const int64_t live = B * (pl->inflight > 1 ? pl->inflight : 1);
-  const bool lane = pl->bp.nt == 9 && (lane_force >= 0 ? lane_force == 1 : live >= kLaneMinLiveStreams);
+  // the lane kernels are written for butter(4) band-pass / low-pass
+  // coefficient shapes: 9 taps and a palindromic 5-tap low-pass
+  const bool lane_ok = pl->bp.nt == 9 && pl->p.lp_sym;
+  const bool lane = lane_ok && (lane_force >= 0 ? lane_force == 1 : live >= kLaneMinLiveStreams);
   pl->last_layout = lane ? AMR_LAYOUT_LANE : AMR_LAYOUT_ROW;
   if (!lane && pl->p.n_sym >= 2)
     if (int rc = ensure_row_buffers(pl)) return rc;

@@ -67,18 +67,35 @@ __device__ __forceinline__ double df2t_step(double (&z)[NS], const Iir& f, doubl
 // |z| >= 2^-1015, never a zero; a stream that fails, or ends non-finite, is
 // flagged and its group re-run with every tap (k_bp_lane in exact mode).
 // 26 instead of 34 FP64 per step, + 2 v_min3_f32.
+// The numerator is also palindromic (b8 == b0, b6 == b2 bit for bit,
+// PskParams::bp_sym), so x*b8 IS x*b0 and x*b6 IS x*b2: 3 products, not 5.
+// 23 FP64 per step instead of 34.
 __device__ __forceinline__ double df2t_step_zo(double (&z)[8], const Iir& f, double x, float& acc) {
   acc = tiny_min3(acc, z[1], z[3]);
   acc = tiny_min3(acc, z[5], z[7]);
-  const double y = z[0] + f.b[0] * x;
+  const double p0 = f.b[0] * x, p2 = x * f.b[2], p4 = x * f.b[4];
+  const double y = z[0] + p0;
   z[0] = z[1] - y * f.a[1];
-  z[1] = (z[2] + x * f.b[2]) - y * f.a[2];
+  z[1] = (z[2] + p2) - y * f.a[2];
   z[2] = z[3] - y * f.a[3];
-  z[3] = (z[4] + x * f.b[4]) - y * f.a[4];
+  z[3] = (z[4] + p4) - y * f.a[4];
   z[4] = z[5] - y * f.a[5];
-  z[5] = (z[6] + x * f.b[6]) - y * f.a[6];
+  z[5] = (z[6] + p2) - y * f.a[6];
   z[6] = z[7] - y * f.a[7];
-  z[7] = x * f.b[8] - y * f.a[8];
+  z[7] = p0 - y * f.a[8];
+  return y;
+}
+
+// The low-pass numerator k*[1,4,6,4,1] is palindromic (PskParams::lp_sym,
+// required for the lane layout): x*b4 IS x*b0 and x*b3 IS x*b1.  15 FP64
+// per step instead of 17, each result identical to df2t_step<4>.
+__device__ __forceinline__ double lp_step(double (&z)[4], const Iir& f, double x) {
+  const double p0 = f.b[0] * x, p1 = x * f.b[1], p2 = x * f.b[2];
+  const double y = z[0] + p0;
+  z[0] = (z[1] + p1) - y * f.a[1];
+  z[1] = (z[2] + p2) - y * f.a[2];
+  z[2] = (z[3] + p1) - y * f.a[3];
+  z[3] = p0 - y * f.a[4];
   return y;
 }
 
@@ -384,11 +401,21 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 // to arrive); the tile's LO multipliers arrive by one 8-B load per lane a tile
 // ahead and are parked in a per-wave LDS double buffer, read back by
 // broadcast ds_read_b128.
+// (Tried: 3 waves per SIMD through a half-tile ring (CH 4), and a 20-sample
+// tile at 4 waves per SIMD: both slower in flight and alone -- the loads
+// need the whole tile of lead.)
+#ifndef AMR_LP_WAVES
+#define AMR_LP_WAVES 1
+#endif
+#ifndef AMR_LP_CH
+#define AMR_LP_CH 8
+#endif
 template <int SPS, int FM, int WPB>
-__global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
+__global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TL = kLpT;
-  constexpr int CH = 8;                         // samples per f chunk (4 x 16 B per lane)
+  constexpr int CH = AMR_LP_CH;                 // samples per f chunk (CH / 2 x 16 B per lane)
   constexpr int NCH = TL / CH, HC = CH / 2;
+  constexpr int R = NCH % 2 == 0 ? NCH / 2 : NCH;   // ring slots: chunk q lands R chunks ahead of its use
   static_assert(TL % CH == 0 && TL <= 64, "tile = whole chunks; one LO value per lane");
   static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
   __shared__ __attribute__((aligned(16))) double lo_lds[WPB][2][TL];
@@ -455,21 +482,21 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
   for (int j = 0; j < 4; ++j) z[j] = f.zi[j] * e0;
   for (int jj = 0; jj < pad; ++jj) {
     const double e = 2.0 * x0 - Xm(pad - jj);
-    const double y = df2t_step<4>(z, f, e);
+    const double y = lp_step(z, f, e);
     acc = tiny_min3(acc, e, y);
     eh[jj * 64] = y;
   }
   const int64_t nh = n < TL ? n : TL;           // tile 0 (holds bb[0]): edge buffer, not recomputed
   for (int64_t i = 0; i < nh; ++i) {
     const double e = i == 0 ? x0 : Xm(i);
-    const double y = df2t_step<4>(z, f, e);
+    const double y = lp_step(z, f, e);
     acc = tiny_min3(acc, i == 0 ? y : e, y);
     eh[(pad + i) * 64] = y;
   }
-  double2 ring[NCH][HC];
+  double2 ring[R][HC];
   if (nt > 1) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) load_chunk(1, c, ring[c]);
+    for (int c = 0; c < R; ++c) load_chunk(1, c, ring[c]);
     put_lo(1, load_lo(1));
   }
   for (int64_t t = 1; t < nt; ++t) {
@@ -481,14 +508,15 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
     for (int c = 0; c < NCH; ++c) {
       double2 fv[HC];
 #pragma unroll
-      for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
-      load_chunk(tn, c, ring[c]);
+      for (int k = 0; k < HC; ++k) fv[k] = ring[c % R][k];
+      if (c + R < NCH) load_chunk(t, c + R, ring[c % R]);
+      else load_chunk(tn, c + R - NCH, ring[c % R]);
       double e[CH];
       chunk_e(t, c, fv, e);
 #pragma unroll
       for (int k = 0; k < CH; k += 2) {
-        const double y0 = df2t_step<4>(z, f, e[k]);
-        const double y1 = df2t_step<4>(z, f, e[k + 1]);
+        const double y0 = lp_step(z, f, e[k]);
+        const double y1 = lp_step(z, f, e[k + 1]);
         acc = tiny_min3(acc, e[k], e[k + 1]);
         acc = tiny_min3(acc, y0, y1);
       }
@@ -499,14 +527,14 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
   int ne = 0;
   for (int64_t i = i_tail; i < n; ++i) {
     const double e = Xm(i);
-    const double y = df2t_step<4>(z, f, e);
+    const double y = lp_step(z, f, e);
     acc = tiny_min3(acc, e, y);
     et[(ne++) * 64] = y;
   }
   double ylast = 0.0;
   for (int jj = 0; jj < pad; ++jj) {
     const double e = 2.0 * xl - Xm(n - 2 - jj);
-    ylast = df2t_step<4>(z, f, e);
+    ylast = lp_step(z, f, e);
     acc = tiny_min3(acc, e, ylast);
     et[(ne++) * 64] = ylast;
   }
@@ -526,7 +554,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
 #pragma unroll
   for (int j = 0; j < 4; ++j) zb[j] = f.zi[j] * ylast;
   for (int e = ne - 1; e >= 0; --e) {
-    const double y = df2t_step<4>(zb, f, et[e * 64]);
+    const double y = lp_step(zb, f, et[e * 64]);
     accb = tiny_min3(accb, y, y);
     const int64_t i = i_tail + e;
     if (i < n) sym_out(i, y);
@@ -537,7 +565,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
 #pragma unroll
     for (int j = 0; j < 4; ++j) cn[j] = ck[((nt - 1) * 4 + j) * 64];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) load_chunk(nt - 1, c, ring[c]);
+    for (int c = 0; c < R; ++c) load_chunk(nt - 1, c, ring[c]);
     put_lo(nt - 1, load_lo(nt - 1));
     for (int64_t t = nt - 1; t >= 1; --t) {
       double zf[4];
@@ -552,17 +580,18 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
       for (int c = 0; c < NCH; ++c) {
         double2 fv[HC];
 #pragma unroll
-        for (int k = 0; k < HC; ++k) fv[k] = ring[c][k];
-        load_chunk(tp, c, ring[c]);
+        for (int k = 0; k < HC; ++k) fv[k] = ring[c % R][k];
+        if (c + R < NCH) load_chunk(t, c + R, ring[c % R]);
+        else load_chunk(tp, c + R - NCH, ring[c % R]);
         double e[CH];
         chunk_e(t, c, fv, e);
 #pragma unroll
-        for (int k = 0; k < CH; ++k) yt[c * CH + k] = df2t_step<4>(zf, f, e[k]);
+        for (int k = 0; k < CH; ++k) yt[c * CH + k] = lp_step(zf, f, e[k]);
       }
 #pragma unroll
       for (int k = TL - 1; k >= 1; k -= 2) {
-        const double y1 = df2t_step<4>(zb, f, yt[k]);
-        const double y0 = df2t_step<4>(zb, f, yt[k - 1]);
+        const double y1 = lp_step(zb, f, yt[k]);
+        const double y0 = lp_step(zb, f, yt[k - 1]);
         accb = tiny_min3(accb, y1, y0);
         if constexpr (SPS > 0) {
           if (k % SPS == FM) symp[(t * (TL / SPS) + (k - FM) / SPS - q0) * 64] = y1;
@@ -576,7 +605,7 @@ __global__ __launch_bounds__(64 * WPB) void k_lp_lane(PskBuffers buf, PskParams 
     }
   }
   for (int e = pad + (int)nh - 1; e >= 0; --e) {
-    const double y = df2t_step<4>(zb, f, eh[e * 64]);
+    const double y = lp_step(zb, f, eh[e * 64]);
     accb = tiny_min3(accb, y, y);
     const int64_t i = e - pad;
     if (i >= 0) sym_out(i, y);
@@ -662,13 +691,13 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
     for (int j = 0; j < 4; ++j) z[j] = f.zi[j] * e0;
     for (int jj = 0; jj < pad; ++jj) {
       const double e = 2.0 * x0 - Xm(pad - jj);
-      const double y = df2t_step<4>(z, f, e);
+      const double y = lp_step(z, f, e);
       acc = tiny_min3(acc, e, y);
       eh[jj * 64] = y;
     }
     for (int64_t i = 0; i < nh; ++i) {
       const double e = i == 0 ? x0 : Xm(i);
-      const double y = df2t_step<4>(z, f, e);
+      const double y = lp_step(z, f, e);
       acc = tiny_min3(acc, i == 0 ? y : e, y);
       eh[(pad + i) * 64] = y;
     }
@@ -693,8 +722,8 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
         chunk_e(t, c, fv, e);
 #pragma unroll
         for (int k = 0; k < CH; k += 2) {
-          const double y0 = df2t_step<4>(z, f, e[k]);
-          const double y1 = df2t_step<4>(z, f, e[k + 1]);
+          const double y0 = lp_step(z, f, e[k]);
+          const double y1 = lp_step(z, f, e[k + 1]);
           acc = tiny_min3(acc, e[k], e[k + 1]);
           acc = tiny_min3(acc, y0, y1);
         }
@@ -704,13 +733,13 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
     int ee = 0;
     for (int64_t i = i_tail; i < n; ++i) {
       const double e = Xm(i);
-      const double y = df2t_step<4>(z, f, e);
+      const double y = lp_step(z, f, e);
       acc = tiny_min3(acc, e, y);
       et[(ee++) * 64] = y;
     }
     for (int jj = 0; jj < pad; ++jj) {
       const double e = 2.0 * xl - Xm(n - 2 - jj);
-      const double y = df2t_step<4>(z, f, e);
+      const double y = lp_step(z, f, e);
       acc = tiny_min3(acc, e, y);
       et[(ee++) * 64] = y;
     }
@@ -751,8 +780,8 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
           chunk_e(t, c, fv, e);
 #pragma unroll
           for (int k = 0; k < CH; k += 2) {
-            const double y0 = df2t_step<4>(zf, f, e[k]);
-            const double y1 = df2t_step<4>(zf, f, e[k + 1]);
+            const double y0 = lp_step(zf, f, e[k]);
+            const double y1 = lp_step(zf, f, e[k + 1]);
             ybuf[(c * CH + k) >> 1][lane] = make_double2(y0, y1);
           }
         }
@@ -773,7 +802,7 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
 #pragma unroll
     for (int j = 0; j < 4; ++j) zb[j] = f.zi[j] * ylast;
     for (int e = ne - 1; e >= 0; --e) {
-      const double y = df2t_step<4>(zb, f, et[e * 64]);
+      const double y = lp_step(zb, f, et[e * 64]);
       accb = tiny_min3(accb, y, y);
       const int64_t i = i_tail + e;
       if (i < n) sym_out(i, y);
@@ -788,8 +817,8 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
 #pragma unroll
       for (int k = TL - 1; k >= 1; k -= 2) {
         const double2 yy = ybuf[k >> 1][lane];
-        const double y1 = df2t_step<4>(zb, f, yy.y);
-        const double y0 = df2t_step<4>(zb, f, yy.x);
+        const double y1 = lp_step(zb, f, yy.y);
+        const double y0 = lp_step(zb, f, yy.x);
         accb = tiny_min3(accb, y1, y0);
         if constexpr (SPS > 0) {
           if (k % SPS == FM) symp[(t * (TL / SPS) + (k - FM) / SPS - q0) * 64] = y1;
@@ -802,7 +831,7 @@ __global__ __launch_bounds__(256) void k_lp_lane2(PskBuffers buf, PskParams p, I
       __syncthreads();
     }
     for (int e = pad + (int)nh - 1; e >= 0; --e) {
-      const double y = df2t_step<4>(zb, f, eh[e * 64]);
+      const double y = lp_step(zb, f, eh[e * 64]);
       accb = tiny_min3(accb, y, y);
       const int64_t i = e - pad;
       if (i >= 0) sym_out(i, y);
@@ -838,7 +867,7 @@ static int bp_zero_taps(const PskParams& p) {
   // skip the band-pass's +0.0 odd taps (detector + exact re-run of flagged
   // groups): AMR_BP_ZO=0 computes every tap instead
   static const int v = [] { const char* e = getenv("AMR_BP_ZO"); return e && e[0] == '0' ? 0 : 1; }();
-  return v && p.bp_zero_odd;
+  return v && p.bp_zero_odd && p.bp_sym;
 }
 
 template <typename T>

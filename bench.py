@@ -484,7 +484,7 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
     ht = min(hts[1:])
     res["one_batch"] = {"ms_per_batch": round(ht * 1e3, 2), "value": round(B * sym_per_stream / ht / 1e6, 3),
                         "what": "amr_%s_demod_host from pageable host float32 (H2D + demod + D2H)"
-                                % ("fsk" if fsk else "psk"), "bytes_equal_device_path": same(h_out, h_len)}
+                                % ("fsk" if fsk else "psk"), "bytes_equal": {"device_path": same(h_out, h_len)}}
     del plan
     gc.collect()
     n_pl, n_batches = (2, 4) if fsk else (3, 6)
@@ -494,15 +494,14 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
             pl.set_inflight(n_pl)
     # the capture buffer and the per-plan outputs in page-locked memory
     # (amr_host_alloc), as a receiver would allocate them once
-    pin = _amr.PinnedArray(xh.shape, np.float32)
-    pin.array[:] = xh
     pouts = [(_amr.PinnedArray((B, cap), np.uint8), _amr.PinnedArray((B,), np.int64), _amr.PinnedArray((B,), np.int64))
              for _ in range(n_pl)]
     outs = [tuple(a.array for a in t) for t in pouts]
-    try:
+
+    def stream(src, dtype):
         for k in range(n_pl):                                       # warm every plan once
             o, ln, sy = outs[k]
-            _amr.check(async_fn(plans[k].handle, _amr.ptr(pin.array), _amr.DTYPE_F32, B, N, _amr.ptr(o), cap,
+            _amr.check(async_fn(plans[k].handle, _amr.ptr(src), dtype, B, N, _amr.ptr(o), cap,
                                 _amr.ptr(ln), _amr.ptr(sy)))
         for pl in plans:
             _amr.check(sync_fn(pl.handle))
@@ -512,22 +511,45 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
             if k >= n_pl:
                 _amr.check(sync_fn(pl.handle))                      # its previous batch's bytes are read
             o, ln, sy = outs[k % n_pl]
-            _amr.check(async_fn(pl.handle, _amr.ptr(pin.array), _amr.DTYPE_F32, B, N, _amr.ptr(o), cap,
+            _amr.check(async_fn(pl.handle, _amr.ptr(src), dtype, B, N, _amr.ptr(o), cap,
                                 _amr.ptr(ln), _amr.ptr(sy)))
         for pl in plans:
             _amr.check(sync_fn(pl.handle))
-        dt = (time.perf_counter() - t1) / n_batches
-        res["stream_of_batches"] = {
-            "ms_per_batch": round(dt * 1e3, 2), "value": round(B * sym_per_stream / dt / 1e6, 3),
-            "h2d_gbs": round(xh.nbytes / dt / 1e9, 1),
-            "what": f"amr_{'fsk' if fsk else 'psk'}_demod_host_async on {n_pl} plans in turn, {n_batches} batches "
-                    "from a page-locked capture buffer (amr_host_alloc): uploads overlap demods",
-            "bytes_equal_device_path": all(same(o, ln) for o, ln, _ in outs)}
+        return (time.perf_counter() - t1) / n_batches
+
+    def entry(dt, nbytes, what, equal):
+        return {"ms_per_batch": round(dt * 1e3, 2), "value": round(B * sym_per_stream / dt / 1e6, 3),
+                "h2d_gbs": round(nbytes / dt / 1e9, 1), "what": what, "bytes_equal": equal}
+
+    try:
+        pin = _amr.PinnedArray(xh.shape, np.float32)
+        pin.array[:] = xh
+        dt = stream(pin.array, _amr.DTYPE_F32)
+        res["stream_of_batches"] = entry(
+            dt, xh.nbytes, f"amr_{'fsk' if fsk else 'psk'}_demod_host_async on {n_pl} plans in turn, {n_batches} "
+            "float32 batches from a page-locked capture buffer (amr_host_alloc): uploads overlap demods",
+            {"device_path": all(same(o, ln) for o, ln, _ in outs)})
+        pin.close()
+        # the same capture as 16-bit PCM (a WAV file's samples, modem.py's
+        # read path): half the PCIe bytes; checked against the synchronous
+        # host entry on the same int16 buffer
+        pin16 = _amr.PinnedArray(xh.shape, np.int16)
+        np.multiply(np.clip(xh, -3.9, 3.9), 8192.0, out=pin16.array, casting="unsafe")
+        dt = stream(pin16.array, _amr.DTYPE_I16)
+        ref = mk()
+        _amr.check(host_fn(ref.handle, _amr.ptr(pin16.array), _amr.DTYPE_I16, B, N, _amr.ptr(h_out), cap,
+                           _amr.ptr(h_len), _amr.ptr(h_sync)))
+        del ref
+        eq16 = all(np.array_equal(ln, h_len) and all(o[i, :ln[i]].tobytes() == h_out[i, :ln[i]].tobytes()
+                                                     for i in range(B)) for o, ln, _ in outs)
+        res["stream_of_batches_pcm16"] = entry(
+            dt, pin16.array.nbytes, f"as stream_of_batches, the capture as int16 PCM ({pin16.array.nbytes / 1e9:.3f} GB "
+            "per batch)", {"sync_host_entry": eq16})
+        pin16.close()
     finally:
         for t in pouts:
             for a in t:
                 a.close()
-        pin.close()
     res["value"] = res["stream_of_batches"]["value"]
     return res
 

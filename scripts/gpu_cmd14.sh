@@ -1,0 +1,6 @@
+set -o pipefail
+for w in qpsk9600 ofdm8 psk8fec fsk9600; do
+  WORKLOAD=$w TAG=r02 bash scripts/profile.sh > gpurun_out/prof14_$w.log 2>&1 || exit 1
+done
+mkdir -p gpurun_out/profiles_r02 && cp profiles/r02_* gpurun_out/profiles_r02/
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || exit 1

@@ -31,14 +31,14 @@ def find(d, pat):
     return m[0] if m else None
 
 
-KERNELS = ["k_bp_lane", "k_lp_lane", "k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
+KERNELS = ["k_bp_lane2", "k_lp_lane2", "k_bp_lane", "k_lp_lane", "k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
            "k_lowpass_bwd_q", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
            "k_sync_pack", "k_fec_decode",
            "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
-    "qpsk9600": {"bandpass": ["k_bp_lane", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass"],
-                 "lowpass_fwd": ["k_lp_lane", "k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
+    "qpsk9600": {"bandpass": ["k_bp_lane2", "k_bp_lane", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass"],
+                 "lowpass_fwd": ["k_lp_lane2", "k_lp_lane", "k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
                  "lowpass_exact": ["k_lowpass_exact"], "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
     "ofdm8": None, "psk8fec": None,
     "fsk9600": {"bandpass": ["k_fsk_bandpass"], "hilbert": ["k_fft_cols", "k_fft_mid", "k_fft_rows"],
@@ -66,9 +66,11 @@ def main():
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{tag}_{workload}_kernel_stats.csv"))
     res = {}
-    for r in rows(stats):
-        res.setdefault(short(r["Name"]), {})["avg_ns"] = float(r["AverageNs"])
-        res[short(r["Name"])]["calls"] = int(r["Calls"])
+    for r in rows(stats):     # template instances of one kernel fold into one row
+        d = res.setdefault(short(r["Name"]), {"calls": 0, "total_ns": 0.0})
+        d["calls"] += int(r["Calls"])
+        d["total_ns"] += float(r["TotalDurationNs"])
+        d["avg_ns"] = d["total_ns"] / d["calls"]
     # the bench's timed steps are the last `steps` dispatches of each kernel
     # (warmup dispatches run one batch at a time, the timed ones in flight)
     trace = find(os.path.join(out, "trace"), "*kernel_trace.csv")
@@ -90,6 +92,12 @@ def main():
             v.sort()
             tail = [d for _, d in v[-steps:]]
             res.setdefault(k, {})["avg_ns_timed_steps"] = sum(tail) / len(tail)
+    bench = {}
+    if os.path.exists(bj):
+        with open(bj) as f:
+            for line in f:
+                if line.startswith("{"):
+                    bench = json.loads(line)
     for which, counter, scale in (("fetch", "FETCH_SIZE", 2.0), ("write", "WRITE_SIZE", 1.0)):
         f = find(os.path.join(out, which), "*counter_collection.csv")
         if not f:
@@ -111,6 +119,8 @@ def main():
         if not got:
             continue
         d = {"kernels": [k for k in ks if k in res], "avg_ns": sum(g.get("avg_ns", 0) for g in got)}
+        if all("avg_ns_timed_steps" in g for g in got):
+            d["avg_ns_timed_steps"] = sum(g["avg_ns_timed_steps"] for g in got)
         for key in ("fetch_bytes_per_dispatch", "write_bytes_per_dispatch", "hbm_bytes_per_dispatch"):
             if all(key in g for g in got):
                 d[key.replace("_per_dispatch", "_per_launch")] = sum(g[key] for g in got)
@@ -124,8 +134,12 @@ def main():
             allres = {}
     allres["source"] = "rocprofv3 kernel-trace --stats + separate --pmc FETCH_SIZE / WRITE_SIZE passes"
     allres["fetch_correction"] = "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads)"
+    rl = bench.get("roofline", {})
     allres[workload] = {"kernels": res, "slots": slots, "inflight": cfg.get("batches_in_flight"),
-                        "layout": cfg.get("kernel_layout")}
+                        "layout": cfg.get("kernel_layout"), "steps": steps,
+                        "bench": {"dominant_slot": rl.get("kernel"), "alg_bytes_per_launch": rl.get("alg_bytes_per_launch"),
+                                  "kernel_ms_hip_events": rl.get("kernel_ms_used"), "ms_per_step": bench.get("ms_per_step"),
+                                  "value": bench.get("value"), "unit": bench.get("unit")}}
     with open(pmc_path, "w") as f:
         json.dump(allres, f, indent=1)
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
@@ -141,6 +155,25 @@ def main():
                         f"{(ts / 1e6) if ts else float('nan'):.3f} | "
                         f"{v.get('fetch_bytes_per_dispatch', 0) / 1e6:.1f} | "
                         f"{v.get('write_bytes_per_dispatch', 0) / 1e6:.1f} |\n")
+            b = r.get("bench", {})
+            sl = r.get("slots", {}).get(b.get("dominant_slot") or "", {})
+            if b.get("alg_bytes_per_launch") and sl.get("avg_ns_timed_steps"):
+                ns = sl["avg_ns_timed_steps"]
+                ach = b["alg_bytes_per_launch"] / ns
+                f.write(f"\nRoofline, reproduced from this profile ({r.get('steps')} timed steps, "
+                        f"{r.get('inflight')} batches in flight, layout {r.get('layout')}): dominant slot "
+                        f"`{b['dominant_slot']}` = {' + '.join(sl['kernels'])}; algorithmic bytes per launch "
+                        f"{b['alg_bytes_per_launch']:,} (SURVEY 8(d)) / rocprofv3 average {ns / 1e6:.3f} ms "
+                        f"= {ach:.2f} GB/s = {ach / 8000:.5f} of 8000 GB/s.  The bench's HIP events over the "
+                        f"same run: {b.get('kernel_ms_hip_events')} ms; step {b.get('ms_per_step')} ms, "
+                        f"{b.get('value')} {b.get('unit')}.\n")
+                if sl.get("hbm_bytes_per_launch"):
+                    f.write(f"HBM traffic of that slot per launch (FETCH_SIZE x2 + WRITE_SIZE): "
+                            f"{sl['hbm_bytes_per_launch'] / 1e6:.1f} MB = "
+                            f"{sl['hbm_bytes_per_launch'] / b['alg_bytes_per_launch']:.2f} x the algorithmic bytes.\n")
+            tot = sum(v.get("hbm_bytes_per_dispatch", 0) * 1 for v in r["kernels"].values())
+            if tot:
+                f.write(f"All kernels, HBM bytes per step (one dispatch each): {tot / 1e9:.2f} GB.\n")
     print(json.dumps(res, indent=1))
 
 
