@@ -370,7 +370,9 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                 pm = json.load(f).get(name, {})
             if pm.get("inflight") == P and pm.get("layout", layout) == layout:
                 traffic = pm.get("slots", {}).get(dom, {}).get("hbm_bytes_per_launch")
-                step_traffic = sum(v.get("hbm_bytes_per_dispatch", 0) for v in pm.get("kernels", {}).values()) or None
+                # the step's kernels only (not the input synthesis before the timed region)
+                step_traffic = sum(v.get("hbm_bytes_per_dispatch", 0) for k, v in pm.get("kernels", {}).items()
+                                   if "synth" not in k) or None
         ach = alg_bytes / (kavg[dom] / 1e3) / 1e9
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -171,9 +171,10 @@ def main():
                     f.write(f"HBM traffic of that slot per launch (FETCH_SIZE x2 + WRITE_SIZE): "
                             f"{sl['hbm_bytes_per_launch'] / 1e6:.1f} MB = "
                             f"{sl['hbm_bytes_per_launch'] / b['alg_bytes_per_launch']:.2f} x the algorithmic bytes.\n")
-            tot = sum(v.get("hbm_bytes_per_dispatch", 0) * 1 for v in r["kernels"].values())
+            tot = sum(v.get("hbm_bytes_per_dispatch", 0) for k, v in r["kernels"].items() if "synth" not in k)
             if tot:
-                f.write(f"All kernels, HBM bytes per step (one dispatch each): {tot / 1e9:.2f} GB.\n")
+                f.write(f"The step's kernels (one dispatch each; input synthesis excluded), HBM bytes per step: "
+                        f"{tot / 1e9:.2f} GB.\n")
     print(json.dumps(res, indent=1))
 
 
