@@ -153,14 +153,17 @@ int amr_psk_demod_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_s
 /* Same contract, all pointers device pointers; asynchronous on the plan's stream. */
 int amr_psk_demod_device(amr_psk_plan *plan, const void *d_x, int dtype, int64_t n_streams, int64_t x_stride,
                          uint8_t *d_out, int64_t out_stride, int64_t *d_out_len, int64_t *d_sync_idx);
-/* The host entry queued on the plan's stream (upload, demod, download) without
- * waiting; the host buffers must stay untouched until amr_psk_plan_synchronize.
+/* qpsk_demodulate / bpsk_demodulate (modem.py:189-266 / 68-135) for a batch,
+ * as amr_psk_demod_host, queued on the plan's stream (upload, demod, download)
+ * without waiting -- the live-capture loop (filebeep_advanced_v2.py:306-324); the host buffers must stay untouched until amr_psk_plan_synchronize.
  * With two or more plans used in turn, batch k+1's upload overlaps batch k's
  * demod (a stream of batches runs at the PCIe rate).  Page-locked buffers
  * (amr_host_register) make the copies fully asynchronous. */
 int amr_psk_demod_host_async(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                              uint8_t *out, int64_t out_stride, int64_t *out_len, int64_t *sync_idx);
-/* page-locked host memory for capture buffers (hipHostMalloc: the full PCIe
+/* (no reference counterpart: the reference's capture buffers are numpy
+ * arrays, sounddevice's callback at filebeep_advanced_v2.py:306)
+ * page-locked host memory for capture buffers (hipHostMalloc: the full PCIe
  * rate, 57.6 GB/s measured on the MI355X box, against 38 GB/s for a
  * registered pageable buffer) */
 int amr_host_alloc(void **ptr, int64_t bytes);
@@ -217,6 +220,8 @@ int amr_fsk_demod_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_s
                        uint8_t *out, int64_t out_stride, int64_t *out_len, int64_t *sync_idx);
 int amr_fsk_demod_device(amr_fsk_plan *plan, const void *d_x, int dtype, int64_t n_streams, int64_t x_stride,
                          uint8_t *d_out, int64_t out_stride, int64_t *d_out_len, int64_t *d_sync_idx);
+/* fsk_demodulate (modem.py:298-341), queued without waiting: as
+ * amr_psk_demod_host_async */
 int amr_fsk_demod_host_async(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                              uint8_t *out, int64_t out_stride, int64_t *out_len, int64_t *sync_idx);
 /* mark_env, space_env: [n_streams][n_samples] doubles, |hilbert(filtfilt(.))|
