@@ -428,7 +428,7 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
       {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
       // + slack: K2q's prefetch runs up to a few chunks past the end (psk_kernels.hip)
       {(void**)&pl->lo2, (n * 2 + 1024) * (int64_t)sizeof(double)},
-      // s1 doubles as the symbol buffer [2G][S][64] after K1 (sym_index in psk_kernels.hip)
+      // s1 doubles as the symbol buffer [2G][S][64] after the band-pass (psk_common.h sym_index)
       // s1 / s3 sized for the lane layout (checkpoints, symbols, K3x's slots);
       // the row layout's full-length intermediates are allocated on its first
       // call (ensure_row_buffers)
@@ -878,15 +878,13 @@ int amr_psk_slice_host(int kind, const double* sym, int64_t n_streams, int64_t n
   p.n_bits = n_sym >= 2 ? (n_sym - 1) * (kind == AMR_PSK_QPSK ? 2 : 1) : 0;
   p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
   if (n_streams == 0 || p.n_bits == 0) return AMR_OK;
-  // the symbol buffer layout K3q/K3x write: [B/32][S][32][re, im] (sym_index)
-  const int64_t g32 = (n_streams + 31) / 32;
-  std::vector<double> h((size_t)(g32 * n_sym * 64), 0.0);
+  // the symbol buffer layout the low-pass kernels write: [B/64][re, im][S][64] (psk_common.h sym_index)
+  const int64_t g64 = (n_streams + 63) / 64;
+  std::vector<double> h((size_t)(g64 * 2 * n_sym * 64), 0.0);
   for (int64_t s = 0; s < n_streams; ++s)
-    for (int64_t k = 0; k < n_sym; ++k) {
-      const size_t d = ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2;
-      h[d] = sym[(s * n_sym + k) * 2];
-      h[d + 1] = sym[(s * n_sym + k) * 2 + 1];
-    }
+    for (int64_t k = 0; k < n_sym; ++k)
+      for (int c = 0; c < 2; ++c)
+        h[(size_t)(((s >> 6) * 2 + c) * n_sym + k) * 64 + (s & 63)] = sym[(s * n_sym + k) * 2 + c];
   double* d_sym = nullptr;
   uint32_t* d_words = nullptr;
   hipError_t e = hipMalloc(&d_sym, h.size() * 8);

@@ -44,8 +44,12 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector: SR
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 // symbol buffer: [stream][symbol][re, im] doubles
+// symbol samples [B/64][re, im][S][64]: a component's symbol k of 64
+// streams is one 512-B line, written whole by the wave that computes it
+// (the earlier [B/32][S][32][re, im] interleave left each store half a line
+// and cost the lane low-pass ~15 % in flight); symbol k+1 is 64 doubles on.
 __device__ __forceinline__ size_t sym_index(int64_t s, int64_t n_sym, int64_t k, int comp) {
-  return ((size_t)(((s >> 5) * n_sym + k) * 32 + (s & 31))) * 2 + comp;
+  return ((size_t)((s >> 6) * 2 + comp) * (size_t)n_sym + (size_t)k) * 64 + (size_t)(s & 63);
 }
 
 typedef __attribute__((address_space(4))) const double CDouble;   // constant AS: uniform loads -> SMEM

@@ -1015,7 +1015,7 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
   const int64_t S = p.n_sym;
   const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
   double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)blockIdx.x * m2 * kWave + lane;
-  double2* __restrict__ sym2 = reinterpret_cast<double2*>(buf.s1);
+  double* __restrict__ sym = buf.s1;
   for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
     const int64_t s = g * kWave + lane;
     const bool live = s < buf.n_streams && buf.flags[s] != 0;
@@ -1063,7 +1063,10 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
       double o0, o1;
       df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
       if (j - pad == next_n && k >= 0) {
-        if (live) sym2[sym_index(s, S, k, 0) >> 1] = make_double2(o0, o1);
+        if (live) {
+          sym[sym_index(s, S, k, 0)] = o0;
+          sym[sym_index(s, S, k, 1)] = o1;
+        }
         --k;
         next_n -= p.sps;
       }
@@ -1135,8 +1138,8 @@ __global__ __launch_bounds__(64) void k_slice(PskBuffers buf, PskParams p) {
   const int per = qpsk ? 16 : 32;
   const int64_t k0 = j * per;
   const int64_t nd = S - 1;                     // number of diffs
-  const double2* __restrict__ sym2 = reinterpret_cast<const double2*>(buf.s1);
-  auto SYM = [&](int64_t k) { return sym2[sym_index(s, S, k, 0) >> 1]; };
+  const double* __restrict__ sym = buf.s1;
+  auto SYM = [&](int64_t k) { return make_double2(sym[sym_index(s, S, k, 0)], sym[sym_index(s, S, k, 1)]); };
   uint32_t word = 0;
   double2 prev = SYM(k0 < S ? k0 : S - 1);
   for (int u = 0; u < per; ++u) {

@@ -68,6 +68,47 @@ int main() {
         hist[it == per_simd.end() ? 0 : it->second]++;
       }
     }
+    // do the workgroups sharing a CU put their wave i on the same SIMD?
+    std::map<std::tuple<int, int, int>, std::vector<std::vector<int>>> cu_maps;
+    for (int b = 0; b < sh.blocks; ++b) {
+      std::vector<int> m;
+      std::tuple<int, int, int> key;
+      for (int w = 0; w < wpb; ++w) {
+        const uint32_t hw = h[((size_t)b * wpb + w) * 2], xcc = h[((size_t)b * wpb + w) * 2 + 1] & 0xF;
+        key = {(int)xcc, (int)((hw >> 13) & 7), (int)((hw >> 8) & 15)};
+        m.push_back((hw >> 4) & 3);
+      }
+      cu_maps[key].push_back(m);
+    }
+    int aligned = 0, multi = 0;
+    for (auto& [k, v] : cu_maps) {
+      if (v.size() < 2) continue;
+      ++multi;
+      bool all = true;
+      for (size_t j = 1; j < v.size(); ++j) all = all && v[j] == v[0];
+      aligned += all;
+    }
+    std::printf("%-62s CUs with >1 WG: %d, of them wave i on the same SIMD in every WG: %d; first map:", sh.what,
+                multi, aligned);
+    for (int x : cu_maps.begin()->second[0]) std::printf(" %d", x);
+    std::printf("\n");
+    if (wpb == 4) {   // k_bp_lane2's roles (role = wave & 1): SIMDs by busy (role 0) waves in the forward phase
+      std::map<std::tuple<int, int, int, int>, int> busy;
+      for (int b = 0; b < sh.blocks; ++b)
+        for (int w = 0; w < wpb; w += 2) {
+          const uint32_t hw = h[((size_t)b * wpb + w) * 2], xcc = h[((size_t)b * wpb + w) * 2 + 1] & 0xF;
+          busy[{(int)xcc, (int)((hw >> 13) & 7), (int)((hw >> 8) & 15), (int)((hw >> 4) & 3)}]++;
+        }
+      std::map<int, int> bh;
+      for (auto& [cu, n] : per_cu)
+        for (int s2 = 0; s2 < 4; ++s2) {
+          auto it = busy.find({std::get<0>(cu), std::get<1>(cu), std::get<2>(cu), s2});
+          bh[it == busy.end() ? 0 : it->second]++;
+        }
+      std::printf("%-62s forward phase, SIMDs by role-0 waves:", sh.what);
+      for (auto& [k, v] : bh) std::printf(" %d:%d", k, v);
+      std::printf("\n");
+    }
     std::printf("%-62s CUs used %zu; SIMDs by waves held:", sh.what, per_cu.size());
     for (auto& [k, v] : hist) std::printf(" %d:%d", k, v);
     std::printf("; WGs with waves sharing a SIMD %d/%d\n", same, wgs);
