@@ -24,7 +24,7 @@
 //                        forward pass -> s3
 //   K3q k_lowpass_bwd_q  same lanes: low-pass backward pass; the baseband at
 //                        each symbol centre goes to the symbol buffer
-//   K4a k_slice          thread = (stream, output word): differential product,
+//   K4a k_slice          workgroup = 64 streams x 32 words, lane = stream: differential product,
 //                        QPSK/BPSK slicer, bit packing -> words (fully parallel)
 //   K3x k_lowpass_exact  lane = stream: the complex low-pass with scipy's full
 //                        signed-zero semantics, only for streams K2q/K3q flagged
@@ -1129,35 +1129,65 @@ __device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
   return qpsk_dibit_slow(dr, di);
 }
 
-__global__ __launch_bounds__(64) void k_slice(PskBuffers buf, PskParams p) {
-  const int64_t j = blockIdx.x;                 // word index
-  const int64_t s = (int64_t)blockIdx.y * kWave + threadIdx.x;
-  if (s >= buf.n_streams) return;
+// Workgroup = 64 streams x kSliceWords consecutive words: wave w slices words
+// w*8 .. w*8+7 of its 64 streams (lane = stream; symbol loads are whole
+// 512-B lines, the running symbol carried from word to word), the words go
+// through LDS and leave as 128-B row segments -- two streams per store
+// instruction instead of 64 scattered 4-B words (which the L2 wrote back as
+// partial lines: 84 MB of HBM writes for 9.8 MB of words per 4096 streams).
+constexpr int kSliceWords = 32;
+template <int WV>
+__global__ __launch_bounds__(64 * WV) void k_slice(PskBuffers buf, PskParams p) {
+  constexpr int WPW = kSliceWords / WV;         // words per wave
+  __shared__ uint32_t wl[kWave][kSliceWords + 1];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.y * kWave + lane;
+  const bool live = s < buf.n_streams;
   const int64_t S = p.n_sym;
   const bool qpsk = p.kind == kQpsk;
   const int per = qpsk ? 16 : 32;
-  const int64_t k0 = j * per;
   const int64_t nd = S - 1;                     // number of diffs
+  const int64_t jw = (int64_t)blockIdx.x * kSliceWords + wv * WPW;   // this wave's first word
   const double* __restrict__ sym = buf.s1;
   auto SYM = [&](int64_t k) { return make_double2(sym[sym_index(s, S, k, 0)], sym[sym_index(s, S, k, 1)]); };
-  uint32_t word = 0;
-  double2 prev = SYM(k0 < S ? k0 : S - 1);
-  for (int u = 0; u < per; ++u) {
-    const int64_t k = k0 + u;
-    if (k >= nd) break;
-    const double2 nx = SYM(k + 1);
-    // diff_k = s_{k+1} * conj(s_k): numpy fma form (see oracle)
-    const double br = prev.x, bi = -prev.y;
-    const double dr = __builtin_fma(nx.x, br, -(nx.y * bi));
-    if (qpsk) {
-      const double di = __builtin_fma(nx.x, bi, nx.y * br);
-      word |= qpsk_dibit(dr, di) << (30 - 2 * u);
-    } else {
-      word |= (dr < 0 ? 1u : 0u) << (31 - u);
-    }
-    prev = nx;
+  double2 prev = make_double2(0.0, 0.0);
+  if (live) {
+    const int64_t k0 = jw * per;
+    prev = SYM(k0 < S ? k0 : S - 1);
   }
-  buf.words[(size_t)s * p.n_words + j] = word;
+  for (int q = 0; q < WPW; ++q) {
+    const int64_t j = jw + q;
+    uint32_t word = 0;
+    if (live && j < p.n_words) {
+      const int64_t k0 = j * per;
+      for (int u = 0; u < per; ++u) {
+        const int64_t k = k0 + u;
+        if (k >= nd) break;
+        const double2 nx = SYM(k + 1);
+        // diff_k = s_{k+1} * conj(s_k): numpy fma form (see oracle)
+        const double br = prev.x, bi = -prev.y;
+        const double dr = __builtin_fma(nx.x, br, -(nx.y * bi));
+        if (qpsk) {
+          const double di = __builtin_fma(nx.x, bi, nx.y * br);
+          word |= qpsk_dibit(dr, di) << (30 - 2 * u);
+        } else {
+          word |= (dr < 0 ? 1u : 0u) << (31 - u);
+        }
+        prev = nx;
+      }
+    }
+    wl[lane][wv * WPW + q] = word;
+  }
+  __syncthreads();
+  const int jj = threadIdx.x & (kSliceWords - 1);
+  const int64_t j = (int64_t)blockIdx.x * kSliceWords + jj;
+#pragma unroll
+  for (int i = 0; i < kWave / (2 * WV); ++i) {
+    const int sl = i * 2 * WV + (threadIdx.x >> 5);   // 2 WV streams per pass, 32 words each
+    const int64_t ss = (int64_t)blockIdx.y * kWave + sl;
+    if (ss < buf.n_streams && j < p.n_words) buf.words[(size_t)ss * p.n_words + j] = wl[sl][jj];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1228,7 +1258,16 @@ hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const
 hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
-  hipLaunchKernelGGL(k_slice, dim3((unsigned)p.n_words, (unsigned)groups), dim3(kWave), 0, st, b, p);
+  // 16 waves (2 words each) per workgroup; AMR_SLICE_WAVES=4/8 for A/B runs
+  // (same-box: 16 ≈ 4 ≈ 8 within noise in flight, 16 fastest alone)
+  static const int waves = [] { const char* w = getenv("AMR_SLICE_WAVES"); return w ? atoi(w) : 16; }();
+  const dim3 grid((unsigned)((p.n_words + kSliceWords - 1) / kSliceWords), (unsigned)groups);
+  if (waves == 4)
+    hipLaunchKernelGGL(k_slice<4>, grid, dim3(256), 0, st, b, p);
+  else if (waves == 8)
+    hipLaunchKernelGGL(k_slice<8>, grid, dim3(512), 0, st, b, p);
+  else
+    hipLaunchKernelGGL(k_slice<16>, grid, dim3(1024), 0, st, b, p);
   return hipGetLastError();
 }
 
