@@ -1258,16 +1258,17 @@ hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const
 hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t st) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
-  // 16 waves (2 words each) per workgroup; AMR_SLICE_WAVES=4/8 for A/B runs
-  // (same-box: 16 ≈ 4 ≈ 8 within noise in flight, 16 fastest alone)
-  static const int waves = [] { const char* w = getenv("AMR_SLICE_WAVES"); return w ? atoi(w) : 16; }();
+  // 4 waves (8 words each) per workgroup: a 256-thread workgroup finds room
+  // beside the resident band-pass / low-pass waves (a 1024-thread one waited
+  // 10-13 ms per launch at 8192 streams); AMR_SLICE_WAVES=8/16 for A/B runs
+  static const int waves = [] { const char* w = getenv("AMR_SLICE_WAVES"); return w ? atoi(w) : 4; }();
   const dim3 grid((unsigned)((p.n_words + kSliceWords - 1) / kSliceWords), (unsigned)groups);
-  if (waves == 4)
-    hipLaunchKernelGGL(k_slice<4>, grid, dim3(256), 0, st, b, p);
+  if (waves == 16)
+    hipLaunchKernelGGL(k_slice<16>, grid, dim3(1024), 0, st, b, p);
   else if (waves == 8)
     hipLaunchKernelGGL(k_slice<8>, grid, dim3(512), 0, st, b, p);
   else
-    hipLaunchKernelGGL(k_slice<16>, grid, dim3(1024), 0, st, b, p);
+    hipLaunchKernelGGL(k_slice<4>, grid, dim3(256), 0, st, b, p);
   return hipGetLastError();
 }
 

@@ -65,7 +65,7 @@ __device__ __forceinline__ double df2t_step(double (&z)[NS], const Iir& f, doubl
 // which makes the final states non-finite).  The detector keeps the minimum
 // |hi word| (as float) of z1, z3, z5, z7 before every step: >= FLT_MIN means
 // |z| >= 2^-1015, never a zero; a stream that fails, or ends non-finite, is
-// flagged and its group re-run with every tap (k_bp_lane in exact mode).
+// flagged and its group re-run with every tap (k_bp_lane2's FIXUP form).
 // 26 instead of 34 FP64 per step, + 2 v_min3_f32.
 // The numerator is also palindromic (b8 == b0, b6 == b2 bit for bit,
 // PskParams::bp_sym), so x*b8 IS x*b0 and x*b6 IS x*b2: 3 products, not 5.
@@ -130,9 +130,7 @@ int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad) {
 // band-pass: lane = stream, wave = 64 streams.  Coefficients are wave-uniform
 // (kernel arguments in SGPRs).  s1 = [G][nt][8][64] checkpoints, then
 // [G][edge][64] tail outputs.
-// FIXUP: re-run (every tap) only the groups the zero-tap kernel flagged;
-// the others exit at once.
-template <typename T, int WPB, bool FIXUP = false>
+template <typename T, int WPB>
 __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);      // samples per 16-B load
@@ -143,9 +141,6 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
   if (w * 64 >= buf.n_streams) return;          // wave-uniform
   const int64_t last = buf.n_streams - 1;
   const int64_t s = w * 64 + lane;
-  if constexpr (FIXUP) {
-    if (!__any(s <= last && buf.bp_flags[s] != 0)) return;   // wave-uniform: nothing to redo here
-  }
   const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
   const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
   const int64_t n = p.n, n2 = (n + 1) >> 1;
@@ -246,7 +241,12 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
 // backward out of the other buffer and stores f -- the backward pass and the
 // re-run overlap, so the kernel takes two passes of latency instead of three
 // and a batch has twice the waves.  One workgroup barrier per tile.
-template <typename T, int GPB, bool ZO>
+// FIXUP (with ZO false): the full-tap re-run of the groups the zero-tap
+// launch flagged; a workgroup whose group has no flagged stream returns
+// before its first barrier (2-wave, 108-VGPR workgroups: they find room
+// beside the resident band-pass / low-pass waves, where the one-wave kernel's
+// 168-VGPR four-wave workgroups waited up to 15 ms at 8192 streams).
+template <typename T, int GPB, bool ZO, bool FIXUP = false>
 __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);
@@ -260,6 +260,11 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
   const bool active = w * 64 < buf.n_streams;   // inactive groups still meet every barrier
   const int64_t last = buf.n_streams - 1;
   const int64_t s = w * 64 + lane;
+  if constexpr (FIXUP) {
+    static_assert(GPB == 1 && !ZO, "the fix-up pass: one group per workgroup, every tap");
+    if (!active) return;                        // workgroup-uniform (one group)
+    if (!__syncthreads_or(s <= last && buf.bp_flags[s] != 0)) return;   // nothing flagged in this group
+  }
   const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
   const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
   const int64_t n = p.n, n2 = (n + 1) >> 1;
@@ -888,7 +893,7 @@ static hipError_t launch_bp(const PskBuffers& b, const PskParams& p, const Iir& 
       else hipLaunchKernelGGL((k_bp_lane2<T, 1, false>), grid, block, 0, st, b, p, f);
     }
     if (zo)   // every tap for the groups holding a flagged stream (the others exit at once)
-      hipLaunchKernelGGL((k_bp_lane<T, 4, true>), dim3((unsigned)((g + 3) / 4)), dim3(256), 0, st, b, p, f);
+      hipLaunchKernelGGL((k_bp_lane2<T, 1, false, true>), dim3((unsigned)g), dim3(128), 0, st, b, p, f);
     return hipGetLastError();
   }
   switch (lane_wpb()) {
