@@ -314,7 +314,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
             if headline and k == 0 and not fsk:
                 idx = np.arange(B)                                  # the whole batch of slot 0
             else:
-                idx = np.linspace(0, B - 1, num=min(B, 256 if k == 0 else 16)).astype(int)
+                idx = np.linspace(0, B - 1, num=min(B, (1024 if fsk else 256) if k == 0 else 16)).astype(int)
             _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[k]["x"], xh.nbytes))
             xs = xh[idx]
             t1 = time.perf_counter()
