@@ -559,7 +559,7 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=list(WORKLOADS), default="qpsk9600",
                     help="the headline; qpsk9600 (BASELINE configs[1]) also reports the other configs as sub-objects")
