@@ -11,8 +11,9 @@ step   : one pass of the whole demod path over ONE batch: band-pass filtfilt
           + pack (and, for N>1 GPUs, the RCCL all-gather of the decoded bytes).
           K steps = K distinct batches (each in-flight slot has its own input
           buffer and noise draw), at most P of them in flight at once on P
-          plans / HIP streams (P = --inflight, default min(16, K // 2): two or
-          more pipeline rounds inside the timed region).
+          plans / HIP streams (P = --inflight, default `default_inflight`:
+          K itself up to 20 (16 for 8192-stream batches), else a divisor of
+          K near 16, so the timed region is whole pipeline rounds).
 scaling: weak for qpsk9600 / fsk9600 (every rank its own batch), strong for
           ofdm8 / psk8fec (a global batch of 8192 sharded over the ranks).
 
@@ -156,7 +157,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     baud = W["baud"]
     mark, space = args.mark, args.space
     K = args.steps
-    P = args.inflight or (min(2, max(1, K // 2)) if fsk else min(16, max(1, K // 2)))
+    P = args.inflight or (min(2, max(1, K // 2)) if fsk else default_inflight(K, 20 if B <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
     t0 = time.perf_counter()
@@ -556,6 +557,20 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
     return res
 
 
+def default_inflight(K, cap=20):
+    """Batches in flight for K timed PSK steps.  Measured on one MI355X
+    (DESIGN.md §4): whole rounds win -- a partial last round runs a few
+    batches on an otherwise idle GPU (K=20: P=10 4.81 ms/step, P=16 5.05,
+    P=20 3.97) -- and past ~20 HIP streams the hardware queues time-slice
+    (K=64: P=16 4.1 ms, P=32 5.1).  So P = K up to `cap`, else the divisor of
+    K in cap/2..cap closest to 16, else 16.  `cap` is 16 for the 8192-stream
+    batches (HBM: ~13 GB of plan scratch + input per batch)."""
+    if K <= cap:
+        return max(1, K)
+    divs = [d for d in range(max(1, cap // 2), cap + 1) if K % d == 0]
+    return min(divs, key=lambda d: abs(d - 16)) if divs else min(16, cap)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -575,7 +590,7 @@ def main():
     ap.add_argument("--parity-all-slots", action="store_true", help="check sampled streams of every in-flight slot")
     ap.add_argument("--hw-queues", type=int, default=32, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight on separate plans / HIP streams (0 = min(16, steps // 2); fsk9600 2)")
+                    help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
     args = ap.parse_args()
 
     dist, world, rank, local = dist_setup()
