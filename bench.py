@@ -256,13 +256,25 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     barrier(dist)
     _amr.check(L.amr_device_synchronize())
     t0 = time.perf_counter()
-    for k in range(K):
-        c = ctx[k % P]
-        if k >= P:
-            collect(c)                                  # that context's previous batch (the others keep running)
-        step(c)
-    for k in range(max(0, K - P), K):
-        collect(ctx[k % P])
+    if args.host_wait:
+        # the host waits for a plan's previous batch before reusing it (and
+        # reads its kernel timings every batch)
+        for k in range(K):
+            c = ctx[k % P]
+            if k >= P:
+                collect(c)                              # that context's previous batch (the others keep running)
+            step(c)
+        for k in range(max(0, K - P), K):
+            collect(ctx[k % P])
+    else:
+        # batch k is queued on plan k % P's stream behind that plan's previous
+        # batch: stream order keeps each plan's batches (and scratch) in
+        # sequence, so at most P run at once, and the host never stalls the
+        # pipeline between rounds; kernel timings from each plan's last batch
+        for k in range(K):
+            step(ctx[k % P])
+        for k in range(max(0, K - P), K):
+            collect(ctx[k % P])
     _amr.check(L.amr_device_synchronize())
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -589,6 +601,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
     ap.add_argument("--parity-all-slots", action="store_true", help="check sampled streams of every in-flight slot")
     ap.add_argument("--hw-queues", type=int, default=32, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
+    ap.add_argument("--host-wait", action="store_true",
+                    help="wait on the host for a plan's previous batch before queueing the next on it")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
     args = ap.parse_args()
