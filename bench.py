@@ -288,7 +288,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     # a plan without the in-flight hint picks the latency layout (row kernels,
     # DESIGN.md §3.2); its bytes must equal the lane layout's on the same input
     lat1 = None
-    if headline and not fsk:
+    if headline and not fsk and not args.no_latency:
         lp = _amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev)
         lo_, ll_, ls_ = mem.alloc(B * cap), mem.alloc(B * 8), mem.alloc(B * 8)
         ts = []
@@ -628,6 +628,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
     ap.add_argument("--parity-all-slots", action="store_true", help="check sampled streams of every in-flight slot")
     ap.add_argument("--hw-queues", type=int, default=32, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the one-batch latency-layout run after timing (profiling)")
     ap.add_argument("--host-wait", action="store_true",
                     help="wait on the host for a plan's previous batch before queueing the next on it")
     ap.add_argument("--inflight", type=int, default=0,
