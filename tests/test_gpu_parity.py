@@ -336,7 +336,8 @@ sys.exit(1 if bad else 0)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-def test_lane_layout_forced_on_every_case(tmp_path):
+@pytest.mark.parametrize("variant", ["default", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps"])
+def test_lane_layout_forced_on_every_case(tmp_path, variant):
     """The lane-per-stream kernels (psk_lane_kernels.hip: checkpointed
     band-pass and low-pass, picked when many streams are in flight) forced on
     for every call: every golden PSK case (incl. silence / -0.0 / denormal /
@@ -344,8 +345,12 @@ def test_lane_layout_forced_on_every_case(tmp_path):
     BPSK, sps 5 / 10 / 20 and a generic sps, streams shorter than one tile,
     a ragged batch (B not a multiple of 64), streams that trip the band-pass
     zero-tap detector among ordinary ones, and the full 4096 x 96000 batch,
-    against the reference / the oracle.  One subprocess (AMR_PSK_LANE is read
-    once per process)."""
+    against the reference / the oracle.  One subprocess per variant (the
+    AMR_* switches are read once per process): the default kernels, the
+    role-split low-pass (AMR_LP_SPLIT=1), the one-wave band-pass
+    (AMR_BP_SPLIT=0), one-wave / one-group workgroups (AMR_LANE_WPB=1), and
+    2-wave workgroups with every band-pass tap computed (AMR_LANE_WPB=2,
+    AMR_BP_ZO=0); the variants skip the full 4096-stream batch."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -390,11 +395,15 @@ x[129, 12345] = np.nan
 x[100, 4000:4100] = 0.0
 x[101] = 0.0
 bad += check("qpsk", x, 9600, "bpzo")
-bad += check("qpsk", synth.qpsk_batch(4096, 96000, 9600, seed=4096, distinct=8), 9600, "b4096")
+if {variant!r} == "default":
+    bad += check("qpsk", synth.qpsk_batch(4096, 96000, 9600, seed=4096, distinct=8), 9600, "b4096")
 print("BAD", bad[:20], len(bad))
 sys.exit(1 if bad else 0)
 ''')
     env = dict(os.environ, AMR_PSK_LANE="1")
+    env.update({"default": {}, "lp_split": {"AMR_LP_SPLIT": "1"},
+                "bp_one_wave": {"AMR_BP_SPLIT": "0"}, "wpb1": {"AMR_LANE_WPB": "1"},
+                "wpb2_no_zero_taps": {"AMR_LANE_WPB": "2", "AMR_BP_ZO": "0"}}[variant])
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
