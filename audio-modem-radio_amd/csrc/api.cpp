@@ -21,9 +21,9 @@ hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, 
 hipError_t launch_psk_lowpass_fwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_lowpass_bwd(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
 hipError_t launch_psk_lowpass_exact(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
-hipError_t launch_psk_slice(const PskBuffers&, const PskParams&, hipStream_t);
+hipError_t launch_psk_slice(const PskBuffers&, const PskParams&, hipStream_t, bool only_flagged = false);
 hipError_t launch_psk_bandpass_lane(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
-hipError_t launch_psk_lowpass_lane(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
+hipError_t launch_psk_lowpass_lane(const PskBuffers&, const PskParams&, const Iir&, hipStream_t, bool* sliced);
 int64_t psk_lane_bp_scratch_doubles(int64_t n_streams, int64_t n, int pad);
 int64_t psk_lane_lp_scratch_doubles(int64_t n_streams, int64_t n, int pad);
 int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2);
@@ -622,19 +622,20 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(mark(AMR_T_BANDPASS, 0));
     HIP_TRY(launch_psk_bandpass_lane(b, pl->p, pl->bp, st));
     HIP_TRY(mark(AMR_T_BANDPASS, 1));
+    bool sliced = false;                        // the low-pass wrote the words itself (k_lp_lane FUSE)
     if (pl->lp_exact_only) {
       HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)pl->flags, 1, (size_t)B, st));
     } else {
       // forward + backward low-pass in one kernel: timed in the lowpass_fwd slot
       HIP_TRY(mark(AMR_T_LOWPASS_FWD, 0));
-      HIP_TRY(launch_psk_lowpass_lane(b, pl->p, pl->lp, st));
+      HIP_TRY(launch_psk_lowpass_lane(b, pl->p, pl->lp, st, &sliced));
       HIP_TRY(mark(AMR_T_LOWPASS_FWD, 1));
     }
     HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 0));
     HIP_TRY(launch_psk_lowpass_exact(b, pl->p, pl->lp, st));
     HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
-    HIP_TRY(launch_psk_slice(b, pl->p, st));
+    HIP_TRY(launch_psk_slice(b, pl->p, st, sliced));   // then only the K3x streams
     HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
   } else {

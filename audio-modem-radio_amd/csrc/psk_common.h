@@ -64,4 +64,53 @@ __device__ __forceinline__ float tiny_min3(float acc, double a, double b) {
 }
 
 
+
+// ---- the slicer decision (K4a, and the low-pass kernels that slice) ------
+// Sector decision: far from a sector edge (|di| vs |dr| differ by more than
+// 2^-30 relative) the sector is read off the signs; near an edge (or for
+// zeros / NaN / inf) the reference's own steps are replayed: atan2, +2pi if
+// negative, the same four comparisons against the same double constants.
+// np.angle near a sector edge.  numpy evaluates arctan2 with its AVX-512
+// (SVML) kernel on the hosts the reference ran on (the golden fixtures' host;
+// numpy._core.__cpu_features__['AVX512_SKX']), which is not correctly rounded
+// and differs from ocml's atan2 by an ulp on ~6 % of near-tie inputs -- the
+// ones where an ulp decides the sector.  Within |t| < 2^-29 of the diagonal
+// and for components of magnitude 2^-1015 .. 2^985 (~1e-306 .. 1e297), its
+// result is, bit for bit (tests/test_gpu_slicer.py; probed on 1.5 M near-tie
+// pairs in the build container, 1 in ~10^5 off by an ulp in the pi-side form):
+//   t  = (|y| - |x|) / (|y| + |x|)
+//   x > 0:  pi4 + (t + pi4_lo)                 x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
+// negated for y < 0, with pi4 / pi split into double hi + lo.  Outside that
+// domain (denormal or huge components, zeros, inf, NaN) ocml's atan2 is used.
+__device__ __forceinline__ bool numpy_atan2_near_diag(double y, double x, double& ang) {
+  const double ay = fabs(y), ax = fabs(x);
+  if (!(ax >= 0x1p-1015 && ax <= 0x1p985 && ay >= 0x1p-1015 && ay <= 0x1p985)) return false;
+  const double t = (ay - ax) / (ay + ax);
+  if (!(fabs(t) < 0x1p-29)) return false;
+  const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;
+  const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53;
+  const double a = x > 0 ? pi4 + (t + pi4_lo) : pi - (pi4 - (pi_lo - (t + pi4_lo)));
+  ang = y < 0 ? -a : a;
+  return true;
+}
+
+static __device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
+  double ang;
+  if (!numpy_atan2_near_diag(di, dr, ang)) ang = atan2(di, dr);
+  if (ang < 0) ang += 2 * M_PI;
+  if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
+  if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
+  if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3u;
+  return 2u;
+}
+
+__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
+  const double adr = fabs(dr), adi = fabs(di);
+  const double d = adi - adr;
+  const double thr = (adr + adi) * 0x1p-30;
+  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
+  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
+  return qpsk_dibit_slow(dr, di);
+}
+
 }  // namespace amr

@@ -1082,53 +1082,7 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 //   diff = s[k+1] * conj(s[k])   numpy complex multiply   modem.py:100, 214
 //   QPSK sectors                                          modem.py:216-241
 //   BPSK real(diff) < 0 -> 1                              modem.py:103-105
-// Sector decision: far from a sector edge (|di| vs |dr| differ by more than
-// 2^-30 relative) the sector is read off the signs; near an edge (or for
-// zeros / NaN / inf) the reference's own steps are replayed: atan2, +2pi if
-// negative, the same four comparisons against the same double constants.
-// np.angle near a sector edge.  numpy evaluates arctan2 with its AVX-512
-// (SVML) kernel on the hosts the reference ran on (the golden fixtures' host;
-// numpy._core.__cpu_features__['AVX512_SKX']), which is not correctly rounded
-// and differs from ocml's atan2 by an ulp on ~6 % of near-tie inputs -- the
-// ones where an ulp decides the sector.  Within |t| < 2^-29 of the diagonal
-// and for components of magnitude 2^-1015 .. 2^985 (~1e-306 .. 1e297), its
-// result is, bit for bit (tests/test_gpu_slicer.py; probed on 1.5 M near-tie
-// pairs in the build container, 1 in ~10^5 off by an ulp in the pi-side form):
-//   t  = (|y| - |x|) / (|y| + |x|)
-//   x > 0:  pi4 + (t + pi4_lo)                 x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
-// negated for y < 0, with pi4 / pi split into double hi + lo.  Outside that
-// domain (denormal or huge components, zeros, inf, NaN) ocml's atan2 is used.
-__device__ __forceinline__ bool numpy_atan2_near_diag(double y, double x, double& ang) {
-  const double ay = fabs(y), ax = fabs(x);
-  if (!(ax >= 0x1p-1015 && ax <= 0x1p985 && ay >= 0x1p-1015 && ay <= 0x1p985)) return false;
-  const double t = (ay - ax) / (ay + ax);
-  if (!(fabs(t) < 0x1p-29)) return false;
-  const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;
-  const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53;
-  const double a = x > 0 ? pi4 + (t + pi4_lo) : pi - (pi4 - (pi_lo - (t + pi4_lo)));
-  ang = y < 0 ? -a : a;
-  return true;
-}
-
-__device__ __noinline__ uint32_t qpsk_dibit_slow(double dr, double di) {
-  double ang;
-  if (!numpy_atan2_near_diag(di, dr, ang)) ang = atan2(di, dr);
-  if (ang < 0) ang += 2 * M_PI;
-  if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0u;
-  if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1u;
-  if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3u;
-  return 2u;
-}
-
-__device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
-  const double adr = fabs(dr), adi = fabs(di);
-  const double d = adi - adr;
-  const double thr = (adr + adi) * 0x1p-30;
-  if (d < -thr) return dr > 0 ? 0u : 3u;        // |angle| < pi/4 -> 00 ; near pi -> 11
-  if (d > thr) return di > 0 ? 1u : 2u;         // near +pi/2 -> 01 ; near -pi/2 -> 10
-  return qpsk_dibit_slow(dr, di);
-}
-
+// Sector decision: qpsk_dibit (psk_common.h).
 // Workgroup = 64 streams x kSliceWords consecutive words: wave w slices words
 // w*8 .. w*8+7 of its 64 streams (lane = stream; symbol loads are whole
 // 512-B lines, the running symbol carried from word to word), the words go
@@ -1136,14 +1090,16 @@ __device__ __forceinline__ uint32_t qpsk_dibit(double dr, double di) {
 // instruction instead of 64 scattered 4-B words (which the L2 wrote back as
 // partial lines: 84 MB of HBM writes for 9.8 MB of words per 4096 streams).
 constexpr int kSliceWords = 32;
+// only_flagged: the low-pass already sliced every stream it computed exactly
+// (k_lp_lane FUSE); only the streams K3x recomputed get their words here.
 template <int WV>
-__global__ __launch_bounds__(64 * WV) void k_slice(PskBuffers buf, PskParams p) {
+__global__ __launch_bounds__(64 * WV) void k_slice(PskBuffers buf, PskParams p, int only_flagged) {
   constexpr int WPW = kSliceWords / WV;         // words per wave
   __shared__ uint32_t wl[kWave][kSliceWords + 1];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t s = (int64_t)blockIdx.y * kWave + lane;
-  const bool live = s < buf.n_streams;
+  const bool live = s < buf.n_streams && (!only_flagged || buf.flags[s] != 0);
   const int64_t S = p.n_sym;
   const bool qpsk = p.kind == kQpsk;
   const int per = qpsk ? 16 : 32;
@@ -1186,7 +1142,8 @@ __global__ __launch_bounds__(64 * WV) void k_slice(PskBuffers buf, PskParams p) 
   for (int i = 0; i < kWave / (2 * WV); ++i) {
     const int sl = i * 2 * WV + (threadIdx.x >> 5);   // 2 WV streams per pass, 32 words each
     const int64_t ss = (int64_t)blockIdx.y * kWave + sl;
-    if (ss < buf.n_streams && j < p.n_words) buf.words[(size_t)ss * p.n_words + j] = wl[sl][jj];
+    if (ss < buf.n_streams && j < p.n_words && (!only_flagged || buf.flags[ss] != 0))
+      buf.words[(size_t)ss * p.n_words + j] = wl[sl][jj];
   }
 }
 
@@ -1255,7 +1212,7 @@ hipError_t launch_psk_lowpass_bwd(const PskBuffers& b, const PskParams& p, const
   return hipGetLastError();
 }
 
-hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t st) {
+hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t st, bool only_flagged) {
   const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
   // 4 waves (8 words each) per workgroup: a 256-thread workgroup finds room
@@ -1264,11 +1221,11 @@ hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t
   static const int waves = [] { const char* w = getenv("AMR_SLICE_WAVES"); return w ? atoi(w) : 4; }();
   const dim3 grid((unsigned)((p.n_words + kSliceWords - 1) / kSliceWords), (unsigned)groups);
   if (waves == 16)
-    hipLaunchKernelGGL(k_slice<16>, grid, dim3(1024), 0, st, b, p);
+    hipLaunchKernelGGL(k_slice<16>, grid, dim3(1024), 0, st, b, p, only_flagged ? 1 : 0);
   else if (waves == 8)
-    hipLaunchKernelGGL(k_slice<8>, grid, dim3(512), 0, st, b, p);
+    hipLaunchKernelGGL(k_slice<8>, grid, dim3(512), 0, st, b, p, only_flagged ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_slice<4>, grid, dim3(256), 0, st, b, p);
+    hipLaunchKernelGGL(k_slice<4>, grid, dim3(256), 0, st, b, p, only_flagged ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -415,8 +415,18 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 #ifndef AMR_LP_CH
 #define AMR_LP_CH 8
 #endif
-template <int SPS, int FM, int WPB>
+// FUSE (static symbol slots, WPB >= 2): the slicer runs inside the backward
+// pass.  Both component waves of a group park their symbol samples in an LDS
+// ring (16 slots: a region -- the tail, a tile, the head -- holds at most
+// TL / SPS = 8, and two consecutive regions never share a slot), meet at one
+// workgroup barrier per region, and the re wave forms s[k+1] * conj(s[k]),
+// the sector decision (qpsk_dibit, as K4a) and the MSB-first words, storing
+// each word as it completes.  No symbol leaves the chip (0.63 GB written and
+// read back per 4096-stream batch before); streams the detector flags get
+// their symbols from K3x and their words from K4a afterwards.
+template <int SPS, int FM, int WPB, bool FUSE = false>
 __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
+  static_assert(!FUSE || (SPS > 0 && WPB >= 2), "fused slicing: static slots, both components in one workgroup");
   constexpr int TL = kLpT;
   constexpr int CH = AMR_LP_CH;                 // samples per f chunk (CH / 2 x 16 B per lane)
   constexpr int NCH = TL / CH, HC = CH / 2;
@@ -424,6 +434,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   static_assert(TL % CH == 0 && TL <= 64, "tile = whole chunks; one LO value per lane");
   static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
   __shared__ __attribute__((aligned(16))) double lo_lds[WPB][2][TL];
+  __shared__ double sring[FUSE ? WPB : 1][FUSE ? 16 : 1][64];   // FUSE: symbol samples k at slot k & 15
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int64_t w;
@@ -436,11 +447,16 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
     w = (int64_t)blockIdx.x * (WPB / 2) + (wv >> 1);
     comp = wv & 1;
   }
-  if (w * 64 >= buf.n_streams) return;          // wave-uniform
-  const int64_t s = w * 64 + lane;
   const int64_t n = p.n, n2 = (n + 1) >> 1;
   const int pad = p.pad2;
   const int64_t nt = n / TL;
+  if (w * 64 >= buf.n_streams) {                // wave-uniform
+    if constexpr (FUSE) {                       // an idle group still meets the backward pass's barriers
+      for (int64_t b = 0; b < (nt > 1 ? nt - 1 : 0) + 2; ++b) __syncthreads();
+    }
+    return;
+  }
+  const int64_t s = w * 64 + lane;
   const int64_t G = (buf.n_streams + 63) / 64;
   const int64_t wc = w * 2 + comp;
   const int64_t ecap = lp_lane_edge_cap(pad);
@@ -551,8 +567,51 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   // ---- backward pass ----------------------------------------------------------
   const int64_t S = p.n_sym, first = p.first, sps = p.sps;
   double* __restrict__ symp = buf.s1 + sym_index(s, S, 0, comp);   // symbol k at symp[k*64]
+  auto put_sym = [&](int64_t k, double y) {
+    if constexpr (FUSE) sring[wv][k & 15][lane] = y;
+    else symp[k * 64] = y;
+  };
   auto sym_out = [&](int64_t i, double y) {     // generic: a symbol sample at i?
-    if (i >= first && (i - first) % sps == 0) symp[((i - first) / sps) * 64] = y;
+    if (i >= first && (i - first) % sps == 0) put_sym((i - first) / sps, y);
+  };
+  // FUSE: the re wave slices the symbols of samples [i_lo, i_hi) once both
+  // components are in the ring (diff_k = s[k+1] * conj(s[k]) in numpy's fma
+  // form, exactly as K4a); words complete as k descends through 16j (32j)
+  double pr = 0.0, pim = 0.0;                   // s[k+1]
+  uint32_t wacc = 0;
+  const bool qpsk = p.kind == kQpsk;
+  auto region_done = [&](int64_t i_lo, int64_t i_hi) {
+    if constexpr (FUSE) {
+      __syncthreads();
+      if (comp == 0) {
+        const int64_t k_lo = i_lo <= first ? 0 : (i_lo - first + sps - 1) / sps;
+        int64_t k_hi = i_hi - 1 < first ? -1 : (i_hi - 1 - first) / sps;
+        if (k_hi > S - 1) k_hi = S - 1;
+        for (int64_t k = k_hi; k >= k_lo; --k) {
+          const double sr = sring[wv][k & 15][lane], si = sring[wv + 1][k & 15][lane];
+          if (k <= S - 2) {
+            const double br = sr, bi = -si;
+            const double dr = __builtin_fma(pr, br, -(pim * bi));
+            if (qpsk) {
+              const double di = __builtin_fma(pr, bi, pim * br);
+              wacc |= qpsk_dibit(dr, di) << (30 - 2 * (int)(k & 15));
+              if ((k & 15) == 0) {
+                if (s < buf.n_streams) buf.words[(size_t)s * p.n_words + (k >> 4)] = wacc;
+                wacc = 0;
+              }
+            } else {
+              wacc |= (dr < 0 ? 1u : 0u) << (31 - (int)(k & 31));
+              if ((k & 31) == 0) {
+                if (s < buf.n_streams) buf.words[(size_t)s * p.n_words + (k >> 5)] = wacc;
+                wacc = 0;
+              }
+            }
+          }
+          pr = sr;
+          pim = si;
+        }
+      }
+    }
   };
   float accb = __builtin_inff();
   double zb[4];
@@ -564,6 +623,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
     const int64_t i = i_tail + e;
     if (i < n) sym_out(i, y);
   }
+  region_done(i_tail, n);
   if (nt > 1) {
     const int64_t q0 = SPS > 0 ? first / SPS : 0;
     double cn[4];
@@ -599,14 +659,15 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
         const double y0 = lp_step(zb, f, yt[k - 1]);
         accb = tiny_min3(accb, y1, y0);
         if constexpr (SPS > 0) {
-          if (k % SPS == FM) symp[(t * (TL / SPS) + (k - FM) / SPS - q0) * 64] = y1;
-          if ((k - 1) % SPS == FM) symp[(t * (TL / SPS) + (k - 1 - FM) / SPS - q0) * 64] = y0;
+          if (k % SPS == FM) put_sym(t * (TL / SPS) + (k - FM) / SPS - q0, y1);
+          if ((k - 1) % SPS == FM) put_sym(t * (TL / SPS) + (k - 1 - FM) / SPS - q0, y0);
         } else {
           sym_out(t * TL + k, y1);
           sym_out(t * TL + k - 1, y0);
         }
       }
       put_lo(tp, lop);
+      region_done(t * TL, (t + 1) * TL);
     }
   }
   for (int e = pad + (int)nh - 1; e >= 0; --e) {
@@ -615,6 +676,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
     const int64_t i = e - pad;
     if (i >= 0) sym_out(i, y);
   }
+  region_done(0, nh);
   bad |= !(accb >= kTinyHi);
 #pragma unroll
   for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(zb[j]);
@@ -923,33 +985,47 @@ static int lp_split() {
 }
 
 template <int S_, int F_>
-static void launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+static bool launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t g = (b.n_streams + 63) / 64;
   if (lp_split()) {
     hipLaunchKernelGGL((k_lp_lane2<S_, F_, kLpT2>), dim3((unsigned)g), dim3(256), 0, st, b, p, f);
-    return;
+    return false;
   }
+  // the slicer inside the low-pass (static slots, both components in one
+  // workgroup); AMR_FUSED_SLICE=0 writes the symbols for K4a instead
+  static const bool fuse_env = [] { const char* e = getenv("AMR_FUSED_SLICE"); return !(e && e[0] == '0'); }();
+  const bool fuse = S_ > 0 && fuse_env && lane_wpb() >= 2;
   switch (lane_wpb()) {
-    case 4: hipLaunchKernelGGL((k_lp_lane<S_, F_, 4>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f); break;
-    case 2: hipLaunchKernelGGL((k_lp_lane<S_, F_, 2>), dim3((unsigned)g), dim3(128), 0, st, b, p, f); break;
+    case 4:
+      if (fuse) hipLaunchKernelGGL((k_lp_lane<S_, F_, 4, S_ != 0>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
+      else hipLaunchKernelGGL((k_lp_lane<S_, F_, 4>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
+      break;
+    case 2:
+      if (fuse) hipLaunchKernelGGL((k_lp_lane<S_, F_, 2, S_ != 0>), dim3((unsigned)g), dim3(128), 0, st, b, p, f);
+      else hipLaunchKernelGGL((k_lp_lane<S_, F_, 2>), dim3((unsigned)g), dim3(128), 0, st, b, p, f);
+      break;
     default:
       // a multiple of 16 blocks: the re/im XCD pairing is a bijection
       hipLaunchKernelGGL((k_lp_lane<S_, F_, 1>), dim3((unsigned)((2 * g + 15) / 16 * 16)), dim3(64), 0, st, b, p, f);
   }
+  return fuse;
 }
 
-hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st,
+                                   bool* sliced) {
   if (f.nt != 5) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(b.flags, 0, (size_t)b.n_streams * 4, st);
   if (e != hipSuccess) return e;
   const int fm = (int)(p.first % (p.sps > 0 ? p.sps : 1));
-  if (p.sps == 10 && fm == 5) launch_lp<10, 5>(b, p, f, st);
-  else if (p.sps == 5 && fm == 2) launch_lp<5, 2>(b, p, f, st);
-  else if (p.sps == 20 && fm == 10) launch_lp<20, 10>(b, p, f, st);
-  else if (p.sps == 10 && fm == 0) launch_lp<10, 0>(b, p, f, st);
-  else if (p.sps == 5 && fm == 0) launch_lp<5, 0>(b, p, f, st);
-  else if (p.sps == 20 && fm == 0) launch_lp<20, 0>(b, p, f, st);
-  else launch_lp<0, 0>(b, p, f, st);
+  bool fused = false;
+  if (p.sps == 10 && fm == 5) fused = launch_lp<10, 5>(b, p, f, st);
+  else if (p.sps == 5 && fm == 2) fused = launch_lp<5, 2>(b, p, f, st);
+  else if (p.sps == 20 && fm == 10) fused = launch_lp<20, 10>(b, p, f, st);
+  else if (p.sps == 10 && fm == 0) fused = launch_lp<10, 0>(b, p, f, st);
+  else if (p.sps == 5 && fm == 0) fused = launch_lp<5, 0>(b, p, f, st);
+  else if (p.sps == 20 && fm == 0) fused = launch_lp<20, 0>(b, p, f, st);
+  else fused = launch_lp<0, 0>(b, p, f, st);
+  if (sliced) *sliced = fused;
   return hipGetLastError();
 }
 
