@@ -992,9 +992,17 @@ static bool launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hip
     return false;
   }
   // the slicer inside the low-pass (static slots, both components in one
-  // workgroup); AMR_FUSED_SLICE=0 writes the symbols for K4a instead
-  static const bool fuse_env = [] { const char* e = getenv("AMR_FUSED_SLICE"); return !(e && e[0] == '0'); }();
-  const bool fuse = S_ > 0 && fuse_env && lane_wpb() >= 2;
+  // workgroup) once at least 32768 streams are live: it saves the symbols'
+  // HBM round trip (+4-5 % per step at 16 x 4096 in flight) but lengthens a
+  // lone batch's low-pass (11.0 -> 14.5 ms: the re wave slices between
+  // barriers), which is what a small live set (a 1024-stream shard) waits
+  // on.  AMR_FUSED_SLICE=1 / 0 forces it on / off.
+  static const int fuse_env = [] {
+    const char* e = getenv("AMR_FUSED_SLICE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  const int64_t live = b.n_streams * (b.inflight > 1 ? b.inflight : 1);
+  const bool fuse = S_ > 0 && lane_wpb() >= 2 && (fuse_env >= 0 ? fuse_env == 1 : live >= 32768);
   switch (lane_wpb()) {
     case 4:
       if (fuse) hipLaunchKernelGGL((k_lp_lane<S_, F_, 4, S_ != 0>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);

@@ -336,7 +336,7 @@ sys.exit(1 if bad else 0)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("variant", ["default", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps"])
+@pytest.mark.parametrize("variant", ["default", "unfused", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps"])
 def test_lane_layout_forced_on_every_case(tmp_path, variant):
     """The lane-per-stream kernels (psk_lane_kernels.hip: checkpointed
     band-pass and low-pass, picked when many streams are in flight) forced on
@@ -346,7 +346,8 @@ def test_lane_layout_forced_on_every_case(tmp_path, variant):
     a ragged batch (B not a multiple of 64), streams that trip the band-pass
     zero-tap detector among ordinary ones, and the full 4096 x 96000 batch,
     against the reference / the oracle.  One subprocess per variant (the
-    AMR_* switches are read once per process): the default kernels, the
+    AMR_* switches are read once per process): the default kernels with the
+    slicer fused into the low-pass forced on (AMR_FUSED_SLICE=1) and off, the
     role-split low-pass (AMR_LP_SPLIT=1), the one-wave band-pass
     (AMR_BP_SPLIT=0), one-wave / one-group workgroups (AMR_LANE_WPB=1), and
     2-wave workgroups with every band-pass tap computed (AMR_LANE_WPB=2,
@@ -401,7 +402,8 @@ print("BAD", bad[:20], len(bad))
 sys.exit(1 if bad else 0)
 ''')
     env = dict(os.environ, AMR_PSK_LANE="1")
-    env.update({"default": {}, "lp_split": {"AMR_LP_SPLIT": "1"},
+    env.update({"default": {"AMR_FUSED_SLICE": "1"}, "unfused": {"AMR_FUSED_SLICE": "0"},
+                "lp_split": {"AMR_LP_SPLIT": "1"},
                 "bp_one_wave": {"AMR_BP_SPLIT": "0"}, "wpb1": {"AMR_LANE_WPB": "1"},
                 "wpb2_no_zero_taps": {"AMR_LANE_WPB": "2", "AMR_BP_ZO": "0"}}[variant])
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=280)
