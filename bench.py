@@ -157,7 +157,14 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     baud = W["baud"]
     mark, space = args.mark, args.space
     K = args.steps
-    P = args.inflight or (min(2, max(1, K // 2)) if fsk else default_inflight(K, 20 if B <= 4096 else 16))
+    # steps per launch: a strong-scaling shard too small to fill the GPU on its
+    # own (8192 / N streams) takes C consecutive global batches per launch, so a
+    # launch holds >= 4096 streams (what one batch of the headline holds); the
+    # timed region is still exactly K steps (the last launch may be partial)
+    C = max(1, min(K, args.coalesce or (-(-4096 // B) if strong else 1)))
+    BL = C * B                                          # streams per launch
+    n_launch = -(-K // C)
+    P = args.inflight or (min(2, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
     t0 = time.perf_counter()
@@ -173,21 +180,22 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     _amr.check(L.amr_memcpy_h2d(d_base, _amr.ptr(base), base.nbytes))
     d_x = []
     for k in range(P):
-        d = mem.alloc(B * N * 4)
+        d = mem.alloc(BL * N * 4)
         seed = int.from_bytes(hashlib.blake2b(f"{name}/{rank}/{k}".encode(), digest_size=8).digest(), "little")
-        _amr.check(L.amr_synth_tile_noise(d_base, D, N, d, B, lo_s + 17 * k, ctypes.c_float(0.05), seed))
+        _amr.check(L.amr_synth_tile_noise(d_base, D, N, d, BL, lo_s + 17 * k, ctypes.c_float(0.05), seed))
         d_x.append(d)
-    log(f"[rank {rank}] {name}: {P} distinct {B}x{N} float32 batches in HBM in {time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] {name}: {P} distinct {BL}x{N} float32 launch inputs ({C} step(s) of {B} streams each) in HBM "
+        f"in {time.perf_counter() - t0:.1f}s")
 
     # ---- plans: one per in-flight batch (own HIP stream + scratch) ----
     if fsk:
         import _fsk
-        plans = [_fsk.FskPlan(N, baud, mark, space, FS, max_streams=B, device=dev) for _ in range(P)]
+        plans = [_fsk.FskPlan(N, baud, mark, space, FS, max_streams=BL, device=dev) for _ in range(P)]
         sym_per_stream = (N - plans[0].sps // 2 + plans[0].sps - 1) // plans[0].sps   # decided bits (modem.py:320)
         demod, sync_fn, names = L.amr_fsk_demod_device, L.amr_fsk_plan_synchronize, _amr.TF_NAMES
         gather_fn = L.amr_fsk_allgather
     else:
-        plans = [_amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=B, device=dev) for _ in range(P)]
+        plans = [_amr.PskPlan("qpsk", N, baud, 3000.0, FS, max_streams=BL, device=dev) for _ in range(P)]
         S = (N - plans[0].first + plans[0].sps - 1) // plans[0].sps
         sym_per_stream = S - 1                          # differential symbols decided per stream
         demod, sync_fn, names = L.amr_psk_demod_device, L.amr_psk_plan_synchronize, _amr.T_NAMES
@@ -197,30 +205,36 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         if not fsk:
             pl.set_inflight(P)
     cap = plans[0].out_cap
+    # a launch's rows: C steps of B real streams; every rank sends C * B_slot
+    # rows to the gather (the strong-scaling slot padding stays at the end)
+    R = C * B_slot
     ctx = []
     for k, pl in enumerate(plans):
-        c = {"plan": pl, "x": d_x[k], "out": mem.alloc(B_slot * cap), "len": mem.alloc(B_slot * 8),
-             "sync": mem.alloc(B_slot * 8)}
+        c = {"plan": pl, "x": d_x[k], "out": mem.alloc(R * cap), "len": mem.alloc(R * 8), "sync": mem.alloc(R * 8)}
         if fec_fused:
-            c.update(fec=mem.alloc(B_slot * cap), flen=mem.alloc(B_slot * 8), ok=mem.alloc(B_slot * 4))
+            c.update(fec=mem.alloc(R * cap), flen=mem.alloc(R * 8), ok=mem.alloc(R * 4))
         if comm is not None:
-            c["gather"], c["gather_len"] = mem.alloc(world * B_slot * cap), mem.alloc(world * B_slot * 8)
+            c["gather"], c["gather_len"] = mem.alloc(world * R * cap), mem.alloc(world * R * 8)
         ctx.append(c)
 
-    def step(c):
+    def step(c, nb=BL):
         pl = c["plan"]
         if fec_fused:
-            _amr.check(L.amr_psk_demod_fec_device(pl.handle, c["x"], _amr.DTYPE_F32, B, N, c["out"], cap, c["len"],
+            _amr.check(L.amr_psk_demod_fec_device(pl.handle, c["x"], _amr.DTYPE_F32, nb, N, c["out"], cap, c["len"],
                                                   c["sync"], c["fec"], cap, c["flen"], c["ok"]))
         else:
-            _amr.check(demod(pl.handle, c["x"], _amr.DTYPE_F32, B, N, c["out"], cap, c["len"], c["sync"]))
+            _amr.check(demod(pl.handle, c["x"], _amr.DTYPE_F32, nb, N, c["out"], cap, c["len"], c["sync"]))
         if comm is not None:
             # the bytes every rank hands to the gather (the FEC output for
             # psk8fec), to every rank (RCCL over xGMI), ordered after this
             # plan's queued demod and before its next batch
             g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
-            _amr.check(gather_fn(comm, g_out, c["gather"], B_slot * cap, pl.handle))
-            _amr.check(gather_fn(comm, g_len, c["gather_len"], B_slot * 8, pl.handle))
+            _amr.check(gather_fn(comm, g_out, c["gather"], R * cap, pl.handle))
+            _amr.check(gather_fn(comm, g_len, c["gather_len"], R * 8, pl.handle))
+
+    def launch_streams(j):
+        """streams of launch j of the timed region (the last one may hold fewer steps)"""
+        return BL if j < n_launch - 1 else (K - j * C) * B
 
     kt = {k: 0.0 for k in names}
     nt = [0]
@@ -259,22 +273,22 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     if args.host_wait:
         # the host waits for a plan's previous batch before reusing it (and
         # reads its kernel timings every batch)
-        for k in range(K):
-            c = ctx[k % P]
-            if k >= P:
+        for j in range(n_launch):
+            c = ctx[j % P]
+            if j >= P:
                 collect(c)                              # that context's previous batch (the others keep running)
-            step(c)
-        for k in range(max(0, K - P), K):
-            collect(ctx[k % P])
+            step(c, launch_streams(j))
+        for j in range(max(0, n_launch - P), n_launch):
+            collect(ctx[j % P])
     else:
-        # batch k is queued on plan k % P's stream behind that plan's previous
-        # batch: stream order keeps each plan's batches (and scratch) in
+        # launch j is queued on plan j % P's stream behind that plan's previous
+        # launch: stream order keeps each plan's batches (and scratch) in
         # sequence, so at most P run at once, and the host never stalls the
-        # pipeline between rounds; kernel timings from each plan's last batch
-        for k in range(K):
-            step(ctx[k % P])
-        for k in range(max(0, K - P), K):
-            collect(ctx[k % P])
+        # pipeline between rounds; kernel timings from each plan's last launch
+        for j in range(n_launch):
+            step(ctx[j % P], launch_streams(j))
+        for j in range(max(0, n_launch - P), n_launch):
+            collect(ctx[j % P])
     _amr.check(L.amr_device_synchronize())
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -309,32 +323,34 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         del lp
 
     # ---- outputs of every slot (after timing) --------------------------------
+    # (a slot whose last launch was partial keeps, past it, its previous
+    # launch's rows of the same input)
     outs = []
     for c in ctx:
-        o = np.empty((B, cap), np.uint8)
-        ln = np.empty(B, np.int64)
+        o = np.empty((BL, cap), np.uint8)
+        ln = np.empty(BL, np.int64)
         g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
-        _amr.check(L.amr_memcpy_d2h(_amr.ptr(o), g_out, B * cap))
-        _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, B * 8))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(o), g_out, BL * cap))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, BL * 8))
         outs.append((o, ln))
 
     # ---- N>1: the gathered buffer must equal every rank's own output ----------
     gather_check = None
     if comm is not None:
-        last = (K - 1) % P
+        last = (n_launch - 1) % P
         o, ln = outs[last]
-        gp = np.empty((world, B_slot, cap), np.uint8)
-        gl = np.empty((world, B_slot), np.int64)
+        gp = np.empty((world, R, cap), np.uint8)
+        gl = np.empty((world, R), np.int64)
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gp), ctx[last]["gather"], gp.nbytes))
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gl), ctx[last]["gather_len"], gl.nbytes))
         own = [None] * world
         dist.all_gather_object(own, row_digest(o, ln))
-        sizes = [workload_sizes(name, args.batch, world, r)[0] for r in range(world)]
+        sizes = [C * workload_sizes(name, args.batch, world, r)[0] for r in range(world)]
         bad = gather_verdict([row_digest(gp[r], gl[r]) for r in range(world)], own, sizes)
         flags = [None] * world
         dist.all_gather_object(flags, bad)
         bad_any = sorted({b for f in flags for b in f})
-        gather_check = (f"ok: every rank's gathered [{world}][{B_slot}][{cap}] buffer == each rank's own bytes and "
+        gather_check = (f"ok: every rank's gathered [{world}][{R}][{cap}] buffer == each rank's own bytes and "
                         "lengths" if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
 
     # ---- parity: sampled streams of in-flight slots vs the oracle; CPU baseline
@@ -343,7 +359,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     if rank == 0:
         from oracle import oracle
         threads = max(1, min(16, os.cpu_count() or 1))
-        xh = np.empty((B, N), np.float32)
+        xh = np.empty((BL, N), np.float32)
         checked, n_slots, bad_total = 0, 0, []
         cpu = None
         slots = [] if args.no_cpu else range(P) if args.parity_all_slots else sorted({0, 1 % P, P - 1})
@@ -351,7 +367,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
             if headline and k == 0 and not fsk:
                 idx = np.arange(B)                                  # the whole batch of slot 0
             else:
-                idx = np.linspace(0, B - 1, num=min(B, (1024 if fsk else 256) if k == 0 else 16)).astype(int)
+                idx = np.linspace(0, BL - 1, num=min(BL, (1024 if fsk else 256) if k == 0 else 16)).astype(int)
             _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[k]["x"], xh.nbytes))
             xs = xh[idx]
             t1 = time.perf_counter()
@@ -364,13 +380,23 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                 if fec_fused:
                     want = [oracle.fec_decode(w)[0] for w in want]
             cdt = time.perf_counter() - t1
+            reps = 1
+            if k == 0 and headline and not fsk:
+                # the CPU baseline: the same streams again until about
+                # --cpu-seconds of wall time have been spent on them
+                while cdt < args.cpu_seconds:
+                    t1 = time.perf_counter()
+                    oracle.psk_demod_batch("qpsk", xs, baud, n_threads=threads)
+                    cdt += time.perf_counter() - t1
+                    reps += 1
             if k == 0:
                 how = ("oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
                        if fsk else "the C restatement oracle/amr_oracle.c, OpenMP over streams" +
                        (" + oracle.fec_decode" if fec_fused else ""))
-                cpu = {"value": round(len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s", "cores": threads,
-                       "kind": "port", "sample": f"{len(idx)} of the {B} streams of benchmark batch 0 ({N} samples "
-                                                 f"each) through {how}, {cdt:.2f} s wall"}
+                cpu = {"value": round(reps * len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s",
+                       "cores": threads, "kind": "port",
+                       "sample": f"{len(idx)} of the {BL} streams of benchmark batch 0 ({N} samples each)"
+                                 + (f", {reps} passes" if reps > 1 else "") + f" through {how}, {cdt:.2f} s wall"}
             o, ln = outs[k]
             bad_total += [(k, int(i)) for j, i in enumerate(idx) if o[i, :ln[i]].tobytes() != want[j]]
             checked += len(idx)
@@ -391,15 +417,20 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         # algorithmic bytes per launch: the path's compulsory input + output,
         # float32 samples in + the decided bits out (40.25 B/symbol at sps 10)
         out_bytes = sym_per_stream * (1 if fsk else 2) / 8
-        alg_bytes = B * (N * 4 + out_bytes)
-        dom = max(kavg, key=kavg.get)
+        alg_bytes = BL * (N * 4 + out_bytes)
+        step_bytes = B * (N * 4 + out_bytes)
+        # the dominant kernel and its duration: one launch alone on the GPU
+        # (the warmup launches, HIP events on the plan's stream), so the
+        # duration is the kernel's own and not its share of an in-flight round
+        dom = max(solo, key=solo.get) if solo else max(kavg, key=kavg.get)
+        dom_ms = solo.get(dom) or kavg[dom]
         # FP64 ops the reference arithmetic needs per sample (scipy's DF-II-T,
         # no FMA): band-pass 33/pass (9 taps), low-pass 17/pass/component,
         # mixer 1/component (PSK); FSK filtfilt 25/pass/tone + FFT ~5 n log2 n
         if fsk:
             fp64 = B * (2 * 2 * (N + 42) * 25 + 2 * 2 * 5 * N * np.log2(N))
         else:
-            fp64 = B * (2 * (N + 54) * 33 + 2 * (N + 30) * 2 * 17 + 2 * N)
+            fp64 = B * (2 * (N + 54) * 33 + 2 * (N + 30) * 2 * 17 + 2 * N)    # per step
         traffic, step_traffic = None, None
         pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
         if os.path.exists(pmc_file) and world == 1 and N == 96000 and not args.batch:
@@ -410,25 +441,28 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                 # the step's kernels only (not the input synthesis before the timed region)
                 step_traffic = sum(v.get("hbm_bytes_per_dispatch", 0) for k, v in pm.get("kernels", {}).items()
                                    if "synth" not in k) or None
-        ach = alg_bytes / (kavg[dom] / 1e3) / 1e9
+        ach = alg_bytes / (dom_ms / 1e3) / 1e9
+        ach_if = alg_bytes / (kavg[dom] / 1e3) / 1e9 if dom in kavg else None
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": int(traffic) if traffic else None,
             "traffic_ratio": round(traffic / alg_bytes, 2) if traffic else None,
             "alg_bytes_per_launch": int(alg_bytes),
             "alg_bytes_def": "SURVEY 8(d): per stream N x 4 B float32 samples in + decided bits / 8 out "
-                             f"({(N * 4 + out_bytes) / sym_per_stream:.2f} B/symbol here)",
-            "kernel_ms_used": round(kavg[dom], 4),
-            "kernel_ms_note": "the dominant kernel's average HIP-event duration over the timed region (its batches "
-                              "share the GPU with the other in-flight batches), as rocprofv3 reports it",
-            "solo": {"kernel_ms": round(solo[dom], 4) if dom in solo else None,
-                     "achieved": round(alg_bytes / (solo[dom] / 1e3) / 1e9, 2) if dom in solo else None,
-                     "frac": round(alg_bytes / (solo[dom] / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if dom in solo else None,
-                     "layout": latency_layout},
-            "pipeline": {"ms_per_step": round(ms_per_step, 4), "achieved": round(alg_bytes / ms_per_step / 1e6, 2),
-                         "frac": round(alg_bytes / ms_per_step / 1e6 / HBM_PEAK_GBS, 5),
-                         "hbm_traffic_per_step": int(step_traffic) if step_traffic else None,
-                         "hbm_traffic_gbs": round(step_traffic / ms_per_step / 1e6, 1) if step_traffic else None},
+                             f"({(N * 4 + out_bytes) / sym_per_stream:.2f} B/symbol here) x {BL} streams per launch",
+            "kernel_ms_used": round(dom_ms, 4),
+            "kernel_ms_note": "the dominant kernel's average HIP-event duration (on its plan's stream) over the "
+                              f"warmup launches, each alone on the GPU ({latency_layout} layout, as in the timed "
+                              "region); rocprofv3 reproduces it from the same dispatches (profiles/<round>_summary.md)",
+            "inflight": {"kernel_ms": round(kavg[dom], 4) if dom in kavg else None,
+                         "achieved": round(ach_if, 2) if ach_if else None,
+                         "frac": round(ach_if / HBM_PEAK_GBS, 5) if ach_if else None,
+                         "note": f"the same kernel's average duration over the timed region, where {P} launches share "
+                                 "the GPU (so it is up to P x its share of a step)"},
+            "pipeline": {"ms_per_step": round(ms_per_step, 4), "achieved": round(step_bytes / ms_per_step / 1e6, 2),
+                         "frac": round(step_bytes / ms_per_step / 1e6 / HBM_PEAK_GBS, 5),
+                         "hbm_traffic_per_step": int(step_traffic / C) if step_traffic else None,
+                         "hbm_traffic_gbs": round(step_traffic / C / ms_per_step / 1e6, 1) if step_traffic else None},
             "fp64_valu": {"ops_per_step": float(fp64), "achieved_tops": round(fp64 / ms_per_step / 1e9, 3),
                           "peak_tops": FP64_PEAK_TOPS, "frac": round(fp64 / ms_per_step / 1e9 / FP64_PEAK_TOPS, 4),
                           "note": "the binding roof of the bit-exact path (SURVEY §0.7): FP64 ops the reference's "
@@ -451,7 +485,8 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload, "global_batch": B_global, "samples_per_stream": N,
                        "symbols_per_stream": sym_per_stream, "parallelism": f"streams sharded over {world} GPU(s)",
-                       "batches_in_flight": P, "kernel_layout": layout,
+                       "batches_in_flight": P, "steps_per_launch": C, "streams_per_launch": BL,
+                       "kernel_layout": layout,
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "inputs": f"{P} distinct device batches per rank: {D} clean frames + per-slot N(0, 0.05^2) "
                                  "noise (amr_synth_tile_noise)"},
@@ -626,12 +661,17 @@ def main():
     ap.add_argument("--distinct", type=int, default=64, help="clean frames per rank (noise is per stream and slot)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="wall time of the headline's CPU baseline (the oracle over batch 0, repeated)")
     ap.add_argument("--parity-all-slots", action="store_true", help="check sampled streams of every in-flight slot")
     ap.add_argument("--hw-queues", type=int, default=32, help="GPU_MAX_HW_QUEUES for this process (<= 32)")
     ap.add_argument("--no-latency", action="store_true",
                     help="skip the one-batch latency-layout run after timing (profiling)")
     ap.add_argument("--host-wait", action="store_true",
                     help="wait on the host for a plan's previous batch before queueing the next on it")
+    ap.add_argument("--coalesce", type=int, default=0,
+                    help="steps per launch (0 = enough for >= 4096 streams per launch on strong-scaling shards, "
+                         "else 1)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
     args = ap.parse_args()
@@ -660,7 +700,7 @@ def main():
                 subs[name] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "parity",
                                                 "latency_ms_one_batch", "kernel_ms", "kernel_ms_solo", "cpu_baseline",
                                                 "config")}
-                subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "solo", "pipeline",
+                subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
                 for k in ("gather_check", "exact_path_streams"):
                     if k in r:

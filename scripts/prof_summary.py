@@ -78,13 +78,16 @@ def main():
     trace = find(os.path.join(out, "trace"), "*kernel_trace.csv")
     bj = os.path.join(out, "trace_bench.json")
     steps = None
+    warmup = 1
     cfg = {}
     if os.path.exists(bj):
         with open(bj) as f:
             for line in f:
                 if line.startswith("{"):
                     steps = json.loads(line).get("steps")
+                    warmup = json.loads(line).get("warmup", 1)
                     cfg = json.loads(line).get("config", {})
+    launches = -(-steps // cfg.get("steps_per_launch", 1)) if steps else None
     if trace and steps:
         per = {}
         for r in rows(trace):
@@ -92,8 +95,12 @@ def main():
                 (int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
         for k, v in per.items():
             v.sort()
-            tail = [d for _, d in v[-steps:]]
+            tail = [d for _, d in v[-launches:]]
             res.setdefault(k, {})["avg_ns_timed_steps"] = sum(tail) / len(tail)
+            # the warmup launches run one at a time (bench.py); the first is cold
+            head = [d for _, d in v[1:warmup]] if warmup > 1 else [d for _, d in v[:1]]
+            if head:
+                res[k]["avg_ns_solo"] = sum(head) / len(head)
     bench = {}
     if os.path.exists(bj):
         with open(bj) as f:
@@ -121,8 +128,9 @@ def main():
         if not got:
             continue
         d = {"kernels": [k for k in ks if k in res], "avg_ns": sum(g.get("avg_ns", 0) for g in got)}
-        if all("avg_ns_timed_steps" in g for g in got):
-            d["avg_ns_timed_steps"] = sum(g["avg_ns_timed_steps"] for g in got)
+        for key in ("avg_ns_timed_steps", "avg_ns_solo"):
+            if all(key in g for g in got):
+                d[key] = sum(g[key] for g in got)
         for key in ("fetch_bytes_per_dispatch", "write_bytes_per_dispatch", "hbm_bytes_per_dispatch"):
             if all(key in g for g in got):
                 d[key.replace("_per_dispatch", "_per_launch")] = sum(g[key] for g in got)
@@ -140,7 +148,9 @@ def main():
     allres[workload] = {"kernels": res, "slots": slots, "inflight": cfg.get("batches_in_flight"),
                         "layout": cfg.get("kernel_layout"), "steps": steps,
                         "bench": {"dominant_slot": rl.get("kernel"), "alg_bytes_per_launch": rl.get("alg_bytes_per_launch"),
-                                  "kernel_ms_hip_events": rl.get("kernel_ms_used"), "ms_per_step": bench.get("ms_per_step"),
+                                  "kernel_ms_hip_events": rl.get("kernel_ms_used"),
+                                  "kernel_ms_hip_events_inflight": (rl.get("inflight") or {}).get("kernel_ms"),
+                                  "ms_per_step": bench.get("ms_per_step"),
                                   "value": bench.get("value"), "unit": bench.get("unit")}}
     with open(pmc_path, "w") as f:
         json.dump(allres, f, indent=1)
@@ -149,25 +159,30 @@ def main():
         for wl, r in allres.items():
             if not isinstance(r, dict) or "kernels" not in r:
                 continue
-            f.write(f"\n## {wl}\n\n| kernel | calls | avg ms (all) | avg ms (timed steps) | "
-                    "HBM read MB/disp (x2 corr.) | HBM write MB/disp |\n|---|---|---|---|---|---|\n")
+            f.write(f"\n## {wl}\n\n| kernel | calls | avg ms (all) | avg ms (solo warmup launches) | "
+                    "avg ms (timed launches, in flight) | "
+                    "HBM read MB/disp (x2 corr.) | HBM write MB/disp |\n|---|---|---|---|---|---|---|\n")
             for k, v in sorted(r["kernels"].items(), key=lambda kv: -kv[1].get("avg_ns", 0)):
                 ts = v.get("avg_ns_timed_steps")
+                so = v.get("avg_ns_solo")
                 f.write(f"| {k} | {v.get('calls', '')} | {v.get('avg_ns', 0) / 1e6:.3f} | "
+                        f"{(so / 1e6) if so else float('nan'):.3f} | "
                         f"{(ts / 1e6) if ts else float('nan'):.3f} | "
                         f"{v.get('fetch_bytes_per_dispatch', 0) / 1e6:.1f} | "
                         f"{v.get('write_bytes_per_dispatch', 0) / 1e6:.1f} |\n")
             b = r.get("bench", {})
             sl = r.get("slots", {}).get(b.get("dominant_slot") or "", {})
-            if b.get("alg_bytes_per_launch") and sl.get("avg_ns_timed_steps"):
-                ns = sl["avg_ns_timed_steps"]
+            if b.get("alg_bytes_per_launch") and sl.get("avg_ns_solo"):
+                ns = sl["avg_ns_solo"]
                 ach = b["alg_bytes_per_launch"] / ns
                 f.write(f"\nRoofline, reproduced from this profile ({r.get('steps')} timed steps, "
-                        f"{r.get('inflight')} batches in flight, layout {r.get('layout')}): dominant slot "
+                        f"{r.get('inflight')} launches in flight, layout {r.get('layout')}): dominant slot "
                         f"`{b['dominant_slot']}` = {' + '.join(sl['kernels'])}; algorithmic bytes per launch "
-                        f"{b['alg_bytes_per_launch']:,} (SURVEY 8(d)) / rocprofv3 average {ns / 1e6:.3f} ms "
-                        f"= {ach:.2f} GB/s = {ach / 8000:.5f} of 8000 GB/s.  The bench's HIP events over the "
-                        f"same run: {b.get('kernel_ms_hip_events')} ms; step {b.get('ms_per_step')} ms, "
+                        f"{b['alg_bytes_per_launch']:,} (SURVEY 8(d)) / rocprofv3 average of the solo warmup "
+                        f"launches {ns / 1e6:.3f} ms = {ach:.2f} GB/s = {ach / 8000:.5f} of 8000 GB/s.  The bench's "
+                        f"HIP events over the same launches: {b.get('kernel_ms_hip_events')} ms.  In flight "
+                        f"(timed launches): rocprofv3 {sl.get('avg_ns_timed_steps', 0) / 1e6:.3f} ms, HIP events "
+                        f"{b.get('kernel_ms_hip_events_inflight')} ms; step {b.get('ms_per_step')} ms, "
                         f"{b.get('value')} {b.get('unit')}.\n")
                 if sl.get("hbm_bytes_per_launch"):
                     f.write(f"HBM traffic of that slot per launch (FETCH_SIZE x2 + WRITE_SIZE): "

@@ -66,13 +66,15 @@ def test_gloo_world2_equals_single_process(tmp_path, world):
     assert got == want
 
 
-def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_file):
+def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_file, C=1):
     """bench.py's N>1 bookkeeping end to end on gloo: each rank takes its
-    shard of the strong-scaling global batch (bench.workload_sizes), decodes
-    it (the oracle stands in for the GPU), packs it into its [B_slot][cap]
-    slot, the slots are all-gathered (gloo stands in for RCCL), and the
-    gathered buffer is checked against every rank's own output exactly as
-    bench.py does it (row_digest + gather_verdict)."""
+    shard of C consecutive strong-scaling global batches (bench.workload_sizes;
+    C steps per launch, bench --coalesce), decodes them as one launch (the
+    oracle stands in for the GPU), packs them into its [C * B_slot][cap] slot,
+    the slots are all-gathered (gloo stands in for RCCL), and the gathered
+    buffer is checked against every rank's own output exactly as bench.py does
+    it (row_digest + gather_verdict); every step's global batch is then read
+    back out of the gathered buffer in rank order."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
@@ -84,15 +86,17 @@ def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B, Bg, lo, B_slot = bench.workload_sizes("ofdm8", B_global, world, rank)
-    allx = synth.qpsk_batch(B_global, 4000, 9600, seed=5, distinct=B_global)
-    outs, _ = oracle.psk_demod_batch("qpsk", allx[lo:lo + B], 9600)
-    own = np.zeros((B_slot, cap), np.uint8)
-    lens = np.zeros(B_slot, np.int64)
+    steps = [synth.qpsk_batch(B_global, 4000, 9600, seed=5 + c, distinct=B_global) for c in range(C)]
+    launch = np.concatenate([x[lo:lo + B] for x in steps])          # the rank's C shards, one launch
+    outs, _ = oracle.psk_demod_batch("qpsk", launch, 9600)
+    R = C * B_slot
+    own = np.zeros((R, cap), np.uint8)
+    lens = np.zeros(R, np.int64)
     for i, o in enumerate(outs):
         own[i, :len(o)] = np.frombuffer(o, np.uint8)
         lens[i] = len(o)
-    slots = [torch.empty((B_slot, cap), dtype=torch.uint8) for _ in range(world)]
-    lslots = [torch.empty(B_slot, dtype=torch.int64) for _ in range(world)]
+    slots = [torch.empty((R, cap), dtype=torch.uint8) for _ in range(world)]
+    lslots = [torch.empty(R, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(slots, torch.from_numpy(own))
     dist.all_gather(lslots, torch.from_numpy(lens))
     gp = np.stack([t.numpy() for t in slots])
@@ -100,13 +104,15 @@ def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_
     if rank == 0 and corrupt_rank is not None:
         gp[corrupt_rank, 0, 0] ^= 0xFF                    # a wrong byte in that rank's slice
     own_digests = [None] * world
-    dist.all_gather_object(own_digests, bench.row_digest(own[:B], lens[:B]))
-    sizes = [bench.workload_sizes("ofdm8", B_global, world, r)[0] for r in range(world)]
+    dist.all_gather_object(own_digests, bench.row_digest(own[:C * B], lens[:C * B]))
+    shard = [bench.workload_sizes("ofdm8", B_global, world, r)[0] for r in range(world)]
+    sizes = [C * b for b in shard]
     bad = bench.gather_verdict([bench.row_digest(gp[r], gl[r]) for r in range(world)], own_digests, sizes)
     if rank == 0:
-        # the gathered rows in rank order are the single-process batch's output
-        want, _ = oracle.psk_demod_batch("qpsk", allx, 9600)
-        got = [gp[r, i, :gl[r, i]].tobytes() for r in range(world) for i in range(sizes[r])]
+        # step c's rows, rank by rank, are the single-process batch's output
+        want = [w for x in steps for w in oracle.psk_demod_batch("qpsk", x, 9600)[0]]
+        got = [gp[r, c * shard[r] + i, :gl[r, c * shard[r] + i]].tobytes()
+               for c in range(C) for r in range(world) for i in range(shard[r])]
         if corrupt_rank is not None:
             got = want                                    # the corruption is the verdict's to find
         np.save(result_file, np.array([str(bad), str(got == want)]))
@@ -114,12 +120,14 @@ def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,B_global,corrupt", [(2, 7, None), (3, 8, None), (3, 8, 2)])
-def test_bench_gather_bookkeeping_gloo(tmp_path, world, B_global, corrupt):
+@pytest.mark.parametrize("world,B_global,corrupt,C", [(2, 7, None, 1), (3, 8, None, 1), (3, 8, 2, 1), (2, 7, None, 3),
+                                                     (3, 8, 1, 2)])
+def test_bench_gather_bookkeeping_gloo(tmp_path, world, B_global, corrupt, C):
     import torch.multiprocessing as mp
     out = str(tmp_path / "res.npy")
     cap = 2 * 4000 // 10 // 8 + 8
-    mp.spawn(_bench_gather_worker, args=(world, _free_port(), B_global, cap, corrupt, out), nprocs=world, join=True)
+    mp.spawn(_bench_gather_worker, args=(world, _free_port(), B_global, cap, corrupt, out, C), nprocs=world,
+             join=True)
     bad, same = list(np.load(out))
     assert same == "True"
     assert bad == ("[]" if corrupt is None else f"[{corrupt}]")
