@@ -156,7 +156,10 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     N = args.samples
     baud = W["baud"]
     mark, space = args.mark, args.space
-    K = args.steps
+    # the sub-workloads of the default run keep their own timed region
+    # (--sub-steps), whatever --steps the headline is given: at N = 8 a
+    # strong-scaling shard of 20 steps is too little work to fill a GPU
+    K = args.steps if headline else args.sub_steps
     # steps per launch: a strong-scaling shard too small to fill the GPU on its
     # own (8192 / N streams) takes C consecutive global batches per launch, so a
     # launch holds >= 4096 streams (what one batch of the headline holds); the
@@ -650,6 +653,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sub-steps", type=int, default=64,
+                    help="timed steps of each sub-workload of the default run (fsk9600, ofdm8, psk8fec)")
     ap.add_argument("--workload", choices=list(WORKLOADS), default="qpsk9600",
                     help="the headline; qpsk9600 (BASELINE configs[1]) also reports the other configs as sub-objects")
     ap.add_argument("--no-sub", action="store_true", help="skip the sub-workloads of the default run")
@@ -697,7 +702,7 @@ def main():
         for name in ("fsk9600", "ofdm8", "psk8fec"):
             r = run_workload(name, args, dist, world, rank, dev, comm, headline=False)
             if rank == 0 and r is not None:
-                subs[name] = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "scaling", "parity",
+                subs[name] = {k: r[k] for k in ("metric", "value", "unit", "steps", "ms_per_step", "scaling", "parity",
                                                 "latency_ms_one_batch", "kernel_ms", "kernel_ms_solo", "cpu_baseline",
                                                 "config")}
                 subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "kernel_ms_used", "inflight", "pipeline",
