@@ -531,7 +531,84 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         # after the benchmark's plans and buffers are released
         result["host_path_pcie_inclusive"] = host_path(L, fsk, host_res[0], B, N, baud, mark, space, dev, cap,
                                                        sym_per_stream, host_res[1], host_res[2])
+        if not args.no_dropin and not fsk:
+            result["dropin"] = dropin_path(host_res[0], baud, sym_per_stream, host_res[1], host_res[2])
     return result
+
+
+def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
+    """The reference's own call surface, as filebeep_advanced_v2.py uses it
+    (never `value`): the drop-in modules from host memory.
+      * one capture: modem.qpsk_demodulate(x) on one 1-s stream, the live
+        receive path's call (plan cached after the first call);
+      * a batch: modem.qpsk_demodulate_batch + decoder.parse_fbp_stream_enhanced_batch
+        (GPU frame scan + payload CRC32) + intelligent_decompress of every
+        frame -- decode_from_buffer without the file writes -- over the
+        benchmark batch (outputs checked equal to the device path's bytes);
+      * the same over 1024 captures at QPSK@1000, a rate at which the
+        reference's own modulator and demodulator round-trip (at 9600 Bd they
+        do not: SURVEY §0 finding 4, so the benchmark batch recovers no file,
+        as the reference recovers none): files recovered = captures whose
+        frame passed its payload CRC32."""
+    import contextlib
+    import io
+    import modem
+    import decoder
+    from compression import intelligent_decompress
+    B = xh.shape[0]
+    res = {"unit": "ms"}
+    x1 = np.ascontiguousarray(xh[0])
+    one = modem.qpsk_demodulate(x1, baud=baud)
+    ts = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        modem.qpsk_demodulate(x1, baud=baud)
+        ts.append(time.perf_counter() - t1)
+    res["one_capture"] = {"ms": round(float(np.median(ts)) * 1e3, 3),
+                          "what": f"modem.qpsk_demodulate(x, baud={int(baud)}) on one {x1.size}-sample float32 capture "
+                                  "(H2D + demod + D2H, cached plan), median of 5",
+                          "bytes_equal": one == out_dev[0, :len_dev[0]].tobytes()}
+
+    def run():
+        raws = modem.qpsk_demodulate_batch(xh, baud=baud)
+        frames = decoder.parse_fbp_stream_enhanced_batch(raws)
+        files = [[intelligent_decompress(f["data"]) for f in fs] for fs in frames]
+        return raws, frames, files
+    with contextlib.redirect_stdout(io.StringIO()):      # the reference's per-frame log lines
+        run()
+        ts = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            raws, frames, files = run()
+            ts.append(time.perf_counter() - t1)
+    dt = min(ts)
+    ok = sum(1 for fs in frames if len(fs) == 1)
+    res["batch"] = {"ms": round(dt * 1e3, 2), "msym_per_s": round(B * sym_per_stream / dt / 1e6, 3),
+                    "files_recovered": f"{ok}/{B} (the reference's QPSK@9600 does not round-trip)",
+                    "bytes_equal": {"device_path": all(r == out_dev[i, :len_dev[i]].tobytes()
+                                                       for i, r in enumerate(raws))},
+                    "what": "qpsk_demodulate_batch + parse_fbp_stream_enhanced_batch + intelligent_decompress over "
+                            f"the {B} x {xh.shape[1]} benchmark batch from pageable host memory (decode_from_buffer "
+                            "per stream, without the file writes)"}
+
+    # files end to end at a round-tripping rate
+    b2, n2 = 1024, xh.shape[1]
+    x2 = synth.qpsk_batch(b2, n2, 1000, seed=7, noise=0.05, distinct=64)
+    with contextlib.redirect_stdout(io.StringIO()):
+        raws = modem.qpsk_demodulate_batch(x2, baud=1000)
+        ts = []
+        for _ in range(2):
+            t1 = time.perf_counter()
+            raws = modem.qpsk_demodulate_batch(x2, baud=1000)
+            frames = decoder.parse_fbp_stream_enhanced_batch(raws)
+            files = [[intelligent_decompress(f["data"]) for f in fs] for fs in frames]
+            ts.append(time.perf_counter() - t1)
+    dt = min(ts)
+    ok = sum(1 for fs in files if len(fs) == 1 and len(fs[0]) > 0)
+    res["files"] = {"ms": round(dt * 1e3, 2), "files_per_s": round(ok / dt, 1), "files_recovered": f"{ok}/{b2}",
+                    "what": f"decode_from_buffer's steps (without the file writes) over {b2} x {n2} float32 QPSK@1000 "
+                            "captures of one FBPC frame each (synth.qpsk_batch, N(0, 0.05^2) noise), from host memory"}
+    return res
 
 
 def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out_dev, len_dev):
@@ -665,6 +742,7 @@ def main():
     ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
     ap.add_argument("--distinct", type=int, default=64, help="clean frames per rank (noise is per stream and slot)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in module timing (modem / decoder calls)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="wall time of the headline's CPU baseline (the oracle over batch 0, repeated)")
