@@ -78,11 +78,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def dist_setup():
+def dist_setup(force=False):
+    """torch.distributed (gloo: barriers, the max over ranks, the gather check's
+    digests) for N > 1, or with `force` for one rank under torch.distributed.run."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or force:
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
         return dist, world, rank, local
@@ -742,6 +744,9 @@ def main():
     ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
     ap.add_argument("--distinct", type=int, default=64, help="clean frames per rank (noise is per stream and slot)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the N > 1 path (RCCL communicator, per-launch all-gather, gather check) even for one "
+                         "rank; needs torch.distributed.run's rendezvous variables")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in module timing (modem / decoder calls)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -759,12 +764,12 @@ def main():
                     help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
     args = ap.parse_args()
 
-    dist, world, rank, local = dist_setup()
+    dist, world, rank, local = dist_setup(args.force_comm)
     dev = local
     L = _amr.lib()
     _amr.check(L.amr_set_device(dev))
     comm = None
-    if world > 1:
+    if world > 1 or args.force_comm:
         uid = (ctypes.c_uint8 * 128)()
         if rank == 0:
             _amr.check(L.amr_comm_unique_id(uid))
