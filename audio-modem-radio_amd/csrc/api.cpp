@@ -229,6 +229,7 @@ struct amr_psk_plan {
   hipEvent_t ev[AMR_T_COUNT + 1][2]{};
   bool ev_used[AMR_T_COUNT]{};
   int64_t last_exact = 0;
+  GatherGate gate;              // an all-gather still reading this plan's outputs
 };
 
 struct amr_comm {
@@ -346,6 +347,7 @@ static void plan_free(amr_psk_plan* pl) {
   if (!pl) return;
   (void)hipSetDevice(pl->device);
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
+  gate_free(pl->gate);
   for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
                   pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
@@ -494,8 +496,10 @@ int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) {
 
 int amr_psk_plan_synchronize(amr_psk_plan* plan) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);
   HIP_TRY(hipSetDevice(plan->device));
   HIP_TRY(hipStreamSynchronize(plan->stream));
+  HIP_TRY(gate_sync(plan->gate));
   return AMR_OK;
 }
 
@@ -616,6 +620,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   };
   if (pl->p.n_sym < 2) {
     // modem.py:95-96, 211: fewer than two symbols -> b''
+    HIP_TRY(gate_wait(pl->gate, st));
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
   } else if (lane) {
@@ -636,6 +641,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
     HIP_TRY(launch_psk_slice(b, pl->p, st, sliced));   // then only the K3x streams
+    HIP_TRY(gate_wait(pl->gate, st));                  // the outputs: after any gather still reading them
     HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
   } else {
@@ -658,6 +664,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
     HIP_TRY(launch_psk_slice(b, pl->p, st));
+    HIP_TRY(gate_wait(pl->gate, st));
     HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
     HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
   }
@@ -974,38 +981,53 @@ int amr_frame_parse_host(const uint8_t* in, int64_t in_stride, const int64_t* in
 }  // extern "C"
 
 namespace amr {
+hipError_t gate_wait(GatherGate& g, hipStream_t st) {
+  if (!g.pending) return hipSuccess;
+  g.pending = false;                                // one wait covers every earlier gather
+  return hipStreamWaitEvent(st, g.ev, 0);
+}
+
+hipError_t gate_sync(GatherGate& g) {
+  if (!g.pending) return hipSuccess;
+  g.pending = false;
+  return hipEventSynchronize(g.ev);
+}
+
+void gate_free(GatherGate& g) {
+  if (!g.ev) return;
+  (void)hipEventSynchronize(g.ev);
+  (void)hipEventDestroy(g.ev);
+  g.ev = nullptr;
+  g.pending = false;
+}
+
 // The gather on the communicator's own stream, in call order (so several
 // plans -- batches in flight on several streams -- can share one
 // communicator without two ranks ever entering its collectives in different
-// orders).  With a producer stream, the gather waits for the work already
-// queued there (event) and the producer's later work waits for the gather
-// (it may reuse the send buffer).
+// orders).  With a gate (the producer plan's), the gather waits for the work
+// already queued on the producer stream (event), and the producer's later
+// work waits for the gather where it writes its outputs (gate_wait): its
+// filters overlap the gather, and no plan's next batch queues behind another
+// plan's gather.
 int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
-                    bool ordered) {
+                    GatherGate* gate) {
   if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
   HIP_TRY(hipSetDevice(comm->device));
-  hipEvent_t before = nullptr, after = nullptr;
-  if (ordered) {
+  hipEvent_t before = nullptr;
+  if (gate) {
+    if (!gate->ev) HIP_TRY(hipEventCreateWithFlags(&gate->ev, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&before, hipEventDisableTiming));
-    hipError_t e = hipEventCreateWithFlags(&after, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(before, producer);
+    hipError_t e = hipEventRecord(before, producer);
     if (e == hipSuccess) e = hipStreamWaitEvent(comm->stream, before, 0);
-    if (e != hipSuccess) {
-      (void)hipEventDestroy(before);
-      if (after) (void)hipEventDestroy(after);
-      return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
-    }
+    (void)hipEventDestroy(before);                 // released once the wait is done
+    if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
   }
   ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, comm->stream);
-  hipError_t e = hipSuccess;
-  if (ordered) {
-    if (r == ncclSuccess) e = hipEventRecord(after, comm->stream);
-    if (r == ncclSuccess && e == hipSuccess) e = hipStreamWaitEvent(producer, after, 0);
-    (void)hipEventDestroy(before);                 // released once the waits are done
-    (void)hipEventDestroy(after);
-  }
   if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-  if (e != hipSuccess) return fail(AMR_E_HIP, std::string("amr_allgather: ") + hipGetErrorString(e));
+  if (gate) {
+    HIP_TRY(hipEventRecord(gate->ev, comm->stream));
+    gate->pending = true;
+  }
   return AMR_OK;
 }
 }  // namespace amr
@@ -1060,9 +1082,12 @@ int amr_comm_destroy(amr_comm* comm) {
 // can share one communicator without two ranks ever entering its collectives
 // in different orders.  With a plan, the gather waits for the work already on
 // the plan's stream (event), and the plan's later work waits for the gather
-// (it reads the plan's output buffer).
+// before it writes any output (the gather reads them); amr_psk_plan_synchronize
+// also waits for it.
 int amr_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_psk_plan* plan) {
-  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan ? plan->stream : nullptr, plan != nullptr);
+  if (!plan) return allgather_after(comm, d_send, d_recv, bytes_per_rank, nullptr, nullptr);
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate);
 }
 
 int amr_comm_synchronize(amr_comm* comm) {

@@ -29,9 +29,24 @@ int copy_batch_h2d(void* dst, const void* src, int64_t row_bytes, int64_t src_pi
 // pageable memory ran as one transfer per row -- 16384 rows took 215 ms.
 int copy_batch_d2h(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t row_bytes, int64_t B,
                    hipStream_t st);
-// the RCCL all-gather of amr_allgather / amr_fsk_allgather (api.cpp)
+// A plan's hold on its outputs while an all-gather reads them
+// (amr_allgather / amr_fsk_allgather with a plan): the gather waits for the
+// plan's queued work, and the plan's later work waits for the gather only
+// where it writes an output (gate_wait before its output kernels), so the
+// next batch's filters run while the gather is in flight.  One event: the
+// communicator's stream runs gathers in call order, so its latest record
+// covers every earlier gather of the plan.
+struct GatherGate {
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+hipError_t gate_wait(GatherGate& g, hipStream_t st);   // `st` waits for the pending gather
+hipError_t gate_sync(GatherGate& g);                   // the host waits for it
+void gate_free(GatherGate& g);
+// the RCCL all-gather of amr_allgather / amr_fsk_allgather (api.cpp); gate
+// NULL: no ordering against the producer stream
 int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
-                    bool ordered);
+                    GatherGate* gate);
 }  // namespace amr
 
 #define HIP_TRY(expr)                                                                              \

@@ -314,6 +314,7 @@ struct amr_fsk_plan {
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
   int64_t scratch_bytes = 0;
+  GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
   void* d_x = nullptr;
   uint8_t* d_out = nullptr;
@@ -331,6 +332,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   if (!pl) return;
   (void)hipSetDevice(pl->device);
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
+  gate_free(pl->gate);
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync})
     if (p) (void)hipFree(p);
@@ -376,6 +378,7 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   hipStream_t st = pl->stream;
   if (pl->p.n_bits == 0) {
     // no decision window (sps // 4 == 0): empty bit string -> b''   (modem.py:320-323)
+    HIP_TRY(gate_wait(pl->gate, st));
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
     return AMR_OK;
@@ -386,6 +389,7 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(hipEventRecord(pl->ev[AMR_TF_DECIDE][0], st));
   }
   HIP_TRY(launch_fsk_decide(pl->cmp, pl->words, B, pl->p, st));
+  HIP_TRY(gate_wait(pl->gate, st));             // the outputs: after any gather still reading them
   HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
   if (pl->timing) HIP_TRY(hipEventRecord(pl->ev[AMR_TF_DECIDE][1], st));
   return AMR_OK;
@@ -491,8 +495,10 @@ int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->
 
 int amr_fsk_plan_synchronize(amr_fsk_plan* plan) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);
   HIP_TRY(hipSetDevice(plan->device));
   HIP_TRY(hipStreamSynchronize(plan->stream));
+  HIP_TRY(gate_sync(plan->gate));
   return AMR_OK;
 }
 
@@ -521,7 +527,9 @@ int amr_fsk_plan_timings(amr_fsk_plan* plan, float* ms, int count) {
 }
 
 int amr_fsk_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_fsk_plan* plan) {
-  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan ? plan->stream : nullptr, plan != nullptr);
+  if (!plan) return allgather_after(comm, d_send, d_recv, bytes_per_rank, nullptr, nullptr);
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate);
 }
 
 int amr_fsk_demod_device(amr_fsk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,

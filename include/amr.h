@@ -322,7 +322,9 @@ int amr_comm_create(amr_comm **comm, const uint8_t *id, int nranks, int rank, in
 int amr_comm_destroy(amr_comm *comm);
 /* ncclAllGather of bytes_per_rank bytes per rank, on the comm's own stream in
  * call order (safe with several plans in flight); with a plan it is ordered
- * after the plan's queued work and before the plan's later work. */
+ * after the plan's queued work, and the plan's later work waits for it before
+ * writing any output (its filters overlap the gather); the plan's
+ * synchronize waits for it too. */
 int amr_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
                   amr_psk_plan *plan);
 /* the same, ordered after / before the FSK plan's queued work */
