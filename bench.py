@@ -436,12 +436,19 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
             fp64 = B * (2 * 2 * (N + 42) * 25 + 2 * 2 * 5 * N * np.log2(N))
         else:
             fp64 = B * (2 * (N + 54) * 33 + 2 * (N + 30) * 2 * 17 + 2 * N)    # per step
-        traffic, step_traffic = None, None
+        # HBM bytes per launch from the rocprofv3 PMC passes (profiles/), when
+        # this run's launches are the profiled ones: same workload, samples,
+        # streams per launch and kernel layout (bytes per launch do not depend
+        # on how many launches are in flight or on the rank count)
+        traffic, step_traffic, traffic_src = None, None, None
         pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
-        if os.path.exists(pmc_file) and world == 1 and N == 96000 and not args.batch:
+        if os.path.exists(pmc_file) and N == 96000 and BL == W["batch"]:
             with open(pmc_file) as f:
                 pm = json.load(f).get(name, {})
-            if pm.get("inflight") == P and pm.get("layout", layout) == layout:
+            if pm.get("layout", layout) == layout:
+                traffic_src = (f"profiles/{PROFILE_ROUND}_pmc.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch "
+                               f"({pm.get('steps')} timed launches at {pm.get('inflight')} in flight, layout "
+                               f"{pm.get('layout')})")
                 traffic = pm.get("slots", {}).get(dom, {}).get("hbm_bytes_per_launch")
                 # the step's kernels only (not the input synthesis before the timed region)
                 step_traffic = sum(v.get("hbm_bytes_per_dispatch", 0) for k, v in pm.get("kernels", {}).items()
@@ -451,7 +458,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": int(traffic) if traffic else None,
-            "traffic_ratio": round(traffic / alg_bytes, 2) if traffic else None,
+            "traffic_ratio": round(traffic / alg_bytes, 2) if traffic else None, "traffic_source": traffic_src,
             "alg_bytes_per_launch": int(alg_bytes),
             "alg_bytes_def": "SURVEY 8(d): per stream N x 4 B float32 samples in + decided bits / 8 out "
                              f"({(N * 4 + out_bytes) / sym_per_stream:.2f} B/symbol here) x {BL} streams per launch",
