@@ -304,6 +304,23 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     value = B_global * sym_per_stream / (dt / K) / 1e6
     kavg = {k: v / max(1, nt[0]) for k, v in kt.items() if v > 0}
 
+    # ---- sustained: the same pipeline for about --sustain-seconds (headline
+    # only, after the timed region; a longer run settles at a lower clock) ----
+    sustained = None
+    if headline and args.sustain_seconds > 0:
+        n_s = max(P, int(round(args.sustain_seconds / max(1e-4, dt / n_launch) / P)) * P)
+        barrier(dist)
+        _amr.check(L.amr_device_synchronize())
+        t1 = time.perf_counter()
+        for j in range(n_s):
+            step(ctx[j % P])
+        _amr.check(L.amr_device_synchronize())
+        barrier(dist)
+        ds = max_over_ranks(dist, time.perf_counter() - t1)
+        sustained = {"steps": n_s * C, "seconds": round(ds, 3), "ms_per_step": round(ds / (n_s * C) * 1e3, 4),
+                     "value": round(B_global * sym_per_stream * n_s * C / ds / 1e6, 3),
+                     "what": f"{n_s} more launches of the same pipeline ({P} in flight), timed as the headline"}
+
     # ---- one batch alone, as a single-batch caller runs it (after timing) ------
     # a plan without the in-flight hint picks the latency layout (row kernels,
     # DESIGN.md §3.2); its bytes must equal the lane layout's on the same input
@@ -524,6 +541,8 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                 "source": "BASELINE.md §2: the reference's modem.py on numpy 2.2.6 / scipy 1.15.3, measured in the "
                           "build container (8 cores), not on the GPU box"},
         }
+        if sustained is not None:
+            result["sustained"] = sustained
         if gather_check is not None:
             result["gather_check"] = gather_check
         if not fsk:
@@ -757,6 +776,9 @@ def main():
     ap.add_argument("--space", type=float, default=24000.0, help="fsk9600: space tone")
     ap.add_argument("--distinct", type=int, default=64, help="clean frames per rank (noise is per stream and slot)")
     ap.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive host-API timing")
+    ap.add_argument("--sustain-seconds", type=float, default=2.0,
+                    help="after the timed region, run the headline pipeline this long again and report it as "
+                         "`sustained` (0 = skip)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the N > 1 path (RCCL communicator, per-launch all-gather, gather check) even for one "
                          "rank; needs torch.distributed.run's rendezvous variables")

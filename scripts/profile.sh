@@ -13,7 +13,7 @@ ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_${TAG}_$WORKLOAD
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1
-ARGS="--workload $WORKLOAD --steps ${STEPS:-64} --warmup 3 --no-cpu --no-host-path --no-sub --no-latency ${BENCH_ARGS:-}"
+ARGS="--workload $WORKLOAD --steps ${STEPS:-64} --warmup 3 --no-cpu --no-host-path --no-sub --no-latency --no-dropin --sustain-seconds 0 ${BENCH_ARGS:-}"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$ROOT/bench.py" $ARGS > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
