@@ -564,7 +564,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     if result is not None and host_res is not None:
         # after the benchmark's plans and buffers are released
         result["host_path_pcie_inclusive"] = host_path(L, fsk, host_res[0], B, N, baud, mark, space, dev, cap,
-                                                       sym_per_stream, host_res[1], host_res[2])
+                                                       sym_per_stream, host_res[1], host_res[2], args.host_plans)
         if not args.no_dropin and not fsk:
             result["dropin"] = dropin_path(host_res[0], baud, sym_per_stream, host_res[1], host_res[2])
     return result
@@ -645,7 +645,7 @@ def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
     return res
 
 
-def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out_dev, len_dev):
+def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out_dev, len_dev, host_plans=0):
     """PCIe-inclusive rates from host memory (never `value`):
       * one batch at a time: amr_*_demod_host from pageable memory, H2D +
         demod + D2H, on a plan without an in-flight hint (latency layout);
@@ -678,7 +678,8 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
                                 % ("fsk" if fsk else "psk"), "bytes_equal": {"device_path": same(h_out, h_len)}}
     del plan
     gc.collect()
-    n_pl, n_batches = (2, 4) if fsk else (3, 6)
+    n_pl = host_plans or (2 if fsk else 3)
+    n_batches = 2 * n_pl
     plans = [mk() for _ in range(n_pl)]
     if not fsk:
         for pl in plans:
@@ -782,6 +783,8 @@ def main():
     ap.add_argument("--force-comm", action="store_true",
                     help="run the N > 1 path (RCCL communicator, per-launch all-gather, gather check) even for one "
                          "rank; needs torch.distributed.run's rendezvous variables")
+    ap.add_argument("--host-plans", type=int, default=0,
+                    help="plans the PCIe-inclusive stream of batches uses in turn (0 = 3 PSK / 2 FSK)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in module timing (modem / decoder calls)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle parity check and CPU baseline (profiling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
