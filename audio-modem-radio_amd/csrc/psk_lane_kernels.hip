@@ -234,6 +234,77 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
 }
 
 // ---------------------------------------------------------------------------
+// The band-pass forward pass of one group (lane = stream): pads + tiles
+// (checkpoint at the start of every tile, no output) + tail (edge outputs);
+// the zero-tap detector flags a stream it cannot vouch for.  Used by
+// k_bp_lane2's forward role and, on its own, by k_bp_fwd.
+template <typename T, bool ZO>
+__device__ __forceinline__ void bp_forward_pass(const PskBuffers& buf, const PskParams& p, const Iir& f, int64_t w,
+                                                int lane) {
+  constexpr int TB = kBpT;
+  constexpr int PER = 16 / (int)sizeof(T);
+  constexpr int NL = TB / PER;
+  const int64_t last = buf.n_streams - 1;
+  const int64_t s = w * 64 + lane;
+  const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + (s < last ? s : last) * buf.x_stride;
+  const uint8_t* __restrict__ xb = reinterpret_cast<const uint8_t*>(x);
+  const int64_t n = p.n;
+  const int pad = p.pad1;
+  const int64_t nt = n / TB;
+  const int64_t G = (buf.n_streams + 63) / 64;
+  const int64_t ecap = bp_lane_edge_cap(pad);
+  const int64_t i_tail = nt * TB;
+  double* __restrict__ ck = buf.s1 + (size_t)w * nt * 8 * 64 + lane;
+  double* __restrict__ eb = buf.s1 + (size_t)G * nt * 8 * 64 + (size_t)w * ecap * 64 + lane;
+  auto load_tile = [&](int64_t t, v4u (&r)[NL]) {
+#pragma unroll
+    for (int k = 0; k < NL; ++k) r[k] = *reinterpret_cast<const v4u*>(xb + (size_t)t * TB * sizeof(T) + k * 16);
+  };
+  auto tile_x = [&](const v4u (&r)[NL], int k) -> double {
+    T v[PER];
+    __builtin_memcpy(v, &r[k / PER], 16);
+    return In<T>::cvt(v[k % PER]);
+  };
+  double z[8];
+  float acc = __builtin_inff();
+  const T x0 = x[0], xl = x[n - 1];
+  {
+    const double e0 = In<T>::ext(x0, x[pad]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
+  }
+  for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, In<T>::ext(x0, x[pad - jj]), acc);
+  v4u xr[NL];
+  if (nt > 0) load_tile(0, xr);
+  for (int64_t t = 0; t < nt; ++t) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ck[(t * 8 + j) * 64] = z[j];
+    v4u cur[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) cur[k] = xr[k];
+    load_tile(t + 1 < nt ? t + 1 : t, xr);
+#pragma unroll
+    for (int k = 0; k < TB; ++k) (void)bp_step<ZO>(z, f, tile_x(cur, k), acc);
+  }
+  int e = 0;
+  for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::cvt(x[i]), acc);
+  for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::ext(xl, x[n - 2 - jj]), acc);
+  if (bp_bad<ZO>(acc, z) && s <= last) atomicOr(&buf.bp_flags[s], 1);
+}
+
+// band-pass forward pass alone, wave = group (AMR_BP_PREFWD): k_bp_lane2<...,
+// PRE> then runs only the re-run / backward roles.  The forward pass no
+// longer holds an idle backward wave and its LDS for half the band-pass's
+// life.
+template <typename T, bool ZO>
+__global__ __launch_bounds__(256) void k_bp_fwd(PskBuffers buf, PskParams p, Iir f) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w * 64 >= buf.n_streams) return;          // wave-uniform
+  bp_forward_pass<T, ZO>(buf, p, f, w, lane);
+}
+
+// ---------------------------------------------------------------------------
 // band-pass, role-split: two waves per group of 64 streams (GPB groups per
 // workgroup).  Wave 0 runs the forward pass (checkpoints + tail edge) while
 // wave 1 waits; then, tile by tile from the end, wave 0 re-runs tile t-1
@@ -246,8 +317,9 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
 // before its first barrier (2-wave, 108-VGPR workgroups: they find room
 // beside the resident band-pass / low-pass waves, where the one-wave kernel's
 // 168-VGPR four-wave workgroups waited up to 15 ms at 8192 streams).
-template <typename T, int GPB, bool ZO, bool FIXUP = false>
+template <typename T, int GPB, bool ZO, bool FIXUP = false, bool PRE = false>
 __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
+  static_assert(!(FIXUP && PRE), "the fix-up pass runs its own forward pass");
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);
   constexpr int NL = TB / PER;
@@ -288,8 +360,10 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
     return In<T>::cvt(v[k % PER]);
   };
 
-  if (role == 0 && active) {
+  if (!PRE && role == 0 && active) {
     // ---- forward pass: pads + tiles (checkpoints only) + tail (edge) ------
+    // (the same steps as bp_forward_pass, written out: through the device
+    // function the compiler kept 238 VGPRs live here against 113)
     double z[8];
     float acc = __builtin_inff();
     const T x0 = x[0], xl = x[n - 1];
@@ -930,6 +1004,13 @@ static int bp_split() {
   return v;
 }
 
+static int bp_prefwd() {
+  // the band-pass forward pass as its own launch (k_bp_fwd) before the
+  // role-split re-run / backward kernel: AMR_BP_PREFWD=1 / 0
+  static const int v = [] { const char* e = getenv("AMR_BP_PREFWD"); return e && e[0] == '1' ? 1 : 0; }();
+  return v;
+}
+
 static int bp_zero_taps(const PskParams& p) {
   // skip the band-pass's +0.0 odd taps (detector + exact re-run of flagged
   // groups): AMR_BP_ZO=0 computes every tap instead
@@ -947,7 +1028,16 @@ static hipError_t launch_bp(const PskBuffers& b, const PskParams& p, const Iir& 
       if (e != hipSuccess) return e;
     }
     const dim3 grid((unsigned)(lane_wpb() >= 2 ? (g + 1) / 2 : g)), block(lane_wpb() >= 2 ? 256 : 128);
-    if (lane_wpb() >= 2) {
+    if (lane_wpb() >= 2 && bp_prefwd()) {
+      const dim3 fgrid((unsigned)((g + 3) / 4));
+      if (zo) {
+        hipLaunchKernelGGL((k_bp_fwd<T, true>), fgrid, dim3(256), 0, st, b, p, f);
+        hipLaunchKernelGGL((k_bp_lane2<T, 2, true, false, true>), grid, block, 0, st, b, p, f);
+      } else {
+        hipLaunchKernelGGL((k_bp_fwd<T, false>), fgrid, dim3(256), 0, st, b, p, f);
+        hipLaunchKernelGGL((k_bp_lane2<T, 2, false, false, true>), grid, block, 0, st, b, p, f);
+      }
+    } else if (lane_wpb() >= 2) {
       if (zo) hipLaunchKernelGGL((k_bp_lane2<T, 2, true>), grid, block, 0, st, b, p, f);
       else hipLaunchKernelGGL((k_bp_lane2<T, 2, false>), grid, block, 0, st, b, p, f);
     } else {

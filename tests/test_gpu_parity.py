@@ -336,7 +336,8 @@ sys.exit(1 if bad else 0)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("variant", ["default", "unfused", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps"])
+@pytest.mark.parametrize("variant", ["default", "unfused", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps",
+                                     "bp_prefwd", "bp_prefwd_no_zero_taps"])
 def test_lane_layout_forced_on_every_case(tmp_path, variant):
     """The lane-per-stream kernels (psk_lane_kernels.hip: checkpointed
     band-pass and low-pass, picked when many streams are in flight) forced on
@@ -405,7 +406,9 @@ sys.exit(1 if bad else 0)
     env.update({"default": {"AMR_FUSED_SLICE": "1"}, "unfused": {"AMR_FUSED_SLICE": "0"},
                 "lp_split": {"AMR_LP_SPLIT": "1"},
                 "bp_one_wave": {"AMR_BP_SPLIT": "0"}, "wpb1": {"AMR_LANE_WPB": "1"},
-                "wpb2_no_zero_taps": {"AMR_LANE_WPB": "2", "AMR_BP_ZO": "0"}}[variant])
+                "wpb2_no_zero_taps": {"AMR_LANE_WPB": "2", "AMR_BP_ZO": "0"},
+                "bp_prefwd": {"AMR_BP_PREFWD": "1"},
+                "bp_prefwd_no_zero_taps": {"AMR_BP_PREFWD": "1", "AMR_BP_ZO": "0"}}[variant])
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
