@@ -1,7 +1,8 @@
 """bench.py's N > 1 path on one GPU (`--force-comm`: torch.distributed.run
 with one rank, a one-rank RCCL communicator, the all-gather after every
-launch, the gather check), small sizes: the headline layout and a
-strong-scaling workload with two global batches per launch (`--coalesce`).
+launch, the gather check), small sizes: the headline layout, a
+strong-scaling workload with two global batches per launch (`--coalesce`),
+and the FSK plans' gather (amr_fsk_allgather).
 The 8-GPU run is the driver's; this keeps the code it runs exercised."""
 import json
 import os
@@ -22,7 +23,8 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("extra", [["--batch", "256"], ["--workload", "ofdm8", "--batch", "512", "--coalesce", "2"]])
+@pytest.mark.parametrize("extra", [["--batch", "256"], ["--workload", "ofdm8", "--batch", "512", "--coalesce", "2"],
+                                   ["--workload", "fsk9600", "--batch", "256"]])
 def test_force_comm_gather_check(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
