@@ -55,7 +55,7 @@ import synth  # noqa: E402
 
 FS = 96000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-HBM_MIXED_GBS = 4800.0         # measured streaming rate at 1:1..3:1 read:write (tools/hbm_mix_probe.hip, profiles/)
+HBM_MIXED_GBS = 5200.0         # measured streaming rate at 1:1..2:1 read:write (tools/hbm_mix_probe.hip, profiles/)
 PROFILE_ROUND = "r02"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
 
@@ -497,7 +497,8 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                          if step_traffic else None,
                          "measured_stream_gbs": HBM_MIXED_GBS,
                          "measured_stream_source": "tools/hbm_mix_probe.hip on one MI355X: a streaming kernel's rate "
-                                                   f"at 1:1 to 3:1 read:write (profiles/{PROFILE_ROUND}_hbm_mix_probe.txt)"},
+                                                   "at 1:1 and 2:1 read:write, 8 accesses per lane in flight "
+                                                   f"(profiles/{PROFILE_ROUND}_hbm_mix_probe.txt)"},
             "fp64_valu": {"ops_per_step": float(fp64), "achieved_tops": round(fp64 / ms_per_step / 1e9, 3),
                           "peak_tops": FP64_PEAK_TOPS, "frac": round(fp64 / ms_per_step / 1e9 / FP64_PEAK_TOPS, 4),
                           "note": "the binding roof of the bit-exact path (SURVEY §0.7): FP64 ops the reference's "
