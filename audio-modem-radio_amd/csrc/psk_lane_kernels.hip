@@ -489,11 +489,16 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 #ifndef AMR_LP_CH
 #define AMR_LP_CH 8
 #endif
+#ifndef AMR_LP_REGION_SYMS
+#define AMR_LP_REGION_SYMS 8     // fused slicer: symbols per slicing region at most (a power of two >= TL / sps)
+#endif
 // FUSE (static symbol slots, WPB >= 2): the slicer runs inside the backward
 // pass.  Both component waves of a group park their symbol samples in an LDS
-// ring (16 slots: a region -- the tail, a tile, the head -- holds at most
-// TL / SPS = 8, and two consecutive regions never share a slot), meet at one
-// workgroup barrier per region, and the re wave forms s[k+1] * conj(s[k]),
+// ring (16 slots: a region -- the tail, RT tiles, the head -- holds at most 8
+// symbols, and two consecutive regions never share a slot), meet at one
+// workgroup barrier per region (RT = 2 tiles at sps 10: half the barriers of
+// one per tile, a lone batch's low-pass 14.5 -> 13.7 ms; 16-symbol regions
+// in a 32-slot ring measured slower), and the re wave forms s[k+1] * conj(s[k]),
 // the sector decision (qpsk_dibit, as K4a) and the MSB-first words, storing
 // each word as it completes.  No symbol leaves the chip (0.63 GB written and
 // read back per 4096-stream batch before); streams the detector flags get
@@ -508,7 +513,15 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   static_assert(TL % CH == 0 && TL <= 64, "tile = whole chunks; one LO value per lane");
   static_assert(SPS == 0 || (TL % SPS == 0 && FM < SPS), "static symbol slots");
   __shared__ __attribute__((aligned(16))) double lo_lds[WPB][2][TL];
-  __shared__ double sring[FUSE ? WPB : 1][FUSE ? 16 : 1][64];   // FUSE: symbol samples k at slot k & 15
+  // FUSE: tiles per slicing region (one barrier each) -- as many as keep a
+  // region within MS symbols -- and a ring of 2 MS symbol slots per wave (two
+  // consecutive regions never share a slot)
+  constexpr int SPR = TL / (SPS > 0 ? SPS : TL);                 // symbols per tile (static slots)
+  constexpr int MS = AMR_LP_REGION_SYMS;
+  constexpr int RT = MS / SPR > 1 ? MS / SPR : 1;
+  constexpr int NSL = FUSE ? 2 * MS : 1;
+  static_assert(!FUSE || (RT * SPR <= MS && (MS & (MS - 1)) == 0), "a region holds at most MS symbols");
+  __shared__ double sring[FUSE ? WPB : 1][NSL][64];   // FUSE: symbol samples k at slot k & (NSL - 1)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int64_t w;
@@ -526,7 +539,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   const int64_t nt = n / TL;
   if (w * 64 >= buf.n_streams) {                // wave-uniform
     if constexpr (FUSE) {                       // an idle group still meets the backward pass's barriers
-      for (int64_t b = 0; b < (nt > 1 ? nt - 1 : 0) + 2; ++b) __syncthreads();
+      for (int64_t b = 0; b < (nt > 1 ? (nt - 1 + RT - 1) / RT : 0) + 2; ++b) __syncthreads();
     }
     return;
   }
@@ -642,7 +655,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   const int64_t S = p.n_sym, first = p.first, sps = p.sps;
   double* __restrict__ symp = buf.s1 + sym_index(s, S, 0, comp);   // symbol k at symp[k*64]
   auto put_sym = [&](int64_t k, double y) {
-    if constexpr (FUSE) sring[wv][k & 15][lane] = y;
+    if constexpr (FUSE) sring[wv][k & (NSL - 1)][lane] = y;
     else symp[k * 64] = y;
   };
   auto sym_out = [&](int64_t i, double y) {     // generic: a symbol sample at i?
@@ -662,7 +675,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
         int64_t k_hi = i_hi - 1 < first ? -1 : (i_hi - 1 - first) / sps;
         if (k_hi > S - 1) k_hi = S - 1;
         for (int64_t k = k_hi; k >= k_lo; --k) {
-          const double sr = sring[wv][k & 15][lane], si = sring[wv + 1][k & 15][lane];
+          const double sr = sring[wv][k & (NSL - 1)][lane], si = sring[wv + 1][k & (NSL - 1)][lane];
           if (k <= S - 2) {
             const double br = sr, bi = -si;
             const double dr = __builtin_fma(pr, br, -(pim * bi));
@@ -706,6 +719,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
 #pragma unroll
     for (int c = 0; c < R; ++c) load_chunk(nt - 1, c, ring[c]);
     put_lo(nt - 1, load_lo(nt - 1));
+    int64_t r_hi = nt * TL;                     // FUSE: upper bound of the region not yet sliced
     for (int64_t t = nt - 1; t >= 1; --t) {
       double zf[4];
 #pragma unroll
@@ -741,7 +755,10 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
         }
       }
       put_lo(tp, lop);
-      region_done(t * TL, (t + 1) * TL);
+      if ((nt - 1 - t) % RT == RT - 1 || t == 1) {
+        region_done(t * TL, r_hi);
+        r_hi = t * TL;
+      }
     }
   }
   for (int e = pad + (int)nh - 1; e >= 0; --e) {
