@@ -1101,7 +1101,7 @@ static bool launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hip
   // the slicer inside the low-pass (static slots, both components in one
   // workgroup) once at least 32768 streams are live: it saves the symbols'
   // HBM round trip (+4-5 % per step at 16 x 4096 in flight) but lengthens a
-  // lone batch's low-pass (11.0 -> 14.5 ms: the re wave slices between
+  // lone batch's low-pass (11.0 -> 13.7 ms: the re wave slices between
   // barriers), which is what a small live set (a 1024-stream shard) waits
   // on.  AMR_FUSED_SLICE=1 / 0 forces it on / off.
   static const int fuse_env = [] {

@@ -51,8 +51,10 @@ SLOTS["ofdm8"] = SLOTS["psk8fec"] = SLOTS["qpsk9600"]
 
 def short(name):
     n = name.replace("amr::", "").replace("(amr::FftEpiMode)", "")
-    if "k_bp_lane2<" in n and ", false, true>" in n:
-        return "k_bp_lane2_fixup"                   # the zero-tap fallback launch (early exit)
+    if "k_bp_lane2<" in n:
+        args = [t.strip() for t in n.split("k_bp_lane2<", 1)[1].split(">", 1)[0].split(",")]
+        if len(args) >= 4 and args[3] == "true":
+            return "k_bp_lane2_fixup"               # the zero-tap fallback launch (early exit)
     for k in KERNELS:
         if k in n:
             return k
