@@ -46,8 +46,11 @@ def source_hash() -> str:
     """sha256 prefix over every source, header, this script and the flags:
     the build id libamr.so reports (amr_build_id), which ties a loaded
     library to the sources of the tree it runs in."""
+    # the flags without the tree's absolute include paths: the id depends on
+    # what is compiled, not on where the tree sits (the GPU box runs a copy)
+    flags = [f for f in CFLAGS if f not in (CSRC, INCLUDE)]
     return _digest([os.path.join(CSRC, s) for s in SOURCES] + _headers() + [os.path.abspath(__file__)],
-                   " ".join(CFLAGS))
+                   " ".join(flags))
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
