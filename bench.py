@@ -167,9 +167,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     # own (8192 / N streams) takes C consecutive global batches per launch, so a
     # launch holds >= 4096 streams (what one batch of the headline holds); the
     # timed region is still exactly K steps (the last launch may be partial)
-    C = max(1, min(K, args.coalesce or (-(-4096 // B) if strong else 1)))
-    BL = C * B                                          # streams per launch
-    n_launch = -(-K // C)
+    C, BL, n_launch, launch_sizes = launch_plan(K, B, strong, args.coalesce)
     P = args.inflight or (min(2, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
@@ -240,7 +238,7 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
 
     def launch_streams(j):
         """streams of launch j of the timed region (the last one may hold fewer steps)"""
-        return BL if j < n_launch - 1 else (K - j * C) * B
+        return launch_sizes[j]
 
     kt = {k: 0.0 for k in names}
     nt = [0]
@@ -759,6 +757,17 @@ def host_path(L, fsk, xh, B, N, baud, mark, space, dev, cap, sym_per_stream, out
                 a.close()
     res["value"] = res["stream_of_batches"]["value"]
     return res
+
+
+def launch_plan(K, B, strong, coalesce=0):
+    """(C, BL, n_launch, streams of each launch) for K timed steps of B
+    streams per rank: a strong-scaling shard too small to fill the GPU alone
+    takes C consecutive global batches per launch (>= 4096 streams, what one
+    headline batch holds); the last launch holds the remaining steps."""
+    C = max(1, min(K, coalesce or (-(-4096 // B) if strong else 1)))
+    n_launch = -(-K // C)
+    sizes = [C * B] * (n_launch - 1) + [(K - (n_launch - 1) * C) * B]
+    return C, C * B, n_launch, sizes
 
 
 def default_inflight(K, cap=20):

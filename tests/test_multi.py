@@ -131,3 +131,22 @@ def test_bench_gather_bookkeeping_gloo(tmp_path, world, B_global, corrupt, C):
     bad, same = list(np.load(out))
     assert same == "True"
     assert bad == ("[]" if corrupt is None else f"[{corrupt}]")
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_bench_launch_plan(world):
+    """bench.py's steps per launch: every step's streams are launched exactly
+    once (K x the rank's shard), launches hold >= 4096 streams on small
+    strong-scaling shards, weak scaling stays one step per launch."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
+    import bench
+    for K in (1, 5, 20, 64):
+        B = bench.workload_sizes("ofdm8", 0, world, 0)[0]
+        C, BL, n, sizes = bench.launch_plan(K, B, True)
+        assert C == min(K, max(1, -(-4096 // B))) and BL == C * B and len(sizes) == n
+        assert sum(sizes) == K * B and all(0 < x <= BL and x % B == 0 for x in sizes)
+        assert all(x == BL for x in sizes[:-1])
+        Bw = bench.workload_sizes("qpsk9600", 0, world, 0)[0]
+        assert bench.launch_plan(K, Bw, False) == (1, Bw, K, [Bw] * K)
