@@ -56,6 +56,7 @@ class FskPlan:
         self.handle = h
         self.out_cap = int(lib().amr_fsk_plan_out_capacity(h))
         self.fft_length = int(lib().amr_fsk_plan_fft_length(h))
+        self.live_columns = bool(lib().amr_fsk_plan_live_columns(h))
 
     def __del__(self):
         h = getattr(self, "handle", None)

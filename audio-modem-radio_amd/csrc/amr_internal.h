@@ -65,6 +65,55 @@ struct PskBuffers {
   int64_t* sync_idx;      // [B]
 };
 
+// FSK live-column layout.  A four-step length n = n1 * n2
+// (sample i = j1 + n1 * j2) with n1 % sps == 0: every decision window of
+// fsk_demodulate (bits[i - sps//4 : i + sps//4] at i = sps//2 + k*sps,
+// modem.py:320-321) holds samples whose residue mod sps lies in
+// [w0, w0 + nw), w0 = sps//2 - sps//4, nw = 2*(sps//4) -- whole columns j1
+// of the four-step grid ("live" columns; 120 of 300 at sps 10).  The other
+// columns feed no decision.  Per stream the filter output z is stored as
+//   L: [j2][l]  the live columns  (nl = n1 / sps * nw of them)
+//   D: [j2][d]  the dead columns  (nd = n1 - nl), right after L
+// and the Hilbert filter's intermediates are kept only where a later pass
+// reads them (fsk_api.cpp, fft_kernels.hip *_live kernels).
+struct LiveCols {
+  int on;                 // 0: natural layout [i]
+  int n1, n2;
+  int sps, w0, nw;        // live residues w0 .. w0 + nw - 1 (mod sps)
+  int nl, nd;             // live / dead column counts
+  float inv_n1, inv_sps, inv_nw, inv_ndp;   // reciprocals for lc_div (ndp = sps - nw)
+};
+
+// floor(i / d) for 0 <= i < 2^20 given inv = 1/d rounded to float, d <= 625:
+// (i + 0.5) / d is >= 0.5/d away from an integer, the float product errs by
+// < 2^-22 * i / d <= 0.25 / d (plan creation checks every index it uses)
+__host__ __device__ inline int lc_div(int i, float inv) { return (int)(((float)i + 0.5f) * inv); }
+
+// column j1 -> its index among the live (l) or dead (d) columns
+__host__ __device__ inline int lc_col_pos(const LiveCols& m, int j1, bool& live) {
+  const int a = lc_div(j1, m.inv_sps);
+  const int v = j1 - a * m.sps;
+  live = (unsigned)(v - m.w0) < (unsigned)m.nw;
+  return live ? a * m.nw + (v - m.w0) : a * (m.sps - m.nw) + (v < m.w0 ? v : v - m.nw);
+}
+__host__ __device__ inline int lc_live_col(const LiveCols& m, int l) {
+  const int a = lc_div(l, m.inv_nw);
+  return a * m.sps + m.w0 + (l - a * m.nw);
+}
+__host__ __device__ inline int lc_dead_col(const LiveCols& m, int d) {
+  const int ndp = m.sps - m.nw;
+  const int a = lc_div(d, m.inv_ndp);
+  const int v = d - a * ndp;
+  return a * m.sps + (v < m.w0 ? v : v + m.nw);
+}
+// sample i of a stream -> its offset in the stream's [L | D] block
+__host__ __device__ inline int64_t lc_zoff(const LiveCols& m, int i) {
+  const int j2 = lc_div(i, m.inv_n1);
+  bool live;
+  const int pos = lc_col_pos(m, i - j2 * m.n1, live);
+  return live ? (int64_t)j2 * m.nl + pos : (int64_t)m.nl * m.n2 + (int64_t)j2 * m.nd + pos;
+}
+
 // FSK (fsk_kernels.hip): both tones' band-pass filters, lane = (stream, tone)
 struct FskParams {
   int64_t n;        // samples per stream
@@ -76,6 +125,7 @@ struct FskParams {
   int64_t rn1, rn2; // compare-bit layout (fft.h fft_bits_stride)
   int64_t bits_stride;
   float inv_rn1;
+  LiveCols lc;      // lc.on: z and the compare bits in the live-column layout
 };
 
 struct FskIir {            // [tone][tap], tone 0 = mark

@@ -255,26 +255,59 @@ int64_t row_s1_bytes(const amr_psk_plan* pl) {
 int64_t row_s3_bytes(const amr_psk_plan* pl) {
   return std::max(2 * pl->groups * pl->m2_pairs * kWave * 16, lane_s3_bytes(pl));
 }
-// grow s1 / s3 to the row layout's sizes (its forward outputs are full length)
-int ensure_row_buffers(amr_psk_plan* pl) {
-  const int64_t b1 = kFrontSlack * 8 + row_s1_bytes(pl), b3 = kFrontSlack * 8 + row_s3_bytes(pl);
-  for (auto [base, have, want] : {std::tuple<double**, int64_t*, int64_t>{&pl->s1_base, &pl->s1_bytes, b1},
-                                  std::tuple<double**, int64_t*, int64_t>{&pl->s3_base, &pl->s3_bytes, b3}}) {
-    if (*have >= want) continue;
-    HIP_TRY(hipStreamSynchronize(pl->stream));
+// Grow one scratch buffer to `want` bytes.  The new block is allocated before
+// the old one is released, so a failed grow leaves the plan exactly as it was
+// (its pointers still valid for the layout that fits); only when that fails
+// is the old block freed first (tight memory), and if even then the new size
+// does not fit the old size is restored, or the buffer is left empty (NULL,
+// 0 bytes) -- run_psk re-checks the sizes before every launch and refuses a
+// plan whose buffers are too small instead of handing the kernels freed memory.
+int grow_scratch(amr_psk_plan* pl, double** base, int64_t* have, int64_t want) {
+  if (*have >= want && *base) return AMR_OK;
+  static const bool fail_grow = [] {             // test hook: make every grow fail
+    const char* e = std::getenv("AMR_TEST_FAIL_SCRATCH_GROW");
+    return e && e[0] == '1';
+  }();
+  HIP_TRY(hipStreamSynchronize(pl->stream));     // queued work may still use the old block
+  double* nb = nullptr;
+  hipError_t e = fail_grow ? hipErrorOutOfMemory : hipMalloc(&nb, (size_t)want);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    const int64_t old = *have;
     HIP_TRY(hipFree(*base));
     *base = nullptr;
-    hipError_t e = hipMalloc(base, (size_t)want);
+    *have = 0;
+    pl->scratch_bytes -= old;
+    e = fail_grow ? hipErrorOutOfMemory : hipMalloc(&nb, (size_t)want);
     if (e != hipSuccess) {
-      *have = 0;
-      return fail(AMR_E_NOMEM, "hipMalloc(" + std::to_string(want) + " B): " + hipGetErrorString(e));
+      (void)hipGetLastError();
+      if (old > 0 && hipMalloc(base, (size_t)old) == hipSuccess) {
+        *have = old;
+        pl->scratch_bytes += old;
+      } else {
+        (void)hipGetLastError();
+        *base = nullptr;
+      }
+      return fail(AMR_E_NOMEM, "hipMalloc(" + std::to_string(want) + " B) for plan scratch: " + hipGetErrorString(e));
     }
-    pl->scratch_bytes += want - *have;
-    *have = want;
+  } else {
+    HIP_TRY(hipFree(*base));
+    pl->scratch_bytes -= *have;
   }
-  pl->s1 = pl->s1_base + kFrontSlack;
-  pl->s3 = pl->s3_base + kFrontSlack;
+  *base = nb;
+  pl->scratch_bytes += want;
+  *have = want;
   return AMR_OK;
+}
+
+// s1 / s3 at least b1 / b3 bytes (incl. the front slack); the kernel pointers
+// follow the (possibly new) blocks
+int ensure_scratch(amr_psk_plan* pl, int64_t b1, int64_t b3) {
+  int rc = grow_scratch(pl, &pl->s1_base, &pl->s1_bytes, b1);
+  if (rc == AMR_OK) rc = grow_scratch(pl, &pl->s3_base, &pl->s3_bytes, b3);
+  pl->s1 = pl->s1_base ? pl->s1_base + kFrontSlack : nullptr;
+  pl->s3 = pl->s3_base ? pl->s3_base + kFrontSlack : nullptr;
+  return rc;
 }
 }  // namespace
 
@@ -433,7 +466,7 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
       // s1 doubles as the symbol buffer [2G][S][64] after the band-pass (psk_common.h sym_index)
       // s1 / s3 sized for the lane layout (checkpoints, symbols, K3x's slots);
       // the row layout's full-length intermediates are allocated on its first
-      // call (ensure_row_buffers)
+      // call (ensure_scratch)
       {(void**)&pl->s1_base, kFrontSlack * 8 + lane_s1_bytes(pl)},
       {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
       {(void**)&pl->s3_base, kFrontSlack * 8 + lane_s3_bytes(pl)},
@@ -580,8 +613,14 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   const bool lane_ok = pl->bp.nt == 9 && pl->p.lp_sym;
   const bool lane = lane_ok && (lane_force >= 0 ? lane_force == 1 : live >= kLaneMinLiveStreams);
   pl->last_layout = lane ? AMR_LAYOUT_LANE : AMR_LAYOUT_ROW;
-  if (!lane && pl->p.n_sym >= 2)
-    if (int rc = ensure_row_buffers(pl)) return rc;
+  if (pl->p.n_sym >= 2) {
+    // the sizes this layout's kernels assume (the row layout's full-length
+    // intermediates are allocated on its first call); a plan whose earlier
+    // grow failed re-tries here and fails cleanly if it still cannot
+    const int64_t b1 = kFrontSlack * 8 + (lane ? lane_s1_bytes(pl) : row_s1_bytes(pl));
+    const int64_t b3 = kFrontSlack * 8 + (lane ? lane_s3_bytes(pl) : row_s3_bytes(pl));
+    if (int rc = ensure_scratch(pl, b1, b3)) return rc;
+  }
   PskBuffers b{};
   b.x = d_x;
   b.x_stride = x_stride;

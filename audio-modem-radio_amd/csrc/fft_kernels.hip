@@ -466,6 +466,168 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
       });
 }
 
+// ---- the Hilbert filter in the live-column layout (amr_internal.h LiveCols) --
+// Per stream: zb = [L | D] (the band-pass output z, live columns then dead
+// columns, rows j2) and cb = C [nl * n2] (the live columns' transform).
+//   column pass  live tiles  L -> C   (z's live columns stay intact: the
+//                                      final pass reads them for |a|)
+//                dead tiles  D -> D   (in place)
+//   middle pass  rows k2 of T from C (live c) and D (dead c); writes only
+//                the live outputs k2' (no later pass reads the others), into
+//                C row k2 at the live index of k2' -- the positions it read
+//   final pass   live columns k2' of C (DFT_n2 down the column), conj, 1/n,
+//                envelopes against z's live samples in L, compare bits
+// so the middle pass writes 40 % and the final pass reads 2 x 40 % of a full
+// pass at sps 10, and the plan holds 1.4 x n complex per
+// stream instead of 3 x.
+template <int PC, int QC>
+__global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
+                                                              LiveCols lc) {
+  extern __shared__ __attribute__((aligned(16))) double2 smem[];
+  const int tl = (lc.nl + kFftTile - 1) / kFftTile, tiles = tl + (lc.nd + kFftTile - 1) / kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int tile = (int)(lb - b * tiles);
+  if (b >= batch) return;
+  const FftLen& f = d.a;
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
+  const bool live = tile < tl;
+  const int c0 = (live ? tile : tile - tl) * kFftTile;
+  const int rl = live ? lc.nl : lc.nd;                  // row length of this region
+  const int64_t n2 = d.n2;
+  // src and dst alias for the dead columns (in place): no __restrict__
+  const double2* src = zb + (size_t)b * d.n + (live ? 0 : (size_t)lc.nl * n2) + c0;
+  double2* dst = live ? cb + (size_t)b * lc.nl * n2 + c0 : zb + (size_t)b * d.n + (size_t)lc.nl * n2 + c0;
+  const int ncol = min(kFftTile, rl - c0);
+  double2* twl = twl_of(smem, f);
+  run_stage1<false, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) { return t < ncol ? src[(unsigned)(t + rl * (j + Q * q))] : make_double2(0.0, 0.0); },
+      [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; }, true);
+  __syncthreads();
+  run_stage2<true, PC, QC>(
+      f, twl, [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; },
+      [&](int t, int m, int p, double2 v) {
+        if (t < ncol) dst[(unsigned)(t + rl * (m + P * p))] = v;
+      },
+      false,
+      [&](int t, int m, double2& base, double2& step) {   // W_n^(j1 (m + P p)), j1 = the column's index
+        const int c = c0 + (t < ncol ? t : 0);
+        const int j1 = live ? lc_live_col(lc, c) : lc_dead_col(lc, c);
+        base = twn(d, (unsigned)(j1 * m));
+        step = twn(d, (unsigned)(j1 * P));
+      });
+}
+
+template <int PC, int QC>
+__global__ __launch_bounds__(kFftThreads) void k_fft_mid_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
+                                                             LiveCols lc) {
+  extern __shared__ __attribute__((aligned(16))) double2 smem[];
+  const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int r0 = (int)(lb - b * tiles) * kFftTile;
+  if (b >= batch) return;
+  const FftLen& f = d.c;
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
+  const int64_t n = d.n;
+  const int n2 = d.n2;
+  const int nrow = min(kFftTile, d.n2 - r0);
+  // rows k2 = r0 + t: live elements in C, dead ones in D (in place: no __restrict__)
+  double2* crow = cb + (size_t)b * lc.nl * n2 + (size_t)r0 * lc.nl;
+  const double2* drow = zb + (size_t)b * n + (size_t)lc.nl * n2 + (size_t)r0 * lc.nd;
+  auto y_ld = [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; };
+  auto y_st = [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; };
+  double2* twl = twl_of(smem, f);
+  run_stage1<true, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) {
+        if (t >= nrow) return make_double2(0.0, 0.0);
+        bool lv;
+        const int pos = lc_col_pos(lc, j + Q * q, lv);
+        return lv ? crow[(unsigned)(t * lc.nl + pos)] : drow[(unsigned)(t * lc.nd + pos)];
+      },
+      y_st, true);
+  __syncthreads();
+  run_stage2<false, PC, QC>(
+      f, twl, y_ld,
+      [&](int t, int m, int p, double2 v) {
+        const int c = m + P * p;
+        const unsigned k = (unsigned)(r0 + t + n2 * c);
+        v = hilbert_mul(v, k, n);
+        const int qq = QC ? c / QC : fdiv(c, f.inv_r2);
+        smem[t * S + (c - Q * qq) + Qp * qq] = conj2(v);
+      },
+      true);
+  __syncthreads();
+  run_stage1<false, PC, QC>(f, twl, y_ld, y_st);
+  __syncthreads();
+  run_stage2<true, PC, QC>(
+      f, twl, y_ld,
+      [&](int t, int m, int p, double2 v) {
+        bool lv;
+        const int pos = lc_col_pos(lc, m + P * p, lv);      // output k2' = m + P p
+        if (t < nrow && lv) crow[(unsigned)(t * lc.nl + pos)] = v;
+      },
+      false,
+      [&](int t, int m, double2& base, double2& step) {   // W_n^(k2 (m + P p))
+        base = twn(d, (unsigned)((r0 + t) * m));
+        step = twn(d, (unsigned)((r0 + t) * P));
+      });
+}
+
+// final pass: live columns l0 .. l0+7 of C (length n2 each, stride nl) ->
+// DFT, conj, 1/n -> compare against z's live samples (L) -> bits, byte
+// (l0 / 8) * n2 + k1' (the decide kernel's live addressing)
+template <int PC, int QC>
+__global__ __launch_bounds__(kFftThreads) void k_fft_rows_live(const double2* __restrict__ zb,
+                                                              const double2* __restrict__ cb, FftDesc d,
+                                                              int64_t batch, double scale, FftEpi e, LiveCols lc) {
+  extern __shared__ __attribute__((aligned(16))) double2 smem[];
+  const int tiles = (lc.nl + kFftTile - 1) / kFftTile;
+  const int64_t lb = xcd_block();
+  const int64_t b = lb / tiles;
+  const int l0 = (int)(lb - b * tiles) * kFftTile;
+  if (b >= batch) return;
+  const FftLen& f = d.a;
+  const int P = PC ? PC : f.r1, Q = QC ? QC : f.r2, L = P * Q;
+  const int S = PC ? fft_row_stride(PC, QC) : f.S, Qp = fft_block(Q);
+  const int nl = lc.nl;
+  const int ncol = min(kFftTile, nl - l0);
+  const double2* __restrict__ src = cb + (size_t)b * nl * d.n2 + l0;
+  const double2* __restrict__ zl = zb + (size_t)b * d.n + l0;     // L: [k1'][l]
+  double2* twl = twl_of(smem, f);
+  constexpr bool kPre = QC > 0;
+  double2 zp[kPre ? QC : 1];
+  if constexpr (kPre) {
+    const int t = threadIdx.x & (kFftTile - 1), m = threadIdx.x / kFftTile;
+    if (threadIdx.x < kFftTile * PC && t < ncol) {
+#pragma unroll
+      for (int p = 0; p < QC; ++p) zp[p] = zl[(unsigned)(t + nl * (m + PC * p))];
+    }
+  }
+  run_stage1<false, PC, QC>(
+      f, twl,
+      [&](int t, int j, int q) { return t < ncol ? src[(unsigned)(t + nl * (j + Q * q))] : make_double2(0.0, 0.0); },
+      [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; }, true);
+  __syncthreads();
+  run_stage2<false, PC, QC>(
+      f, twl, [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; },
+      [&](int t, int m, int p, double2 v) {
+        const int kk = m + P * p;
+        bool gt = false;
+        if (t < ncol) {
+          v = make_double2(v.x * scale, -v.y * scale);
+          if constexpr (kPre) gt = env_gt(zp[p], v);
+          else gt = env_gt(zl[(unsigned)(t + nl * kk)], v);
+        }
+        const uint64_t mask = __ballot(gt);
+        if (t == 0) e.bits[(size_t)b * e.bits_stride + (size_t)(l0 >> 3) * L + kk] = (uint8_t)(mask >> (threadIdx.x & 56));
+      });
+}
+
 // Bluestein (n not 5-smooth): X_k = conj(w_k) * sum_j (x_j conj(w_j)) w_(k-j),
 // w_j = exp(i pi j^2 / n), as a length-M circular convolution, M >= 2n-1.
 //   pre:  a[b][j] = x[b][j] * conj(w_j) (j < n), 0 (n <= j < M); inv conjugates x
@@ -614,6 +776,32 @@ hipError_t launch_fft_filter(const double2* in, double2* t1, double2* t2, double
   return hipGetLastError();
 }
 
+// The Hilbert filter + envelope compare of launch_fft_filter (kHilbert,
+// kEnvelope) in the live-column layout: zb = [B][L | D] (z), cb = [B][nl * n2].
+hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, int64_t batch, const LiveCols& lc,
+                                   const FftEpi& epi, hipStream_t st) {
+  if (!lc.on || epi.mode != kEnvelope) return hipErrorInvalidValue;
+  const int tl = (lc.nl + kFftTile - 1) / kFftTile, td = (lc.nd + kFftTile - 1) / kFftTile;
+  const unsigned gcol = grid8(batch * (tl + td));
+  const unsigned gmid = grid8(batch * ((d.n2 + kFftTile - 1) / kFftTile));
+  const unsigned gfin = grid8(batch * tl);
+  const double scale = 1.0 / (double)d.n;
+#define COLSL(P, Q) \
+  hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, batch, lc)
+  AMR_FFT_PQ(d.a, COLSL);
+#undef COLSL
+#define MIDL(P, Q) \
+  hipLaunchKernelGGL((k_fft_mid_live<P, Q>), dim3(gmid), dim3(kFftThreads), fft_smem_bytes(d.c), st, zb, cb, d, batch, lc)
+  AMR_FFT_PQ(d.c, MIDL);
+#undef MIDL
+#define FINL(P, Q)                                                                                          \
+  hipLaunchKernelGGL((k_fft_rows_live<P, Q>), dim3(gfin), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, \
+                     batch, scale, epi, lc)
+  AMR_FFT_PQ(d.a, FINL);
+#undef FINL
+  return hipGetLastError();
+}
+
 hipError_t launch_bs_pre(const double2* x, double2* a, const double2* w, int64_t n, int64_t M, int64_t batch,
                          bool inverse, hipStream_t st) {
   const int64_t tot = batch * M;
@@ -739,7 +927,8 @@ static hipError_t fft_set_smem(int bytes) {
       (const void*)k_fft_cols<false, P, Q>, (const void*)k_fft_cols<true, P, Q>,
       (const void*)k_fft_mid<kHilbert, P, Q>, (const void*)k_fft_mid<kMulTab, P, Q>,
       (const void*)k_fft_rows<false, kStore, P, Q>, (const void*)k_fft_rows<true, kStore, P, Q>,
-      (const void*)k_fft_rows<true, kEnvelope, P, Q>, (const void*)k_fft_rows<true, kEnvOut, P, Q>};
+      (const void*)k_fft_rows<true, kEnvelope, P, Q>, (const void*)k_fft_rows<true, kEnvOut, P, Q>,
+      (const void*)k_fft_cols_live<P, Q>, (const void*)k_fft_mid_live<P, Q>, (const void*)k_fft_rows_live<P, Q>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;

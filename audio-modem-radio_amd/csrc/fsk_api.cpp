@@ -308,9 +308,14 @@ struct amr_fsk_plan {
   int64_t max_streams = 0;
   int64_t out_cap = 0;
   // HBM scratch
-  double2* z = nullptr;        // [B][n]
-  double2* u = nullptr;        // [B][M]  (also F1's checkpoint scratch)
-  double2* v = nullptr;        // [B][M]
+  // natural layout (p.lc.on == 0): z [B][n], u / v [B][M] (u also F1's
+  // checkpoint scratch).  Live-column layout (p.lc.on, amr_internal.h
+  // LiveCols): z = [B][L | D] (n per stream), u = C [B][nl * n2] -- also F1's
+  // checkpoint scratch and, on the host entries, the staged input -- and no v.
+  double2* z = nullptr;
+  double2* u = nullptr;
+  double2* v = nullptr;
+  int64_t u_bytes = 0;
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
   int64_t scratch_bytes = 0;
@@ -344,62 +349,187 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   delete pl;
 }
 
-// F1, F2: x -> cmp (or -> the two envelopes in hilbert_out(u, v) when env_out).  Caller holds mu.
-int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
-  hipStream_t st = pl->stream;
-  auto mark = [&](int slot, int which) -> hipError_t {
-    if (!pl->timing) return hipSuccess;
-    pl->ev_used[slot] = true;
-    return hipEventRecord(pl->ev[slot][which], st);
-  };
-  HIP_TRY(mark(AMR_TF_BANDPASS, 0));
-  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, pl->p, pl->f, st));
-  HIP_TRY(mark(AMR_TF_BANDPASS, 1));
+hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which) {
+  if (!pl->timing) return hipSuccess;
+  pl->ev_used[slot] = true;
+  return hipEventRecord(pl->ev[slot][which], pl->stream);
+}
+
+// F1 for the nb streams s0 .. s0 + nb - 1 of the batch: x (nb rows,
+// x_stride apart) -> z's blocks of those streams.  Caller holds mu.
+int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t nb, int64_t x_stride, int64_t s0,
+               double* scratch) {
+  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, nb, scratch, pl->z + (size_t)s0 * pl->p.n, pl->p, pl->f,
+                              pl->stream));
+  return AMR_OK;
+}
+
+// F2 over the B streams of z: the Hilbert filter, whose last pass forms both
+// envelopes and packs the compare bits (or, env_out on a natural-layout
+// plan, stores the envelopes themselves in hilbert_out(u, v)).
+int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   FftEpi env{};
   env.mode = env_out ? kEnvOut : kEnvelope;
   env.z = pl->z;
   env.bits = pl->cmp;
   env.bits_stride = pl->p.bits_stride;
-  // one timing slot for the whole Hilbert filter (column, middle and final row passes)
-  HIP_TRY(mark(AMR_TF_HILBERT, 0));
-  HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, st));
-  HIP_TRY(mark(AMR_TF_HILBERT, 1));
+  // one timing slot for the whole Hilbert filter (column, middle and final passes)
+  HIP_TRY(mark_fsk(pl, AMR_TF_HILBERT, 0));
+  if (pl->p.lc.on) {
+    if (env_out) return fail(AMR_E_INVALID, "live-column plan: envelopes go through a natural-layout plan");
+    HIP_TRY(launch_fft_hilbert_live(pl->z, pl->u, pl->fft.d, B, pl->p.lc, env, pl->stream));
+  } else {
+    HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, pl->stream));
+  }
+  HIP_TRY(mark_fsk(pl, AMR_TF_HILBERT, 1));
+  return AMR_OK;
+}
+
+// F1, F2 on a device-resident batch: x -> cmp (or the envelopes).  Caller holds mu.
+int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
+  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
+  if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, 0, reinterpret_cast<double*>(pl->u))) return rc;
+  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
+  return run_fsk_f2(pl, B, env_out);
+}
+
+int check_fsk_args(amr_fsk_plan* pl, int dtype, int64_t B, int64_t x_stride, int64_t out_stride) {
+  if (B < 0 || B > pl->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (dtype_size(dtype) == 0) return fail(AMR_E_INVALID, "unknown dtype");
+  if (x_stride < pl->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (out_stride < pl->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
+  return AMR_OK;
+}
+
+// no decision window (sps // 4 == 0): empty bit string -> b''   (modem.py:320-323)
+int fsk_empty_outputs(amr_fsk_plan* pl, int64_t B, int64_t* d_len, int64_t* d_sync) {
+  HIP_TRY(gate_wait(pl->gate, pl->stream));
+  HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, pl->stream));
+  HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, pl->stream));
+  return AMR_OK;
+}
+
+// F3: compare bits -> decided words -> sync + pack.  Caller holds mu.
+int run_fsk_back(amr_fsk_plan* pl, int64_t B, uint8_t* d_out, int64_t out_stride, int64_t* d_len, int64_t* d_sync) {
+  hipStream_t st = pl->stream;
+  HIP_TRY(mark_fsk(pl, AMR_TF_DECIDE, 0));
+  HIP_TRY(launch_fsk_decide(pl->cmp, pl->words, B, pl->p, st));
+  HIP_TRY(gate_wait(pl->gate, st));             // the outputs: after any gather still reading them
+  HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
+  HIP_TRY(mark_fsk(pl, AMR_TF_DECIDE, 1));
   return AMR_OK;
 }
 
 int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, uint8_t* d_out,
             int64_t out_stride, int64_t* d_len, int64_t* d_sync) {
-  if (B < 0 || B > pl->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
-  if (dtype_size(dtype) == 0) return fail(AMR_E_INVALID, "unknown dtype");
-  if (x_stride < pl->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
-  if (out_stride < pl->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
+  if (int rc = check_fsk_args(pl, dtype, B, x_stride, out_stride)) return rc;
   for (bool& u : pl->ev_used) u = false;
   if (B == 0) return AMR_OK;
-  hipStream_t st = pl->stream;
-  if (pl->p.n_bits == 0) {
-    // no decision window (sps // 4 == 0): empty bit string -> b''   (modem.py:320-323)
-    HIP_TRY(gate_wait(pl->gate, st));
-    HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
-    HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
-    return AMR_OK;
-  }
+  if (pl->p.n_bits == 0) return fsk_empty_outputs(pl, B, d_len, d_sync);
   if (int rc = run_fsk_front(pl, d_x, dtype, B, x_stride, false)) return rc;
-  if (pl->timing) {
-    pl->ev_used[AMR_TF_DECIDE] = true;
-    HIP_TRY(hipEventRecord(pl->ev[AMR_TF_DECIDE][0], st));
+  return run_fsk_back(pl, B, d_out, out_stride, d_len, d_sync);
+}
+
+constexpr int64_t kStageAlign = 256;
+int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Streams per staged chunk of a live-column plan's host entries: the input
+// rows (n * es bytes each) and F1's checkpoints for them share C.  A multiple
+// of F1's 32-stream groups (or the whole batch).
+int64_t live_stage_chunk(const amr_fsk_plan* pl, int64_t es, int64_t B) {
+  const int64_t n = pl->p.n;
+  auto need = [&](int64_t nb) {
+    return align_up(nb * n * es, kStageAlign) + fsk_bandpass_scratch_bytes(nb, n, pl->p.pad);
+  };
+  if (need(B) <= pl->u_bytes) return B;
+  int64_t nb = (pl->u_bytes / (n * es + fsk_bandpass_scratch_bytes(32, n, pl->p.pad) / 32 + 1)) / 32 * 32;
+  while (nb > 32 && need(nb) > pl->u_bytes) nb -= 32;
+  return nb < 32 ? std::min<int64_t>(B, 32) : nb;     // the plan sizes C for one group at least
+}
+
+// Host input -> F1 for a live-column plan: the batch is uploaded into C in
+// chunks (live_stage_chunk), each filtered into z before the next arrives.
+// async: hipMemcpy(2D)Async on the plan's stream (page-locked input overlaps);
+// else the synchronous copies of copy_batch_h2d.  Caller holds mu.
+int stage_f1_live(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride, bool async) {
+  const int64_t es = dtype_size(dtype);
+  const int64_t n = pl->p.n;
+  const int64_t chunk = live_stage_chunk(pl, es, B);
+  uint8_t* c = reinterpret_cast<uint8_t*>(pl->u);
+  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
+  for (int64_t s0 = 0; s0 < B; s0 += chunk) {
+    const int64_t nb = std::min(chunk, B - s0);
+    const uint8_t* src = static_cast<const uint8_t*>(x) + (size_t)(s0 * x_stride * es);
+    if (async) {
+      if (x_stride == n)
+        HIP_TRY(hipMemcpyAsync(c, src, (size_t)(nb * n * es), hipMemcpyHostToDevice, pl->stream));
+      else
+        HIP_TRY(hipMemcpy2DAsync(c, (size_t)(n * es), src, (size_t)(x_stride * es), (size_t)(n * es), (size_t)nb,
+                                 hipMemcpyHostToDevice, pl->stream));
+    } else if (int rc = copy_batch_h2d(c, src, n * es, x_stride * es, nb, pl->stream)) {
+      return rc;
+    }
+    double* scratch = reinterpret_cast<double*>(c + align_up(nb * n * es, kStageAlign));
+    if (int rc = run_fsk_f1(pl, c, dtype, nb, n, s0, scratch)) return rc;
   }
-  HIP_TRY(launch_fsk_decide(pl->cmp, pl->words, B, pl->p, st));
-  HIP_TRY(gate_wait(pl->gate, st));             // the outputs: after any gather still reading them
-  HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
-  if (pl->timing) HIP_TRY(hipEventRecord(pl->ev[AMR_TF_DECIDE][1], st));
+  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
   return AMR_OK;
 }
 
+// Natural-layout plans stage the host input in d_x (max_streams rows of up to 8 B per sample).
 int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride) {
   const int64_t es = dtype_size(dtype);
   const int64_t n = pl->p.n;
   if (!pl->d_x) HIP_TRY(hipMalloc(&pl->d_x, (size_t)(pl->max_streams * n * 8)));
   return copy_batch_h2d(pl->d_x, x, n * es, x_stride * es, B, pl->stream);
+}
+
+int ensure_out_staging(amr_fsk_plan* pl) {
+  if (pl->d_out) return AMR_OK;
+  HIP_TRY(hipMalloc(&pl->d_out, (size_t)(pl->max_streams * pl->out_cap)));
+  HIP_TRY(hipMalloc(&pl->d_len, (size_t)pl->max_streams * 8));
+  HIP_TRY(hipMalloc(&pl->d_sync, (size_t)pl->max_streams * 8));
+  return AMR_OK;
+}
+
+// Live-column layout for this plan (amr_internal.h LiveCols), or off: needs a
+// two-pass length n = n1 * n2 with n1 a multiple of sps and a decision window.
+// Every index the kernels use is checked here on the host (the float
+// divisions of lc_div, the [L | D] offsets as a bijection onto [0, n)).
+LiveCols plan_live_cols(const FftPlan& f, const FskParams& p) {
+  LiveCols lc{};
+  static const bool off = [] { const char* e = std::getenv("AMR_FSK_LIVE"); return e && e[0] == '0'; }();
+  const int64_t q = p.sps / 4, half = p.sps / 2;
+  if (off || f.bluestein || f.six || p.n_bits == 0 || q < 1) return lc;
+  const int n1 = f.d.n1, n2 = f.d.n2;
+  if (p.sps > n1 || n1 % p.sps != 0 || (int64_t)n1 * n2 != p.n) return lc;
+  lc.n1 = n1;
+  lc.n2 = n2;
+  lc.sps = (int)p.sps;
+  lc.w0 = (int)(half - q);
+  lc.nw = (int)(2 * q);
+  lc.nl = n1 / lc.sps * lc.nw;
+  lc.nd = n1 - lc.nl;
+  lc.inv_n1 = 1.0f / (float)n1;
+  lc.inv_sps = 1.0f / (float)lc.sps;
+  lc.inv_nw = 1.0f / (float)lc.nw;
+  lc.inv_ndp = 1.0f / (float)(lc.sps - lc.nw);
+  if (lc.nd < 1) return LiveCols{};
+  for (int j1 = 0; j1 < n1; ++j1) {
+    bool live = false;
+    const int pos = lc_col_pos(lc, j1, live);
+    const int v = j1 % lc.sps;
+    if (live != (v >= lc.w0 && v < lc.w0 + lc.nw)) return LiveCols{};
+    if ((live ? lc_live_col(lc, pos) : lc_dead_col(lc, pos)) != j1) return LiveCols{};
+  }
+  std::vector<uint8_t> seen((size_t)p.n, 0);
+  for (int64_t i = 0; i < p.n; ++i) {
+    const int64_t o = lc_zoff(lc, (int)i);
+    if (o < 0 || o >= p.n || seen[(size_t)o]) return LiveCols{};
+    seen[(size_t)o] = 1;
+  }
+  lc.on = 1;
+  return lc;
 }
 
 }  // namespace
@@ -458,18 +588,31 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   p.rn1 = plain ? n : pl->fft.d.n1;
   p.rn2 = plain ? 1 : pl->fft.d.n2;
   if (pl->fft.six) pl->scratch_bytes += 2 * max_streams * M * 16;
-  p.bits_stride = fft_bits_stride(p.rn1, p.rn2);
+  p.lc = plan_live_cols(pl->fft, p);
+  p.bits_stride = p.lc.on ? (int64_t)((p.lc.nl + 7) >> 3) * p.rn2 : fft_bits_stride(p.rn1, p.rn2);
   p.inv_rn1 = 1.0f / (float)p.rn1;
   const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
+  if (p.lc.on) {
+    // C: the live columns' transform; before the column pass it holds F1's
+    // checkpoints and (host entries) the staged input -- 4 B per sample for
+    // float32 / int16 in one chunk, float64 in chunks of >= 32 streams
+    const int64_t g = std::min<int64_t>(max_streams, 32);
+    pl->u_bytes = std::max({max_streams * (int64_t)p.lc.nl * p.lc.n2 * 16,
+                            align_up(max_streams * n * 4, kStageAlign) + s1_bytes,
+                            align_up(g * n * 8, kStageAlign) + fsk_bandpass_scratch_bytes(g, n, p.pad)});
+  } else {
+    pl->u_bytes = std::max(max_streams * M * 16, s1_bytes);
+  }
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, max_streams * n * 16},
-      {(void**)&pl->u, std::max(max_streams * M * 16, s1_bytes)},
-      {(void**)&pl->v, max_streams * M * 16},
+      {(void**)&pl->u, pl->u_bytes},
+      {(void**)&pl->v, p.lc.on ? 0 : max_streams * M * 16},
       {(void**)&pl->cmp, max_streams * p.bits_stride},
       {(void**)&pl->words, max_streams * p.n_words * 4},
   };
   for (const A& a : allocs) {
+    if (a.bytes == 0) continue;
     e = hipMalloc(a.ptr, (size_t)a.bytes);
     if (e != hipSuccess) {
       fsk_plan_free(pl);
@@ -488,10 +631,13 @@ int amr_fsk_plan_destroy(amr_fsk_plan* plan) {
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
-  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host)
-  return plan->scratch_bytes + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
+  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host;
+  // a live-column plan stages its input inside C)
+  const int64_t staging = plan->p.lc.on ? 0 : plan->max_streams * plan->p.n * 8;
+  return plan->scratch_bytes + staging + plan->max_streams * (plan->out_cap + 16);
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
+int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
 
 int amr_fsk_plan_synchronize(amr_fsk_plan* plan) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
@@ -553,13 +699,18 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   if (out_stride < plan->out_cap - 1 || out_stride < 1) return fail(AMR_E_INVALID, "out_stride too small");
   if (B == 0) return AMR_OK;
   const int64_t cap = plan->out_cap;
-  if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
-  if (!plan->d_out) {
-    HIP_TRY(hipMalloc(&plan->d_out, (size_t)(plan->max_streams * cap)));
-    HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
-    HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
+  if (int rc = ensure_out_staging(plan)) return rc;
+  for (bool& u : plan->ev_used) u = false;
+  if (plan->p.n_bits == 0) {
+    if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
+  } else if (plan->p.lc.on) {
+    if (int rc = stage_f1_live(plan, x, dtype, B, x_stride, false)) return rc;
+    if (int rc = run_fsk_f2(plan, B, false)) return rc;
+    if (int rc = run_fsk_back(plan, B, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+  } else {
+    if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
+    if (int rc = run_fsk(plan, plan->d_x, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   }
-  if (int rc = run_fsk(plan, plan->d_x, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   if (int rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B,
                               plan->stream))
     return rc;
@@ -585,19 +736,24 @@ int amr_fsk_demod_host_async(amr_fsk_plan* plan, const void* x, int dtype, int64
   if (B == 0) return AMR_OK;
   const int64_t n = plan->p.n;
   const int64_t cap = plan->out_cap;
-  if (!plan->d_x) HIP_TRY(hipMalloc(&plan->d_x, (size_t)(plan->max_streams * n * 8)));
-  if (!plan->d_out) {
-    HIP_TRY(hipMalloc(&plan->d_out, (size_t)(plan->max_streams * cap)));
-    HIP_TRY(hipMalloc(&plan->d_len, (size_t)plan->max_streams * 8));
-    HIP_TRY(hipMalloc(&plan->d_sync, (size_t)plan->max_streams * 8));
-  }
+  if (int rc = ensure_out_staging(plan)) return rc;
   hipStream_t st = plan->stream;
-  if (x_stride == n)
-    HIP_TRY(hipMemcpyAsync(plan->d_x, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
-  else
-    HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
-                             hipMemcpyHostToDevice, st));
-  if (int rc = run_fsk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+  for (bool& u : plan->ev_used) u = false;
+  if (plan->p.n_bits == 0) {
+    if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
+  } else if (plan->p.lc.on) {
+    if (int rc = stage_f1_live(plan, x, dtype, B, x_stride, true)) return rc;
+    if (int rc = run_fsk_f2(plan, B, false)) return rc;
+    if (int rc = run_fsk_back(plan, B, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+  } else {
+    if (!plan->d_x) HIP_TRY(hipMalloc(&plan->d_x, (size_t)(plan->max_streams * n * 8)));
+    if (x_stride == n)
+      HIP_TRY(hipMemcpyAsync(plan->d_x, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
+    else
+      HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
+                               hipMemcpyHostToDevice, st));
+    if (int rc = run_fsk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+  }
   if (out_stride == cap)
     HIP_TRY(hipMemcpyAsync(out, plan->d_out, (size_t)(B * cap), hipMemcpyDeviceToHost, st));
   else
@@ -618,12 +774,51 @@ int amr_fsk_envelopes_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t
   if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
   if (B == 0) return AMR_OK;
   const int64_t n = plan->p.n;
-  if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
-  if (int rc = run_fsk_front(plan, plan->d_x, dtype, B, n, true)) return rc;
   std::vector<double> h((size_t)(B * n * 2));
-  HIP_TRY(hipMemcpyAsync(h.data(), hilbert_out(plan->fft, plan->u, plan->v), h.size() * 8, hipMemcpyDeviceToHost,
-                         plan->stream));
-  HIP_TRY(hipStreamSynchronize(plan->stream));
+  if (plan->p.lc.on) {
+    // the envelopes at every sample need the natural layout's full passes: run
+    // them on temporary buffers (a diagnostic entry, tests/test_gpu_fsk.py)
+    const int64_t M = plan->fft.M;
+    const int64_t ub = std::max(B * M * 16, fsk_bandpass_scratch_bytes(B, n, plan->p.pad));
+    double2 *z = nullptr, *u = nullptr, *v = nullptr;
+    void* xs = nullptr;
+    hipError_t e = hipMalloc(&z, (size_t)(B * n * 16));
+    if (e == hipSuccess) e = hipMalloc(&u, (size_t)ub);
+    if (e == hipSuccess) e = hipMalloc(&v, (size_t)(B * M * 16));
+    if (e == hipSuccess) e = hipMalloc(&xs, (size_t)(B * n * 8));
+    int rc = e == hipSuccess ? copy_batch_h2d(xs, x, n * dtype_size(dtype), x_stride * dtype_size(dtype), B,
+                                              plan->stream)
+                             : fail(AMR_E_NOMEM, std::string("envelope buffers: ") + hipGetErrorString(e));
+    if (rc == AMR_OK) {
+      FskParams pn = plan->p;
+      pn.lc = LiveCols{};
+      std::swap(plan->z, z);
+      std::swap(plan->u, u);
+      std::swap(plan->v, v);
+      std::swap(plan->p, pn);
+      rc = run_fsk_front(plan, xs, dtype, B, n, true);
+      if (rc == AMR_OK) {
+        e = hipMemcpyAsync(h.data(), hilbert_out(plan->fft, plan->u, plan->v), h.size() * 8, hipMemcpyDeviceToHost,
+                           plan->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(plan->stream);
+        if (e != hipSuccess) rc = fail(AMR_E_HIP, std::string("envelopes: ") + hipGetErrorString(e));
+      }
+      std::swap(plan->z, z);
+      std::swap(plan->u, u);
+      std::swap(plan->v, v);
+      std::swap(plan->p, pn);
+    }
+    (void)hipStreamSynchronize(plan->stream);
+    for (void* q : {(void*)z, (void*)u, (void*)v, xs})
+      if (q) (void)hipFree(q);
+    if (rc) return rc;
+  } else {
+    if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
+    if (int rc = run_fsk_front(plan, plan->d_x, dtype, B, n, true)) return rc;
+    HIP_TRY(hipMemcpyAsync(h.data(), hilbert_out(plan->fft, plan->u, plan->v), h.size() * 8, hipMemcpyDeviceToHost,
+                           plan->stream));
+    HIP_TRY(hipStreamSynchronize(plan->stream));
+  }
   for (int64_t i = 0; i < B * n; ++i) {
     mark_env[i] = h[(size_t)(2 * i)];
     space_env[i] = h[(size_t)(2 * i + 1)];

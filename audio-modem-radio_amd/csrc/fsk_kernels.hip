@@ -90,7 +90,14 @@ __host__ __device__ inline int64_t fsk_scratch_doubles_per_wave(int64_t n, int p
 // re-reading the forward outputs.  Input tiles are loaded 16 B
 // per lane and transposed through LDS; outputs are written back into the same
 // LDS slots and stored as 1 KiB rows of z (stream-major f_mark + i f_space).
-template <typename T, bool ZO>
+// LIVE: z in the live-column layout (amr_internal.h LiveCols), else [s][i].
+template <bool LIVE>
+__device__ __forceinline__ int64_t fsk_zoff(const FskParams& p, int64_t i) {
+  if constexpr (LIVE) return lc_zoff(p.lc, (int)i);
+  else return i;
+}
+
+template <typename T, bool ZO, bool LIVE>
 __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_stride, int64_t n_streams,
                                                      double* __restrict__ scratch, double2* __restrict__ z,
                                                      FskParams p, FskIir f) {
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   double* __restrict__ zd = reinterpret_cast<double*>(z);
   for (int64_t i = n - 1; i >= n_main; --i) {          // tail outputs, one sample at a time
     const double y = fsk_step<ZO>(zs, b, a, tl[(size_t)(i - n_main) * 64]);
-    if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
+    if (s < n_streams) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
   }
   if (n_tiles > 0) {
     double zf[6], zb[6];
@@ -212,12 +219,12 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       for (int k = kFskTile - 1; k >= 0; --k) yb[k][lane] = fsk_step<ZO>(zs, b, a, yb[k][lane]);
       __syncthreads();
       // 32 rows x 64 samples of z, one 1 KiB row per store instruction
-      const int64_t i0 = t * kFskTile;
+      const int64_t zo = fsk_zoff<LIVE>(p, t * kFskTile + lane);
 #pragma unroll 4
       for (int row = 0; row < 32; ++row) {
         const int64_t so = w * 32 + row;
         const double2 v = *reinterpret_cast<const double2*>(&yb[lane][2 * row]);
-        if (so < n_streams) z[(size_t)so * n + i0 + lane] = v;
+        if (so < n_streams) z[(size_t)so * n + zo] = v;
       }
       __syncthreads();
       __builtin_amdgcn_sched_barrier(0);
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-template <typename T, bool ZO>
+template <typename T, bool ZO, bool LIVE>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -351,7 +358,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     for (int64_t j = ntail - 1; j >= n - n_main; --j) (void)fsk_step<ZO>(zs, b, a, tb[(size_t)j * YP + lane]);
     for (int64_t i = n - 1; i >= n_main; --i) {
       const double y = fsk_step<ZO>(zs, b, a, tb[(size_t)(i - n_main) * YP + lane]);
-      if (s < n_streams) zd[((size_t)s * n + i) * 2 + tone] = y;
+      if (s < n_streams) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
     }
   }
   __syncthreads();                                     // the tail rows of yb are free again
@@ -375,14 +382,14 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     auto store_tile = [&](int bb, int64_t tz) {
       constexpr int RPS = 64 / TL;
       const double (*buf)[YP] = &yb[bb * TL];
-      const int64_t i0 = tz * TL;
       const int sub = lane / TL, k = lane % TL;
+      const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
 #pragma unroll 4
       for (int row = 0; row < 32; row += RPS) {
         const int rr = row + sub;
         const int64_t so = w * 32 + rr;
         const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
-        if (so < n_streams) z[(size_t)so * n + i0 + k] = v;
+        if (so < n_streams) z[(size_t)so * n + zo] = v;
       }
     };
     auto refwd = [&](v4u (&r)[NI], double (&c)[6], int64_t it) {
@@ -456,11 +463,22 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
       int64_t kk = (int64_t)(((float)lo + 0.5f) * p.inv_rn1);   // sample lo = r + rn1*kk
       int64_t r = lo - kk * p.rn1;
       int64_t ones = 0;
-      for (int64_t k = lo; k < hi; ++k) {
-        ones += (sb[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
-        if (++r == p.rn1) {
-          r = 0;
-          ++kk;
+      if (p.lc.on) {
+        // live-column bits: bit row = the column's live index; a window is
+        // nw consecutive live columns of one sps block, so one row kk
+        bool lv;
+        const int l0 = lc_col_pos(p.lc, (int)r, lv);
+        for (int64_t k = 0; k < hi - lo; ++k) {
+          const int64_t l = l0 + k;
+          ones += (sb[(l >> 3) * p.rn2 + kk] >> (l & 7)) & 1;
+        }
+      } else {
+        for (int64_t k = lo; k < hi; ++k) {
+          ones += (sb[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
+          if (++r == p.rn1) {
+            r = 0;
+            ++kk;
+          }
         }
       }
       word |= (2 * ones > hi - lo ? 1u : 0u) << (31 - u);
@@ -487,32 +505,38 @@ static bool fsk_zero_odd_taps(const FskIir& f) {
   return true;
 }
 
-template <bool ZO>
+template <bool ZO, bool LIVE>
 static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1,
                                         double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
   if (!fsk_one_wave()) {
     switch (dtype) {
-      case kF32: hipLaunchKernelGGL((k_fsk_bandpass2<float, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kF64: hipLaunchKernelGGL((k_fsk_bandpass2<double, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kI16: hipLaunchKernelGGL((k_fsk_bandpass2<int16_t, ZO>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF32: hipLaunchKernelGGL((k_fsk_bandpass2<float, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF64: hipLaunchKernelGGL((k_fsk_bandpass2<double, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kI16: hipLaunchKernelGGL((k_fsk_bandpass2<int16_t, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
   }
   switch (dtype) {
-    case kF32: hipLaunchKernelGGL((k_fsk_bandpass<float, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kF64: hipLaunchKernelGGL((k_fsk_bandpass<double, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kI16: hipLaunchKernelGGL((k_fsk_bandpass<int16_t, ZO>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kF32: hipLaunchKernelGGL((k_fsk_bandpass<float, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kF64: hipLaunchKernelGGL((k_fsk_bandpass<double, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kI16: hipLaunchKernelGGL((k_fsk_bandpass<int16_t, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
+// z: stream 0's block of this launch (callers staging a batch in chunks pass
+// the chunk's first stream); p.lc.on selects the live-column layout
 hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
                                const FskParams& p, const FskIir& f, hipStream_t st) {
-  return fsk_zero_odd_taps(f) ? launch_fsk_bandpass_t<true>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
-                              : launch_fsk_bandpass_t<false>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
+  const bool zo = fsk_zero_odd_taps(f);
+  if (p.lc.on)
+    return zo ? launch_fsk_bandpass_t<true, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
+              : launch_fsk_bandpass_t<false, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
+  return zo ? launch_fsk_bandpass_t<true, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
+            : launch_fsk_bandpass_t<false, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
 }
 
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,

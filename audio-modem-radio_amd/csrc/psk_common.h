@@ -76,19 +76,22 @@ __device__ __forceinline__ float tiny_min3(float acc, double a, double b) {
 // and differs from ocml's atan2 by an ulp on ~6 % of near-tie inputs -- the
 // ones where an ulp decides the sector.  Within |t| < 2^-29 of the diagonal
 // and for components of magnitude 2^-1015 .. 2^985 (~1e-306 .. 1e297), its
-// result is, bit for bit (tests/test_gpu_slicer.py; probed on 1.5 M near-tie
-// pairs in the build container, 1 in ~10^5 off by an ulp in the pi-side form):
+// result is, bit for bit (tests/test_gpu_slicer.py, tests/test_oracle_slicer.py):
 //   t  = (|y| - |x|) / (|y| + |x|)
 //   x > 0:  pi4 + (t + pi4_lo)                 x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
-// negated for y < 0, with pi4 / pi split into double hi + lo.  Outside that
-// domain (denormal or huge components, zeros, inf, NaN) ocml's atan2 is used.
+// negated for y < 0, with pi4 split into double hi + lo (pi4_lo = pi/4 - pi4)
+// and pi into hi + SVML's SHORT lo, 0x1.1a64p-53 (not pi - hi = 0x1.1a62633145c07p-53:
+// bisecting numpy's rounding boundaries in the pi-side form located exactly
+// this constant; with it 20 M near-tie angles agree bit for bit,
+// tests/test_oracle_slicer.py).  Outside that domain (denormal or huge
+// components, zeros, inf, NaN) ocml's atan2 is used.
 __device__ __forceinline__ bool numpy_atan2_near_diag(double y, double x, double& ang) {
   const double ay = fabs(y), ax = fabs(x);
   if (!(ax >= 0x1p-1015 && ax <= 0x1p985 && ay >= 0x1p-1015 && ay <= 0x1p985)) return false;
   const double t = (ay - ax) / (ay + ax);
   if (!(fabs(t) < 0x1p-29)) return false;
   const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;
-  const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53;
+  const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a64p-53;   // SVML's short pi_lo
   const double a = x > 0 ? pi4 + (t + pi4_lo) : pi - (pi4 - (pi_lo - (t + pi4_lo)));
   ang = y < 0 ? -a : a;
   return true;

@@ -995,17 +995,29 @@ __device__ __forceinline__ void cmul_np(double ar, double ai, double br, double 
   im = __builtin_fma(ar, bi, ai * br);
 }
 
-// K3x scratch: kExactSlots waves, each owning one [m2][64] double2 slot and
-// walking the groups g = slot, slot + kExactSlots, ... (flagged streams are
-// rare: silence, NaN/inf captures), so the scratch does not scale with B.
-constexpr int kExactSlots = 8;
-int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2) {
+// K3x scratch: one slot per workgroup, up to kExactSlots of them, each walking
+// the groups g = slot, slot + slots, ...  A slot keeps only the forward
+// pass's state (8 doubles per lane) at the start of every kExactTile
+// samples; the backward pass re-runs each tile forward from its checkpoint
+// into LDS and filters it backward from there (the lane kernels' scheme,
+// psk_lane_kernels.hip).  A slot is then m2/32 x 4 KiB (12 MB at n = 96 000)
+// instead of the m2 x 1 KiB (98 MB) a stored forward pass takes, so a batch
+// whose every stream is flagged (digital silence, gated captures,
+// AMR_FORCE_EXACT_LOWPASS) runs one workgroup per group up to 8192 streams.
+constexpr int kExactSlots = 128;
+constexpr int kExactTile = 32;
+int64_t psk_exact_slots(int64_t n_streams) {
   const int64_t g = (n_streams + kWave - 1) / kWave;
-  return (g < kExactSlots ? g : kExactSlots) * m2 * kWave * 16;
+  return g < kExactSlots ? g : kExactSlots;
+}
+int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2) {
+  const int64_t tiles = (m2 + kExactTile - 1) / kExactTile;
+  return psk_exact_slots(n_streams) * tiles * 8 * kWave * 8;
 }
 
 template <int NT>
 __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams p, Iir f) {
+  static_assert(NT == 5, "checkpoint layout holds 2 x 4 states");
   const int lane = threadIdx.x;
   const int64_t n_groups = (buf.n_streams + kWave - 1) / kWave;
   const int64_t n = p.n;
@@ -1013,9 +1025,12 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
   const int pad = p.pad2;
   const int64_t m2 = p.m2;
   const int64_t S = p.n_sym;
+  const int64_t tiles = (m2 + kExactTile - 1) / kExactTile;
   const double4* __restrict__ lo = reinterpret_cast<const double4*>(buf.lo);   // [n]: (lr, c1, li, c2)
-  double2* __restrict__ sc = reinterpret_cast<double2*>(buf.s3) + (size_t)blockIdx.x * m2 * kWave + lane;
+  // checkpoints [slot][tile][8][64] doubles
+  double* __restrict__ ck = buf.s3 + (size_t)blockIdx.x * tiles * 8 * kWave + lane;
   double* __restrict__ sym = buf.s1;
+  __shared__ double2 tile_out[kExactTile][kWave];
   for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
     const int64_t s = g * kWave + lane;
     const bool live = s < buf.n_streams && buf.flags[s] != 0;
@@ -1046,32 +1061,52 @@ __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams 
 #pragma unroll
       for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, e0.x, e0.y, zr[i], zc[i]);
     }
+    // forward pass: keep the state at the start of every tile
     double y0 = 0, y1 = 0;
-    for (int64_t j = 0; j < m2; ++j) {
-      const double2 e = ext(j);
-      df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, y0, y1);
-      sc[(size_t)j * kWave] = make_double2(y0, y1);
-    }
-    __threadfence();
+    for (int64_t t = 0; t < tiles; ++t) {
+      double* c = ck + (size_t)t * 8 * kWave;
 #pragma unroll
-    for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, y0, y1, zr[i], zc[i]);
+      for (int i = 0; i < NT - 1; ++i) { c[i * kWave] = zr[i]; c[(NT - 1 + i) * kWave] = zc[i]; }
+      const int64_t j1 = (t + 1) * kExactTile < m2 ? (t + 1) * kExactTile : m2;
+      for (int64_t j = t * kExactTile; j < j1; ++j) {
+        const double2 e = ext(j);
+        df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, y0, y1);
+      }
+    }
+    double wr[NT - 1], wc[NT - 1];              // backward state: zi * y[-1]
+#pragma unroll
+    for (int i = 0; i < NT - 1; ++i) cmul_np(f.zi[i], 0.0, y0, y1, wr[i], wc[i]);
 
     int64_t k = S - 1;
     int64_t next_n = p.first + k * p.sps;
-    for (int64_t j = m2 - 1; j >= 0; --j) {
-      const double2 e = sc[(size_t)j * kWave];
-      double o0, o1;
-      df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
-      if (j - pad == next_n && k >= 0) {
-        if (live) {
-          sym[sym_index(s, S, k, 0)] = o0;
-          sym[sym_index(s, S, k, 1)] = o1;
+    for (int64_t t = tiles - 1; t >= 0; --t) {
+      // re-run tile t forward from its checkpoint (each lane reads back its own
+      // stores: program order, no barrier needed), outputs into LDS
+      const double* c = ck + (size_t)t * 8 * kWave;
+#pragma unroll
+      for (int i = 0; i < NT - 1; ++i) { zr[i] = c[i * kWave]; zc[i] = c[(NT - 1 + i) * kWave]; }
+      const int64_t j0 = t * kExactTile;
+      const int64_t j1 = j0 + kExactTile < m2 ? j0 + kExactTile : m2;
+      for (int64_t j = j0; j < j1; ++j) {
+        const double2 e = ext(j);
+        double o0, o1;
+        df2t_cplx_step<NT>(zr, zc, b, a, e.x, e.y, o0, o1);
+        tile_out[j - j0][lane] = make_double2(o0, o1);
+      }
+      for (int64_t j = j1 - 1; j >= j0; --j) {
+        const double2 e = tile_out[j - j0][lane];
+        double o0, o1;
+        df2t_cplx_step<NT>(wr, wc, b, a, e.x, e.y, o0, o1);
+        if (j - pad == next_n && k >= 0) {
+          if (live) {
+            sym[sym_index(s, S, k, 0)] = o0;
+            sym[sym_index(s, S, k, 1)] = o1;
+          }
+          --k;
+          next_n -= p.sps;
         }
-        --k;
-        next_n -= p.sps;
       }
     }
-    __threadfence();                            // the slot's scratch is rewritten for the next group
   }
 }
 
@@ -1230,9 +1265,8 @@ hipError_t launch_psk_slice(const PskBuffers& b, const PskParams& p, hipStream_t
 }
 
 hipError_t launch_psk_lowpass_exact(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
-  const int64_t groups = (b.n_streams + kWave - 1) / kWave;
   if (f.nt != 5) return hipErrorInvalidValue;
-  const int64_t slots = groups < kExactSlots ? groups : kExactSlots;
+  const int64_t slots = psk_exact_slots(b.n_streams);
   hipLaunchKernelGGL((k_lowpass_exact<5>), dim3((unsigned)slots), dim3(kWave), 0, st, b, p, f);
   return hipGetLastError();
 }

@@ -1133,7 +1133,11 @@ hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, cons
   if (e != hipSuccess) return e;
   const int fm = (int)(p.first % (p.sps > 0 ? p.sps : 1));
   bool fused = false;
-  if (p.sps == 10 && fm == 5) fused = launch_lp<10, 5>(b, p, f, st);
+  // the static symbol slots number tile t's symbols from t * (TL / SPS) - first / SPS:
+  // valid (>= 0 from the first whole tile on) while first <= the tile length;
+  // a later first (the C ABI allows any) takes the generic path
+  if (p.first > kLpT2) fused = launch_lp<0, 0>(b, p, f, st);
+  else if (p.sps == 10 && fm == 5) fused = launch_lp<10, 5>(b, p, f, st);
   else if (p.sps == 5 && fm == 2) fused = launch_lp<5, 2>(b, p, f, st);
   else if (p.sps == 20 && fm == 10) fused = launch_lp<20, 10>(b, p, f, st);
   else if (p.sps == 10 && fm == 0) fused = launch_lp<10, 0>(b, p, f, st);

@@ -211,6 +211,10 @@ int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan *plan);
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan *plan);
 /* FFT length actually run: n_samples, or the Bluestein length when n is not 5-smooth */
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan *plan);
+/* 1: the plan keeps z and the Hilbert filter's intermediates only for the
+ * samples fsk_demodulate's decision windows read (modem.py:320-321: the
+ * "live" columns of the four-step grid); 0: every sample */
+int amr_fsk_plan_live_columns(const amr_fsk_plan *plan);
 int amr_fsk_plan_synchronize(amr_fsk_plan *plan);
 int amr_fsk_plan_enable_timing(amr_fsk_plan *plan, int on);
 /* milliseconds of each AMR_TF_* stage in the last call (-1 = not run) */

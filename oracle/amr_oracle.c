@@ -27,7 +27,15 @@
  *       re = fma(ar, br, -(ai*bi)),  im = fma(ar, bi, ai*br)
  *     (measured bit for bit in this container);
  *     restated here with the C99 fma().
- *   QPSK slicer   modem.py:216-241   atan2, +2pi if negative, 4 sectors
+ *   QPSK slicer   modem.py:216-241   np.angle, +2pi if negative, 4 sectors.
+ *     np.angle is numpy's arctan2, which numpy 2.2 evaluates with its AVX-512
+ *     (SVML) kernel on the hosts the golden fixtures came from
+ *     (numpy._core.__cpu_features__['AVX512_SKX'], recorded in
+ *     tests/golden/manifest.json).  That kernel is not correctly rounded: within
+ *     an ulp of a sector edge it differs from libm's atan2 on ~6 % of inputs,
+ *     enough to flip a decision.  np_angle() below restates its result there
+ *     (numpy_atan2_near_diag) and uses libm elsewhere; tests/test_oracle_slicer.py
+ *     checks it against numpy on the sector edges and 1.5 M near-tie pairs.
  *   BPSK slicer   modem.py:102-105   real(diff) < 0 -> 1
  *   sync + pack   modem.py:111-135 (BPSK), 243-266 (QPSK), 326-341 (FSK)
  *     first index of "0100011001000010" at any bit offset; pack MSB first
@@ -163,6 +171,61 @@ static int filtfilt_complex(const double *b, const double *a, int nt, const doub
     return 0;
 }
 
+/* ---- np.angle near a sector edge (modem.py:219) ---------------------------
+ * numpy's AVX-512 arctan2 within |t| < 2^-29 of the diagonal |y| = |x|, for
+ * components of magnitude 2^-1015 .. 2^985, bit for bit:
+ *   t  = (|y| - |x|) / (|y| + |x|)
+ *   x > 0:  pi4 + (t + pi4_lo)            x < 0:  pi - (pi4 - (pi_lo - (t + pi4_lo)))
+ * negated for y < 0, with pi/4 split into double hi + lo and pi into hi +
+ * SVML's short lo 0x1.1a64p-53 (bisecting numpy's rounding boundaries in the
+ * pi-side form located exactly this constant, not pi - hi).  Outside that
+ * domain (and for zeros / inf / NaN) libm's atan2 is numpy's result on every
+ * input the tests cover.  The GPU slicer (psk_common.h) uses the same model. */
+static int numpy_atan2_near_diag(double y, double x, double *ang)
+{
+    const double ay = fabs(y), ax = fabs(x);
+    if (!(ax >= 0x1p-1015 && ax <= 0x1p985 && ay >= 0x1p-1015 && ay <= 0x1p985)) return 0;
+    const double t = (ay - ax) / (ay + ax);
+    if (!(fabs(t) < 0x1p-29)) return 0;
+    const double pi4 = 0x1.921fb54442d18p-1, pi4_lo = 0x1.1a62633145c07p-55;
+    const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a64p-53;   // SVML's short pi_lo
+    const double a = x > 0 ? pi4 + (t + pi4_lo) : pi - (pi4 - (pi_lo - (t + pi4_lo)));
+    *ang = y < 0 ? -a : a;
+    return 1;
+}
+
+static double np_angle(double re, double im)
+{
+    double ang;
+    if (!numpy_atan2_near_diag(im, re, &ang)) ang = atan2(im, re);
+    return ang;
+}
+
+/* the reference's sector decision for one differential product (modem.py:219-241):
+ * returns the dibit as 2*hi + lo */
+static int qpsk_dibit(double dr, double di)
+{
+    double ang = np_angle(dr, di);                   /* np.angle, modem.py:219 */
+    if (ang < 0) ang += 2 * M_PI;                    /* modem.py:232 */
+    if (ang < M_PI / 4 || ang > 7 * M_PI / 4) return 0;
+    if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) return 1;
+    if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) return 3;
+    return 2;
+}
+
+/* np.angle of n complex values (re, im interleaved), as the model above */
+void oracle_np_angle(const double *d, int64_t n, double *ang)
+{
+    for (int64_t k = 0; k < n; ++k) ang[k] = np_angle(d[2 * k], d[2 * k + 1]);
+}
+
+/* The slicer alone over n differential products (re, im interleaved):
+ * dibits[k] = 2*hi + lo (tests/test_oracle_slicer.py). */
+void oracle_qpsk_slice(const double *d, int64_t n, uint8_t *dibits)
+{
+    for (int64_t k = 0; k < n; ++k) dibits[k] = (uint8_t)qpsk_dibit(d[2 * k], d[2 * k + 1]);
+}
+
 /* ---- sync + pack (modem.py:244-264) -------------------------------------- */
 static const uint8_t SYNC16[16] = {0,1,0,0,0,1,1,0, 0,1,0,0,0,0,1,0};   /* "FB" */
 
@@ -226,15 +289,9 @@ int64_t oracle_psk_demod(int kind, const void *x, int dtype, int64_t n,
                 bits[k] = (dr < 0) ? 1 : 0;              /* modem.py:103-105 */
                 continue;
             }
-            double ang = atan2(di, dr);                  /* np.angle, modem.py:219 */
-            if (ang < 0) ang += 2 * M_PI;                /* modem.py:232 */
-            uint8_t h, l;
-            if (ang < M_PI / 4 || ang > 7 * M_PI / 4) { h = 0; l = 0; }
-            else if (M_PI / 4 <= ang && ang < 3 * M_PI / 4) { h = 0; l = 1; }
-            else if (3 * M_PI / 4 <= ang && ang < 5 * M_PI / 4) { h = 1; l = 1; }
-            else { h = 1; l = 0; }
-            bits[2 * k] = h;
-            bits[2 * k + 1] = l;
+            const int db = qpsk_dibit(dr, di);           /* modem.py:219-241 */
+            bits[2 * k] = (uint8_t)(db >> 1);
+            bits[2 * k + 1] = (uint8_t)(db & 1);
         }
         int64_t s = oracle_find_sync(bits, L);
         *sync_out = s;

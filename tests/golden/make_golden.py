@@ -305,6 +305,9 @@ def main():
     manifest = {"generator": "tests/golden/make_golden.py",
                 "reference": "szumanski/Audio-Modem-Radio @ /root/reference",
                 "numpy": np.__version__, "scipy": scipy.__version__,
+                # numpy's arctan2 (np.angle) dispatch on the generating host: the
+                # QPSK slicer's near-tie decisions depend on it
+                "numpy_cpu_features": numpy_cpu_features(),
                 "cases": cases, "fec": fec_golden, "decoder": dec_cases}
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
@@ -313,6 +316,11 @@ def main():
         print(c["id"], c["status"], (len(c["out"]) // 2) if c["status"] == "ok" else c["emsg"][:70])
     for d in dec_cases:
         print(d["id"], [f["name"] for f in d["files"]])
+
+
+def numpy_cpu_features() -> dict:
+    from numpy._core._multiarray_umath import __cpu_features__ as f
+    return {k: bool(f.get(k, False)) for k in ("AVX512F", "AVX512_SKX", "AVX2", "FMA3")}
 
 
 if __name__ == "__main__":

@@ -98,6 +98,9 @@ def test_fsk_envelopes_within_tolerance(golden, case_id):
     (33, 48000, 1200, 2400.0, 4800.0, np.float64),
     (20, 30011, 4800, 8000.0, 16000.0, np.float32),     # Bluestein length
     (17, 9600, 19200, 21000.0, 27000.0, np.float32),    # sps 5: windows of 2
+    (70, 96000, 9600, 12000.0, 24000.0, np.float64),    # live columns, float64 staged in chunks
+    (40, 96000, 4800, 8000.0, 16000.0, np.float32),     # sps 20: 150 live columns (a partial tile)
+    (24, 96000, 19200, 21000.0, 27000.0, np.int16),     # sps 5, PCM input
 ])
 def test_fsk_batch_vs_oracle(B, N, baud, mark, space, dtype):
     import _fsk
@@ -137,6 +140,8 @@ def test_fsk_full_batch_round_trip():
     base = synth.fsk_batch(U, N, 9600, 12000.0, 24000.0, seed=9, distinct=16, noise=0.05)
     x = np.tile(base, (B // U, 1))
     pl = _fsk.get_fsk_plan(N, 9600, 12000.0, 24000.0, 96000, B)
+    assert pl.live_columns
+    assert pl.scratch_bytes() <= 40e9, pl.scratch_bytes()     # 1.4 x n complex per stream + C's staging
     got, sync = pl.demod_host(x)
     bad = [i for i in range(U, B) if got[i] != got[i % U]]
     assert not bad, f"{len(bad)} repeated streams decode differently, first {bad[:5]}"
@@ -211,3 +216,67 @@ def test_fsk_20s_stream_vs_oracle():
     got, _ = pl.demod_host(x)
     assert got[0] == oracle.fsk_demodulate(x[0], 1200, 2400.0, 4800.0)
     assert len(got[0]) > 1000
+
+
+@pytest.mark.parametrize("N,baud,live", [(96000, 9600, True), (96000, 19200, True), (96000, 4800, True),
+                                         (96000, 1200, False), (30011, 4800, False), (48000, 1200, False)])
+def test_fsk_live_column_layout_chosen(N, baud, live):
+    """The live-column layout runs when the four-step grid's
+    row length n1 is a multiple of sps (96000 = 300 x 320: sps 5, 10, 20),
+    else the natural layout (sps 80 at 96000 / 48000, Bluestein lengths)."""
+    import _fsk
+    pl = _fsk.FskPlan(N, baud, 12000.0 if baud > 1200 else 2400.0, 24000.0 if baud > 1200 else 4800.0, max_streams=4)
+    assert pl.live_columns == live
+
+
+def test_fsk_natural_layout_forced(tmp_path):
+    """AMR_FSK_LIVE=0 (the natural layout: every sample through all three
+    Hilbert passes) on the live-column cases: == oracle, and == the live path."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    script = tmp_path / "nat.py"
+    script.write_text(f'''
+import sys
+sys.path[:0] = [{os.path.join(root, "audio-modem-radio_amd")!r}, {root!r}, {here!r}]
+import numpy as np
+import _fsk, synth
+from oracle import oracle
+bad = []
+for (B, N, baud, m, s) in ((40, 96000, 9600, 12000.0, 24000.0), (9, 96000, 19200, 21000.0, 27000.0)):
+    x = synth.fsk_batch(B, N, baud, m, s, seed=B, distinct=4, noise=0.3)
+    pl = _fsk.FskPlan(N, baud, m, s, max_streams=B)
+    assert not pl.live_columns
+    got, _ = pl.demod_host(x)
+    bad += [(N, baud, i) for i in range(B) if got[i] != oracle.fsk_demodulate(x[i], baud, m, s)]
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+''')
+    env = dict(os.environ, AMR_FSK_LIVE="0")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=250)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_fsk_live_async_host_entry():
+    """amr_fsk_demod_host_async on a live-column plan: the input is staged in
+    C in chunks on the plan's stream (float64: 2 chunks for 64 streams) while
+    nothing waits on the host; == the synchronous entry == oracle."""
+    import _amr
+    import _fsk
+    import synth
+    from oracle import oracle
+    B, N = 64, 96000
+    x = synth.fsk_batch(B, N, 9600, 12000.0, 24000.0, seed=5, distinct=6, noise=0.3).astype(np.float64)
+    pl = _fsk.FskPlan(N, 9600, 12000.0, 24000.0, max_streams=B)
+    assert pl.live_columns
+    o = np.zeros((B, pl.out_cap), np.uint8)
+    ln = np.zeros(B, np.int64)
+    sy = np.zeros(B, np.int64)
+    L = _amr.lib()
+    _amr.check(L.amr_fsk_demod_host_async(pl.handle, _amr.ptr(x), _amr.DTYPE_F64, B, N, _amr.ptr(o), pl.out_cap,
+                                          _amr.ptr(ln), _amr.ptr(sy)))
+    _amr.check(L.amr_fsk_plan_synchronize(pl.handle))
+    got = [o[i, :ln[i]].tobytes() for i in range(B)]
+    assert got == pl.demod_host(x)[0]
+    assert got == [oracle.fsk_demodulate(r, 9600, 12000.0, 24000.0) for r in x]

@@ -89,25 +89,60 @@ def test_int16_pcm_path_equals_float64_reference(golden):
     assert outs[0].hex() == [c for c in manifest["cases"] if c["id"] == "qpsk9600_wav"][0]["out"]
 
 
+_BATCHES = {}
+
+
+def _seeded_batch(kind, baud, B, N):
+    """The seeded input of a batch test and the oracle's bytes + sync for it,
+    built once per module (the full-size row and lane tests share them; the
+    three full-size batches hold ~8 GB of host memory)."""
+    import synth
+    from oracle import oracle
+    key = (kind, baud, B, N)
+    if key not in _BATCHES:
+        if kind == "qpsk" and baud == 19200:
+            x = synth.dpsk8_batch(B, N, baud, seed=B, distinct=8 if B < 8192 else 64)
+        elif kind == "qpsk":
+            x = synth.qpsk_batch(B, N, baud, seed=B, distinct=8)
+        else:
+            x = np.stack([synth.fit(synth.bpsk_waveform(synth.random_frame(np.random.default_rng(i), 200), baud), N)
+                          + np.random.default_rng(i).normal(0, 0.05, N).astype(np.float32) for i in range(B)])
+        want, wsync = oracle.psk_demod_batch(kind, x, baud, n_threads=min(16, os.cpu_count() or 1))
+        _BATCHES[key] = (x, want, wsync)
+    return _BATCHES[key]
+
+
 @pytest.mark.parametrize("kind,baud,B,N", [("qpsk", 9600, 4096, 96000), ("qpsk", 9600, 8192, 96000),
                                            ("qpsk", 19200, 257, 96000),
                                            ("bpsk", 1200, 130, 48000), ("qpsk", 2400, 65, 30001)])
 def test_batch_vs_oracle(kind, baud, B, N):
     """Seeded batches up to the BASELINE config-2 size (and the 8192-stream
     single launch of configs 4/5 on one GPU), every stream checked against the
-    oracle (bit-exact bytes and sync index)."""
+    oracle (bit-exact bytes and sync index).  One batch alone: the row layout."""
     import _amr
-    import synth
-    from oracle import oracle
-    if kind == "qpsk" and baud == 19200:
-        x = synth.dpsk8_batch(B, N, baud, seed=B, distinct=8)
-    else:
-        x = synth.qpsk_batch(B, N, baud, seed=B, distinct=8) if kind == "qpsk" else \
-            np.stack([synth.fit(synth.bpsk_waveform(synth.random_frame(np.random.default_rng(i), 200), baud), N)
-                      + np.random.default_rng(i).normal(0, 0.05, N).astype(np.float32) for i in range(B)])
+    x, want, wsync = _seeded_batch(kind, baud, B, N)
     plan = _amr.PskPlan(kind, N, baud, max_streams=B)
     got, gsync = plan.demod_host(x)
-    want, wsync = oracle.psk_demod_batch(kind, x, baud, n_threads=min(16, os.cpu_count() or 1))
+    assert plan.last_layout() == "row"
+    mism = [i for i in range(B) if got[i] != want[i]]
+    assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
+    assert np.array_equal(gsync, wsync)
+
+
+@pytest.mark.parametrize("baud", [9600, 19200])
+def test_full_size_lane_layout_as_benched(baud):
+    """Configs 4 (OFDM8 = the QPSK@9600 path, modem.py:375-376) and 5's demod
+    (8PSK@19200 = the QPSK path, modem.py:348) at their full 8192 x 96000, in
+    the layout bench.py times: a plan told 16 batches are in flight (so the
+    lane-per-stream kernels with the slicer fused into the low-pass run: sps
+    10 and sps 5), every stream's bytes and sync index == the oracle."""
+    import _amr
+    B, N = 8192, 96000
+    x, want, wsync = _seeded_batch("qpsk", baud, B, N)
+    plan = _amr.PskPlan("qpsk", N, baud, max_streams=B)
+    plan.set_inflight(16)
+    got, gsync = plan.demod_host(x)
+    assert plan.last_layout() == "lane"
     mism = [i for i in range(B) if got[i] != want[i]]
     assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
     assert np.array_equal(gsync, wsync)
@@ -139,18 +174,21 @@ def test_fec_gpu_matches_reference(golden):
     assert ("Aviso: CRC" in buf.getvalue()) == manifest["fec"][-1]["crc_warn"]
 
 
-@pytest.mark.parametrize("B", [64, 8192])
-def test_fec_fused_after_8psk_demod(B):
+@pytest.mark.parametrize("B,layout", [(64, "row"), (8192, "row"), (8192, "lane")])
+def test_fec_fused_after_8psk_demod(B, layout):
     """Config 5: 8PSK@19200 demod + FEC decode fused on the device == oracle
-    chain (psk_demod_batch then fec_decode, fec.py:34-69), every stream -- at
-    B=64 and at BASELINE configs[5]'s full batch of 8192 (one launch: K1g)."""
+    chain (psk_demod_batch then fec_decode, fec.py:34-69), every stream's
+    demod bytes, sync index, FEC bytes and CRC flag -- at B=64 and at BASELINE
+    configs[4]'s full batch of 8192, both as one batch alone (row layout) and
+    as bench.py times it (16 in flight: lane layout, fused slicer at sps 5)."""
     import ctypes
     import _amr
-    import synth
     from oracle import oracle
     N = 96000
-    x = synth.dpsk8_batch(B, N, 19200, seed=11, distinct=4 if B < 256 else 64)
+    x, dem, wsync = _seeded_batch("qpsk", 19200, B, N)
     plan = _amr.PskPlan("qpsk", N, 19200, max_streams=B)
+    if layout == "lane":
+        plan.set_inflight(16)
     L = _amr.lib()
     cap = plan.out_cap
     ptrs = {}
@@ -159,25 +197,26 @@ def test_fec_fused_after_8psk_demod(B):
         p = ctypes.c_void_p()
         _amr.check(L.amr_malloc(ctypes.byref(p), nbytes))
         ptrs[name] = p
+    host = {}
     try:
         _amr.check(L.amr_memcpy_h2d(ptrs["x"], _amr.ptr(x), x.nbytes))
         _amr.check(L.amr_psk_demod_fec_device(plan.handle, ptrs["x"], _amr.DTYPE_F32, B, N, ptrs["out"], cap,
                                               ptrs["len"], ptrs["sync"], ptrs["fec"], cap, ptrs["flen"], ptrs["ok"]))
         _amr.check(L.amr_psk_plan_synchronize(plan.handle))
-        fec_out = np.empty((B, cap), np.uint8)
-        flen = np.empty(B, np.int64)
-        ok = np.empty(B, np.int32)
-        _amr.check(L.amr_memcpy_d2h(_amr.ptr(fec_out), ptrs["fec"], B * cap))
-        _amr.check(L.amr_memcpy_d2h(_amr.ptr(flen), ptrs["flen"], B * 8))
-        _amr.check(L.amr_memcpy_d2h(_amr.ptr(ok), ptrs["ok"], B * 4))
+        for name, shape, dt in (("out", (B, cap), np.uint8), ("len", B, np.int64), ("sync", B, np.int64),
+                                ("fec", (B, cap), np.uint8), ("flen", B, np.int64), ("ok", B, np.int32)):
+            host[name] = np.empty(shape, dt)
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(host[name]), ptrs[name], host[name].nbytes))
     finally:
         for p in ptrs.values():
             L.amr_free(p)
-    dem, _ = oracle.psk_demod_batch("qpsk", x, 19200, n_threads=min(16, os.cpu_count() or 1))
+    assert plan.last_layout() == layout
+    assert np.array_equal(host["sync"], wsync)
     bad = []
     for i in range(B):
         want, wok = oracle.fec_decode(dem[i])
-        if fec_out[i, :flen[i]].tobytes() != want or bool(ok[i]) != wok:
+        if (host["out"][i, :host["len"][i]].tobytes() != dem[i] or host["fec"][i, :host["flen"][i]].tobytes() != want
+                or bool(host["ok"][i]) != wok):
             bad.append(i)
     assert not bad, f"{len(bad)} of {B} streams differ, first {bad[:5]}"
 
@@ -454,3 +493,117 @@ def test_async_host_entry_stream_of_batches():
                                           _amr.ptr(ln), _amr.ptr(sy)))
     _amr.check(L.amr_fsk_plan_synchronize(pf.handle))
     assert [o[i, :ln[i]].tobytes() for i in range(8)] == [oracle.fsk_demodulate(r, 9600, 12000.0, 24000.0) for r in xf]
+
+
+@pytest.mark.parametrize("layout", ["row", "lane"])
+def test_batch_of_flagged_streams(layout):
+    """Every stream of a 1030-stream batch holds exact zeros (a gated capture:
+    digital silence before the burst and a dropout inside it), so the low-pass
+    detector flags all of them and the whole batch takes K3x, the exact
+    complex low-pass -- checkpointed, one workgroup per 64-stream group.
+    Bytes and sync == the oracle, in both layouts."""
+    import time
+    import _amr
+    import synth
+    from oracle import oracle
+    B, N = 1030, 96000
+    x = synth.qpsk_batch(B, N, 9600, seed=99, distinct=6)
+    rng = np.random.default_rng(99)
+    for i in range(B):
+        x[i, :int(rng.integers(1, 3000))] = 0.0
+        d0 = int(rng.integers(20000, 90000))
+        x[i, d0:d0 + int(rng.integers(1, 400))] = 0.0
+    plan = _amr.PskPlan("qpsk", N, 9600, max_streams=B)
+    if layout == "lane":
+        plan.set_inflight(16)
+    plan.demod_host(x[:64])                                  # warm up (first-call allocations)
+    t0 = time.perf_counter()
+    got, gsync = plan.demod_host(x)
+    dt = time.perf_counter() - t0
+    assert plan.last_layout() == layout
+    assert plan.exact_streams() == B
+    want, wsync = oracle.psk_demod_batch("qpsk", x, 9600, n_threads=min(16, os.cpu_count() or 1))
+    mism = [i for i in range(B) if got[i] != want[i]]
+    assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
+    assert np.array_equal(gsync, wsync)
+    print(f"all-flagged {B} x {N} ({layout}): {dt * 1e3:.1f} ms host call")
+
+
+def test_failed_scratch_grow_leaves_plan_usable(tmp_path):
+    """The row layout grows a plan's s1 / s3 on its first call.  With every
+    grow forced to fail (AMR_TEST_FAIL_SCRATCH_GROW=1): the row call raises
+    AmrError (no memory) and the plan's lane-layout buffers are still intact,
+    so the next lane call is == the oracle (no kernel ever sees freed memory)."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    script = tmp_path / "grow.py"
+    script.write_text(f'''
+import sys
+sys.path[:0] = [{os.path.join(root, "audio-modem-radio_amd")!r}, {root!r}, {here!r}]
+import numpy as np
+import _amr, synth
+from oracle import oracle
+x = synth.qpsk_batch(70, 24000, 9600, seed=3, distinct=5)
+want, _ = oracle.psk_demod_batch("qpsk", x, 9600)
+pl = _amr.PskPlan("qpsk", 24000, 9600, max_streams=70)
+pl.set_inflight(1000)
+assert pl.demod_host(x)[0] == want and pl.last_layout() == "lane"
+before = pl.scratch_bytes()
+pl.set_inflight(1)
+try:
+    pl.demod_host(x)
+    raise SystemExit("row call did not fail")
+except _amr.AmrError as e:
+    assert e.code == _amr.AMR_E_NOMEM, e
+pl.set_inflight(1000)
+assert pl.demod_host(x)[0] == want and pl.last_layout() == "lane"
+assert pl.scratch_bytes() == before, (pl.scratch_bytes(), before)
+print("OK")
+''')
+    env = dict(os.environ, AMR_TEST_FAIL_SCRATCH_GROW="1")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("first", [5, 20, 21, 55, 397])
+def test_lane_layout_any_first(first):
+    """The C ABI takes any first symbol index (amr_psk_plan_create); the
+    reference's are sps // 2 and sps (modem.py:209, :92).  The lane kernels'
+    static symbol slots hold only while first <= their tile; later ones take
+    the generic path.  Bytes and sync == the oracle run with the same first."""
+    import ctypes
+    import _amr
+    import synth
+    from oracle import oracle
+    B, N, baud = 70, 24000, 9600
+    x = synth.qpsk_batch(B, N, baud, seed=first, distinct=5)
+    sps, _, (b, a, zi), (bl, al, zil), lo4 = _amr.design_psk("qpsk", N, baud)
+    h = ctypes.c_void_p()
+    _amr.check(_amr.lib().amr_psk_plan_create(ctypes.byref(h), _amr.default_device(), _amr.PSK_QPSK, N, sps, first,
+                                              _amr.ptr(b), _amr.ptr(a), _amr.ptr(zi), len(b), _amr.ptr(bl),
+                                              _amr.ptr(al), _amr.ptr(zil), len(bl), _amr.ptr(lo4), B))
+    try:
+        _amr.check(_amr.lib().amr_psk_plan_set_inflight(h, 1000))
+        cap = int(_amr.lib().amr_psk_plan_out_capacity(h))
+        out = np.zeros((B, cap), np.uint8)
+        ln = np.zeros(B, np.int64)
+        sy = np.zeros(B, np.int64)
+        _amr.check(_amr.lib().amr_psk_demod_host(h, _amr.ptr(x), _amr.DTYPE_F32, B, N, _amr.ptr(out), cap,
+                                                 _amr.ptr(ln), _amr.ptr(sy)))
+        assert _amr.lib().amr_psk_plan_last_layout(h) == 1
+    finally:
+        _amr.lib().amr_psk_plan_destroy(h)
+    op = oracle.PskPlan("qpsk", N, baud)
+    ocap = (2 * N) // sps // 8 + 8
+    wout = np.zeros((B, ocap), np.uint8)
+    wln = np.zeros(B, np.int64)
+    wsy = np.zeros(B, np.int64)
+    ob, oa, ozi = op.bp
+    obl, oal, ozil = op.lp
+    P = oracle._p
+    oracle.lib().oracle_psk_demod_batch(0, P(x), oracle.DT_F32, B, N, N, sps, first, P(ob), P(oa), len(ob), P(ozi),
+                                        P(obl), P(oal), len(obl), P(ozil), P(op.lo), P(wout), ocap, P(wln), P(wsy), 8)
+    assert np.array_equal(ln, wln) and np.array_equal(sy, wsy)
+    assert all(out[i, :ln[i]].tobytes() == wout[i, :wln[i]].tobytes() for i in range(B))

@@ -20,6 +20,9 @@ per symbol."""
 import numpy as np
 import pytest
 
+from slicer_cases import (edge_diffs, near_tie_diffs, numpy_is_fixture_host, reference_bits, reference_dibits,
+                          symbols_for)
+
 pytestmark = pytest.mark.gpu
 
 
@@ -30,70 +33,11 @@ def gpu(built_lib):
         pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
 
 
-def reference_bits(kind, symbols):
-    diff_symbols = symbols[1:] * np.conj(symbols[:-1])
-    bits = []
-    for s in diff_symbols:
-        if kind == "bpsk":
-            bits.append(1 if np.real(s) < 0 else 0)
-            continue
-        decision_angle = np.angle(s)
-        if decision_angle < 0:
-            decision_angle += 2 * np.pi
-        if decision_angle < np.pi / 4 or decision_angle > 7 * np.pi / 4:
-            bits.extend([0, 0])
-        elif np.pi / 4 <= decision_angle < 3 * np.pi / 4:
-            bits.extend([0, 1])
-        elif 3 * np.pi / 4 <= decision_angle < 5 * np.pi / 4:
-            bits.extend([1, 1])
-        else:
-            bits.extend([1, 0])
-    return np.array(bits, np.uint8)
-
-
-def edge_diffs():
-    d = []
-    specials = [0.0, -0.0, np.inf, -np.inf, np.nan]
-    for a in specials + [1.0, -1.0]:
-        for b in specials + [1.0, -1.0]:
-            d.append(complex(a, b))
-    for m in (5e-324, 2.2250738585072014e-308, 1e-300, 1e-20, 0.7, 1.0, 3.0, 1e20, 1e289, 1e300):
-        for sr in (1.0, -1.0):
-            for si in (1.0, -1.0):
-                base_r, base_i = sr * m, si * m
-                # |dr| vs |di| within 3 ulp of equal: the pi/4 + k*pi/2 edges, where
-                # an ulp of np.angle decides -- inside the domain of K4a's model of
-                # numpy's arctan2 (component magnitudes 2^-1015 .. 2^985)
-                for k in (range(-3, 4) if 1e-300 <= m <= 1e289 else ()):
-                    r = base_r
-                    for _ in range(abs(k)):
-                        r = np.nextafter(r, np.inf if k > 0 else -np.inf)
-                    d.append(complex(r, base_i))
-                    d.append(complex(base_i, r))
-                d.append(complex(base_r, 0.0))     # the 0, pi/2, pi, 3pi/2 axes, both zero signs
-                d.append(complex(base_r, -0.0))
-                d.append(complex(0.0, base_i))
-                d.append(complex(-0.0, base_i))
-    rng = np.random.default_rng(5)
-    for k in range(8):                             # just off the edges, by relative 1e-16 .. 1e-9
-        for e in (1e-16, 3e-16, 1e-15, 1e-12, 1e-9):
-            for sgn in (1, -1):
-                th = k * np.pi / 4 + sgn * e
-                r = 10 ** rng.uniform(-5, 5)
-                d.append(complex(r * np.cos(th), r * np.sin(th)))
-    return d
-
-
-def symbols_for(ds):
-    s = np.empty(2 * len(ds) + 1, np.complex128)
-    s[0::2] = 1.0 + 0.0j
-    s[1::2] = ds
-    return s
-
-
 @pytest.mark.parametrize("kind", ["qpsk", "bpsk"])
 def test_slicer_edges_match_reference_steps(kind):
     import _amr
+    if kind == "qpsk" and not numpy_is_fixture_host():
+        pytest.skip("this host's numpy arctan2 is not the fixtures' AVX-512 kernel: near-tie angles differ by design")
     ds = edge_diffs()
     rows = [symbols_for(ds[i:i + 61]) for i in range(0, len(ds), 61)]
     S = max(len(r) for r in rows)
@@ -119,3 +63,22 @@ def test_slicer_random_symbols_match_reference_steps():
         got = _amr.psk_slice(kind, sym)
         for i in range(16):
             assert np.array_equal(got[i], reference_bits(kind, sym[i])), (kind, i)
+
+
+def test_slicer_near_ties_match_numpy_and_oracle():
+    """400 k products within ulps of the sector edges (slicer_cases.near_tie_diffs)
+    through K4a: the decisions equal numpy's (the reference's np.angle steps)
+    and the oracle's (oracle/amr_oracle.c qpsk_dibit, the batch tests' checker)."""
+    import _amr
+    from oracle import oracle
+    if not numpy_is_fixture_host():
+        pytest.skip("this host's numpy arctan2 is not the fixtures' AVX-512 kernel")
+    rows, per = 32, 6250
+    ds = near_tie_diffs(rows * per, seed=31).reshape(rows, per)
+    sym = np.stack([symbols_for(r) for r in ds])
+    bits = _amr.psk_slice("qpsk", sym)
+    got = (bits[:, 0::2] * 2 + bits[:, 1::2]).astype(np.uint8)
+    prods = sym[:, 1:] * np.conj(sym[:, :-1])
+    want = reference_dibits(prods)
+    assert np.array_equal(got, want), int(np.count_nonzero(got != want))
+    assert np.array_equal(oracle.qpsk_slice(prods).reshape(got.shape), want)
