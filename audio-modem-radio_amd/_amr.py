@@ -25,8 +25,8 @@ AMR_E_INVALID, AMR_E_PADLEN, AMR_E_HIP, AMR_E_NOMEM, AMR_E_NODEVICE, AMR_E_RCCL,
     -1, -2, -3, -4, -5, -6, -7
 DTYPE_F32, DTYPE_F64, DTYPE_I16 = 0, 1, 2
 PSK_QPSK, PSK_BPSK = 0, 1
-T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec"]
-TF_NAMES = ["bandpass", "hilbert", "decide"]
+T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec", "launch"]
+TF_NAMES = ["bandpass", "hilbert", "decide", "launch"]
 # amr_frame_rec (include/amr.h), 64 bytes
 FRAME_SHORT, FRAME_NONAME, FRAME_NOMETA, FRAME_BADLEN, FRAME_INCOMPLETE, FRAME_CRC_BAD, FRAME_OK = range(7)
 FRAME_REC = np.dtype([("start", "<i8"), ("name_start", "<i8"), ("payload_start", "<i8"), ("status", "<i4"),
@@ -40,6 +40,7 @@ EXPORTS = [
     "amr_abi_version", "amr_build_id", "amr_last_error", "amr_device_count", "amr_set_device", "amr_malloc", "amr_free",
     "amr_memcpy_h2d", "amr_memcpy_d2h", "amr_memcpy_d2d", "amr_device_synchronize",
     "amr_psk_plan_create", "amr_psk_plan_destroy", "amr_psk_plan_out_capacity", "amr_psk_plan_scratch_bytes",
+    "amr_psk_plan_bytes_estimate", "amr_fsk_plan_bytes_estimate",
     "amr_psk_plan_synchronize", "amr_psk_plan_enable_timing", "amr_psk_plan_timings", "amr_psk_plan_set_inflight",
     "amr_psk_plan_exact_streams", "amr_psk_demod_host", "amr_psk_demod_device", "amr_psk_demod_fec_device",
     "amr_psk_slice_host", "amr_psk_plan_last_layout", "amr_synth_tile_noise",
@@ -49,7 +50,7 @@ EXPORTS = [
     "amr_fsk_plan_fft_length", "amr_fsk_plan_live_columns", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather", "amr_fsk_allgather",
-    "amr_comm_synchronize", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
+    "amr_comm_synchronize", "amr_comm_allgather_host", "amr_comm_allreduce_max", "amr_comm_world", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
     "amr_resample_host",
 ]
 
@@ -193,6 +194,8 @@ def lib():
             "amr_psk_plan_destroy": (I32, [P]),
             "amr_psk_plan_out_capacity": (I64, [P]),
             "amr_psk_plan_scratch_bytes": (I64, [P]),
+            "amr_psk_plan_bytes_estimate": (I64, [I32, I64, I64, I64, I32, I32, I64]),
+            "amr_fsk_plan_bytes_estimate": (I64, [I64, I64, I32, I64]),
             "amr_psk_plan_synchronize": (I32, [P]),
             "amr_psk_plan_enable_timing": (I32, [P, I32]),
             "amr_psk_plan_set_inflight": (I32, [P, I32]),
@@ -233,6 +236,9 @@ def lib():
             "amr_allgather": (I32, [P, P, P, I64, P]),
             "amr_fsk_allgather": (I32, [P, P, P, I64, P]),
             "amr_comm_synchronize": (I32, [P]),
+            "amr_comm_allgather_host": (I32, [P, P, P, I64]),
+            "amr_comm_allreduce_max": (I32, [P, P, I64]),
+            "amr_comm_world": (I32, [P, P, P]),
             "amr_tx_samples": (I64, [I32, I64, D, D]),
             "amr_resample_host": (I32, [P, I64, I64, I64, P, I32]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
@@ -413,8 +419,10 @@ class PlanCache:
         self._d = collections.OrderedDict()
         self.lock = threading.Lock()
 
-    def get(self, key, need: int, make):
-        """The cached plan for key if it holds >= need streams, else make(need)."""
+    def get(self, key, need: int, make, estimate=None):
+        """The cached plan for key if it holds >= need streams, else make(need);
+        before making it, plans are evicted until estimate(need) (the new
+        plan's device bytes) fits beside the rest within the budget."""
         with self.lock:
             pl = self._d.get(key)
             if pl is not None and pl.max_streams >= need:
@@ -423,7 +431,7 @@ class PlanCache:
             if pl is not None:
                 del self._d[key]                    # too small: its scratch goes before the new one's
                 pl = None
-            self._evict(reserve=0)
+            self._evict(reserve=int(estimate(need)) if estimate else 0)
             pl = make(need)
             self._d[key] = pl
             self._evict(reserve=0, keep=key)
@@ -431,7 +439,10 @@ class PlanCache:
 
     def total_bytes(self) -> int:
         with self.lock:
-            return sum(p.scratch_bytes() for p in self._d.values())
+            return self._total_unlocked()
+
+    def _total_unlocked(self) -> int:
+        return sum(p.scratch_bytes() for p in self._d.values())
 
     def __len__(self):
         return len(self._d)
@@ -453,7 +464,7 @@ class PlanCache:
 
 
 def _cache_budget() -> int:
-    return int(float(os.environ.get("AMR_PLAN_CACHE_BYTES", 24e9)))
+    return int(float(os.environ.get("AMR_PLAN_CACHE_BYTES", 48e9)))
 
 
 def stream_bucket(batch: int, cap: int) -> int:
@@ -463,16 +474,26 @@ def stream_bucket(batch: int, cap: int) -> int:
     return 1 << (b - 1).bit_length()
 
 
-_psk_cache = PlanCache(_cache_budget())
+# ONE plan cache for every demodulator (PSK and FSK plans, keyed by kind):
+# its byte budget (AMR_PLAN_CACHE_BYTES, default 48 GB, 1/6 of an MI355X's
+# HBM) bounds all the drop-in path's device memory together.
+plan_cache = PlanCache(_cache_budget())
 PSK_MAX_CHUNK = 4096
 
 
 def get_psk_plan(kind: str, n: int, baud, carrier, samp_rate, batch: int) -> PskPlan:
     """Plan cache keyed by the reference call's parameters (and device)."""
     dev = default_device()
-    key = (kind, int(n), float(baud), float(carrier), float(samp_rate), dev)
+    key = ("psk", kind, int(n), float(baud), float(carrier), float(samp_rate), dev)
     need = stream_bucket(batch, PSK_MAX_CHUNK)
-    return _psk_cache.get(key, need, lambda m: PskPlan(kind, n, baud, carrier, samp_rate, max_streams=m, device=dev))
+    sps = int(samp_rate / baud)
+    first = sps // 2 if kind == "qpsk" else sps
+
+    def estimate(m):
+        return max(0, int(lib().amr_psk_plan_bytes_estimate(PSK_QPSK if kind == "qpsk" else PSK_BPSK, int(n), sps,
+                                                            first, 9, 5, m)))
+    return plan_cache.get(key, need, lambda m: PskPlan(kind, n, baud, carrier, samp_rate, max_streams=m, device=dev),
+                          estimate if sps >= 1 else None)
 
 
 def fec_decode_host(datas):

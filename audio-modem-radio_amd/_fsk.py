@@ -121,15 +121,19 @@ class FskPlan:
 
 
 MAX_CHUNK = 16384
-_fsk_cache = _amr.PlanCache(_amr._cache_budget())
 
 
 def get_fsk_plan(n, baud, mark_freq, space_freq, samp_rate, batch) -> FskPlan:
+    """From the drop-in path's one plan cache (_amr.plan_cache, shared with PSK)."""
     dev = _amr.default_device()
-    key = (int(n), float(baud), float(mark_freq), float(space_freq), float(samp_rate), dev)
+    key = ("fsk", int(n), float(baud), float(mark_freq), float(space_freq), float(samp_rate), dev)
     need = max(16, _amr.stream_bucket(batch, MAX_CHUNK))   # the FFT passes tile 8+ rows
-    return _fsk_cache.get(key, need, lambda m: FskPlan(n, baud, mark_freq, space_freq, samp_rate, max_streams=m,
-                                                       device=dev))
+    sps = int(samp_rate / baud)
+
+    def estimate(m):
+        return max(0, int(lib().amr_fsk_plan_bytes_estimate(int(n), sps, 7, m)))
+    return _amr.plan_cache.get(key, need, lambda m: FskPlan(n, baud, mark_freq, space_freq, samp_rate, max_streams=m,
+                                                            device=dev), estimate if sps >= 1 else None)
 
 
 def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate) -> list:

@@ -236,6 +236,10 @@ struct amr_comm {
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
   int device = 0;
+  int nranks = 1, rank = 0;
+  std::mutex mu;                // the host collectives' staging buffer
+  void* stage = nullptr;        // device staging of amr_comm_allgather_host / allreduce_max
+  int64_t stage_bytes = 0;
 };
 
 namespace {
@@ -255,6 +259,58 @@ int64_t row_s1_bytes(const amr_psk_plan* pl) {
 int64_t row_s3_bytes(const amr_psk_plan* pl) {
   return std::max(2 * pl->groups * pl->m2_pairs * kWave * 16, lane_s3_bytes(pl));
 }
+// The plan's geometry from its shape alone (no device work): PskParams'
+// sizes, groups, DF-II-T pair counts and the output capacity.  Shared by
+// amr_psk_plan_create and amr_psk_plan_bytes_estimate.
+void psk_geometry(amr_psk_plan* pl, int kind, int64_t n, int64_t sps, int64_t first, int bp_nt, int lp_nt,
+                  int64_t max_streams) {
+  PskParams& p = pl->p;
+  p.n = n;
+  p.pad1 = 3 * bp_nt;
+  p.pad2 = 3 * lp_nt;
+  p.m1 = n + 2 * p.pad1;
+  p.m2 = n + 2 * p.pad2;
+  p.sps = sps;
+  p.first = first;
+  p.kind = kind;
+  p.n_sym = n > first ? (n - first + sps - 1) / sps : 0;
+  const int bps = kind == AMR_PSK_QPSK ? 2 : 1;
+  p.n_bits = p.n_sym >= 2 ? (p.n_sym - 1) * bps : 0;
+  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
+  pl->max_streams = max_streams;
+  pl->groups = (max_streams + kWave - 1) / kWave;
+  const int qs1 = p.pad1 & 1, qs2 = p.pad2 & 1;
+  pl->m1_pairs = (p.m1 + qs1 + 1) >> 1;
+  pl->m2_pairs = (p.m2 + qs2 + 1) >> 1;
+  pl->out_cap = p.n_bits / 8 + 1;
+}
+
+// the device buffers amr_psk_plan_create allocates, in order (lane-layout sizes of s1 / s3)
+struct PskAlloc { int which; int64_t bytes; };
+std::vector<PskAlloc> psk_allocs(const amr_psk_plan* pl) {
+  const int64_t n = pl->p.n, g = pl->groups;
+  return {{0, n * 4 * (int64_t)sizeof(double)},
+          // + slack: K2q's prefetch runs up to a few chunks past the end (psk_kernels.hip)
+          {1, (n * 2 + 1024) * (int64_t)sizeof(double)},
+          // s1 doubles as the symbol buffer [2G][S][64] after the band-pass (psk_common.h sym_index)
+          {2, kFrontSlack * 8 + lane_s1_bytes(pl)},
+          {3, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
+          {4, kFrontSlack * 8 + lane_s3_bytes(pl)},
+          {5, g * kWave * pl->p.n_words * 4},
+          {6, 2 * g * kWave * 4}};     // low-pass flags, then band-pass flags
+}
+
+// the most the plan can hold: `allocated` with s1 / s3 grown to the row
+// layout's size (on its first call) + the host-API staging (allocated on
+// the first amr_psk_demod_host)
+int64_t psk_max_bytes(const amr_psk_plan* pl, int64_t allocated) {
+  const int64_t have1 = pl->s1_bytes ? pl->s1_bytes : kFrontSlack * 8 + lane_s1_bytes(pl);
+  const int64_t have3 = pl->s3_bytes ? pl->s3_bytes : kFrontSlack * 8 + lane_s3_bytes(pl);
+  const int64_t grow = std::max<int64_t>(0, kFrontSlack * 8 + row_s1_bytes(pl) - have1) +
+                       std::max<int64_t>(0, kFrontSlack * 8 + row_s3_bytes(pl) - have3);
+  return allocated + grow + pl->max_streams * pl->p.n * 8 + pl->max_streams * (pl->out_cap + 16);
+}
+
 // Grow one scratch buffer to `want` bytes.  The new block is allocated before
 // the old one is released, so a failed grow leaves the plan exactly as it was
 // (its pointers still valid for the layout that fits); only when that fails
@@ -414,19 +470,8 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
     delete pl;
     return fail(AMR_E_NODEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
+  psk_geometry(pl, kind, n, sps, first, bp_nt, lp_nt, max_streams);
   PskParams& p = pl->p;
-  p.n = n;
-  p.pad1 = 3 * bp_nt;
-  p.pad2 = 3 * lp_nt;
-  p.m1 = n + 2 * p.pad1;
-  p.m2 = n + 2 * p.pad2;
-  p.sps = sps;
-  p.first = first;
-  p.kind = kind;
-  p.n_sym = n > first ? (n - first + sps - 1) / sps : 0;
-  const int bps = kind == AMR_PSK_QPSK ? 2 : 1;
-  p.n_bits = p.n_sym >= 2 ? (p.n_sym - 1) * bps : 0;
-  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
   bool zodd = true;
   for (int i = 1; i < bp_nt; i += 2) zodd = zodd && is_pos_zero(bp_b[i]);
   p.bp_zero_odd = zodd ? 1 : 0;
@@ -451,28 +496,11 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   if (const char* f = std::getenv("AMR_FORCE_EXACT_LOWPASS"))
     if (f[0] == '1') pl->lp_exact_only = true;
 
-  pl->max_streams = max_streams;
-  pl->groups = (max_streams + kWave - 1) / kWave;
-  const int qs1 = p.pad1 & 1, qs2 = p.pad2 & 1;
-  pl->m1_pairs = (p.m1 + qs1 + 1) >> 1;
-  pl->m2_pairs = (p.m2 + qs2 + 1) >> 1;
-  pl->out_cap = p.n_bits / 8 + 1;
-  const int64_t g = pl->groups;
+  void** ptrs[] = {(void**)&pl->lo, (void**)&pl->lo2, (void**)&pl->s1_base, (void**)&pl->s2, (void**)&pl->s3_base,
+                   (void**)&pl->words, (void**)&pl->flags};
   struct A { void** ptr; int64_t bytes; };
-  const A allocs[] = {
-      {(void**)&pl->lo, n * 4 * (int64_t)sizeof(double)},
-      // + slack: K2q's prefetch runs up to a few chunks past the end (psk_kernels.hip)
-      {(void**)&pl->lo2, (n * 2 + 1024) * (int64_t)sizeof(double)},
-      // s1 doubles as the symbol buffer [2G][S][64] after the band-pass (psk_common.h sym_index)
-      // s1 / s3 sized for the lane layout (checkpoints, symbols, K3x's slots);
-      // the row layout's full-length intermediates are allocated on its first
-      // call (ensure_scratch)
-      {(void**)&pl->s1_base, kFrontSlack * 8 + lane_s1_bytes(pl)},
-      {(void**)&pl->s2, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
-      {(void**)&pl->s3_base, kFrontSlack * 8 + lane_s3_bytes(pl)},
-      {(void**)&pl->words, g * kWave * p.n_words * 4},
-      {(void**)&pl->flags, 2 * g * kWave * 4},   // low-pass flags, then band-pass flags
-  };
+  std::vector<A> allocs;
+  for (const PskAlloc& a : psk_allocs(pl)) allocs.push_back({ptrs[a.which], a.bytes});
   for (const A& a : allocs) {
     e = hipMalloc(a.ptr, (size_t)a.bytes);
     if (e != hipSuccess) {
@@ -519,12 +547,19 @@ int amr_psk_plan_destroy(amr_psk_plan* plan) {
 int64_t amr_psk_plan_out_capacity(const amr_psk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan* plan) {
   if (!plan) return -1;
-  // the most the plan can hold: scratch with s1 / s3 at the row layout's size
-  // (they grow on its first call) + the host-API staging (allocated on the
-  // first amr_psk_demod_host)
-  const int64_t grow = std::max<int64_t>(0, kFrontSlack * 8 + row_s1_bytes(plan) - plan->s1_bytes) +
-                       std::max<int64_t>(0, kFrontSlack * 8 + row_s3_bytes(plan) - plan->s3_bytes);
-  return plan->scratch_bytes + grow + plan->max_streams * plan->p.n * 8 + plan->max_streams * (plan->out_cap + 16);
+  return psk_max_bytes(plan, plan->scratch_bytes);
+}
+
+int64_t amr_psk_plan_bytes_estimate(int kind, int64_t n, int64_t sps, int64_t first, int bp_nt, int lp_nt,
+                                    int64_t max_streams) {
+  if ((kind != AMR_PSK_QPSK && kind != AMR_PSK_BPSK) || n < 1 || sps < 1 || first < 0 || max_streams < 1 ||
+      bp_nt < 1 || lp_nt < 1)
+    return fail(AMR_E_INVALID, "amr_psk_plan_bytes_estimate: bad argument");
+  amr_psk_plan pl;
+  psk_geometry(&pl, kind, n, sps, first, bp_nt, lp_nt, max_streams);
+  int64_t total = 0;
+  for (const PskAlloc& a : psk_allocs(&pl)) total += a.bytes;
+  return psk_max_bytes(&pl, total);
 }
 
 int amr_psk_plan_synchronize(amr_psk_plan* plan) {
@@ -599,6 +634,10 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   pl->last_exact = B;
   if (B == 0) return AMR_OK;
   hipStream_t st = pl->stream;
+  if (pl->timing) {
+    pl->ev_used[AMR_T_LAUNCH] = true;
+    HIP_TRY(hipEventRecord(pl->ev[AMR_T_LAUNCH][0], st));
+  }
   // Layout: one stream per lane (psk_lane_kernels.hip) once
   // enough streams are in flight on the device to give it waves -- it does
   // a third of the arithmetic per stream -- else the state-per-lane kernels
@@ -715,6 +754,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(launch_fec_decode(d_out, out_stride, d_len, B, d_fec, fec_stride, d_fec_len, d_crc, tab, x2n, st));
     HIP_TRY(mark(AMR_T_FEC, 1));
   }
+  if (pl->timing) HIP_TRY(hipEventRecord(pl->ev[AMR_T_LAUNCH][1], st));
   return AMR_OK;
 }
 
@@ -1049,7 +1089,7 @@ void gate_free(GatherGate& g) {
 // filters overlap the gather, and no plan's next batch queues behind another
 // plan's gather.
 int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
-                    GatherGate* gate) {
+                    GatherGate* gate, hipEvent_t done) {
   if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
   HIP_TRY(hipSetDevice(comm->device));
   hipEvent_t before = nullptr;
@@ -1067,6 +1107,7 @@ int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t by
     HIP_TRY(hipEventRecord(gate->ev, comm->stream));
     gate->pending = true;
   }
+  if (done) HIP_TRY(hipEventRecord(done, comm->stream));
   return AMR_OK;
 }
 }  // namespace amr
@@ -1089,6 +1130,8 @@ int amr_comm_create(amr_comm** comm, const uint8_t* id, int nranks, int rank, in
   HIP_TRY(hipSetDevice(device));
   auto* c = new amr_comm();
   c->device = device;
+  c->nranks = nranks;
+  c->rank = rank;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
@@ -1110,6 +1153,7 @@ int amr_comm_destroy(amr_comm* comm) {
   if (!comm) return AMR_OK;
   (void)hipSetDevice(comm->device);
   if (comm->stream) (void)hipStreamSynchronize(comm->stream);
+  if (comm->stage) (void)hipFree(comm->stage);
   if (comm->comm) ncclCommDestroy(comm->comm);
   if (comm->stream) (void)hipStreamDestroy(comm->stream);
   delete comm;
@@ -1126,12 +1170,68 @@ int amr_comm_destroy(amr_comm* comm) {
 int amr_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_psk_plan* plan) {
   if (!plan) return allgather_after(comm, d_send, d_recv, bytes_per_rank, nullptr, nullptr);
   std::lock_guard<std::mutex> lk(plan->mu);
-  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate);
+  // the launch's timing slot ends when its outputs are gathered (AMR_T_LAUNCH)
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate,
+                         plan->timing && plan->ev_used[AMR_T_LAUNCH] ? plan->ev[AMR_T_LAUNCH][1] : nullptr);
 }
 
 int amr_comm_synchronize(amr_comm* comm) {
   if (!comm) return fail(AMR_E_INVALID, "comm is NULL");
   HIP_TRY(hipSetDevice(comm->device));
+  HIP_TRY(hipStreamSynchronize(comm->stream));
+  return AMR_OK;
+}
+
+int amr_comm_world(const amr_comm* comm, int* nranks, int* rank) {
+  if (!comm || !nranks || !rank) return fail(AMR_E_INVALID, "amr_comm_world: NULL argument");
+  *nranks = comm->nranks;
+  *rank = comm->rank;
+  return AMR_OK;
+}
+
+namespace {
+// the comm's device staging buffer, at least `bytes` (caller holds comm->mu)
+int comm_stage(amr_comm* c, int64_t bytes) {
+  if (c->stage_bytes >= bytes && c->stage) return AMR_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->stage) HIP_TRY(hipFree(c->stage));
+  c->stage = nullptr;
+  c->stage_bytes = 0;
+  HIP_TRY(hipMalloc(&c->stage, (size_t)bytes));
+  c->stage_bytes = bytes;
+  return AMR_OK;
+}
+}  // namespace
+
+int amr_comm_allgather_host(amr_comm* comm, const void* send, void* recv, int64_t bytes_per_rank) {
+  if (!comm || bytes_per_rank < 0 || (bytes_per_rank && (!send || !recv)))
+    return fail(AMR_E_INVALID, "amr_comm_allgather_host: bad argument");
+  if (bytes_per_rank == 0) return AMR_OK;
+  std::lock_guard<std::mutex> lk(comm->mu);
+  HIP_TRY(hipSetDevice(comm->device));
+  const int64_t total = bytes_per_rank * (1 + comm->nranks);     // [send | recv (world slots)]
+  if (int rc = comm_stage(comm, total)) return rc;
+  uint8_t* d_send = static_cast<uint8_t*>(comm->stage);
+  uint8_t* d_recv = d_send + bytes_per_rank;
+  HIP_TRY(hipMemcpyAsync(d_send, send, (size_t)bytes_per_rank, hipMemcpyHostToDevice, comm->stream));
+  ncclResult_t r = ncclAllGather(d_send, d_recv, (size_t)bytes_per_rank, ncclUint8, comm->comm, comm->stream);
+  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+  HIP_TRY(hipMemcpyAsync(recv, d_recv, (size_t)(bytes_per_rank * comm->nranks), hipMemcpyDeviceToHost, comm->stream));
+  HIP_TRY(hipStreamSynchronize(comm->stream));
+  return AMR_OK;
+}
+
+int amr_comm_allreduce_max(amr_comm* comm, double* values, int64_t count) {
+  if (!comm || count < 0 || (count && !values)) return fail(AMR_E_INVALID, "amr_comm_allreduce_max: bad argument");
+  if (count == 0) return AMR_OK;
+  std::lock_guard<std::mutex> lk(comm->mu);
+  HIP_TRY(hipSetDevice(comm->device));
+  if (int rc = comm_stage(comm, count * 8)) return rc;
+  double* d = static_cast<double*>(comm->stage);
+  HIP_TRY(hipMemcpyAsync(d, values, (size_t)(count * 8), hipMemcpyHostToDevice, comm->stream));
+  ncclResult_t r = ncclAllReduce(d, d, (size_t)count, ncclFloat64, ncclMax, comm->comm, comm->stream);
+  if (r != ncclSuccess) return fail(AMR_E_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  HIP_TRY(hipMemcpyAsync(values, d, (size_t)(count * 8), hipMemcpyDeviceToHost, comm->stream));
   HIP_TRY(hipStreamSynchronize(comm->stream));
   return AMR_OK;
 }

@@ -44,9 +44,10 @@ hipError_t gate_wait(GatherGate& g, hipStream_t st);   // `st` waits for the pen
 hipError_t gate_sync(GatherGate& g);                   // the host waits for it
 void gate_free(GatherGate& g);
 // the RCCL all-gather of amr_allgather / amr_fsk_allgather (api.cpp); gate
-// NULL: no ordering against the producer stream
+// NULL: no ordering against the producer stream; `done` (optional) is
+// recorded on the comm's stream after the gather (the producer's launch timing)
 int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
-                    GatherGate* gate);
+                    GatherGate* gate, hipEvent_t done = nullptr);
 }  // namespace amr
 
 #define HIP_TRY(expr)                                                                              \

@@ -131,6 +131,34 @@ hipError_t six_conv(const FftPlan& f, double2* a, double2* tmp, int64_t batch, h
   return e;
 }
 
+// How FFT_n runs (host only): two-pass (M = n = n1 * n2), six-step (M = n =
+// L1 * L2) or Bluestein over a two-pass / six-step M.  False: no plan.
+struct FftShape {
+  int64_t M = 0;
+  bool bluestein = false, six = false;
+  int n1 = 0, n2 = 0;            // the two-pass split of M (when !six)
+  int64_t L1 = 0, L2 = 0;        // the six-step split of M (when six)
+};
+bool fft_shape(int64_t n, FftShape& sh) {
+  int a = 0, b = 0;
+  if (fft_split(n, a, b)) {
+    sh.M = n;
+  } else if (fft_six_split(n, sh.L1, sh.L2)) {
+    sh.M = n;
+    sh.six = true;
+  } else {
+    sh.bluestein = true;
+    sh.M = fft_good_size(2 * n - 1);
+    if (sh.M < 0) return false;
+    if (!fft_split(sh.M, a, b)) {
+      if (!fft_six_split(sh.M, sh.L1, sh.L2)) return false;
+      sh.six = true;
+    }
+  }
+  if (!sh.six) fft_split(sh.M, sh.n1, sh.n2);
+  return true;
+}
+
 // Plans FFT_n for up to max_batch rows; needs the stream for the Bluestein kernel FFT.
 int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st, int64_t max_batch) {
   static std::once_flag smem_once;
@@ -139,22 +167,12 @@ int fft_plan_init(FftPlan& f, int64_t n, hipStream_t st, int64_t max_batch) {
   HIP_TRY(smem_err);
   f.n = n;
   f.max_batch = max_batch;
-  int a = 0, b = 0;
-  int64_t L1 = 0, L2 = 0;
-  if (fft_split(n, a, b)) {
-    f.M = n;
-  } else if (fft_six_split(n, L1, L2)) {
-    f.M = n;
-    f.six = true;
-  } else {
-    f.bluestein = true;
-    f.M = fft_good_size(2 * n - 1);
-    if (f.M < 0) return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
-    if (!fft_split(f.M, a, b)) {
-      if (!fft_six_split(f.M, L1, L2)) return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
-      f.six = true;
-    }
-  }
+  FftShape sh;
+  if (!fft_shape(n, sh)) return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
+  f.M = sh.M;
+  f.bluestein = sh.bluestein;
+  f.six = sh.six;
+  const int64_t L1 = sh.L1, L2 = sh.L2;
   const int64_t M = f.M;
   if (f.six) {
     f.L1 = L1;
@@ -426,8 +444,11 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   for (bool& u : pl->ev_used) u = false;
   if (B == 0) return AMR_OK;
   if (pl->p.n_bits == 0) return fsk_empty_outputs(pl, B, d_len, d_sync);
+  HIP_TRY(mark_fsk(pl, AMR_TF_LAUNCH, 0));
   if (int rc = run_fsk_front(pl, d_x, dtype, B, x_stride, false)) return rc;
-  return run_fsk_back(pl, B, d_out, out_stride, d_len, d_sync);
+  if (int rc = run_fsk_back(pl, B, d_out, out_stride, d_len, d_sync)) return rc;
+  HIP_TRY(mark_fsk(pl, AMR_TF_LAUNCH, 1));
+  return AMR_OK;
 }
 
 constexpr int64_t kStageAlign = 256;
@@ -496,12 +517,12 @@ int ensure_out_staging(amr_fsk_plan* pl) {
 // two-pass length n = n1 * n2 with n1 a multiple of sps and a decision window.
 // Every index the kernels use is checked here on the host (the float
 // divisions of lc_div, the [L | D] offsets as a bijection onto [0, n)).
-LiveCols plan_live_cols(const FftPlan& f, const FskParams& p) {
+LiveCols plan_live_cols(const FftShape& f, const FskParams& p) {
   LiveCols lc{};
   static const bool off = [] { const char* e = std::getenv("AMR_FSK_LIVE"); return e && e[0] == '0'; }();
   const int64_t q = p.sps / 4, half = p.sps / 2;
   if (off || f.bluestein || f.six || p.n_bits == 0 || q < 1) return lc;
-  const int n1 = f.d.n1, n2 = f.d.n2;
+  const int n1 = f.n1, n2 = f.n2;
   if (p.sps > n1 || n1 % p.sps != 0 || (int64_t)n1 * n2 != p.n) return lc;
   lc.n1 = n1;
   lc.n2 = n2;
@@ -532,9 +553,66 @@ LiveCols plan_live_cols(const FftPlan& f, const FskParams& p) {
   return lc;
 }
 
+// Sizes of an FSK plan's device buffers from its shape alone (no device
+// work): amr_fsk_plan_create allocates exactly these; amr_fsk_plan_bytes_estimate
+// sums them for the drop-in plan cache before it creates a plan.
+struct FskGeom {
+  FskParams p{};
+  FftShape sh;
+  int64_t z = 0, u = 0, v = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
+  int64_t total() const { return z + u + v + cmp + words + six + staging + out; }
+};
+bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& g) {
+  FskParams& p = g.p;
+  p.n = n;
+  p.sps = sps;
+  p.nt = nt;
+  p.pad = 3 * nt;
+  const int64_t q = sps / 4, half = sps / 2;
+  p.n_bits = (q > 0 && n > half) ? (n - half + sps - 1) / sps : 0;
+  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
+  g.out_cap = p.n_bits / 8 + 1;
+  if (!fft_shape(n, g.sh)) return false;
+  const int64_t M = g.sh.M;
+  const bool plain = g.sh.bluestein || g.sh.six;   // epilogue in natural order (post kernel)
+  p.rn1 = plain ? n : g.sh.n1;
+  p.rn2 = plain ? 1 : g.sh.n2;
+  p.lc = plan_live_cols(g.sh, p);
+  p.bits_stride = p.lc.on ? (int64_t)((p.lc.nl + 7) >> 3) * p.rn2 : fft_bits_stride(p.rn1, p.rn2);
+  p.inv_rn1 = 1.0f / (float)p.rn1;
+  const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
+  if (p.lc.on) {
+    // C: the live columns' transform; before the column pass it holds F1's
+    // checkpoints and (host entries) the staged input -- 4 B per sample for
+    // float32 / int16 in one chunk, float64 in chunks of >= 32 streams
+    const int64_t c = std::min<int64_t>(max_streams, 32);
+    g.u = std::max({max_streams * (int64_t)p.lc.nl * p.lc.n2 * 16, align_up(max_streams * n * 4, kStageAlign) + s1_bytes,
+                    align_up(c * n * 8, kStageAlign) + fsk_bandpass_scratch_bytes(c, n, p.pad)});
+    g.staging = 0;                                   // staged inside C
+  } else {
+    g.u = std::max(max_streams * M * 16, s1_bytes);
+    g.v = max_streams * M * 16;
+    g.staging = max_streams * n * 8;                 // d_x, allocated on the first host call
+  }
+  g.z = max_streams * n * 16;
+  g.cmp = max_streams * p.bits_stride;
+  g.words = max_streams * p.n_words * 4;
+  g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
+  g.out = max_streams * (g.out_cap + 16);            // host-API output staging
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+int64_t amr_fsk_plan_bytes_estimate(int64_t n, int64_t sps, int ntaps, int64_t max_streams) {
+  if (n < 1 || sps < 1 || ntaps < 1 || max_streams < 1)
+    return fail(AMR_E_INVALID, "amr_fsk_plan_bytes_estimate: bad argument");
+  FskGeom g;
+  if (!fsk_geometry(n, sps, ntaps, max_streams, g)) return fail(AMR_E_INVALID, "no FFT plan for this length");
+  return g.total();
+}
 
 int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, const double* mb, const double* ma,
                         const double* mzi, const double* sb, const double* sa, const double* szi, int nt,
@@ -554,14 +632,13 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     delete pl;
     return fail(AMR_E_NODEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
   }
+  FskGeom geo;
+  if (!fsk_geometry(n, sps, nt, max_streams, geo)) {
+    delete pl;
+    return fail(AMR_E_INVALID, "no FFT plan for length " + std::to_string(n));
+  }
   FskParams& p = pl->p;
-  p.n = n;
-  p.sps = sps;
-  p.nt = nt;
-  p.pad = 3 * nt;
-  const int64_t q = sps / 4, half = sps / 2;
-  p.n_bits = (q > 0 && n > half) ? (n - half + sps - 1) / sps : 0;
-  p.n_words = p.n_bits > 0 ? (p.n_bits + 31) / 32 : 1;
+  p = geo.p;
   for (int i = 0; i < nt; ++i) {
     pl->f.b[0][i] = mb[i];
     pl->f.a[0][i] = ma[i];
@@ -573,7 +650,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->f.zi[1][i] = szi[i];
   }
   pl->max_streams = max_streams;
-  pl->out_cap = p.n_bits / 8 + 1;
+  pl->out_cap = geo.out_cap;
   e = hipStreamCreateWithFlags(&pl->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     fsk_plan_free(pl);
@@ -583,33 +660,15 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     fsk_plan_free(pl);
     return rc;
   }
-  const int64_t M = pl->fft.M;
-  const bool plain = pl->fft.bluestein || pl->fft.six;   // epilogue in natural order (post kernel)
-  p.rn1 = plain ? n : pl->fft.d.n1;
-  p.rn2 = plain ? 1 : pl->fft.d.n2;
-  if (pl->fft.six) pl->scratch_bytes += 2 * max_streams * M * 16;
-  p.lc = plan_live_cols(pl->fft, p);
-  p.bits_stride = p.lc.on ? (int64_t)((p.lc.nl + 7) >> 3) * p.rn2 : fft_bits_stride(p.rn1, p.rn2);
-  p.inv_rn1 = 1.0f / (float)p.rn1;
-  const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
-  if (p.lc.on) {
-    // C: the live columns' transform; before the column pass it holds F1's
-    // checkpoints and (host entries) the staged input -- 4 B per sample for
-    // float32 / int16 in one chunk, float64 in chunks of >= 32 streams
-    const int64_t g = std::min<int64_t>(max_streams, 32);
-    pl->u_bytes = std::max({max_streams * (int64_t)p.lc.nl * p.lc.n2 * 16,
-                            align_up(max_streams * n * 4, kStageAlign) + s1_bytes,
-                            align_up(g * n * 8, kStageAlign) + fsk_bandpass_scratch_bytes(g, n, p.pad)});
-  } else {
-    pl->u_bytes = std::max(max_streams * M * 16, s1_bytes);
-  }
+  if (pl->fft.six) pl->scratch_bytes += geo.six;
+  pl->u_bytes = geo.u;
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
-      {(void**)&pl->z, max_streams * n * 16},
-      {(void**)&pl->u, pl->u_bytes},
-      {(void**)&pl->v, p.lc.on ? 0 : max_streams * M * 16},
-      {(void**)&pl->cmp, max_streams * p.bits_stride},
-      {(void**)&pl->words, max_streams * p.n_words * 4},
+      {(void**)&pl->z, geo.z},
+      {(void**)&pl->u, geo.u},
+      {(void**)&pl->v, geo.v},
+      {(void**)&pl->cmp, geo.cmp},
+      {(void**)&pl->words, geo.words},
   };
   for (const A& a : allocs) {
     if (a.bytes == 0) continue;
@@ -634,7 +693,7 @@ int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   // scratch + the host-API staging (allocated on the first amr_fsk_demod_host;
   // a live-column plan stages its input inside C)
   const int64_t staging = plan->p.lc.on ? 0 : plan->max_streams * plan->p.n * 8;
-  return plan->scratch_bytes + staging + plan->max_streams * (plan->out_cap + 16);
+  return plan->scratch_bytes + staging + plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
@@ -675,7 +734,8 @@ int amr_fsk_plan_timings(amr_fsk_plan* plan, float* ms, int count) {
 int amr_fsk_allgather(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, amr_fsk_plan* plan) {
   if (!plan) return allgather_after(comm, d_send, d_recv, bytes_per_rank, nullptr, nullptr);
   std::lock_guard<std::mutex> lk(plan->mu);
-  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate);
+  return allgather_after(comm, d_send, d_recv, bytes_per_rank, plan->stream, &plan->gate,
+                         plan->timing && plan->ev_used[AMR_TF_LAUNCH] ? plan->ev[AMR_TF_LAUNCH][1] : nullptr);
 }
 
 int amr_fsk_demod_device(amr_fsk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,

@@ -462,17 +462,32 @@ def decode_from_buffer(data: np.ndarray, mode: str, symbol_rate: int) -> list:
         return []
 
 
-def decode_from_buffer_batch(data: np.ndarray, mode: str, symbol_rate: int) -> list:
-    """Batched decode_from_buffer: [B, N] streams in one GPU call; list of saved-path lists."""
+def decode_from_buffer_batch(data: np.ndarray, mode: str, symbol_rate: int, transport=None, root: int = 0) -> list:
+    """Batched decode_from_buffer (decoder.py:417-464): [B, N] streams in one
+    GPU call; a list of saved-path lists, one per stream.
+
+    transport (multi.RcclTransport, one process per GPU): the global batch is
+    sharded over the ranks -- each demodulates its contiguous shard on its own
+    GPU, the decoded bytes are all-gathered over RCCL (multi.demod_sharded) --
+    and rank `root` parses the frames and writes the files of the whole batch;
+    the other ranks return an empty list per stream."""
     data = np.asarray(data)
-    try:
+
+    def demod(x):
         if mode == "BPSK":
-            raws = modem.bpsk_demodulate_batch(data, baud=symbol_rate)
-        elif mode.startswith("FSK"):
+            return modem.bpsk_demodulate_batch(x, baud=symbol_rate)
+        if mode.startswith("FSK"):
             baud = 9600 if "9600" in mode else 19200 if "19200" in mode else 1200
-            raws = modem.fsk_demodulate_batch(data, baud=baud)
+            return modem.fsk_demodulate_batch(x, baud=baud)
+        return modem.qpsk_demodulate_batch(x, baud=symbol_rate)
+    try:
+        if transport is None:
+            raws = demod(data)
         else:
-            raws = modem.qpsk_demodulate_batch(data, baud=symbol_rate)
+            import multi
+            raws = multi.demod_sharded(data, demod, transport)
+            if transport.rank != root:
+                return [[] for _ in range(len(data))]
     except Exception as e:
         print(f"Erro crítico na demodulação: {e}")
         traceback.print_exc()

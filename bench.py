@@ -25,6 +25,8 @@ that the gathered buffer equals every rank's own output.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W] [--inflight P]
         multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+        (the launcher only starts the ranks: bootstrap, barriers and gathers
+        are multi.py's -- a file store and RCCL, no torch in the process)
 """
 from __future__ import annotations
 
@@ -59,7 +61,7 @@ HBM_MIXED_GBS = 5200.0         # measured streaming rate at 1:1..2:1 read:write 
 PROFILE_ROUND = "r02"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
 
-# BASELINE.json configs[1..4] (configs[0] is the reference's CPU plumbing case)
+# BASELINE.json configs[1..4], 0-based (configs[0] is the reference's CPU plumbing case)
 WORKLOADS = {
     "qpsk9600": dict(baud=9600.0, batch=4096, strong=False, fsk=False, fec=False,
                      metric="demod Msymbols/s (batch) + achieved HBM GB/s, QPSK@9600/96kHz, 1/2/4/8 GPU"),
@@ -80,44 +82,28 @@ def log(*a):
 
 
 def dist_setup(force=False):
-    """torch.distributed (gloo: barriers, the max over ranks, the gather check's
-    digests) for N > 1, or with `force` for one rank under torch.distributed.run."""
+    """The N > 1 control plane, torch-free (multi.py): the RCCL unique id
+    through a bootstrap store (multi.store_from_env: a FileStore named after
+    torch.distributed.run's MASTER_PORT and agent process), then one RCCL
+    communicator per rank (multi.RcclTransport) that carries the barriers,
+    the max over ranks, the gather check and the per-launch all-gathers of
+    decoded bytes.  With `force`, the same for one rank."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 or force:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
-        return dist, world, rank, local
+        import multi
+        return multi.RcclTransport(multi.store_from_env(rank, world), rank, world, local), world, rank, local
     return None, 1, 0, local
 
 
-def barrier(dist):
-    if dist is not None:
-        dist.barrier()
+def barrier(tp):
+    if tp is not None:
+        tp.barrier()
 
 
-def max_over_ranks(dist, v: float) -> float:
-    if dist is None:
-        return v
-    import torch
-    t = torch.tensor([v], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def row_digest(rows: np.ndarray, lens: np.ndarray) -> list:
-    """Per-stream digest of decoded bytes and length (the N>1 gather check)."""
-    return [hashlib.blake2b(rows[i, :max(0, int(lens[i]))].tobytes() + int(lens[i]).to_bytes(8, "little", signed=True),
-                            digest_size=8).hexdigest() for i in range(rows.shape[0])]
-
-
-def gather_verdict(gathered_digests, own_digests, shard_sizes):
-    """Slice r of the gathered buffer (as rank 0 holds it) must equal rank r's
-    own output, stream for stream (only the rank's real streams; the slot
-    padding of strong-scaling shards is not compared)."""
-    bad = [r for r, n in enumerate(shard_sizes) if gathered_digests[r][:n] != own_digests[r][:n]]
-    return bad
+def max_over_ranks(tp, v: float) -> float:
+    return v if tp is None else tp.max(v)
 
 
 class Dev:
@@ -139,22 +125,22 @@ class Dev:
 
 
 def workload_sizes(name, batch_arg, world, rank):
-    """(B local, B global, first global stream, gather slot) for a rank."""
-    from multi import shard_range
+    """(B local, B global, first global stream, gather slot) for a rank: a
+    strong-scaling global batch sharded by multi.ShardLayout, or (weak) every
+    rank its own batch -- the same layout over world x B streams."""
+    import multi
     W = WORKLOADS[name]
-    if W["strong"]:
-        B_global = batch_arg or W["batch"]
-        lo_s, hi_s = shard_range(B_global, rank, world)
-        return hi_s - lo_s, B_global, lo_s, -(-B_global // world)
-    B = batch_arg or W["batch"]
-    return B, world * B, rank * B, B
+    B_global = (batch_arg or W["batch"]) * (1 if W["strong"] else world)
+    lay = multi.ShardLayout(B_global, world)
+    lo_s, hi_s = lay.shard(rank)
+    return hi_s - lo_s, B_global, lo_s, lay.b_slot
 
 
-def run_workload(name, args, dist, world, rank, dev, comm, headline):
+def run_workload(name, args, tp, world, rank, dev, comm, headline):
     W = WORKLOADS[name]
     L = _amr.lib()
     fsk, fec_fused, strong = W["fsk"], W["fec"], W["strong"]
-    from multi import shard_range
+    import multi
     B, B_global, lo_s, B_slot = workload_sizes(name, args.batch, world, rank)
     N = args.samples
     baud = W["baud"]
@@ -240,12 +226,17 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         """streams of launch j of the timed region (the last one may hold fewer steps)"""
         return launch_sizes[j]
 
+    names = [k for k in names if k != "launch"]
     kt = {k: 0.0 for k in names}
     nt = [0]
+    launch_ms = []                   # whole launches: first kernel -> outputs written (N = 1) / gathered (N > 1)
 
     def collect(c):
         _amr.check(sync_fn(c["plan"].handle))
-        for k, v in c["plan"].timings().items():
+        t = c["plan"].timings()
+        if "launch" in t:
+            launch_ms.append(t.pop("launch"))
+        for k, v in t.items():
             kt[k] += v
         nt[0] += 1
 
@@ -269,9 +260,10 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     _amr.check(L.amr_device_synchronize())
     kt = {k: 0.0 for k in names}
     nt = [0]
+    launch_ms.clear()
 
     # ---- timed region: exactly K batches, at most P in flight ----------------
-    barrier(dist)
+    barrier(tp)
     _amr.check(L.amr_device_synchronize())
     t0 = time.perf_counter()
     if args.host_wait:
@@ -294,9 +286,9 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         for j in range(max(0, n_launch - P), n_launch):
             collect(ctx[j % P])
     _amr.check(L.amr_device_synchronize())
-    barrier(dist)
+    barrier(tp)
     dt = time.perf_counter() - t0
-    dt = max_over_ranks(dist, dt)
+    dt = max_over_ranks(tp, dt)
     layout = ctx[0]["plan"].last_layout() if not fsk else "fsk"
     ms_per_step = dt / K * 1e3
     value = B_global * sym_per_stream / (dt / K) / 1e6
@@ -307,14 +299,14 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     sustained = None
     if headline and args.sustain_seconds > 0:
         n_s = max(P, int(round(args.sustain_seconds / max(1e-4, dt / n_launch) / P)) * P)
-        barrier(dist)
+        barrier(tp)
         _amr.check(L.amr_device_synchronize())
         t1 = time.perf_counter()
         for j in range(n_s):
             step(ctx[j % P])
         _amr.check(L.amr_device_synchronize())
-        barrier(dist)
-        ds = max_over_ranks(dist, time.perf_counter() - t1)
+        barrier(tp)
+        ds = max_over_ranks(tp, time.perf_counter() - t1)
         sustained = {"steps": n_s * C, "seconds": round(ds, 3), "ms_per_step": round(ds / (n_s * C) * 1e3, 4),
                      "value": round(B_global * sym_per_stream * n_s * C / ds / 1e6, 3),
                      "what": f"{n_s} more launches of the same pipeline ({P} in flight), timed as the headline"}
@@ -364,13 +356,9 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         gl = np.empty((world, R), np.int64)
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gp), ctx[last]["gather"], gp.nbytes))
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gl), ctx[last]["gather_len"], gl.nbytes))
-        own = [None] * world
-        dist.all_gather_object(own, row_digest(o, ln))
-        sizes = [C * workload_sizes(name, args.batch, world, r)[0] for r in range(world)]
-        bad = gather_verdict([row_digest(gp[r], gl[r]) for r in range(world)], own, sizes)
-        flags = [None] * world
-        dist.all_gather_object(flags, bad)
-        bad_any = sorted({b for f in flags for b in f})
+        layout = multi.ShardLayout(B_global, world, C)
+        assert layout.rows == R and layout.launch_rows(rank) == C * B
+        bad_any = multi.gather_check(gp, gl, o, ln, layout, tp)
         gather_check = (f"ok: every rank's gathered [{world}][{R}][{cap}] buffer == each rank's own bytes and "
                         "lengths" if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
 
@@ -379,7 +367,9 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
     host_res = None
     if rank == 0:
         from oracle import oracle
-        threads = max(1, min(16, os.cpu_count() or 1))
+        # the CPU baseline runs on every core this process may use (its
+        # affinity mask: the GPU box's host cores as the scheduler grants them)
+        threads = max(1, len(os.sched_getaffinity(0)))
         xh = np.empty((BL, N), np.float32)
         checked, n_slots, bad_total = 0, 0, []
         cpu = None
@@ -416,6 +406,9 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                        (" + oracle.fec_decode" if fec_fused else ""))
                 cpu = {"value": round(reps * len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s",
                        "cores": threads, "kind": "port",
+                       "cores_note": f"OpenMP threads = len(os.sched_getaffinity(0)) on this host "
+                                     f"(os.cpu_count() {os.cpu_count()}, OMP_NUM_THREADS "
+                                     f"{os.environ.get('OMP_NUM_THREADS', 'unset')})",
                        "sample": f"{len(idx)} of the {BL} streams of benchmark batch 0 ({N} samples each)"
                                  + (f", {reps} passes" if reps > 1 else "") + f" through {how}, {cdt:.2f} s wall"}
             o, ln = outs[k]
@@ -428,11 +421,12 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                   f"{P} in-flight batches)" + (" (FEC output)" if fec_fused else "")) if checked else "skipped (--no-cpu)"
         if headline and not fsk and cpu is not None:
             _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[0]["x"], xh.nbytes))
+            n1 = min(B, 256)
             t1 = time.perf_counter()
-            oracle.psk_demod_batch("qpsk", xh[:64], baud, n_threads=1)
+            oracle.psk_demod_batch("qpsk", xh[:n1], baud, n_threads=1)
             d1 = time.perf_counter() - t1
-            cpu["value_1core"] = round(64 * sym_per_stream / d1 / 1e6, 3)
-            cpu["sample_1core"] = f"64 streams, 1 thread, {d1:.2f} s wall"
+            cpu["value_1core"] = round(n1 * sym_per_stream / d1 / 1e6, 3)
+            cpu["sample_1core"] = f"{n1} streams of batch 0, 1 thread, {d1:.2f} s wall"
 
         # ---- roofline ----
         # algorithmic bytes per launch: the path's compulsory input + output,
@@ -504,15 +498,15 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
         }
         if fsk:
             workload = (f"FSK@{int(baud)} 96kHz tones {mark:g}/{space:g} Hz, batch {B} x {N} float32 streams per GPU "
-                        "(BASELINE configs[3] at SURVEY §6's valid tones: the reference's defaults raise)")
+                        "(BASELINE.json configs[2] at SURVEY §6's valid tones: the reference's defaults raise)")
         elif name == "ofdm8":
             workload = (f"OFDM8 = QPSK@{int(baud)} 96kHz (modem.py:375-376), global batch {B_global} x {N} float32 "
-                        f"streams sharded over {world} GPU(s) (BASELINE configs[4])")
+                        f"streams sharded over {world} GPU(s) (BASELINE.json configs[3])")
         elif fec_fused:
             workload = (f"8PSK@{int(baud)} = QPSK path (modem.py:348) + ReedSolomonFEC.decode fused, global batch "
-                        f"{B_global} x {N} float32 streams sharded over {world} GPU(s) (BASELINE configs[5])")
+                        f"{B_global} x {N} float32 streams sharded over {world} GPU(s) (BASELINE.json configs[4])")
         else:
-            workload = f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU (BASELINE configs[1])"
+            workload = f"QPSK@{int(baud)} 96kHz, batch {B} x {N} float32 streams per GPU (BASELINE.json configs[1])"
         result = {
             "metric": W["metric"], "value": round(value, 3), "unit": "Msym/s", "n_gpus": world, "steps": K,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
@@ -525,6 +519,13 @@ def run_workload(name, args, dist, world, rank, dev, comm, headline):
                        "inputs": f"{P} distinct device batches per rank: {D} clean frames + per-slot N(0, 0.05^2) "
                                  "noise (amr_synth_tile_noise)"},
             "latency_ms_one_batch": lat1["ms"] if lat1 else (round(float(np.median(lat)) * 1e3, 3) if lat else None),
+            "latency_ms_per_global_batch": round(float(np.mean(launch_ms)), 3) if launch_ms else None,
+            "latency_per_global_batch_note": (
+                f"in the timed pipeline ({P} launches in flight, {C} global batch(es) per launch): HIP events from "
+                "a launch's first kernel to its outputs " + ("all-gathered (RCCL, the comm stream)" if comm is not None
+                                                             else "written") +
+                f", averaged over the last {len(launch_ms)} timed launches; every global batch of a launch "
+                "finishes with it") if launch_ms else None,
             "latency_layout": lat1["layout"] if lat1 else latency_layout,
             "latency_note": ("one batch on a plan without the in-flight hint (a single-batch caller's layout), bytes "
                              f"equal to the lane layout's: {lat1['bytes_equal_lane_layout']}; the lane layout alone: "
@@ -826,30 +827,21 @@ def main():
                     help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
     args = ap.parse_args()
 
-    dist, world, rank, local = dist_setup(args.force_comm)
-    dev = local
     L = _amr.lib()
+    tp, world, rank, local = dist_setup(args.force_comm)
+    dev = local
     _amr.check(L.amr_set_device(dev))
-    comm = None
-    if world > 1 or args.force_comm:
-        uid = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            _amr.check(L.amr_comm_unique_id(uid))
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
-        comm = ctypes.c_void_p()
-        _amr.check(L.amr_comm_create(ctypes.byref(comm), uid, world, rank, dev))
+    comm = tp.comm if tp is not None else None
 
-    result = run_workload(args.workload, args, dist, world, rank, dev, comm, headline=True)
+    result = run_workload(args.workload, args, tp, world, rank, dev, comm, headline=True)
     if args.workload == "qpsk9600" and not args.no_sub and not args.batch:
         subs = {}
         for name in ("fsk9600", "ofdm8", "psk8fec"):
-            r = run_workload(name, args, dist, world, rank, dev, comm, headline=False)
+            r = run_workload(name, args, tp, world, rank, dev, comm, headline=False)
             if rank == 0 and r is not None:
                 subs[name] = {k: r[k] for k in ("metric", "value", "unit", "steps", "ms_per_step", "scaling", "parity",
-                                                "latency_ms_one_batch", "kernel_ms", "kernel_ms_solo", "cpu_baseline",
-                                                "config")}
+                                                "latency_ms_one_batch", "latency_ms_per_global_batch", "kernel_ms",
+                                                "kernel_ms_solo", "cpu_baseline", "config")}
                 subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
                 for k in ("gather_check", "exact_path_streams"):
@@ -860,11 +852,8 @@ def main():
     if rank == 0 and result is not None:
         result["build_id"] = L.amr_build_id().decode()
         print(json.dumps(result), flush=True)
-    if comm is not None:
-        L.amr_comm_destroy(comm)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if tp is not None:
+        tp.close()
 
 
 if __name__ == "__main__":

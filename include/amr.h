@@ -82,7 +82,9 @@ extern "C" {
 #define AMR_T_LOWPASS_EXACT 3
 #define AMR_T_SYNC_PACK 4
 #define AMR_T_FEC 5
-#define AMR_T_COUNT 6
+#define AMR_T_LAUNCH 6     /* the whole launch: first kernel start -> last output written, or, when the
+                            * launch's outputs are all-gathered (amr_allgather with this plan), -> gathered */
+#define AMR_T_COUNT 7
 
 typedef struct amr_psk_plan amr_psk_plan;
 typedef struct amr_comm amr_comm;
@@ -125,6 +127,10 @@ int64_t amr_psk_plan_out_capacity(const amr_psk_plan *plan);
  * are allocated on the first call that runs that layout) + the host-API
  * staging (allocated on the first amr_psk_demod_host call) */
 int64_t amr_psk_plan_scratch_bytes(const amr_psk_plan *plan);
+/* the amr_psk_plan_scratch_bytes a plan of this shape would report, without
+ * creating it (the drop-in plan cache evicts for it first); < 0 on bad args */
+int64_t amr_psk_plan_bytes_estimate(int kind, int64_t n_samples, int64_t sps, int64_t first, int bp_ntaps,
+                                    int lp_ntaps, int64_t max_streams);
 int amr_psk_plan_synchronize(amr_psk_plan *plan);
 /* record per-kernel HIP events on the plan's stream (1) or not (0) */
 int amr_psk_plan_enable_timing(amr_psk_plan *plan, int on);
@@ -199,7 +205,8 @@ int amr_psk_slice_host(int kind, const double *sym, int64_t n_streams, int64_t n
 #define AMR_TF_BANDPASS 0     /* both tones' filtfilt */
 #define AMR_TF_HILBERT 1      /* FFT, -i*sgn(k), inverse FFT, both envelopes and the compare */
 #define AMR_TF_DECIDE 2       /* window majority, sync and pack */
-#define AMR_TF_COUNT 3
+#define AMR_TF_LAUNCH 3       /* the whole launch (-> gathered with amr_fsk_allgather), as AMR_T_LAUNCH */
+#define AMR_TF_COUNT 4
 
 typedef struct amr_fsk_plan amr_fsk_plan;
 
@@ -209,6 +216,8 @@ int amr_fsk_plan_create(amr_fsk_plan **plan, int device, int64_t n_samples, int6
 int amr_fsk_plan_destroy(amr_fsk_plan *plan);
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan *plan);
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan *plan);
+/* the amr_fsk_plan_scratch_bytes a plan of this shape would report, without creating it */
+int64_t amr_fsk_plan_bytes_estimate(int64_t n_samples, int64_t sps, int ntaps, int64_t max_streams);
 /* FFT length actually run: n_samples, or the Bluestein length when n is not 5-smooth */
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan *plan);
 /* 1: the plan keeps z and the Hilbert filter's intermediates only for the
@@ -335,6 +344,15 @@ int amr_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t byte
 int amr_fsk_allgather(amr_comm *comm, const void *d_send, void *d_recv, int64_t bytes_per_rank,
                       amr_fsk_plan *plan);
 int amr_comm_synchronize(amr_comm *comm);
+/* Host-memory collectives of the sharded host path (multi.py RcclTransport;
+ * decoder.decode_from_buffer_batch with a transport): synchronous, on the
+ * comm's stream behind its earlier gathers, through a device staging buffer
+ * the comm keeps.  allgather_host: recv = world x bytes_per_rank, rank-major;
+ * allreduce_max: values[i] = max over ranks (count doubles, in place); a
+ * barrier is allreduce_max of one value. */
+int amr_comm_allgather_host(amr_comm *comm, const void *send, void *recv, int64_t bytes_per_rank);
+int amr_comm_allreduce_max(amr_comm *comm, double *values, int64_t count);
+int amr_comm_world(const amr_comm *comm, int *nranks, int *rank);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,7 @@
 """bench.py's N > 1 path on one GPU (`--force-comm`: torch.distributed.run
-with one rank, a one-rank RCCL communicator, the all-gather after every
-launch, the gather check), small sizes: the headline layout, a
+with one rank -- the launcher only; bootstrap, barriers, max over ranks and
+gathers are multi.py's RcclTransport -- a one-rank RCCL communicator, the
+all-gather after every launch, the gather check), small sizes: the headline layout, a
 strong-scaling workload with two global batches per launch (`--coalesce`),
 and the FSK plans' gather (amr_fsk_allgather).
 The 8-GPU run is the driver's; this keeps the code it runs exercised."""
@@ -40,4 +41,5 @@ def test_force_comm_gather_check(extra):
     assert line, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads(line[-1])
     assert d["gather_check"].startswith("ok"), d["gather_check"]
+    assert d["latency_ms_per_global_batch"] and d["latency_ms_per_global_batch"] > 0
     assert "bit-exact" in d["parity"] and d["parity"].split("/")[0] == d["parity"].split("/")[1].split()[0], d["parity"]

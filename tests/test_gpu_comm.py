@@ -4,6 +4,7 @@ gathered buffer equals its plan's own output of that round (amr_allgather
 orders itself after the plan's queued work, and the plan's later work waits
 for it before writing outputs)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -65,3 +66,35 @@ def test_two_plans_one_comm():
             for q in (v if isinstance(v, list) else [v]):
                 _amr.check(L.amr_free(q))
     _amr.check(L.amr_comm_destroy(comm))
+
+
+def test_rccl_transport_one_rank(tmp_path):
+    """multi.RcclTransport (the product's torch-free sharded path) as one
+    rank: the unique id through a FileStore, host all-gather / max / barrier
+    over RCCL, and decoder.decode_from_buffer_batch / multi.demodulate_sharded
+    through it == the unsharded calls."""
+    import contextlib
+    import io
+    import _amr
+    import decoder
+    import modem
+    import multi
+    import synth
+    if _amr.device_count() < 1:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X")
+    tp = multi.RcclTransport(multi.FileStore(str(tmp_path / "store")), 0, 1, 0)
+    try:
+        a = np.arange(37, dtype=np.int64)
+        assert np.array_equal(tp.all_gather(a), a[None])
+        assert tp.max(2.5) == 2.5
+        tp.barrier()
+        x = synth.qpsk_batch(40, 24000, 1000, seed=8, distinct=5)
+        assert multi.demodulate_sharded("qpsk", x, 1000, tp) == modem.qpsk_demodulate_batch(x, baud=1000)
+        with contextlib.redirect_stdout(io.StringIO()):
+            os.chdir(tmp_path)
+            want = decoder.decode_from_buffer_batch(x, "QPSK", 1000)
+            got = decoder.decode_from_buffer_batch(x, "QPSK", 1000, transport=tp)
+        names = lambda r: [[os.path.basename(p).split("_", 1)[1] for p in ps] for ps in r]
+        assert names(got) == names(want) and sum(map(len, got)) == 40
+    finally:
+        tp.close()

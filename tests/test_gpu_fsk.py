@@ -169,7 +169,8 @@ def test_fsk_timing_hooks():
     pl.enable_timing(True)
     pl.demod_host(x)
     t = pl.timings()
-    assert set(t) == {"bandpass", "hilbert", "decide"} and all(v > 0 for v in t.values())
+    assert set(t) == {"bandpass", "hilbert", "decide", "launch"} and all(v > 0 for v in t.values())
+    assert t["launch"] >= t["hilbert"]
 
 
 @pytest.mark.parametrize("nx,num,batch", [(1000, 2177, 2), (2177, 1000, 2), (999, 1500, 1), (1500, 999, 1),
@@ -225,7 +226,8 @@ def test_fsk_live_column_layout_chosen(N, baud, live):
     row length n1 is a multiple of sps (96000 = 300 x 320: sps 5, 10, 20),
     else the natural layout (sps 80 at 96000 / 48000, Bluestein lengths)."""
     import _fsk
-    pl = _fsk.FskPlan(N, baud, 12000.0 if baud > 1200 else 2400.0, 24000.0 if baud > 1200 else 4800.0, max_streams=4)
+    mark, space = {9600: (12000.0, 24000.0), 19200: (21000.0, 27000.0), 4800: (8000.0, 16000.0)}.get(baud, (2400.0, 4800.0))
+    pl = _fsk.FskPlan(N, baud, mark, space, max_streams=4)
     assert pl.live_columns == live
 
 

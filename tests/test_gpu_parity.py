@@ -497,11 +497,12 @@ def test_async_host_entry_stream_of_batches():
 
 @pytest.mark.parametrize("layout", ["row", "lane"])
 def test_batch_of_flagged_streams(layout):
-    """Every stream of a 1030-stream batch holds exact zeros (a gated capture:
-    digital silence before the burst and a dropout inside it), so the low-pass
-    detector flags all of them and the whole batch takes K3x, the exact
-    complex low-pass -- checkpointed, one workgroup per 64-stream group.
-    Bytes and sync == the oracle, in both layouts."""
+    """Every stream of a 1030-stream batch is a gated capture -- a burst, then
+    >= 66 000 samples of digital silence, over which the filters decay to
+    exact zeros and denormals -- or all silence, so the low-pass detector
+    flags all of them and the whole batch takes K3x, the exact complex
+    low-pass (checkpointed, one workgroup per 64-stream group).  Bytes and
+    sync == the oracle, in both layouts."""
     import time
     import _amr
     import synth
@@ -510,9 +511,7 @@ def test_batch_of_flagged_streams(layout):
     x = synth.qpsk_batch(B, N, 9600, seed=99, distinct=6)
     rng = np.random.default_rng(99)
     for i in range(B):
-        x[i, :int(rng.integers(1, 3000))] = 0.0
-        d0 = int(rng.integers(20000, 90000))
-        x[i, d0:d0 + int(rng.integers(1, 400))] = 0.0
+        x[i, 0 if i % 8 == 0 else int(rng.integers(8000, 30000)):] = 0.0
     plan = _amr.PskPlan("qpsk", N, 9600, max_streams=B)
     if layout == "lane":
         plan.set_inflight(16)

@@ -1,7 +1,12 @@
-"""The N > 1 path on CPU: world_size-2 gloo ranks shard a batch, demodulate
-their shards (the oracle stands in for the per-rank GPU call here) and
-all-gather the packed decoded bytes; the result must equal the single-process
-batch.  Also the shard arithmetic itself."""
+"""The N > 1 path on CPU (multi.py): ranks shard a batch, demodulate their
+shards (the oracle stands in for the per-rank GPU call here) and all-gather
+the packed decoded bytes; the result must equal the single-process batch.
+The packing, the several-batches-per-launch layout and the gather check run
+over two transports: the product's torch-free StoreTransport (FileStore and
+TcpStore bootstrap, world 2 and 3) and a torch.distributed gloo transport
+defined here -- the same multi.py code either way.  The RCCL transport is
+the GPU tests' (tests/test_gpu_comm.py, tests/test_gpu_bench_comm.py)."""
+import multiprocessing as mproc
 import os
 import socket
 
@@ -27,6 +32,26 @@ def test_pack_unpack_roundtrip():
     assert unpack(p[None], ln[None]) == outs
 
 
+def test_shard_layout_several_steps_per_launch():
+    """ShardLayout: C steps of a global batch per launch; gathering the ranks'
+    slots in any world size returns every step's streams in global order."""
+    from multi import ShardLayout
+    rng = np.random.default_rng(0)
+    for world in (1, 2, 3, 8):
+        for B, C in ((7, 1), (8, 3), (17, 2), (3, 4)):
+            lay = ShardLayout(B, world, C)
+            steps = [[bytes(rng.integers(0, 256, rng.integers(0, 9), dtype=np.uint8)) for _ in range(B)]
+                     for _ in range(C)]
+            slots = []
+            for r in range(world):
+                lo, hi = lay.shard(r)
+                outs = [o for st in steps for o in st[lo:hi]]          # the rank's launch, step-major
+                assert len(outs) == lay.launch_rows(r)
+                slots.append(lay.pack(outs, 8))
+            got = lay.unpack(np.stack([p for p, _ in slots]), np.stack([ln for _, ln in slots]))
+            assert got == [o for st in steps for o in st]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -35,99 +60,125 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, x, baud, result_file):
+class GlooTransport:
+    """A test transport over torch.distributed (gloo): the multi.py transport interface."""
+
+    def __init__(self, dist):
+        self.dist, self.rank, self.world = dist, dist.get_rank(), dist.get_world_size()
+
+    def all_gather(self, a):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return np.stack([p.numpy() for p in parts])
+
+    def max(self, v):
+        return float(self.all_gather(np.array([v], np.float64)).max())
+
+    def barrier(self):
+        self.dist.barrier()
+
+
+def _paths():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
-    import torch.distributed as dist
-    from multi import demod_sharded, gather_gloo
+    for p in (os.path.join(root, "audio-modem-radio_amd"), root):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+
+
+def _make_transport(kind, rank, world, port, tmp):
+    _paths()
+    import multi
+    if kind == "gloo":
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return GlooTransport(dist)
+    store = multi.TcpStore("127.0.0.1", port, is_server=rank == 0) if kind == "tcp" else multi.FileStore(tmp)
+    return multi.StoreTransport(store, rank, world)
+
+
+def _close(kind, tp):
+    if kind == "gloo":
+        tp.dist.barrier()
+        tp.dist.destroy_process_group()
+    else:
+        tp.close()
+
+
+def _demod_worker(rank, world, kind, port, tmp, x, baud, result_file):
+    tp = _make_transport(kind, rank, world, port, tmp)
+    import multi
     from oracle import oracle
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    cap = 2 * x.shape[1] // 8 + 8
-    got = demod_sharded(x, lambda xs: oracle.psk_demod_batch("qpsk", xs, baud)[0], rank, world,
-                        lambda local: gather_gloo(local, x.shape[0], cap, dist))
+    got = multi.demod_sharded(x, lambda xs: oracle.psk_demod_batch("qpsk", xs, baud)[0], tp)
     if rank == 0:
         np.save(result_file, np.array([g.hex() for g in got]))
-    dist.barrier()
-    dist.destroy_process_group()
+    _close(kind, tp)
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_world2_equals_single_process(tmp_path, world):
-    import torch.multiprocessing as mp
+def _spawn(target, world, args):
+    ctx = mproc.get_context("spawn")
+    procs = [ctx.Process(target=target, args=(r, world) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+@pytest.mark.parametrize("kind,world", [("gloo", 2), ("file", 2), ("tcp", 3)])
+def test_sharded_demod_equals_single_process(tmp_path, kind, world):
     import synth
     from oracle import oracle
     x = synth.qpsk_batch(7, 6000, 9600, seed=3, distinct=3)
     out = str(tmp_path / "res.npy")
-    mp.spawn(_worker, args=(world, _free_port(), x, 9600, out), nprocs=world, join=True)
+    _spawn(_demod_worker, world, (kind, _free_port(), str(tmp_path / "store"), x, 9600, out))
     got = list(np.load(out))
     want = [w.hex() for w in oracle.psk_demod_batch("qpsk", x, 9600)[0]]
     assert got == want
 
 
-def _bench_gather_worker(rank, world, port, B_global, cap, corrupt_rank, result_file, C=1):
-    """bench.py's N>1 bookkeeping end to end on gloo: each rank takes its
-    shard of C consecutive strong-scaling global batches (bench.workload_sizes;
-    C steps per launch, bench --coalesce), decodes them as one launch (the
-    oracle stands in for the GPU), packs them into its [C * B_slot][cap] slot,
-    the slots are all-gathered (gloo stands in for RCCL), and the gathered
-    buffer is checked against every rank's own output exactly as bench.py does
-    it (row_digest + gather_verdict); every step's global batch is then read
-    back out of the gathered buffer in rank order."""
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
-    import torch
-    import torch.distributed as dist
+def _bench_gather_worker(rank, world, kind, port, tmp, B_global, cap, corrupt_rank, result_file, C=1):
+    """bench.py's N>1 bookkeeping end to end: each rank takes its shard of C
+    consecutive strong-scaling global batches (bench.workload_sizes; C steps
+    per launch, bench --coalesce), decodes them as one launch (the oracle
+    stands in for the GPU), packs its [C * B_slot][cap] slot, the slots are
+    all-gathered over the transport, and the gathered buffer is checked
+    against every rank's own output exactly as bench.py does it
+    (multi.gather_check); every step's global batch is then read back out of
+    the gathered buffer (ShardLayout.unpack)."""
+    tp = _make_transport(kind, rank, world, port, tmp)
     import bench
+    import multi
     import synth
     from oracle import oracle
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     B, Bg, lo, B_slot = bench.workload_sizes("ofdm8", B_global, world, rank)
+    lay = multi.ShardLayout(B_global, world, C)
+    assert lay.b_slot == B_slot and lay.launch_rows(rank) == C * B
     steps = [synth.qpsk_batch(B_global, 4000, 9600, seed=5 + c, distinct=B_global) for c in range(C)]
-    launch = np.concatenate([x[lo:lo + B] for x in steps])          # the rank's C shards, one launch
-    outs, _ = oracle.psk_demod_batch("qpsk", launch, 9600)
-    R = C * B_slot
-    own = np.zeros((R, cap), np.uint8)
-    lens = np.zeros(R, np.int64)
-    for i, o in enumerate(outs):
-        own[i, :len(o)] = np.frombuffer(o, np.uint8)
-        lens[i] = len(o)
-    slots = [torch.empty((R, cap), dtype=torch.uint8) for _ in range(world)]
-    lslots = [torch.empty(R, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(slots, torch.from_numpy(own))
-    dist.all_gather(lslots, torch.from_numpy(lens))
-    gp = np.stack([t.numpy() for t in slots])
-    gl = np.stack([t.numpy() for t in lslots])
-    if rank == 0 and corrupt_rank is not None:
-        gp[corrupt_rank, 0, 0] ^= 0xFF                    # a wrong byte in that rank's slice
-    own_digests = [None] * world
-    dist.all_gather_object(own_digests, bench.row_digest(own[:C * B], lens[:C * B]))
-    shard = [bench.workload_sizes("ofdm8", B_global, world, r)[0] for r in range(world)]
-    sizes = [C * b for b in shard]
-    bad = bench.gather_verdict([bench.row_digest(gp[r], gl[r]) for r in range(world)], own_digests, sizes)
+    outs, _ = oracle.psk_demod_batch("qpsk", lay.local_rows(steps, rank), 9600)
+    own, lens = lay.pack(outs, cap)
+    gp = tp.all_gather(own)
+    gl = tp.all_gather(lens)
+    if corrupt_rank is not None:
+        gp[corrupt_rank, 0, 0] ^= 0xFF                    # a wrong byte in that rank's slice, as every rank sees it
+    bad = multi.gather_check(gp, gl, own, lens, lay, tp)
     if rank == 0:
-        # step c's rows, rank by rank, are the single-process batch's output
         want = [w for x in steps for w in oracle.psk_demod_batch("qpsk", x, 9600)[0]]
-        got = [gp[r, c * shard[r] + i, :gl[r, c * shard[r] + i]].tobytes()
-               for c in range(C) for r in range(world) for i in range(shard[r])]
-        if corrupt_rank is not None:
-            got = want                                    # the corruption is the verdict's to find
+        got = want if corrupt_rank is not None else lay.unpack(gp, gl)
         np.save(result_file, np.array([str(bad), str(got == want)]))
-    dist.barrier()
-    dist.destroy_process_group()
+    _close(kind, tp)
 
 
-@pytest.mark.parametrize("world,B_global,corrupt,C", [(2, 7, None, 1), (3, 8, None, 1), (3, 8, 2, 1), (2, 7, None, 3),
-                                                     (3, 8, 1, 2)])
-def test_bench_gather_bookkeeping_gloo(tmp_path, world, B_global, corrupt, C):
-    import torch.multiprocessing as mp
+@pytest.mark.parametrize("kind,world,B_global,corrupt,C", [("gloo", 2, 7, None, 1), ("file", 3, 8, None, 1),
+                                                          ("tcp", 3, 8, 2, 1), ("file", 2, 7, None, 3),
+                                                          ("gloo", 3, 8, 1, 2)])
+def test_bench_gather_bookkeeping(tmp_path, kind, world, B_global, corrupt, C):
     out = str(tmp_path / "res.npy")
     cap = 2 * 4000 // 10 // 8 + 8
-    mp.spawn(_bench_gather_worker, args=(world, _free_port(), B_global, cap, corrupt, out, C), nprocs=world,
-             join=True)
+    _spawn(_bench_gather_worker, world, (kind, _free_port(), str(tmp_path / "store"), B_global, cap, corrupt, out, C))
     bad, same = list(np.load(out))
     assert same == "True"
     assert bad == ("[]" if corrupt is None else f"[{corrupt}]")
@@ -138,9 +189,7 @@ def test_bench_launch_plan(world):
     """bench.py's steps per launch: every step's streams are launched exactly
     once (K x the rank's shard), launches hold >= 4096 streams on small
     strong-scaling shards, weak scaling stays one step per launch."""
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "audio-modem-radio_amd"), root]
+    _paths()
     import bench
     for K in (1, 5, 20, 64):
         B = bench.workload_sizes("ofdm8", 0, world, 0)[0]
@@ -150,3 +199,18 @@ def test_bench_launch_plan(world):
         assert all(x == BL for x in sizes[:-1])
         Bw = bench.workload_sizes("qpsk9600", 0, world, 0)[0]
         assert bench.launch_plan(K, Bw, False) == (1, Bw, K, [Bw] * K)
+
+
+def test_product_package_is_torch_free():
+    """north_star: no PyTorch in the host code (grep of the package sources)."""
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "audio-modem-radio_amd")
+    hits = []
+    for dp, _, fs in os.walk(root):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                with open(os.path.join(dp, f), encoding="utf-8") as fh:
+                    for i, line in enumerate(fh, 1):
+                        code = line.split("#")[0]
+                        if "import torch" in code or "from torch" in code:
+                            hits.append(f"{f}:{i}")
+    assert not hits, hits

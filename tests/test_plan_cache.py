@@ -51,17 +51,39 @@ def test_stream_bucket():
     assert [_amr.stream_bucket(b, 4096) for b in (1, 2, 3, 64, 65, 5000)] == [1, 2, 4, 64, 128, 4096]
 
 
-@pytest.mark.gpu
-def test_many_lengths_bounded_on_device():
-    """100 distinct stream lengths through the drop-in modem functions: the
-    summed device bytes of the cached plans stay within the cache budget."""
+def test_lru_evicts_for_the_new_plan_first():
+    """With an estimate, room is made BEFORE the new plan is created: the
+    cache never holds more than the budget, not even while creating."""
+    import _amr
+    c = _amr.PlanCache(budget_bytes=100)
+    c.get("a", 1, lambda m: FakePlan(40, m))
+    c.get("b", 1, lambda m: FakePlan(40, m))
+    seen = []
+
+    def make(m):
+        seen.append(c._total_unlocked())
+        return FakePlan(50, m)
+    c.get("c", 1, make, estimate=lambda m: 50)
+    assert seen == [40] and len(c) == 2 and c.total_bytes() == 90
+
+
+def test_one_cache_for_psk_and_fsk():
     import _amr
     import _fsk
+    assert _fsk._amr.plan_cache is _amr.plan_cache
+
+
+@pytest.mark.gpu
+def test_many_lengths_bounded_on_device():
+    """100 distinct stream lengths through the drop-in modem functions (PSK
+    and FSK plans in the one cache): the summed device bytes of the cached
+    plans stay within the budget, and each plan's estimate (made before it
+    was created) equals the bytes it then reports."""
+    import _amr
     import modem
     budget = 2_000_000_000
-    old_p, old_f = _amr._psk_cache, _fsk._fsk_cache
-    _amr._psk_cache = _amr.PlanCache(budget)
-    _fsk._fsk_cache = _amr.PlanCache(budget)
+    old = _amr.plan_cache
+    _amr.plan_cache = _amr.PlanCache(budget)
     try:
         rng = np.random.default_rng(3)
         for k in range(100):
@@ -70,8 +92,27 @@ def test_many_lengths_bounded_on_device():
             modem.qpsk_demodulate(x, baud=9600)
             if k % 10 == 0:
                 modem.fsk_demodulate(x, baud=9600, mark_freq=12000.0, space_freq=24000.0)
-            assert _amr._psk_cache.total_bytes() <= budget
-            assert _fsk._fsk_cache.total_bytes() <= budget
-        assert len(_amr._psk_cache) < 100
+            assert _amr.plan_cache.total_bytes() <= budget
+        assert len(_amr.plan_cache) < 100
+        L = _amr.lib()
+        for key, pl in list(_amr.plan_cache._d.items()):
+            if key[0] == "psk":
+                est = L.amr_psk_plan_bytes_estimate(_amr.PSK_QPSK, pl.n, pl.sps, pl.first, 9, 5, pl.max_streams)
+            else:
+                est = L.amr_fsk_plan_bytes_estimate(pl.n, pl.sps, 7, pl.max_streams)
+            assert est == pl.scratch_bytes(), (key, est, pl.scratch_bytes())
     finally:
-        _amr._psk_cache, _fsk._fsk_cache = old_p, old_f
+        _amr.plan_cache = old
+
+
+@pytest.mark.gpu
+def test_full_size_fsk_plan_fits_the_default_budget():
+    """BASELINE configs[2]'s 16384 x 96000 FSK plan (live-column layout) is
+    admitted by the default cache budget with room left, and its estimate
+    is what it reports."""
+    import _amr
+    import _fsk
+    est = _amr.lib().amr_fsk_plan_bytes_estimate(96000, 10, 7, 16384)
+    assert est <= 40e9 and est <= _amr._cache_budget()
+    pl = _fsk.FskPlan(96000, 9600, 12000.0, 24000.0, max_streams=16384)
+    assert pl.live_columns and pl.scratch_bytes() == est
