@@ -598,7 +598,9 @@ int amr_psk_plan_timings(amr_psk_plan* plan, float* ms, int count) {
   HIP_TRY(hipStreamSynchronize(plan->stream));
   for (int i = 0; i < count && i < AMR_T_COUNT; ++i) {
     ms[i] = -1.0f;
-    if (plan->timing && plan->ev_used[i]) HIP_TRY(hipEventElapsedTime(&ms[i], plan->ev[i][0], plan->ev[i][1]));
+    if (!plan->timing || !plan->ev_used[i]) continue;
+    HIP_TRY(hipEventSynchronize(plan->ev[i][1]));   // the launch slot may end on a comm stream (a gather)
+    HIP_TRY(hipEventElapsedTime(&ms[i], plan->ev[i][0], plan->ev[i][1]));
   }
   return AMR_OK;
 }

@@ -317,9 +317,16 @@ __global__ __launch_bounds__(256) void k_bp_fwd(PskBuffers buf, PskParams p, Iir
 // before its first barrier (2-wave, 108-VGPR workgroups: they find room
 // beside the resident band-pass / low-pass waves, where the one-wave kernel's
 // 168-VGPR four-wave workgroups waited up to 15 ms at 8192 streams).
-template <typename T, int GPB, bool ZO, bool FIXUP = false, bool PRE = false>
+// CK = 2 (AMR_BP_CK=2): a checkpoint every 2 tiles (64 samples: half the
+// checkpoint bytes) while the LDS hand-off stays at one 32-sample tile, so
+// the workgroup keeps its 64 KiB and two fit a CU.  The re-run role then
+// reaches the second tile of a pair by first re-running the pair's first
+// tile without outputs (1.5x its steps), holding the pair's inputs in
+// registers (one more tile of them) -- bit for bit the same outputs.
+template <typename T, int GPB, bool ZO, bool FIXUP = false, bool PRE = false, int CK = 1>
 __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
   static_assert(!(FIXUP && PRE), "the fix-up pass runs its own forward pass");
+  static_assert(CK == 1 || (CK == 2 && !PRE), "64-sample checkpoints: the kernel's own forward pass");
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);
   constexpr int NL = TB / PER;
@@ -376,8 +383,10 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
     v4u xr[NL];
     if (nt > 0) load_tile(0, xr);
     for (int64_t t = 0; t < nt; ++t) {
+      if (t % CK == 0) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ck[(t * 8 + j) * 64] = z[j];
+        for (int j = 0; j < 8; ++j) ck[((t / CK) * 8 + j) * 64] = z[j];
+      }
       v4u cur[NL];
 #pragma unroll
       for (int k = 0; k < NL; ++k) cur[k] = xr[k];
@@ -393,7 +402,63 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
   }
   __syncthreads();
 
-  if (role == 0) {
+  if (role == 0 && CK == 2) {
+    // ---- re-run tiles nt-1 ... 0 into LDS, checkpoints every 2 tiles -------
+    // pair c = tiles (2c, 2c+1) from checkpoint c; tile 2c+1 re-runs tile 2c
+    // first (no outputs).  Registers: the pair's inputs (xa, xb), the next
+    // pair's arriving one tile ahead (xbn at the odd tile, xan at the even).
+    v4u xa[NL], xb[NL], xan[NL], xbn[NL];
+    double cc[8], ccn[8];
+    if (active && nt > 0) {
+      const int64_t c = (nt - 1) >> 1;
+      load_tile(2 * c, xa);
+      if (2 * c + 1 < nt) load_tile(2 * c + 1, xb);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cc[j] = ck[(c * 8 + j) * 64];
+    }
+    for (int64_t it = 0; it <= nt; ++it) {
+      const int64_t t = nt - 1 - it;
+      if (active && t >= 0) {
+        const int64_t c = t >> 1, cp = c > 0 ? c - 1 : 0;
+        double zf[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) zf[j] = cc[j];
+        double2 (*ybuf)[64] = yb[gi][it & 1];
+        float dummy = 0.0f;                     // the re-run repeats checked steps: no detector
+        if (t & 1) {
+          load_tile(2 * cp + 1, xbn);           // the next pair's second tile and checkpoint
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ccn[j] = ck[(cp * 8 + j) * 64];
+#pragma unroll
+          for (int k = 0; k < TB; ++k) (void)bp_step<ZO>(zf, f, tile_x(xa, k), dummy);
+#pragma unroll
+          for (int k = 0; k < TB; k += 2) {
+            const double y0 = bp_step<ZO>(zf, f, tile_x(xb, k), dummy);
+            const double y1 = bp_step<ZO>(zf, f, tile_x(xb, k + 1), dummy);
+            ybuf[k >> 1][lane] = make_double2(y0, y1);
+          }
+        } else {
+          if (2 * c + 1 >= nt) {                // a top pair of one tile: nothing was prefetched for the next
+            load_tile(2 * cp + 1, xbn);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ccn[j] = ck[(cp * 8 + j) * 64];
+          }
+          load_tile(2 * cp, xan);
+#pragma unroll
+          for (int k = 0; k < TB; k += 2) {
+            const double y0 = bp_step<ZO>(zf, f, tile_x(xa, k), dummy);
+            const double y1 = bp_step<ZO>(zf, f, tile_x(xa, k + 1), dummy);
+            ybuf[k >> 1][lane] = make_double2(y0, y1);
+          }
+#pragma unroll
+          for (int k = 0; k < NL; ++k) { xa[k] = xan[k]; xb[k] = xbn[k]; }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cc[j] = ccn[j];
+        }
+      }
+      __syncthreads();
+    }
+  } else if (role == 0) {
     // ---- re-run tiles nt-1, nt-2, ... 0 forward into LDS --------------------
     v4u xr[NL];
     double cn[8];
@@ -1028,6 +1093,12 @@ static int bp_prefwd() {
   return v;
 }
 
+static int bp_ck() {
+  // band-pass checkpoint every AMR_BP_CK tiles (1 or 2; the LDS hand-off stays one tile)
+  static const int v = [] { const char* e = getenv("AMR_BP_CK"); return e && e[0] == '2' ? 2 : 1; }();
+  return v;
+}
+
 static int bp_zero_taps(const PskParams& p) {
   // skip the band-pass's +0.0 odd taps (detector + exact re-run of flagged
   // groups): AMR_BP_ZO=0 computes every tap instead
@@ -1054,6 +1125,9 @@ static hipError_t launch_bp(const PskBuffers& b, const PskParams& p, const Iir& 
         hipLaunchKernelGGL((k_bp_fwd<T, false>), fgrid, dim3(256), 0, st, b, p, f);
         hipLaunchKernelGGL((k_bp_lane2<T, 2, false, false, true>), grid, block, 0, st, b, p, f);
       }
+    } else if (lane_wpb() >= 2 && bp_ck() == 2) {
+      if (zo) hipLaunchKernelGGL((k_bp_lane2<T, 2, true, false, false, 2>), grid, block, 0, st, b, p, f);
+      else hipLaunchKernelGGL((k_bp_lane2<T, 2, false, false, false, 2>), grid, block, 0, st, b, p, f);
     } else if (lane_wpb() >= 2) {
       if (zo) hipLaunchKernelGGL((k_bp_lane2<T, 2, true>), grid, block, 0, st, b, p, f);
       else hipLaunchKernelGGL((k_bp_lane2<T, 2, false>), grid, block, 0, st, b, p, f);

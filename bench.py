@@ -356,9 +356,9 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
         gl = np.empty((world, R), np.int64)
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gp), ctx[last]["gather"], gp.nbytes))
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gl), ctx[last]["gather_len"], gl.nbytes))
-        layout = multi.ShardLayout(B_global, world, C)
-        assert layout.rows == R and layout.launch_rows(rank) == C * B
-        bad_any = multi.gather_check(gp, gl, o, ln, layout, tp)
+        shards = multi.ShardLayout(B_global, world, C)
+        assert shards.rows == R and shards.launch_rows(rank) == C * B
+        bad_any = multi.gather_check(gp, gl, o, ln, shards, tp)
         gather_check = (f"ok: every rank's gathered [{world}][{R}][{cap}] buffer == each rank's own bytes and "
                         "lengths" if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
 

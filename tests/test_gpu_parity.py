@@ -376,7 +376,7 @@ sys.exit(1 if bad else 0)
 
 
 @pytest.mark.parametrize("variant", ["default", "unfused", "lp_split", "bp_one_wave", "wpb1", "wpb2_no_zero_taps",
-                                     "bp_prefwd", "bp_prefwd_no_zero_taps"])
+                                     "bp_prefwd", "bp_prefwd_no_zero_taps", "bp_ck2", "bp_ck2_no_zero_taps"])
 def test_lane_layout_forced_on_every_case(tmp_path, variant):
     """The lane-per-stream kernels (psk_lane_kernels.hip: checkpointed
     band-pass and low-pass, picked when many streams are in flight) forced on
@@ -436,7 +436,7 @@ x[129, 12345] = np.nan
 x[100, 4000:4100] = 0.0
 x[101] = 0.0
 bad += check("qpsk", x, 9600, "bpzo")
-if {variant!r} == "default":
+if {variant!r} in ("default", "bp_ck2"):
     bad += check("qpsk", synth.qpsk_batch(4096, 96000, 9600, seed=4096, distinct=8), 9600, "b4096")
 print("BAD", bad[:20], len(bad))
 sys.exit(1 if bad else 0)
@@ -447,7 +447,8 @@ sys.exit(1 if bad else 0)
                 "bp_one_wave": {"AMR_BP_SPLIT": "0"}, "wpb1": {"AMR_LANE_WPB": "1"},
                 "wpb2_no_zero_taps": {"AMR_LANE_WPB": "2", "AMR_BP_ZO": "0"},
                 "bp_prefwd": {"AMR_BP_PREFWD": "1"},
-                "bp_prefwd_no_zero_taps": {"AMR_BP_PREFWD": "1", "AMR_BP_ZO": "0"}}[variant])
+                "bp_prefwd_no_zero_taps": {"AMR_BP_PREFWD": "1", "AMR_BP_ZO": "0"},
+                "bp_ck2": {"AMR_BP_CK": "2"}, "bp_ck2_no_zero_taps": {"AMR_BP_CK": "2", "AMR_BP_ZO": "0"}}[variant])
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
