@@ -58,7 +58,7 @@ import synth  # noqa: E402
 FS = 96000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MIXED_GBS = 5200.0         # measured streaming rate at 1:1..2:1 read:write (tools/hbm_mix_probe.hip, profiles/)
-PROFILE_ROUND = "r02"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
+PROFILE_ROUND = "r03"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
 
 # BASELINE.json configs[1..4], 0-based (configs[0] is the reference's CPU plumbing case)
@@ -95,6 +95,32 @@ def dist_setup(force=False):
         import multi
         return multi.RcclTransport(multi.store_from_env(rank, world), rank, world, local), world, rank, local
     return None, 1, 0, local
+
+
+def host_cores():
+    """(threads for the CPU baseline, how they were counted): every CPU in
+    this process's affinity mask, capped by its cgroup CPU quota when one is
+    set (the GPU box's share of a many-core host: threads beyond the quota
+    only time-slice, e.g. 256 threads on a 16-CPU quota ran the oracle at
+    28 Msym/s against 72 for 16)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), open(
+                            "/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()])):
+        try:
+            with open(path) as f:
+                q, per = parse(f.read())[:2]
+            if q not in ("max", "-1") and int(per) > 0:
+                quota = -(-int(q) // int(per))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    n = min(aff, quota) if quota else aff
+    how = (f"{n} threads: the {aff} CPUs of os.sched_getaffinity(0)"
+           + (f", capped by the cgroup CPU quota of {quota} CPUs" if quota and quota < aff else "")
+           + f" (os.cpu_count() {os.cpu_count()}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', 'unset')})")
+    return max(1, n), how
 
 
 def barrier(tp):
@@ -368,9 +394,29 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
     if rank == 0:
         from oracle import oracle
         # the CPU baseline runs on every core this process may use (its
-        # affinity mask: the GPU box's host cores as the scheduler grants them)
-        threads = max(1, len(os.sched_getaffinity(0)))
+        # affinity mask, within its cgroup CPU quota: the GPU box's host cores
+        # as the scheduler grants them)
+        threads, cores_how = host_cores()
         xh = np.empty((BL, N), np.float32)
+        if headline and not fsk and not args.no_cpu:
+            # how many threads these host cores run fastest at: the affinity /
+            # quota count, or the box's OMP_NUM_THREADS share -- when the
+            # scheduler grants fewer CPUs than the mask shows, threads beyond
+            # them only time-slice.  The baseline then uses the fastest.
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[0]["x"], xh.nbytes))
+            cands = sorted({threads, *([int(os.environ["OMP_NUM_THREADS"])] if os.environ.get(
+                "OMP_NUM_THREADS", "").isdigit() else [])} - {0})
+            probe = {}
+            for nt_ in cands:
+                xs_ = xh[:min(B, 1024)]
+                t1 = time.perf_counter()
+                oracle.psk_demod_batch("qpsk", xs_, baud, n_threads=nt_)
+                probe[nt_] = round(len(xs_) * sym_per_stream / (time.perf_counter() - t1) / 1e6, 2)
+            if len(probe) > 1:
+                best = max(probe, key=probe.get)
+                cores_how += (f"; probed {', '.join(f'{k} threads {v} Msym/s' for k, v in probe.items())} on "
+                              f"{min(B, 1024)} streams: {best} used")
+                threads = best
         checked, n_slots, bad_total = 0, 0, []
         cpu = None
         slots = [] if args.no_cpu else range(P) if args.parity_all_slots else sorted({0, 1 % P, P - 1})
@@ -406,9 +452,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                        (" + oracle.fec_decode" if fec_fused else ""))
                 cpu = {"value": round(reps * len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s",
                        "cores": threads, "kind": "port",
-                       "cores_note": f"OpenMP threads = len(os.sched_getaffinity(0)) on this host "
-                                     f"(os.cpu_count() {os.cpu_count()}, OMP_NUM_THREADS "
-                                     f"{os.environ.get('OMP_NUM_THREADS', 'unset')})",
+                       "cores_note": cores_how,
                        "sample": f"{len(idx)} of the {BL} streams of benchmark batch 0 ({N} samples each)"
                                  + (f", {reps} passes" if reps > 1 else "") + f" through {how}, {cdt:.2f} s wall"}
             o, ln = outs[k]
@@ -490,7 +534,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                          "measured_stream_gbs": HBM_MIXED_GBS,
                          "measured_stream_source": "tools/hbm_mix_probe.hip on one MI355X: a streaming kernel's rate "
                                                    "at 1:1 and 2:1 read:write, 8 accesses per lane in flight "
-                                                   f"(profiles/{PROFILE_ROUND}_hbm_mix_probe.txt)"},
+                                                   "(profiles/r02_hbm_mix_probe.txt)"},
             "fp64_valu": {"ops_per_step": float(fp64), "achieved_tops": round(fp64 / ms_per_step / 1e9, 3),
                           "peak_tops": FP64_PEAK_TOPS, "frac": round(fp64 / ms_per_step / 1e9 / FP64_PEAK_TOPS, 4),
                           "note": "the binding roof of the bit-exact path (SURVEY §0.7): FP64 ops the reference's "

@@ -34,6 +34,7 @@ def find(d, pat):
 KERNELS = ["k_bp_lane2", "k_lp_lane2", "k_bp_lane", "k_lp_lane", "k_fsk_bandpass", "k_fsk_decide", "k_bandpass_row", "k_bandpass_g8", "k_bandpass_quad", "k_bandpass", "k_lowpass_fwd_q",
            "k_lowpass_bwd_q", "k_lowpass_fwd", "k_lowpass_bwd", "k_lowpass_exact", "k_slice",
            "k_sync_pack", "k_fec_decode",
+           "k_fft_cols_live", "k_fft_mid_live", "k_fft_rows_live",
            "k_fft_cols", "k_fft_mid", "k_fft_rows", "k_bs_pre", "k_bs_post"]
 # bench.py timing slot -> the kernels it brackets (one launch each per step)
 SLOTS = {
@@ -41,7 +42,8 @@ SLOTS = {
                  "lowpass_fwd": ["k_lp_lane2", "k_lp_lane", "k_lowpass_fwd_q", "k_lowpass_fwd"], "lowpass_bwd": ["k_lowpass_bwd_q", "k_lowpass_bwd"],
                  "lowpass_exact": ["k_lowpass_exact"], "sync_pack": ["k_slice", "k_sync_pack"], "fec": ["k_fec_decode"]},
     "ofdm8": None, "psk8fec": None,
-    "fsk9600": {"bandpass": ["k_fsk_bandpass"], "hilbert": ["k_fft_cols", "k_fft_mid", "k_fft_rows"],
+    "fsk9600": {"bandpass": ["k_fsk_bandpass"],
+                "hilbert": ["k_fft_cols_live", "k_fft_mid_live", "k_fft_rows_live", "k_fft_cols", "k_fft_mid", "k_fft_rows"],
                 "decide": ["k_fsk_decide", "k_sync_pack"]},
 }
 
