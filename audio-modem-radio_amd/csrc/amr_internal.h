@@ -82,6 +82,7 @@ struct LiveCols {
   int sps, w0, nw;        // live residues w0 .. w0 + nw - 1 (mod sps)
   int nl, nd;             // live / dead column counts
   float inv_n1, inv_sps, inv_nw, inv_ndp;   // reciprocals for lc_div (ndp = sps - nw)
+  int prune;              // the middle pass computes only the live outputs of its last stage
 };
 
 // floor(i / d) for 0 <= i < 2^20 given inv = 1/d rounded to float, d <= 625:

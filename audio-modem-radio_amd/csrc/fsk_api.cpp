@@ -550,6 +550,8 @@ LiveCols plan_live_cols(const FftShape& f, const FskParams& p) {
     seen[(size_t)o] = 1;
   }
   lc.on = 1;
+  static const bool no_prune = [] { const char* e = std::getenv("AMR_FFT_PRUNE"); return e && e[0] == '0'; }();
+  lc.prune = !no_prune;
   return lc;
 }
 
