@@ -610,221 +610,6 @@ __global__ __launch_bounds__(kFftThreads) __attribute__((amdgpu_waves_per_eu(TWG
       mlive, nmlive);
 }
 
-// ---- the live middle pass, pipelined (specialised radices, L = P*Q even) ----
-// k_fft_mid_live stalls on HBM: each workgroup loads its 8 rows, then runs
-// four dependent stages with block barriers, and three workgroups per CU do
-// not cover the load latency (SQ_WAIT_ANY 64 % of wave cycles, r3e).  Here a
-// persistent workgroup loops over tiles and gathers the NEXT tile's 8 x L
-// inputs from C / D straight into LDS by LDS-DMA (global_load_lds_dwordx4:
-// per-lane source through the position table, lane-linear destination) while
-// the current tile's stages run:
-//   tile i:  stage 1 of FFT 1 reads IN -> W;  barrier;  DMA tile i+1 -> IN;
-//            stage 2 (Hilbert mask, conj) -> W;  stage 1 of FFT 2 in W;
-//            wait for this wave's DMA;  barrier;  pruned stage 2 -> C
-// LDS per workgroup: IN [8][L] (rounded to whole 64-slot DMA instructions),
-// W [8][S], half the W_L table (W^(k + L/2) = -W^k), the position table:
-// 81.2 KB at L = 300, two workgroups per CU.  No vector-memory wait the
-// compiler places may fall inside a DMA's flight (it would wait for the DMA:
-// loads retire in order), so the tile's post-twiddles are loaded and consumed
-// before the DMA is issued, and the only other global accesses are stores.
-template <int P, int Q>
-__device__ __forceinline__ double2 tw_half(const double2* t, int k) {   // W_L^k, 0 <= k < L
-  constexpr int H = P * Q / 2;
-  const bool hi = k >= H;
-  const double2 w = t[hi ? k - H : k];
-  return hi ? make_double2(-w.x, -w.y) : w;
-}
-
-template <int R, int P, int Q>
-__device__ __forceinline__ void bfly_half(double2 (&v)[R], const double2* th, int tstride) {
-  constexpr int A = RadixF<R>::A, B = RadixF<R>::B;
-  if constexpr (B == 1) {
-    dftp<A>(v);
-  } else {
-#pragma unroll
-    for (int q2 = 0; q2 < B; ++q2) {
-      double2 a[A];
-#pragma unroll
-      for (int q1 = 0; q1 < A; ++q1) a[q1] = v[B * q1 + q2];
-      dftp<A>(a);
-#pragma unroll
-      for (int m1 = 0; m1 < A; ++m1)
-        v[B * m1 + q2] = q2 > 0 && m1 > 0 ? cmul(a[m1], tw_half<P, Q>(th, q2 * m1 * tstride)) : a[m1];
-    }
-#pragma unroll
-    for (int m1 = 0; m1 < A; ++m1) {
-      double2 c[B];
-#pragma unroll
-      for (int q2 = 0; q2 < B; ++q2) c[q2] = v[B * m1 + q2];
-      dftp<B>(c);
-#pragma unroll
-      for (int m2 = 0; m2 < B; ++m2) v[B * m1 + m2] = c[m2];
-    }
-  }
-}
-
-template <int P, int Q>
-__host__ __device__ constexpr int mid_in_slots() { return (kFftTile * P * Q + 63) / 64 * 64; }
-template <int P, int Q>
-__host__ __device__ constexpr int mid_pipe_slots(int n1) {   // dynamic LDS, double2 units
-  return mid_in_slots<P, Q>() + kFftTile * fft_row_stride(P, Q) + P * Q / 2 + (2 * n1 + 15) / 16 + (P + 4) / 4;
-}
-
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int P, int Q>
-__global__ __launch_bounds__(kFftThreads) void k_fft_mid_live_pipe(double2* zb, double2* cb, FftDesc d,
-                                                                  int64_t batch, LiveCols lc) {
-  extern __shared__ __attribute__((aligned(16))) double2 smem[];
-  constexpr int L = P * Q, S = fft_row_stride(P, Q), Qp = fft_block(Q);
-  constexpr int NIN = mid_in_slots<P, Q>();
-  double2* in = smem;                                   // [8][L] gathered inputs
-  double2* w = smem + NIN;                              // [8][S] work rows
-  double2* th = w + kFftTile * S;                       // W_L^k, k < L/2
-  int16_t* cpos = reinterpret_cast<int16_t*>(th + L / 2);
-  int* mlive = reinterpret_cast<int*>(cpos) + (2 * L + 15) / 16 * 4;   // count, then up to P values of m
-  const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
-  const int64_t total = batch * tiles;
-  const int64_t n = d.n;
-  const int n2 = d.n2, nl = lc.nl, nd = lc.nd;
-  const int idx = threadIdx.x, lane = idx & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(idx >> 6);
-  for (int k = idx; k < L / 2; k += kFftThreads) th[k] = d.c.tw[k];
-  for (int c = idx; c < L; c += kFftThreads) {
-    bool lv;
-    const int pos = lc_col_pos(lc, c, lv);
-    cpos[c] = (int16_t)(lv ? pos : ~pos);
-  }
-  __syncthreads();
-  if (idx == 0) {
-    const bool prune = lc.prune && P % lc.sps == 0;
-    int k = 0;
-    for (int m = 0; m < P; ++m)
-      if (!prune || cpos[m] >= 0) mlive[1 + k++] = m;
-    mlive[0] = k;
-  }
-  __syncthreads();
-  const int nm = mlive[0];
-  // gather tile `tile`'s inputs into IN: slot s = t * L + c holds element c of
-  // row k2 = r0 + t (from C when c is live, else D); slots past the rows take
-  // a dummy source (never read)
-  auto dma = [&](int64_t tile) {
-    const int64_t b = tile / tiles;
-    const int r0 = (int)(tile - b * tiles) * kFftTile;
-    const int nrow = min(kFftTile, n2 - r0);
-    const double2* crow = cb + (size_t)b * nl * n2 + (size_t)r0 * nl;
-    const double2* drow = zb + (size_t)b * n + (size_t)nl * n2 + (size_t)r0 * nd;
-    for (int k = wv; k < NIN / 64; k += kFftThreads / 64) {
-      const int s = k * 64 + lane;
-      const int t = s / L, c = s - t * L;
-      const double2* src = crow;
-      if (t < nrow) {
-        const int pos = cpos[c];
-        src = pos >= 0 ? crow + t * nl + pos : drow + t * nd + ~pos;
-      }
-      // LDS byte address of the instruction's 64 slots (wave-uniform)
-      const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(in + k * 64);
-      unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
-                   : "memory");
-    }
-  };
-  int64_t tile = blockIdx.x;
-  if (tile < total) dma(tile);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-  for (; tile < total; tile += gridDim.x) {
-    const int64_t b = tile / tiles;
-    const int r0 = (int)(tile - b * tiles) * kFftTile;
-    const int nrow = min(kFftTile, n2 - r0);
-    double2* crow = cb + (size_t)b * nl * n2 + (size_t)r0 * nl;
-    // post-twiddles of the last stage, W_n^(k2 (m + P p)) = base * step^p,
-    // loaded and consumed before this tile's DMA goes out
-    const int t2 = idx & (kFftTile - 1);
-    const bool on2 = idx < kFftTile * nm;
-    const int m2 = on2 ? mlive[1 + idx / kFftTile] : 0;
-    double2 base = twn(d, (unsigned)((r0 + t2) * m2));
-    double2 step = twn(d, (unsigned)((r0 + t2) * P));
-    // ---- FFT 1, stage 1: radix P over q, from IN
-    {
-      const int t = idx & (kFftTile - 1), j = idx / kFftTile;
-      if (idx < kFftTile * Q) {
-        double2 v[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) v[q] = in[t * L + j + Q * q];
-        bfly_half<P, P, Q>(v, th, Q);
-#pragma unroll
-        for (int i = 0; i < P; ++i) w[t * S + j + Qp * bfly_out<P>(i)] = v[i];
-      }
-    }
-    lds_barrier();                                       // IN is free, W holds Y
-    asm volatile("" : "+v"(base.x), "+v"(base.y), "+v"(step.x), "+v"(step.y));   // landed before the DMA
-    if (tile + gridDim.x < total) dma(tile + gridDim.x);
-    // ---- FFT 1, stage 2: twiddle, radix Q; Hilbert mask; conj; natural order back to W
-    {
-      const int t = idx & (kFftTile - 1), m = idx / kFftTile;
-      const bool on = idx < kFftTile * P;
-      double2 v[Q];
-      if (on) {
-#pragma unroll
-        for (int j = 0; j < Q; ++j) v[j] = w[t * S + j + Qp * m];
-#pragma unroll
-        for (int j = 1; j < Q; ++j) v[j] = cmul(v[j], tw_half<P, Q>(th, j * m));
-        bfly_half<Q, P, Q>(v, th, P);
-      }
-      lds_barrier();
-      if (on) {
-#pragma unroll
-        for (int p = 0; p < Q; ++p) {
-          const int c = m + P * p;
-          const unsigned k = (unsigned)(r0 + t + n2 * c);
-          const double2 x = hilbert_mul(v[bfly_slot<Q>(p)], k, n);
-          const int qq = c / Q;
-          w[t * S + (c - Q * qq) + Qp * qq] = conj2(x);
-        }
-      }
-    }
-    lds_barrier();
-    // ---- FFT 2, stage 1 (in place in W)
-    {
-      const int t = idx & (kFftTile - 1), j = idx / kFftTile;
-      if (idx < kFftTile * Q) {
-        double2 v[P];
-#pragma unroll
-        for (int q = 0; q < P; ++q) v[q] = w[t * S + j + Qp * q];
-        bfly_half<P, P, Q>(v, th, Q);
-#pragma unroll
-        for (int i = 0; i < P; ++i) w[t * S + j + Qp * bfly_out<P>(i)] = v[i];
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's DMA (and last tile's stores)
-    lds_barrier();                                       // every wave's: IN holds the next tile
-    // ---- FFT 2, stage 2, live m only: twiddle, radix Q, post-twiddle, live outputs -> C
-    if (on2) {
-      double2 v[Q];
-#pragma unroll
-      for (int j = 0; j < Q; ++j) v[j] = w[t2 * S + j + Qp * m2];
-#pragma unroll
-      for (int j = 1; j < Q; ++j) v[j] = cmul(v[j], tw_half<P, Q>(th, j * m2));
-      bfly_half<Q, P, Q>(v, th, P);
-#pragma unroll
-      for (int p = 0; p < Q; ++p) {
-        const double2 x = cmul(v[bfly_slot<Q>(p)], base);
-        base = cmul(base, step);
-        const int pos = cpos[m2 + P * p];
-        if (t2 < nrow && pos >= 0) crow[(unsigned)(t2 * nl + pos)] = x;
-      }
-    }
-    lds_barrier();                                       // W is free for the next tile
-  }
-}
-
 // final pass: live columns l0 .. l0+7 of C (length n2 each, stride nl) ->
 // DFT, conj, 1/n -> compare against z's live samples (L) -> bits, byte
 // (l0 / 8) * n2 + k1' (the decide kernel's live addressing)
@@ -1037,24 +822,8 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
   hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, batch, lc)
   AMR_FFT_PQ(d.a, COLSL);
 #undef COLSL
-  // AMR_FFT_MID_PIPE=1: the pipelined kernel; AMR_FFT_MID_TWG=1: the
-  // one-tile kernel with the W_L table in global memory (four workgroups per CU)
-  static const bool pipe = [] { const char* e = getenv("AMR_FFT_MID_PIPE"); return e && e[0] == '1'; }();
-  static const bool twg = [] { const char* e = getenv("AMR_FFT_MID_TWG"); return e && e[0] == '1'; }();
-  static const int cus = [] {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    return v;
-  }();
-  const int64_t mid_tiles = batch * ((d.n2 + kFftTile - 1) / kFftTile);
-  const unsigned gpipe = (unsigned)std::min<int64_t>(mid_tiles, 2 * (int64_t)cus);
-#define MIDP(P, Q)                                                                                               \
-  hipLaunchKernelGGL((k_fft_mid_live_pipe<P, Q>), dim3(gpipe), dim3(kFftThreads),                               \
-                     (size_t)(mid_pipe_slots<P, Q>(P * Q) * sizeof(double2)), st, zb, cb, d, batch, lc)
-  // (two workgroups of the pipelined kernel must fit a CU's 160 KB of LDS)
-  if (pipe && d.c.r1 == 20 && d.c.r2 == 15 && 2 * mid_pipe_slots<20, 15>(300) * 16 <= 160 * 1024) {
-    MIDP(20, 15);
-  } else {
+  // AMR_FFT_MID_TWG=0: the W_L table in LDS (three workgroups per CU instead of four)
+  static const bool twg = [] { const char* e = getenv("AMR_FFT_MID_TWG"); return !(e && e[0] == '0'); }();
   const size_t sm_mid = twg ? (size_t)kFftTile * d.c.S * sizeof(double2) : fft_smem_bytes(d.c);
 #define MIDL(P, Q)                                                                                              \
   do {                                                                                                          \
@@ -1066,9 +835,7 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
                          batch, lc);                                                                            \
   } while (0)
   AMR_FFT_PQ(d.c, MIDL);
-  }
 #undef MIDL
-#undef MIDP
 #define FINL(P, Q)                                                                                          \
   hipLaunchKernelGGL((k_fft_rows_live<P, Q>), dim3(gfin), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, \
                      batch, scale, epi, lc)
@@ -1209,9 +976,6 @@ static hipError_t fft_set_smem(int bytes) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
   }
-  if constexpr (P > 0 && (P * Q) % 2 == 0)
-    return hipFuncSetAttribute((const void*)k_fft_mid_live_pipe<P, Q>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               mid_pipe_slots<P, Q>(P * Q) * (int)sizeof(double2));
   return hipSuccess;
 }
 

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-template <typename T, bool ZO, bool LIVE>
+template <typename T, bool ZO, bool LIVE, bool W1S>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -362,7 +362,24 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     }
   }
   __syncthreads();                                     // the tail rows of yb are free again
+  // tile tz's 32 rows of z from yb buffer bb, after wave 1 has run it backward:
+  // RPS rows per 1-KiB store instruction, lane -> (row, sample)
+  auto store_tile = [&](int bb, int64_t tz) {
+    constexpr int RPS = 64 / TL;
+    const double (*buf)[YP] = &yb[bb * TL];
+    const int sub = lane / TL, k = lane % TL;
+    const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
+#pragma unroll 4
+    for (int row = 0; row < 32; row += RPS) {
+      const int rr = row + sub;
+      const int64_t so = w * 32 + rr;
+      const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
+      if (so < n_streams) z[(size_t)so * n + zo] = v;
+    }
+  };
   // ---- phase 2: wave 0 re-forwards tile T-1-i while wave 1 runs tile T-i backward
+  // (W1S: and stores it right away -- the stores ride on the wave with less
+  // arithmetic per tile; otherwise wave 0 stores it an iteration later)
   if (role == 0) {
     // tiles top-down; inputs and checkpoints two tiles ahead
     double c0[6], c1[6];
@@ -377,24 +394,9 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       fetch(r1, n_tiles - 2);
       ldck(c1, n_tiles - 2);
     }
-    // tile tz's 32 rows of z from yb buffer bb, after wave 1 has run it backward:
-    // RPS rows per 1-KiB store instruction, lane -> (row, sample)
-    auto store_tile = [&](int bb, int64_t tz) {
-      constexpr int RPS = 64 / TL;
-      const double (*buf)[YP] = &yb[bb * TL];
-      const int sub = lane / TL, k = lane % TL;
-      const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
-#pragma unroll 4
-      for (int row = 0; row < 32; row += RPS) {
-        const int rr = row + sub;
-        const int64_t so = w * 32 + rr;
-        const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
-        if (so < n_streams) z[(size_t)so * n + zo] = v;
-      }
-    };
     auto refwd = [&](v4u (&r)[NI], double (&c)[6], int64_t it) {
       const int64_t t = n_tiles - 1 - it;
-      if (it >= 2) store_tile((int)(it & 1), t + 2);     // done by wave 1 in iteration it-1
+      if (!W1S && it >= 2) store_tile((int)(it & 1), t + 2);   // done by wave 1 in iteration it-1
       if (t >= 0) {
         deposit(r);
 #pragma unroll
@@ -413,13 +415,14 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       refwd(r1, c1, it + 1);
     }
     if (it <= n_tiles) refwd(r0, c0, it);
-    if (n_tiles >= 1) store_tile((int)((n_tiles - 1) & 1), 0);   // wave 1's last tile
+    if (!W1S && n_tiles >= 1) store_tile((int)((n_tiles - 1) & 1), 0);   // wave 1's last tile
   } else {
     for (int64_t it = 0; it <= n_tiles; ++it) {
       if (it >= 1) {                                     // tile n_tiles - it, re-run forward by wave 0
         double (*buf)[YP] = &yb[((it - 1) & 1) * TL];
 #pragma unroll 8
         for (int k = TL - 1; k >= 0; --k) buf[k][lane] = fsk_step<ZO>(zs, b, a, buf[k][lane]);
+        if constexpr (W1S) store_tile((int)((it - 1) & 1), n_tiles - it);
       }
       __syncthreads();
     }
@@ -510,12 +513,16 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
                                         double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
   if (!fsk_one_wave()) {
+    // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
+    static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
+#define BP2(T, S) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
     switch (dtype) {
-      case kF32: hipLaunchKernelGGL((k_fsk_bandpass2<float, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kF64: hipLaunchKernelGGL((k_fsk_bandpass2<double, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-      case kI16: hipLaunchKernelGGL((k_fsk_bandpass2<int16_t, ZO, LIVE>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+      case kF32: if (w1s) BP2(float, true); else BP2(float, false); break;
+      case kF64: if (w1s) BP2(double, true); else BP2(double, false); break;
+      case kI16: if (w1s) BP2(int16_t, true); else BP2(int16_t, false); break;
       default: return hipErrorInvalidValue;
     }
+#undef BP2
     return hipGetLastError();
   }
   switch (dtype) {

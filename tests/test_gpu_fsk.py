@@ -282,3 +282,39 @@ def test_fsk_live_async_host_entry():
     got = [o[i, :ln[i]].tobytes() for i in range(B)]
     assert got == pl.demod_host(x)[0]
     assert got == [oracle.fsk_demodulate(r, 9600, 12000.0, 24000.0) for r in x]
+
+
+@pytest.mark.parametrize("env", [{"AMR_FFT_MID_TWG": "0"}, {"AMR_FFT_PRUNE": "0"}, {"AMR_FSK_W1S": "0"},
+                                 {"AMR_FSK_BP1": "1"}],
+                         ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
+def test_fsk_live_kernel_variants(tmp_path, env):
+    """Every kernel variant of the live-column path, forced through its switch
+    (DESIGN.md §3b): middle pass with the W_L table in LDS / with every output
+    of the last stage computed, F1 storing z from wave 0 / the one-wave F1:
+    float32, float64 and int16 batches == the oracle, bit for bit."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    script = tmp_path / "var.py"
+    script.write_text(f'''
+import sys
+sys.path[:0] = [{os.path.join(root, "audio-modem-radio_amd")!r}, {root!r}, {here!r}]
+import numpy as np
+import _fsk, synth
+from oracle import oracle
+bad = []
+for (B, N, baud, m, s, dt) in ((40, 96000, 9600, 12000.0, 24000.0, np.float32), (9, 96000, 19200, 21000.0, 27000.0, np.float64),
+                               (33, 96000, 4800, 8000.0, 16000.0, np.int16)):
+    x = synth.fsk_batch(B, N, baud, m, s, seed=B + 1, distinct=5, noise=0.3)
+    x = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16) if dt == np.int16 else x.astype(dt)
+    pl = _fsk.FskPlan(N, baud, m, s, max_streams=B)
+    assert pl.live_columns
+    got, _ = pl.demod_host(x)
+    bad += [(N, baud, i) for i in range(B) if got[i] != oracle.fsk_demodulate(x[i], baud, m, s)]
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+''')
+    r = subprocess.run([sys.executable, str(script)], env=dict(os.environ, **env), capture_output=True, text=True,
+                       timeout=250)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
