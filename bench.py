@@ -180,7 +180,8 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
     # launch holds >= 4096 streams (what one batch of the headline holds); the
     # timed region is still exactly K steps (the last launch may be partial)
     C, BL, n_launch, launch_sizes = launch_plan(K, B, strong, args.coalesce)
-    P = args.inflight or (min(2, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
+    # fsk9600: 4 in flight (35.4 GB of plan scratch each; K = 64, one MI355X: P = 2 34.4 ms/step, 3 33.7, 4 33.1)
+    P = args.inflight or (min(4, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
     t0 = time.perf_counter()
@@ -868,7 +869,7 @@ def main():
                     help="steps per launch (0 = enough for >= 4096 streams per launch on strong-scaling shards, "
                          "else 1)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 2)")
+                    help="batches in flight on separate plans / HIP streams (0 = default_inflight(steps); fsk9600 4)")
     args = ap.parse_args()
 
     L = _amr.lib()
