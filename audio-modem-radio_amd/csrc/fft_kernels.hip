@@ -531,8 +531,12 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, doub
 // TWG: the row's W_L table is read from global memory (L1 / scalar-cache
 // resident: 4.8 KB shared by every workgroup) instead of LDS, and the position
 // table is 16-bit, so four workgroups fit a CU's LDS instead of three.
-template <int PC, int QC, bool TWG>
-__global__ __launch_bounds__(kFftThreads) __attribute__((amdgpu_waves_per_eu(TWG && PC > 0 ? 4 : 1))) void k_fft_mid_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
+// NT: threads per workgroup.  No stage runs more than 8 * 20 = 160 butterflies
+// at the benchmark lengths, so NT = 192 (three waves) leaves one wave less idle
+// per workgroup, and four workgroups per CU are then three waves per SIMD:
+// 168 VGPRs, no spills (NT = 256 holds 128 and spills).
+template <int PC, int QC, bool TWG, int NT = kFftThreads>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(TWG && PC > 0 ? (NT == kFftThreads ? 4 : 3) : 1))) void k_fft_mid_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
                                                              LiveCols lc) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(kFftThreads) __attribute__((amdgpu_waves_per_eu(TWG
   // column c -> its live index l (>= 0) or ~(dead index d), once per workgroup
   // (the per-element form cost the pass more ALU than its FFT: 12.7 vs 10.9 ms)
   __shared__ int16_t cpos[kFftMaxL];
-  for (int c = threadIdx.x; c < lc.n1; c += kFftThreads) {
+  for (int c = threadIdx.x; c < lc.n1; c += NT) {
     bool lv;
     const int pos = lc_col_pos(lc, c, lv);
     cpos[c] = lv ? pos : ~pos;
@@ -824,10 +828,15 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
 #undef COLSL
   // AMR_FFT_MID_TWG=0: the W_L table in LDS (three workgroups per CU instead of four)
   static const bool twg = [] { const char* e = getenv("AMR_FFT_MID_TWG"); return !(e && e[0] == '0'); }();
+  // AMR_FFT_MID_NT=192: three-wave workgroups (specialised lengths, TWG form)
+  static const bool nt192 = [] { const char* e = getenv("AMR_FFT_MID_NT"); return e && atoi(e) == 192; }();
   const size_t sm_mid = twg ? (size_t)kFftTile * d.c.S * sizeof(double2) : fft_smem_bytes(d.c);
 #define MIDL(P, Q)                                                                                              \
   do {                                                                                                          \
-    if (twg)                                                                                                    \
+    if (twg && nt192 && P > 0 && kFftTile * d.c.r1 <= 192 && kFftTile * d.c.r2 <= 192)                          \
+      hipLaunchKernelGGL((k_fft_mid_live<P, Q, true, 192>), dim3(gmid), dim3(192), sm_mid, st, zb, cb, d,      \
+                         batch, lc);                                                                            \
+    else if (twg)                                                                                               \
       hipLaunchKernelGGL((k_fft_mid_live<P, Q, true>), dim3(gmid), dim3(kFftThreads), sm_mid, st, zb, cb, d,  \
                          batch, lc);                                                                            \
     else                                                                                                        \
@@ -971,7 +980,8 @@ static hipError_t fft_set_smem(int bytes) {
       (const void*)k_fft_rows<false, kStore, P, Q>, (const void*)k_fft_rows<true, kStore, P, Q>,
       (const void*)k_fft_rows<true, kEnvelope, P, Q>, (const void*)k_fft_rows<true, kEnvOut, P, Q>,
       (const void*)k_fft_cols_live<P, Q>, (const void*)k_fft_mid_live<P, Q, false>,
-      (const void*)k_fft_mid_live<P, Q, true>, (const void*)k_fft_rows_live<P, Q>};
+      (const void*)k_fft_mid_live<P, Q, true>, (const void*)k_fft_mid_live<P, Q, true, 192>,
+      (const void*)k_fft_rows_live<P, Q>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
