@@ -148,6 +148,34 @@ def test_full_size_lane_layout_as_benched(baud):
     assert np.array_equal(gsync, wsync)
 
 
+@pytest.mark.parametrize("layout", ["lane", "row"])
+def test_ten_second_captures_past_2g_samples(layout):
+    """10-s captures (960 000 samples, what decode_wav_file hands the demod
+    after resampling a 10-s WAV, decoder.py:385-389) in a batch of 2304:
+    2.2e9 samples, past 2^31, so every sample, state, checkpoint and symbol
+    offset of both layouts must be 64-bit.  The batch cycles through 61
+    distinct noisy captures (prime, so a stream that read another stream's
+    rows, 64 or 128 groups away, would decode a different frame); every
+    stream's bytes and sync index == the oracle's for its capture."""
+    import _amr
+    import synth
+    from oracle import oracle
+    B, N, U = 2304, 960000, 61
+    assert B * N > 2 ** 31
+    base = synth.qpsk_batch(U, N, 9600, seed=61, distinct=U)
+    want, wsync = oracle.psk_demod_batch("qpsk", base, 9600, n_threads=min(16, os.cpu_count() or 1))
+    x = base[np.arange(B) % U]
+    plan = _amr.PskPlan("qpsk", N, 9600, max_streams=B)
+    if layout == "lane":
+        plan.set_inflight(16)
+    got, gsync = plan.demod_host(x)
+    assert plan.last_layout() == layout
+    del plan
+    mism = [i for i in range(B) if got[i] != want[i % U]]
+    assert not mism, f"{len(mism)} streams differ, first {mism[:5]}"
+    assert np.array_equal(gsync, wsync[np.arange(B) % U])
+
+
 def test_ragged_streams():
     import modem
     from oracle import oracle
