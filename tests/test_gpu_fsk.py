@@ -161,6 +161,31 @@ def test_fsk_full_batch_round_trip():
         assert cg[j][:m] == frames[j][:m]
 
 
+def test_fsk_batch_past_2g_samples():
+    """22 400 one-second FSK9600 streams in one plan: 2.15e9 samples, past
+    2^31, through the live-column path (F1's z offsets, the FFT passes' per
+    stream bases, the compare bits and words must all be 64-bit).  The batch
+    cycles through 61 distinct noisy captures (prime: a stream that read
+    another stream's rows would decode a different frame); every stream ==
+    the oracle's bytes for its capture."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    B, N, U = 22400, 96000, 61
+    assert B * N > 2 ** 31
+    base = synth.fsk_batch(U, N, 9600, 12000.0, 24000.0, seed=61, distinct=U, noise=0.3)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        want = list(ex.map(lambda r: oracle.fsk_demodulate(r, 9600, 12000.0, 24000.0), base))
+    x = base[np.arange(B) % U]
+    pl = _fsk.FskPlan(N, 9600, 12000.0, 24000.0, max_streams=B)
+    assert pl.live_columns
+    got, _ = pl.demod_host(x)
+    del pl
+    bad = [i for i in range(B) if got[i] != want[i % U]]
+    assert not bad, f"{len(bad)} streams differ, first {bad[:5]}"
+
+
 def test_fsk_timing_hooks():
     import _fsk
     import synth
