@@ -399,7 +399,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
         # as the scheduler grants them)
         threads, cores_how = host_cores()
         xh = np.empty((BL, N), np.float32)
-        if headline and not fsk and not args.no_cpu:
+        if headline and not fsk and not args.no_cpu and world == 1:
             # how many threads these host cores run fastest at: the affinity /
             # quota count, or the box's OMP_NUM_THREADS share -- when the
             # scheduler grants fewer CPUs than the mask shows, threads beyond
@@ -439,7 +439,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                     want = [oracle.fec_decode(w)[0] for w in want]
             cdt = time.perf_counter() - t1
             reps = 1
-            if k == 0 and headline and not fsk:
+            if k == 0 and headline and not fsk and world == 1:
                 # the CPU baseline: the same streams again until about
                 # --cpu-seconds of wall time have been spent on them
                 while cdt < args.cpu_seconds:
@@ -447,7 +447,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                     oracle.psk_demod_batch("qpsk", xs, baud, n_threads=threads)
                     cdt += time.perf_counter() - t1
                     reps += 1
-            if k == 0:
+            if k == 0 and world == 1:                     # the CPU baseline: rank 0 at N = 1 only
                 how = ("oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
                        if fsk else "the C restatement oracle/amr_oracle.c, OpenMP over streams" +
                        (" + oracle.fec_decode" if fec_fused else ""))
