@@ -237,7 +237,7 @@ struct amr_comm {
   hipStream_t stream = nullptr;
   int device = 0;
   int nranks = 1, rank = 0;
-  std::mutex mu;                // the host collectives' staging buffer
+  std::mutex mu;                // every RCCL call on comm (amr_allgather*, the host collectives) and the staging buffer
   void* stage = nullptr;        // device staging of amr_comm_allgather_host / allreduce_max
   int64_t stage_bytes = 0;
 };
@@ -1093,6 +1093,9 @@ void gate_free(GatherGate& g) {
 int allgather_after(amr_comm* comm, const void* d_send, void* d_recv, int64_t bytes_per_rank, hipStream_t producer,
                     GatherGate* gate, hipEvent_t done) {
   if (!comm || !d_send || !d_recv || bytes_per_rank < 0) return fail(AMR_E_INVALID, "bad allgather args");
+  // one RCCL call on the communicator at a time, whichever host thread makes
+  // it (the host collectives take the same lock; lock order: plan, then comm)
+  std::lock_guard<std::mutex> lk(comm->mu);
   HIP_TRY(hipSetDevice(comm->device));
   hipEvent_t before = nullptr;
   if (gate) {
