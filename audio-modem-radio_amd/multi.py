@@ -164,6 +164,12 @@ class FileStore:
         with open(f, "rb") as fh:
             return fh.read()
 
+    def delete(self, key: str):
+        try:
+            os.remove(self._file(key))
+        except FileNotFoundError:
+            pass
+
     def close(self, owner: bool = False):
         if owner:
             import shutil
@@ -203,6 +209,10 @@ class _TcpServer(threading.Thread):
                             self.cv.wait_for(lambda: key in self.data or self.stop)
                             v = self.data.get(key, b"")
                         _send_msg(conn, b"V", key, v)
+                    elif op == b"D":
+                        with self.cv:
+                            self.data.pop(key, None)
+                        _send_msg(conn, b"K", key, b"")
             except (ConnectionError, OSError):
                 return
 
@@ -269,6 +279,11 @@ class TcpStore:
             _send_msg(self.conn, b"G", key, b"")
             return _recv_msg(self.conn)[2]
 
+    def delete(self, key: str):
+        with self.lock:
+            _send_msg(self.conn, b"D", key, b"")
+            _recv_msg(self.conn)
+
     def close(self, owner: bool = False):
         try:
             self.conn.close()
@@ -319,7 +334,13 @@ class StoreTransport:
         tag = f"x{self.seq}"
         self.seq += 1
         self.store.set(f"{tag}/{self.rank}", blob)
-        return [self.store.get(f"{tag}/{r}") for r in range(self.world)]
+        parts = [self.store.get(f"{tag}/{r}") for r in range(self.world)]
+        # every rank has posted this exchange, so every rank is done reading
+        # the previous one: this rank's key of it can go (a long-lived
+        # transport keeps at most two exchanges in the store)
+        if self.seq >= 2:
+            self.store.delete(f"x{self.seq - 2}/{self.rank}")
+        return parts
 
     def all_gather(self, a: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(a)

@@ -214,3 +214,26 @@ def test_product_package_is_torch_free():
                         if "import torch" in code or "from torch" in code:
                             hits.append(f"{f}:{i}")
     assert not hits, hits
+
+
+def _many_exchanges_worker(rank, world, kind, port, tmp, result_file):
+    tp = _make_transport(kind, rank, world, port, tmp)
+    for i in range(60):
+        got = tp.all_gather(np.array([rank, i], np.int64))
+        assert got.tolist() == [[r, i] for r in range(world)]
+    tp.barrier()
+    if rank == 0 and kind == "file":
+        np.save(result_file, np.array([len(os.listdir(tmp))]))
+    tp.barrier()
+    _close(kind, tp)
+
+
+@pytest.mark.parametrize("kind", ["file", "tcp"])
+def test_store_transport_keeps_few_keys(tmp_path, kind):
+    """A long-lived StoreTransport deletes each exchange's keys once every rank
+    has moved past it: after 60 all-gathers (+ barriers) the file store holds
+    at most the last two exchanges' keys, and every gather is right."""
+    out = str(tmp_path / "n.npy")
+    _spawn(_many_exchanges_worker, 3, (kind, _free_port(), str(tmp_path / "store"), out))
+    if kind == "file":
+        assert int(np.load(out)[0]) <= 2 * 3
