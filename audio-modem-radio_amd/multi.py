@@ -442,9 +442,22 @@ def demod_sharded(x, demod_batch, transport, cap: int | None = None, steps=None)
     n = np.asarray(xs[0]).shape[0] if xs else 0
     layout = ShardLayout(n, transport.world, len(xs))
     local = layout.local_rows(xs, transport.rank)
-    outs = demod_batch(local) if len(local) else []
+    err = None
+    try:
+        outs = demod_batch(local) if len(local) else []
+    except Exception as e:                     # reported on every rank below
+        outs, err = [], e
+    # one small collective carries whether any rank failed and the longest
+    # local output (the gather's capacity): a rank whose demodulation raised
+    # still joins it, so no rank is left waiting in the gather for it
+    st = transport.all_gather(np.array([err is not None, max((len(o) for o in outs), default=0)], np.int64))
+    failed = [int(r) for r in np.flatnonzero(st[:, 0])]
+    if failed:
+        if err is not None:
+            raise err
+        raise RuntimeError(f"demodulation failed on rank(s) {failed}")
     if cap is None:
-        cap = int(transport.max(float(max((len(o) for o in outs), default=0))))
+        cap = int(st[:, 1].max())
     return gather_outputs(outs, layout, max(1, cap), transport)
 
 

@@ -237,3 +237,33 @@ def test_store_transport_keeps_few_keys(tmp_path, kind):
     _spawn(_many_exchanges_worker, 3, (kind, _free_port(), str(tmp_path / "store"), out))
     if kind == "file":
         assert int(np.load(out)[0]) <= 2 * 3
+
+
+def _failing_rank_worker(rank, world, kind, port, tmp, result_file):
+    tp = _make_transport(kind, rank, world, port, tmp)
+    import multi
+
+    def demod(xs):
+        if rank == 1:
+            raise ValueError("rank 1's demodulation fails")
+        return [bytes(8)] * len(xs)
+    try:
+        multi.demod_sharded(np.zeros((6, 100), np.float32), demod, tp)
+        what = "no error"
+    except ValueError as e:
+        what = f"ValueError: {e}"
+    except RuntimeError as e:
+        what = f"RuntimeError: {e}"
+    np.save(result_file.format(rank=rank), np.array([what]))
+    _close(kind, tp)
+
+
+def test_failing_rank_is_reported_on_every_rank(tmp_path):
+    """A rank whose demodulation raises still joins the status collective:
+    it re-raises its own error, the other ranks raise naming it -- nobody is
+    left waiting in the gather."""
+    out = str(tmp_path / "r{rank}.npy")
+    _spawn(_failing_rank_worker, 3, ("file", _free_port(), str(tmp_path / "store"), out))
+    got = [str(np.load(out.format(rank=r))[0]) for r in range(3)]
+    assert got[1] == "ValueError: rank 1's demodulation fails"
+    assert got[0] == got[2] == "RuntimeError: demodulation failed on rank(s) [1]"
