@@ -488,10 +488,8 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
 // so the middle pass writes 40 % and the final pass reads 2 x 40 % of a full
 // pass at sps 10, and the plan holds 1.4 x n complex per
 // stream instead of 3 x.
-// NT: threads per workgroup (192: the three waves the 8 x 16 / 8 x 20
-// butterflies of the specialised stages need; AMR_FFT_CR_NT)
-template <int PC, int QC, int NT = kFftThreads>
-__global__ __launch_bounds__(NT) void k_fft_cols_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
+template <int PC, int QC>
+__global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
                                                               LiveCols lc) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tl = (lc.nl + kFftTile - 1) / kFftTile, tiles = tl + (lc.nd + kFftTile - 1) / kFftTile;
@@ -619,8 +617,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(TWG && PC > 
 // final pass: live columns l0 .. l0+7 of C (length n2 each, stride nl) ->
 // DFT, conj, 1/n -> compare against z's live samples (L) -> bits, byte
 // (l0 / 8) * n2 + k1' (the decide kernel's live addressing)
-template <int PC, int QC, int NT = kFftThreads>
-__global__ __launch_bounds__(NT) void k_fft_rows_live(const double2* __restrict__ zb,
+template <int PC, int QC>
+__global__ __launch_bounds__(kFftThreads) void k_fft_rows_live(const double2* __restrict__ zb,
                                                               const double2* __restrict__ cb, FftDesc d,
                                                               int64_t batch, double scale, FftEpi e, LiveCols lc) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
@@ -824,19 +822,10 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
   const unsigned gmid = grid8(batch * ((d.n2 + kFftTile - 1) / kFftTile));
   const unsigned gfin = grid8(batch * tl);
   const double scale = 1.0 / (double)d.n;
-  // AMR_FFT_CR_NT=192 / 256: the column and final passes in three- / four-wave
-  // workgroups (specialised lengths only)
-  static const int cr_nt = [] { const char* e = getenv("AMR_FFT_CR_NT"); return e ? atoi(e) : 256; }();
-  const bool cr192 = cr_nt == 192 && kFftTile * d.a.r1 <= 192 && kFftTile * d.a.r2 <= 192;
-#define COLSL(P, Q)                                                                                              \
-  do {                                                                                                           \
-    if (P > 0 && cr192)                                                                                          \
-      hipLaunchKernelGGL((k_fft_cols_live<P, Q, 192>), dim3(gcol), dim3(192), fft_smem_bytes(d.a), st, zb, cb, d, \
-                         batch, lc);                                                                             \
-    else                                                                                                         \
-      hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, \
-                         d, batch, lc);                                                                          \
-  } while (0)
+  // (the column and final passes stay four-wave: three-wave workgroups
+  // measured slower for them)
+#define COLSL(P, Q) \
+  hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, batch, lc)
   AMR_FFT_PQ(d.a, COLSL);
 #undef COLSL
   // AMR_FFT_MID_TWG=0: the W_L table in LDS (three workgroups per CU instead of four)
@@ -859,15 +848,9 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
   } while (0)
   AMR_FFT_PQ(d.c, MIDL);
 #undef MIDL
-#define FINL(P, Q)                                                                                               \
-  do {                                                                                                           \
-    if (P > 0 && cr192)                                                                                          \
-      hipLaunchKernelGGL((k_fft_rows_live<P, Q, 192>), dim3(gfin), dim3(192), fft_smem_bytes(d.a), st, zb, cb, d, \
-                         batch, scale, epi, lc);                                                                 \
-    else                                                                                                         \
-      hipLaunchKernelGGL((k_fft_rows_live<P, Q>), dim3(gfin), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, \
-                         d, batch, scale, epi, lc);                                                              \
-  } while (0)
+#define FINL(P, Q)                                                                                          \
+  hipLaunchKernelGGL((k_fft_rows_live<P, Q>), dim3(gfin), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, \
+                     batch, scale, epi, lc)
   AMR_FFT_PQ(d.a, FINL);
 #undef FINL
   return hipGetLastError();
@@ -1001,8 +984,7 @@ static hipError_t fft_set_smem(int bytes) {
       (const void*)k_fft_rows<true, kEnvelope, P, Q>, (const void*)k_fft_rows<true, kEnvOut, P, Q>,
       (const void*)k_fft_cols_live<P, Q>, (const void*)k_fft_mid_live<P, Q, false>,
       (const void*)k_fft_mid_live<P, Q, true>, (const void*)k_fft_mid_live<P, Q, true, 192>,
-      (const void*)k_fft_rows_live<P, Q>, (const void*)k_fft_cols_live<P, Q, 192>,
-      (const void*)k_fft_rows_live<P, Q, 192>};
+      (const void*)k_fft_rows_live<P, Q>};
   for (const void* f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;

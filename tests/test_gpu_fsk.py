@@ -351,7 +351,7 @@ def test_fsk_live_async_host_entry():
 
 
 @pytest.mark.parametrize("env", [{"AMR_FFT_MID_TWG": "0"}, {"AMR_FFT_PRUNE": "0"}, {"AMR_FSK_W1S": "0"},
-                                 {"AMR_FSK_BP1": "1"}, {"AMR_FFT_MID_NT": "256"}, {"AMR_FFT_CR_NT": "192"}],
+                                 {"AMR_FSK_BP1": "1"}, {"AMR_FFT_MID_NT": "256"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_fsk_live_kernel_variants(tmp_path, env):
     """Every kernel variant of the live-column path, forced through its switch
