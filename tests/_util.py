@@ -31,3 +31,12 @@ def expected(case):
     if case["status"] == "ok":
         return ("ok", case["out"])
     return ("err", case["etype"], case["emsg"])
+
+
+def call_sweep_case(mod, case, x):
+    """Dispatch one sweep case (tests/golden/sweep_manifest.json) to `mod`."""
+    fn, p = case["fn"], case["params"]
+    if fn == "fsk":
+        return mod.fsk_demodulate(x, baud=p["baud"], mark_freq=p["f0"], space_freq=p["f1"], samp_rate=p["samp_rate"])
+    f = mod.qpsk_demodulate if fn == "qpsk" else mod.bpsk_demodulate
+    return f(x, baud=p["baud"], carrier=p["f0"], samp_rate=p["samp_rate"])

@@ -27,6 +27,19 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def sweep_golden():
+    """The reference's outputs over a seeded draw of configurations
+    (tests/golden/make_sweep_golden.py)."""
+    import json
+
+    import numpy as np
+    g = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(g, "sweep_manifest.json")) as f:
+        manifest = json.load(f)
+    return manifest, np.load(os.path.join(g, "sweep.npz"))
+
+
+@pytest.fixture(scope="session")
 def built_lib():
     """libamr.so, built in-tree if missing (hipcc cross-compiles without a GPU)."""
     import build

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Reference outputs over a seeded draw of demod configurations (this
+container only): the REFERENCE's own modem.qpsk_demodulate / bpsk_demodulate
+/ fsk_demodulate (modem.py:189-266, 68-135, 298-341) on inputs drawn across
+the parameter space their signatures accept -- baud, carrier / tones, sample
+rate, length, input dtype, signal level, leading silence (PSK), noise.
+Committed data only:
+
+  tests/golden/sweep.npz            the inputs (their own dtype), key c<i>
+  tests/golden/sweep_manifest.json  per case: function, parameters, and the
+                                    reference's bytes (hex) or exception
+
+tests/test_oracle_golden.py pins the oracle to these on the CPU;
+tests/test_gpu_sweep.py checks the GPU against them.  FSK inputs keep a
+noise floor (decisions inside exact digital silence
+next to signal are pocketfft's rounding, not reproducible).
+
+Run:  python tests/golden/make_sweep_golden.py   (needs /root/reference)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import make_golden as mg  # noqa: E402  (the reference import helpers; its main() is not run)
+import synth  # noqa: E402
+
+N_CASES = 72
+
+
+def draw(rng, c):
+    kind = ["qpsk", "bpsk", "fsk"][c % 3]
+    fs = float(rng.choice([96000, 96000, 48000, 44100]))
+    n = int(rng.choice([int(rng.integers(28, 600)), int(rng.integers(600, 8000)), int(rng.integers(8000, 24000))]))
+    if kind == "fsk":
+        baud = int(rng.choice([300, 600, 1200, 2400, 4800, 9600]))
+        nyq = fs / 2
+        lo, hi = baud * 1.1, nyq - baud * 1.1
+        if rng.random() < 0.15 or hi <= lo:
+            f0, f1 = 1200.0, 2200.0                      # the reference's defaults (raise above ~1000 Bd)
+        else:
+            f0, f1 = sorted(round(float(v), 3) for v in rng.uniform(lo, hi, 2))
+    else:
+        baud = int(rng.choice([300, 600, 1000, 1200, 1500, 2400, 3000, 4800, 9600, 19200]))
+        f0, f1 = float(rng.choice([3000.0, 3000.0, 1800.0, 6000.0, 12000.0])), 0.0
+    noise = float(rng.choice([0.0, 0.02, 0.1, 0.4])) if kind != "fsk" else float(rng.choice([0.02, 0.1, 0.4]))
+    if rng.random() < 0.1:
+        x = rng.normal(0, 0.5, n)
+    else:
+        fr = synth.random_frame(rng, int(rng.integers(4, 48)))
+        try:
+            if kind == "qpsk":
+                w = synth.qpsk_waveform(fr, baud, f0, fs)
+            elif kind == "bpsk":
+                w = synth.bpsk_waveform(fr, baud, f0, fs)
+            else:
+                w = synth.fsk_waveform(fr, baud, f0, f1, fs)
+        except ValueError:                               # the PSK modulators raise below 10 samples per symbol
+            w = rng.normal(0, 0.5, n)
+        off = int(rng.integers(0, max(1, n // 4))) if kind != "fsk" else 0
+        x = np.zeros(n)
+        seg = w[:max(0, n - off)]
+        x[off:off + seg.size] = seg * float(rng.choice([1.0, 0.3, 0.01]))
+        x = x + rng.normal(0, noise, n) * (float(np.abs(x).max()) if np.abs(x).max() > 0 else 1.0)
+    dt = str(rng.choice(["float32", "float64", "int16"]))
+    if dt == "int16":
+        x = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16)
+    else:
+        x = x.astype(dt)
+    return kind, dict(baud=baud, f0=f0, f1=f1, samp_rate=fs), x
+
+
+def main():
+    rng = np.random.default_rng(20261017)
+    draws = [draw(rng, c) for c in range(N_CASES)]
+    scratch = tempfile.mkdtemp(prefix="amr_sweep_golden_")
+    cwd = os.getcwd()
+    try:
+        modem, _, _ = mg._import_reference(scratch)
+        cases, arrays = [], {}
+        for c, (kind, p, x) in enumerate(draws):
+            # the reference reads int16 WAV samples as int16 / 32768 (soundfile, decoder.py:383)
+            xr = x.astype(np.float64) / 32768.0 if x.dtype == np.int16 else x
+            if kind == "qpsk":
+                res = mg._run(modem.qpsk_demodulate, xr, baud=p["baud"], carrier=p["f0"], samp_rate=p["samp_rate"])
+            elif kind == "bpsk":
+                res = mg._run(modem.bpsk_demodulate, xr, baud=p["baud"], carrier=p["f0"], samp_rate=p["samp_rate"])
+            else:
+                res = mg._run(modem.fsk_demodulate, xr, baud=p["baud"], mark_freq=p["f0"], space_freq=p["f1"],
+                              samp_rate=p["samp_rate"])
+            arrays[f"c{c}"] = x
+            cases.append(dict(id=f"c{c}", fn=kind, params=p, dtype=str(x.dtype), n=int(x.size), **res))
+    finally:
+        os.chdir(cwd)
+    np.savez_compressed(os.path.join(HERE, "sweep.npz"), **arrays)
+    with open(os.path.join(HERE, "sweep_manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_sweep_golden.py", "numpy": np.__version__,
+                   "numpy_cpu_features": mg.numpy_cpu_features(), "cases": cases}, f, indent=1)
+    ok = sum(c["status"] == "ok" for c in cases)
+    print(f"{len(cases)} cases ({ok} ok, {len(cases) - ok} raise)")
+
+
+if __name__ == "__main__":
+    main()

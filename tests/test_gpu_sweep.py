@@ -126,3 +126,19 @@ def test_fsk_sweep():
         if g != w:
             bad.append((c, baud, mark, space, fs, n, B, str(x.dtype), g[0], w[0], str(g[1])[:80], str(w[1])[:80]))
     assert not bad, f"{len(bad)} of {N_FSK} configurations differ: {bad[:5]}"
+
+
+def test_reference_sweep_through_the_drop_in(sweep_golden):
+    """The drop-in modules (modem.qpsk_demodulate / bpsk_demodulate /
+    fsk_demodulate on the GPU) against the REFERENCE's own outputs on the 72
+    seeded configurations of tests/golden/make_sweep_golden.py: bytes or
+    exception text equal, every case."""
+    import modem
+    from _util import call_sweep_case, expected, outcome
+    manifest, inputs = sweep_golden
+    bad = []
+    for c in manifest["cases"]:
+        got = outcome(lambda: call_sweep_case(modem, c, inputs[c["id"]]))
+        if got != expected(c):
+            bad.append((c["id"], c["fn"], c["params"], c["dtype"], c["n"], got[0]))
+    assert not bad, f"{len(bad)} of {len(manifest['cases'])} differ from the reference: {bad[:5]}"
