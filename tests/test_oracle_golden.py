@@ -96,3 +96,32 @@ def test_oracle_matches_reference_sweep(sweep_golden):
     bad = [c["id"] for c in manifest["cases"]
            if outcome(lambda: call_sweep_case(oracle, c, inputs[c["id"]])) != expected(c)]
     assert not bad, f"oracle differs from the reference on {bad}"
+
+
+def _smooth5(n):
+    for p in (2, 3, 5):
+        while n % p == 0:
+            n //= p
+    return n == 1
+
+
+def test_oracle_hilbert_is_scipys():
+    """The oracle's restatement of |scipy.signal.hilbert(x)| (amr_hilbert.c:
+    pocketfft's real forward and complex backward transforms, their twiddle
+    generator, scipy's h, numpy's AVX-512 complex abs) equals scipy + numpy
+    bit for bit, on every 5-smooth length up to 500 and the FSK lengths, for
+    noise and for signal between exact-zero stretches (where the envelopes
+    are rounding noise -- DESIGN.md §2 item 6)."""
+    from scipy import signal
+    rng = np.random.default_rng(7)
+    sizes = [n for n in range(1, 500) if _smooth5(n)] + [960, 1920, 9600, 19200, 48000, 96000, 153600]
+    bad = []
+    for n in sizes:
+        for kind in ("noise", "silence"):
+            x = rng.normal(size=n)
+            if kind == "silence":
+                x[: n // 3] = 0.0
+                x[2 * n // 3:] = 0.0
+            if not np.array_equal(oracle.hilbert_env(x), np.abs(signal.hilbert(x))):
+                bad.append((n, kind))
+    assert not bad, bad
