@@ -12,8 +12,10 @@ Committed data only:
 
 tests/test_oracle_golden.py pins the oracle to these on the CPU;
 tests/test_gpu_sweep.py checks the GPU against them.  FSK inputs keep a
-noise floor (decisions inside exact digital silence
-next to signal are pocketfft's rounding, not reproducible).
+noise floor, and 12 extra FSK cases sit between stretches of exact digital
+silence (params.silence): there only pocketfft's own rounding decides
+(DESIGN.md §2 item 6) -- the oracle, which restates it, must match them;
+the GPU is held to them only outside that ambiguity.
 
 Run:  python tests/golden/make_sweep_golden.py   (needs /root/reference)
 """
@@ -76,9 +78,31 @@ def draw(rng, c):
     return kind, dict(baud=baud, f0=f0, f1=f1, samp_rate=fs), x
 
 
+N_SILENCE = 12
+
+
+def draw_silence(rng):
+    """FSK between stretches of exact digital silence, no noise: the inputs on
+    which only pocketfft's own rounding decides."""
+    fs = 96000.0
+    baud = int(rng.choice([1200, 2400, 4800, 9600]))
+    f0, f1 = sorted(round(float(v), 3) for v in rng.uniform(baud * 1.1, fs / 2 - baud * 1.1, 2))
+    n = int(rng.choice([9600, 19200, 24000, 30000]))
+    fr = synth.random_frame(rng, int(rng.integers(4, 24)))
+    w = synth.fsk_waveform(fr, baud, f0, f1, fs)
+    off = int(rng.integers(n // 8, n // 3))
+    x = np.zeros(n)
+    seg = w[:max(0, n - off)]
+    x[off:off + seg.size] = seg
+    dt = str(rng.choice(["float32", "float64", "int16"]))
+    x = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16) if dt == "int16" else x.astype(dt)
+    return "fsk", dict(baud=baud, f0=f0, f1=f1, samp_rate=fs, silence=True), x
+
+
 def main():
     rng = np.random.default_rng(20261017)
     draws = [draw(rng, c) for c in range(N_CASES)]
+    draws += [draw_silence(rng) for _ in range(N_SILENCE)]
     scratch = tempfile.mkdtemp(prefix="amr_sweep_golden_")
     cwd = os.getcwd()
     try:

@@ -90,8 +90,10 @@ def test_oracle_matches_reference_sweep(sweep_golden):
     """The oracle against the reference's own outputs on a seeded draw of 72
     configurations (PSK and FSK; baud 300-19200, carriers / tones, 96 / 48 /
     44.1 kHz, 28-24 000 samples, f32 / f64 / int16, levels down to 1 %,
-    leading silence, noise; tests/golden/make_sweep_golden.py): bytes or
-    exception text equal, every case."""
+    leading silence, noise) and 12 FSK streams between stretches of exact
+    digital silence, where only pocketfft's own rounding decides
+    (tests/golden/make_sweep_golden.py): bytes or exception text equal,
+    every case."""
     manifest, inputs = sweep_golden
     bad = [c["id"] for c in manifest["cases"]
            if outcome(lambda: call_sweep_case(oracle, c, inputs[c["id"]])) != expected(c)]
