@@ -127,6 +127,9 @@ struct FskParams {
   int64_t bits_stride;
   float inv_rn1;
   LiveCols lc;      // lc.on: z and the compare bits in the live-column layout
+  uint32_t* xflags; // non-null: F1 writes [B / 32] bit s = stream s has digital silence (the exact
+                    // fallback), F3 then reads that stream's compare bits from xbits
+  const uint8_t* xbits;
 };
 
 struct FskIir {            // [tone][tap], tone 0 = mark

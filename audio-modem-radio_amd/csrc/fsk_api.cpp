@@ -20,6 +20,7 @@
 
 #include "amr_internal.h"
 #include "api_common.h"
+#include "fsk_exact.h"
 #include "fft.h"
 
 namespace amr {
@@ -336,6 +337,15 @@ struct amr_fsk_plan {
   int64_t u_bytes = 0;
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
+  // the exact fallback for streams with digital silence (fsk_exact_kernels.hip)
+  bool exact_on = false;
+  uint32_t* xflags = nullptr;  // [B / 32] F1's digital-silence flags, bit s of word s / 32 (written every batch)
+  double* xslots = nullptr;    // [n_slots][slot_doubles]
+  uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
+  double* xtw = nullptr;       // the transforms' twiddle tables (real, then complex)
+  int64_t slot_doubles = 0;
+  int n_slots = 0;
+  ExactFft xfft{};
   int64_t scratch_bytes = 0;
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
@@ -357,7 +367,8 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->cmp, (void*)pl->words, pl->d_x,
-                  (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync})
+                  (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags,
+                  (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xtw})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -376,9 +387,18 @@ hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which) {
 // F1 for the nb streams s0 .. s0 + nb - 1 of the batch: x (nb rows,
 // x_stride apart) -> z's blocks of those streams.  Caller holds mu.
 int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t nb, int64_t x_stride, int64_t s0,
-               double* scratch) {
-  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, nb, scratch, pl->z + (size_t)s0 * pl->p.n, pl->p, pl->f,
+               double* scratch, bool exact = true) {
+  FskParams p = pl->p;
+  const bool ex = exact && pl->exact_on;
+  if (ex && s0 % 32 != 0) return fail(AMR_E_INVALID, "F1 launch not on a 32-stream boundary");
+  p.xflags = ex ? pl->xflags + s0 / 32 : nullptr;    // s0: a multiple of 32 (live_stage_chunk)
+  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, nb, scratch, pl->z + (size_t)s0 * pl->p.n, p, pl->f,
                               pl->stream));
+  // the flagged streams of this launch, while their input is still at hand
+  // (the host entries stage it in C, which the column pass overwrites)
+  if (ex)
+    HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, s0, nb, pl->xflags + s0 / 32, pl->xslots, pl->slot_doubles, pl->n_slots,
+                             pl->xbits, pl->p, pl->f, pl->xfft, pl->stream));
   return AMR_OK;
 }
 
@@ -406,7 +426,7 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
 // F1, F2 on a device-resident batch: x -> cmp (or the envelopes).  Caller holds mu.
 int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
-  if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, 0, reinterpret_cast<double*>(pl->u))) return rc;
+  if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, 0, reinterpret_cast<double*>(pl->u), !env_out)) return rc;
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
   return run_fsk_f2(pl, B, env_out);
 }
@@ -558,11 +578,124 @@ LiveCols plan_live_cols(const FftShape& f, const FskParams& p) {
 // Sizes of an FSK plan's device buffers from its shape alone (no device
 // work): amr_fsk_plan_create allocates exactly these; amr_fsk_plan_bytes_estimate
 // sums them for the drop-in plan cache before it creates a plan.
+// ---- the exact fallback's transform plan (fsk_exact.h): pocketfft's
+// factorisations of n and its sincos_2pibyn twiddles, exactly as
+// oracle/amr_hilbert.c restates them (that file pins them against scipy)
+struct Twid2pi {
+  int64_t n = 0, mask = 0, shift = 0;
+  std::vector<double2> v1, v2;
+  static double2 calc(int64_t x, int64_t n, double ang) {
+    x <<= 3;
+    if (x < 4 * n) {
+      if (x < 2 * n) {
+        if (x < n) return make_double2(std::cos((double)x * ang), std::sin((double)x * ang));
+        return make_double2(std::sin((double)(2 * n - x) * ang), std::cos((double)(2 * n - x) * ang));
+      }
+      x -= 2 * n;
+      if (x < n) return make_double2(-std::sin((double)x * ang), std::cos((double)x * ang));
+      return make_double2(-std::cos((double)(2 * n - x) * ang), std::sin((double)(2 * n - x) * ang));
+    }
+    x = 8 * n - x;
+    if (x < 2 * n) {
+      if (x < n) return make_double2(std::cos((double)x * ang), -std::sin((double)x * ang));
+      return make_double2(std::sin((double)(2 * n - x) * ang), -std::cos((double)(2 * n - x) * ang));
+    }
+    x -= 2 * n;
+    if (x < n) return make_double2(-std::sin((double)x * ang), -std::cos((double)x * ang));
+    return make_double2(-std::cos((double)(2 * n - x) * ang), -std::sin((double)(2 * n - x) * ang));
+  }
+  explicit Twid2pi(int64_t len) : n(len) {
+    const double ang = (double)(0.25L * 3.141592653589793238462643383279502884197L / (long double)len);
+    const int64_t nval = (len + 2) / 2;
+    shift = 1;
+    while (((int64_t)1 << shift) * ((int64_t)1 << shift) < nval) ++shift;
+    mask = ((int64_t)1 << shift) - 1;
+    v1.resize((size_t)(mask + 1));
+    v1[0] = make_double2(1.0, 0.0);
+    for (int64_t i = 1; i <= mask; ++i) v1[(size_t)i] = calc(i, len, ang);
+    v2.resize((size_t)((nval + mask) / (mask + 1)));
+    v2[0] = make_double2(1.0, 0.0);
+    for (size_t i = 1; i < v2.size(); ++i) v2[i] = calc((int64_t)i * (mask + 1), len, ang);
+  }
+  double2 operator[](int64_t idx) const {
+    const bool hi = 2 * idx > n;
+    if (hi) idx = n - idx;
+    const double2 a = v1[(size_t)(idx & mask)], b = v2[(size_t)(idx >> shift)];
+    const double re = a.x * b.x - a.y * b.y, im = a.x * b.y + a.y * b.x;
+    return make_double2(re, hi ? -im : im);
+  }
+};
+
+int exact_factorize(int64_t n, bool with8, int* f) {
+  int nf = 0;
+  if (with8)
+    while (n % 8 == 0) { f[nf++] = 8; n /= 8; }
+  while (n % 4 == 0) { f[nf++] = 4; n /= 4; }
+  if (n % 2 == 0) { n /= 2; f[nf++] = 2; std::swap(f[0], f[nf - 1]); }
+  for (int64_t d = 3; d * d <= n; d += 2)
+    while (n % d == 0) { f[nf++] = (int)d; n /= d; }
+  if (n > 1) f[nf++] = (int)n;
+  for (int k = 0; k < nf; ++k)
+    if ((f[k] > 5 && f[k] != 8) || nf > kExactMaxFactors - 1) return -1;
+  return nf;
+}
+
+// tables into tw (real twiddles, then the complex ones from an even offset)
+bool build_exact_fft(int64_t n, std::vector<double>& tw, ExactFft& X) {
+  int fr[kExactMaxFactors], fc[kExactMaxFactors];
+  const int nr = exact_factorize(n, false, fr), nc = exact_factorize(n, true, fc);
+  if (nr < 1 || nc < 1) return false;
+  const Twid2pi T(n);
+  X = ExactFft{};
+  X.n = n;
+  X.nr = nr;
+  X.nc = nc;
+  tw.clear();
+  int64_t l1 = 1;
+  for (int k = 0; k < nr; ++k) {
+    const int64_t ip = fr[k], ido = n / (l1 * ip);
+    X.fr[k] = (int)ip;
+    X.rto[k] = (int64_t)tw.size();
+    std::vector<double> t((size_t)((ip - 1) * (ido - 1)), 0.0);
+    if (k < nr - 1)
+      for (int64_t j = 1; j < ip; ++j)
+        for (int64_t i = 1; i <= (ido - 1) / 2; ++i) {
+          const double2 w = T[j * l1 * i];
+          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 2)] = w.x;
+          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 1)] = w.y;
+        }
+    tw.insert(tw.end(), t.begin(), t.end());
+    l1 *= ip;
+  }
+  if (tw.size() & 1) tw.push_back(0.0);
+  const int64_t cbase = (int64_t)tw.size() / 2;      // in complex units
+  l1 = 1;
+  for (int k = 0; k < nc; ++k) {
+    const int64_t ip = fc[k], ido = n / (l1 * ip);
+    X.fc[k] = (int)ip;
+    X.cto[k] = (int64_t)tw.size() / 2 - cbase;
+    for (int64_t j = 1; j < ip; ++j)
+      for (int64_t i = 1; i < ido; ++i) {
+        const double2 w = T[j * l1 * i];
+        tw.push_back(w.x);
+        tw.push_back(w.y);
+      }
+    l1 *= ip;
+  }
+  X.fct = (double)(1.0L / (long double)n);
+  X.rto[kExactMaxFactors - 1] = cbase;              // where the complex tables start (doubles / 2)
+  return true;
+}
+
 struct FskGeom {
   FskParams p{};
   FftShape sh;
   int64_t z = 0, u = 0, v = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
-  int64_t total() const { return z + u + v + cmp + words + six + staging + out; }
+  // the exact fallback: flags, list, slots, exact bits, tables
+  bool exact = false;
+  int n_slots = 0;
+  int64_t slot_doubles = 0, xflags = 0, xslots = 0, xbits = 0, xtw = 0;
+  int64_t total() const { return z + u + v + cmp + words + six + staging + out + xflags + xslots + xbits + xtw; }
 };
 bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& g) {
   FskParams& p = g.p;
@@ -601,6 +734,22 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
   g.out = max_streams * (g.out_cap + 16);            // host-API output staging
+  // the exact fallback (AMR_FSK_EXACT=0: off): four-step lengths with pocketfft
+  // factors 2..5 (and 8), decisions to make
+  static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
+  int ftmp[kExactMaxFactors];
+  g.exact = exact_env && !g.sh.bluestein && !g.sh.six && p.n_bits > 0 && exact_factorize(n, false, ftmp) > 0 &&
+            exact_factorize(n, true, ftmp) > 0;
+  if (g.exact) {
+    const int64_t m = n + 2 * (int64_t)p.pad;
+    g.slot_doubles = 2 * m + 8 * n;
+    // one workgroup per slot: up to 128, within 1 GiB of slots
+    g.n_slots = (int)std::max<int64_t>(1, std::min<int64_t>({max_streams, 128, ((int64_t)1 << 30) / (g.slot_doubles * 8)}));
+    g.xflags = (max_streams + 31) / 32 * 4;
+    g.xslots = (int64_t)g.n_slots * g.slot_doubles * 8;
+    g.xbits = max_streams * p.bits_stride;
+    g.xtw = (6 * n + 64) * 8;
+  }
   return true;
 }
 
@@ -671,6 +820,10 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       {(void**)&pl->v, geo.v},
       {(void**)&pl->cmp, geo.cmp},
       {(void**)&pl->words, geo.words},
+      {(void**)&pl->xflags, geo.xflags},
+      {(void**)&pl->xslots, geo.xslots},
+      {(void**)&pl->xbits, geo.xbits},
+      {(void**)&pl->xtw, geo.xtw},
   };
   for (const A& a : allocs) {
     if (a.bytes == 0) continue;
@@ -680,6 +833,24 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       return fail(AMR_E_NOMEM, "hipMalloc(" + std::to_string(a.bytes) + " B): " + hipGetErrorString(e));
     }
     pl->scratch_bytes += a.bytes;
+  }
+  if (geo.exact) {
+    std::vector<double> tw;
+    if (build_exact_fft(n, tw, pl->xfft) && (int64_t)tw.size() * 8 <= geo.xtw) {
+      e = hipMemcpy(pl->xtw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMemset(pl->xflags, 0, (size_t)geo.xflags);
+      if (e != hipSuccess) {
+        fsk_plan_free(pl);
+        return fail(AMR_E_HIP, std::string("exact tables: ") + hipGetErrorString(e));
+      }
+      pl->xfft.rtw = pl->xtw;
+      pl->xfft.ctw = reinterpret_cast<const double2*>(pl->xtw) + pl->xfft.rto[kExactMaxFactors - 1];
+      pl->exact_on = true;
+      pl->p.xflags = pl->xflags;         // F3 reads a flagged stream's bits from xbits
+      pl->p.xbits = pl->xbits;
+      pl->n_slots = geo.n_slots;
+      pl->slot_doubles = geo.slot_doubles;
+    }
   }
   *out = pl;
   return AMR_OK;

@@ -250,7 +250,35 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-template <typename T, bool ZO, bool LIVE, bool W1S>
+// digital silence, for the exact fallback (fsk_exact_kernels.hip): there
+// the band-pass output decays to the FFT's rounding floor and only
+// pocketfft's own rounding decides.  That takes >= ~130 silent samples next
+// to signal (r^j < 1e-15 for the slowest band-pass pole r over every valid
+// rate / baud / tone: min j = 129), so F1 samples one
+// input value in 16 (|x| < 2^-60, integer work on the raw bits: float/double
+// sign-cleared against 2^-60's, int16 == 0) and flags a stream when
+// kExactRun / 16 consecutive samples are tiny: every silent run of >= 79
+// samples is flagged (a superset; quiet int16 input can be flagged too,
+// which only costs time).
+constexpr int kExactRun = 64;
+constexpr int kExactStride = 16;
+template <typename T> struct Tiny;
+template <> struct Tiny<float> {
+  static constexpr unsigned kLim = 0x21800000u;        // 2^-60 as float bits
+  static __device__ bool first(v4u v) { return (v.x & 0x7fffffffu) < kLim; }
+  static __device__ bool one(float x) { return (__float_as_uint(x) & 0x7fffffffu) < kLim; }
+};
+template <> struct Tiny<double> {
+  static constexpr unsigned kLim = 0x3C300000u;        // 2^-60's high word
+  static __device__ bool first(v4u v) { return (v.y & 0x7fffffffu) < kLim; }
+  static __device__ bool one(double x) { return ((unsigned)(__double_as_longlong(x) >> 32) & 0x7fffffffu) < kLim; }
+};
+template <> struct Tiny<int16_t> {
+  static __device__ bool first(v4u v) { return (v.x & 0xffffu) == 0u; }
+  static __device__ bool one(int16_t x) { return x == 0; }
+};
+
+template <typename T, bool ZO, bool LIVE, bool W1S, bool DET = false>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -302,15 +330,27 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 #pragma unroll
     for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][RPI * i + rsub][cb]) = r[i];
   };
-  auto run_tile = [&](auto emit) {
+  int srun = 0;                    // DET: current run of near-zero input samples
+  bool silent = false;
+  auto detect = [&](bool tiny, int k) {
+    if constexpr (DET) {
+      srun = tiny ? srun + k : 0;
+      silent = silent || srun >= kExactRun;
+    }
+  };
+  auto run_tile = [&](auto emit, bool det) {
     constexpr int PER = 16 / (int)sizeof(T);
 #pragma unroll
     for (int k = 0; k < TL; k += PER) {
       const v4u v = *reinterpret_cast<const v4u*>(&tin[0][sl][k * sizeof(T)]);
+      if (DET && det && k % kExactStride == 0) detect(Tiny<T>::first(v), kExactStride);
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
-      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step<ZO>(zs, b, a, FIn<T>::cvt(xs[u])));
+      for (int u = 0; u < PER; ++u) {
+        const double xv = FIn<T>::cvt(xs[u]);
+        emit(k + u, fsk_step<ZO>(zs, b, a, xv));
+      }
     }
   };
   if (role == 0) {
@@ -329,7 +369,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 6; ++i) ck[((size_t)t * 6 + i) * 64] = zs[i];
-        run_tile([](int, double) {});
+        run_tile([](int, double) {}, true);
         __builtin_amdgcn_sched_barrier(0);
       };
       int64_t t = 0;
@@ -340,7 +380,25 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       if (t < n_tiles) fwd(r0, t);
     }
     // the tail's forward outputs -> yb rows 0..ntail-1 (flat), the last -> ylast
-    for (int64_t i = n_main; i < n; ++i) (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
+    for (int64_t i = n_main; i < n; ++i) {
+      const T xi = x[i];
+      detect(Tiny<T>::one(xi), 1);
+      const double xv = FIn<T>::cvt(xi);
+      (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step<ZO>(zs, b, a, xv);
+    }
+    if constexpr (DET)
+      {
+        // the group's 32 streams, one word (written for every group, every
+        // batch): tone-0 lanes are the even ones -- compress the even bits
+        uint64_t v = __ballot(silent && tone == 0 && s < n_streams);
+        v &= 0x5555555555555555ull;
+        v = (v | (v >> 1)) & 0x3333333333333333ull;
+        v = (v | (v >> 2)) & 0x0f0f0f0f0f0f0f0full;
+        v = (v | (v >> 4)) & 0x00ff00ff00ff00ffull;
+        v = (v | (v >> 8)) & 0x0000ffff0000ffffull;
+        v = (v | (v >> 16)) & 0x00000000ffffffffull;
+        if (lane == 0) p.xflags[w] = (uint32_t)v;
+      }
     double yl = 0.0;
     for (int j = 0; j < pad; ++j) {
       yl = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
@@ -405,7 +463,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
         ldck(c, t - 2);
         __builtin_amdgcn_sched_barrier(0);
         double (*dst)[YP] = &yb[(it & 1) * TL];
-        run_tile([&](int k, double y) { dst[k][lane] = y; });
+        run_tile([&](int k, double y) { dst[k][lane] = y; }, false);
       }
       __syncthreads();
     };
@@ -446,7 +504,9 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
                                                                FskParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_bits[];
   const int64_t s = blockIdx.x;
-  const uint8_t* __restrict__ c = bits + (size_t)s * p.bits_stride;
+  // a stream the exact fallback recomputed: its bits from there (fsk_exact_kernels.hip)
+  const bool exact = p.xflags && ((p.xflags[s >> 5] >> (s & 31)) & 1u);
+  const uint8_t* __restrict__ c = (exact ? p.xbits : bits) + (size_t)s * p.bits_stride;
   const uint8_t* __restrict__ sb = c;
   if constexpr (LDS) {
     const int nb = (int)p.bits_stride;
@@ -515,15 +575,21 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
   if (!fsk_one_wave()) {
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
-#define BP2(T, S) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
+#define BP2(T, S, D) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
+#define BP2D(T) do { if (p.xflags) { if (w1s) BP2(T, true, true); else BP2(T, false, true); } else if (w1s) BP2(T, true, false); else BP2(T, false, false); } while (0)
     switch (dtype) {
-      case kF32: if (w1s) BP2(float, true); else BP2(float, false); break;
-      case kF64: if (w1s) BP2(double, true); else BP2(double, false); break;
-      case kI16: if (w1s) BP2(int16_t, true); else BP2(int16_t, false); break;
+      case kF32: BP2D(float); break;
+      case kF64: BP2D(double); break;
+      case kI16: BP2D(int16_t); break;
       default: return hipErrorInvalidValue;
     }
+#undef BP2D
 #undef BP2
     return hipGetLastError();
+  }
+  if (p.xflags) {      // the one-wave form does not look for silence: nothing flagged
+    const hipError_t e = hipMemsetAsync(p.xflags, 0, (size_t)(n_streams + 31) / 32 * 4, st);
+    if (e != hipSuccess) return e;
   }
   switch (dtype) {
     case kF32: hipLaunchKernelGGL((k_fsk_bandpass<float, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;

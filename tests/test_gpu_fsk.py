@@ -227,6 +227,47 @@ def test_fsk_digital_silence_flips_only_where_ambiguous():
     assert amb_total > 0          # the case exists: silent stretches were generated
 
 
+def _silence_batch(rng, B, n, baud, mark, space, dtype):
+    import synth
+    rows = []
+    for i in range(B):
+        w = synth.fsk_waveform(synth.random_frame(rng, int(rng.integers(4, 30))), baud, mark, space, 96000.0)
+        off = (0, 150, int(rng.integers(0, n // 3)), int(rng.integers(80, 300)))[i % 4]   # short silences too
+        row = np.zeros(n)
+        seg = w[:max(0, n - off)]
+        row[off:off + seg.size] = seg
+        if i % 5 == 4:
+            row[off + seg.size // 2:off + seg.size // 2 + 700] = 0.0     # a gap inside the frame
+        rows.append(row)
+    x = np.stack(rows)
+    return np.round(np.clip(x, -1, 1) * 32767).astype(np.int16) if dtype == np.int16 else x.astype(dtype)
+
+
+@pytest.mark.parametrize("n,baud,mark,space,dtype", [
+    (30000, 2400, 11229.28, 29833.37, np.float64),
+    (24000, 4800, 7000.0, 19000.0, np.float32),
+    (19200, 9600, 12000.0, 24000.0, np.int16),
+    (96000, 9600, 12000.0, 24000.0, np.float32),     # live columns
+    (96000, 1200, 2400.0, 4800.0, np.float64),
+])
+def test_fsk_digital_silence_exact(n, baud, mark, space, dtype):
+    """Digital silence next to signal on a 5-smooth length: F1 flags the
+    stream and the exact fallback (fsk_exact_kernels.hip) recomputes its
+    compare bits in scipy's and pocketfft's own operation order -- bytes and
+    sync equal to the oracle's (whose Hilbert restatement is pinned against
+    scipy, tests/test_oracle_golden.py) on every stream, silent or not."""
+    import _fsk
+    from oracle import oracle
+    rng = np.random.default_rng(n + baud)
+    B = 12
+    x = _silence_batch(rng, B, n, baud, mark, space, dtype)
+    pl = _fsk.FskPlan(n, baud, mark, space, max_streams=B)
+    got, _ = pl.demod_host(x)
+    want = [oracle.fsk_demodulate(x[i], baud, mark, space) for i in range(B)]
+    mism = [i for i in range(B) if got[i] != want[i]]
+    assert not mism, f"{len(mism)} of {B} streams differ, first {mism[:5]}"
+
+
 def test_fsk_timing_hooks():
     import _fsk
     import synth

@@ -132,15 +132,13 @@ def test_reference_sweep_through_the_drop_in(sweep_golden):
     """The drop-in modules (modem.qpsk_demodulate / bpsk_demodulate /
     fsk_demodulate on the GPU) against the REFERENCE's own outputs on the 72
     seeded configurations of tests/golden/make_sweep_golden.py: bytes or
-    exception text equal, every case (the 12 FSK cases inside exact digital
-    silence are the oracle's alone)."""
+    exception text equal, every case -- the 12 FSK cases inside exact digital
+    silence too, through the exact fallback."""
     import modem
     from _util import call_sweep_case, expected, outcome
     manifest, inputs = sweep_golden
     bad = []
     for c in manifest["cases"]:
-        if c["params"].get("silence"):
-            continue      # FSK inside exact digital silence: DESIGN.md §2 item 6 (the oracle matches these)
         got = outcome(lambda: call_sweep_case(modem, c, inputs[c["id"]]))
         if got != expected(c):
             bad.append((c["id"], c["fn"], c["params"], c["dtype"], c["n"], got[0]))
