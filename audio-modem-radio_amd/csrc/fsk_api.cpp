@@ -344,6 +344,7 @@ struct amr_fsk_plan {
   uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
   double* xtw = nullptr;       // the transforms' twiddle tables (real, then complex)
   int64_t slot_doubles = 0;
+  int x_group = 1;             // streams per exact-fallback workgroup and round (<= 4)
   int n_slots = 0;
   ExactFft xfft{};
   int64_t scratch_bytes = 0;
@@ -397,8 +398,8 @@ int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t nb, int64_t
   // the flagged streams of this launch, while their input is still at hand
   // (the host entries stage it in C, which the column pass overwrites)
   if (ex)
-    HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, s0, nb, pl->xflags + s0 / 32, pl->xslots, pl->slot_doubles, pl->n_slots,
-                             pl->xbits, pl->p, pl->f, pl->xfft, pl->stream));
+    HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, s0, nb, pl->xflags + s0 / 32, pl->x_group, pl->xslots,
+                             pl->slot_doubles, pl->n_slots, pl->xbits, pl->p, pl->f, pl->xfft, pl->stream));
   return AMR_OK;
 }
 
@@ -694,6 +695,7 @@ struct FskGeom {
   // the exact fallback: flags, list, slots, exact bits, tables
   bool exact = false;
   int n_slots = 0;
+  int x_group = 1;
   int64_t slot_doubles = 0, xflags = 0, xslots = 0, xbits = 0, xtw = 0;
   int64_t total() const { return z + u + v + cmp + words + six + staging + out + xflags + xslots + xbits + xtw; }
 };
@@ -742,7 +744,10 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
             exact_factorize(n, true, ftmp) > 0;
   if (g.exact) {
     const int64_t m = n + 2 * (int64_t)p.pad;
-    g.slot_doubles = 2 * m + 8 * n;
+    // streams per workgroup and round: up to 4 (the envelopes run one stream
+    // at a time, so workgroups beat grouping), a slot within 1 GiB
+    g.x_group = (int)std::max<int64_t>(1, std::min<int64_t>({max_streams, 4, (((int64_t)1 << 27) - 8 * n) / (2 * m)}));
+    g.slot_doubles = 8 * n + (int64_t)g.x_group * 2 * m;
     // one workgroup per slot: up to 128, within 1 GiB of slots
     g.n_slots = (int)std::max<int64_t>(1, std::min<int64_t>({max_streams, 128, ((int64_t)1 << 30) / (g.slot_doubles * 8)}));
     g.xflags = (max_streams + 31) / 32 * 4;
@@ -850,6 +855,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       pl->p.xbits = pl->xbits;
       pl->n_slots = geo.n_slots;
       pl->slot_doubles = geo.slot_doubles;
+      pl->x_group = geo.x_group;
     }
   }
   *out = pl;

@@ -26,7 +26,7 @@ struct ExactFft {
 // multiple of 32; x: its rows) -> their exact compare bits in xbits (the
 // batch's), which F3 reads
 hipError_t launch_fsk_exact(int dtype, const void* x, int64_t x_stride, int64_t s0, int64_t nb, const uint32_t* flags,
-                            double* slots, int64_t slot_doubles, int n_slots, uint8_t* xbits, const FskParams& p,
+                            int group, double* slots, int64_t slot_doubles, int n_slots, uint8_t* xbits, const FskParams& p,
                             const FskIir& f, const ExactFft& X, hipStream_t st);
 
 }  // namespace amr

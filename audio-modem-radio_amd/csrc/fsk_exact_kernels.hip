@@ -46,14 +46,35 @@ template <> struct XIn<int16_t> {
 };
 
 // ---- the serial filtfilt, scipy's order (one lane per tone) ----------------
+// y (m samples, step +-1, in global scratch) is filtered in place.  Blocks of
+// kDfBlock samples: the next block's loads are issued before this block's
+// recursion, so the serial chain waits on FP64 latency, not on memory.
+constexpr int kDfBlock = 16;
+__device__ __forceinline__ double df2t_step(const double* b, const double* a, double* z, double xn) {
+  const double yn = z[0] + b[0] * xn;
+  for (int i = 0; i < 5; ++i) z[i] = z[i + 1] + xn * b[i + 1] - yn * a[i + 1];
+  z[5] = xn * b[6] - yn * a[6];
+  return yn;
+}
 __device__ void df2t_exact(const double* b, const double* a, double* z, double* y, int64_t m, int64_t step) {
-  for (int64_t k = 0; k < m; ++k) {
-    const double xn = y[k * step];
-    const double yn = z[0] + b[0] * xn;
-    for (int i = 0; i < 5; ++i) z[i] = z[i + 1] + xn * b[i + 1] - yn * a[i + 1];
-    z[5] = xn * b[6] - yn * a[6];
-    y[k * step] = yn;
+  const int64_t nblk = m / kDfBlock;
+  double cur[kDfBlock], nxt[kDfBlock];
+  if (nblk > 0)
+#pragma unroll
+    for (int j = 0; j < kDfBlock; ++j) cur[j] = y[j * step];
+  for (int64_t blk = 0; blk < nblk; ++blk) {
+    const int64_t k0 = blk * kDfBlock;
+    if (blk + 1 < nblk)
+#pragma unroll
+      for (int j = 0; j < kDfBlock; ++j) nxt[j] = y[(k0 + kDfBlock + j) * step];
+#pragma unroll
+    for (int j = 0; j < kDfBlock; ++j) cur[j] = df2t_step(b, a, z, cur[j]);
+#pragma unroll
+    for (int j = 0; j < kDfBlock; ++j) y[(k0 + j) * step] = cur[j];
+#pragma unroll
+    for (int j = 0; j < kDfBlock; ++j) cur[j] = nxt[j];
   }
+  for (int64_t k = nblk * kDfBlock; k < m; ++k) y[k * step] = df2t_step(b, a, z, y[k * step]);
 }
 
 // ---- pocketfft passes over global scratch, spread across the workgroup ----
@@ -394,42 +415,87 @@ __device__ void exact_env(const ExactFft& X, const double* f, double* r1, double
   __syncthreads();
 }
 
-// The flagged streams of this launch's [s0, s0 + nb), the k-th (in stream
-// order) by workgroup k mod gridDim (slot = blockIdx.x): exact filtfilt of
-// both tones, exact envelopes, compare bits in the final pass's byte layout
-// -> xbits.
+constexpr int kExactThreads = 512;    // the envelope passes are latency-bound: 8 waves in flight
+
+// The flagged streams of this launch's [s0, s0 + nb), in groups of G <= group
+// per workgroup and round (G = the flagged count spread over the grid): the
+// group's odd extensions, then its filtfilts one lane per (stream, tone) in
+// wave 0 (the serial recursion is instruction-issue bound, so 64 lanes cost
+// what 2 do), then per stream the exact envelopes with the whole workgroup
+// and the compare bits in the final pass's byte layout -> xbits.
+// Slot (blockIdx.x): r1, r2 (n), c1, c2 (n complex), e0, e1 (n), y[group][2][m].
 template <typename T>
-__global__ __launch_bounds__(256) void k_fsk_exact(const void* xv, int64_t x_stride, int64_t s0, int64_t nb,
-                                                   const uint32_t* __restrict__ flags,
+__global__ __launch_bounds__(kExactThreads) void k_fsk_exact(const void* xv, int64_t x_stride, int64_t s0, int64_t nb,
+                                                   const uint32_t* __restrict__ flags, int group,
                                                    double* __restrict__ slots, int64_t slot_doubles,
                                                    uint8_t* __restrict__ xbits, FskParams p, FskIir f, ExactFft X) {
   const int64_t n = p.n;
   const int pad = p.pad;
   const int64_t m = n + 2 * (int64_t)pad;
   double* sl = slots + (size_t)blockIdx.x * slot_doubles;
-  double* y0 = sl;                 // [2][m] extended signal / filter outputs, per tone
-  double* r1 = sl + 2 * m;
+  double* r1 = sl;
   double* r2 = r1 + n;
   Cx* c1 = reinterpret_cast<Cx*>(r2 + n);
   Cx* c2 = c1 + n;
   double* e0 = reinterpret_cast<double*>(c2 + n);
   double* e1 = e0 + n;
-  auto process = [&](int64_t sl_) {
-    const int64_t s = s0 + sl_;
-    const T* x = reinterpret_cast<const T*>(xv) + (size_t)(s - s0) * x_stride;
-    // the odd extension, in the input's precision (numpy's odd_ext)
-    for (int64_t j = threadIdx.x; j < m; j += blockDim.x) {
-      double v;
-      if (j >= pad && j < pad + n) v = XIn<T>::cvt(x, j - pad);
-      else if (j < pad) v = XIn<T>::ext(x, 0, pad - j);
-      else v = XIn<T>::ext(x, n - 1, n - 2 - (j - pad - n));
-      y0[j] = v;
-      y0[m + j] = v;
+  double* yall = e1 + n;           // [group][2][m] extended signal / filter outputs
+  __shared__ uint32_t words_sh[kExactThreads];
+  __shared__ int32_t sel_sh[32];
+  __shared__ int64_t total_sh;
+  __shared__ int nsel_sh;
+  const int64_t nw = (nb + 31) / 32;
+  if (threadIdx.x == 0) total_sh = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < nw; i += blockDim.x) {
+    const uint32_t wd = flags[i];
+    if (wd) atomicAdd(reinterpret_cast<unsigned long long*>(&total_sh), (unsigned long long)__popc(wd));
+  }
+  __syncthreads();
+  const int64_t total = total_sh;
+  if (total == 0) return;
+  const int64_t G = min((int64_t)group, (total + gridDim.x - 1) / gridDim.x);
+  for (int64_t lo = (int64_t)blockIdx.x * G; lo < total; lo += (int64_t)gridDim.x * G) {
+    const int64_t hi = min(lo + G, total);
+    // the flagged streams of ordinals [lo, hi) -> sel_sh (thread 0 walks the words)
+    int64_t seen = 0;
+    if (threadIdx.x == 0) nsel_sh = 0;
+    for (int64_t base = 0; base < nw; base += kExactThreads) {
+      __syncthreads();
+      words_sh[threadIdx.x] = base + threadIdx.x < nw ? flags[base + threadIdx.x] : 0u;
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int t = 0; t < kExactThreads && seen < hi; ++t) {
+          uint32_t mm = words_sh[t];
+          const int c = __popc(mm);
+          if (seen + c <= lo) { seen += c; continue; }
+          while (mm) {
+            const int bit = __builtin_ctz(mm);
+            mm &= mm - 1;
+            if (seen >= lo && seen < hi) sel_sh[nsel_sh++] = (int32_t)((base + t) * 32 + bit);
+            ++seen;
+          }
+        }
     }
     __syncthreads();
-    if (threadIdx.x < 2) {
-      const int tone = threadIdx.x;
-      double* y = y0 + (size_t)tone * m;
+    const int gn = nsel_sh;
+    // the odd extensions, in the input's precision (numpy's odd_ext)
+    for (int g = 0; g < gn; ++g) {
+      const T* x = reinterpret_cast<const T*>(xv) + (size_t)sel_sh[g] * x_stride;
+      double* y0 = yall + (size_t)g * 2 * m;
+      for (int64_t j = threadIdx.x; j < m; j += blockDim.x) {
+        double v;
+        if (j >= pad && j < pad + n) v = XIn<T>::cvt(x, j - pad);
+        else if (j < pad) v = XIn<T>::ext(x, 0, pad - j);
+        else v = XIn<T>::ext(x, n - 1, n - 2 - (j - pad - n));
+        y0[j] = v;
+        y0[m + j] = v;
+      }
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < 2 * gn) {
+      const int tone = threadIdx.x & 1;
+      double* y = yall + (size_t)(threadIdx.x >> 1) * 2 * m + (size_t)tone * m;
       double b[7], a[7], z[6];
       for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
       for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * y[0];
@@ -438,55 +504,40 @@ __global__ __launch_bounds__(256) void k_fsk_exact(const void* xv, int64_t x_str
       df2t_exact(b, a, z, y + m - 1, m, -1);
     }
     __syncthreads();
-    exact_env(X, y0 + pad, r1, r2, c1, c2, e0);
-    exact_env(X, y0 + m + pad, r1, r2, c1, c2, e1);
-    // bits: byte (c0 / 8) * n2 + kk holds columns c0 .. c0 + 7 of row kk
-    // (column c -> sample col(c) + n1 * kk; col = the live columns or all)
-    const int ncol = p.lc.on ? p.lc.nl : (int)p.rn1;
-    const int64_t n2 = p.rn2, n1 = p.lc.on ? p.lc.n1 : p.rn1;
-    const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
-    uint8_t* ob = xbits + (size_t)s * p.bits_stride;
-    for (int64_t q = threadIdx.x; q < nbytes; q += blockDim.x) {
-      const int64_t cb = q / n2, kk = q - cb * n2;
-      unsigned byte = 0;
-      for (int t = 0; t < 8; ++t) {
-        const int c = (int)cb * 8 + t;
-        if (c >= ncol) break;
-        const int64_t col = p.lc.on ? lc_live_col(p.lc, c) : c;
-        const int64_t i = col + n1 * kk;
-        if (i < n && e0[i] > e1[i]) byte |= 1u << t;
+    for (int g = 0; g < gn; ++g) {
+      const double* y0 = yall + (size_t)g * 2 * m;
+      exact_env(X, y0 + pad, r1, r2, c1, c2, e0);
+      exact_env(X, y0 + m + pad, r1, r2, c1, c2, e1);
+      // bits: byte (c0 / 8) * n2 + kk holds columns c0 .. c0 + 7 of row kk
+      // (column c -> sample col(c) + n1 * kk; col = the live columns or all)
+      const int ncol = p.lc.on ? p.lc.nl : (int)p.rn1;
+      const int64_t n2 = p.rn2, n1 = p.lc.on ? p.lc.n1 : p.rn1;
+      const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
+      uint8_t* ob = xbits + (size_t)(s0 + sel_sh[g]) * p.bits_stride;
+      for (int64_t q = threadIdx.x; q < nbytes; q += blockDim.x) {
+        const int64_t cb = q / n2, kk = q - cb * n2;
+        unsigned byte = 0;
+        for (int t = 0; t < 8; ++t) {
+          const int c = (int)cb * 8 + t;
+          if (c >= ncol) break;
+          const int64_t col = p.lc.on ? lc_live_col(p.lc, c) : c;
+          const int64_t i = col + n1 * kk;
+          if (i < n && e0[i] > e1[i]) byte |= 1u << t;
+        }
+        ob[q] = (uint8_t)byte;
       }
-      ob[q] = (uint8_t)byte;
-    }
-    __syncthreads();
-  };
-  __shared__ uint32_t words_sh[256];
-  const int64_t nw = (nb + 31) / 32;
-  int64_t seen = 0;                            // flagged streams before this chunk (uniform)
-  for (int64_t base = 0; base < nw; base += 256) {
-    const uint32_t fw = base + threadIdx.x < nw ? flags[base + threadIdx.x] : 0u;
-    __syncthreads();                           // the previous chunk's words are read
-    words_sh[threadIdx.x] = fw;
-    if (!__syncthreads_or(fw != 0u)) continue;
-    for (int t = 0; t < 256; ++t) {
-      uint32_t mm = words_sh[t];
-      while (mm) {
-        const int bit = __builtin_ctz(mm);
-        mm &= mm - 1;
-        if (seen++ % gridDim.x != blockIdx.x) continue;
-        process((base + t) * 32 + bit);
-      }
+      __syncthreads();
     }
   }
 }
 
 hipError_t launch_fsk_exact(int dtype, const void* x, int64_t x_stride, int64_t s0, int64_t nb, const uint32_t* flags,
-                            double* slots, int64_t slot_doubles, int n_slots, uint8_t* xbits,
+                            int group, double* slots, int64_t slot_doubles, int n_slots, uint8_t* xbits,
                             const FskParams& p, const FskIir& f, const ExactFft& X, hipStream_t st) {
   switch (dtype) {
-    case kF32: hipLaunchKernelGGL(k_fsk_exact<float>, dim3(n_slots), dim3(256), 0, st, x, x_stride, s0, nb, flags, slots, slot_doubles, xbits, p, f, X); break;
-    case kF64: hipLaunchKernelGGL(k_fsk_exact<double>, dim3(n_slots), dim3(256), 0, st, x, x_stride, s0, nb, flags, slots, slot_doubles, xbits, p, f, X); break;
-    case kI16: hipLaunchKernelGGL(k_fsk_exact<int16_t>, dim3(n_slots), dim3(256), 0, st, x, x_stride, s0, nb, flags, slots, slot_doubles, xbits, p, f, X); break;
+    case kF32: hipLaunchKernelGGL(k_fsk_exact<float>, dim3(n_slots), dim3(kExactThreads), 0, st, x, x_stride, s0, nb, flags, group, slots, slot_doubles, xbits, p, f, X); break;
+    case kF64: hipLaunchKernelGGL(k_fsk_exact<double>, dim3(n_slots), dim3(kExactThreads), 0, st, x, x_stride, s0, nb, flags, group, slots, slot_doubles, xbits, p, f, X); break;
+    case kI16: hipLaunchKernelGGL(k_fsk_exact<int16_t>, dim3(n_slots), dim3(kExactThreads), 0, st, x, x_stride, s0, nb, flags, group, slots, slot_doubles, xbits, p, f, X); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
