@@ -100,30 +100,82 @@ def test_oracle_matches_reference_sweep(sweep_golden):
     assert not bad, f"oracle differs from the reference on {bad}"
 
 
-def _smooth5(n):
-    for p in (2, 3, 5):
-        while n % p == 0:
-            n //= p
-    return n == 1
+def _host_numpy_is_modelled():
+    """The restatement models numpy's complex multiply (FMA) and complex abs
+    (AVX-512 hypot form) as the fixtures' host runs them; on a host whose
+    numpy dispatches differently the live-scipy comparisons are skipped
+    (the reference fixtures still pin the oracle)."""
+    if not oracle.numpy_complex_is_modelled():
+        pytest.skip("this host's numpy complex multiply / abs differ from the modelled AVX-512 kernels")
+
+
+def test_oracle_pocketfft_every_length():
+    """amr_pocketfft.c's scipy.fft.rfft / irfft / fft / ifft and
+    |scipy.signal.hilbert| equal scipy + numpy bit for bit on EVERY length
+    1..2000: FFTPACK-style plans of every radix (2, 3, 4, 5, 7, 8, 11 and the
+    generic pass) and the Bluestein plans pocketfft picks (488 real / 748
+    complex lengths in that range)."""
+    import scipy.fft as sf
+    from scipy import signal
+    _host_numpy_is_modelled()
+    rng = np.random.default_rng(11)
+    bad = []
+    for n in range(1, 2001):
+        x = rng.standard_normal(n)
+        if not np.array_equal(oracle.rfft(x).view(np.float64), sf.rfft(x).view(np.float64)):
+            bad.append(("rfft", n))
+        X = sf.rfft(rng.standard_normal(n))
+        if not np.array_equal(oracle.irfft(X, n), sf.irfft(X, n)):
+            bad.append(("irfft", n))
+        c = rng.standard_normal(n) + 1j * rng.standard_normal(n)
+        if not np.array_equal(oracle.cfft(c).view(np.float64), sf.fft(c).view(np.float64)):
+            bad.append(("fft", n))
+        if not np.array_equal(oracle.cfft(c, True).view(np.float64), sf.ifft(c).view(np.float64)):
+            bad.append(("ifft", n))
+        if not np.array_equal(oracle.hilbert_env(x), np.abs(signal.hilbert(x))):
+            bad.append(("hilbert", n))
+    assert not bad, bad[:20]
+    assert sum(oracle.pf_uses_bluestein(n, True) for n in range(1, 2001)) == 488
+    assert sum(oracle.pf_uses_bluestein(n, False) for n in range(1, 2001)) == 748
 
 
 def test_oracle_hilbert_is_scipys():
-    """The oracle's restatement of |scipy.signal.hilbert(x)| (amr_hilbert.c:
-    pocketfft's real forward and complex backward transforms, their twiddle
-    generator, scipy's h, numpy's AVX-512 complex abs) equals scipy + numpy
-    bit for bit, on every 5-smooth length up to 500 and the FSK lengths, for
-    noise and for signal between exact-zero stretches (where the envelopes
+    """The oracle's |scipy.signal.hilbert(x)| equals scipy + numpy bit for bit
+    on the FSK lengths -- 5-smooth four-step ones, Bluestein ones (24001,
+    30011, 96001, 400001) and a generic-radix one (77880 = 59 * 1320) -- for
+    noise, for signal between exact-zero stretches, next to a stretch 1e-17
+    below the signal and next to a constant (DC) stretch (where the envelopes
     are rounding noise -- DESIGN.md §2 item 6)."""
     from scipy import signal
+    _host_numpy_is_modelled()
     rng = np.random.default_rng(7)
-    sizes = [n for n in range(1, 500) if _smooth5(n)] + [960, 1920, 9600, 19200, 48000, 96000, 153600]
+    sizes = [960, 1920, 9600, 19200, 24001, 30011, 48000, 77880, 96000, 96001, 153600, 400001]
     bad = []
     for n in sizes:
-        for kind in ("noise", "silence"):
+        for kind in ("noise", "silence", "tiny", "dc"):
             x = rng.normal(size=n)
             if kind == "silence":
                 x[: n // 3] = 0.0
                 x[2 * n // 3:] = 0.0
+            elif kind == "tiny":
+                x[n // 4: n // 2] *= 1e-17
+            elif kind == "dc":
+                x[n // 2:] = -0.25
             if not np.array_equal(oracle.hilbert_env(x), np.abs(signal.hilbert(x))):
                 bad.append((n, kind))
+    assert not bad, bad
+
+
+def test_oracle_resample_is_scipys():
+    """oracle.resample == scipy.signal.resample bit for bit on the lengths
+    decode_wav_file produces (decoder.py:385-387: 44.1 / 48 / 22.05 / 8 kHz
+    captures to 96 kHz; 441000 = 2^3 3^2 5^3 7^2 runs the generic radix-7
+    pass) and on down-sampling, odd and Bluestein lengths."""
+    from scipy import signal
+    _host_numpy_is_modelled()
+    rng = np.random.default_rng(5)
+    cases = [(441000, 960000), (480000, 960000), (44100, 96000), (48000, 96000), (22050, 96000),
+             (8000, 96000), (100000, 96000), (77, 1000), (1000, 77), (24001, 52247), (1009, 2003)]
+    bad = [(nx, num) for nx, num in cases
+           if not np.array_equal(oracle.resample(x := rng.standard_normal(nx), num), signal.resample(x, num))]
     assert not bad, bad
