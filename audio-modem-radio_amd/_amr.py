@@ -26,7 +26,7 @@ AMR_E_INVALID, AMR_E_PADLEN, AMR_E_HIP, AMR_E_NOMEM, AMR_E_NODEVICE, AMR_E_RCCL,
 DTYPE_F32, DTYPE_F64, DTYPE_I16 = 0, 1, 2
 PSK_QPSK, PSK_BPSK = 0, 1
 T_NAMES = ["bandpass", "lowpass_fwd", "lowpass_bwd", "lowpass_exact", "sync_pack", "fec", "launch"]
-TF_NAMES = ["bandpass", "hilbert", "decide", "launch"]
+TF_NAMES = ["bandpass", "hilbert", "decide", "launch", "exact"]
 # amr_frame_rec (include/amr.h), 64 bytes
 FRAME_SHORT, FRAME_NONAME, FRAME_NOMETA, FRAME_BADLEN, FRAME_INCOMPLETE, FRAME_CRC_BAD, FRAME_OK = range(7)
 FRAME_REC = np.dtype([("start", "<i8"), ("name_start", "<i8"), ("payload_start", "<i8"), ("status", "<i4"),
@@ -51,7 +51,8 @@ EXPORTS = [
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather", "amr_fsk_allgather",
     "amr_comm_synchronize", "amr_comm_allgather_host", "amr_comm_allreduce_max", "amr_comm_world", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
-    "amr_resample_host",
+    "amr_resample_host", "amr_hilbert_env_exact_host", "amr_fsk_plan_exact_streams",
+    "amr_fsk_plan_set_exact_mode",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -241,6 +242,9 @@ def lib():
             "amr_comm_world": (I32, [P, P, P]),
             "amr_tx_samples": (I64, [I32, I64, D, D]),
             "amr_resample_host": (I32, [P, I64, I64, I64, P, I32]),
+            "amr_hilbert_env_exact_host": (I32, [P, I64, I64, P, I32]),
+            "amr_fsk_plan_exact_streams": (I32, [P, P]),
+            "amr_fsk_plan_set_exact_mode": (I32, [P, I32]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
             "amr_modulate_host": (I32, [I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64]),
             "amr_modulate_device": (I32, [P, I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64, P, I64]),
@@ -464,7 +468,7 @@ class PlanCache:
 
 
 def _cache_budget() -> int:
-    return int(float(os.environ.get("AMR_PLAN_CACHE_BYTES", 48e9)))
+    return int(float(os.environ.get("AMR_PLAN_CACHE_BYTES", 64e9)))
 
 
 def stream_bucket(batch: int, cap: int) -> int:
@@ -475,7 +479,7 @@ def stream_bucket(batch: int, cap: int) -> int:
 
 
 # ONE plan cache for every demodulator (PSK and FSK plans, keyed by kind):
-# its byte budget (AMR_PLAN_CACHE_BYTES, default 48 GB, 1/6 of an MI355X's
+# its byte budget (AMR_PLAN_CACHE_BYTES, default 64 GB, 2/9 of an MI355X's
 # HBM) bounds all the drop-in path's device memory together.
 plan_cache = PlanCache(_cache_budget())
 PSK_MAX_CHUNK = 4096
@@ -534,9 +538,21 @@ def hilbert(x: np.ndarray) -> np.ndarray:
     return out
 
 
+def hilbert_env_exact(x: np.ndarray) -> np.ndarray:
+    """np.abs(scipy.signal.hilbert(x)) along the last axis of a real [batch][n]
+    array on the GPU, bit for bit (pocketfft's own transforms and numpy's
+    complex arithmetic restated -- the FSK exact path's envelope stage)."""
+    require_gpu()
+    x = np.array(np.atleast_2d(x), np.float64, copy=True, order="C")
+    out = np.empty_like(x)
+    check(lib().amr_hilbert_env_exact_host(ptr(x), x.shape[1], x.shape[0], ptr(out), default_device()))
+    return out
+
+
 def resample(x: np.ndarray, num: int) -> np.ndarray:
     """scipy.signal.resample(x, num) for real float64 input (1-D, or rows of a
-    2-D array resampled along the last axis) on the GPU -- the resample of
+    2-D array resampled along the last axis) on the GPU, bit for bit
+    (pocketfft's rfft / irfft restated) -- the resample of
     decoder.decode_wav_file (decoder.py:385-387)."""
     require_gpu()
     a = np.asarray(x)

@@ -114,6 +114,16 @@ class FskPlan:
     def enable_timing(self, on=True):
         check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
 
+    def set_exact_mode(self, mode: int):
+        """0 off, 1 the streams F2 flags (default), 2 every stream (include/amr.h)."""
+        check(lib().amr_fsk_plan_set_exact_mode(self.handle, int(mode)))
+
+    def exact_streams(self) -> int:
+        """Streams the exact path recomputed in the last call (F2 flagged them)."""
+        c = ctypes.c_int64(0)
+        check(lib().amr_fsk_plan_exact_streams(self.handle, ctypes.byref(c)))
+        return int(c.value)
+
     def timings(self) -> dict:
         ms = (ctypes.c_float * len(_amr.TF_NAMES))()
         check(lib().amr_fsk_plan_timings(self.handle, ms, len(_amr.TF_NAMES)))

@@ -127,10 +127,30 @@ struct FskParams {
   int64_t bits_stride;
   float inv_rn1;
   LiveCols lc;      // lc.on: z and the compare bits in the live-column layout
-  uint32_t* xflags; // non-null: F1 writes [B / 32] bit s = stream s has digital silence (the exact
-                    // fallback), F3 then reads that stream's compare bits from xbits
+  double* amb;       // non-null: F1 writes [B] each stream's ambiguity scale (amb_scale) and
+                    // clears xflags; F2's last pass sets bit s of xflags[s / 32] for a stream
+                    // with a compare inside the margin, F3 then reads its bits from xbits
+                    // (the exact path, fsk_exact_kernels.hip)
+  uint32_t* xflags;
   const uint8_t* xbits;
+  int force_exact;  // AMR_FSK_FORCE_EXACT=1 (tests): every stream's scale +inf, all go exact
 };
+
+// F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within
+// reach of the fast path's and pocketfft's rounding;
+// tau = 2^-36 ~ 1.5e-11, ~10^4 times the largest observed difference between
+// the fast path's envelopes and the reference's
+// (tests/test_gpu_fsk.py::test_envelope_error_is_far_below_the_margin)
+constexpr double kAmbTau = 0x1p-36;
+// c = 8 (tau peak)^2 (fft_kernels.hip env_ambiguous compares squares);
+// -1 for a stream of exact zeros (both paths' envelopes are exact zeros),
+// +inf for tiny / huge / non-finite input (every compare goes exact)
+__host__ __device__ inline double amb_scale(double peak) {
+  if (peak == 0.0) return -1.0;
+  if (!(peak >= 0x1p-400 && peak <= 0x1p400)) return __builtin_inf();
+  const double d = kAmbTau * peak;
+  return 8.0 * d * d;
+}
 
 struct FskIir {            // [tone][tap], tone 0 = mark
   double b[2][8];

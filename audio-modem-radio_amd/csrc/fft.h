@@ -74,6 +74,8 @@ struct FftEpi {
   uint8_t* bits;           // kEnvelope: [b][bits_stride] bytes
   int64_t bits_stride;
   const double2* tab;      // kMulTab
+  const double* amb;       // kEnvelope, optional: [b] the stream's ambiguity scale (amr_internal.h
+  uint32_t* xflags;        // amb_scale) -> bit b of xflags[b / 32] set on a compare inside the margin
 };
 
 // X = FFT_n(in) or IFFT_n(in) (inverse: conj on load, conj and 1/n on store).

@@ -303,6 +303,24 @@ __device__ __forceinline__ bool env_gt(double2 f, double2 v) {
   return hypot(f.x, v.x) > hypot(f.y, v.y);
 }
 
+// a compare the exact path must settle: |a_mark| and |a_space| closer than
+// 2 delta (delta = tau peak|x|, c = 8 delta^2 = amb_scale) -- as squares,
+// (m2 - s2)^2 <= c (m2 + s2) implies |.| - |.| <= 2 delta; c < 0: never,
+// c = inf or NaN envelopes: always.  Envelopes past 1e150 only occur with
+// c = inf (peak > 2^400), so the squares stay finite here.
+__device__ __forceinline__ bool env_ambiguous(double2 f, double2 v, double c) {
+  if (c < 0.0) return false;
+  const double m2 = __builtin_fma(f.x, f.x, v.x * v.x), s2 = __builtin_fma(f.y, f.y, v.y * v.y);
+  const double d = m2 - s2;
+  return !(d * d > c * (m2 + s2));
+}
+
+// one wave's ambiguity votes for stream b -> its flag bit (one atomic per wave that found one)
+__device__ __forceinline__ void flag_ambiguous(const FftEpi& e, int64_t b, bool amb) {
+  if (__ballot(amb) != 0 && (threadIdx.x & 63) == 0)
+    atomicOr(&e.xflags[b >> 5], 1u << (unsigned)(b & 31));
+}
+
 template <int MODE>
 __device__ __forceinline__ void fft_epilogue(const FftEpi& e, double2* __restrict__ dst, int64_t b, int64_t k,
                                              double2 v) {
@@ -440,6 +458,7 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
   // produces kk = m + P*p, p < Q)
   constexpr bool kPre = MODE == kEnvelope && QC > 0;
   double2 zp[kPre ? QC : 1];
+  const double ambc = (MODE == kEnvelope && e.amb) ? e.amb[b] : -1.0;
   if constexpr (kPre) {
     const int t = threadIdx.x & (kFftTile - 1), m = threadIdx.x / kFftTile;
     if (threadIdx.x < kFftTile * PC && t < nrow) {
@@ -459,12 +478,14 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
         const int kk = m + P * p;
         if constexpr (MODE == kEnvelope) {
           // 8 lanes (t = 0..7) of one kk -> one byte of compare bits
-          bool gt = false;
+          bool gt = false, amb = false;
           if (t < nrow) {
             v = make_double2(v.x * scale, -v.y * scale);
-            if constexpr (kPre) gt = env_gt(zp[p], v);
-            else gt = env_gt(e.z[(size_t)b * n + (unsigned)(r0 + t + nrow_all * kk)], v);
+            const double2 f = kPre ? zp[p] : e.z[(size_t)b * n + (unsigned)(r0 + t + nrow_all * kk)];
+            gt = env_gt(f, v);
+            if (e.amb) amb = env_ambiguous(f, v, ambc);
           }
+          if (e.amb) flag_ambiguous(e, b, amb);
           const uint64_t mask = __ballot(gt);
           if (t == 0) e.bits[(size_t)b * e.bits_stride + (size_t)(r0 >> 3) * L + kk] = (uint8_t)(mask >> (threadIdx.x & 56));
         } else if (t < nrow) {
@@ -635,6 +656,7 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows_live(const double2* __
   const double2* __restrict__ src = cb + (size_t)b * nl * d.n2 + l0;
   const double2* __restrict__ zl = zb + (size_t)b * d.n + l0;     // L: [k1'][l]
   double2* twl = twl_of(smem, f);
+  const double ambc = e.amb ? e.amb[b] : -1.0;
   constexpr bool kPre = QC > 0;
   double2 zp[kPre ? QC : 1];
   if constexpr (kPre) {
@@ -653,12 +675,14 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows_live(const double2* __
       f, twl, [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; },
       [&](int t, int m, int p, double2 v) {
         const int kk = m + P * p;
-        bool gt = false;
+        bool gt = false, amb = false;
         if (t < ncol) {
           v = make_double2(v.x * scale, -v.y * scale);
-          if constexpr (kPre) gt = env_gt(zp[p], v);
-          else gt = env_gt(zl[(unsigned)(t + nl * kk)], v);
+          const double2 f = kPre ? zp[p] : zl[(unsigned)(t + nl * kk)];
+          gt = env_gt(f, v);
+          if (e.amb) amb = env_ambiguous(f, v, ambc);
         }
+        if (e.amb) flag_ambiguous(e, b, amb);
         const uint64_t mask = __ballot(gt);
         if (t == 0) e.bits[(size_t)b * e.bits_stride + (size_t)(l0 >> 3) * L + kk] = (uint8_t)(mask >> (threadIdx.x & 56));
       });
@@ -704,14 +728,19 @@ __global__ __launch_bounds__(256) void k_bs_post_env(const double2* __restrict__
   if (i >= batch * nbytes) return;
   const int64_t b = i / nbytes, jb = i - b * nbytes;
   unsigned byte = 0;
+  bool amb = false;
+  const double ambc = e.amb ? e.amb[b] : -1.0;
   for (int u = 0; u < 8; ++u) {
     const int64_t k = jb * 8 + u;
     if (k >= n) break;
     double2 v = cmul(y[(size_t)b * M + k], conj2(w[k]));
     v = make_double2(v.x * scale, -v.y * scale);
-    byte |= (env_gt(e.z[(size_t)b * n + k], v) ? 1u : 0u) << u;
+    const double2 f = e.z[(size_t)b * n + k];
+    byte |= (env_gt(f, v) ? 1u : 0u) << u;
+    amb = amb || env_ambiguous(f, v, ambc);
   }
   e.bits[(size_t)b * e.bits_stride + jb] = (uint8_t)byte;
+  if (amb) atomicOr(&e.xflags[b >> 5], 1u << (unsigned)(b & 31));   // rows vary across the wave
 }
 
 static size_t fft_smem_bytes(const FftLen& f) { return ((size_t)kFftTile * f.S + f.L) * sizeof(double2); }

@@ -337,16 +337,19 @@ struct amr_fsk_plan {
   int64_t u_bytes = 0;
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
-  // the exact fallback for streams with digital silence (fsk_exact_kernels.hip)
+  // the exact path for streams with a compare inside F2's margin (fsk_exact_kernels.hip)
   bool exact_on = false;
-  uint32_t* xflags = nullptr;  // [B / 32] F1's digital-silence flags, bit s of word s / 32 (written every batch)
-  double* xslots = nullptr;    // [n_slots][slot_doubles]
+  uint32_t* xflags = nullptr;  // [B / 32] F2's flags, bit s of word s / 32 (cleared by F1 every batch)
+  double* amb = nullptr;       // [B] F1's ambiguity scale per stream
+  int32_t* xlist = nullptr;    // [B] flagged ordinal -> stream, then [1] the count
+  double* xslots = nullptr;    // [n_slots][slot_doubles] envelope scratch
   uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
-  double* xtw = nullptr;       // the transforms' twiddle tables (real, then complex)
+  double* xpool = nullptr;     // pocketfft's twiddle / chirp tables of length n
+  PfLen* xL = nullptr;         // pocketfft's plans of length n (device copy)
   int64_t slot_doubles = 0;
-  int x_group = 1;             // streams per exact-fallback workgroup and round (<= 4)
   int n_slots = 0;
-  ExactFft xfft{};
+  bool ran_exact = false;      // the last call ran the exact path (its count is in xlist[max_streams])
+  int exact_mode = 1;          // amr_fsk_plan_set_exact_mode: 0 off, 1 F2's flags, 2 every stream
   int64_t scratch_bytes = 0;
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
@@ -368,8 +371,8 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->cmp, (void*)pl->words, pl->d_x,
-                  (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags,
-                  (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xtw})
+                  (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
+                  (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -385,33 +388,31 @@ hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which) {
   return hipEventRecord(pl->ev[slot][which], pl->stream);
 }
 
-// F1 for the nb streams s0 .. s0 + nb - 1 of the batch: x (nb rows,
-// x_stride apart) -> z's blocks of those streams.  Caller holds mu.
-int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t nb, int64_t x_stride, int64_t s0,
-               double* scratch, bool exact = true) {
+// F1 over the B streams of x -> z (and, with the exact path on, each
+// stream's ambiguity scale; the flag words cleared).  Caller holds mu.
+int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool exact) {
   FskParams p = pl->p;
-  const bool ex = exact && pl->exact_on;
-  if (ex && s0 % 32 != 0) return fail(AMR_E_INVALID, "F1 launch not on a 32-stream boundary");
-  p.xflags = ex ? pl->xflags + s0 / 32 : nullptr;    // s0: a multiple of 32 (live_stage_chunk)
-  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, nb, scratch, pl->z + (size_t)s0 * pl->p.n, p, pl->f,
+  if (!(exact && pl->exact_on && pl->exact_mode != 0)) p.amb = nullptr;
+  p.force_exact = pl->exact_mode == 2 ? 1 : 0;
+  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p, pl->f,
                               pl->stream));
-  // the flagged streams of this launch, while their input is still at hand
-  // (the host entries stage it in C, which the column pass overwrites)
-  if (ex)
-    HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, s0, nb, pl->xflags + s0 / 32, pl->x_group, pl->xslots,
-                             pl->slot_doubles, pl->n_slots, pl->xbits, pl->p, pl->f, pl->xfft, pl->stream));
   return AMR_OK;
 }
 
 // F2 over the B streams of z: the Hilbert filter, whose last pass forms both
-// envelopes and packs the compare bits (or, env_out on a natural-layout
-// plan, stores the envelopes themselves in hilbert_out(u, v)).
+// envelopes, packs the compare bits and flags the streams with a compare
+// inside the margin (or, env_out on a natural-layout plan, stores the
+// envelopes themselves in hilbert_out(u, v)).
 int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   FftEpi env{};
   env.mode = env_out ? kEnvOut : kEnvelope;
   env.z = pl->z;
   env.bits = pl->cmp;
   env.bits_stride = pl->p.bits_stride;
+  if (!env_out && pl->exact_on && pl->exact_mode != 0) {
+    env.amb = pl->amb;
+    env.xflags = pl->xflags;
+  }
   // one timing slot for the whole Hilbert filter (column, middle and final passes)
   HIP_TRY(mark_fsk(pl, AMR_TF_HILBERT, 0));
   if (pl->p.lc.on) {
@@ -424,12 +425,36 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   return AMR_OK;
 }
 
-// F1, F2 on a device-resident batch: x -> cmp (or the envelopes).  Caller holds mu.
+// The exact path over F2's flagged streams (their input x still resident).
+int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride) {
+  if (!pl->exact_on || pl->exact_mode == 0) return AMR_OK;
+  FskExact X{};
+  X.flags = pl->xflags;
+  X.list = pl->xlist;
+  X.count = pl->xlist + pl->max_streams;
+  X.rows = reinterpret_cast<double*>(pl->z);
+  X.slots = pl->xslots;
+  X.slot_doubles = pl->slot_doubles;
+  X.n_slots = pl->n_slots;
+  X.L = pl->xL;
+  X.pool = pl->xpool;
+  X.fct = (double)(1.0L / (long double)pl->p.n);
+  X.xbits = pl->xbits;
+  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
+  pl->ran_exact = true;
+  HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, B, pl->p, pl->f, X, pl->stream));
+  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1));
+  return AMR_OK;
+}
+
+// F1, F2 (and the exact path) on a device-resident batch: x -> cmp (or the envelopes).  Caller holds mu.
 int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
-  if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, 0, reinterpret_cast<double*>(pl->u), !env_out)) return rc;
+  if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, !env_out)) return rc;
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
-  return run_fsk_f2(pl, B, env_out);
+  if (int rc = run_fsk_f2(pl, B, env_out)) return rc;
+  if (env_out) return AMR_OK;
+  return run_fsk_exact(pl, d_x, dtype, B, x_stride);
 }
 
 int check_fsk_args(amr_fsk_plan* pl, int dtype, int64_t B, int64_t x_stride, int64_t out_stride) {
@@ -463,6 +488,7 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
             int64_t out_stride, int64_t* d_len, int64_t* d_sync) {
   if (int rc = check_fsk_args(pl, dtype, B, x_stride, out_stride)) return rc;
   for (bool& u : pl->ev_used) u = false;
+  pl->ran_exact = false;
   if (B == 0) return AMR_OK;
   if (pl->p.n_bits == 0) return fsk_empty_outputs(pl, B, d_len, d_sync);
   HIP_TRY(mark_fsk(pl, AMR_TF_LAUNCH, 0));
@@ -472,53 +498,8 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   return AMR_OK;
 }
 
-constexpr int64_t kStageAlign = 256;
-int64_t align_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
-
-// Streams per staged chunk of a live-column plan's host entries: the input
-// rows (n * es bytes each) and F1's checkpoints for them share C.  A multiple
-// of F1's 32-stream groups (or the whole batch).
-int64_t live_stage_chunk(const amr_fsk_plan* pl, int64_t es, int64_t B) {
-  const int64_t n = pl->p.n;
-  auto need = [&](int64_t nb) {
-    return align_up(nb * n * es, kStageAlign) + fsk_bandpass_scratch_bytes(nb, n, pl->p.pad);
-  };
-  if (need(B) <= pl->u_bytes) return B;
-  int64_t nb = (pl->u_bytes / (n * es + fsk_bandpass_scratch_bytes(32, n, pl->p.pad) / 32 + 1)) / 32 * 32;
-  while (nb > 32 && need(nb) > pl->u_bytes) nb -= 32;
-  return nb < 32 ? std::min<int64_t>(B, 32) : nb;     // the plan sizes C for one group at least
-}
-
-// Host input -> F1 for a live-column plan: the batch is uploaded into C in
-// chunks (live_stage_chunk), each filtered into z before the next arrives.
-// async: hipMemcpy(2D)Async on the plan's stream (page-locked input overlaps);
-// else the synchronous copies of copy_batch_h2d.  Caller holds mu.
-int stage_f1_live(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride, bool async) {
-  const int64_t es = dtype_size(dtype);
-  const int64_t n = pl->p.n;
-  const int64_t chunk = live_stage_chunk(pl, es, B);
-  uint8_t* c = reinterpret_cast<uint8_t*>(pl->u);
-  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
-  for (int64_t s0 = 0; s0 < B; s0 += chunk) {
-    const int64_t nb = std::min(chunk, B - s0);
-    const uint8_t* src = static_cast<const uint8_t*>(x) + (size_t)(s0 * x_stride * es);
-    if (async) {
-      if (x_stride == n)
-        HIP_TRY(hipMemcpyAsync(c, src, (size_t)(nb * n * es), hipMemcpyHostToDevice, pl->stream));
-      else
-        HIP_TRY(hipMemcpy2DAsync(c, (size_t)(n * es), src, (size_t)(x_stride * es), (size_t)(n * es), (size_t)nb,
-                                 hipMemcpyHostToDevice, pl->stream));
-    } else if (int rc = copy_batch_h2d(c, src, n * es, x_stride * es, nb, pl->stream)) {
-      return rc;
-    }
-    double* scratch = reinterpret_cast<double*>(c + align_up(nb * n * es, kStageAlign));
-    if (int rc = run_fsk_f1(pl, c, dtype, nb, n, s0, scratch)) return rc;
-  }
-  HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
-  return AMR_OK;
-}
-
-// Natural-layout plans stage the host input in d_x (max_streams rows of up to 8 B per sample).
+// The host entries stage the input in d_x (max_streams rows of up to 8 B per
+// sample), where it stays for the exact path after F2.
 int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride) {
   const int64_t es = dtype_size(dtype);
   const int64_t n = pl->p.n;
@@ -579,125 +560,17 @@ LiveCols plan_live_cols(const FftShape& f, const FskParams& p) {
 // Sizes of an FSK plan's device buffers from its shape alone (no device
 // work): amr_fsk_plan_create allocates exactly these; amr_fsk_plan_bytes_estimate
 // sums them for the drop-in plan cache before it creates a plan.
-// ---- the exact fallback's transform plan (fsk_exact.h): pocketfft's
-// factorisations of n and its sincos_2pibyn twiddles, exactly as
-// oracle/amr_hilbert.c restates them (that file pins them against scipy)
-struct Twid2pi {
-  int64_t n = 0, mask = 0, shift = 0;
-  std::vector<double2> v1, v2;
-  static double2 calc(int64_t x, int64_t n, double ang) {
-    x <<= 3;
-    if (x < 4 * n) {
-      if (x < 2 * n) {
-        if (x < n) return make_double2(std::cos((double)x * ang), std::sin((double)x * ang));
-        return make_double2(std::sin((double)(2 * n - x) * ang), std::cos((double)(2 * n - x) * ang));
-      }
-      x -= 2 * n;
-      if (x < n) return make_double2(-std::sin((double)x * ang), std::cos((double)x * ang));
-      return make_double2(-std::cos((double)(2 * n - x) * ang), std::sin((double)(2 * n - x) * ang));
-    }
-    x = 8 * n - x;
-    if (x < 2 * n) {
-      if (x < n) return make_double2(std::cos((double)x * ang), -std::sin((double)x * ang));
-      return make_double2(std::sin((double)(2 * n - x) * ang), -std::cos((double)(2 * n - x) * ang));
-    }
-    x -= 2 * n;
-    if (x < n) return make_double2(-std::sin((double)x * ang), -std::cos((double)x * ang));
-    return make_double2(-std::cos((double)(2 * n - x) * ang), -std::sin((double)(2 * n - x) * ang));
-  }
-  explicit Twid2pi(int64_t len) : n(len) {
-    const double ang = (double)(0.25L * 3.141592653589793238462643383279502884197L / (long double)len);
-    const int64_t nval = (len + 2) / 2;
-    shift = 1;
-    while (((int64_t)1 << shift) * ((int64_t)1 << shift) < nval) ++shift;
-    mask = ((int64_t)1 << shift) - 1;
-    v1.resize((size_t)(mask + 1));
-    v1[0] = make_double2(1.0, 0.0);
-    for (int64_t i = 1; i <= mask; ++i) v1[(size_t)i] = calc(i, len, ang);
-    v2.resize((size_t)((nval + mask) / (mask + 1)));
-    v2[0] = make_double2(1.0, 0.0);
-    for (size_t i = 1; i < v2.size(); ++i) v2[i] = calc((int64_t)i * (mask + 1), len, ang);
-  }
-  double2 operator[](int64_t idx) const {
-    const bool hi = 2 * idx > n;
-    if (hi) idx = n - idx;
-    const double2 a = v1[(size_t)(idx & mask)], b = v2[(size_t)(idx >> shift)];
-    const double re = a.x * b.x - a.y * b.y, im = a.x * b.y + a.y * b.x;
-    return make_double2(re, hi ? -im : im);
-  }
-};
-
-int exact_factorize(int64_t n, bool with8, int* f) {
-  int nf = 0;
-  if (with8)
-    while (n % 8 == 0) { f[nf++] = 8; n /= 8; }
-  while (n % 4 == 0) { f[nf++] = 4; n /= 4; }
-  if (n % 2 == 0) { n /= 2; f[nf++] = 2; std::swap(f[0], f[nf - 1]); }
-  for (int64_t d = 3; d * d <= n; d += 2)
-    while (n % d == 0) { f[nf++] = (int)d; n /= d; }
-  if (n > 1) f[nf++] = (int)n;
-  for (int k = 0; k < nf; ++k)
-    if ((f[k] > 5 && f[k] != 8) || nf > kExactMaxFactors - 1) return -1;
-  return nf;
-}
-
-// tables into tw (real twiddles, then the complex ones from an even offset)
-bool build_exact_fft(int64_t n, std::vector<double>& tw, ExactFft& X) {
-  int fr[kExactMaxFactors], fc[kExactMaxFactors];
-  const int nr = exact_factorize(n, false, fr), nc = exact_factorize(n, true, fc);
-  if (nr < 1 || nc < 1) return false;
-  const Twid2pi T(n);
-  X = ExactFft{};
-  X.n = n;
-  X.nr = nr;
-  X.nc = nc;
-  tw.clear();
-  int64_t l1 = 1;
-  for (int k = 0; k < nr; ++k) {
-    const int64_t ip = fr[k], ido = n / (l1 * ip);
-    X.fr[k] = (int)ip;
-    X.rto[k] = (int64_t)tw.size();
-    std::vector<double> t((size_t)((ip - 1) * (ido - 1)), 0.0);
-    if (k < nr - 1)
-      for (int64_t j = 1; j < ip; ++j)
-        for (int64_t i = 1; i <= (ido - 1) / 2; ++i) {
-          const double2 w = T[j * l1 * i];
-          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 2)] = w.x;
-          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 1)] = w.y;
-        }
-    tw.insert(tw.end(), t.begin(), t.end());
-    l1 *= ip;
-  }
-  if (tw.size() & 1) tw.push_back(0.0);
-  const int64_t cbase = (int64_t)tw.size() / 2;      // in complex units
-  l1 = 1;
-  for (int k = 0; k < nc; ++k) {
-    const int64_t ip = fc[k], ido = n / (l1 * ip);
-    X.fc[k] = (int)ip;
-    X.cto[k] = (int64_t)tw.size() / 2 - cbase;
-    for (int64_t j = 1; j < ip; ++j)
-      for (int64_t i = 1; i < ido; ++i) {
-        const double2 w = T[j * l1 * i];
-        tw.push_back(w.x);
-        tw.push_back(w.y);
-      }
-    l1 *= ip;
-  }
-  X.fct = (double)(1.0L / (long double)n);
-  X.rto[kExactMaxFactors - 1] = cbase;              // where the complex tables start (doubles / 2)
-  return true;
-}
-
 struct FskGeom {
   FskParams p{};
   FftShape sh;
   int64_t z = 0, u = 0, v = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
-  // the exact fallback: flags, list, slots, exact bits, tables
+  // the exact path: flags, scales, list, slots, exact bits, pocketfft tables
   bool exact = false;
   int n_slots = 0;
-  int x_group = 1;
-  int64_t slot_doubles = 0, xflags = 0, xslots = 0, xbits = 0, xtw = 0;
-  int64_t total() const { return z + u + v + cmp + words + six + staging + out + xflags + xslots + xbits + xtw; }
+  int64_t slot_doubles = 0, xflags = 0, amb = 0, xlist = 0, xslots = 0, xbits = 0, xpool = 0, xplan = 0;
+  int64_t total() const {
+    return z + u + v + cmp + words + six + staging + out + xflags + amb + xlist + xslots + xbits + xpool + xplan;
+  }
 };
 bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& g) {
   FskParams& p = g.p;
@@ -719,41 +592,35 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   p.inv_rn1 = 1.0f / (float)p.rn1;
   const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
   if (p.lc.on) {
-    // C: the live columns' transform; before the column pass it holds F1's
-    // checkpoints and (host entries) the staged input -- 4 B per sample for
-    // float32 / int16 in one chunk, float64 in chunks of >= 32 streams
-    const int64_t c = std::min<int64_t>(max_streams, 32);
-    g.u = std::max({max_streams * (int64_t)p.lc.nl * p.lc.n2 * 16, align_up(max_streams * n * 4, kStageAlign) + s1_bytes,
-                    align_up(c * n * 8, kStageAlign) + fsk_bandpass_scratch_bytes(c, n, p.pad)});
-    g.staging = 0;                                   // staged inside C
+    // C: the live columns' transform; before the column pass it holds F1's checkpoints
+    g.u = std::max(max_streams * (int64_t)p.lc.nl * p.lc.n2 * 16, s1_bytes);
   } else {
     g.u = std::max(max_streams * M * 16, s1_bytes);
     g.v = max_streams * M * 16;
-    g.staging = max_streams * n * 8;                 // d_x, allocated on the first host call
   }
-  g.z = max_streams * n * 16;
+  g.staging = max_streams * n * 8;                   // d_x, allocated on the first host call
+  const int64_t m = n + 2 * (int64_t)p.pad;
+  // z; after F2, the exact path's filtfilt rows ([ordinal][tone][m] doubles)
+  g.z = std::max(max_streams * n * 16, max_streams * 2 * m * 8);
   g.cmp = max_streams * p.bits_stride;
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
   g.out = max_streams * (g.out_cap + 16);            // host-API output staging
-  // the exact fallback (AMR_FSK_EXACT=0: off): four-step lengths with pocketfft
-  // factors 2..5 (and 8), decisions to make
+  // the exact path (AMR_FSK_EXACT=0: off), at every length with decisions to make
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
-  int ftmp[kExactMaxFactors];
-  g.exact = exact_env && !g.sh.bluestein && !g.sh.six && p.n_bits > 0 && exact_factorize(n, false, ftmp) > 0 &&
-            exact_factorize(n, true, ftmp) > 0;
+  g.exact = exact_env && p.n_bits > 0;
   if (g.exact) {
-    const int64_t m = n + 2 * (int64_t)p.pad;
-    // streams per workgroup and round: up to 4 (the envelopes run one stream
-    // at a time, so workgroups beat grouping), a slot within 1 GiB
-    g.x_group = (int)std::max<int64_t>(1, std::min<int64_t>({max_streams, 4, (((int64_t)1 << 27) - 8 * n) / (2 * m)}));
-    g.slot_doubles = 8 * n + (int64_t)g.x_group * 2 * m;
-    // one workgroup per slot: up to 128, within 1 GiB of slots
-    g.n_slots = (int)std::max<int64_t>(1, std::min<int64_t>({max_streams, 128, ((int64_t)1 << 30) / (g.slot_doubles * 8)}));
+    g.slot_doubles = pf_scratch_doubles_n(n);
+    // one workgroup per slot: up to 2 per stream and 256, within 1 GiB of slots
+    g.n_slots = (int)std::max<int64_t>(
+        1, std::min<int64_t>({2 * max_streams, 256, ((int64_t)1 << 30) / (g.slot_doubles * 8)}));
     g.xflags = (max_streams + 31) / 32 * 4;
+    g.amb = max_streams * 8;
+    g.xlist = (max_streams + 1) * 4;
     g.xslots = (int64_t)g.n_slots * g.slot_doubles * 8;
     g.xbits = max_streams * p.bits_stride;
-    g.xtw = (6 * n + 64) * 8;
+    g.xpool = pf_pool_doubles_bound(n) * 8;
+    g.xplan = (int64_t)sizeof(PfLen);
   }
   return true;
 }
@@ -826,9 +693,12 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       {(void**)&pl->cmp, geo.cmp},
       {(void**)&pl->words, geo.words},
       {(void**)&pl->xflags, geo.xflags},
+      {(void**)&pl->amb, geo.amb},
+      {(void**)&pl->xlist, geo.xlist},
       {(void**)&pl->xslots, geo.xslots},
       {(void**)&pl->xbits, geo.xbits},
-      {(void**)&pl->xtw, geo.xtw},
+      {(void**)&pl->xpool, geo.xpool},
+      {(void**)&pl->xL, geo.xplan},
   };
   for (const A& a : allocs) {
     if (a.bytes == 0) continue;
@@ -840,23 +710,28 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->scratch_bytes += a.bytes;
   }
   if (geo.exact) {
-    std::vector<double> tw;
-    if (build_exact_fft(n, tw, pl->xfft) && (int64_t)tw.size() * 8 <= geo.xtw) {
-      e = hipMemcpy(pl->xtw, tw.data(), tw.size() * 8, hipMemcpyHostToDevice);
-      if (e == hipSuccess) e = hipMemset(pl->xflags, 0, (size_t)geo.xflags);
-      if (e != hipSuccess) {
-        fsk_plan_free(pl);
-        return fail(AMR_E_HIP, std::string("exact tables: ") + hipGetErrorString(e));
-      }
-      pl->xfft.rtw = pl->xtw;
-      pl->xfft.ctw = reinterpret_cast<const double2*>(pl->xtw) + pl->xfft.rto[kExactMaxFactors - 1];
-      pl->exact_on = true;
-      pl->p.xflags = pl->xflags;         // F3 reads a flagged stream's bits from xbits
-      pl->p.xbits = pl->xbits;
-      pl->n_slots = geo.n_slots;
-      pl->slot_doubles = geo.slot_doubles;
-      pl->x_group = geo.x_group;
+    // pocketfft's plans of length n: tables to the device, then the Bluestein
+    // tables that need a device transform (into the envelope slots' scratch)
+    std::vector<double> pool;
+    PfLen L{};
+    if (!pf_len_build(n, L, pool) || (int64_t)pool.size() > geo.xpool / 8 || geo.xslots / 8 < 4 * L.bl.n2) {
+      fsk_plan_free(pl);
+      return fail(AMR_E_INVALID, "exact path: pocketfft plan of length " + std::to_string(n));
     }
+    e = hipMemcpy(pl->xpool, pool.data(), pool.size() * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(pl->xL, &L, sizeof(PfLen), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = pf_finish(L, pl->xL, pl->xpool, pl->xslots, pl->stream);
+    if (e == hipSuccess) e = hipMemset(pl->xflags, 0, (size_t)geo.xflags);
+    if (e != hipSuccess) {
+      fsk_plan_free(pl);
+      return fail(AMR_E_HIP, std::string("exact path tables: ") + hipGetErrorString(e));
+    }
+    pl->exact_on = true;
+    pl->p.amb = pl->amb;
+    pl->p.xflags = pl->xflags;         // F3 reads a flagged stream's bits from xbits
+    pl->p.xbits = pl->xbits;
+    pl->n_slots = geo.n_slots;
+    pl->slot_doubles = geo.slot_doubles;
   }
   *out = pl;
   return AMR_OK;
@@ -869,9 +744,8 @@ int amr_fsk_plan_destroy(amr_fsk_plan* plan) {
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
-  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host;
-  // a live-column plan stages its input inside C)
-  const int64_t staging = plan->p.lc.on ? 0 : plan->max_streams * plan->p.n * 8;
+  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host)
+  const int64_t staging = plan->max_streams * plan->p.n * 8;
   return plan->scratch_bytes + staging + plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
@@ -895,6 +769,29 @@ int amr_fsk_plan_enable_timing(amr_fsk_plan* plan, int on) {
       for (auto& h : e) HIP_TRY(hipEventCreate(&h));
   }
   plan->timing = on != 0;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_set_exact_mode(amr_fsk_plan* plan, int mode) {
+  if (!plan || mode < 0 || mode > 2) return fail(AMR_E_INVALID, "amr_fsk_plan_set_exact_mode: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  if (mode != 0 && !plan->exact_on) return fail(AMR_E_INVALID, "this plan has no exact path (no decisions, or AMR_FSK_EXACT=0)");
+  plan->exact_mode = mode;
+  // F3 reads a flagged stream's bits from xbits only while the exact path runs
+  plan->p.xflags = mode ? plan->xflags : nullptr;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_exact_streams(amr_fsk_plan* plan, int64_t* count) {
+  if (!plan || !count) return fail(AMR_E_INVALID, "NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  *count = 0;
+  if (!plan->exact_on || !plan->ran_exact) return AMR_OK;
+  int32_t c = 0;
+  HIP_TRY(hipMemcpy(&c, plan->xlist + plan->max_streams, 4, hipMemcpyDeviceToHost));
+  *count = c;
   return AMR_OK;
 }
 
@@ -944,10 +841,6 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   for (bool& u : plan->ev_used) u = false;
   if (plan->p.n_bits == 0) {
     if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
-  } else if (plan->p.lc.on) {
-    if (int rc = stage_f1_live(plan, x, dtype, B, x_stride, false)) return rc;
-    if (int rc = run_fsk_f2(plan, B, false)) return rc;
-    if (int rc = run_fsk_back(plan, B, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   } else {
     if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
     if (int rc = run_fsk(plan, plan->d_x, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
@@ -982,10 +875,6 @@ int amr_fsk_demod_host_async(amr_fsk_plan* plan, const void* x, int dtype, int64
   for (bool& u : plan->ev_used) u = false;
   if (plan->p.n_bits == 0) {
     if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
-  } else if (plan->p.lc.on) {
-    if (int rc = stage_f1_live(plan, x, dtype, B, x_stride, true)) return rc;
-    if (int rc = run_fsk_f2(plan, B, false)) return rc;
-    if (int rc = run_fsk_back(plan, B, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   } else {
     if (!plan->d_x) HIP_TRY(hipMalloc(&plan->d_x, (size_t)(plan->max_streams * n * 8)));
     if (x_stride == n)
@@ -1132,45 +1021,92 @@ int amr_hilbert_host(const double* xr, double* analytic, int64_t n, int64_t batc
   return AMR_OK;
 }
 
+// pocketfft plans of one length on the device (plan struct + tables), for the
+// one-shot host entries below
+struct PfDev {
+  PfLen L{};
+  PfLen* dL = nullptr;
+  double* pool = nullptr;
+  ~PfDev() {
+    if (dL) (void)hipFree(dL);
+    if (pool) (void)hipFree(pool);
+  }
+};
+int pf_dev_init(PfDev& D, int64_t n, double* tmp, hipStream_t st) {
+  std::vector<double> pool;
+  if (!pf_len_build(n, D.L, pool)) return fail(AMR_E_INVALID, "no pocketfft plan for length " + std::to_string(n));
+  HIP_TRY(hipMalloc(&D.pool, pool.size() * 8 + 16));
+  HIP_TRY(hipMalloc(&D.dL, sizeof(PfLen)));
+  HIP_TRY(hipMemcpy(D.pool, pool.data(), pool.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(D.dL, &D.L, sizeof(PfLen), hipMemcpyHostToDevice));
+  HIP_TRY(pf_finish(D.L, D.dL, D.pool, tmp, st));
+  return AMR_OK;
+}
+
 int amr_resample_host(const double* x, int64_t nx, int64_t num, int64_t batch, double* y, int device) {
   if (!x || !y || nx < 1 || num < 1 || batch < 0) return fail(AMR_E_INVALID, "amr_resample_host: bad argument");
   if (batch == 0) return AMR_OK;
   HIP_TRY(hipSetDevice(device));
   hipStream_t st = nullptr;
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  FftPlan fx{}, fy{};
-  int rc = fft_plan_init(fx, nx, st, batch);
-  if (!rc) rc = fft_plan_init(fy, num, st, batch);
-  double2 *X = nullptr, *Y = nullptr, *u = nullptr, *v = nullptr;
-  double* yd = nullptr;
-  hipError_t e = hipSuccess;
-  if (!rc) {
-    const int64_t mu = std::max(fx.M, fy.M);
-    std::vector<double> h((size_t)(batch * nx * 2), 0.0);
-    for (int64_t i = 0; i < batch * nx; ++i) h[(size_t)(2 * i)] = x[i];
-    e = hipMalloc(&X, (size_t)(batch * nx * 16));
-    if (e == hipSuccess) e = hipMalloc(&Y, (size_t)(batch * num * 16));
-    if (e == hipSuccess) e = hipMalloc(&u, (size_t)(batch * mu * 16));
-    if (e == hipSuccess) e = hipMalloc(&v, (size_t)(batch * mu * 16));
-    if (e == hipSuccess) e = hipMalloc(&yd, (size_t)(batch * num * 8));
-    if (e == hipSuccess) e = hipMemcpyAsync(X, h.data(), h.size() * 8, hipMemcpyHostToDevice, st);
-    // X = rfft(x) (the full spectrum; the kernel reads bins 0..nx/2)
-    if (e == hipSuccess) e = fft_c2c(fx, X, u, v, X, batch, false, st);
-    if (e == hipSuccess) e = launch_resample_spec(X, Y, nx, num, batch, st);
-    // y = irfft(Y, num) = Re(IFFT_num(Hermitian Y)), then y *= num / nx
-    if (e == hipSuccess) e = fft_c2c(fy, Y, u, v, Y, batch, true, st);
-    if (e == hipSuccess) e = launch_real_scale(Y, yd, batch * num, (double)num / (double)nx, st);
+  PfDev Dx, Dy;
+  double *xd = nullptr, *yd = nullptr, *slots = nullptr;
+  const int n_slots = (int)std::min<int64_t>(batch, 64);
+  // scratch for the slots, and for pf_finish's transform before that
+  const int64_t sd = std::max(pf_scratch_doubles_n(nx), pf_scratch_doubles_n(num)) + std::max(nx, num);
+  int rc = AMR_OK;
+  hipError_t e = hipMalloc(&slots, (size_t)(n_slots * sd * 8));
+  if (e == hipSuccess) e = hipMalloc(&xd, (size_t)(batch * nx * 8));
+  if (e == hipSuccess) e = hipMalloc(&yd, (size_t)(batch * num * 8));
+  if (e != hipSuccess) rc = fail(AMR_E_NOMEM, std::string("resample buffers: ") + hipGetErrorString(e));
+  if (rc == AMR_OK) rc = pf_dev_init(Dx, nx, slots, st);
+  if (rc == AMR_OK) rc = pf_dev_init(Dy, num, slots, st);
+  if (rc == AMR_OK) {
+    const int64_t slot = pf_resample_slot_doubles(Dx.L, Dy.L);
+    e = hipMemcpyAsync(xd, x, (size_t)(batch * nx * 8), hipMemcpyHostToDevice, st);
+    // irfft's 1/num (pocketfft: double(1 / long double num)), then numpy's y *= num / nx
+    if (e == hipSuccess)
+      e = launch_pf_resample(Dx.dL, Dx.pool, Dy.dL, Dy.pool, xd, nx, yd, num, batch, slots, slot, n_slots,
+                             (double)(1.0L / (long double)num), (double)num / (double)nx, st);
     if (e == hipSuccess) e = hipMemcpyAsync(y, yd, (size_t)(batch * num * 8), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = fail(AMR_E_HIP, std::string("resample: ") + hipGetErrorString(e));
   }
-  for (void* p : {(void*)X, (void*)Y, (void*)u, (void*)v, (void*)yd})
+  (void)hipStreamSynchronize(st);
+  for (void* p : {(void*)xd, (void*)yd, (void*)slots})
     if (p) (void)hipFree(p);
-  fft_plan_free(fx);
-  fft_plan_free(fy);
   (void)hipStreamDestroy(st);
-  if (rc) return rc;
-  HIP_TRY(e);
-  return AMR_OK;
+  return rc;
+}
+
+int amr_hilbert_env_exact_host(const double* x, int64_t n, int64_t batch, double* env, int device) {
+  if (!x || !env || n < 1 || batch < 0) return fail(AMR_E_INVALID, "amr_hilbert_env_exact_host: bad argument");
+  if (batch == 0) return AMR_OK;
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  PfDev D;
+  double *xd = nullptr, *slots = nullptr;
+  const int n_slots = (int)std::min<int64_t>(batch, 128);
+  const int64_t sd = pf_scratch_doubles_n(n);
+  int rc = AMR_OK;
+  hipError_t e = hipMalloc(&slots, (size_t)(n_slots * sd * 8));
+  if (e == hipSuccess) e = hipMalloc(&xd, (size_t)(batch * n * 8));
+  if (e != hipSuccess) rc = fail(AMR_E_NOMEM, std::string("envelope buffers: ") + hipGetErrorString(e));
+  if (rc == AMR_OK) rc = pf_dev_init(D, n, slots, st);
+  if (rc == AMR_OK) {
+    e = hipMemcpyAsync(xd, x, (size_t)(batch * n * 8), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess)
+      e = launch_pf_hilbert_env(D.dL, D.pool, xd, n, batch, slots, sd, n_slots, (double)(1.0L / (long double)n), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(env, xd, (size_t)(batch * n * 8), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = fail(AMR_E_HIP, std::string("exact envelopes: ") + hipGetErrorString(e));
+  }
+  (void)hipStreamSynchronize(st);
+  for (void* p : {(void*)xd, (void*)slots})
+    if (p) (void)hipFree(p);
+  (void)hipStreamDestroy(st);
+  return rc;
 }
 
 }  // extern "C"

@@ -71,6 +71,48 @@ __device__ __forceinline__ double fsk_step(double (&z)[6], const double (&b)[7],
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector (HIP's uint4 is a struct)
 
+// F1's input peak, for F2's ambiguity margin (amr_internal.h amb_scale,
+// fsk_exact_kernels.hip): max |x| over the stream on the raw bits (integer
+// work; NaN / inf dominate every finite value)
+template <typename T> struct PeakT;
+template <> struct PeakT<float> {
+  static __device__ void acc(v4u v, uint32_t& hi, uint32_t&) {
+    const uint32_t m = 0x7fffffffu;
+    hi = max(hi, max(max(v.x & m, v.y & m), max(v.z & m, v.w & m)));
+  }
+  static __device__ void one(float x, uint32_t& hi, uint32_t&) { hi = max(hi, __float_as_uint(x) & 0x7fffffffu); }
+  static __device__ double peak(uint32_t hi, uint32_t) { return (double)__uint_as_float(hi); }
+};
+template <> struct PeakT<double> {
+  // hi: the largest |x| high word; lo: the low words OR-ed (denormals)
+  static __device__ void acc(v4u v, uint32_t& hi, uint32_t& lo) {
+    hi = max(hi, max(v.y & 0x7fffffffu, v.w & 0x7fffffffu));
+    lo |= v.x | v.z;
+  }
+  static __device__ void one(double x, uint32_t& hi, uint32_t& lo) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    hi = max(hi, (uint32_t)(b >> 32) & 0x7fffffffu);
+    lo |= (uint32_t)b;
+  }
+  // an upper bound (low word all ones); 0 only for a stream of exact zeros
+  static __device__ double peak(uint32_t hi, uint32_t lo) {
+    if (hi == 0 && lo == 0) return 0.0;
+    return __hiloint2double((int)hi, (int)0xffffffffu);
+  }
+};
+template <> struct PeakT<int16_t> {
+  static __device__ uint32_t a2(uint32_t w) {
+    const int l = (int)(int16_t)(w & 0xffffu), h = (int)w >> 16;
+    return (uint32_t)max(abs(l), abs(h));
+  }
+  static __device__ void acc(v4u v, uint32_t& hi, uint32_t&) {
+    hi = max(hi, max(max(a2(v.x), a2(v.y)), max(a2(v.z), a2(v.w))));
+  }
+  static __device__ void one(int16_t x, uint32_t& hi, uint32_t&) { hi = max(hi, (uint32_t)abs((int)x)); }
+  static __device__ double peak(uint32_t hi, uint32_t) { return (double)hi / 32768.0; }
+};
+
+
 constexpr int kFskTile = 64;          // samples per input tile (and per checkpoint)
 
 // F1 scratch, per wave: checkpoints ck[tile][6 states][64 lanes] doubles, then
@@ -97,7 +139,7 @@ __device__ __forceinline__ int64_t fsk_zoff(const FskParams& p, int64_t i) {
   else return i;
 }
 
-template <typename T, bool ZO, bool LIVE>
+template <typename T, bool ZO, bool LIVE, bool AMB = false>
 __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_stride, int64_t n_streams,
                                                      double* __restrict__ scratch, double2* __restrict__ z,
                                                      FskParams p, FskIir f) {
@@ -142,12 +184,14 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 #pragma unroll
     for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[buf][RPI * i + rsub][cb]) = r[i];
   };
+  uint32_t pk_hi = 0, pk_lo = 0;   // AMB: the input peak (PeakT)
   // forward steps over tile `buf`; emit(k, y)
-  auto run_tile = [&](int buf, auto emit) {
+  auto run_tile = [&](int buf, auto emit, bool det = false) {
     constexpr int PER = 16 / (int)sizeof(T);
 #pragma unroll
     for (int k = 0; k < kFskTile; k += PER) {
       const v4u v = *reinterpret_cast<const v4u*>(&tin[buf][sl][k * sizeof(T)]);
+      if (AMB && det) PeakT<T>::acc(v, pk_hi, pk_lo);
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
@@ -171,13 +215,20 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 6; ++i) ck[((size_t)t * 6 + i) * 64] = zs[i];
-      run_tile(cur, [](int, double) {});
+      run_tile(cur, [](int, double) {}, true);
       __builtin_amdgcn_sched_barrier(0);
       deposit(cur ^ 1);
       __syncthreads();
     }
   }
-  for (int64_t i = n_main; i < n; ++i) tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
+  for (int64_t i = n_main; i < n; ++i) {
+    if constexpr (AMB) PeakT<T>::one(x[i], pk_hi, pk_lo);
+    tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
+  }
+  if constexpr (AMB) {
+    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+    if (lane == 0) p.xflags[w] = 0u;
+  }
   double ylast = 0.0;
   for (int j = 0; j < pad; ++j) {
     ylast = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
@@ -250,35 +301,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-// digital silence, for the exact fallback (fsk_exact_kernels.hip): there
-// the band-pass output decays to the FFT's rounding floor and only
-// pocketfft's own rounding decides.  That takes >= ~130 silent samples next
-// to signal (r^j < 1e-15 for the slowest band-pass pole r over every valid
-// rate / baud / tone: min j = 129), so F1 samples one
-// input value in 16 (|x| < 2^-60, integer work on the raw bits: float/double
-// sign-cleared against 2^-60's, int16 == 0) and flags a stream when
-// kExactRun / 16 consecutive samples are tiny: every silent run of >= 79
-// samples is flagged (a superset; quiet int16 input can be flagged too,
-// which only costs time).
-constexpr int kExactRun = 64;
-constexpr int kExactStride = 16;
-template <typename T> struct Tiny;
-template <> struct Tiny<float> {
-  static constexpr unsigned kLim = 0x21800000u;        // 2^-60 as float bits
-  static __device__ bool first(v4u v) { return (v.x & 0x7fffffffu) < kLim; }
-  static __device__ bool one(float x) { return (__float_as_uint(x) & 0x7fffffffu) < kLim; }
-};
-template <> struct Tiny<double> {
-  static constexpr unsigned kLim = 0x3C300000u;        // 2^-60's high word
-  static __device__ bool first(v4u v) { return (v.y & 0x7fffffffu) < kLim; }
-  static __device__ bool one(double x) { return ((unsigned)(__double_as_longlong(x) >> 32) & 0x7fffffffu) < kLim; }
-};
-template <> struct Tiny<int16_t> {
-  static __device__ bool first(v4u v) { return (v.x & 0xffffu) == 0u; }
-  static __device__ bool one(int16_t x) { return x == 0; }
-};
-
-template <typename T, bool ZO, bool LIVE, bool W1S, bool DET = false>
+template <typename T, bool ZO, bool LIVE, bool W1S, bool AMB = false>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -330,20 +353,13 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 #pragma unroll
     for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][RPI * i + rsub][cb]) = r[i];
   };
-  int srun = 0;                    // DET: current run of near-zero input samples
-  bool silent = false;
-  auto detect = [&](bool tiny, int k) {
-    if constexpr (DET) {
-      srun = tiny ? srun + k : 0;
-      silent = silent || srun >= kExactRun;
-    }
-  };
+  uint32_t pk_hi = 0, pk_lo = 0;   // AMB: the input peak (PeakT), first forward pass
   auto run_tile = [&](auto emit, bool det) {
     constexpr int PER = 16 / (int)sizeof(T);
 #pragma unroll
     for (int k = 0; k < TL; k += PER) {
       const v4u v = *reinterpret_cast<const v4u*>(&tin[0][sl][k * sizeof(T)]);
-      if (DET && det && k % kExactStride == 0) detect(Tiny<T>::first(v), kExactStride);
+      if (AMB && det) PeakT<T>::acc(v, pk_hi, pk_lo);
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
@@ -382,23 +398,15 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     // the tail's forward outputs -> yb rows 0..ntail-1 (flat), the last -> ylast
     for (int64_t i = n_main; i < n; ++i) {
       const T xi = x[i];
-      detect(Tiny<T>::one(xi), 1);
+      if constexpr (AMB) PeakT<T>::one(xi, pk_hi, pk_lo);
       const double xv = FIn<T>::cvt(xi);
       (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step<ZO>(zs, b, a, xv);
     }
-    if constexpr (DET)
-      {
-        // the group's 32 streams, one word (written for every group, every
-        // batch): tone-0 lanes are the even ones -- compress the even bits
-        uint64_t v = __ballot(silent && tone == 0 && s < n_streams);
-        v &= 0x5555555555555555ull;
-        v = (v | (v >> 1)) & 0x3333333333333333ull;
-        v = (v | (v >> 2)) & 0x0f0f0f0f0f0f0f0full;
-        v = (v | (v >> 4)) & 0x00ff00ff00ff00ffull;
-        v = (v | (v >> 8)) & 0x0000ffff0000ffffull;
-        v = (v | (v >> 16)) & 0x00000000ffffffffull;
-        if (lane == 0) p.xflags[w] = (uint32_t)v;
-      }
+    if constexpr (AMB) {
+      // this batch's margin scale, and the group's flag word cleared for F2
+      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+      if (lane == 0) p.xflags[w] = 0u;
+    }
     double yl = 0.0;
     for (int j = 0; j < pad; ++j) {
       yl = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
@@ -576,7 +584,7 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
 #define BP2(T, S, D) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
-#define BP2D(T) do { if (p.xflags) { if (w1s) BP2(T, true, true); else BP2(T, false, true); } else if (w1s) BP2(T, true, false); else BP2(T, false, false); } while (0)
+#define BP2D(T) do { if (p.amb) { if (w1s) BP2(T, true, true); else BP2(T, false, true); } else if (w1s) BP2(T, true, false); else BP2(T, false, false); } while (0)
     switch (dtype) {
       case kF32: BP2D(float); break;
       case kF64: BP2D(double); break;
@@ -587,16 +595,16 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
 #undef BP2
     return hipGetLastError();
   }
-  if (p.xflags) {      // the one-wave form does not look for silence: nothing flagged
-    const hipError_t e = hipMemsetAsync(p.xflags, 0, (size_t)(n_streams + 31) / 32 * 4, st);
-    if (e != hipSuccess) return e;
-  }
+#define BP1(T, A) hipLaunchKernelGGL((k_fsk_bandpass<T, ZO, LIVE, A>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f)
+#define BP1D(T) do { if (p.amb) BP1(T, true); else BP1(T, false); } while (0)
   switch (dtype) {
-    case kF32: hipLaunchKernelGGL((k_fsk_bandpass<float, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kF64: hipLaunchKernelGGL((k_fsk_bandpass<double, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
-    case kI16: hipLaunchKernelGGL((k_fsk_bandpass<int16_t, ZO, LIVE>), dim3(grid), dim3(64), 0, st, x, x_stride, n_streams, s1, z, p, f); break;
+    case kF32: BP1D(float); break;
+    case kF64: BP1D(double); break;
+    case kI16: BP1D(int16_t); break;
     default: return hipErrorInvalidValue;
   }
+#undef BP1D
+#undef BP1
   return hipGetLastError();
 }
 

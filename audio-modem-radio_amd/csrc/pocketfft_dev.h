@@ -1,0 +1,1068 @@
+// pocketfft_dev.h -- device restatement of pocketfft's transforms (plans:
+// pocketfft.h), bit for bit: every butterfly evaluates pocketfft's expressions
+// in its order, without contraction (-ffp-contract=off), so the results equal
+// scipy.fft's (oracle/amr_pocketfft.c is the CPU statement of the same
+// algorithm, pinned against scipy; tests/test_gpu_pocketfft.py pins these).
+//
+// Each routine is run by ONE whole workgroup over global scratch: a pass
+// spreads its independent butterflies (pocketfft's (k, i) loop nests) over
+// the workgroup's threads, passes are separated by barriers, and the generic
+// passes (radfg / radbg / passg) run their phases between barriers, each
+// thread owning the accumulation chains of its outputs (so their order is
+// pocketfft's).  Every thread of the workgroup must call these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pocketfft.h"
+
+namespace amr {
+namespace pf {
+
+struct Cx {
+  double r, i;
+};
+__device__ __forceinline__ Cx add(Cx a, Cx b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ Cx sub(Cx a, Cx b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ Cx scale(Cx a, double f) { return {a.r * f, a.i * f}; }
+// special_mul<fwd>: v * conj(w) forward, v * w backward
+template <bool FWD>
+__device__ __forceinline__ Cx smul(Cx v, Cx w) {
+  if (FWD) return {v.r * w.r + v.i * w.i, v.i * w.r - v.r * w.i};
+  return {v.r * w.r - v.i * w.i, v.r * w.i + v.i * w.r};
+}
+__device__ __forceinline__ Cx smul(Cx v, Cx w, bool fwd) { return fwd ? smul<true>(v, w) : smul<false>(v, w); }
+// ROTX90<fwd>: times -i forward, +i backward
+template <bool FWD>
+__device__ __forceinline__ Cx rot90(Cx a) {
+  if (FWD) return {a.i, -a.r};
+  return {-a.i, a.r};
+}
+template <bool FWD>
+__device__ __forceinline__ Cx rot45(Cx a) {
+  const double h = 0.707106781186547524400844362104849;
+  if (FWD) return {h * (a.r + a.i), h * (a.i - a.r)};
+  return {h * (a.r - a.i), h * (a.i + a.r)};
+}
+template <bool FWD>
+__device__ __forceinline__ Cx rot135(Cx a) {
+  const double h = 0.707106781186547524400844362104849;
+  if (FWD) return {h * (a.i - a.r), h * (-a.r - a.i)};
+  return {h * (-a.r - a.i), h * (a.r - a.i)};
+}
+
+#define PF_FOR(t, N) for (int64_t t = threadIdx.x; t < (N); t += blockDim.x)
+
+// ======================= complex passes (cfftp) =============================
+#define CC(a, b, c) cc[(a) + ido * ((b) + IP * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define WA(x, i) wa[(i) - 1 + (x) * (ido - 1)]
+
+template <bool FWD>
+__device__ void pass2(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
+  constexpr int64_t IP = 2;
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    CH(i, k, 0) = add(CC(i, 0, k), CC(i, 1, k));
+    const Cx d = sub(CC(i, 0, k), CC(i, 1, k));
+    CH(i, k, 1) = i == 0 ? d : smul<FWD>(d, WA(0, i));
+  }
+}
+
+template <bool FWD>
+__device__ void pass3(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
+  constexpr int64_t IP = 3;
+  const double tw1r = -0.5, tw1i = (FWD ? -1 : 1) * 0.8660254037844386467637231707529362;
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    const Cx t0 = CC(i, 0, k), t1 = add(CC(i, 1, k), CC(i, 2, k)), t2 = sub(CC(i, 1, k), CC(i, 2, k));
+    CH(i, k, 0) = add(t0, t1);
+    const Cx ca = {t0.r + t1.r * tw1r, t0.i + t1.i * tw1r};
+    const Cx cb = {-(t2.i * tw1i), t2.r * tw1i};
+    if (i == 0) {
+      CH(0, k, 1) = add(ca, cb);
+      CH(0, k, 2) = sub(ca, cb);
+    } else {
+      CH(i, k, 1) = smul<FWD>(add(ca, cb), WA(0, i));
+      CH(i, k, 2) = smul<FWD>(sub(ca, cb), WA(1, i));
+    }
+  }
+}
+
+template <bool FWD>
+__device__ void pass4(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
+  constexpr int64_t IP = 4;
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    const Cx t2 = add(CC(i, 0, k), CC(i, 2, k)), t1 = sub(CC(i, 0, k), CC(i, 2, k));
+    const Cx t3 = add(CC(i, 1, k), CC(i, 3, k)), t4 = rot90<FWD>(sub(CC(i, 1, k), CC(i, 3, k)));
+    if (i == 0) {
+      CH(0, k, 0) = add(t2, t3);
+      CH(0, k, 2) = sub(t2, t3);
+      CH(0, k, 1) = add(t1, t4);
+      CH(0, k, 3) = sub(t1, t4);
+    } else {
+      CH(i, k, 0) = add(t2, t3);
+      CH(i, k, 1) = smul<FWD>(add(t1, t4), WA(0, i));
+      CH(i, k, 2) = smul<FWD>(sub(t2, t3), WA(1, i));
+      CH(i, k, 3) = smul<FWD>(sub(t1, t4), WA(2, i));
+    }
+  }
+}
+
+// passes 5, 7, 11 (pocketfft's PREPn / PARTSTEPn): pairs t[j] = CC(j) +
+// CC(ip-j), d[j] = CC(j) - CC(ip-j); output u = 1..h:
+//   ca = t0 + c(u,1) t[1] + ... + c(u,h) t[h]        (left to right)
+//   cb = (-(s(u,1) d[1].i +- ...), s(u,1) d[1].r +- ...)
+// with c(u,j), s(u,j) the cos / sin of 2 pi (u j mod ip) / ip, the sin's sign
+// flipped (a subtraction in the chain) where u j mod ip lies above ip / 2
+template <int IPN>
+struct OddTw;
+template <>
+struct OddTw<5> {
+  static constexpr double c[3] = {1.0, 0.3090169943749474241022934171828191, -0.8090169943749474241022934171828191};
+  static constexpr double s[3] = {0.0, 0.9510565162951535721164393333793821, 0.5877852522924731291687059546390728};
+};
+template <>
+struct OddTw<7> {
+  static constexpr double c[4] = {1.0, 0.6234898018587335305250048840042398, -0.2225209339563144042889025644967948,
+                                  -0.9009688679024191262361023195074451};
+  static constexpr double s[4] = {0.0, 0.7818314824680298087084445266740578, 0.9749279121818236070181316829939312,
+                                  0.433883739117558120475768332848359};
+};
+template <>
+struct OddTw<11> {
+  static constexpr double c[6] = {1.0, 0.8412535328311811688618116489193677, 0.4154150130018864255292741492296232,
+                                  -0.1423148382732851404437926686163697, -0.6548607339452850640569250724662936,
+                                  -0.9594929736144973898903680570663277};
+  static constexpr double s[6] = {0.0, 0.5406408174555975821076359543186917, 0.9096319953545183714117153830790285,
+                                  0.9898214418809327323760920377767188, 0.7557495743542582837740358439723444,
+                                  0.2817325568414296977114179153466169};
+};
+
+template <bool FWD, int IPN>
+__device__ void passodd(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
+  constexpr int64_t IP = IPN;
+  constexpr int H = (IPN - 1) / 2;
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    Cx tt[H + 1], dd[H + 1];
+    const Cx t0 = CC(i, 0, k);
+#pragma unroll
+    for (int j = 1; j <= H; ++j) {
+      tt[j] = add(CC(i, j, k), CC(i, IPN - j, k));
+      dd[j] = sub(CC(i, j, k), CC(i, IPN - j, k));
+    }
+    Cx s0 = t0;
+#pragma unroll
+    for (int j = 1; j <= H; ++j) s0.r = s0.r + tt[j].r;
+#pragma unroll
+    for (int j = 1; j <= H; ++j) s0.i = s0.i + tt[j].i;
+    CH(i, k, 0) = s0;
+#pragma unroll
+    for (int u = 1; u <= H; ++u) {
+      Cx ca = t0;
+      double cbr = 0.0, cbi = 0.0;
+#pragma unroll
+      for (int j = 1; j <= H; ++j) {
+        int r = (u * j) % IPN;
+        const bool neg = r > H;
+        if (neg) r = IPN - r;
+        const double cr = OddTw<IPN>::c[r], si = (FWD ? -1.0 : 1.0) * OddTw<IPN>::s[r];
+        ca.r = ca.r + cr * tt[j].r;
+        ca.i = ca.i + cr * tt[j].i;
+        if (j == 1) {
+          cbi = si * dd[j].r;
+          cbr = si * dd[j].i;
+        } else if (!neg) {
+          cbi = cbi + si * dd[j].r;
+          cbr = cbr + si * dd[j].i;
+        } else {
+          cbi = cbi - si * dd[j].r;
+          cbr = cbr - si * dd[j].i;
+        }
+      }
+      const Cx cb = {-cbr, cbi};
+      if (i == 0) {
+        CH(0, k, u) = add(ca, cb);
+        CH(0, k, IPN - u) = sub(ca, cb);
+      } else {
+        CH(i, k, u) = smul<FWD>(add(ca, cb), WA(u - 1, i));
+        CH(i, k, IPN - u) = smul<FWD>(sub(ca, cb), WA(IPN - u - 1, i));
+      }
+    }
+  }
+}
+
+template <bool FWD>
+__device__ void pass8(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
+  constexpr int64_t IP = 8;
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    Cx a1 = add(CC(i, 1, k), CC(i, 5, k)), a5 = sub(CC(i, 1, k), CC(i, 5, k));
+    Cx a3 = add(CC(i, 3, k), CC(i, 7, k)), a7 = sub(CC(i, 3, k), CC(i, 7, k));
+    Cx u = a1;
+    a1 = add(u, a3);
+    a3 = rot90<FWD>(sub(u, a3));
+    a7 = rot90<FWD>(a7);
+    u = a5;
+    a5 = rot45<FWD>(add(u, a7));
+    a7 = rot135<FWD>(sub(u, a7));
+    Cx a0 = add(CC(i, 0, k), CC(i, 4, k)), a4 = sub(CC(i, 0, k), CC(i, 4, k));
+    Cx a2 = add(CC(i, 2, k), CC(i, 6, k)), a6 = sub(CC(i, 2, k), CC(i, 6, k));
+    if (i == 0) {
+      const Cx s02 = add(a0, a2), d02 = sub(a0, a2);
+      CH(0, k, 0) = add(s02, a1);
+      CH(0, k, 4) = sub(s02, a1);
+      CH(0, k, 2) = add(d02, a3);
+      CH(0, k, 6) = sub(d02, a3);
+      a6 = rot90<FWD>(a6);
+      const Cx s46 = add(a4, a6), d46 = sub(a4, a6);
+      CH(0, k, 1) = add(s46, a5);
+      CH(0, k, 5) = sub(s46, a5);
+      CH(0, k, 3) = add(d46, a7);
+      CH(0, k, 7) = sub(d46, a7);
+    } else {
+      u = a0;
+      a0 = add(u, a2);
+      a2 = sub(u, a2);
+      CH(i, k, 0) = add(a0, a1);
+      CH(i, k, 4) = smul<FWD>(sub(a0, a1), WA(3, i));
+      CH(i, k, 2) = smul<FWD>(add(a2, a3), WA(1, i));
+      CH(i, k, 6) = smul<FWD>(sub(a2, a3), WA(5, i));
+      a6 = rot90<FWD>(a6);
+      u = a4;
+      a4 = add(u, a6);
+      a6 = sub(u, a6);
+      CH(i, k, 1) = smul<FWD>(add(a4, a5), WA(0, i));
+      CH(i, k, 5) = smul<FWD>(sub(a4, a5), WA(4, i));
+      CH(i, k, 3) = smul<FWD>(add(a6, a7), WA(2, i));
+      CH(i, k, 7) = smul<FWD>(sub(a6, a7), WA(6, i));
+    }
+  }
+}
+#undef CC
+#undef CH
+#undef WA
+
+// generic pass (ip > 11): the result lands in cc
+template <bool FWD>
+__device__ void passg(int64_t ido, int64_t ip, int64_t l1, Cx* cc, Cx* ch, const Cx* wa, const Cx* csarr) {
+  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
+#define CX(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define CX2(a, b) cc[(a) + idl1 * (b)]
+#define CH2(a, b) ch[(a) + idl1 * (b)]
+  auto wal = [&](int64_t x) -> Cx {
+    if (x == 0) return {1.0, 0.0};
+    const Cx c = csarr[x];
+    return {c.r, FWD ? -c.i : c.i};
+  };
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    CH(i, k, 0) = CC(i, 0, k);
+    for (int64_t j = 1, jc = ip - 1; j < ipph; ++j, --jc) {
+      CH(i, k, j) = add(CC(i, j, k), CC(i, jc, k));
+      CH(i, k, jc) = sub(CC(i, j, k), CC(i, jc, k));
+    }
+  }
+  __syncthreads();
+  PF_FOR(ik, idl1) {
+    Cx tmp = CH2(ik, 0);
+    for (int64_t j = 1; j < ipph; ++j) tmp = add(tmp, CH2(ik, j));
+    CX2(ik, 0) = tmp;
+    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+      const Cx w1 = wal(l), w2 = wal(2 * l);
+      Cx xl, xlc;
+      xl.r = CH2(ik, 0).r + w1.r * CH2(ik, 1).r + w2.r * CH2(ik, 2).r;
+      xl.i = CH2(ik, 0).i + w1.r * CH2(ik, 1).i + w2.r * CH2(ik, 2).i;
+      xlc.r = -(w1.i * CH2(ik, ip - 1).i + w2.i * CH2(ik, ip - 2).i);
+      xlc.i = w1.i * CH2(ik, ip - 1).r + w2.i * CH2(ik, ip - 2).r;
+      int64_t iwal = 2 * l;
+      int64_t j = 3, jc = ip - 3;
+      for (; j < ipph - 1; j += 2, jc -= 2) {
+        iwal += l;
+        if (iwal > ip) iwal -= ip;
+        const Cx xw = wal(iwal);
+        iwal += l;
+        if (iwal > ip) iwal -= ip;
+        const Cx xw2 = wal(iwal);
+        xl.r += CH2(ik, j).r * xw.r + CH2(ik, j + 1).r * xw2.r;
+        xl.i += CH2(ik, j).i * xw.r + CH2(ik, j + 1).i * xw2.r;
+        xlc.r -= CH2(ik, jc).i * xw.i + CH2(ik, jc - 1).i * xw2.i;
+        xlc.i += CH2(ik, jc).r * xw.i + CH2(ik, jc - 1).r * xw2.i;
+      }
+      for (; j < ipph; ++j, --jc) {
+        iwal += l;
+        if (iwal > ip) iwal -= ip;
+        const Cx xw = wal(iwal);
+        xl.r += CH2(ik, j).r * xw.r;
+        xl.i += CH2(ik, j).i * xw.r;
+        xlc.r -= CH2(ik, jc).i * xw.i;
+        xlc.i += CH2(ik, jc).r * xw.i;
+      }
+      CX2(ik, l) = xl;
+      CX2(ik, lc) = xlc;
+    }
+  }
+  __syncthreads();
+  // shuffling and twiddling
+  if (ido == 1) {
+    PF_FOR(t, (ipph - 1) * idl1) {
+      const int64_t j = 1 + t / idl1, ik = t - (j - 1) * idl1, jc = ip - j;
+      const Cx t1 = CX2(ik, j), t2 = CX2(ik, jc);
+      CX2(ik, j) = add(t1, t2);
+      CX2(ik, jc) = sub(t1, t2);
+    }
+  } else {
+    PF_FOR(t, (ipph - 1) * l1 * ido) {
+      const int64_t j = 1 + t / (l1 * ido), r = t - (j - 1) * l1 * ido, k = r / ido, i = r - k * ido, jc = ip - j;
+      if (i == 0) {
+        const Cx t1 = CX(0, k, j), t2 = CX(0, k, jc);
+        CX(0, k, j) = add(t1, t2);
+        CX(0, k, jc) = sub(t1, t2);
+      } else {
+        const Cx x1 = add(CX(i, k, j), CX(i, k, jc)), x2 = sub(CX(i, k, j), CX(i, k, jc));
+        CX(i, k, j) = smul<FWD>(x1, wa[(j - 1) * (ido - 1) + i - 1]);
+        CX(i, k, jc) = smul<FWD>(x2, wa[(jc - 1) * (ido - 1) + i - 1]);
+      }
+    }
+  }
+#undef CH
+#undef CC
+#undef CX
+#undef CX2
+#undef CH2
+}
+
+// c (P.len) in place, scratch ch (P.len): the transform, times fct (not when fct == 1)
+template <bool FWD>
+__device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, double fct) {
+  const int64_t len = P.len;
+  if (len == 1) {
+    if (threadIdx.x == 0) c[0] = scale(c[0], fct);
+    __syncthreads();
+    return;
+  }
+  Cx *p1 = c, *p2 = ch;
+  for (int k = 0; k < P.nf; ++k) {
+    const PfFact F = P.f[k];
+    const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
+    switch (F.ip) {
+      case 4: pass4<FWD>(F.ido, F.l1, p1, p2, wa); break;
+      case 8: pass8<FWD>(F.ido, F.l1, p1, p2, wa); break;
+      case 2: pass2<FWD>(F.ido, F.l1, p1, p2, wa); break;
+      case 3: pass3<FWD>(F.ido, F.l1, p1, p2, wa); break;
+      case 5: passodd<FWD, 5>(F.ido, F.l1, p1, p2, wa); break;
+      case 7: passodd<FWD, 7>(F.ido, F.l1, p1, p2, wa); break;
+      case 11: passodd<FWD, 11>(F.ido, F.l1, p1, p2, wa); break;
+      default: {
+        passg<FWD>(F.ido, F.ip, F.l1, p1, p2, wa, reinterpret_cast<const Cx*>(pool + F.tws));
+        Cx* t = p1;
+        p1 = p2;
+        p2 = t;
+      }
+    }
+    Cx* t = p1;
+    p1 = p2;
+    p2 = t;
+    __syncthreads();
+  }
+  if (p1 != c) {
+    PF_FOR(i, len) c[i] = fct != 1.0 ? scale(p1[i], fct) : p1[i];
+  } else if (fct != 1.0) {
+    PF_FOR(i, len) c[i] = scale(c[i], fct);
+  }
+  __syncthreads();
+}
+
+// ========================= real passes (rfftp) ==============================
+#define CC(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+
+__device__ void radf2(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+#define CH(a, b, c) ch[(a) + ido * ((b) + 2 * (c))]
+  PF_FOR(k, l1) {
+    CH(0, 0, k) = CC(0, k, 0) + CC(0, k, 1);
+    CH(ido - 1, 1, k) = CC(0, k, 0) - CC(0, k, 1);
+    if ((ido & 1) == 0) {
+      CH(0, 1, k) = -CC(ido - 1, k, 1);
+      CH(ido - 1, 0, k) = CC(ido - 1, k, 0);
+    }
+  }
+  if (ido <= 2) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double tr2 = wa[i - 2] * CC(i - 1, k, 1) + wa[i - 1] * CC(i, k, 1);
+    const double ti2 = wa[i - 2] * CC(i, k, 1) - wa[i - 1] * CC(i - 1, k, 1);
+    CH(i - 1, 0, k) = CC(i - 1, k, 0) + tr2;
+    CH(ic - 1, 1, k) = CC(i - 1, k, 0) - tr2;
+    CH(i, 0, k) = ti2 + CC(i, k, 0);
+    CH(ic, 1, k) = ti2 - CC(i, k, 0);
+  }
+#undef CH
+}
+
+__device__ void radf3(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
+#define CH(a, b, c) ch[(a) + ido * ((b) + 3 * (c))]
+  PF_FOR(k, l1) {
+    const double cr2 = CC(0, k, 1) + CC(0, k, 2);
+    CH(0, 0, k) = CC(0, k, 0) + cr2;
+    CH(0, 2, k) = taui * (CC(0, k, 2) - CC(0, k, 1));
+    CH(ido - 1, 1, k) = CC(0, k, 0) + taur * cr2;
+  }
+  if (ido == 1) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
+    const double di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
+    const double dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
+    const double di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2);
+    const double cr2 = dr2 + dr3, ci2 = di2 + di3;
+    CH(i - 1, 0, k) = CC(i - 1, k, 0) + cr2;
+    CH(i, 0, k) = CC(i, k, 0) + ci2;
+    const double tr2 = CC(i - 1, k, 0) + taur * cr2, ti2 = CC(i, k, 0) + taur * ci2;
+    const double tr3 = taui * (di2 - di3), ti3 = taui * (dr3 - dr2);
+    CH(i - 1, 2, k) = tr2 + tr3;
+    CH(ic - 1, 1, k) = tr2 - tr3;
+    CH(i, 2, k) = ti2 + ti3;
+    CH(ic, 1, k) = ti3 - ti2;
+  }
+#undef CH
+}
+
+__device__ void radf4(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  const double hsqt2 = 0.707106781186547524400844362104849;
+#define CH(a, b, c) ch[(a) + ido * ((b) + 4 * (c))]
+  PF_FOR(k, l1) {
+    const double tr1 = CC(0, k, 3) + CC(0, k, 1);
+    CH(0, 2, k) = CC(0, k, 3) - CC(0, k, 1);
+    const double tr2 = CC(0, k, 0) + CC(0, k, 2);
+    CH(ido - 1, 1, k) = CC(0, k, 0) - CC(0, k, 2);
+    CH(0, 0, k) = tr2 + tr1;
+    CH(ido - 1, 3, k) = tr2 - tr1;
+    if ((ido & 1) == 0) {
+      const double ti1 = -hsqt2 * (CC(ido - 1, k, 1) + CC(ido - 1, k, 3));
+      const double tr1b = hsqt2 * (CC(ido - 1, k, 1) - CC(ido - 1, k, 3));
+      CH(ido - 1, 0, k) = CC(ido - 1, k, 0) + tr1b;
+      CH(ido - 1, 2, k) = CC(ido - 1, k, 0) - tr1b;
+      CH(0, 3, k) = ti1 + CC(ido - 1, k, 2);
+      CH(0, 1, k) = ti1 - CC(ido - 1, k, 2);
+    }
+  }
+  if (ido <= 2) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double cr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
+    const double ci2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
+    const double cr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
+    const double ci3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2);
+    const double cr4 = WA(2, i - 2) * CC(i - 1, k, 3) + WA(2, i - 1) * CC(i, k, 3);
+    const double ci4 = WA(2, i - 2) * CC(i, k, 3) - WA(2, i - 1) * CC(i - 1, k, 3);
+    const double tr1 = cr4 + cr2, tr4 = cr4 - cr2;
+    const double ti1 = ci2 + ci4, ti4 = ci2 - ci4;
+    const double tr2 = CC(i - 1, k, 0) + cr3, tr3 = CC(i - 1, k, 0) - cr3;
+    const double ti2 = CC(i, k, 0) + ci3, ti3 = CC(i, k, 0) - ci3;
+    CH(i - 1, 0, k) = tr2 + tr1;
+    CH(ic - 1, 3, k) = tr2 - tr1;
+    CH(i, 0, k) = ti1 + ti2;
+    CH(ic, 3, k) = ti1 - ti2;
+    CH(i - 1, 2, k) = tr3 + ti4;
+    CH(ic - 1, 1, k) = tr3 - ti4;
+    CH(i, 2, k) = tr4 + ti3;
+    CH(ic, 1, k) = tr4 - ti3;
+  }
+#undef CH
+}
+
+__device__ void radf5(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
+  const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
+#define CH(a, b, c) ch[(a) + ido * ((b) + 5 * (c))]
+  PF_FOR(k, l1) {
+    const double cr2 = CC(0, k, 4) + CC(0, k, 1), ci5 = CC(0, k, 4) - CC(0, k, 1);
+    const double cr3 = CC(0, k, 3) + CC(0, k, 2), ci4 = CC(0, k, 3) - CC(0, k, 2);
+    CH(0, 0, k) = CC(0, k, 0) + cr2 + cr3;
+    CH(ido - 1, 1, k) = CC(0, k, 0) + tr11 * cr2 + tr12 * cr3;
+    CH(0, 2, k) = ti11 * ci5 + ti12 * ci4;
+    CH(ido - 1, 3, k) = CC(0, k, 0) + tr12 * cr2 + tr11 * cr3;
+    CH(0, 4, k) = ti12 * ci5 - ti11 * ci4;
+  }
+  if (ido == 1) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
+    const double di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
+    const double dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
+    const double di3 = WA(1, i - 2) * CC(i, k, 2) - WA(1, i - 1) * CC(i - 1, k, 2);
+    const double dr4 = WA(2, i - 2) * CC(i - 1, k, 3) + WA(2, i - 1) * CC(i, k, 3);
+    const double di4 = WA(2, i - 2) * CC(i, k, 3) - WA(2, i - 1) * CC(i - 1, k, 3);
+    const double dr5 = WA(3, i - 2) * CC(i - 1, k, 4) + WA(3, i - 1) * CC(i, k, 4);
+    const double di5 = WA(3, i - 2) * CC(i, k, 4) - WA(3, i - 1) * CC(i - 1, k, 4);
+    const double cr2 = dr5 + dr2, ci5 = dr5 - dr2;
+    const double ci2 = di2 + di5, cr5 = di2 - di5;
+    const double cr3 = dr4 + dr3, ci4 = dr4 - dr3;
+    const double ci3 = di3 + di4, cr4 = di3 - di4;
+    CH(i - 1, 0, k) = CC(i - 1, k, 0) + cr2 + cr3;
+    CH(i, 0, k) = CC(i, k, 0) + ci2 + ci3;
+    const double tr2 = CC(i - 1, k, 0) + tr11 * cr2 + tr12 * cr3;
+    const double ti2 = CC(i, k, 0) + tr11 * ci2 + tr12 * ci3;
+    const double tr3 = CC(i - 1, k, 0) + tr12 * cr2 + tr11 * cr3;
+    const double ti3 = CC(i, k, 0) + tr12 * ci2 + tr11 * ci3;
+    const double tr5 = cr5 * ti11 + cr4 * ti12, tr4 = cr5 * ti12 - cr4 * ti11;
+    const double ti5 = ci5 * ti11 + ci4 * ti12, ti4 = ci5 * ti12 - ci4 * ti11;
+    CH(i - 1, 2, k) = tr2 + tr5;
+    CH(ic - 1, 1, k) = tr2 - tr5;
+    CH(i, 2, k) = ti2 + ti5;
+    CH(ic, 1, k) = ti5 - ti2;
+    CH(i - 1, 4, k) = tr3 + tr4;
+    CH(ic - 1, 3, k) = tr3 - tr4;
+    CH(i, 4, k) = ti3 + ti4;
+    CH(ic, 3, k) = ti4 - ti3;
+  }
+#undef CH
+}
+#undef CC
+#undef WA
+
+// generic forward pass (ip odd > 5, ido odd): the result lands in cc
+__device__ void radfg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* ch, const double* wa,
+                      const double* csarr) {
+  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+#define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define C1(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define C2(a, b) cc[(a) + idl1 * (b)]
+#define CH2(a, b) ch[(a) + idl1 * (b)]
+  // phase 1: twiddles of the j / jc pairs (i >= 1) and the k column sums (i = 0)
+  const int64_t hp = (ido - 1) / 2;
+  PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
+    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+                  q = r - k * (hp + 1), jc = ip - j;
+    if (q == 0) {
+      const double t1 = C1(0, k, j), t2 = C1(0, k, jc);
+      C1(0, k, j) = t2 + t1;
+      C1(0, k, jc) = t2 - t1;
+    } else {
+      const int64_t i = 2 * q - 1;
+      const int64_t idij = (j - 1) * (ido - 1) + (i - 1), idij2 = (jc - 1) * (ido - 1) + (i - 1);
+      const double t1 = C1(i, k, j), t2 = C1(i + 1, k, j), t3 = C1(i, k, jc), t4 = C1(i + 1, k, jc);
+      const double x1 = wa[idij] * t1 + wa[idij + 1] * t2, x2 = wa[idij] * t2 - wa[idij + 1] * t1,
+                   x3 = wa[idij2] * t3 + wa[idij2 + 1] * t4, x4 = wa[idij2] * t4 - wa[idij2 + 1] * t3;
+      C1(i, k, j) = x3 + x1;
+      C1(i + 1, k, jc) = x3 - x1;
+      C1(i + 1, k, j) = x2 + x4;
+      C1(i, k, jc) = x2 - x4;
+    }
+  }
+  __syncthreads();
+  // phase 2: the ip-point real DFT across columns, per ik
+  PF_FOR(ik, idl1) {
+    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+      double a = C2(ik, 0) + csarr[2 * l] * C2(ik, 1) + csarr[4 * l] * C2(ik, 2);
+      double b = csarr[2 * l + 1] * C2(ik, ip - 1) + csarr[4 * l + 1] * C2(ik, ip - 2);
+      int64_t iang = 2 * l;
+      int64_t j = 3, jc = ip - 3;
+      for (; j < ipph - 3; j += 4, jc -= 4) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar1 = csarr[2 * iang], ai1 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar2 = csarr[2 * iang], ai2 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar3 = csarr[2 * iang], ai3 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar4 = csarr[2 * iang], ai4 = csarr[2 * iang + 1];
+        a += ar1 * C2(ik, j) + ar2 * C2(ik, j + 1) + ar3 * C2(ik, j + 2) + ar4 * C2(ik, j + 3);
+        b += ai1 * C2(ik, jc) + ai2 * C2(ik, jc - 1) + ai3 * C2(ik, jc - 2) + ai4 * C2(ik, jc - 3);
+      }
+      for (; j < ipph - 1; j += 2, jc -= 2) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar1 = csarr[2 * iang], ai1 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar2 = csarr[2 * iang], ai2 = csarr[2 * iang + 1];
+        a += ar1 * C2(ik, j) + ar2 * C2(ik, j + 1);
+        b += ai1 * C2(ik, jc) + ai2 * C2(ik, jc - 1);
+      }
+      for (; j < ipph; ++j, --jc) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar = csarr[2 * iang], ai = csarr[2 * iang + 1];
+        a += ar * C2(ik, j);
+        b += ai * C2(ik, jc);
+      }
+      CH2(ik, l) = a;
+      CH2(ik, lc) = b;
+    }
+    double s = C2(ik, 0);
+    for (int64_t j = 1; j < ipph; ++j) s += C2(ik, j);
+    CH2(ik, 0) = s;
+  }
+  __syncthreads();
+  // phase 3: into the halfcomplex layout
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    CC(i, 0, k) = CH(i, k, 0);
+  }
+  PF_FOR(t, (ipph - 1) * l1) {
+    const int64_t j = 1 + t / l1, k = t - (j - 1) * l1, jc = ip - j, j2 = 2 * j - 1;
+    CC(ido - 1, j2, k) = CH(0, k, j);
+    CC(0, j2 + 1, k) = CH(0, k, jc);
+  }
+  if (ido > 1) {
+    PF_FOR(t, (ipph - 1) * l1 * hp) {
+      const int64_t j = 1 + t / (l1 * hp), r = t - (j - 1) * l1 * hp, k = r / hp, q = r - k * hp;
+      const int64_t jc = ip - j, j2 = 2 * j - 1, i = 1 + 2 * q, ic = ido - i - 2;
+      CC(i, j2 + 1, k) = CH(i, k, j) + CH(i, k, jc);
+      CC(ic, j2, k) = CH(i, k, j) - CH(i, k, jc);
+      CC(i + 1, j2 + 1, k) = CH(i + 1, k, j) + CH(i + 1, k, jc);
+      CC(ic + 1, j2, k) = CH(i + 1, k, jc) - CH(i + 1, k, j);
+    }
+  }
+#undef CC
+#undef CH
+#undef C1
+#undef C2
+#undef CH2
+}
+
+#define CC(a, b, c) cc[(a) + ido * ((b) + IP * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define WA(x, i) wa[(i) + (x) * (ido - 1)]
+
+__device__ void radb2(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  constexpr int64_t IP = 2;
+  PF_FOR(k, l1) {
+    CH(0, k, 0) = CC(0, 0, k) + CC(ido - 1, 1, k);
+    CH(0, k, 1) = CC(0, 0, k) - CC(ido - 1, 1, k);
+    if ((ido & 1) == 0) {
+      CH(ido - 1, k, 0) = 2 * CC(ido - 1, 0, k);
+      CH(ido - 1, k, 1) = -2 * CC(0, 1, k);
+    }
+  }
+  if (ido <= 2) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    CH(i - 1, k, 0) = CC(i - 1, 0, k) + CC(ic - 1, 1, k);
+    const double tr2 = CC(i - 1, 0, k) - CC(ic - 1, 1, k);
+    const double ti2 = CC(i, 0, k) + CC(ic, 1, k);
+    CH(i, k, 0) = CC(i, 0, k) - CC(ic, 1, k);
+    CH(i, k, 1) = WA(0, i - 2) * ti2 + WA(0, i - 1) * tr2;
+    CH(i - 1, k, 1) = WA(0, i - 2) * tr2 - WA(0, i - 1) * ti2;
+  }
+}
+
+__device__ void radb3(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  constexpr int64_t IP = 3;
+  const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
+  PF_FOR(k, l1) {
+    const double tr2 = 2 * CC(ido - 1, 1, k);
+    const double cr2 = CC(0, 0, k) + taur * tr2;
+    CH(0, k, 0) = CC(0, 0, k) + tr2;
+    const double ci3 = 2 * taui * CC(0, 2, k);
+    CH(0, k, 2) = cr2 + ci3;
+    CH(0, k, 1) = cr2 - ci3;
+  }
+  if (ido == 1) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double tr2 = CC(i - 1, 2, k) + CC(ic - 1, 1, k);
+    const double ti2 = CC(i, 2, k) - CC(ic, 1, k);
+    const double cr2 = CC(i - 1, 0, k) + taur * tr2;
+    const double ci2 = CC(i, 0, k) + taur * ti2;
+    CH(i - 1, k, 0) = CC(i - 1, 0, k) + tr2;
+    CH(i, k, 0) = CC(i, 0, k) + ti2;
+    const double cr3 = taui * (CC(i - 1, 2, k) - CC(ic - 1, 1, k));
+    const double ci3 = taui * (CC(i, 2, k) + CC(ic, 1, k));
+    const double dr3 = cr2 + ci3, dr2 = cr2 - ci3;
+    const double di2 = ci2 + cr3, di3 = ci2 - cr3;
+    CH(i, k, 1) = WA(0, i - 2) * di2 + WA(0, i - 1) * dr2;
+    CH(i - 1, k, 1) = WA(0, i - 2) * dr2 - WA(0, i - 1) * di2;
+    CH(i, k, 2) = WA(1, i - 2) * di3 + WA(1, i - 1) * dr3;
+    CH(i - 1, k, 2) = WA(1, i - 2) * dr3 - WA(1, i - 1) * di3;
+  }
+}
+
+__device__ void radb4(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  constexpr int64_t IP = 4;
+  const double sqrt2 = 1.414213562373095048801688724209698;
+  PF_FOR(k, l1) {
+    const double tr2 = CC(0, 0, k) + CC(ido - 1, 3, k), tr1 = CC(0, 0, k) - CC(ido - 1, 3, k);
+    const double tr3 = 2 * CC(ido - 1, 1, k);
+    const double tr4 = 2 * CC(0, 2, k);
+    CH(0, k, 0) = tr2 + tr3;
+    CH(0, k, 2) = tr2 - tr3;
+    CH(0, k, 3) = tr1 + tr4;
+    CH(0, k, 1) = tr1 - tr4;
+    if ((ido & 1) == 0) {
+      const double ti1 = CC(0, 3, k) + CC(0, 1, k), ti2 = CC(0, 3, k) - CC(0, 1, k);
+      const double tr2b = CC(ido - 1, 0, k) + CC(ido - 1, 2, k), tr1b = CC(ido - 1, 0, k) - CC(ido - 1, 2, k);
+      CH(ido - 1, k, 0) = tr2b + tr2b;
+      CH(ido - 1, k, 1) = sqrt2 * (tr1b - ti1);
+      CH(ido - 1, k, 2) = ti2 + ti2;
+      CH(ido - 1, k, 3) = -sqrt2 * (tr1b + ti1);
+    }
+  }
+  if (ido <= 2) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double tr2 = CC(i - 1, 0, k) + CC(ic - 1, 3, k), tr1 = CC(i - 1, 0, k) - CC(ic - 1, 3, k);
+    const double ti1 = CC(i, 0, k) + CC(ic, 3, k), ti2 = CC(i, 0, k) - CC(ic, 3, k);
+    const double tr4 = CC(i, 2, k) + CC(ic, 1, k), ti3 = CC(i, 2, k) - CC(ic, 1, k);
+    const double tr3 = CC(i - 1, 2, k) + CC(ic - 1, 1, k), ti4 = CC(i - 1, 2, k) - CC(ic - 1, 1, k);
+    CH(i - 1, k, 0) = tr2 + tr3;
+    const double cr3 = tr2 - tr3;
+    CH(i, k, 0) = ti2 + ti3;
+    const double ci3 = ti2 - ti3;
+    const double cr4 = tr1 + tr4, cr2 = tr1 - tr4;
+    const double ci2 = ti1 + ti4, ci4 = ti1 - ti4;
+    CH(i, k, 1) = WA(0, i - 2) * ci2 + WA(0, i - 1) * cr2;
+    CH(i - 1, k, 1) = WA(0, i - 2) * cr2 - WA(0, i - 1) * ci2;
+    CH(i, k, 2) = WA(1, i - 2) * ci3 + WA(1, i - 1) * cr3;
+    CH(i - 1, k, 2) = WA(1, i - 2) * cr3 - WA(1, i - 1) * ci3;
+    CH(i, k, 3) = WA(2, i - 2) * ci4 + WA(2, i - 1) * cr4;
+    CH(i - 1, k, 3) = WA(2, i - 2) * cr4 - WA(2, i - 1) * ci4;
+  }
+}
+
+__device__ void radb5(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+  constexpr int64_t IP = 5;
+  const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
+  const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
+  PF_FOR(k, l1) {
+    const double ti5 = CC(0, 2, k) + CC(0, 2, k);
+    const double ti4 = CC(0, 4, k) + CC(0, 4, k);
+    const double tr2 = CC(ido - 1, 1, k) + CC(ido - 1, 1, k);
+    const double tr3 = CC(ido - 1, 3, k) + CC(ido - 1, 3, k);
+    CH(0, k, 0) = CC(0, 0, k) + tr2 + tr3;
+    const double cr2 = CC(0, 0, k) + tr11 * tr2 + tr12 * tr3;
+    const double cr3 = CC(0, 0, k) + tr12 * tr2 + tr11 * tr3;
+    const double ci5 = ti5 * ti11 + ti4 * ti12, ci4 = ti5 * ti12 - ti4 * ti11;
+    CH(0, k, 4) = cr2 + ci5;
+    CH(0, k, 1) = cr2 - ci5;
+    CH(0, k, 3) = cr3 + ci4;
+    CH(0, k, 2) = cr3 - ci4;
+  }
+  if (ido == 1) return;
+  const int64_t hi = (ido - 1) / 2;
+  PF_FOR(t, l1 * hi) {
+    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double tr2 = CC(i - 1, 2, k) + CC(ic - 1, 1, k), tr5 = CC(i - 1, 2, k) - CC(ic - 1, 1, k);
+    const double ti5 = CC(i, 2, k) + CC(ic, 1, k), ti2 = CC(i, 2, k) - CC(ic, 1, k);
+    const double tr3 = CC(i - 1, 4, k) + CC(ic - 1, 3, k), tr4 = CC(i - 1, 4, k) - CC(ic - 1, 3, k);
+    const double ti4 = CC(i, 4, k) + CC(ic, 3, k), ti3 = CC(i, 4, k) - CC(ic, 3, k);
+    CH(i - 1, k, 0) = CC(i - 1, 0, k) + tr2 + tr3;
+    CH(i, k, 0) = CC(i, 0, k) + ti2 + ti3;
+    const double cr2 = CC(i - 1, 0, k) + tr11 * tr2 + tr12 * tr3;
+    const double ci2 = CC(i, 0, k) + tr11 * ti2 + tr12 * ti3;
+    const double cr3 = CC(i - 1, 0, k) + tr12 * tr2 + tr11 * tr3;
+    const double ci3 = CC(i, 0, k) + tr12 * ti2 + tr11 * ti3;
+    const double cr5 = tr5 * ti11 + tr4 * ti12, cr4 = tr5 * ti12 - tr4 * ti11;
+    const double ci5 = ti5 * ti11 + ti4 * ti12, ci4 = ti5 * ti12 - ti4 * ti11;
+    const double dr4 = cr3 + ci4, dr3 = cr3 - ci4;
+    const double di3 = ci3 + cr4, di4 = ci3 - cr4;
+    const double dr5 = cr2 + ci5, dr2 = cr2 - ci5;
+    const double di2 = ci2 + cr5, di5 = ci2 - cr5;
+    CH(i, k, 1) = WA(0, i - 2) * di2 + WA(0, i - 1) * dr2;
+    CH(i - 1, k, 1) = WA(0, i - 2) * dr2 - WA(0, i - 1) * di2;
+    CH(i, k, 2) = WA(1, i - 2) * di3 + WA(1, i - 1) * dr3;
+    CH(i - 1, k, 2) = WA(1, i - 2) * dr3 - WA(1, i - 1) * di3;
+    CH(i, k, 3) = WA(2, i - 2) * di4 + WA(2, i - 1) * dr4;
+    CH(i - 1, k, 3) = WA(2, i - 2) * dr4 - WA(2, i - 1) * di4;
+    CH(i, k, 4) = WA(3, i - 2) * di5 + WA(3, i - 1) * dr5;
+    CH(i - 1, k, 4) = WA(3, i - 2) * dr5 - WA(3, i - 1) * di5;
+  }
+}
+#undef CC
+#undef CH
+#undef WA
+
+// generic backward pass (ip odd > 5, ido odd): the result lands in ch
+__device__ void radbg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* ch, const double* wa,
+                      const double* csarr) {
+  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+#define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
+#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+#define C1(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
+#define C2(a, b) cc[(a) + idl1 * (b)]
+#define CH2(a, b) ch[(a) + idl1 * (b)]
+  const int64_t hp = (ido - 1) / 2;
+  // phase 1: unpack the halfcomplex columns into CH
+  PF_FOR(t, l1 * ido) {
+    const int64_t k = t / ido, i = t - k * ido;
+    CH(i, k, 0) = CC(i, 0, k);
+  }
+  PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
+    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+                  q = r - k * (hp + 1), jc = ip - j, j2 = 2 * j - 1;
+    if (q == 0) {
+      CH(0, k, j) = 2 * CC(ido - 1, j2, k);
+      CH(0, k, jc) = 2 * CC(0, j2 + 1, k);
+    } else {
+      const int64_t i = 2 * q - 1, ic = ido - i - 2;
+      CH(i, k, j) = CC(i, j2 + 1, k) + CC(ic, j2, k);
+      CH(i, k, jc) = CC(i, j2 + 1, k) - CC(ic, j2, k);
+      CH(i + 1, k, j) = CC(i + 1, j2 + 1, k) - CC(ic + 1, j2, k);
+      CH(i + 1, k, jc) = CC(i + 1, j2 + 1, k) + CC(ic + 1, j2, k);
+    }
+  }
+  __syncthreads();
+  // phase 2: the column DFT (into C2, columns >= 1), then CH2 column 0's sum
+  PF_FOR(ik, idl1) {
+    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+      double a = CH2(ik, 0) + csarr[2 * l] * CH2(ik, 1) + csarr[4 * l] * CH2(ik, 2);
+      double b = csarr[2 * l + 1] * CH2(ik, ip - 1) + csarr[4 * l + 1] * CH2(ik, ip - 2);
+      int64_t iang = 2 * l;
+      int64_t j = 3, jc = ip - 3;
+      for (; j < ipph - 3; j += 4, jc -= 4) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar1 = csarr[2 * iang], ai1 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar2 = csarr[2 * iang], ai2 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar3 = csarr[2 * iang], ai3 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar4 = csarr[2 * iang], ai4 = csarr[2 * iang + 1];
+        a += ar1 * CH2(ik, j) + ar2 * CH2(ik, j + 1) + ar3 * CH2(ik, j + 2) + ar4 * CH2(ik, j + 3);
+        b += ai1 * CH2(ik, jc) + ai2 * CH2(ik, jc - 1) + ai3 * CH2(ik, jc - 2) + ai4 * CH2(ik, jc - 3);
+      }
+      for (; j < ipph - 1; j += 2, jc -= 2) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar1 = csarr[2 * iang], ai1 = csarr[2 * iang + 1];
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double ar2 = csarr[2 * iang], ai2 = csarr[2 * iang + 1];
+        a += ar1 * CH2(ik, j) + ar2 * CH2(ik, j + 1);
+        b += ai1 * CH2(ik, jc) + ai2 * CH2(ik, jc - 1);
+      }
+      for (; j < ipph; ++j, --jc) {
+        iang += l;
+        if (iang > ip) iang -= ip;
+        const double war = csarr[2 * iang], wai = csarr[2 * iang + 1];
+        a += war * CH2(ik, j);
+        b += wai * CH2(ik, jc);
+      }
+      C2(ik, l) = a;
+      C2(ik, lc) = b;
+    }
+    double s = CH2(ik, 0);
+    for (int64_t j = 1; j < ipph; ++j) s += CH2(ik, j);
+    CH2(ik, 0) = s;
+  }
+  __syncthreads();
+  // phase 3: recombine the pairs into CH, then the twiddles (same thread, same elements)
+  PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
+    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+                  q = r - k * (hp + 1), jc = ip - j;
+    if (q == 0) {
+      CH(0, k, jc) = C1(0, k, j) + C1(0, k, jc);
+      CH(0, k, j) = C1(0, k, j) - C1(0, k, jc);
+    } else {
+      const int64_t i = 2 * q - 1;
+      const double a = C1(i, k, j) - C1(i + 1, k, jc), b = C1(i, k, j) + C1(i + 1, k, jc);
+      const double c = C1(i + 1, k, j) + C1(i, k, jc), d = C1(i + 1, k, j) - C1(i, k, jc);
+      const int64_t is = (j - 1) * (ido - 1) + (i - 1), isc = (jc - 1) * (ido - 1) + (i - 1);
+      CH(i, k, j) = wa[is] * a - wa[is + 1] * c;
+      CH(i + 1, k, j) = wa[is] * c + wa[is + 1] * a;
+      CH(i, k, jc) = wa[isc] * b - wa[isc + 1] * d;
+      CH(i + 1, k, jc) = wa[isc] * d + wa[isc + 1] * b;
+    }
+  }
+#undef CC
+#undef CH
+#undef C1
+#undef C2
+#undef CH2
+}
+
+// c (P.len) in place, scratch ch (P.len); r2hc: forward (halfcomplex out), else backward
+__device__ void rfftp(const PfPasses& P, const double* pool, double* c, double* ch, double fct, bool r2hc) {
+  const int64_t n = P.len;
+  if (n == 1) {
+    if (threadIdx.x == 0) c[0] *= fct;
+    __syncthreads();
+    return;
+  }
+  double *p1 = c, *p2 = ch;
+  for (int k1 = 0; k1 < P.nf; ++k1) {
+    const int k = r2hc ? P.nf - k1 - 1 : k1;
+    const PfFact F = P.f[k];
+    const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
+    const double* ws = pool + (F.tws >= 0 ? F.tws : 0);
+    bool swap = true;
+    if (r2hc) {
+      switch (F.ip) {
+        case 4: radf4(F.ido, F.l1, p1, p2, wa); break;
+        case 2: radf2(F.ido, F.l1, p1, p2, wa); break;
+        case 3: radf3(F.ido, F.l1, p1, p2, wa); break;
+        case 5: radf5(F.ido, F.l1, p1, p2, wa); break;
+        default: radfg(F.ido, F.ip, F.l1, p1, p2, wa, ws); swap = false;
+      }
+    } else {
+      switch (F.ip) {
+        case 4: radb4(F.ido, F.l1, p1, p2, wa); break;
+        case 2: radb2(F.ido, F.l1, p1, p2, wa); break;
+        case 3: radb3(F.ido, F.l1, p1, p2, wa); break;
+        case 5: radb5(F.ido, F.l1, p1, p2, wa); break;
+        default: radbg(F.ido, F.ip, F.l1, p1, p2, wa, ws);
+      }
+    }
+    if (swap) {
+      double* t = p1;
+      p1 = p2;
+      p2 = t;
+    }
+    __syncthreads();
+  }
+  // copy_and_norm
+  if (p1 != c) {
+    PF_FOR(i, n) c[i] = fct != 1.0 ? fct * p1[i] : p1[i];
+  } else if (fct != 1.0) {
+    PF_FOR(i, n) c[i] *= fct;
+  }
+  __syncthreads();
+}
+
+// ============================ Bluestein =====================================
+template <bool FWD>
+__device__ void blue_fft(const PfBlue& B, const double* pool, Cx* c, Cx* akf, Cx* ch, double fct) {
+  const int64_t n = B.n, n2 = B.n2;
+  const Cx* bk = reinterpret_cast<const Cx*>(pool + B.bk);
+  const Cx* bkf = reinterpret_cast<const Cx*>(pool + B.bkf);
+  const Cx zero = scale(smul<FWD>(c[0], bk[0]), 0.);
+  PF_FOR(m, n2) akf[m] = m < n ? smul<FWD>(c[m], bk[m]) : zero;
+  __syncthreads();
+  cfftp<true>(B.plan, pool, akf, ch, 1.);
+  // the convolution
+  PF_FOR(m, n2) akf[m] = smul<!FWD>(akf[m], bkf[2 * m <= n2 ? m : n2 - m]);
+  __syncthreads();
+  cfftp<false>(B.plan, pool, akf, ch, 1.);
+  PF_FOR(m, n) c[m] = scale(smul<FWD>(akf[m], bk[m]), fct);
+  __syncthreads();
+}
+
+// exec_r: real data through the complex Bluestein transform; tmp: n complex
+__device__ void blue_r(const PfBlue& B, const double* pool, double* c, Cx* tmp, Cx* akf, Cx* ch, double fct,
+                       bool r2hc) {
+  const int64_t n = B.n;
+  if (r2hc) {
+    const double zero = 0. * c[0];
+    PF_FOR(m, n) tmp[m] = {c[m], zero};
+    __syncthreads();
+    blue_fft<true>(B, pool, tmp, akf, ch, fct);
+    PF_FOR(m, n) c[m] = m == 0 ? tmp[0].r : ((m & 1) ? tmp[(m + 1) / 2].r : tmp[m / 2].i);
+    __syncthreads();
+  } else {
+    // tmp[0] = (c0, c0 * 0); tmp[k] = (c[2k-1], c[2k]); n even: tmp[n/2].i = 0 * c0
+    PF_FOR(k, n / 2 + 1) {
+      Cx v;
+      if (k == 0) v = {c[0], c[0] * 0.};
+      else if (2 * k == n) v = {c[n - 1], 0. * c[0]};
+      else v = {c[2 * k - 1], c[2 * k]};
+      tmp[k] = v;
+    }
+    __syncthreads();
+    PF_FOR(m, (n - 1) / 2) {
+      const int64_t q = m + 1;   // 2q < n
+      tmp[n - q] = {tmp[q].r, -tmp[q].i};
+    }
+    __syncthreads();
+    blue_fft<false>(B, pool, tmp, akf, ch, fct);
+    PF_FOR(m, n) c[m] = tmp[m].r;
+    __syncthreads();
+  }
+}
+
+// ============================ entry points ==================================
+// per-transform scratch (pocketfft.h pf_scratch_doubles): a (2n), x (2n), and
+// for Bluestein akf, ch2 (2 n2 each)
+struct PfScratch {
+  double* a;
+  Cx* x;
+  Cx* akf;
+  Cx* ch2;
+};
+__device__ inline PfScratch pf_scratch(const PfLen& L, double* slot) {
+  PfScratch s;
+  s.a = slot;
+  s.x = reinterpret_cast<Cx*>(slot + 2 * L.n);
+  s.akf = reinterpret_cast<Cx*>(slot + 4 * L.n);
+  s.ch2 = reinterpret_cast<Cx*>(slot + 4 * L.n + 2 * ((L.rblue || L.cblue) ? L.bl.n2 : 0));
+  return s;
+}
+
+// scipy.fft.rfft's pocketfft_r forward on c (n reals, in place -> halfcomplex)
+__device__ inline void pf_r2hc(const PfLen& L, const double* pool, double* c, const PfScratch& s, double fct) {
+  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, true);
+  else rfftp(L.r, pool, c, s.a, fct, true);
+}
+// pocketfft_r backward on c (halfcomplex in place -> n reals)
+__device__ inline void pf_hc2r(const PfLen& L, const double* pool, double* c, const PfScratch& s, double fct) {
+  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, false);
+  else rfftp(L.r, pool, c, s.a, fct, false);
+}
+// pocketfft_c backward on c (n complex, in place); c must not be s.x when Bluestein
+__device__ inline void pf_c2c_bwd(const PfLen& L, const double* pool, Cx* c, const PfScratch& s, double fct) {
+  if (L.cblue) blue_fft<false>(L.bl, pool, c, s.akf, s.ch2, fct);
+  else cfftp<false>(L.c, pool, c, reinterpret_cast<Cx*>(s.a), fct);
+}
+
+// |scipy.signal.hilbert(f)| of one real row (modem.py:309, 315): f (n) is
+// overwritten by its halfcomplex spectrum, env (n) receives the envelope
+// (env may be f).  fct = double(1 / long double n).
+__device__ inline void pf_hilbert_env(const PfLen& L, const double* pool, double* f, double* env, double* slot,
+                                      double fct) {
+  const int64_t n = L.n;
+  const PfScratch s = pf_scratch(L, slot);
+  pf_r2hc(L, pool, f, s, 1.0);
+  // the spectrum as pypocketfft's c2c_sym leaves it (bins 0..n/2 from r2c,
+  // conjugated into n - i -- bins 0 and n/2 onto themselves, imaginary -0.0),
+  // times scipy's h with numpy's FMA complex multiply -> x
+  Cx* X = s.x;
+  PF_FOR(i, n) {
+    double xr, xi;
+    if (i == 0) { xr = f[0]; xi = -0.0; }
+    else if (2 * i == n) { xr = f[n - 1]; xi = -0.0; }
+    else if (2 * i < n) { xr = f[2 * i - 1]; xi = f[2 * i]; }
+    else { xr = f[2 * (n - i) - 1]; xi = -f[2 * (n - i)]; }
+    const double hr = (i == 0 || 2 * i == n) ? 1.0 : (2 * i < n ? 2.0 : 0.0), hi = 0.0;
+    X[i] = {__builtin_fma(xr, hr, -(xi * hi)), __builtin_fma(xr, hi, xi * hr)};
+  }
+  __syncthreads();
+  // ifft: pocketfft_c backward, times 1/n; then numpy's complex abs
+  if (L.cblue) {
+    blue_fft<false>(L.bl, pool, X, s.akf, s.ch2, fct);
+  } else {
+    cfftp<false>(L.c, pool, X, reinterpret_cast<Cx*>(s.a), fct);
+  }
+  PF_FOR(i, n) {
+    const double ar = fabs(X[i].r), ai = fabs(X[i].i);
+    const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
+    env[i] = h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0));
+  }
+  __syncthreads();
+}
+
+#undef PF_FOR
+
+}  // namespace pf
+}  // namespace amr

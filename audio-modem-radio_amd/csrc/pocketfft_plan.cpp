@@ -1,0 +1,332 @@
+// pocketfft_plan.cpp -- host construction of the device pocketfft plans
+// (pocketfft.h): pocketfft's plan choice, factorisations and twiddle tables
+// (sincos_2pibyn), by the rules oracle/amr_pocketfft.c restates and pins
+// against scipy 1.15.3.  Host code; compiled by hipcc.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <vector>
+
+#include "pocketfft.h"
+
+namespace amr {
+namespace {
+
+// pocketfft's sincos_2pibyn(n): W_n^k = v1[k & mask] * v2[k >> shift],
+// entries from libm cos / sin by octant, ang = double(0.25L * pi / n)
+struct Twid2pi {
+  int64_t n = 0, mask = 0, shift = 0;
+  std::vector<double2> v1, v2;
+  static double2 calc(int64_t x, int64_t n, double ang) {
+    x <<= 3;
+    if (x < 4 * n) {
+      if (x < 2 * n) {
+        if (x < n) return make_double2(std::cos((double)x * ang), std::sin((double)x * ang));
+        return make_double2(std::sin((double)(2 * n - x) * ang), std::cos((double)(2 * n - x) * ang));
+      }
+      x -= 2 * n;
+      if (x < n) return make_double2(-std::sin((double)x * ang), std::cos((double)x * ang));
+      return make_double2(-std::cos((double)(2 * n - x) * ang), std::sin((double)(2 * n - x) * ang));
+    }
+    x = 8 * n - x;
+    if (x < 2 * n) {
+      if (x < n) return make_double2(std::cos((double)x * ang), -std::sin((double)x * ang));
+      return make_double2(std::sin((double)(2 * n - x) * ang), -std::cos((double)(2 * n - x) * ang));
+    }
+    x -= 2 * n;
+    if (x < n) return make_double2(-std::sin((double)x * ang), -std::cos((double)x * ang));
+    return make_double2(-std::cos((double)(2 * n - x) * ang), -std::sin((double)(2 * n - x) * ang));
+  }
+  explicit Twid2pi(int64_t len) : n(len) {
+    const double ang = (double)(0.25L * 3.141592653589793238462643383279502884197L / (long double)len);
+    const int64_t nval = (len + 2) / 2;
+    shift = 1;
+    while (((int64_t)1 << shift) * ((int64_t)1 << shift) < nval) ++shift;
+    mask = ((int64_t)1 << shift) - 1;
+    v1.resize((size_t)(mask + 1));
+    v1[0] = make_double2(1.0, 0.0);
+    for (int64_t i = 1; i <= mask; ++i) v1[(size_t)i] = calc(i, len, ang);
+    v2.resize((size_t)((nval + mask) / (mask + 1)));
+    v2[0] = make_double2(1.0, 0.0);
+    for (size_t i = 1; i < v2.size(); ++i) v2[i] = calc((int64_t)i * (mask + 1), len, ang);
+  }
+  double2 operator[](int64_t idx) const {
+    const bool hi = 2 * idx > n;
+    if (hi) idx = n - idx;
+    const double2 a = v1[(size_t)(idx & mask)], b = v2[(size_t)(idx >> shift)];
+    const double re = a.x * b.x - a.y * b.y, im = a.x * b.y + a.y * b.x;
+    return make_double2(re, hi ? -im : im);
+  }
+};
+
+int64_t largest_prime_factor(int64_t n) {
+  int64_t res = 1;
+  while ((n & 1) == 0) {
+    res = 2;
+    n >>= 1;
+  }
+  for (int64_t x = 3; x * x <= n; x += 2)
+    while (n % x == 0) {
+      res = x;
+      n /= x;
+    }
+  if (n > 1) res = n;
+  return res;
+}
+
+double cost_guess(int64_t n) {
+  const double lfp = 1.1;   // pocketfft's penalty for non-hardcoded larger factors
+  const int64_t ni = n;
+  double result = 0.;
+  while ((n & 1) == 0) {
+    result += 2;
+    n >>= 1;
+  }
+  for (int64_t x = 3; x * x <= n; x += 2)
+    while (n % x == 0) {
+      result += (x <= 5) ? (double)x : lfp * (double)x;
+      n /= x;
+    }
+  if (n > 1) result += (n <= 5) ? (double)n : lfp * (double)n;
+  return result * (double)ni;
+}
+
+// the smallest 2^a 3^b 5^c 7^d 11^e >= n
+int64_t good_size_cmplx(int64_t n) {
+  if (n <= 12) return n;
+  int64_t best = 2 * n;
+  for (int64_t f11 = 1; f11 < best; f11 *= 11)
+    for (int64_t f117 = f11; f117 < best; f117 *= 7)
+      for (int64_t f1175 = f117; f1175 < best; f1175 *= 5) {
+        int64_t x = f1175;
+        while (x < n) x *= 2;
+        for (;;) {
+          if (x < n) {
+            x *= 3;
+          } else if (x > n) {
+            if (x < best) best = x;
+            if (x & 1) break;
+            x >>= 1;
+          } else {
+            return n;
+          }
+        }
+      }
+  return best;
+}
+
+bool use_bluestein(int64_t n, bool real) {
+  const int64_t tmp = n < 50 ? 0 : largest_prime_factor(n);
+  if (tmp * tmp <= n) return false;
+  const double comp1 = real ? 0.5 * cost_guess(n) : cost_guess(n);
+  const double comp2 = 2 * cost_guess(good_size_cmplx(2 * n - 1)) * 1.5;
+  return comp2 < comp1;
+}
+
+int factorize(int64_t n, bool with8, int64_t* f) {
+  int nf = 0;
+  if (with8)
+    while ((n & 7) == 0) {
+      f[nf++] = 8;
+      n >>= 3;
+    }
+  while ((n & 3) == 0) {
+    f[nf++] = 4;
+    n >>= 2;
+  }
+  if ((n & 1) == 0) {
+    n >>= 1;
+    f[nf++] = 2;
+    std::swap(f[0], f[nf - 1]);
+  }
+  for (int64_t d = 3; d * d <= n; d += 2)
+    while (n % d == 0) {
+      f[nf++] = d;
+      n /= d;
+    }
+  if (n > 1) f[nf++] = n;
+  return nf;
+}
+
+void align2(std::vector<double>& pool) {
+  if (pool.size() & 1) pool.push_back(0.0);
+}
+
+// pocketfft's cfftp(len): factors and twiddles
+bool build_cfftp(int64_t len, PfPasses& P, std::vector<double>& pool) {
+  P = PfPasses{};
+  P.len = len;
+  if (len == 1) return true;
+  int64_t f[64];
+  const int nf = factorize(len, true, f);
+  if (nf > kPfMaxF) return false;
+  P.nf = nf;
+  const Twid2pi comp(len);
+  int64_t l1 = 1;
+  for (int k = 0; k < nf; ++k) {
+    const int64_t ip = f[k], ido = len / (l1 * ip);
+    PfFact& F = P.f[k];
+    F.ip = ip;
+    F.l1 = l1;
+    F.ido = ido;
+    align2(pool);
+    F.tw = (int64_t)pool.size();
+    for (int64_t j = 1; j < ip; ++j)
+      for (int64_t i = 1; i < ido; ++i) {
+        const double2 w = comp[j * l1 * i];
+        pool.push_back(w.x);
+        pool.push_back(w.y);
+      }
+    F.tws = -1;
+    if (ip > 11) {
+      F.tws = (int64_t)pool.size();
+      for (int64_t j = 0; j < ip; ++j) {
+        const double2 w = comp[j * l1 * ido];
+        pool.push_back(w.x);
+        pool.push_back(w.y);
+      }
+    }
+    l1 *= ip;
+  }
+  return true;
+}
+
+// pocketfft's rfftp(len): factors, twiddles and the generic passes' tables
+bool build_rfftp(int64_t len, PfPasses& P, std::vector<double>& pool) {
+  P = PfPasses{};
+  P.len = len;
+  if (len == 1) return true;
+  int64_t f[64];
+  const int nf = factorize(len, false, f);
+  if (nf > kPfMaxF) return false;
+  P.nf = nf;
+  const Twid2pi twid(len);
+  int64_t l1 = 1;
+  for (int k = 0; k < nf; ++k) {
+    const int64_t ip = f[k], ido = len / (l1 * ip);
+    PfFact& F = P.f[k];
+    F.ip = ip;
+    F.l1 = l1;
+    F.ido = ido;
+    F.tw = F.tws = -1;
+    if (k < nf - 1) {   // the last factor needs no twiddles
+      F.tw = (int64_t)pool.size();
+      std::vector<double> t((size_t)((ip - 1) * (ido - 1)), 0.0);
+      for (int64_t j = 1; j < ip; ++j)
+        for (int64_t i = 1; i <= (ido - 1) / 2; ++i) {
+          const double2 w = twid[j * l1 * i];
+          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 2)] = w.x;
+          t[(size_t)((j - 1) * (ido - 1) + 2 * i - 1)] = w.y;
+        }
+      pool.insert(pool.end(), t.begin(), t.end());
+    }
+    if (ip > 5) {   // the generic passes' factors
+      F.tws = (int64_t)pool.size();
+      std::vector<double> t((size_t)(2 * ip), 0.0);
+      t[0] = 1.;
+      t[1] = 0.;
+      for (int64_t i = 2, ic = 2 * ip - 2; i <= ic; i += 2, ic -= 2) {
+        const double2 w = twid[i / 2 * (len / ip)];
+        t[(size_t)i] = w.x;
+        t[(size_t)(i + 1)] = w.y;
+        t[(size_t)ic] = w.x;
+        t[(size_t)(ic + 1)] = -w.y;
+      }
+      pool.insert(pool.end(), t.begin(), t.end());
+    }
+    l1 *= ip;
+  }
+  return true;
+}
+
+// pocketfft's fftblue(n) without bkf (pf_finish)
+bool build_blue(int64_t n, PfBlue& B, std::vector<double>& pool) {
+  B = PfBlue{};
+  B.n = n;
+  B.n2 = good_size_cmplx(n * 2 - 1);
+  if (!build_cfftp(B.n2, B.plan, pool)) return false;
+  const Twid2pi tmp(2 * n);
+  align2(pool);
+  B.bk = (int64_t)pool.size();
+  pool.push_back(1.0);
+  pool.push_back(0.0);
+  int64_t coeff = 0;
+  for (int64_t m = 1; m < n; ++m) {
+    coeff += 2 * m - 1;
+    if (coeff >= 2 * n) coeff -= 2 * n;
+    const double2 w = tmp[coeff];
+    pool.push_back(w.x);
+    pool.push_back(w.y);
+  }
+  B.bkf = (int64_t)pool.size();
+  pool.resize(pool.size() + (size_t)(2 * (B.n2 / 2 + 1)), 0.0);
+  return true;
+}
+
+}  // namespace
+
+bool pf_len_build(int64_t n, PfLen& L, std::vector<double>& pool) {
+  if (n < 1) return false;
+  L = PfLen{};
+  L.n = n;
+  L.rblue = use_bluestein(n, true);
+  L.cblue = use_bluestein(n, false);
+  if (!L.rblue && !build_rfftp(n, L.r, pool)) return false;
+  if (!L.cblue && !build_cfftp(n, L.c, pool)) return false;
+  if ((L.rblue || L.cblue) && !build_blue(n, L.bl, pool)) return false;
+  align2(pool);
+  return true;
+}
+
+int64_t pf_scratch_doubles(const PfLen& L) {
+  return 4 * L.n + ((L.rblue || L.cblue) ? 4 * L.bl.n2 : 0);
+}
+
+int64_t pf_scratch_doubles_n(int64_t n) {
+  const bool blue = use_bluestein(n, true) || use_bluestein(n, false);
+  return 4 * n + (blue ? 4 * good_size_cmplx(2 * n - 1) : 0);
+}
+
+namespace {
+int64_t cfftp_doubles(int64_t len) {
+  if (len == 1) return 0;
+  int64_t f[64];
+  const int nf = factorize(len, true, f);
+  int64_t d = 0, l1 = 1;
+  for (int k = 0; k < nf; ++k) {
+    const int64_t ip = f[k], ido = len / (l1 * ip);
+    d += 1 + 2 * (ip - 1) * (ido - 1) + (ip > 11 ? 2 * ip : 0);
+    l1 *= ip;
+  }
+  return d;
+}
+int64_t rfftp_doubles(int64_t len) {
+  if (len == 1) return 0;
+  int64_t f[64];
+  const int nf = factorize(len, false, f);
+  int64_t d = 0, l1 = 1;
+  for (int k = 0; k < nf; ++k) {
+    const int64_t ip = f[k], ido = len / (l1 * ip);
+    d += (k < nf - 1 ? (ip - 1) * (ido - 1) : 0) + (ip > 5 ? 2 * ip : 0);
+    l1 *= ip;
+  }
+  return d;
+}
+}  // namespace
+
+int64_t pf_pool_doubles_bound(int64_t n) {
+  const bool rb = use_bluestein(n, true), cb = use_bluestein(n, false);
+  int64_t d = 8 + (rb ? 0 : rfftp_doubles(n)) + (cb ? 0 : cfftp_doubles(n));
+  if (rb || cb) {
+    const int64_t n2 = good_size_cmplx(2 * n - 1);
+    d += cfftp_doubles(n2) + 2 + 2 * n + 2 * (n2 / 2 + 1);
+  }
+  return d;
+}
+
+int64_t pf_resample_slot_doubles(const PfLen& Lx, const PfLen& Ly) {
+  // the row (max n) + one transform's scratch at a time
+  return std::max(Lx.n, Ly.n) + std::max(pf_scratch_doubles(Lx), pf_scratch_doubles(Ly));
+}
+
+}  // namespace amr

@@ -57,7 +57,8 @@
 extern "C" {
 #endif
 
-#define AMR_ABI_VERSION 1
+#define AMR_ABI_VERSION 2   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
+                                 amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -200,13 +201,17 @@ int amr_psk_slice_host(int kind, const double *sym, int64_t n_streams, int64_t n
  * mark_* space_* butter(3, [(f-baud)/nyq, (f+baud)/nyq], 'band') b, a and
  *               lfilter_zi (ntaps each, a[0] == 1)              modem.py:307
  * The envelopes |hilbert(filtfilt(...))| (modem.py:308-309) use a double-precision
- * FFT of length n_samples (mixed radix 2/3/4/5, Bluestein otherwise).
+ * FFT of length n_samples (mixed radix 2/3/4/5, Bluestein otherwise); a stream
+ * with a compare the two envelopes' rounding could flip is recomputed exactly
+ * (scipy's filtfilt order, pocketfft's transforms), so the decided bytes are
+ * the reference's at every length.
  */
 #define AMR_TF_BANDPASS 0     /* both tones' filtfilt */
 #define AMR_TF_HILBERT 1      /* FFT, -i*sgn(k), inverse FFT, both envelopes and the compare */
 #define AMR_TF_DECIDE 2       /* window majority, sync and pack */
 #define AMR_TF_LAUNCH 3       /* the whole launch (-> gathered with amr_fsk_allgather), as AMR_T_LAUNCH */
-#define AMR_TF_COUNT 4
+#define AMR_TF_EXACT 4        /* the exact path over the streams F2 flagged (list, filtfilt, envelopes, bits) */
+#define AMR_TF_COUNT 5
 
 typedef struct amr_fsk_plan amr_fsk_plan;
 
@@ -226,6 +231,12 @@ int64_t amr_fsk_plan_fft_length(const amr_fsk_plan *plan);
 int amr_fsk_plan_live_columns(const amr_fsk_plan *plan);
 int amr_fsk_plan_synchronize(amr_fsk_plan *plan);
 int amr_fsk_plan_enable_timing(amr_fsk_plan *plan, int on);
+/* the exact path: 0 off (the fast path's bits everywhere -- a diagnostic; decided
+ * bytes may then differ from the reference where F2 would have flagged), 1 the
+ * streams F2 flags (the default), 2 every stream (tests, timing) */
+int amr_fsk_plan_set_exact_mode(amr_fsk_plan *plan, int mode);
+/* number of streams the exact path recomputed in the last call (synchronises the plan's stream) */
+int amr_fsk_plan_exact_streams(amr_fsk_plan *plan, int64_t *count);
 /* milliseconds of each AMR_TF_* stage in the last call (-1 = not run) */
 int amr_fsk_plan_timings(amr_fsk_plan *plan, float *ms, int count);
 /* Same contracts as amr_psk_demod_host / _device. */
@@ -249,10 +260,15 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
 int amr_fft_c2c_host(const double *in, double *out, int64_t n, int64_t batch, int inverse, int device);
 int amr_hilbert_host(const double *x, double *analytic, int64_t n, int64_t batch, int device);
 /* scipy.signal.resample(x, num) of each real row (x: [batch][nx] -> y: [batch][num]),
- * as decoder.decode_wav_file calls it (decoder.py:385-387): FFT, the
- * reference's spectrum truncation / zero-padding with its Nyquist-bin rule,
- * inverse FFT, times num/nx.  Lengths past the two-pass FFT limit run six-step. */
+ * as decoder.decode_wav_file calls it (decoder.py:385-387), bit for bit:
+ * pocketfft's rfft (every radix, Bluestein), the reference's spectrum
+ * truncation / zero-padding with its Nyquist-bin rule, pocketfft's irfft,
+ * times num/nx (pocketfft_dev.h). */
 int amr_resample_host(const double *x, int64_t nx, int64_t num, int64_t batch, double *y, int device);
+/* |scipy.signal.hilbert(x)| of each real row (x: [batch][n] -> env), evaluated
+ * as pocketfft + numpy do, bit for bit (the FSK exact path's envelope stage,
+ * modem.py:309; a diagnostic entry for tests) */
+int amr_hilbert_env_exact_host(const double *x, int64_t n, int64_t batch, double *env, int device);
 
 /* ---- FEC (fec.py:34-69) -----------------------------------------------------
  * in: [n][in_stride] bytes, in_len[n]; out: [n][out_stride] (>= in_len each);

@@ -13,9 +13,13 @@ Committed data only:
 tests/test_oracle_golden.py pins the oracle to these on the CPU;
 tests/test_gpu_sweep.py checks the GPU against them.  FSK inputs keep a
 noise floor, and 12 extra FSK cases sit between stretches of exact digital
-silence (params.silence): there only pocketfft's own rounding decides
-(DESIGN.md §2 item 6) -- the oracle, which restates it, must match them;
-the GPU is held to them only outside that ambiguity.
+silence at 5-smooth lengths (params.silence): there only pocketfft's own
+rounding decides.  Round 4 appends 16 more (their own
+seed, so the first 84 cases are unchanged) at lengths with a prime factor
+above 5 -- Bluestein and generic-radix plans in pocketfft -- with digital
+silence, a DC (constant) stretch or a stretch 1e-17 below the signal
+(params.quiet).  The oracle and the GPU (through its exact path) must match
+all of them.
 
 Run:  python tests/golden/make_sweep_golden.py   (needs /root/reference)
 """
@@ -99,10 +103,41 @@ def draw_silence(rng):
     return "fsk", dict(baud=baud, f0=f0, f1=f1, samp_rate=fs, silence=True), x
 
 
+N_QUIET = 16
+QUIET_LENGTHS = [24001, 30011, 77880, 9601, 19207, 12347, 96001, 29999, 14007, 50021, 21001, 7919, 33033, 47999,
+                 96017, 11011]
+
+
+def draw_quiet(rng, i):
+    """FSK at a length with a prime factor above 5, next to a stretch whose
+    envelopes sink to rounding level: exact digital silence, a DC offset
+    (butter(3, band) cancels constants) or a stretch 1e-17 below the signal."""
+    fs = 96000.0
+    baud = int(rng.choice([1200, 2400, 4800, 9600]))
+    f0, f1 = sorted(round(float(v), 3) for v in rng.uniform(baud * 1.1, fs / 2 - baud * 1.1, 2))
+    n = QUIET_LENGTHS[i]
+    quiet = ["silence", "dc", "tiny", "silence"][i % 4]
+    fr = synth.random_frame(rng, int(rng.integers(4, 24)))
+    w = synth.fsk_waveform(fr, baud, f0, f1, fs)
+    off = int(rng.integers(n // 8, n // 3))
+    x = np.zeros(n)
+    seg = w[:max(0, n - off)]
+    x[off:off + seg.size] = seg
+    if quiet == "dc":
+        x[:off] = float(rng.choice([0.25, -3.0 / 32768, 1e-3]))
+    elif quiet == "tiny":
+        x[:off] = rng.normal(0, 1e-17, off)
+    dt = str(rng.choice(["float32", "float64", "int16"])) if quiet != "tiny" else "float64"
+    x = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16) if dt == "int16" else x.astype(dt)
+    return "fsk", dict(baud=baud, f0=f0, f1=f1, samp_rate=fs, silence=True, quiet=quiet), x
+
+
 def main():
     rng = np.random.default_rng(20261017)
     draws = [draw(rng, c) for c in range(N_CASES)]
     draws += [draw_silence(rng) for _ in range(N_SILENCE)]
+    rng_q = np.random.default_rng(20261018)
+    draws += [draw_quiet(rng_q, i) for i in range(N_QUIET)]
     scratch = tempfile.mkdtemp(prefix="amr_sweep_golden_")
     cwd = os.getcwd()
     try:

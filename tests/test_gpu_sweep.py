@@ -7,7 +7,9 @@ plan told many batches are in flight), every stream's bytes and sync index
 bit-exact with the oracle -- or the same ValueError text, where the
 reference's scipy design raises.  Input: a framed, modulated signal at the
 drawn rate (after a drawn stretch of silence) plus noise of a drawn level
-(none to heavy; FSK at least 0.02), or plain noise."""
+(none to heavy -- FSK too: its digital-silence stretches, where only
+pocketfft's own rounding decides, go through the exact path at every
+length), or plain noise."""
 import os
 
 import numpy as np
@@ -28,12 +30,6 @@ def gpu(built_lib):
 def _signal(rng, kind, B, n, baud, f0, f1, fs):
     import synth
     noise = float(rng.choice([0.0, 0.02, 0.1, 0.4]))
-    if kind == "fsk":
-        # FSK inputs keep a noise floor: where a stream is digital silence next
-        # to signal, both envelopes are FFT rounding noise and the decisions
-        # there are pocketfft's alone (bounded by
-        # test_gpu_fsk.py::test_fsk_digital_silence_flips_only_where_ambiguous)
-        noise = max(noise, 0.02)
     if rng.random() < 0.15:
         x = rng.normal(0, 0.5, (B, n))
     else:
