@@ -2,6 +2,7 @@
 // (pocketfft_dev.h): the Bluestein plans' bkf table (plan construction) and
 // scipy.signal.resample for decode_wav_file (decoder.py:385-387), bit for bit.
 #include <algorithm>
+#include <cstdlib>
 
 #include "amr_internal.h"
 #include "pocketfft.h"
@@ -105,11 +106,17 @@ hipError_t launch_pf_resample(const PfLen* dLx, const double* poolx, const PfLen
 
 __global__ __launch_bounds__(kPfThreads) void k_pf_hilbert_env(const PfLen* __restrict__ L, const double* pool,
                                                                double* x, int64_t n, int64_t batch, double* slots,
-                                                               int64_t slot_doubles, double fct) {
+                                                               int64_t slot_doubles, double fct, int stage) {
   double* slot = slots + (size_t)blockIdx.x * slot_doubles;
   for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
     double* f = x + (size_t)b * n;
-    pf::pf_hilbert_env(*L, pool, f, f, slot, fct);
+    if (stage == 1) {   // diagnostic: the forward real transform alone (halfcomplex)
+      pf::pf_r2hc(*L, pool, f, pf::pf_scratch(*L, slot), 1.0);
+    } else if (stage == 2) {   // diagnostic: the backward real transform alone
+      pf::pf_hc2r(*L, pool, f, pf::pf_scratch(*L, slot), 1.0);
+    } else {
+      pf::pf_hilbert_env(*L, pool, f, f, slot, fct);
+    }
   }
 }
 
@@ -117,8 +124,15 @@ hipError_t launch_pf_hilbert_env(const PfLen* dL, const double* pool, double* x,
                                  double* slots, int64_t slot_doubles, int n_slots, double fct, hipStream_t st) {
   if (batch < 1) return hipSuccess;
   const unsigned g = (unsigned)std::min<int64_t>(batch, n_slots);
-  hipLaunchKernelGGL(k_pf_hilbert_env, dim3(g), dim3(kPfThreads), 0, st, dL, pool, x, n, batch, slots, slot_doubles,
-                     fct);
+  // AMR_PF_THREADS (diagnostic): a smaller workgroup (the routines take any size)
+  static const unsigned nt = [] {
+    const char* e = getenv("AMR_PF_THREADS");
+    const int v = e ? atoi(e) : 0;
+    return (unsigned)(v >= 64 && v <= kPfThreads ? v : kPfThreads);
+  }();
+  static const int stage = [] { const char* e = getenv("AMR_PF_STAGE"); return e ? atoi(e) : 0; }();
+  hipLaunchKernelGGL(k_pf_hilbert_env, dim3(g), dim3(nt), 0, st, dL, pool, x, n, batch, slots, slot_doubles, fct,
+                     stage);
   return hipGetLastError();
 }
 

@@ -13,29 +13,51 @@ namespace amr {
 namespace {
 
 // pocketfft's sincos_2pibyn(n): W_n^k = v1[k & mask] * v2[k >> shift],
-// entries from libm cos / sin by octant, ang = double(0.25L * pi / n)
+// entries from glibc's sincos by octant, ang = double(0.25L * pi / n)
 struct Twid2pi {
   int64_t n = 0, mask = 0, shift = 0;
   std::vector<double2> v1, v2;
+  // cos / sin of one argument from glibc's sincos, as scipy's gcc-built
+  // pocketfft gets them (gcc merges calc's std::cos / std::sin pair into one
+  // sincos call, and sincos differs from sin / cos in the last ulp for some
+  // arguments -- oracle/amr_pocketfft.c)
+  static double2 cs(double v) {
+    double s, c;
+    sincos(v, &s, &c);
+    return make_double2(c, s);
+  }
   static double2 calc(int64_t x, int64_t n, double ang) {
     x <<= 3;
     if (x < 4 * n) {
       if (x < 2 * n) {
-        if (x < n) return make_double2(std::cos((double)x * ang), std::sin((double)x * ang));
-        return make_double2(std::sin((double)(2 * n - x) * ang), std::cos((double)(2 * n - x) * ang));
+        if (x < n) return cs((double)x * ang);
+        const double2 t = cs((double)(2 * n - x) * ang);
+        return make_double2(t.y, t.x);
       }
       x -= 2 * n;
-      if (x < n) return make_double2(-std::sin((double)x * ang), std::cos((double)x * ang));
-      return make_double2(-std::cos((double)(2 * n - x) * ang), std::sin((double)(2 * n - x) * ang));
+      if (x < n) {
+        const double2 t = cs((double)x * ang);
+        return make_double2(-t.y, t.x);
+      }
+      const double2 t = cs((double)(2 * n - x) * ang);
+      return make_double2(-t.x, t.y);
     }
     x = 8 * n - x;
     if (x < 2 * n) {
-      if (x < n) return make_double2(std::cos((double)x * ang), -std::sin((double)x * ang));
-      return make_double2(std::sin((double)(2 * n - x) * ang), -std::cos((double)(2 * n - x) * ang));
+      if (x < n) {
+        const double2 t = cs((double)x * ang);
+        return make_double2(t.x, -t.y);
+      }
+      const double2 t = cs((double)(2 * n - x) * ang);
+      return make_double2(t.y, -t.x);
     }
     x -= 2 * n;
-    if (x < n) return make_double2(-std::sin((double)x * ang), -std::cos((double)x * ang));
-    return make_double2(-std::cos((double)(2 * n - x) * ang), -std::sin((double)(2 * n - x) * ang));
+    if (x < n) {
+      const double2 t = cs((double)x * ang);
+      return make_double2(-t.y, -t.x);
+    }
+    const double2 t = cs((double)(2 * n - x) * ang);
+    return make_double2(-t.x, -t.y);
   }
   explicit Twid2pi(int64_t len) : n(len) {
     const double ang = (double)(0.25L * 3.141592653589793238462643383279502884197L / (long double)len);

@@ -31,9 +31,10 @@
  *   Bluestein (fftblue): chirp b_m = w_2n^(m^2 mod 2n) from sincos_2pibyn(2n),
  *     a length-n2 cfftp convolution with the FFT of b/n2 precomputed.
  *   Twiddles: sincos_2pibyn -- two tables v1 (fine) and v2 (coarse), entries
- *     from libm cos / sin of x * ang by octant, ang = double(0.25L * pi / n)
- *     in long double; entry k = v1[k & mask] * v2[k >> shift] (conjugated
- *     mirror above n / 2).
+ *     from glibc's sincos of x * ang by octant (gcc merges pocketfft's
+ *     cos / sin pair; sincos differs from sin / cos in the last ulp for some
+ *     arguments), ang = double(0.25L * pi / n) in long double; entry k =
+ *     v1[k & mask] * v2[k >> shift] (conjugated mirror above n / 2).
  *   scipy.fft.fft of REAL input: the real plan forward, then the spectrum's
  *     second half filled by conjugate symmetry over bins 0..n/2 (pypocketfft
  *     c2c_sym_internal's rev_iter -- which also conjugates bins 0 and n/2,
@@ -70,27 +71,35 @@ static inline cpx rot90(cpx a, int fwd) { cpx c; if (fwd) { c.r = a.i; c.i = -a.
 /* ---- sincos_2pibyn -------------------------------------------------------- */
 typedef struct { int64_t n, mask, shift; cpx *v1, *v2; } twid_t;
 
+/* cos and sin of one argument through glibc's sincos: scipy's pocketfft is
+ * built by gcc, which merges the std::cos / std::sin pair of sincos_2pibyn's
+ * calc into one sincos call -- and glibc's sincos differs from its sin / cos
+ * in the last ulp for some arguments (e.g. sin(70 * pi / 372)), so the pair
+ * must come from sincos to equal scipy's twiddles */
+static void sc(double v, double *s, double *c) { sincos(v, s, c); }
+
 static cpx calc(int64_t x, int64_t n, double ang)
 {
   cpx c;
+  double sv, cv;
   x <<= 3;
   if (x < 4 * n) {
     if (x < 2 * n) {
-      if (x < n) { c.r = cos((double)x * ang); c.i = sin((double)x * ang); return c; }
-      c.r = sin((double)(2 * n - x) * ang); c.i = cos((double)(2 * n - x) * ang); return c;
+      if (x < n) { sc((double)x * ang, &sv, &cv); c.r = cv; c.i = sv; return c; }
+      sc((double)(2 * n - x) * ang, &sv, &cv); c.r = sv; c.i = cv; return c;
     }
     x -= 2 * n;
-    if (x < n) { c.r = -sin((double)x * ang); c.i = cos((double)x * ang); return c; }
-    c.r = -cos((double)(2 * n - x) * ang); c.i = sin((double)(2 * n - x) * ang); return c;
+    if (x < n) { sc((double)x * ang, &sv, &cv); c.r = -sv; c.i = cv; return c; }
+    sc((double)(2 * n - x) * ang, &sv, &cv); c.r = -cv; c.i = sv; return c;
   }
   x = 8 * n - x;
   if (x < 2 * n) {
-    if (x < n) { c.r = cos((double)x * ang); c.i = -sin((double)x * ang); return c; }
-    c.r = sin((double)(2 * n - x) * ang); c.i = -cos((double)(2 * n - x) * ang); return c;
+    if (x < n) { sc((double)x * ang, &sv, &cv); c.r = cv; c.i = -sv; return c; }
+    sc((double)(2 * n - x) * ang, &sv, &cv); c.r = sv; c.i = -cv; return c;
   }
   x -= 2 * n;
-  if (x < n) { c.r = -sin((double)x * ang); c.i = -cos((double)x * ang); return c; }
-  c.r = -cos((double)(2 * n - x) * ang); c.i = -sin((double)(2 * n - x) * ang); return c;
+  if (x < n) { sc((double)x * ang, &sv, &cv); c.r = -sv; c.i = -cv; return c; }
+  sc((double)(2 * n - x) * ang, &sv, &cv); c.r = -cv; c.i = -sv; return c;
 }
 
 static int twid_init(twid_t *t, int64_t n)
