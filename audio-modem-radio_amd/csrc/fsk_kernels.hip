@@ -46,27 +46,43 @@ template <> struct FIn<int16_t> {
   static __device__ __forceinline__ double ext(int16_t e, int16_t v) { return 2.0 * cvt(e) - cvt(v); }
 };
 
-// lfilter step (DF-II-T), 7 taps, per-lane coefficients, contracted:
-//   y = b0*x + z0 ; z[i] = z[i+1] + x*b[i+1] - y*a[i+1] ; z[5] = x*b6 - y*a6
-// The FSK decision compares two envelopes that already pass through an FFT
-// whose rounding differs from pocketfft's, so this stage is held to the
-// envelope tolerance (1e-9 relative, tests/test_gpu_fsk.py), not op order;
-// fused multiply-adds halve its FP64 instruction count.
-// ZO: the plan's b1 = b3 = b5 = 0 exactly for both tones (always so for
-// butter(3, band): b is k * poly([1,1,1,-1,-1,-1]) = k * [1,0,-3,0,3,0,-1]);
-// then fma(x, 0, z) == z for every z != 0 and those three FMAs are dropped
-// (10 FP64 instructions per sample instead of 13; only the sign of an exact
-// zero state can differ, which the envelope tolerance does not see).
-template <bool ZO>
+// lfilter step (DF-II-T), 7 taps, per-lane coefficients, in scipy's own
+// operation order (scipy.signal.lfilter's real DF-II-T loop, no contraction):
+//   y = z0 + b0*x ; z[i] = (z[i+1] + x*b[i+1]) - y*a[i+1] ; z[5] = x*b6 - y*a6
+// so the band-pass output f equals scipy's filtfilt bit for bit (the odd
+// extension in the input's precision, zi * x0 and the checkpointed re-runs
+// are exact too), and the envelopes differ from the reference's only by
+// the FFTs' rounding -- the margin F2's exact-path flags are sized for.
+// ZO (MODE 1): the plan's b1 = b3 = b5 = 0 exactly for both tones (always so
+// for butter(3, band): b is k * poly([1,1,1,-1,-1,-1]) = k * [1,0,-3,0,3,0,-1]);
+// then (z + x*0) == z for every z != 0 and those three products and sums are
+// dropped (19 FP64 operations per step instead of 25; only the sign of an
+// exact zero state can differ, which no envelope |.| sees).
+// MODE 2 (AMR_FSK_F1_FMA=1, a timing A/B only): the round-3 contracted form
+// (10 FMAs per step), whose f is NOT scipy's -- its rounding grows with the
+// band-pass filter's noise gain (~1e-10 of the peak at 1200 Bd), beyond the
+// exact path's margin.
+template <int MODE>
 __device__ __forceinline__ double fsk_step(double (&z)[6], const double (&b)[7], const double (&a)[7], double x) {
-  const double y = __builtin_fma(b[0], x, z[0]);
+  if constexpr (MODE == 2) {
+    const double y = __builtin_fma(b[0], x, z[0]);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const double zin = (ZO && (i & 1) == 0) ? z[i + 1] : __builtin_fma(x, b[i + 1], z[i + 1]);
-    z[i] = __builtin_fma(-y, a[i + 1], zin);
+    for (int i = 0; i < 5; ++i) {
+      const double zin = ((i & 1) == 0) ? z[i + 1] : __builtin_fma(x, b[i + 1], z[i + 1]);
+      z[i] = __builtin_fma(-y, a[i + 1], zin);
+    }
+    z[5] = __builtin_fma(-y, a[6], x * b[6]);
+    return y;
+  } else {
+    const double y = z[0] + b[0] * x;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const double zin = (MODE == 1 && (i & 1) == 0) ? z[i + 1] : z[i + 1] + x * b[i + 1];
+      z[i] = zin - y * a[i + 1];
+    }
+    z[5] = x * b[6] - y * a[6];
+    return y;
   }
-  z[5] = __builtin_fma(-y, a[6], x * b[6]);
-  return y;
 }
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));   // native vector (HIP's uint4 is a struct)
@@ -139,7 +155,7 @@ __device__ __forceinline__ int64_t fsk_zoff(const FskParams& p, int64_t i) {
   else return i;
 }
 
-template <typename T, bool ZO, bool LIVE, bool AMB = false>
+template <typename T, int ZO, bool LIVE, bool AMB = false>
 __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_stride, int64_t n_streams,
                                                      double* __restrict__ scratch, double2* __restrict__ z,
                                                      FskParams p, FskIir f) {
@@ -226,7 +242,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
     tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
   }
   if constexpr (AMB) {
-    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo), p.amb_tau);
     if (lane == 0) p.xflags[w] = 0u;
   }
   double ylast = 0.0;
@@ -301,7 +317,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 constexpr int kFsk2Tile = 64;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
 
-template <typename T, bool ZO, bool LIVE, bool W1S, bool AMB = false>
+template <typename T, int ZO, bool LIVE, bool W1S, bool AMB = false>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
@@ -404,7 +420,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     }
     if constexpr (AMB) {
       // this batch's margin scale, and the group's flag word cleared for F2
-      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo), p.amb_tau);
       if (lane == 0) p.xflags[w] = 0u;
     }
     double yl = 0.0;
@@ -568,15 +584,19 @@ static bool fsk_one_wave() {
   return v;
 }
 
-static bool fsk_zero_odd_taps(const FskIir& f) {
+// fsk_step's MODE: 1 when the odd taps are zero (always, for butter(3, band)),
+// else 0; AMR_FSK_ZO=0 forces 0; AMR_FSK_F1_FMA=1 the contracted form (2)
+static int fsk_step_mode(const FskIir& f) {
   static const bool off = [] { const char* e = getenv("AMR_FSK_ZO"); return e && e[0] == '0'; }();
-  if (off) return false;
+  static const bool fma = [] { const char* e = getenv("AMR_FSK_F1_FMA"); return e && e[0] == '1'; }();
+  bool zo = !off;
   for (int t = 0; t < 2; ++t)
-    if (f.b[t][1] != 0.0 || f.b[t][3] != 0.0 || f.b[t][5] != 0.0) return false;
-  return true;
+    if (f.b[t][1] != 0.0 || f.b[t][3] != 0.0 || f.b[t][5] != 0.0) zo = false;
+  if (fma && zo) return 2;
+  return zo ? 1 : 0;
 }
 
-template <bool ZO, bool LIVE>
+template <int ZO, bool LIVE>
 static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1,
                                         double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
@@ -612,12 +632,12 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
 // the chunk's first stream); p.lc.on selects the live-column layout
 hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
                                const FskParams& p, const FskIir& f, hipStream_t st) {
-  const bool zo = fsk_zero_odd_taps(f);
-  if (p.lc.on)
-    return zo ? launch_fsk_bandpass_t<true, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
-              : launch_fsk_bandpass_t<false, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
-  return zo ? launch_fsk_bandpass_t<true, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st)
-            : launch_fsk_bandpass_t<false, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st);
+  const int mode = fsk_step_mode(f);
+#define BPM(M) (p.lc.on ? launch_fsk_bandpass_t<M, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st) \
+                        : launch_fsk_bandpass_t<M, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st))
+  if (mode == 2) return BPM(2);
+  return mode == 1 ? BPM(1) : BPM(0);
+#undef BPM
 }
 
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,

@@ -143,7 +143,7 @@ def test_fsk_full_batch_round_trip():
     x = np.tile(base, (B // U, 1))
     pl = _fsk.get_fsk_plan(N, 9600, 12000.0, 24000.0, 96000, B)
     assert pl.live_columns
-    assert pl.scratch_bytes() <= 40e9, pl.scratch_bytes()     # 1.4 x n complex per stream + C's staging
+    assert pl.scratch_bytes() <= 50e9, pl.scratch_bytes()     # 1.4 x n complex per stream + 8 B/sample staging
     got, sync = pl.demod_host(x)
     bad = [i for i in range(U, B) if got[i] != got[i % U]]
     assert not bad, f"{len(bad)} repeated streams decode differently, first {bad[:5]}"
@@ -192,11 +192,12 @@ def test_fsk_batch_past_2g_samples():
                                                 (24001, 1200, 2400.0, 4800.0), (30000, 300, 1200.0, 2200.0)])
 def test_envelope_error_is_far_below_the_margin(n, baud, mark, space):
     """F2 flags a stream for the exact path when some compare has
-    |env_mark - env_space| <= 2 tau peak|x| (tau = 2^-36, amr_internal.h
-    kAmbTau); unflagged compares are then bit-exact only if the fast path's
-    envelopes are within tau peak|x| of the reference's.  Measure that error
-    (GPU natural-layout envelopes vs the reference's |hilbert(filtfilt(.))|,
-    the oracle's restatement) on noise, signal, digital silence and quiet
+    |env_mark - env_space| <= 2 tau peak|x| (amr_internal.h: tau = 2^-36 for
+    two-pass FFT lengths, 2^-30 where the fast FFT is six-step or Bluestein);
+    unflagged compares are then bit-exact only if the fast path's envelopes
+    are within tau peak|x| of the reference's.  Measure that error (GPU
+    natural-layout envelopes vs the reference's |hilbert(filtfilt(.))|, the
+    oracle's restatement) on noise, signal, digital silence and quiet
     stretches: it must stay below tau / 100."""
     import _fsk
     import synth
@@ -225,7 +226,7 @@ def test_envelope_error_is_far_below_the_margin(n, baud, mark, space):
             return oracle.hilbert_env(oracle.filtfilt(b, a, xi))
         peak = np.abs(xi).max()
         worst = max(worst, np.abs(gm[i] - env(mark)).max() / peak, np.abs(gs[i] - env(space)).max() / peak)
-    tau = 2.0 ** -36
+    tau = 2.0 ** -30 if pl.fft_length != n or n > 390625 else 2.0 ** -36   # Bluestein / six-step fast FFT
     print(f"n={n}: max |env_gpu - env_ref| / peak|x| = {worst:.3e} (tau = {tau:.3e}, ratio {tau / worst:.0f})")
     assert worst < tau / 100
 
