@@ -134,25 +134,22 @@ struct FskParams {
   uint32_t* xflags;
   const uint8_t* xbits;
   int force_exact;  // exact mode 2 (amr_fsk_plan_set_exact_mode): every stream's scale +inf, all go exact
-  double amb_tau;   // the margin's tau (kAmbTau, or kAmbTauLong for six-step / Bluestein fast FFTs)
 };
 
 // F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within
 // reach of the fast path's and pocketfft's rounding.
-// tau = 2^-36 ~ 1.5e-11 for the two-pass FFT lengths (the live-column and
-// natural layouts), 2^-30 ~ 9.3e-10 where the fast FFT is six-step or
-// Bluestein (its envelopes carry ~100x the rounding); each >= 100 times the
-// largest difference measured between the fast path's envelopes and the
-// reference's (tests/test_gpu_fsk.py::test_envelope_error_is_far_below_the_margin)
+// F1 computes scipy's filtfilt bit for bit, so the envelopes differ from the
+// reference's by the two FFTs' rounding alone: measured <= 4.3e-15 peak|x|
+// (two-pass and Bluestein lengths, 300-9600 Bd); tau = 2^-36 ~ 1.5e-11 is
+// >= 3000 times that (tests/test_gpu_fsk.py::test_envelope_error_is_far_below_the_margin)
 constexpr double kAmbTau = 0x1p-36;
-constexpr double kAmbTauLong = 0x1p-30;
 // c = 8 (tau peak)^2 (fft_kernels.hip env_ambiguous compares squares);
 // -1 for a stream of exact zeros (both paths' envelopes are exact zeros),
 // +inf for tiny / huge / non-finite input (every compare goes exact)
-__host__ __device__ inline double amb_scale(double peak, double tau) {
+__host__ __device__ inline double amb_scale(double peak) {
   if (peak == 0.0) return -1.0;
   if (!(peak >= 0x1p-400 && peak <= 0x1p400)) return __builtin_inf();
-  const double d = tau * peak;
+  const double d = kAmbTau * peak;
   return 8.0 * d * d;
 }
 

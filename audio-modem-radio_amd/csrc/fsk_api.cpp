@@ -590,7 +590,6 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   p.lc = plan_live_cols(g.sh, p);
   p.bits_stride = p.lc.on ? (int64_t)((p.lc.nl + 7) >> 3) * p.rn2 : fft_bits_stride(p.rn1, p.rn2);
   p.inv_rn1 = 1.0f / (float)p.rn1;
-  p.amb_tau = plain ? kAmbTauLong : kAmbTau;
   const int64_t s1_bytes = fsk_bandpass_scratch_bytes(max_streams, n, p.pad);
   if (p.lc.on) {
     // C: the live columns' transform; before the column pass it holds F1's checkpoints

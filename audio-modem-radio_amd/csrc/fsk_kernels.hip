@@ -242,7 +242,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
     tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
   }
   if constexpr (AMB) {
-    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo), p.amb_tau);
+    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
     if (lane == 0) p.xflags[w] = 0u;
   }
   double ylast = 0.0;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     }
     if constexpr (AMB) {
       // this batch's margin scale, and the group's flag word cleared for F2
-      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo), p.amb_tau);
+      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
       if (lane == 0) p.xflags[w] = 0u;
     }
     double yl = 0.0;
