@@ -128,14 +128,32 @@ def test_reference_sweep_through_the_drop_in(sweep_golden):
     """The drop-in modules (modem.qpsk_demodulate / bpsk_demodulate /
     fsk_demodulate on the GPU) against the REFERENCE's own outputs on the 72
     seeded configurations of tests/golden/make_sweep_golden.py: bytes or
-    exception text equal, every case -- the 12 FSK cases inside exact digital
-    silence too, through the exact fallback."""
+    exception text equal, every case -- the FSK cases inside exact digital
+    silence, DC and near-silent stretches too, at 5-smooth, generic-radix and
+    Bluestein lengths, through the exact path.
+    The reference saw int16 fixtures as int16 / 32768 (as libsndfile reads a
+    WAV); the public drop-in functions treat integer input as raw values, as
+    the reference itself would -- identical decisions up to 2^15 scaling,
+    except where the envelopes are rounding noise (c85: a DC lead-in) -- so
+    int16 cases go in as int16 / 32768, and the FSK ones also through the
+    plans' own PCM16 path (int16 on the device, converted exactly)."""
+    import _fsk
     import modem
     from _util import call_sweep_case, expected, outcome
     manifest, inputs = sweep_golden
     bad = []
     for c in manifest["cases"]:
-        got = outcome(lambda: call_sweep_case(modem, c, inputs[c["id"]]))
+        x = inputs[c["id"]]
+        if x.dtype == np.int16:
+            xs = x.astype(np.float64) / 32768.0
+            got = outcome(lambda: call_sweep_case(modem, c, xs))
+            if c["fn"] == "fsk" and got == expected(c) and got[0] == "ok":
+                p = c["params"]
+                pcm = outcome(lambda: _fsk.fsk_demodulate_batch(x[None], p["baud"], p["f0"], p["f1"], p["samp_rate"])[0])
+                if pcm != got:
+                    bad.append((c["id"], "pcm16", c["params"], c["n"]))
+        else:
+            got = outcome(lambda: call_sweep_case(modem, c, x))
         if got != expected(c):
             bad.append((c["id"], c["fn"], c["params"], c["dtype"], c["n"], got[0]))
     assert not bad, f"{len(bad)} of {len(manifest['cases'])} differ from the reference: {bad[:5]}"
