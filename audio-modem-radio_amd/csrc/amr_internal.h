@@ -134,6 +134,8 @@ struct FskParams {
   uint32_t* xflags;
   const uint8_t* xbits;
   int force_exact;  // exact mode 2 (amr_fsk_plan_set_exact_mode): every stream's scale +inf, all go exact
+  const int32_t* xlist;   // F1 list mode (the exact path): z row r <- x row xlist[r], r < *xcount
+  const int32_t* xcount;
 };
 
 // F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within

@@ -442,7 +442,16 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.xbits = pl->xbits;
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
   pl->ran_exact = true;
-  HIP_TRY(launch_fsk_exact(dtype, d_x, x_stride, B, pl->p, pl->f, X, pl->stream));
+  HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));
+  // E1: F1 again over the flagged streams only (list mode), natural z layout
+  FskParams p1 = pl->p;
+  p1.amb = nullptr;
+  p1.lc = LiveCols{};
+  p1.xlist = X.list;
+  p1.xcount = X.count;
+  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f,
+                              pl->stream));
+  HIP_TRY(launch_fsk_exact_env(B, pl->p, X, pl->stream));
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1));
   return AMR_OK;
 }
@@ -599,9 +608,8 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
     g.v = max_streams * M * 16;
   }
   g.staging = max_streams * n * 8;                   // d_x, allocated on the first host call
-  const int64_t m = n + 2 * (int64_t)p.pad;
-  // z; after F2, the exact path's filtfilt rows ([ordinal][tone][m] doubles)
-  g.z = std::max(max_streams * n * 16, max_streams * 2 * m * 8);
+  // z; after F2, the exact path's rows ([ordinal][n] (f_mark, f_space))
+  g.z = max_streams * n * 16;
   g.cmp = max_streams * p.bits_stride;
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
@@ -610,10 +618,11 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
   g.exact = exact_env && p.n_bits > 0;
   if (g.exact) {
-    g.slot_doubles = pf_scratch_doubles_n(n);
-    // one workgroup per slot: up to 2 per stream and 256, within 1 GiB of slots
+    g.slot_doubles = n + pf_scratch_doubles_n(n);    // the row, then its transforms' scratch
+    // one workgroup per slot: up to 2 per stream and 1024 (4 per CU: each
+    // pass is latency-bound), within 2 GiB of slots
     g.n_slots = (int)std::max<int64_t>(
-        1, std::min<int64_t>({2 * max_streams, 256, ((int64_t)1 << 30) / (g.slot_doubles * 8)}));
+        1, std::min<int64_t>({2 * max_streams, 1024, ((int64_t)1 << 31) / (g.slot_doubles * 8)}));
     g.xflags = (max_streams + 31) / 32 * 4;
     g.amb = max_streams * 8;
     g.xlist = (max_streams + 1) * 4;

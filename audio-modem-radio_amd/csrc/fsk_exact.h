@@ -15,7 +15,7 @@ struct FskExact {
   const uint32_t* flags;   // [B / 32] F2's flags: bit s of word s / 32
   int32_t* list;           // [B] ordinal -> stream (E0)
   int32_t* count;          // [1] flagged streams (E0)
-  double* rows;            // [B][2][m] the flagged streams' filtfilt rows (the plan's z), by ordinal
+  double* rows;            // the plan's z: [ordinal][n] (f_mark, f_space), then (env_mark, env_space)
   double* slots;           // [n_slots][slot_doubles] envelope scratch (E2)
   int64_t slot_doubles;
   int n_slots;
@@ -25,9 +25,10 @@ struct FskExact {
   uint8_t* xbits;          // [B][bits_stride] exact compare bits, F3 reads them for flagged streams
 };
 
-// the flagged streams of the batch (x: B rows, x_stride apart) -> their exact
-// compare bits in X.xbits; every kernel exits at once when nothing is flagged
-hipError_t launch_fsk_exact(int dtype, const void* x, int64_t x_stride, int64_t B, const FskParams& p,
-                            const FskIir& f, const FskExact& X, hipStream_t st);
+// E0: F2's flags -> X.list / X.count.  Then F1 in list mode (fsk_api.cpp),
+// then E2 + E3: the flagged streams' exact compare bits in X.xbits.  Every
+// kernel exits at once when nothing is flagged.
+hipError_t launch_fsk_exact_list(int64_t B, const FskExact& X, hipStream_t st);
+hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st);
 
 }  // namespace amr

@@ -10,18 +10,20 @@
 // recomputes the flagged streams' compare bits the reference's own way, bit
 // for bit, at any length:
 //   E0 k_exact_list      flag words -> list of flagged streams (ordinals)
-//   E1 k_exact_filtfilt  lane = (ordinal, tone): filtfilt in scipy's operation
-//                        order (DF-II-T without contraction, odd extension in
-//                        the input's precision -- oracle/amr_oracle.c
-//                        oracle_filtfilt) into row 2q + tone of the plan's z
-//   E2 k_exact_env       workgroup = row: |scipy.signal.hilbert(f)| as
-//                        pocketfft + numpy evaluate it (pocketfft_dev.h, every
-//                        radix and Bluestein), in place
+//   E1 F1 in list mode   the flagged streams' band-pass filtfilt again
+//                        (fsk_kernels.hip k_fsk_bandpass2: scipy's order, so
+//                        f is the reference's), z row q = ordinal q's
+//                        f_mark + i f_space -- F2 has consumed z by now
+//   E2 k_exact_env       workgroup = row (q, tone): |scipy.signal.hilbert(f)|
+//                        as pocketfft + numpy evaluate it (pocketfft_dev.h,
+//                        every radix and Bluestein), back into z
 //   E3 k_exact_bits      bit = env_mark > env_space in the final pass's byte
 //                        layout -> xbits, which F3 (k_fsk_decide) reads for a
 //                        flagged stream instead of the fast path's bytes
 // With nothing flagged (every noisy capture) each kernel reads the count and
 // exits.
+#include <algorithm>
+
 #include "amr_internal.h"
 #include "fsk_exact.h"
 #include "pocketfft_dev.h"
@@ -104,57 +106,21 @@ __global__ __launch_bounds__(kListThreads) void k_exact_list(const uint32_t* __r
   if (threadIdx.x == kListThreads - 1) *count = part[threadIdx.x];
 }
 
-// E1: lane = (ordinal q, tone); filtfilt of the stream's input into row 2q + tone (m doubles)
-template <typename T>
-__global__ __launch_bounds__(64) void k_exact_filtfilt(const void* xv, int64_t x_stride, FskParams p, FskIir f,
-                                                       FskExact X) {
-  const int64_t q = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 1);
-  if (q >= *X.count) return;   // no barriers below
-  const int tone = threadIdx.x & 1;
-  const T* __restrict__ x = reinterpret_cast<const T*>(xv) + (size_t)X.list[q] * x_stride;
-  const int64_t n = p.n, pad = p.pad, m = n + 2 * pad;
-  double* __restrict__ y = X.rows + (size_t)(2 * q + tone) * m;
-  double b[7], a[7], z[6];
-  for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
-  // forward over numpy's odd extension (evaluated in the input's precision)
-  const double e0 = XIn<T>::ext(x, 0, pad);
-  for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * e0;
-  for (int64_t j = 0; j < pad; ++j) y[j] = df2t_step(b, a, z, XIn<T>::ext(x, 0, pad - j));
-  {   // x[0, n) in blocks, the next block's loads issued before this one's recursion
-    const int64_t nblk = n / kDfBlock;
-    double cur[kDfBlock], nxt[kDfBlock];
-    if (nblk > 0)
-#pragma unroll
-      for (int u = 0; u < kDfBlock; ++u) cur[u] = XIn<T>::cvt(x, u);
-    for (int64_t blk = 0; blk < nblk; ++blk) {
-      const int64_t i0 = blk * kDfBlock;
-      if (blk + 1 < nblk)
-#pragma unroll
-        for (int u = 0; u < kDfBlock; ++u) nxt[u] = XIn<T>::cvt(x, i0 + kDfBlock + u);
-#pragma unroll
-      for (int u = 0; u < kDfBlock; ++u) cur[u] = df2t_step(b, a, z, cur[u]);
-#pragma unroll
-      for (int u = 0; u < kDfBlock; ++u) y[pad + i0 + u] = cur[u];
-#pragma unroll
-      for (int u = 0; u < kDfBlock; ++u) cur[u] = nxt[u];
-    }
-    for (int64_t i = nblk * kDfBlock; i < n; ++i) y[pad + i] = df2t_step(b, a, z, XIn<T>::cvt(x, i));
-  }
-  for (int64_t j = 0; j < pad; ++j) y[pad + n + j] = df2t_step(b, a, z, XIn<T>::ext(x, n - 1, n - 2 - j));
-  // backward over the forward outputs, in place
-  for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * y[m - 1];
-  df2t_exact(b, a, z, y + m - 1, m, -1);
-}
-
-// E2: workgroup = row r = 2q + tone: |hilbert| of the row's n outputs, in place
+// E2: workgroup = row r = 2q + tone: the tone's band-pass output (F1 in list
+// mode left ordinal q's z row = f_mark + i f_space) -> the slot, |hilbert| of
+// it, back into the same interleaved positions of z
 constexpr int kEnvThreads = 512;
 __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact X) {
   const int64_t cnt = *X.count;
-  const int64_t pad = p.pad, m = p.n + 2 * pad;
-  double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
+  const int64_t n = p.n;
+  double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
-    double* f = X.rows + (size_t)r * m + pad;
-    pf::pf_hilbert_env(*X.L, X.pool, f, f, slot, X.fct);
+    double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = zr[2 * i];
+    __syncthreads();
+    pf::pf_hilbert_env(*X.L, X.pool, c, c, c + n, X.fct);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) zr[2 * i] = c[i];
+    __syncthreads();
   }
 }
 
@@ -164,13 +130,12 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
 constexpr int kBitsThreads = 256;
 __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExact X) {
   const int64_t cnt = *X.count;
-  const int64_t n = p.n, pad = p.pad, m = n + 2 * pad;
+  const int64_t n = p.n;
   const int ncol = p.lc.on ? p.lc.nl : (int)p.rn1;
   const int64_t n2 = p.rn2, n1 = p.lc.on ? p.lc.n1 : p.rn1;
   const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
   for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {
-    const double* e0 = X.rows + (size_t)(2 * q) * m + pad;
-    const double* e1 = e0 + m;
+    const double2* e = reinterpret_cast<const double2*>(X.rows) + (size_t)q * n;   // (env_mark, env_space)
     uint8_t* ob = X.xbits + (size_t)X.list[q] * p.bits_stride;
     for (int64_t qb = threadIdx.x; qb < nbytes; qb += blockDim.x) {
       const int64_t cb = qb / n2, kk = qb - cb * n2;
@@ -180,24 +145,21 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
         if (c >= ncol) break;
         const int64_t col = p.lc.on ? lc_live_col(p.lc, c) : c;
         const int64_t i = col + n1 * kk;
-        if (i < n && e0[i] > e1[i]) byte |= 1u << t;
+        if (i < n && e[i].x > e[i].y) byte |= 1u << t;
       }
       ob[qb] = (uint8_t)byte;
     }
   }
 }
 
-hipError_t launch_fsk_exact(int dtype, const void* x, int64_t x_stride, int64_t B, const FskParams& p,
-                            const FskIir& f, const FskExact& X, hipStream_t st) {
+hipError_t launch_fsk_exact_list(int64_t B, const FskExact& X, hipStream_t st) {
   if (B < 1) return hipSuccess;
-  const int64_t nw = (B + 31) / 32;
-  hipLaunchKernelGGL(k_exact_list, dim3(1), dim3(kListThreads), 0, st, X.flags, nw, X.list, X.count);
-  switch (dtype) {
-    case kF32: hipLaunchKernelGGL(k_exact_filtfilt<float>, dim3((unsigned)nw), dim3(64), 0, st, x, x_stride, p, f, X); break;
-    case kF64: hipLaunchKernelGGL(k_exact_filtfilt<double>, dim3((unsigned)nw), dim3(64), 0, st, x, x_stride, p, f, X); break;
-    case kI16: hipLaunchKernelGGL(k_exact_filtfilt<int16_t>, dim3((unsigned)nw), dim3(64), 0, st, x, x_stride, p, f, X); break;
-    default: return hipErrorInvalidValue;
-  }
+  hipLaunchKernelGGL(k_exact_list, dim3(1), dim3(kListThreads), 0, st, X.flags, (B + 31) / 32, X.list, X.count);
+  return hipGetLastError();
+}
+
+hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st) {
+  if (B < 1) return hipSuccess;
   hipLaunchKernelGGL(k_exact_env, dim3((unsigned)X.n_slots), dim3(kEnvThreads), 0, st, p, X);
   hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 2048)), dim3(kBitsThreads), 0, st, p, X);
   return hipGetLastError();

@@ -58,6 +58,10 @@ template <> struct FIn<int16_t> {
 // then (z + x*0) == z for every z != 0 and those three products and sums are
 // dropped (19 FP64 operations per step instead of 25; only the sign of an
 // exact zero state can differ, which no envelope |.| sees).
+// MODE 3: ZO and, as butter(3, band) always has (the plan checks), an
+// antisymmetric numerator b6 = -b0, b4 = -b2 bit for bit: x*b6 IS -(x*b0),
+// so z5 = x*b6 - y*a6 is (-(x*b0)) - y*a6 = -(x*b0) - y*a6 exactly, and
+// z4 + x*b4 is z4 - x*b2: two products per step instead of four (17 FP64).
 // MODE 2 (AMR_FSK_F1_FMA=1, a timing A/B only): the round-3 contracted form
 // (10 FMAs per step), whose f is NOT scipy's -- its rounding grows with the
 // band-pass filter's noise gain (~1e-10 of the peak at 1200 Bd), beyond the
@@ -72,6 +76,16 @@ __device__ __forceinline__ double fsk_step(double (&z)[6], const double (&b)[7],
       z[i] = __builtin_fma(-y, a[i + 1], zin);
     }
     z[5] = __builtin_fma(-y, a[6], x * b[6]);
+    return y;
+  } else if constexpr (MODE == 3) {
+    const double xb0 = x * b[0], xb2 = x * b[2];
+    const double y = z[0] + xb0;
+    z[0] = z[1] - y * a[1];
+    z[1] = (z[2] + xb2) - y * a[2];
+    z[2] = z[3] - y * a[3];
+    z[3] = (z[4] - xb2) - y * a[4];
+    z[4] = z[5] - y * a[5];
+    z[5] = -xb0 - y * a[6];
     return y;
   } else {
     const double y = z[0] + b[0] * x;
@@ -336,9 +350,21 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   const int tone = lane & 1, sl = lane >> 1;
   const int64_t w = blockIdx.x;
   const int64_t s = w * 32 + sl;
-  const int64_t last = n_streams - 1;
+  // list mode (p.xlist, the exact path): the streams F2 flagged, by ordinal
+  // (row r of z is ordinal r's, x row p.xlist[r]); the count is read here
+  int64_t ns = n_streams;
+  if (p.xlist) {
+    const int64_t c = *p.xcount;
+    ns = c < n_streams ? c : n_streams;
+    if (w * 32 >= ns) return;              // whole workgroup, before any barrier
+  }
+  const int64_t last = ns - 1;
   const T* __restrict__ xall = reinterpret_cast<const T*>(xv);
-  const T* __restrict__ x = xall + (s < last ? s : last) * x_stride;
+  auto xrow = [&](int64_t r) -> const T* {
+    const int64_t rr = r < last ? r : last;
+    return xall + (p.xlist ? (int64_t)p.xlist[rr] : rr) * x_stride;
+  };
+  const T* __restrict__ x = xrow(s);
   const int64_t n = p.n;
   const int pad = p.pad;
   const int64_t n_tiles = n / TL;
@@ -357,7 +383,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int64_t rs = w * 32 + RPI * i + rsub;
-    rowp[i] = reinterpret_cast<const uint8_t*>(xall + (rs < last ? rs : last) * x_stride) + cb;
+    rowp[i] = reinterpret_cast<const uint8_t*>(xrow(rs)) + cb;
   }
   v4u r0[NI], r1[NI];
   auto fetch = [&](v4u (&r)[NI], int64_t t) {
@@ -420,7 +446,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     }
     if constexpr (AMB) {
       // this batch's margin scale, and the group's flag word cleared for F2
-      if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+      if (tone == 0 && s < ns) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
       if (lane == 0) p.xflags[w] = 0u;
     }
     double yl = 0.0;
@@ -440,7 +466,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     for (int64_t j = ntail - 1; j >= n - n_main; --j) (void)fsk_step<ZO>(zs, b, a, tb[(size_t)j * YP + lane]);
     for (int64_t i = n - 1; i >= n_main; --i) {
       const double y = fsk_step<ZO>(zs, b, a, tb[(size_t)(i - n_main) * YP + lane]);
-      if (s < n_streams) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
+      if (s < ns) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
     }
   }
   __syncthreads();                                     // the tail rows of yb are free again
@@ -456,7 +482,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       const int rr = row + sub;
       const int64_t so = w * 32 + rr;
       const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
-      if (so < n_streams) z[(size_t)so * n + zo] = v;
+      if (so < ns) z[(size_t)so * n + zo] = v;
     }
   };
   // ---- phase 2: wave 0 re-forwards tile T-1-i while wave 1 runs tile T-i backward
@@ -584,15 +610,19 @@ static bool fsk_one_wave() {
   return v;
 }
 
-// fsk_step's MODE: 1 when the odd taps are zero (always, for butter(3, band)),
+// fsk_step's MODE: 3 when the odd taps are zero and the numerator is
+// antisymmetric (always, for butter(3, band)), 1 with zero odd taps only,
 // else 0; AMR_FSK_ZO=0 forces 0; AMR_FSK_F1_FMA=1 the contracted form (2)
-static int fsk_step_mode(const FskIir& f) {
+static int fsk_step_mode(const FskIir& f, bool allow_fma) {
   static const bool off = [] { const char* e = getenv("AMR_FSK_ZO"); return e && e[0] == '0'; }();
   static const bool fma = [] { const char* e = getenv("AMR_FSK_F1_FMA"); return e && e[0] == '1'; }();
-  bool zo = !off;
-  for (int t = 0; t < 2; ++t)
+  bool zo = !off, anti = true;
+  for (int t = 0; t < 2; ++t) {
     if (f.b[t][1] != 0.0 || f.b[t][3] != 0.0 || f.b[t][5] != 0.0) zo = false;
-  if (fma && zo) return 2;
+    if (f.b[t][6] != -f.b[t][0] || f.b[t][4] != -f.b[t][2]) anti = false;
+  }
+  if (fma && allow_fma && zo) return 2;
+  if (zo && anti) return 3;
   return zo ? 1 : 0;
 }
 
@@ -600,7 +630,7 @@ template <int ZO, bool LIVE>
 static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1,
                                         double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
   const unsigned grid = (unsigned)((n_streams + 31) / 32);
-  if (!fsk_one_wave()) {
+  if (!fsk_one_wave() || p.xlist) {
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
 #define BP2(T, S, D) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
@@ -632,9 +662,10 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
 // the chunk's first stream); p.lc.on selects the live-column layout
 hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1, double2* z,
                                const FskParams& p, const FskIir& f, hipStream_t st) {
-  const int mode = fsk_step_mode(f);
+  const int mode = fsk_step_mode(f, !p.xlist);   // the exact path: scipy's order always
 #define BPM(M) (p.lc.on ? launch_fsk_bandpass_t<M, true>(dtype, x, x_stride, n_streams, s1, z, p, f, st) \
                         : launch_fsk_bandpass_t<M, false>(dtype, x, x_stride, n_streams, s1, z, p, f, st))
+  if (mode == 3) return BPM(3);
   if (mode == 2) return BPM(2);
   return mode == 1 ? BPM(1) : BPM(0);
 #undef BPM

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""How long the FSK exact fallback takes when every stream is flagged
-(zero-padded captures), against the same batch with a
-noise floor (nothing flagged).  GPU box:  python tools/fsk_exact_timing.py"""
+"""How long the FSK exact path takes: zero-padded captures (F2 flags the
+streams whose compares fall inside the margin), every
+stream forced through it (exact mode 2), against the same batch with a noise
+floor (nothing flagged).  GPU box:  python tools/fsk_exact_timing.py"""
 import os
 import sys
 import time
@@ -33,16 +34,22 @@ def batch(B, n, noise, seed=5):
 
 def main():
     n = 96000
-    for B in (16, 128, 512, 2048):
+    sizes = [int(v) for v in sys.argv[1:]] or [1, 16, 128, 512, 2048]
+    for B in sizes:
         pl = _fsk.FskPlan(n, 9600, 12000.0, 24000.0, max_streams=B)
-        for label, noise in (("silent-padded", 0.0), ("noise floor", 0.01)):
+        pl.enable_timing(True)
+        for label, noise, mode in (("silent-padded", 0.0, 1), ("all exact", 0.0, 2), ("noise floor", 0.01, 1)):
             x = batch(B, n, noise)
+            pl.set_exact_mode(mode)
             pl.demod_host(x)                       # warm
             t = time.perf_counter()
             for _ in range(3):
                 pl.demod_host(x)
             ms = (time.perf_counter() - t) / 3 * 1e3
-            print(f"B={B:4d} {label:14s} {ms:9.2f} ms per batch (host entry, incl. copies)", flush=True)
+            tm = pl.timings()
+            print(f"B={B:4d} {label:14s} {ms:9.2f} ms per batch (host entry, incl. copies); flagged "
+                  f"{pl.exact_streams():4d}; exact stage {tm.get('exact', -1):8.2f} ms, launch {tm.get('launch', -1):8.2f} ms",
+                  flush=True)
 
 
 if __name__ == "__main__":
