@@ -471,30 +471,36 @@ def demodulate_sharded(kind: str, x: np.ndarray, baud, transport, **kw):
     return demod_sharded(np.asarray(x), lambda xs: fn(xs, baud=baud, **kw), transport)
 
 
-def digests(rows: np.ndarray, lens: np.ndarray) -> np.ndarray:
-    """Per-stream 8-byte digest of decoded bytes + length (the gather check), [n] int64."""
+def digests(rows: np.ndarray, lens: np.ndarray, sync: np.ndarray = None) -> np.ndarray:
+    """Per-stream 8-byte digest of decoded bytes + length (+ the sync index,
+    SURVEY §8(e)'s third gathered array, when given) -- the gather check, [n] int64."""
     import hashlib
     return np.array([int.from_bytes(hashlib.blake2b(rows[i, :max(0, int(lens[i]))].tobytes()
-                                                    + int(lens[i]).to_bytes(8, "little", signed=True),
+                                                    + int(lens[i]).to_bytes(8, "little", signed=True)
+                                                    + (b"" if sync is None else
+                                                       int(sync[i]).to_bytes(8, "little", signed=True)),
                                                     digest_size=8).digest(), "little", signed=True)
                      for i in range(rows.shape[0])], np.int64)
 
 
 def gather_check(gathered_payload: np.ndarray, gathered_lengths: np.ndarray, own_payload: np.ndarray,
-                 own_lengths: np.ndarray, layout: ShardLayout, transport) -> list:
+                 own_lengths: np.ndarray, layout: ShardLayout, transport, gathered_sync: np.ndarray = None,
+                 own_sync: np.ndarray = None) -> list:
     """Rank r's slice of the gathered buffer must equal rank r's own launch
     output, stream for stream (its real rows; the slot padding is not
-    compared).  Every rank checks every slice against digests all-gathered
-    from the ranks themselves; returns the sorted ranks whose slices differ
-    (as seen by any rank)."""
+    compared): bytes, lengths and, when given, sync indices.  Every rank
+    checks every slice against digests all-gathered from the ranks
+    themselves; returns the sorted ranks whose slices differ (as seen by any
+    rank)."""
     n_own = layout.launch_rows(transport.rank)
     mine = np.zeros(layout.rows, np.int64)
-    mine[:n_own] = digests(own_payload[:n_own], own_lengths[:n_own])
+    mine[:n_own] = digests(own_payload[:n_own], own_lengths[:n_own], None if own_sync is None else own_sync[:n_own])
     own_all = transport.all_gather(mine)
     bad = np.zeros(transport.world, np.float64)
     for r in range(transport.world):
         n = layout.launch_rows(r)
-        got = digests(gathered_payload[r][:n], gathered_lengths[r][:n])
+        got = digests(gathered_payload[r][:n], gathered_lengths[r][:n],
+                      None if gathered_sync is None else gathered_sync[r][:n])
         bad[r] = float(not np.array_equal(got, own_all[r][:n]))
     flags = transport.all_gather(bad)
     return sorted(int(r) for r in np.flatnonzero(flags.max(axis=0) > 0))

@@ -232,6 +232,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
             c.update(fec=mem.alloc(R * cap), flen=mem.alloc(R * 8), ok=mem.alloc(R * 4))
         if comm is not None:
             c["gather"], c["gather_len"] = mem.alloc(world * R * cap), mem.alloc(world * R * 8)
+            c["gather_sync"] = mem.alloc(world * R * 8)
         ctx.append(c)
 
     def step(c, nb=BL):
@@ -248,6 +249,8 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
             g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
             _amr.check(gather_fn(comm, g_out, c["gather"], R * cap, pl.handle))
             _amr.check(gather_fn(comm, g_len, c["gather_len"], R * 8, pl.handle))
+            # the sync indices: SURVEY §8(e)'s wire format is bytes, lengths and sync_idx
+            _amr.check(gather_fn(comm, c["sync"], c["gather_sync"], R * 8, pl.handle))
 
     def launch_streams(j):
         """streams of launch j of the timed region (the last one may hold fewer steps)"""
@@ -369,25 +372,33 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
     for c in ctx:
         o = np.empty((BL, cap), np.uint8)
         ln = np.empty(BL, np.int64)
+        sy = np.empty(BL, np.int64)
         g_out, g_len = (c["fec"], c["flen"]) if fec_fused else (c["out"], c["len"])
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(o), g_out, BL * cap))
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(ln), g_len, BL * 8))
-        outs.append((o, ln))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(sy), c["sync"], BL * 8))
+        outs.append((o, ln, sy))
 
     # ---- N>1: the gathered buffer must equal every rank's own output ----------
     gather_check = None
     if comm is not None:
         last = (n_launch - 1) % P
-        o, ln = outs[last]
+        o, ln, sy = outs[last]
         gp = np.empty((world, R, cap), np.uint8)
         gl = np.empty((world, R), np.int64)
+        gs = np.empty((world, R), np.int64)
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gp), ctx[last]["gather"], gp.nbytes))
         _amr.check(L.amr_memcpy_d2h(_amr.ptr(gl), ctx[last]["gather_len"], gl.nbytes))
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(gs), ctx[last]["gather_sync"], gs.nbytes))
         shards = multi.ShardLayout(B_global, world, C)
         assert shards.rows == R and shards.launch_rows(rank) == C * B
-        bad_any = multi.gather_check(gp, gl, o, ln, shards, tp)
-        gather_check = (f"ok: every rank's gathered [{world}][{R}][{cap}] buffer == each rank's own bytes and "
-                        "lengths" if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
+        bad_any = multi.gather_check(gp, gl, o, ln, shards, tp, gs, sy)
+        # the RCCL communicator's own view of the job: every rank joined
+        cw, cr = ctypes.c_int(0), ctypes.c_int(-1)
+        _amr.check(L.amr_comm_world(comm, ctypes.byref(cw), ctypes.byref(cr)))
+        gather_check = (f"ok: every rank's gathered [{world}][{R}][{cap}] buffer == each rank's own bytes, "
+                        f"lengths and sync indices; RCCL world {cw.value}, this rank {cr.value}"
+                        if not bad_any else f"MISMATCH: slices of ranks {bad_any}")
 
     # ---- parity: sampled streams of in-flight slots vs the oracle; CPU baseline
     result = None
@@ -448,7 +459,8 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                     cdt += time.perf_counter() - t1
                     reps += 1
             if k == 0 and world == 1:                     # the CPU baseline: rank 0 at N = 1 only
-                how = ("oracle.fsk_demodulate (C filtfilt + scipy.signal.hilbert + C decide), thread pool over streams"
+                how = ("oracle.fsk_demodulate (C filtfilt + the C restatement of pocketfft's Hilbert "
+                       "(oracle/amr_pocketfft.c) + C decide), thread pool over streams"
                        if fsk else "the C restatement oracle/amr_oracle.c, OpenMP over streams" +
                        (" + oracle.fec_decode" if fec_fused else ""))
                 cpu = {"value": round(reps * len(idx) * sym_per_stream / cdt / 1e6, 3), "unit": "Msym/s",
@@ -456,7 +468,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                        "cores_note": cores_how,
                        "sample": f"{len(idx)} of the {BL} streams of benchmark batch 0 ({N} samples each)"
                                  + (f", {reps} passes" if reps > 1 else "") + f" through {how}, {cdt:.2f} s wall"}
-            o, ln = outs[k]
+            o, ln = outs[k][:2]
             bad_total += [(k, int(i)) for j, i in enumerate(idx) if o[i, :ln[i]].tobytes() != want[j]]
             checked += len(idx)
             n_slots += 1
@@ -604,14 +616,13 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                 "parity": parity, "scaling_1_to_8": "measured by the driver from this line at N = 1, 2, 4, 8"}
         if gather_check is not None:
             result["gather_check"] = gather_check
-        if not fsk:
-            result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
+        result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
 
         # PCIe-inclusive rate (never `value`): the host API on the
         # same batch from host memory, H2D + demod + D2H, one batch at a time
         if headline and world == 1 and not fec_fused and not args.no_host_path:
             _amr.check(L.amr_memcpy_d2h(_amr.ptr(xh), ctx[0]["x"], xh.nbytes))
-            o0, ln0 = outs[0]
+            o0, ln0 = outs[0][:2]
             host_res = (xh, o0, ln0)
     elif gather_check is not None and "MISMATCH" in gather_check:
         log(f"[rank {rank}] {name}: {gather_check}")
@@ -626,7 +637,48 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
                                                        sym_per_stream, host_res[1], host_res[2], args.host_plans)
         if not args.no_dropin and not fsk:
             result["dropin"] = dropin_path(host_res[0], baud, sym_per_stream, host_res[1], host_res[2])
+    if result is not None and fsk and world == 1 and not args.no_cpu:
+        result["exact_probe"] = fsk_exact_probe(N, baud, mark, space, dev)
     return result
+
+
+def fsk_exact_probe(N, baud, mark, space, dev, B=2048):
+    """The FSK exact path at scale (never `value`): B
+    zero-padded captures -- digital silence before the frame, as a gated
+    receiver records them -- whose compares F2 flags, every stream forced
+    through the exact path (mode 2), and the same batch with a noise floor
+    (nothing flagged); device time of one launch (HIP events, first kernel to
+    last output), H2D / D2H excluded, median of 3."""
+    import _fsk
+    import synth
+    rng = np.random.default_rng(5)
+    rows = []
+    for i in range(B):
+        w = synth.fsk_waveform(synth.random_frame(rng, 40), baud, mark, space, float(FS))
+        off = 2000 + 37 * (i % 512)
+        row = np.zeros(N, np.float32)
+        seg = w[:N - off]
+        row[off:off + seg.size] = seg
+        rows.append(row)
+    x = np.stack(rows)
+    pl = _fsk.FskPlan(N, baud, mark, space, FS, max_streams=B, device=dev)
+    pl.enable_timing(True)
+    res = {"streams": B, "samples": N, "unit": "ms"}
+    for label, xx, mode in (("silent_padded", x, 1), ("all_exact", x, 2),
+                            ("noise_floor", x + rng.normal(0, 0.01, x.shape).astype(np.float32), 1)):
+        pl.set_exact_mode(mode)
+        pl.demod_host(xx)
+        ts, ex = [], []
+        for _ in range(3):
+            pl.demod_host(xx)
+            t = pl.timings()
+            ts.append(t["launch"])
+            ex.append(t.get("exact", 0.0))
+        res[label] = {"launch_ms": round(float(np.median(ts)), 2), "exact_stage_ms": round(float(np.median(ex)), 2),
+                      "exact_path_streams": pl.exact_streams()}
+    del pl
+    gc.collect()
+    return res
 
 
 def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
@@ -661,6 +713,44 @@ def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
                           "what": f"modem.qpsk_demodulate(x, baud={int(baud)}) on one {x1.size}-sample float32 capture "
                                   "(H2D + demod + D2H, cached plan), median of 5",
                           "bytes_equal": one == out_dev[0, :len_dev[0]].tobytes()}
+    # the same capture through the C port on one host core (the CPU side of
+    # the single-capture call pattern, filebeep_advanced_v2.py:324), and where
+    # the GPU drop-in overtakes one core / all host cores as the batch grows
+    from oracle import oracle
+    threads, _ = host_cores()
+    tc = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        oracle.psk_demod_batch("qpsk", x1[None], baud, n_threads=1)
+        tc.append(time.perf_counter() - t1)
+    c1 = float(np.median(tc))
+    res["one_capture"]["c_port_1core_ms"] = round(c1 * 1e3, 3)
+    nb = min(B, 64)
+    t1 = time.perf_counter()
+    oracle.psk_demod_batch("qpsk", xh[:nb], baud, n_threads=threads)
+    cn = (time.perf_counter() - t1) / nb
+    gpu = {}
+    for b in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        if b > B:
+            break
+        xb = np.ascontiguousarray(xh[:b])
+        modem.qpsk_demodulate_batch(xb, baud=baud)          # plan for this bucket
+        tg = []
+        for _ in range(3):
+            t1 = time.perf_counter()
+            modem.qpsk_demodulate_batch(xb, baud=baud)
+            tg.append(time.perf_counter() - t1)
+        gpu[b] = min(tg)
+    over1 = next((b for b, t in gpu.items() if t < b * c1), None)
+    overn = next((b for b, t in gpu.items() if t < b * cn), None)
+    res["crossover"] = {
+        "gpu_dropin_ms": {str(b): round(t * 1e3, 3) for b, t in gpu.items()},
+        "cpu_1core_ms_per_capture": round(c1 * 1e3, 3),
+        f"cpu_{threads}core_ms_per_capture": round(cn * 1e3, 3),
+        "gpu_overtakes_1core_at_batch": over1, f"gpu_overtakes_{threads}core_at_batch": overn,
+        "what": "modem.qpsk_demodulate_batch (host memory in and out, cached plans) vs the C port "
+                "(oracle.psk_demod_batch) on the same 1-s captures; the first batch size measured at which "
+                "the GPU call is faster (None: not within the sizes measured)"}
 
     def run():
         raws = modem.qpsk_demodulate_batch(xh, baud=baud)
@@ -889,7 +979,7 @@ def main():
                                                 "kernel_ms_solo", "cpu_baseline", "config")}
                 subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
-                for k in ("gather_check", "exact_path_streams"):
+                for k in ("gather_check", "exact_path_streams", "exact_probe"):
                     if k in r:
                         subs[name][k] = r[k]
         if rank == 0 and result is not None:
