@@ -293,11 +293,25 @@ class TcpStore:
             self.server.shutdown()
 
 
+def _parent_instance() -> str:
+    """The parent process's pid and start time (/proc/<ppid>/stat field 22):
+    the ranks of one torch.distributed.run launch, or of one multiprocessing
+    pool, share it, and a later launch cannot -- even one whose agent got the
+    same pid -- so a store left behind by a crashed run is never read again
+    (ADVICE r3)."""
+    ppid = os.getppid()
+    try:
+        with open(f"/proc/{ppid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return f"{ppid}_{fields[19]}"
+    except (OSError, IndexError):
+        return str(ppid)
+
+
 def store_from_env(rank: int, world: int):
     """The bootstrap store: AMR_STORE=file:<dir> or tcp://<host>:<port> (rank 0
-    serves), else a FileStore under the temp directory named after MASTER_PORT
-    and the parent process (the ranks of one torch.distributed.run launch, or
-    of one multiprocessing pool, share both)."""
+    serves), else a FileStore under the temp directory named after MASTER_PORT,
+    the torchrun run id and the parent process instance (pid + start time)."""
     spec = os.environ.get("AMR_STORE", "")
     if spec.startswith("tcp://"):
         host, port = spec[6:].rsplit(":", 1)
@@ -305,7 +319,8 @@ def store_from_env(rank: int, world: int):
     if spec.startswith("file:"):
         return FileStore(spec[5:])
     import tempfile
-    tag = f"amr_store_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{world}"
+    tag = (f"amr_store_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', '')}_"
+           f"{_parent_instance()}_{world}")
     return FileStore(os.path.join(tempfile.gettempdir(), tag))
 
 
