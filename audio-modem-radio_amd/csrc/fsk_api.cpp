@@ -346,6 +346,7 @@ struct amr_fsk_plan {
   uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
   double* xpool = nullptr;     // pocketfft's twiddle / chirp tables of length n
   PfLen* xL = nullptr;         // pocketfft's plans of length n (device copy)
+  bool x_lean = false;         // pf_hilbert_lean: E2 runs the lean fused kernel
   int64_t slot_doubles = 0;
   int n_slots = 0;
   bool ran_exact = false;      // the last call ran the exact path (its count is in xlist[max_streams])
@@ -440,6 +441,8 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.pool = pl->xpool;
   X.fct = (double)(1.0L / (long double)pl->p.n);
   X.xbits = pl->xbits;
+  X.fuse = (int)pf_fuse_on();
+  X.lean = X.fuse && pl->x_lean;
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
   pl->ran_exact = true;
   HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));
@@ -619,10 +622,11 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.exact = exact_env && p.n_bits > 0;
   if (g.exact) {
     g.slot_doubles = n + pf_scratch_doubles_n(n);    // the row, then its transforms' scratch
-    // one workgroup per slot: up to 2 per stream and 1024 (4 per CU: each
-    // pass is latency-bound), within 2 GiB of slots
+    // one persistent workgroup per slot: up to 2 per stream and 512 (2 per
+    // CU; the launch takes no more than are resident at once, E2's register
+    // budget allows one per CU), within 2 GiB of slots
     g.n_slots = (int)std::max<int64_t>(
-        1, std::min<int64_t>({2 * max_streams, 1024, ((int64_t)1 << 31) / (g.slot_doubles * 8)}));
+        1, std::min<int64_t>({2 * max_streams, 512, ((int64_t)1 << 31) / (g.slot_doubles * 8)}));
     g.xflags = (max_streams + 31) / 32 * 4;
     g.amb = max_streams * 8;
     g.xlist = (max_streams + 1) * 4;
@@ -736,6 +740,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       return fail(AMR_E_HIP, std::string("exact path tables: ") + hipGetErrorString(e));
     }
     pl->exact_on = true;
+    pl->x_lean = pf_hilbert_lean(L);
     pl->p.amb = pl->amb;
     pl->p.xflags = pl->xflags;         // F3 reads a flagged stream's bits from xbits
     pl->p.xbits = pl->xbits;
@@ -1097,7 +1102,7 @@ int amr_hilbert_env_exact_host(const double* x, int64_t n, int64_t batch, double
   PfDev D;
   double *xd = nullptr, *slots = nullptr;
   const int n_slots = (int)std::min<int64_t>(batch, 128);
-  const int64_t sd = pf_scratch_doubles_n(n);
+  const int64_t sd = n + pf_scratch_doubles_n(n);   // the fused envelope keeps the spectrum in its slot
   int rc = AMR_OK;
   hipError_t e = hipMalloc(&slots, (size_t)(n_slots * sd * 8));
   if (e == hipSuccess) e = hipMalloc(&xd, (size_t)(batch * n * 8));
@@ -1106,7 +1111,8 @@ int amr_hilbert_env_exact_host(const double* x, int64_t n, int64_t batch, double
   if (rc == AMR_OK) {
     e = hipMemcpyAsync(xd, x, (size_t)(batch * n * 8), hipMemcpyHostToDevice, st);
     if (e == hipSuccess)
-      e = launch_pf_hilbert_env(D.dL, D.pool, xd, n, batch, slots, sd, n_slots, (double)(1.0L / (long double)n), st);
+      e = launch_pf_hilbert_env(D.dL, D.pool, xd, n, batch, slots, sd, n_slots, (double)(1.0L / (long double)n),
+                                pf_hilbert_lean(D.L), st);
     if (e == hipSuccess) e = hipMemcpyAsync(env, xd, (size_t)(batch * n * 8), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) rc = fail(AMR_E_HIP, std::string("exact envelopes: ") + hipGetErrorString(e));

@@ -23,6 +23,8 @@ struct FskExact {
   const double* pool;
   double fct;              // double(1 / long double n)
   uint8_t* xbits;          // [B][bits_stride] exact compare bits, F3 reads them for flagged streams
+  int fuse;                // LDS-fused transforms (pf_fuse_on)
+  int lean;                // ... and every radix hard-coded: k_exact_env_lean
 };
 
 // E0: F2's flags -> X.list / X.count.  Then F1 in list mode (fsk_api.cpp),

@@ -111,16 +111,43 @@ __global__ __launch_bounds__(kListThreads) void k_exact_list(const uint32_t* __r
 // it, back into the same interleaved positions of z
 constexpr int kEnvThreads = 512;
 __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact X) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  const int64_t cnt = *X.count;
+  const int64_t n = p.n;
+  double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
+  if (X.fuse && pf_hilbert_fusable(*X.L)) {   // straight from z and back, every transform in LDS tiles
+    for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+      double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
+      pf::pf_hilbert_env_x(
+          *X.L, X.pool, [=](int64_t i) { return zr[2 * i]; }, [=](int64_t i, double e) { zr[2 * i] = e; }, c, X.fct,
+          lds);
+    }
+    return;
+  }
+  for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+    double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = zr[2 * i];
+    __syncthreads();
+    pf::pf_hilbert_env(*X.L, X.pool, c, c, c + n, X.fct, X.fuse ? lds : nullptr);
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) zr[2 * i] = c[i];
+    __syncthreads();
+  }
+}
+
+// E2, lean: plans with only hard-coded radices, every transform fused (no
+// fallback code in the kernel, so a smaller register budget than k_exact_env)
+// two workgroups per CU (4 waves per SIMD: <= 128 VGPRs)
+__global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_env_lean(FskParams p,
+                                                                                                         FskExact X) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
   const int64_t cnt = *X.count;
   const int64_t n = p.n;
   double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
     double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = zr[2 * i];
-    __syncthreads();
-    pf::pf_hilbert_env(*X.L, X.pool, c, c, c + n, X.fct);
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) zr[2 * i] = c[i];
-    __syncthreads();
+    auto src = [=](int i) { return zr[2 * i]; };
+    auto fin = [=](int i, double e) { zr[2 * i] = e; };
+    pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
   }
 }
 
@@ -160,7 +187,23 @@ hipError_t launch_fsk_exact_list(int64_t B, const FskExact& X, hipStream_t st) {
 
 hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st) {
   if (B < 1) return hipSuccess;
-  hipLaunchKernelGGL(k_exact_env, dim3((unsigned)X.n_slots), dim3(kEnvThreads), 0, st, p, X);
+  // a persistent grid no larger than what is resident at once: a workgroup
+  // beyond that would start its rows only after a resident one finished all of
+  // its own
+  auto resident = [](const void* k) {
+    int dev = 0, per_cu = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kEnvThreads, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return std::max(1, per_cu * cus);
+  };
+  static const int res_full = resident((const void*)k_exact_env), res_lean = resident((const void*)k_exact_env_lean);
+  if (X.lean)
+    hipLaunchKernelGGL(k_exact_env_lean, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0, st, p,
+                       X);
+  else
+    hipLaunchKernelGGL(k_exact_env, dim3((unsigned)std::min(X.n_slots, res_full)), dim3(kEnvThreads), 0, st, p, X);
   hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 2048)), dim3(kBitsThreads), 0, st, p, X);
   return hipGetLastError();
 }

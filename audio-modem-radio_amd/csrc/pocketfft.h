@@ -16,7 +16,8 @@
 
 namespace amr {
 
-constexpr int kPfMaxF = 32;   // factors of one plan (a length < 2^31 has at most 30)
+constexpr int kPfMaxF = 32;
+constexpr int64_t kPfMaxLen = (int64_t)1 << 27;   // longest row the device transforms take   // factors of one plan (a length < 2^31 has at most 30)
 
 // one factor of a plan: radix ip, l1 = product of the factors before it,
 // ido = len / (l1 * ip); tw / tws: offsets (in doubles) of its twiddles and of
@@ -25,11 +26,38 @@ struct PfFact {
   int64_t ip, l1, ido, tw, tws;
 };
 
-// an FFTPACK-style plan (pocketfft's cfftp or rfftp)
+// LDS-fused execution of consecutive complex passes (pocketfft_dev.h
+// cgroup): passes f0 .. f0 + nf - 1 with radix product P, the last one's ido
+// D and the first one's l1 L (len = L * P * D).  A tile is Qi consecutive
+// residues i (mod D) times Qk consecutive blocks k: its Q = Qi * Qk columns
+// of P elements (i + D (j + P k), j < P) go through every pass of the group
+// in LDS and come out at i + D (k + L j) -- the same butterflies, in the same
+// order, as the passes run one by one over the whole array.
+constexpr int kPfTileElems = 2048;   // complex elements per LDS buffer (32 KiB; two buffers)
+constexpr int kPfMaxGroupP = 512;    // radix product of a group (>= 4 columns per tile)
+// rfftp forward (r2hc) groups, in executed order (ido growing): passes
+// f0, f0 - 1, ..., f0 - nf + 1; D = the first one's ido, L = the last one's l1;
+// a multi-pass group couples every residue mod D, so a tile is Qk whole
+// blocks k of D * P reals (read at a + D (k + L w), written to k D P + ...).
+// Q = 0 marks a pass run unfused over the whole array (too large a block, or
+// a generic radix).
+constexpr int kPfTileDoubles = 2 * kPfTileElems;
+constexpr int kPfMinRun = 16;        // doubles a tile reads contiguously, at least
+struct PfGroup {
+  int f0, nf;
+  int64_t P, D, L;
+  int Q, Qi, Qk;
+};
+
+// an FFTPACK-style plan (pocketfft's cfftp or rfftp); fused: the passes are
+// grouped (g[0..ng)): cfftp when every radix is hard-coded, rfftp (forward)
+// always
 struct PfPasses {
   int64_t len;
   int nf;
   PfFact f[kPfMaxF];
+  int fused, ng;
+  PfGroup g[kPfMaxF];
 };
 
 // pocketfft's fftblue(n): chirp bk (n complex), FFT of the padded chirp / n2
@@ -48,6 +76,23 @@ struct PfLen {
   PfPasses r, c;
   PfBlue bl;
 };
+
+// AMR_PF_FUSE=0 (A/B switch): run the complex transforms pass by pass
+// instead of through the LDS-fused groups; default on
+bool pf_fuse_on();
+
+// whether |hilbert| of a length-L.n row runs every transform LDS-fused
+// (pf_hilbert_env_x), and whether with hard-coded radices only (the lean
+// kernels, no generic or unfused fallback code)
+__host__ __device__ inline bool pf_hilbert_fusable(const PfLen& L) {
+  return !L.rblue && !L.cblue && L.r.fused && L.c.fused && L.r.nf > 0;
+}
+__host__ __device__ inline bool pf_hilbert_lean(const PfLen& L) {
+  if (!pf_hilbert_fusable(L)) return false;
+  for (int k = 0; k < L.r.nf; ++k)
+    if (L.r.f[k].ip > 5) return false;
+  return true;
+}
 
 // host: the plans of length n, twiddles appended to pool (aligned to a
 // complex); bkf (Bluestein) is left to pf_finish on the device
@@ -73,6 +118,7 @@ hipError_t launch_pf_resample(const PfLen* dLx, const double* poolx, const PfLen
 // |scipy.signal.hilbert(x)| of `batch` real rows of x, in place (diagnostic
 // entry amr_hilbert_env_exact_host; the FSK exact path runs the same routine)
 hipError_t launch_pf_hilbert_env(const PfLen* dL, const double* pool, double* x, int64_t n, int64_t batch,
-                                 double* slots, int64_t slot_doubles, int n_slots, double fct, hipStream_t st);
+                                 double* slots, int64_t slot_doubles, int n_slots, double fct, bool lean,
+                                 hipStream_t st);
 
 }  // namespace amr

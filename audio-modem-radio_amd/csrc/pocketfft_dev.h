@@ -51,66 +51,58 @@ __device__ __forceinline__ Cx rot135(Cx a) {
   return {h * (-a.r - a.i), h * (a.r - a.i)};
 }
 
-#define PF_FOR(t, N) for (int64_t t = threadIdx.x; t < (N); t += blockDim.x)
+#define PF_FOR(t, N) for (int t = (int)threadIdx.x; t < (int)(N); t += (int)blockDim.x)
 
 // ======================= complex passes (cfftp) =============================
-#define CC(a, b, c) cc[(a) + ido * ((b) + IP * (c))]
-#define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
+// One butterfly of pocketfft's pass of radix IP at index i of a pass with ido:
+// v[m] = CC(i, m, k) in, v[m] = CH(i, k, m) out (pass2b / pass3b / pass4b /
+// pass5b / pass7 / pass8 / pass11 and their forward twins).  The per-pass
+// loops (passk) and the LDS tile executor (cgroup) both run these, so the
+// arithmetic is one statement.
 #define WA(x, i) wa[(i) - 1 + (x) * (ido - 1)]
 
 template <bool FWD>
-__device__ void pass2(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
-  constexpr int64_t IP = 2;
-  PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
-    CH(i, k, 0) = add(CC(i, 0, k), CC(i, 1, k));
-    const Cx d = sub(CC(i, 0, k), CC(i, 1, k));
-    CH(i, k, 1) = i == 0 ? d : smul<FWD>(d, WA(0, i));
-  }
+__device__ __forceinline__ void bfly2(Cx* v, int i, const Cx* wa, int ido) {
+  const Cx a = v[0], b = v[1];
+  v[0] = add(a, b);
+  const Cx d = sub(a, b);
+  v[1] = i == 0 ? d : smul<FWD>(d, WA(0, i));
 }
 
 template <bool FWD>
-__device__ void pass3(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
-  constexpr int64_t IP = 3;
+__device__ __forceinline__ void bfly3(Cx* v, int i, const Cx* wa, int ido) {
   const double tw1r = -0.5, tw1i = (FWD ? -1 : 1) * 0.8660254037844386467637231707529362;
-  PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
-    const Cx t0 = CC(i, 0, k), t1 = add(CC(i, 1, k), CC(i, 2, k)), t2 = sub(CC(i, 1, k), CC(i, 2, k));
-    CH(i, k, 0) = add(t0, t1);
-    const Cx ca = {t0.r + t1.r * tw1r, t0.i + t1.i * tw1r};
-    const Cx cb = {-(t2.i * tw1i), t2.r * tw1i};
-    if (i == 0) {
-      CH(0, k, 1) = add(ca, cb);
-      CH(0, k, 2) = sub(ca, cb);
-    } else {
-      CH(i, k, 1) = smul<FWD>(add(ca, cb), WA(0, i));
-      CH(i, k, 2) = smul<FWD>(sub(ca, cb), WA(1, i));
-    }
+  const Cx t0 = v[0], t1 = add(v[1], v[2]), t2 = sub(v[1], v[2]);
+  v[0] = add(t0, t1);
+  const Cx ca = {t0.r + t1.r * tw1r, t0.i + t1.i * tw1r};
+  const Cx cb = {-(t2.i * tw1i), t2.r * tw1i};
+  if (i == 0) {
+    v[1] = add(ca, cb);
+    v[2] = sub(ca, cb);
+  } else {
+    v[1] = smul<FWD>(add(ca, cb), WA(0, i));
+    v[2] = smul<FWD>(sub(ca, cb), WA(1, i));
   }
 }
 
 template <bool FWD>
-__device__ void pass4(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
-  constexpr int64_t IP = 4;
-  PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
-    const Cx t2 = add(CC(i, 0, k), CC(i, 2, k)), t1 = sub(CC(i, 0, k), CC(i, 2, k));
-    const Cx t3 = add(CC(i, 1, k), CC(i, 3, k)), t4 = rot90<FWD>(sub(CC(i, 1, k), CC(i, 3, k)));
-    if (i == 0) {
-      CH(0, k, 0) = add(t2, t3);
-      CH(0, k, 2) = sub(t2, t3);
-      CH(0, k, 1) = add(t1, t4);
-      CH(0, k, 3) = sub(t1, t4);
-    } else {
-      CH(i, k, 0) = add(t2, t3);
-      CH(i, k, 1) = smul<FWD>(add(t1, t4), WA(0, i));
-      CH(i, k, 2) = smul<FWD>(sub(t2, t3), WA(1, i));
-      CH(i, k, 3) = smul<FWD>(sub(t1, t4), WA(2, i));
-    }
+__device__ __forceinline__ void bfly4(Cx* v, int i, const Cx* wa, int ido) {
+  const Cx t2 = add(v[0], v[2]), t1 = sub(v[0], v[2]);
+  const Cx t3 = add(v[1], v[3]), t4 = rot90<FWD>(sub(v[1], v[3]));
+  if (i == 0) {
+    v[0] = add(t2, t3);
+    v[2] = sub(t2, t3);
+    v[1] = add(t1, t4);
+    v[3] = sub(t1, t4);
+  } else {
+    v[0] = add(t2, t3);
+    v[1] = smul<FWD>(add(t1, t4), WA(0, i));
+    v[2] = smul<FWD>(sub(t2, t3), WA(1, i));
+    v[3] = smul<FWD>(sub(t1, t4), WA(2, i));
   }
 }
 
-// passes 5, 7, 11 (pocketfft's PREPn / PARTSTEPn): pairs t[j] = CC(j) +
+// radices 5, 7, 11 (pocketfft's PREPn / PARTSTEPn): pairs t[j] = CC(j) +
 // CC(ip-j), d[j] = CC(j) - CC(ip-j); output u = 1..h:
 //   ca = t0 + c(u,1) t[1] + ... + c(u,h) t[h]        (left to right)
 //   cb = (-(s(u,1) d[1].i +- ...), s(u,1) d[1].r +- ...)
@@ -141,128 +133,141 @@ struct OddTw<11> {
 };
 
 template <bool FWD, int IPN>
-__device__ void passodd(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
-  constexpr int64_t IP = IPN;
+__device__ __forceinline__ void bflyodd(Cx* v, int i, const Cx* wa, int ido) {
   constexpr int H = (IPN - 1) / 2;
-  PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
-    Cx tt[H + 1], dd[H + 1];
-    const Cx t0 = CC(i, 0, k);
+  Cx tt[H + 1], dd[H + 1];
+  const Cx t0 = v[0];
+#pragma unroll
+  for (int j = 1; j <= H; ++j) {
+    tt[j] = add(v[j], v[IPN - j]);
+    dd[j] = sub(v[j], v[IPN - j]);
+  }
+  Cx s0 = t0;
+#pragma unroll
+  for (int j = 1; j <= H; ++j) s0.r = s0.r + tt[j].r;
+#pragma unroll
+  for (int j = 1; j <= H; ++j) s0.i = s0.i + tt[j].i;
+  v[0] = s0;
+#pragma unroll
+  for (int u = 1; u <= H; ++u) {
+    Cx ca = t0;
+    double cbr = 0.0, cbi = 0.0;
 #pragma unroll
     for (int j = 1; j <= H; ++j) {
-      tt[j] = add(CC(i, j, k), CC(i, IPN - j, k));
-      dd[j] = sub(CC(i, j, k), CC(i, IPN - j, k));
-    }
-    Cx s0 = t0;
-#pragma unroll
-    for (int j = 1; j <= H; ++j) s0.r = s0.r + tt[j].r;
-#pragma unroll
-    for (int j = 1; j <= H; ++j) s0.i = s0.i + tt[j].i;
-    CH(i, k, 0) = s0;
-#pragma unroll
-    for (int u = 1; u <= H; ++u) {
-      Cx ca = t0;
-      double cbr = 0.0, cbi = 0.0;
-#pragma unroll
-      for (int j = 1; j <= H; ++j) {
-        int r = (u * j) % IPN;
-        const bool neg = r > H;
-        if (neg) r = IPN - r;
-        const double cr = OddTw<IPN>::c[r], si = (FWD ? -1.0 : 1.0) * OddTw<IPN>::s[r];
-        ca.r = ca.r + cr * tt[j].r;
-        ca.i = ca.i + cr * tt[j].i;
-        if (j == 1) {
-          cbi = si * dd[j].r;
-          cbr = si * dd[j].i;
-        } else if (!neg) {
-          cbi = cbi + si * dd[j].r;
-          cbr = cbr + si * dd[j].i;
-        } else {
-          cbi = cbi - si * dd[j].r;
-          cbr = cbr - si * dd[j].i;
-        }
-      }
-      const Cx cb = {-cbr, cbi};
-      if (i == 0) {
-        CH(0, k, u) = add(ca, cb);
-        CH(0, k, IPN - u) = sub(ca, cb);
+      int r = (u * j) % IPN;
+      const bool neg = r > H;
+      if (neg) r = IPN - r;
+      const double cr = OddTw<IPN>::c[r], si = (FWD ? -1.0 : 1.0) * OddTw<IPN>::s[r];
+      ca.r = ca.r + cr * tt[j].r;
+      ca.i = ca.i + cr * tt[j].i;
+      if (j == 1) {
+        cbi = si * dd[j].r;
+        cbr = si * dd[j].i;
+      } else if (!neg) {
+        cbi = cbi + si * dd[j].r;
+        cbr = cbr + si * dd[j].i;
       } else {
-        CH(i, k, u) = smul<FWD>(add(ca, cb), WA(u - 1, i));
-        CH(i, k, IPN - u) = smul<FWD>(sub(ca, cb), WA(IPN - u - 1, i));
+        cbi = cbi - si * dd[j].r;
+        cbr = cbr - si * dd[j].i;
       }
+    }
+    const Cx cb = {-cbr, cbi};
+    if (i == 0) {
+      v[u] = add(ca, cb);
+      v[IPN - u] = sub(ca, cb);
+    } else {
+      v[u] = smul<FWD>(add(ca, cb), WA(u - 1, i));
+      v[IPN - u] = smul<FWD>(sub(ca, cb), WA(IPN - u - 1, i));
     }
   }
 }
 
 template <bool FWD>
-__device__ void pass8(int64_t ido, int64_t l1, const Cx* cc, Cx* ch, const Cx* wa) {
-  constexpr int64_t IP = 8;
-  PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
-    Cx a1 = add(CC(i, 1, k), CC(i, 5, k)), a5 = sub(CC(i, 1, k), CC(i, 5, k));
-    Cx a3 = add(CC(i, 3, k), CC(i, 7, k)), a7 = sub(CC(i, 3, k), CC(i, 7, k));
-    Cx u = a1;
-    a1 = add(u, a3);
-    a3 = rot90<FWD>(sub(u, a3));
-    a7 = rot90<FWD>(a7);
-    u = a5;
-    a5 = rot45<FWD>(add(u, a7));
-    a7 = rot135<FWD>(sub(u, a7));
-    Cx a0 = add(CC(i, 0, k), CC(i, 4, k)), a4 = sub(CC(i, 0, k), CC(i, 4, k));
-    Cx a2 = add(CC(i, 2, k), CC(i, 6, k)), a6 = sub(CC(i, 2, k), CC(i, 6, k));
-    if (i == 0) {
-      const Cx s02 = add(a0, a2), d02 = sub(a0, a2);
-      CH(0, k, 0) = add(s02, a1);
-      CH(0, k, 4) = sub(s02, a1);
-      CH(0, k, 2) = add(d02, a3);
-      CH(0, k, 6) = sub(d02, a3);
-      a6 = rot90<FWD>(a6);
-      const Cx s46 = add(a4, a6), d46 = sub(a4, a6);
-      CH(0, k, 1) = add(s46, a5);
-      CH(0, k, 5) = sub(s46, a5);
-      CH(0, k, 3) = add(d46, a7);
-      CH(0, k, 7) = sub(d46, a7);
-    } else {
-      u = a0;
-      a0 = add(u, a2);
-      a2 = sub(u, a2);
-      CH(i, k, 0) = add(a0, a1);
-      CH(i, k, 4) = smul<FWD>(sub(a0, a1), WA(3, i));
-      CH(i, k, 2) = smul<FWD>(add(a2, a3), WA(1, i));
-      CH(i, k, 6) = smul<FWD>(sub(a2, a3), WA(5, i));
-      a6 = rot90<FWD>(a6);
-      u = a4;
-      a4 = add(u, a6);
-      a6 = sub(u, a6);
-      CH(i, k, 1) = smul<FWD>(add(a4, a5), WA(0, i));
-      CH(i, k, 5) = smul<FWD>(sub(a4, a5), WA(4, i));
-      CH(i, k, 3) = smul<FWD>(add(a6, a7), WA(2, i));
-      CH(i, k, 7) = smul<FWD>(sub(a6, a7), WA(6, i));
-    }
+__device__ __forceinline__ void bfly8(Cx* v, int i, const Cx* wa, int ido) {
+  Cx a1 = add(v[1], v[5]), a5 = sub(v[1], v[5]);
+  Cx a3 = add(v[3], v[7]), a7 = sub(v[3], v[7]);
+  Cx u = a1;
+  a1 = add(u, a3);
+  a3 = rot90<FWD>(sub(u, a3));
+  a7 = rot90<FWD>(a7);
+  u = a5;
+  a5 = rot45<FWD>(add(u, a7));
+  a7 = rot135<FWD>(sub(u, a7));
+  Cx a0 = add(v[0], v[4]), a4 = sub(v[0], v[4]);
+  Cx a2 = add(v[2], v[6]), a6 = sub(v[2], v[6]);
+  if (i == 0) {
+    const Cx s02 = add(a0, a2), d02 = sub(a0, a2);
+    v[0] = add(s02, a1);
+    v[4] = sub(s02, a1);
+    v[2] = add(d02, a3);
+    v[6] = sub(d02, a3);
+    a6 = rot90<FWD>(a6);
+    const Cx s46 = add(a4, a6), d46 = sub(a4, a6);
+    v[1] = add(s46, a5);
+    v[5] = sub(s46, a5);
+    v[3] = add(d46, a7);
+    v[7] = sub(d46, a7);
+  } else {
+    u = a0;
+    a0 = add(u, a2);
+    a2 = sub(u, a2);
+    v[0] = add(a0, a1);
+    v[4] = smul<FWD>(sub(a0, a1), WA(3, i));
+    v[2] = smul<FWD>(add(a2, a3), WA(1, i));
+    v[6] = smul<FWD>(sub(a2, a3), WA(5, i));
+    a6 = rot90<FWD>(a6);
+    u = a4;
+    a4 = add(u, a6);
+    a6 = sub(u, a6);
+    v[1] = smul<FWD>(add(a4, a5), WA(0, i));
+    v[5] = smul<FWD>(sub(a4, a5), WA(4, i));
+    v[3] = smul<FWD>(add(a6, a7), WA(2, i));
+    v[7] = smul<FWD>(sub(a6, a7), WA(6, i));
   }
 }
-#undef CC
-#undef CH
 #undef WA
+
+template <bool FWD, int IP>
+__device__ __forceinline__ void bfly(Cx* v, int i, const Cx* wa, int ido) {
+  if constexpr (IP == 2) bfly2<FWD>(v, i, wa, ido);
+  else if constexpr (IP == 3) bfly3<FWD>(v, i, wa, ido);
+  else if constexpr (IP == 4) bfly4<FWD>(v, i, wa, ido);
+  else if constexpr (IP == 8) bfly8<FWD>(v, i, wa, ido);
+  else bflyodd<FWD, IP>(v, i, wa, ido);
+}
+
+// one whole pass over global memory (the unfused executor)
+template <bool FWD, int IP>
+__device__ void passk(int ido, int l1, const Cx* __restrict__ cc, Cx* __restrict__ ch, const Cx* wa) {
+  PF_FOR(t, l1 * ido) {
+    const int k = t / ido, i = t - k * ido;
+    Cx v[IP];
+#pragma unroll
+    for (int m = 0; m < IP; ++m) v[m] = cc[i + ido * (m + IP * k)];
+    bfly<FWD, IP>(v, i, wa, ido);
+#pragma unroll
+    for (int m = 0; m < IP; ++m) ch[i + ido * (k + l1 * m)] = v[m];
+  }
+}
 
 // generic pass (ip > 11): the result lands in cc
 template <bool FWD>
-__device__ void passg(int64_t ido, int64_t ip, int64_t l1, Cx* cc, Cx* ch, const Cx* wa, const Cx* csarr) {
-  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+__device__ void passg(int ido, int ip, int l1, Cx* cc, Cx* ch, const Cx* wa, const Cx* csarr) {
+  const int cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
 #define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
 #define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
 #define CX(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
 #define CX2(a, b) cc[(a) + idl1 * (b)]
 #define CH2(a, b) ch[(a) + idl1 * (b)]
-  auto wal = [&](int64_t x) -> Cx {
+  auto wal = [&](int x) -> Cx {
     if (x == 0) return {1.0, 0.0};
     const Cx c = csarr[x];
     return {c.r, FWD ? -c.i : c.i};
   };
   PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
+    const int k = t / ido, i = t - k * ido;
     CH(i, k, 0) = CC(i, 0, k);
-    for (int64_t j = 1, jc = ip - 1; j < ipph; ++j, --jc) {
+    for (int j = 1, jc = ip - 1; j < ipph; ++j, --jc) {
       CH(i, k, j) = add(CC(i, j, k), CC(i, jc, k));
       CH(i, k, jc) = sub(CC(i, j, k), CC(i, jc, k));
     }
@@ -270,17 +275,17 @@ __device__ void passg(int64_t ido, int64_t ip, int64_t l1, Cx* cc, Cx* ch, const
   __syncthreads();
   PF_FOR(ik, idl1) {
     Cx tmp = CH2(ik, 0);
-    for (int64_t j = 1; j < ipph; ++j) tmp = add(tmp, CH2(ik, j));
+    for (int j = 1; j < ipph; ++j) tmp = add(tmp, CH2(ik, j));
     CX2(ik, 0) = tmp;
-    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+    for (int l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
       const Cx w1 = wal(l), w2 = wal(2 * l);
       Cx xl, xlc;
       xl.r = CH2(ik, 0).r + w1.r * CH2(ik, 1).r + w2.r * CH2(ik, 2).r;
       xl.i = CH2(ik, 0).i + w1.r * CH2(ik, 1).i + w2.r * CH2(ik, 2).i;
       xlc.r = -(w1.i * CH2(ik, ip - 1).i + w2.i * CH2(ik, ip - 2).i);
       xlc.i = w1.i * CH2(ik, ip - 1).r + w2.i * CH2(ik, ip - 2).r;
-      int64_t iwal = 2 * l;
-      int64_t j = 3, jc = ip - 3;
+      int iwal = 2 * l;
+      int j = 3, jc = ip - 3;
       for (; j < ipph - 1; j += 2, jc -= 2) {
         iwal += l;
         if (iwal > ip) iwal -= ip;
@@ -310,14 +315,14 @@ __device__ void passg(int64_t ido, int64_t ip, int64_t l1, Cx* cc, Cx* ch, const
   // shuffling and twiddling
   if (ido == 1) {
     PF_FOR(t, (ipph - 1) * idl1) {
-      const int64_t j = 1 + t / idl1, ik = t - (j - 1) * idl1, jc = ip - j;
+      const int j = 1 + t / idl1, ik = t - (j - 1) * idl1, jc = ip - j;
       const Cx t1 = CX2(ik, j), t2 = CX2(ik, jc);
       CX2(ik, j) = add(t1, t2);
       CX2(ik, jc) = sub(t1, t2);
     }
   } else {
     PF_FOR(t, (ipph - 1) * l1 * ido) {
-      const int64_t j = 1 + t / (l1 * ido), r = t - (j - 1) * l1 * ido, k = r / ido, i = r - k * ido, jc = ip - j;
+      const int j = 1 + t / (l1 * ido), r = t - (j - 1) * l1 * ido, k = r / ido, i = r - k * ido, jc = ip - j;
       if (i == 0) {
         const Cx t1 = CX(0, k, j), t2 = CX(0, k, jc);
         CX(0, k, j) = add(t1, t2);
@@ -336,10 +341,11 @@ __device__ void passg(int64_t ido, int64_t ip, int64_t l1, Cx* cc, Cx* ch, const
 #undef CH2
 }
 
-// c (P.len) in place, scratch ch (P.len): the transform, times fct (not when fct == 1)
+// c (P.len) in place, scratch ch (P.len): the transform, times fct (not when
+// fct == 1), pass by pass over global memory
 template <bool FWD>
-__device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, double fct) {
-  const int64_t len = P.len;
+__device__ void cfftp_passes(const PfPasses& P, const double* pool, Cx* c, Cx* ch, double fct) {
+  const int len = P.len;
   if (len == 1) {
     if (threadIdx.x == 0) c[0] = scale(c[0], fct);
     __syncthreads();
@@ -350,13 +356,13 @@ __device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, doub
     const PfFact F = P.f[k];
     const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
     switch (F.ip) {
-      case 4: pass4<FWD>(F.ido, F.l1, p1, p2, wa); break;
-      case 8: pass8<FWD>(F.ido, F.l1, p1, p2, wa); break;
-      case 2: pass2<FWD>(F.ido, F.l1, p1, p2, wa); break;
-      case 3: pass3<FWD>(F.ido, F.l1, p1, p2, wa); break;
-      case 5: passodd<FWD, 5>(F.ido, F.l1, p1, p2, wa); break;
-      case 7: passodd<FWD, 7>(F.ido, F.l1, p1, p2, wa); break;
-      case 11: passodd<FWD, 11>(F.ido, F.l1, p1, p2, wa); break;
+      case 4: passk<FWD, 4>(F.ido, F.l1, p1, p2, wa); break;
+      case 8: passk<FWD, 8>(F.ido, F.l1, p1, p2, wa); break;
+      case 2: passk<FWD, 2>(F.ido, F.l1, p1, p2, wa); break;
+      case 3: passk<FWD, 3>(F.ido, F.l1, p1, p2, wa); break;
+      case 5: passk<FWD, 5>(F.ido, F.l1, p1, p2, wa); break;
+      case 7: passk<FWD, 7>(F.ido, F.l1, p1, p2, wa); break;
+      case 11: passk<FWD, 11>(F.ido, F.l1, p1, p2, wa); break;
       default: {
         passg<FWD>(F.ido, F.ip, F.l1, p1, p2, wa, reinterpret_cast<const Cx*>(pool + F.tws));
         Cx* t = p1;
@@ -377,13 +383,158 @@ __device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, doub
   __syncthreads();
 }
 
+// ------------------------- LDS-fused executor -------------------------------
+constexpr int kPfLoadU = 8;   // tile loads a thread issues before it writes any to LDS
+// One tile pass: radix IP over the tile's Q columns, local sizes idol = ido / D,
+// l1l = l1 / L; column uu holds residue i = i0 + uu % Qi of the group's
+// global index (the butterfly's twiddle index is i + D * i_loc).
+template <bool FWD, int IP>
+__device__ __forceinline__ void tile_pass(const Cx* cur, Cx* nxt, int Q, int Qi, int qi, int qk, int i0, int D,
+                          int idol, int l1l, const Cx* wa, int ido) {
+  const int nb = (int)Q * idol * l1l;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const int uu = (int)(b % Q);
+    const int ii = uu % Qi, kk = uu / Qi;
+    if (ii >= qi || kk >= qk) continue;
+    const int r = b / Q, i_loc = r % idol, k_loc = r / idol;
+    Cx v[IP];
+#pragma unroll
+    for (int m = 0; m < IP; ++m) v[m] = cur[(i_loc + idol * (m + IP * k_loc)) * Q + uu];
+    bfly<FWD, IP>(v, i0 + ii + D * i_loc, wa, ido);
+#pragma unroll
+    for (int m = 0; m < IP; ++m) nxt[(i_loc + idol * (k_loc + l1l * m)) * Q + uu] = v[m];
+  }
+}
+
+// the passes of group G over the whole array: element pos = rd(pos) in,
+// wr(pos, v) out (every tile reads i + D (j + P k) and writes i + D (k + L j);
+// a group with L == 1 reads and writes the same positions per tile, so it may
+// run in place).  lds: 2 * kPfTileElems complex.
+template <bool FWD, class Rd, class Wr>
+__device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, const double* pool, Rd rd, Wr wr, Cx* lds) {
+  const int D = G.D, L = G.L, P = G.P;
+  const int Q = G.Q, Qi = G.Qi, Qk = G.Qk;
+  const int nti = (D + Qi - 1) / Qi, ntk = (L + Qk - 1) / Qk;
+  for (int tile = 0; tile < nti * ntk; ++tile) {
+    const int tk = tile / nti, ti = tile - tk * nti;
+    const int i0 = ti * Qi, k0 = tk * Qk;
+    const int qi = (int)(D - i0 < Qi ? D - i0 : Qi), qk = (int)(L - k0 < Qk ? L - k0 : Qk);
+    Cx* cur = lds;
+    Cx* nxt = lds + kPfTileElems;
+    // load in memory order (k, j, i), kPfLoadU independent loads in flight per thread
+    const int ne = (int)qk * P * qi;
+    for (int e0 = threadIdx.x; e0 < ne; e0 += kPfLoadU * blockDim.x) {
+      Cx v[kPfLoadU];
+      int li[kPfLoadU];
+#pragma unroll
+      for (int u = 0; u < kPfLoadU; ++u) {
+        const int e = e0 + u * (int)blockDim.x;
+        li[u] = -1;
+        if (e < ne) {
+          const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+          li[u] = j * Q + kk * Qi + ii;
+          v[u] = rd(i0 + ii + D * (j + P * (k0 + kk)));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kPfLoadU; ++u)
+        if (li[u] >= 0) cur[li[u]] = v[u];
+    }
+    __syncthreads();
+    for (int q = G.f0; q < G.f0 + G.nf; ++q) {
+      const PfFact F = Pl.f[q];
+      const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
+      const int idol = F.ido / D, l1l = F.l1 / L;
+      switch (F.ip) {
+        case 4: tile_pass<FWD, 4>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 8: tile_pass<FWD, 8>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 2: tile_pass<FWD, 2>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 3: tile_pass<FWD, 3>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 5: tile_pass<FWD, 5>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 7: tile_pass<FWD, 7>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        default: tile_pass<FWD, 11>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+      }
+      __syncthreads();
+      Cx* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+    // store in memory order (j, k, i)
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+      const int ii = (int)(e % qi);
+      const int r = e / qi, kk = r % qk, j = r / qk;
+      wr(i0 + ii + D * (k0 + kk + L * j), cur[j * Q + kk * Qi + ii]);
+    }
+    __syncthreads();
+  }
+}
+
+struct RdBuf {
+  const Cx* p;
+  __device__ Cx operator()(int i) const { return p[i]; }
+};
+struct RdD {
+  const double* p;
+  __device__ double operator()(int i) const { return p[i]; }
+};
+struct WrBuf {
+  Cx* p;
+  __device__ void operator()(int i, Cx v) const { p[i] = v; }
+};
+
+// pocketfft's cfftp transform of the sequence src(0 .. len-1), each result
+// handed to fin(pos, v) (unscaled); A, B: len complex of scratch each.  src
+// may read A (not B); fin must not write B.  Fused plans run group by group
+// (the last one reads B); others materialise src into A, run the passes and
+// hand A's entries to fin.
+template <bool FWD, class Src, class Fin, bool LEAN = false>
+__device__ void cfftp_x(const PfPasses& P, const double* pool, Src src, Cx* A, Cx* B, Fin fin, Cx* lds) {
+  const int len = P.len;
+  if (!LEAN && (!P.fused || lds == nullptr)) {
+    PF_FOR(i, len) A[i] = src(i);
+    __syncthreads();
+    cfftp_passes<FWD>(P, pool, A, B, 1.0);
+    PF_FOR(i, len) fin(i, A[i]);
+    __syncthreads();
+    return;
+  }
+  const int G = P.ng;
+  if (G == 1) {   // one group of one tile: every load precedes every store
+    cgroup<FWD>(P, P.g[0], pool, src, fin, lds);
+    return;
+  }
+  // outputs: group G-2 -> B, G-3 -> A, ...
+  auto outbuf = [&](int g) { return ((G - 2 - g) & 1) == 0 ? B : A; };
+  cgroup<FWD>(P, P.g[0], pool, src, WrBuf{outbuf(0)}, lds);
+  for (int g = 1; g < G - 1; ++g) cgroup<FWD>(P, P.g[g], pool, RdBuf{outbuf(g - 1)}, WrBuf{outbuf(g)}, lds);
+  cgroup<FWD>(P, P.g[G - 1], pool, RdBuf{B}, fin, lds);
+}
+
+// c (P.len) in place, scratch ch (P.len): the transform, times fct (not when
+// fct == 1); lds (2 * kPfTileElems complex) or nullptr for the unfused passes
+template <bool FWD>
+__device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, double fct, Cx* lds) {
+  if (P.len == 1 || !P.fused || lds == nullptr) {
+    cfftp_passes<FWD>(P, pool, c, ch, fct);
+    return;
+  }
+  cfftp_x<FWD>(P, pool, RdBuf{c}, c, ch,
+               [=](int i, Cx v) { c[i] = fct != 1.0 ? scale(v, fct) : v; }, lds);
+}
+
 // ========================= real passes (rfftp) ==============================
 #define CC(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
 #define WA(x, i) wa[(i) + (x) * (ido - 1)]
 
-__device__ void radf2(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+// nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
+// whole-array pass)
+__device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
+                      int bs = 0) {
 #define CH(a, b, c) ch[(a) + ido * ((b) + 2 * (c))]
-  PF_FOR(k, l1) {
+  PF_FOR(tb, nb * l1) {
+    const int b = tb / l1, k = tb - b * l1;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     CH(0, 0, k) = CC(0, k, 0) + CC(0, k, 1);
     CH(ido - 1, 1, k) = CC(0, k, 0) - CC(0, k, 1);
     if ((ido & 1) == 0) {
@@ -392,9 +543,12 @@ __device__ void radf2(int64_t ido, int64_t l1, const double* cc, double* ch, con
     }
   }
   if (ido <= 2) return;
-  const int64_t hi = (ido - 1) / 2;
-  PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+  const int hi = (ido - 1) / 2;
+  PF_FOR(tb, nb * l1 * hi) {
+    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double tr2 = wa[i - 2] * CC(i - 1, k, 1) + wa[i - 1] * CC(i, k, 1);
     const double ti2 = wa[i - 2] * CC(i, k, 1) - wa[i - 1] * CC(i - 1, k, 1);
     CH(i - 1, 0, k) = CC(i - 1, k, 0) + tr2;
@@ -405,19 +559,28 @@ __device__ void radf2(int64_t ido, int64_t l1, const double* cc, double* ch, con
 #undef CH
 }
 
-__device__ void radf3(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+// nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
+// whole-array pass)
+__device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
+                      int bs = 0) {
   const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 3 * (c))]
-  PF_FOR(k, l1) {
+  PF_FOR(tb, nb * l1) {
+    const int b = tb / l1, k = tb - b * l1;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double cr2 = CC(0, k, 1) + CC(0, k, 2);
     CH(0, 0, k) = CC(0, k, 0) + cr2;
     CH(0, 2, k) = taui * (CC(0, k, 2) - CC(0, k, 1));
     CH(ido - 1, 1, k) = CC(0, k, 0) + taur * cr2;
   }
   if (ido == 1) return;
-  const int64_t hi = (ido - 1) / 2;
-  PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+  const int hi = (ido - 1) / 2;
+  PF_FOR(tb, nb * l1 * hi) {
+    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
     const double di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
     const double dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
@@ -435,10 +598,16 @@ __device__ void radf3(int64_t ido, int64_t l1, const double* cc, double* ch, con
 #undef CH
 }
 
-__device__ void radf4(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+// nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
+// whole-array pass)
+__device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
+                      int bs = 0) {
   const double hsqt2 = 0.707106781186547524400844362104849;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 4 * (c))]
-  PF_FOR(k, l1) {
+  PF_FOR(tb, nb * l1) {
+    const int b = tb / l1, k = tb - b * l1;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double tr1 = CC(0, k, 3) + CC(0, k, 1);
     CH(0, 2, k) = CC(0, k, 3) - CC(0, k, 1);
     const double tr2 = CC(0, k, 0) + CC(0, k, 2);
@@ -455,9 +624,12 @@ __device__ void radf4(int64_t ido, int64_t l1, const double* cc, double* ch, con
     }
   }
   if (ido <= 2) return;
-  const int64_t hi = (ido - 1) / 2;
-  PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+  const int hi = (ido - 1) / 2;
+  PF_FOR(tb, nb * l1 * hi) {
+    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double cr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
     const double ci2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
     const double cr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
@@ -480,11 +652,17 @@ __device__ void radf4(int64_t ido, int64_t l1, const double* cc, double* ch, con
 #undef CH
 }
 
-__device__ void radf5(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
+// nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
+// whole-array pass)
+__device__ void radf5(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
+                      int bs = 0) {
   const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
   const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 5 * (c))]
-  PF_FOR(k, l1) {
+  PF_FOR(tb, nb * l1) {
+    const int b = tb / l1, k = tb - b * l1;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double cr2 = CC(0, k, 4) + CC(0, k, 1), ci5 = CC(0, k, 4) - CC(0, k, 1);
     const double cr3 = CC(0, k, 3) + CC(0, k, 2), ci4 = CC(0, k, 3) - CC(0, k, 2);
     CH(0, 0, k) = CC(0, k, 0) + cr2 + cr3;
@@ -494,9 +672,12 @@ __device__ void radf5(int64_t ido, int64_t l1, const double* cc, double* ch, con
     CH(0, 4, k) = ti12 * ci5 - ti11 * ci4;
   }
   if (ido == 1) return;
-  const int64_t hi = (ido - 1) / 2;
-  PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+  const int hi = (ido - 1) / 2;
+  PF_FOR(tb, nb * l1 * hi) {
+    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const double* cc = cc0 + b * bs;
+    double* ch = ch0 + b * bs;
     const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
     const double di2 = WA(0, i - 2) * CC(i, k, 1) - WA(0, i - 1) * CC(i - 1, k, 1);
     const double dr3 = WA(1, i - 2) * CC(i - 1, k, 2) + WA(1, i - 1) * CC(i, k, 2);
@@ -532,26 +713,26 @@ __device__ void radf5(int64_t ido, int64_t l1, const double* cc, double* ch, con
 #undef WA
 
 // generic forward pass (ip odd > 5, ido odd): the result lands in cc
-__device__ void radfg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* ch, const double* wa,
+__device__ void radfg(int ido, int ip, int l1, double* cc, double* ch, const double* wa,
                       const double* csarr) {
-  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+  const int cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
 #define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
 #define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
 #define C1(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
 #define C2(a, b) cc[(a) + idl1 * (b)]
 #define CH2(a, b) ch[(a) + idl1 * (b)]
   // phase 1: twiddles of the j / jc pairs (i >= 1) and the k column sums (i = 0)
-  const int64_t hp = (ido - 1) / 2;
+  const int hp = (ido - 1) / 2;
   PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
-    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+    const int j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
                   q = r - k * (hp + 1), jc = ip - j;
     if (q == 0) {
       const double t1 = C1(0, k, j), t2 = C1(0, k, jc);
       C1(0, k, j) = t2 + t1;
       C1(0, k, jc) = t2 - t1;
     } else {
-      const int64_t i = 2 * q - 1;
-      const int64_t idij = (j - 1) * (ido - 1) + (i - 1), idij2 = (jc - 1) * (ido - 1) + (i - 1);
+      const int i = 2 * q - 1;
+      const int idij = (j - 1) * (ido - 1) + (i - 1), idij2 = (jc - 1) * (ido - 1) + (i - 1);
       const double t1 = C1(i, k, j), t2 = C1(i + 1, k, j), t3 = C1(i, k, jc), t4 = C1(i + 1, k, jc);
       const double x1 = wa[idij] * t1 + wa[idij + 1] * t2, x2 = wa[idij] * t2 - wa[idij + 1] * t1,
                    x3 = wa[idij2] * t3 + wa[idij2 + 1] * t4, x4 = wa[idij2] * t4 - wa[idij2 + 1] * t3;
@@ -564,11 +745,11 @@ __device__ void radfg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
   __syncthreads();
   // phase 2: the ip-point real DFT across columns, per ik
   PF_FOR(ik, idl1) {
-    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+    for (int l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
       double a = C2(ik, 0) + csarr[2 * l] * C2(ik, 1) + csarr[4 * l] * C2(ik, 2);
       double b = csarr[2 * l + 1] * C2(ik, ip - 1) + csarr[4 * l + 1] * C2(ik, ip - 2);
-      int64_t iang = 2 * l;
-      int64_t j = 3, jc = ip - 3;
+      int iang = 2 * l;
+      int j = 3, jc = ip - 3;
       for (; j < ipph - 3; j += 4, jc -= 4) {
         iang += l;
         if (iang > ip) iang -= ip;
@@ -606,24 +787,24 @@ __device__ void radfg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
       CH2(ik, lc) = b;
     }
     double s = C2(ik, 0);
-    for (int64_t j = 1; j < ipph; ++j) s += C2(ik, j);
+    for (int j = 1; j < ipph; ++j) s += C2(ik, j);
     CH2(ik, 0) = s;
   }
   __syncthreads();
   // phase 3: into the halfcomplex layout
   PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
+    const int k = t / ido, i = t - k * ido;
     CC(i, 0, k) = CH(i, k, 0);
   }
   PF_FOR(t, (ipph - 1) * l1) {
-    const int64_t j = 1 + t / l1, k = t - (j - 1) * l1, jc = ip - j, j2 = 2 * j - 1;
+    const int j = 1 + t / l1, k = t - (j - 1) * l1, jc = ip - j, j2 = 2 * j - 1;
     CC(ido - 1, j2, k) = CH(0, k, j);
     CC(0, j2 + 1, k) = CH(0, k, jc);
   }
   if (ido > 1) {
     PF_FOR(t, (ipph - 1) * l1 * hp) {
-      const int64_t j = 1 + t / (l1 * hp), r = t - (j - 1) * l1 * hp, k = r / hp, q = r - k * hp;
-      const int64_t jc = ip - j, j2 = 2 * j - 1, i = 1 + 2 * q, ic = ido - i - 2;
+      const int j = 1 + t / (l1 * hp), r = t - (j - 1) * l1 * hp, k = r / hp, q = r - k * hp;
+      const int jc = ip - j, j2 = 2 * j - 1, i = 1 + 2 * q, ic = ido - i - 2;
       CC(i, j2 + 1, k) = CH(i, k, j) + CH(i, k, jc);
       CC(ic, j2, k) = CH(i, k, j) - CH(i, k, jc);
       CC(i + 1, j2 + 1, k) = CH(i + 1, k, j) + CH(i + 1, k, jc);
@@ -641,8 +822,8 @@ __device__ void radfg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
 #define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
 #define WA(x, i) wa[(i) + (x) * (ido - 1)]
 
-__device__ void radb2(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
-  constexpr int64_t IP = 2;
+__device__ void radb2(int ido, int l1, const double* __restrict__ cc, double* __restrict__ ch, const double* wa) {
+  constexpr int IP = 2;
   PF_FOR(k, l1) {
     CH(0, k, 0) = CC(0, 0, k) + CC(ido - 1, 1, k);
     CH(0, k, 1) = CC(0, 0, k) - CC(ido - 1, 1, k);
@@ -652,9 +833,9 @@ __device__ void radb2(int64_t ido, int64_t l1, const double* cc, double* ch, con
     }
   }
   if (ido <= 2) return;
-  const int64_t hi = (ido - 1) / 2;
+  const int hi = (ido - 1) / 2;
   PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
     CH(i - 1, k, 0) = CC(i - 1, 0, k) + CC(ic - 1, 1, k);
     const double tr2 = CC(i - 1, 0, k) - CC(ic - 1, 1, k);
     const double ti2 = CC(i, 0, k) + CC(ic, 1, k);
@@ -664,8 +845,8 @@ __device__ void radb2(int64_t ido, int64_t l1, const double* cc, double* ch, con
   }
 }
 
-__device__ void radb3(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
-  constexpr int64_t IP = 3;
+__device__ void radb3(int ido, int l1, const double* __restrict__ cc, double* __restrict__ ch, const double* wa) {
+  constexpr int IP = 3;
   const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
   PF_FOR(k, l1) {
     const double tr2 = 2 * CC(ido - 1, 1, k);
@@ -676,9 +857,9 @@ __device__ void radb3(int64_t ido, int64_t l1, const double* cc, double* ch, con
     CH(0, k, 1) = cr2 - ci3;
   }
   if (ido == 1) return;
-  const int64_t hi = (ido - 1) / 2;
+  const int hi = (ido - 1) / 2;
   PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double tr2 = CC(i - 1, 2, k) + CC(ic - 1, 1, k);
     const double ti2 = CC(i, 2, k) - CC(ic, 1, k);
     const double cr2 = CC(i - 1, 0, k) + taur * tr2;
@@ -696,8 +877,8 @@ __device__ void radb3(int64_t ido, int64_t l1, const double* cc, double* ch, con
   }
 }
 
-__device__ void radb4(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
-  constexpr int64_t IP = 4;
+__device__ void radb4(int ido, int l1, const double* __restrict__ cc, double* __restrict__ ch, const double* wa) {
+  constexpr int IP = 4;
   const double sqrt2 = 1.414213562373095048801688724209698;
   PF_FOR(k, l1) {
     const double tr2 = CC(0, 0, k) + CC(ido - 1, 3, k), tr1 = CC(0, 0, k) - CC(ido - 1, 3, k);
@@ -717,9 +898,9 @@ __device__ void radb4(int64_t ido, int64_t l1, const double* cc, double* ch, con
     }
   }
   if (ido <= 2) return;
-  const int64_t hi = (ido - 1) / 2;
+  const int hi = (ido - 1) / 2;
   PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double tr2 = CC(i - 1, 0, k) + CC(ic - 1, 3, k), tr1 = CC(i - 1, 0, k) - CC(ic - 1, 3, k);
     const double ti1 = CC(i, 0, k) + CC(ic, 3, k), ti2 = CC(i, 0, k) - CC(ic, 3, k);
     const double tr4 = CC(i, 2, k) + CC(ic, 1, k), ti3 = CC(i, 2, k) - CC(ic, 1, k);
@@ -739,8 +920,8 @@ __device__ void radb4(int64_t ido, int64_t l1, const double* cc, double* ch, con
   }
 }
 
-__device__ void radb5(int64_t ido, int64_t l1, const double* cc, double* ch, const double* wa) {
-  constexpr int64_t IP = 5;
+__device__ void radb5(int ido, int l1, const double* __restrict__ cc, double* __restrict__ ch, const double* wa) {
+  constexpr int IP = 5;
   const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
   const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
   PF_FOR(k, l1) {
@@ -758,9 +939,9 @@ __device__ void radb5(int64_t ido, int64_t l1, const double* cc, double* ch, con
     CH(0, k, 2) = cr3 - ci4;
   }
   if (ido == 1) return;
-  const int64_t hi = (ido - 1) / 2;
+  const int hi = (ido - 1) / 2;
   PF_FOR(t, l1 * hi) {
-    const int64_t k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double tr2 = CC(i - 1, 2, k) + CC(ic - 1, 1, k), tr5 = CC(i - 1, 2, k) - CC(ic - 1, 1, k);
     const double ti5 = CC(i, 2, k) + CC(ic, 1, k), ti2 = CC(i, 2, k) - CC(ic, 1, k);
     const double tr3 = CC(i - 1, 4, k) + CC(ic - 1, 3, k), tr4 = CC(i - 1, 4, k) - CC(ic - 1, 3, k);
@@ -792,28 +973,28 @@ __device__ void radb5(int64_t ido, int64_t l1, const double* cc, double* ch, con
 #undef WA
 
 // generic backward pass (ip odd > 5, ido odd): the result lands in ch
-__device__ void radbg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* ch, const double* wa,
+__device__ void radbg(int ido, int ip, int l1, double* cc, double* ch, const double* wa,
                       const double* csarr) {
-  const int64_t cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
+  const int cdim = ip, ipph = (ip + 1) / 2, idl1 = ido * l1;
 #define CC(a, b, c) cc[(a) + ido * ((b) + cdim * (c))]
 #define CH(a, b, c) ch[(a) + ido * ((b) + l1 * (c))]
 #define C1(a, b, c) cc[(a) + ido * ((b) + l1 * (c))]
 #define C2(a, b) cc[(a) + idl1 * (b)]
 #define CH2(a, b) ch[(a) + idl1 * (b)]
-  const int64_t hp = (ido - 1) / 2;
+  const int hp = (ido - 1) / 2;
   // phase 1: unpack the halfcomplex columns into CH
   PF_FOR(t, l1 * ido) {
-    const int64_t k = t / ido, i = t - k * ido;
+    const int k = t / ido, i = t - k * ido;
     CH(i, k, 0) = CC(i, 0, k);
   }
   PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
-    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+    const int j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
                   q = r - k * (hp + 1), jc = ip - j, j2 = 2 * j - 1;
     if (q == 0) {
       CH(0, k, j) = 2 * CC(ido - 1, j2, k);
       CH(0, k, jc) = 2 * CC(0, j2 + 1, k);
     } else {
-      const int64_t i = 2 * q - 1, ic = ido - i - 2;
+      const int i = 2 * q - 1, ic = ido - i - 2;
       CH(i, k, j) = CC(i, j2 + 1, k) + CC(ic, j2, k);
       CH(i, k, jc) = CC(i, j2 + 1, k) - CC(ic, j2, k);
       CH(i + 1, k, j) = CC(i + 1, j2 + 1, k) - CC(ic + 1, j2, k);
@@ -823,11 +1004,11 @@ __device__ void radbg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
   __syncthreads();
   // phase 2: the column DFT (into C2, columns >= 1), then CH2 column 0's sum
   PF_FOR(ik, idl1) {
-    for (int64_t l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
+    for (int l = 1, lc = ip - 1; l < ipph; ++l, --lc) {
       double a = CH2(ik, 0) + csarr[2 * l] * CH2(ik, 1) + csarr[4 * l] * CH2(ik, 2);
       double b = csarr[2 * l + 1] * CH2(ik, ip - 1) + csarr[4 * l + 1] * CH2(ik, ip - 2);
-      int64_t iang = 2 * l;
-      int64_t j = 3, jc = ip - 3;
+      int iang = 2 * l;
+      int j = 3, jc = ip - 3;
       for (; j < ipph - 3; j += 4, jc -= 4) {
         iang += l;
         if (iang > ip) iang -= ip;
@@ -865,22 +1046,22 @@ __device__ void radbg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
       C2(ik, lc) = b;
     }
     double s = CH2(ik, 0);
-    for (int64_t j = 1; j < ipph; ++j) s += CH2(ik, j);
+    for (int j = 1; j < ipph; ++j) s += CH2(ik, j);
     CH2(ik, 0) = s;
   }
   __syncthreads();
   // phase 3: recombine the pairs into CH, then the twiddles (same thread, same elements)
   PF_FOR(t, (ipph - 1) * l1 * (hp + 1)) {
-    const int64_t j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
+    const int j = 1 + t / (l1 * (hp + 1)), r = t - (j - 1) * l1 * (hp + 1), k = r / (hp + 1),
                   q = r - k * (hp + 1), jc = ip - j;
     if (q == 0) {
       CH(0, k, jc) = C1(0, k, j) + C1(0, k, jc);
       CH(0, k, j) = C1(0, k, j) - C1(0, k, jc);
     } else {
-      const int64_t i = 2 * q - 1;
+      const int i = 2 * q - 1;
       const double a = C1(i, k, j) - C1(i + 1, k, jc), b = C1(i, k, j) + C1(i + 1, k, jc);
       const double c = C1(i + 1, k, j) + C1(i, k, jc), d = C1(i + 1, k, j) - C1(i, k, jc);
-      const int64_t is = (j - 1) * (ido - 1) + (i - 1), isc = (jc - 1) * (ido - 1) + (i - 1);
+      const int is = (j - 1) * (ido - 1) + (i - 1), isc = (jc - 1) * (ido - 1) + (i - 1);
       CH(i, k, j) = wa[is] * a - wa[is + 1] * c;
       CH(i + 1, k, j) = wa[is] * c + wa[is + 1] * a;
       CH(i, k, jc) = wa[isc] * b - wa[isc + 1] * d;
@@ -896,7 +1077,7 @@ __device__ void radbg(int64_t ido, int64_t ip, int64_t l1, double* cc, double* c
 
 // c (P.len) in place, scratch ch (P.len); r2hc: forward (halfcomplex out), else backward
 __device__ void rfftp(const PfPasses& P, const double* pool, double* c, double* ch, double fct, bool r2hc) {
-  const int64_t n = P.len;
+  const int n = P.len;
   if (n == 1) {
     if (threadIdx.x == 0) c[0] *= fct;
     __syncthreads();
@@ -942,33 +1123,133 @@ __device__ void rfftp(const PfPasses& P, const double* pool, double* c, double* 
   __syncthreads();
 }
 
+// one unfused forward real pass over the whole array: in -> out (radfg's
+// result lands in its input, then copied)
+__device__ inline void radf_whole(const PfPasses& P, const PfFact& F, const double* pool, double* in, double* out) {
+  const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
+  switch (F.ip) {
+    case 4: radf4(F.ido, F.l1, in, out, wa); break;
+    case 2: radf2(F.ido, F.l1, in, out, wa); break;
+    case 3: radf3(F.ido, F.l1, in, out, wa); break;
+    case 5: radf5(F.ido, F.l1, in, out, wa); break;
+    default:
+      radfg(F.ido, F.ip, F.l1, in, out, wa, pool + (F.tws >= 0 ? F.tws : 0));
+      __syncthreads();
+      PF_FOR(i, P.len) out[i] = in[i];
+  }
+  __syncthreads();
+}
+
+// pocketfft's rfftp forward (r2hc, fct 1) of the sequence src(0 .. n-1) into
+// f (halfcomplex); tmp: n doubles of scratch; src must read neither f nor
+// tmp.  Groups in executed order (pocketfft.h), the last one writing f;
+// lds: 2 * kPfTileDoubles doubles.
+template <class Src, bool LEAN = false>
+__device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, double* f, double* tmp,
+                                double* lds) {
+  const int G = P.ng;
+  auto outbuf = [&](int g) { return ((G - 1 - g) & 1) == 0 ? f : tmp; };
+  for (int g = 0; g < G; ++g) {
+    const PfGroup& Gr = P.g[g];
+    double* out = outbuf(g);
+    double* in = g == 0 ? nullptr : outbuf(g - 1);
+    if (Gr.Q == 0) {
+      if (g == 0) {   // materialise the source in the other buffer
+        in = out == f ? tmp : f;
+        PF_FOR(i, P.len) in[i] = src(i);
+        __syncthreads();
+      }
+      if constexpr (LEAN) {   // hard-coded radices only (pf_hilbert_lean)
+        const PfFact& F = P.f[Gr.f0];
+        const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
+        switch (F.ip) {
+          case 4: radf4(F.ido, F.l1, in, out, wa); break;
+          case 2: radf2(F.ido, F.l1, in, out, wa); break;
+          case 3: radf3(F.ido, F.l1, in, out, wa); break;
+          default: radf5(F.ido, F.l1, in, out, wa); break;
+        }
+        __syncthreads();
+      } else {
+        radf_whole(P, P.f[Gr.f0], pool, in, out);
+      }
+      continue;
+    }
+    const int D = Gr.D, Pp = Gr.P, Lr = Gr.L, DP = D * Pp;
+    const int Qk = Gr.Qk;
+    for (int k0 = 0; k0 < Lr; k0 += Qk) {
+      const int qk = Lr - k0 < Qk ? Lr - k0 : Qk;
+      double* cur = lds;
+      double* nxt = lds + kPfTileDoubles;
+      // load in memory order (w, k, a): global a + D (k + Lr w) -> local k DP + a + D w
+      const int ne = qk * DP;
+      for (int e0 = threadIdx.x; e0 < ne; e0 += kPfLoadU * blockDim.x) {
+        double v[kPfLoadU];
+        int li[kPfLoadU];
+#pragma unroll
+        for (int u = 0; u < kPfLoadU; ++u) {
+          const int e = e0 + u * (int)blockDim.x;
+          li[u] = -1;
+          if (e < ne) {
+            const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+            const int pos = a + D * (k0 + kk) + D * Lr * w;
+            li[u] = kk * DP + a + D * w;
+            v[u] = g == 0 ? src(pos) : in[pos];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kPfLoadU; ++u)
+          if (li[u] >= 0) cur[li[u]] = v[u];
+      }
+      __syncthreads();
+      for (int q = Gr.f0; q > Gr.f0 - Gr.nf; --q) {
+        const PfFact F = P.f[q];
+        const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
+        const int l1l = F.l1 / Lr;
+        switch (F.ip) {
+          case 4: radf4(F.ido, l1l, cur, nxt, wa, qk, DP); break;
+          case 2: radf2(F.ido, l1l, cur, nxt, wa, qk, DP); break;
+          case 3: radf3(F.ido, l1l, cur, nxt, wa, qk, DP); break;
+          default: radf5(F.ido, l1l, cur, nxt, wa, qk, DP); break;
+        }
+        __syncthreads();
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+      }
+      // blocks k0 .. k0 + qk - 1 are contiguous in the output
+      for (int e = threadIdx.x; e < ne; e += blockDim.x) out[k0 * DP + e] = cur[e];
+      __syncthreads();
+    }
+  }
+}
+
 // ============================ Bluestein =====================================
 template <bool FWD>
-__device__ void blue_fft(const PfBlue& B, const double* pool, Cx* c, Cx* akf, Cx* ch, double fct) {
-  const int64_t n = B.n, n2 = B.n2;
+__device__ void blue_fft(const PfBlue& B, const double* pool, Cx* c, Cx* akf, Cx* ch, double fct, Cx* lds) {
+  const int n = B.n, n2 = B.n2;
   const Cx* bk = reinterpret_cast<const Cx*>(pool + B.bk);
   const Cx* bkf = reinterpret_cast<const Cx*>(pool + B.bkf);
   const Cx zero = scale(smul<FWD>(c[0], bk[0]), 0.);
   PF_FOR(m, n2) akf[m] = m < n ? smul<FWD>(c[m], bk[m]) : zero;
   __syncthreads();
-  cfftp<true>(B.plan, pool, akf, ch, 1.);
+  cfftp<true>(B.plan, pool, akf, ch, 1., lds);
   // the convolution
   PF_FOR(m, n2) akf[m] = smul<!FWD>(akf[m], bkf[2 * m <= n2 ? m : n2 - m]);
   __syncthreads();
-  cfftp<false>(B.plan, pool, akf, ch, 1.);
+  cfftp<false>(B.plan, pool, akf, ch, 1., lds);
   PF_FOR(m, n) c[m] = scale(smul<FWD>(akf[m], bk[m]), fct);
   __syncthreads();
 }
 
 // exec_r: real data through the complex Bluestein transform; tmp: n complex
 __device__ void blue_r(const PfBlue& B, const double* pool, double* c, Cx* tmp, Cx* akf, Cx* ch, double fct,
-                       bool r2hc) {
-  const int64_t n = B.n;
+                       bool r2hc, Cx* lds) {
+  const int n = B.n;
   if (r2hc) {
     const double zero = 0. * c[0];
     PF_FOR(m, n) tmp[m] = {c[m], zero};
     __syncthreads();
-    blue_fft<true>(B, pool, tmp, akf, ch, fct);
+    blue_fft<true>(B, pool, tmp, akf, ch, fct, lds);
     PF_FOR(m, n) c[m] = m == 0 ? tmp[0].r : ((m & 1) ? tmp[(m + 1) / 2].r : tmp[m / 2].i);
     __syncthreads();
   } else {
@@ -982,11 +1263,11 @@ __device__ void blue_r(const PfBlue& B, const double* pool, double* c, Cx* tmp, 
     }
     __syncthreads();
     PF_FOR(m, (n - 1) / 2) {
-      const int64_t q = m + 1;   // 2q < n
+      const int q = m + 1;   // 2q < n
       tmp[n - q] = {tmp[q].r, -tmp[q].i};
     }
     __syncthreads();
-    blue_fft<false>(B, pool, tmp, akf, ch, fct);
+    blue_fft<false>(B, pool, tmp, akf, ch, fct, lds);
     PF_FOR(m, n) c[m] = tmp[m].r;
     __syncthreads();
   }
@@ -994,15 +1275,18 @@ __device__ void blue_r(const PfBlue& B, const double* pool, double* c, Cx* tmp, 
 
 // ============================ entry points ==================================
 // per-transform scratch (pocketfft.h pf_scratch_doubles): a (2n), x (2n), and
-// for Bluestein akf, ch2 (2 n2 each)
+// for Bluestein akf, ch2 (2 n2 each); lds: the fused executor's tile buffers
+// (2 * kPfTileElems complex of the calling kernel's LDS) or nullptr
 struct PfScratch {
   double* a;
   Cx* x;
   Cx* akf;
   Cx* ch2;
+  Cx* lds;
 };
-__device__ inline PfScratch pf_scratch(const PfLen& L, double* slot) {
+__device__ inline PfScratch pf_scratch(const PfLen& L, double* slot, Cx* lds) {
   PfScratch s;
+  s.lds = lds;
   s.a = slot;
   s.x = reinterpret_cast<Cx*>(slot + 2 * L.n);
   s.akf = reinterpret_cast<Cx*>(slot + 4 * L.n);
@@ -1012,54 +1296,89 @@ __device__ inline PfScratch pf_scratch(const PfLen& L, double* slot) {
 
 // scipy.fft.rfft's pocketfft_r forward on c (n reals, in place -> halfcomplex)
 __device__ inline void pf_r2hc(const PfLen& L, const double* pool, double* c, const PfScratch& s, double fct) {
-  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, true);
+  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, true, s.lds);
   else rfftp(L.r, pool, c, s.a, fct, true);
 }
 // pocketfft_r backward on c (halfcomplex in place -> n reals)
 __device__ inline void pf_hc2r(const PfLen& L, const double* pool, double* c, const PfScratch& s, double fct) {
-  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, false);
+  if (L.rblue) blue_r(L.bl, pool, c, s.x, s.akf, s.ch2, fct, false, s.lds);
   else rfftp(L.r, pool, c, s.a, fct, false);
 }
 // pocketfft_c backward on c (n complex, in place); c must not be s.x when Bluestein
 __device__ inline void pf_c2c_bwd(const PfLen& L, const double* pool, Cx* c, const PfScratch& s, double fct) {
-  if (L.cblue) blue_fft<false>(L.bl, pool, c, s.akf, s.ch2, fct);
-  else cfftp<false>(L.c, pool, c, reinterpret_cast<Cx*>(s.a), fct);
+  if (L.cblue) blue_fft<false>(L.bl, pool, c, s.akf, s.ch2, fct, s.lds);
+  else cfftp<false>(L.c, pool, c, reinterpret_cast<Cx*>(s.a), fct, s.lds);
 }
 
 // |scipy.signal.hilbert(f)| of one real row (modem.py:309, 315): f (n) is
 // overwritten by its halfcomplex spectrum, env (n) receives the envelope
 // (env may be f).  fct = double(1 / long double n).
 __device__ inline void pf_hilbert_env(const PfLen& L, const double* pool, double* f, double* env, double* slot,
-                                      double fct) {
-  const int64_t n = L.n;
-  const PfScratch s = pf_scratch(L, slot);
+                                      double fct, Cx* lds) {
+  const int n = (int)L.n;
+  const PfScratch s = pf_scratch(L, slot, lds);
   pf_r2hc(L, pool, f, s, 1.0);
   // the spectrum as pypocketfft's c2c_sym leaves it (bins 0..n/2 from r2c,
   // conjugated into n - i -- bins 0 and n/2 onto themselves, imaginary -0.0),
-  // times scipy's h with numpy's FMA complex multiply -> x
-  Cx* X = s.x;
-  PF_FOR(i, n) {
+  // times scipy's h with numpy's FMA complex multiply
+  auto spec = [=](int i) -> Cx {
     double xr, xi;
     if (i == 0) { xr = f[0]; xi = -0.0; }
     else if (2 * i == n) { xr = f[n - 1]; xi = -0.0; }
     else if (2 * i < n) { xr = f[2 * i - 1]; xi = f[2 * i]; }
     else { xr = f[2 * (n - i) - 1]; xi = -f[2 * (n - i)]; }
     const double hr = (i == 0 || 2 * i == n) ? 1.0 : (2 * i < n ? 2.0 : 0.0), hi = 0.0;
-    X[i] = {__builtin_fma(xr, hr, -(xi * hi)), __builtin_fma(xr, hi, xi * hr)};
-  }
-  __syncthreads();
+    return {__builtin_fma(xr, hr, -(xi * hi)), __builtin_fma(xr, hi, xi * hr)};
+  };
   // ifft: pocketfft_c backward, times 1/n; then numpy's complex abs
-  if (L.cblue) {
-    blue_fft<false>(L.bl, pool, X, s.akf, s.ch2, fct);
-  } else {
-    cfftp<false>(L.c, pool, X, reinterpret_cast<Cx*>(s.a), fct);
-  }
-  PF_FOR(i, n) {
-    const double ar = fabs(X[i].r), ai = fabs(X[i].i);
+  auto absw = [=](int i, Cx v) {
+    const double ar = fabs(v.r), ai = fabs(v.i);
     const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
     env[i] = h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0));
+  };
+  Cx* X = s.x;
+  if (L.cblue) {   // Bluestein scales inside its last chirp multiply
+    PF_FOR(i, n) X[i] = spec(i);
+    __syncthreads();
+    blue_fft<false>(L.bl, pool, X, s.akf, s.ch2, fct, lds);
+    PF_FOR(i, n) absw(i, X[i]);
+    __syncthreads();
+    return;
   }
-  __syncthreads();
+  // spec reads f, which neither X nor the scratch aliases; the envelope goes
+  // straight from the last group's tiles to env (cfftp's copy_and_norm scale
+  // first)
+  cfftp_x<false>(L.c, pool, spec, X, reinterpret_cast<Cx*>(s.a),
+                 [=](int i, Cx v) { absw(i, fct != 1.0 ? scale(v, fct) : v); }, lds);
+}
+
+// the same envelope with the row read through src(i) and the envelope handed
+// to fin(i, env) -- every transform LDS-fused, no copies in or out.  Needs
+// pf_hilbert_fusable(L); slot as pf_hilbert_env's (f = slot, then the
+// scratch); src is read before fin is first called.
+template <class Src, class Fin, bool LEAN = false>
+__device__ void pf_hilbert_env_x(const PfLen& L, const double* pool, Src src, Fin fin, double* slot, double fct,
+                                 Cx* lds) {
+  const int n = (int)L.n;
+  double* f = slot;
+  const PfScratch s = pf_scratch(L, slot + n, lds);
+  rfftp_fwd_fused<Src, LEAN>(L.r, pool, src, f, s.a, reinterpret_cast<double*>(lds));
+  auto spec = [=](int i) -> Cx {
+    double xr, xi;
+    if (i == 0) { xr = f[0]; xi = -0.0; }
+    else if (2 * i == n) { xr = f[n - 1]; xi = -0.0; }
+    else if (2 * i < n) { xr = f[2 * i - 1]; xi = f[2 * i]; }
+    else { xr = f[2 * (n - i) - 1]; xi = -f[2 * (n - i)]; }
+    const double hr = (i == 0 || 2 * i == n) ? 1.0 : (2 * i < n ? 2.0 : 0.0), hi = 0.0;
+    return {__builtin_fma(xr, hr, -(xi * hi)), __builtin_fma(xr, hi, xi * hr)};
+  };
+  auto envf = [=](int i, Cx v) {
+    if (fct != 1.0) v = scale(v, fct);
+    const double ar = fabs(v.r), ai = fabs(v.i);
+    const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
+    fin(i, h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0)));
+  };
+  cfftp_x<false, decltype(spec), decltype(envf), LEAN>(L.c, pool, spec, s.x, reinterpret_cast<Cx*>(s.a), envf, lds);
 }
 
 #undef PF_FOR

@@ -14,7 +14,9 @@ constexpr int kPfThreads = 512;
 
 // fftblue's constructor: tbkf = bk / n2 zero-padded and mirrored, its
 // forward cfftp transform, first n2 / 2 + 1 entries -> bkf (one workgroup)
-__global__ __launch_bounds__(kPfThreads) void k_pf_bkf(const PfLen* __restrict__ L, double* pool, double* tmp) {
+__global__ __launch_bounds__(kPfThreads) void k_pf_bkf(const PfLen* __restrict__ L, double* pool, double* tmp,
+                                                       int fuse) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
   const PfBlue& B = L->bl;
   const int64_t n = B.n, n2 = B.n2;
   pf::Cx* tb = reinterpret_cast<pf::Cx*>(tmp);
@@ -28,14 +30,14 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_bkf(const PfLen* __restrict__
     tb[m] = v;
   }
   __syncthreads();
-  pf::cfftp<true>(B.plan, pool, tb, ch, 1.);
+  pf::cfftp<true>(B.plan, pool, tb, ch, 1., fuse ? lds : nullptr);
   pf::Cx* bkf = reinterpret_cast<pf::Cx*>(pool + B.bkf);
   for (int64_t i = threadIdx.x; i < n2 / 2 + 1; i += blockDim.x) bkf[i] = tb[i];
 }
 
 hipError_t pf_finish(const PfLen& L, const PfLen* dL, double* dpool, double* tmp, hipStream_t st) {
   if (!L.rblue && !L.cblue) return hipSuccess;
-  hipLaunchKernelGGL(k_pf_bkf, dim3(1), dim3(kPfThreads), 0, st, dL, dpool, tmp);
+  hipLaunchKernelGGL(k_pf_bkf, dim3(1), dim3(kPfThreads), 0, st, dL, dpool, tmp, (int)pf_fuse_on());
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return e;
@@ -52,7 +54,9 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_resample(const PfLen* __restr
                                                             const double* __restrict__ x, int64_t nx,
                                                             double* __restrict__ y, int64_t num, int64_t batch,
                                                             double* slots, int64_t slot_doubles, double fct,
-                                                            double scale) {
+                                                            double scale, int fuse) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  pf::Cx* tl = fuse ? lds : nullptr;
   double* c = slots + (size_t)blockIdx.x * slot_doubles;
   double* scr = c + std::max(nx, num);
   const int64_t N = std::min(num, nx), nyq = N / 2 + 1;
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_resample(const PfLen* __restr
     const double* xr = x + (size_t)b * nx;
     for (int64_t i = threadIdx.x; i < nx; i += blockDim.x) c[i] = xr[i];
     __syncthreads();
-    pf::pf_r2hc(*Lx, poolx, c, pf::pf_scratch(*Lx, scr), 1.0);
+    pf::pf_r2hc(*Lx, poolx, c, pf::pf_scratch(*Lx, scr, tl), 1.0);
     // halfcomplex of x (c) -> halfcomplex of Y (into the scratch, then back to c)
     double* yh = scr;
     for (int64_t i = threadIdx.x; i < num; i += blockDim.x) {
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_resample(const PfLen* __restr
     __syncthreads();
     for (int64_t i = threadIdx.x; i < num; i += blockDim.x) c[i] = yh[i];
     __syncthreads();
-    pf::pf_hc2r(*Ly, pooly, c, pf::pf_scratch(*Ly, scr), fct);
+    pf::pf_hc2r(*Ly, pooly, c, pf::pf_scratch(*Ly, scr, tl), fct);
     double* yr = y + (size_t)b * num;
     for (int64_t i = threadIdx.x; i < num; i += blockDim.x) yr[i] = c[i] * scale;
     __syncthreads();
@@ -100,28 +104,50 @@ hipError_t launch_pf_resample(const PfLen* dLx, const double* poolx, const PfLen
   if (batch < 1) return hipSuccess;
   const unsigned g = (unsigned)std::min<int64_t>(batch, n_slots);
   hipLaunchKernelGGL(k_pf_resample, dim3(g), dim3(kPfThreads), 0, st, dLx, poolx, dLy, pooly, x, nx, y, num, batch,
-                     slots, slot_doubles, fct, scale);
+                     slots, slot_doubles, fct, scale, (int)pf_fuse_on());
   return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kPfThreads) void k_pf_hilbert_env(const PfLen* __restrict__ L, const double* pool,
                                                                double* x, int64_t n, int64_t batch, double* slots,
-                                                               int64_t slot_doubles, double fct, int stage) {
+                                                               int64_t slot_doubles, double fct, int stage,
+                                                               int fuse) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  pf::Cx* tl = fuse ? lds : nullptr;
   double* slot = slots + (size_t)blockIdx.x * slot_doubles;
   for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
     double* f = x + (size_t)b * n;
     if (stage == 1) {   // diagnostic: the forward real transform alone (halfcomplex)
-      pf::pf_r2hc(*L, pool, f, pf::pf_scratch(*L, slot), 1.0);
+      pf::pf_r2hc(*L, pool, f, pf::pf_scratch(*L, slot, tl), 1.0);
     } else if (stage == 2) {   // diagnostic: the backward real transform alone
-      pf::pf_hc2r(*L, pool, f, pf::pf_scratch(*L, slot), 1.0);
+      pf::pf_hc2r(*L, pool, f, pf::pf_scratch(*L, slot, tl), 1.0);
+    } else if (tl && pf_hilbert_fusable(*L)) {
+      pf::pf_hilbert_env_x(
+          *L, pool, [=](int64_t i) { return f[i]; }, [=](int64_t i, double e) { f[i] = e; }, slot, fct, tl);
     } else {
-      pf::pf_hilbert_env(*L, pool, f, f, slot, fct);
+      pf::pf_hilbert_env(*L, pool, f, f, slot, fct, tl);
     }
   }
 }
 
+// the lean instantiation (pf_hilbert_lean plans; the FSK exact path's E2 runs
+// the same code, fsk_exact_kernels.hip k_exact_env_lean)
+__global__ __launch_bounds__(kPfThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_hilbert_env_lean(
+    const PfLen* __restrict__ L, const double* pool, double* x, int64_t n, int64_t batch, double* slots,
+    int64_t slot_doubles, double fct) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  double* slot = slots + (size_t)blockIdx.x * slot_doubles;
+  for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
+    double* f = x + (size_t)b * n;
+    auto src = [=](int i) { return f[i]; };
+    auto fin = [=](int i, double e) { f[i] = e; };
+    pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*L, pool, src, fin, slot, fct, lds);
+  }
+}
+
 hipError_t launch_pf_hilbert_env(const PfLen* dL, const double* pool, double* x, int64_t n, int64_t batch,
-                                 double* slots, int64_t slot_doubles, int n_slots, double fct, hipStream_t st) {
+                                 double* slots, int64_t slot_doubles, int n_slots, double fct, bool lean,
+                                 hipStream_t st) {
   if (batch < 1) return hipSuccess;
   const unsigned g = (unsigned)std::min<int64_t>(batch, n_slots);
   // AMR_PF_THREADS (diagnostic): a smaller workgroup (the routines take any size)
@@ -131,8 +157,13 @@ hipError_t launch_pf_hilbert_env(const PfLen* dL, const double* pool, double* x,
     return (unsigned)(v >= 64 && v <= kPfThreads ? v : kPfThreads);
   }();
   static const int stage = [] { const char* e = getenv("AMR_PF_STAGE"); return e ? atoi(e) : 0; }();
+  if (lean && stage == 0 && nt == kPfThreads && pf_fuse_on()) {
+    hipLaunchKernelGGL(k_pf_hilbert_env_lean, dim3(g), dim3(kPfThreads), 0, st, dL, pool, x, n, batch, slots,
+                       slot_doubles, fct);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_pf_hilbert_env, dim3(g), dim3(nt), 0, st, dL, pool, x, n, batch, slots, slot_doubles, fct,
-                     stage);
+                     stage, (int)pf_fuse_on());
   return hipGetLastError();
 }
 

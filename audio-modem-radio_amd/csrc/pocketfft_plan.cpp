@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "pocketfft.h"
@@ -174,6 +176,37 @@ void align2(std::vector<double>& pool) {
   if (pool.size() & 1) pool.push_back(0.0);
 }
 
+// greedy grouping of a cfftp plan's passes for the LDS-fused executor: runs
+// of consecutive passes whose radix product stays <= kPfMaxGroupP; a plan
+// with a generic pass (ip > 11) runs unfused
+void build_groups(PfPasses& P) {
+  P.fused = 0;
+  P.ng = 0;
+  if (P.nf == 0) return;
+  for (int k = 0; k < P.nf; ++k)
+    if (P.f[k].ip > 11) return;
+  int k = 0;
+  while (k < P.nf) {
+    PfGroup& G = P.g[P.ng++];
+    G.f0 = k;
+    G.P = P.f[k].ip;
+    G.L = P.f[k].l1;
+    ++k;
+    while (k < P.nf && G.P * P.f[k].ip <= kPfMaxGroupP) G.P *= P.f[k++].ip;
+    G.nf = k - G.f0;
+    G.D = P.f[k - 1].ido;
+    G.Q = (int)(kPfTileElems / G.P);
+    if (G.D >= G.Q) {
+      G.Qi = G.Q;
+      G.Qk = 1;
+    } else {
+      G.Qi = (int)G.D;
+      G.Qk = (int)(G.Q / G.D);
+    }
+  }
+  P.fused = 1;
+}
+
 // pocketfft's cfftp(len): factors and twiddles
 bool build_cfftp(int64_t len, PfPasses& P, std::vector<double>& pool) {
   P = PfPasses{};
@@ -210,7 +243,40 @@ bool build_cfftp(int64_t len, PfPasses& P, std::vector<double>& pool) {
     }
     l1 *= ip;
   }
+  build_groups(P);
   return true;
+}
+
+// grouping of an rfftp plan's passes in forward (r2hc) order for the fused
+// real executor (pocketfft.h)
+void build_rgroups(PfPasses& P) {
+  P.fused = 0;
+  P.ng = 0;
+  if (P.nf == 0) return;
+  int k = P.nf - 1;
+  while (k >= 0) {
+    PfGroup& G = P.g[P.ng++];
+    G.f0 = k;
+    const int64_t D = P.f[k].ido;
+    const int64_t qmin = std::max<int64_t>(1, (kPfMinRun + D - 1) / D);
+    G.D = D;
+    G.P = P.f[k].ip;
+    const bool hard = G.P <= 5;
+    --k;
+    if (hard)
+      while (k >= 0 && P.f[k].ip <= 5 && D * G.P * P.f[k].ip * qmin <= kPfTileDoubles) G.P *= P.f[k--].ip;
+    G.nf = G.f0 - k;
+    G.L = P.f[k + 1].l1;
+    G.Qi = 0;
+    if (hard && D * G.P * qmin <= kPfTileDoubles) {
+      G.Q = 1;
+      G.Qk = (int)std::min<int64_t>(G.L, kPfTileDoubles / (D * G.P));
+    } else {
+      G.Q = 0;
+      G.Qk = 0;
+    }
+  }
+  P.fused = 1;
 }
 
 // pocketfft's rfftp(len): factors, twiddles and the generic passes' tables
@@ -258,6 +324,7 @@ bool build_rfftp(int64_t len, PfPasses& P, std::vector<double>& pool) {
     }
     l1 *= ip;
   }
+  build_rgroups(P);
   return true;
 }
 
@@ -287,8 +354,18 @@ bool build_blue(int64_t n, PfBlue& B, std::vector<double>& pool) {
 
 }  // namespace
 
+bool pf_fuse_on() {
+  static const bool on = [] {
+    const char* e = getenv("AMR_PF_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 bool pf_len_build(int64_t n, PfLen& L, std::vector<double>& pool) {
-  if (n < 1) return false;
+  // the device transforms index in 32 bits (a row and its Bluestein scratch
+  // stay below 2^31 doubles)
+  if (n < 1 || n > kPfMaxLen) return false;
   L = PfLen{};
   L.n = n;
   L.rblue = use_bluestein(n, true);
