@@ -90,8 +90,8 @@ hipError_t launch_fft_filter(const double2* in, double2* t1, double2* t2, double
                              int64_t batch, int mid, const double2* tab, const FftEpi& epi, hipStream_t st);
 // launch_fft_filter(kHilbert, kEnvelope) in the live-column layout
 // (amr_internal.h LiveCols; fft_kernels.hip k_*_live): zb = [B][L | D], cb = [B][nl * n2]
-hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, int64_t batch, const LiveCols& lc,
-                                   const FftEpi& epi, hipStream_t st);
+hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, double2* db, const FftDesc& d, int64_t batch,
+                                   const LiveCols& lc, const FftEpi& epi, hipStream_t st);
 hipError_t launch_bs_pre(const double2* x, double2* a, const double2* w, int64_t n, int64_t M, int64_t batch,
                          bool inverse, hipStream_t st);
 hipError_t launch_bs_post(const double2* y, double2* out, const double2* w, int64_t n, int64_t M, int64_t batch,

@@ -500,7 +500,9 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
 // columns, rows j2) and cb = C [nl * n2] (the live columns' transform).
 //   column pass  live tiles  L -> C   (z's live columns stay intact: the
 //                                      final pass reads them for |a|)
-//                dead tiles  D -> D   (in place)
+//                dead tiles  D -> D   (in place), or D -> db [nd * n2] when
+//                                      the plan keeps all of z for the FSK
+//                                      exact path (fsk_api.cpp keep_z)
 //   middle pass  rows k2 of T from C (live c) and D (dead c); writes only
 //                the live outputs k2' (no later pass reads the others), into
 //                C row k2 at the live index of k2' -- the positions it read
@@ -510,8 +512,8 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_rows(const double2* __restr
 // pass at sps 10, and the plan holds 1.4 x n complex per
 // stream instead of 3 x.
 template <int PC, int QC>
-__global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
-                                                              LiveCols lc) {
+__global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, double2* cb, double2* db, FftDesc d,
+                                                              int64_t batch, LiveCols lc) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tl = (lc.nl + kFftTile - 1) / kFftTile, tiles = tl + (lc.nd + kFftTile - 1) / kFftTile;
   const int64_t lb = xcd_block();
@@ -525,9 +527,10 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, doub
   const int c0 = (live ? tile : tile - tl) * kFftTile;
   const int rl = live ? lc.nl : lc.nd;                  // row length of this region
   const int64_t n2 = d.n2;
-  // src and dst alias for the dead columns (in place): no __restrict__
+  // src and dst alias for the dead columns in place (db == nullptr): no __restrict__
   const double2* src = zb + (size_t)b * d.n + (live ? 0 : (size_t)lc.nl * n2) + c0;
-  double2* dst = live ? cb + (size_t)b * lc.nl * n2 + c0 : zb + (size_t)b * d.n + (size_t)lc.nl * n2 + c0;
+  double2* dst = live ? cb + (size_t)b * lc.nl * n2 + c0
+                      : (db ? db + (size_t)b * lc.nd * n2 : zb + (size_t)b * d.n + (size_t)lc.nl * n2) + c0;
   const int ncol = min(kFftTile, rl - c0);
   double2* twl = twl_of(smem, f);
   run_stage1<false, PC, QC>(
@@ -557,7 +560,7 @@ __global__ __launch_bounds__(kFftThreads) void k_fft_cols_live(double2* zb, doub
 // per workgroup, and four workgroups per CU are then three waves per SIMD:
 // 168 VGPRs, no spills (NT = 256 holds 128 and spills).
 template <int PC, int QC, bool TWG, int NT = kFftThreads>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(TWG && PC > 0 ? (NT == kFftThreads ? 4 : 3) : 1))) void k_fft_mid_live(double2* zb, double2* cb, FftDesc d, int64_t batch,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(TWG && PC > 0 ? (NT == kFftThreads ? 4 : 3) : 1))) void k_fft_mid_live(double2* zb, double2* cb, double2* db, FftDesc d, int64_t batch,
                                                              LiveCols lc) {
   extern __shared__ __attribute__((aligned(16))) double2 smem[];
   const int tiles = (d.n2 + kFftTile - 1) / kFftTile;
@@ -573,7 +576,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(TWG && PC > 
   const int nrow = min(kFftTile, d.n2 - r0);
   // rows k2 = r0 + t: live elements in C, dead ones in D (in place: no __restrict__)
   double2* crow = cb + (size_t)b * lc.nl * n2 + (size_t)r0 * lc.nl;
-  const double2* drow = zb + (size_t)b * n + (size_t)lc.nl * n2 + (size_t)r0 * lc.nd;
+  const double2* drow = (db ? db + (size_t)b * lc.nd * n2 : zb + (size_t)b * n + (size_t)lc.nl * n2) +
+                        (size_t)r0 * lc.nd;
   auto y_ld = [&](int t, int j, int m) { return smem[t * S + j + Qp * m]; };
   auto y_st = [&](int t, int j, int m, double2 v) { smem[t * S + j + Qp * m] = v; };
   // (TWG: never written -- the stage-1 fill is off)
@@ -843,8 +847,8 @@ hipError_t launch_fft_filter(const double2* in, double2* t1, double2* t2, double
 
 // The Hilbert filter + envelope compare of launch_fft_filter (kHilbert,
 // kEnvelope) in the live-column layout: zb = [B][L | D] (z), cb = [B][nl * n2].
-hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, int64_t batch, const LiveCols& lc,
-                                   const FftEpi& epi, hipStream_t st) {
+hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, double2* db, const FftDesc& d, int64_t batch,
+                                   const LiveCols& lc, const FftEpi& epi, hipStream_t st) {
   if (!lc.on || epi.mode != kEnvelope) return hipErrorInvalidValue;
   const int tl = (lc.nl + kFftTile - 1) / kFftTile, td = (lc.nd + kFftTile - 1) / kFftTile;
   const unsigned gcol = grid8(batch * (tl + td));
@@ -854,7 +858,8 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
   // (the column and final passes stay four-wave: three-wave workgroups
   // measured slower for them)
 #define COLSL(P, Q) \
-  hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, d, batch, lc)
+  hipLaunchKernelGGL((k_fft_cols_live<P, Q>), dim3(gcol), dim3(kFftThreads), fft_smem_bytes(d.a), st, zb, cb, db, d, batch, \
+                     lc)
   AMR_FFT_PQ(d.a, COLSL);
 #undef COLSL
   // AMR_FFT_MID_TWG=0: the W_L table in LDS (three workgroups per CU instead of four)
@@ -866,14 +871,14 @@ hipError_t launch_fft_hilbert_live(double2* zb, double2* cb, const FftDesc& d, i
 #define MIDL(P, Q)                                                                                              \
   do {                                                                                                          \
     if (twg && nt192 && P > 0 && kFftTile * d.c.r1 <= 192 && kFftTile * d.c.r2 <= 192)                          \
-      hipLaunchKernelGGL((k_fft_mid_live<P, Q, true, 192>), dim3(gmid), dim3(192), sm_mid, st, zb, cb, d,      \
+      hipLaunchKernelGGL((k_fft_mid_live<P, Q, true, 192>), dim3(gmid), dim3(192), sm_mid, st, zb, cb, db, d,  \
                          batch, lc);                                                                            \
     else if (twg)                                                                                               \
-      hipLaunchKernelGGL((k_fft_mid_live<P, Q, true>), dim3(gmid), dim3(kFftThreads), sm_mid, st, zb, cb, d,  \
-                         batch, lc);                                                                            \
+      hipLaunchKernelGGL((k_fft_mid_live<P, Q, true>), dim3(gmid), dim3(kFftThreads), sm_mid, st, zb, cb, db, \
+                         d, batch, lc);                                                                            \
     else                                                                                                        \
-      hipLaunchKernelGGL((k_fft_mid_live<P, Q, false>), dim3(gmid), dim3(kFftThreads), sm_mid, st, zb, cb, d, \
-                         batch, lc);                                                                            \
+      hipLaunchKernelGGL((k_fft_mid_live<P, Q, false>), dim3(gmid), dim3(kFftThreads), sm_mid, st, zb, cb, db, \
+                         d, batch, lc);                                                                            \
   } while (0)
   AMR_FFT_PQ(d.c, MIDL);
 #undef MIDL

@@ -334,6 +334,13 @@ struct amr_fsk_plan {
   double2* z = nullptr;
   double2* u = nullptr;
   double2* v = nullptr;
+  // keep_z (live layout with the exact path): the column pass writes the dead
+  // tiles' transform to dd [B][nd * n2] instead of over z's dead columns, so
+  // all of z (the band-pass output) survives F2 for the exact path; dd also
+  // takes the host entries' staged input (>= 8 B per sample: nd >= n1 / 2)
+  double2* dd = nullptr;
+  bool keep_z = false;
+  int64_t staging_bytes = 0;   // d_x of the host entries (0 with keep_z)
   int64_t u_bytes = 0;
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
   uint32_t* words = nullptr;   // [B][n_words]
@@ -371,7 +378,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   (void)hipSetDevice(pl->device);
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
-  for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->cmp, (void*)pl->words, pl->d_x,
+  for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
                   (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL})
     if (p) (void)hipFree(p);
@@ -418,7 +425,8 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   HIP_TRY(mark_fsk(pl, AMR_TF_HILBERT, 0));
   if (pl->p.lc.on) {
     if (env_out) return fail(AMR_E_INVALID, "live-column plan: envelopes go through a natural-layout plan");
-    HIP_TRY(launch_fft_hilbert_live(pl->z, pl->u, pl->fft.d, B, pl->p.lc, env, pl->stream));
+    HIP_TRY(launch_fft_hilbert_live(pl->z, pl->u, pl->keep_z ? pl->dd : nullptr, pl->fft.d, B, pl->p.lc, env,
+                                    pl->stream));
   } else {
     HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, pl->stream));
   }
@@ -426,7 +434,8 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   return AMR_OK;
 }
 
-// The exact path over F2's flagged streams (their input x still resident).
+// The exact path over F2's flagged streams: with keep_z straight from z (F2
+// left it whole), otherwise F1 again over their input x (still resident).
 int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride) {
   if (!pl->exact_on || pl->exact_mode == 0) return AMR_OK;
   FskExact X{};
@@ -434,6 +443,8 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.list = pl->xlist;
   X.count = pl->xlist + pl->max_streams;
   X.rows = reinterpret_cast<double*>(pl->z);
+  X.live = pl->keep_z ? 1 : 0;
+  X.lc = pl->p.lc;
   X.slots = pl->xslots;
   X.slot_doubles = pl->slot_doubles;
   X.n_slots = pl->n_slots;
@@ -446,14 +457,16 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
   pl->ran_exact = true;
   HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));
-  // E1: F1 again over the flagged streams only (list mode), natural z layout
-  FskParams p1 = pl->p;
-  p1.amb = nullptr;
-  p1.lc = LiveCols{};
-  p1.xlist = X.list;
-  p1.xcount = X.count;
-  HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f,
-                              pl->stream));
+  if (!pl->keep_z) {
+    // E1: F1 again over the flagged streams only (list mode), natural z layout
+    FskParams p1 = pl->p;
+    p1.amb = nullptr;
+    p1.lc = LiveCols{};
+    p1.xlist = X.list;
+    p1.xcount = X.count;
+    HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f,
+                                pl->stream));
+  }
   HIP_TRY(launch_fsk_exact_env(B, pl->p, X, pl->stream));
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1));
   return AMR_OK;
@@ -510,13 +523,23 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   return AMR_OK;
 }
 
-// The host entries stage the input in d_x (max_streams rows of up to 8 B per
-// sample), where it stays for the exact path after F2.
-int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride) {
+// Where the host entries stage the input (max_streams rows of up to 8 B per
+// sample): dd with keep_z (the column pass overwrites it after F1 read it),
+// else d_x, where it stays for the exact path's F1 re-run after F2.
+int staging_buffer(amr_fsk_plan* pl, void** buf) {
+  if (pl->keep_z) {
+    *buf = pl->dd;
+    return AMR_OK;
+  }
+  if (!pl->d_x) HIP_TRY(hipMalloc(&pl->d_x, (size_t)(pl->max_streams * pl->p.n * 8)));
+  *buf = pl->d_x;
+  return AMR_OK;
+}
+int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x_stride, void** staged) {
   const int64_t es = dtype_size(dtype);
   const int64_t n = pl->p.n;
-  if (!pl->d_x) HIP_TRY(hipMalloc(&pl->d_x, (size_t)(pl->max_streams * n * 8)));
-  return copy_batch_h2d(pl->d_x, x, n * es, x_stride * es, B, pl->stream);
+  if (int rc = staging_buffer(pl, staged)) return rc;
+  return copy_batch_h2d(*staged, x, n * es, x_stride * es, B, pl->stream);
 }
 
 int ensure_out_staging(amr_fsk_plan* pl) {
@@ -575,13 +598,14 @@ LiveCols plan_live_cols(const FftShape& f, const FskParams& p) {
 struct FskGeom {
   FskParams p{};
   FftShape sh;
-  int64_t z = 0, u = 0, v = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
+  int64_t z = 0, u = 0, v = 0, dd = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
+  bool keep_z = false;
   // the exact path: flags, scales, list, slots, exact bits, pocketfft tables
   bool exact = false;
   int n_slots = 0;
   int64_t slot_doubles = 0, xflags = 0, amb = 0, xlist = 0, xslots = 0, xbits = 0, xpool = 0, xplan = 0;
   int64_t total() const {
-    return z + u + v + cmp + words + six + staging + out + xflags + amb + xlist + xslots + xbits + xpool + xplan;
+    return z + u + v + dd + cmp + words + six + staging + out + xflags + amb + xlist + xslots + xbits + xpool + xplan;
   }
 };
 bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& g) {
@@ -634,6 +658,15 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
     g.xbits = max_streams * p.bits_stride;
     g.xpool = pf_pool_doubles_bound(n) * 8;
     g.xplan = (int64_t)sizeof(PfLen);
+    // live layout: keep all of z through F2 (the exact path then needs no F1
+    // re-run); the dead tiles' transform and the staged input go to dd
+    // (AMR_FSK_KEEPZ=0, an A/B switch: dead tiles in place, the F1 re-run)
+    static const bool keepz_env = [] { const char* e = std::getenv("AMR_FSK_KEEPZ"); return !(e && e[0] == '0'); }();
+    g.keep_z = keepz_env && p.lc.on && (int64_t)p.lc.nd * p.lc.n2 * 2 >= n;
+    if (g.keep_z) {
+      g.dd = max_streams * (int64_t)p.lc.nd * p.lc.n2 * 16;
+      g.staging = 0;
+    }
   }
   return true;
 }
@@ -698,11 +731,13 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   }
   if (pl->fft.six) pl->scratch_bytes += geo.six;
   pl->u_bytes = geo.u;
+  pl->staging_bytes = geo.staging;
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, geo.z},
       {(void**)&pl->u, geo.u},
       {(void**)&pl->v, geo.v},
+      {(void**)&pl->dd, geo.dd},
       {(void**)&pl->cmp, geo.cmp},
       {(void**)&pl->words, geo.words},
       {(void**)&pl->xflags, geo.xflags},
@@ -741,6 +776,13 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     }
     pl->exact_on = true;
     pl->x_lean = pf_hilbert_lean(L);
+    // keep_z reads z in the [L | D] layout through the lean kernel only; a
+    // live-layout length is 5-smooth, so pocketfft's plans are always lean
+    pl->keep_z = geo.keep_z;
+    if (pl->keep_z && !pl->x_lean) {
+      fsk_plan_free(pl);
+      return fail(AMR_E_INVALID, "exact path: live-layout length " + std::to_string(n) + " without a lean plan");
+    }
     pl->p.amb = pl->amb;
     pl->p.xflags = pl->xflags;         // F3 reads a flagged stream's bits from xbits
     pl->p.xbits = pl->xbits;
@@ -759,8 +801,8 @@ int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
   // scratch + the host-API staging (allocated on the first amr_fsk_demod_host)
-  const int64_t staging = plan->max_streams * plan->p.n * 8;
-  return plan->scratch_bytes + staging + plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
+  return plan->scratch_bytes + plan->staging_bytes +
+         plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
@@ -856,8 +898,9 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   if (plan->p.n_bits == 0) {
     if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
   } else {
-    if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
-    if (int rc = run_fsk(plan, plan->d_x, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+    void* xs = nullptr;
+    if (int rc = stage_input(plan, x, dtype, B, x_stride, &xs)) return rc;
+    if (int rc = run_fsk(plan, xs, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   }
   if (int rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B,
                               plan->stream))
@@ -890,13 +933,14 @@ int amr_fsk_demod_host_async(amr_fsk_plan* plan, const void* x, int dtype, int64
   if (plan->p.n_bits == 0) {
     if (int rc = fsk_empty_outputs(plan, B, plan->d_len, plan->d_sync)) return rc;
   } else {
-    if (!plan->d_x) HIP_TRY(hipMalloc(&plan->d_x, (size_t)(plan->max_streams * n * 8)));
+    void* xs = nullptr;
+    if (int rc = staging_buffer(plan, &xs)) return rc;
     if (x_stride == n)
-      HIP_TRY(hipMemcpyAsync(plan->d_x, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(xs, x, (size_t)(B * n * es), hipMemcpyHostToDevice, st));
     else
-      HIP_TRY(hipMemcpy2DAsync(plan->d_x, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
+      HIP_TRY(hipMemcpy2DAsync(xs, (size_t)(n * es), x, (size_t)(x_stride * es), (size_t)(n * es), (size_t)B,
                                hipMemcpyHostToDevice, st));
-    if (int rc = run_fsk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+    if (int rc = run_fsk(plan, xs, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
   }
   if (out_stride == cap)
     HIP_TRY(hipMemcpyAsync(out, plan->d_out, (size_t)(B * cap), hipMemcpyDeviceToHost, st));
@@ -957,8 +1001,9 @@ int amr_fsk_envelopes_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t
       if (q) (void)hipFree(q);
     if (rc) return rc;
   } else {
-    if (int rc = stage_input(plan, x, dtype, B, x_stride)) return rc;
-    if (int rc = run_fsk_front(plan, plan->d_x, dtype, B, n, true)) return rc;
+    void* xs = nullptr;
+    if (int rc = stage_input(plan, x, dtype, B, x_stride, &xs)) return rc;
+    if (int rc = run_fsk_front(plan, xs, dtype, B, n, true)) return rc;
     HIP_TRY(hipMemcpyAsync(h.data(), hilbert_out(plan->fft, plan->u, plan->v), h.size() * 8, hipMemcpyDeviceToHost,
                            plan->stream));
     HIP_TRY(hipStreamSynchronize(plan->stream));

@@ -15,7 +15,7 @@ struct FskExact {
   const uint32_t* flags;   // [B / 32] F2's flags: bit s of word s / 32
   int32_t* list;           // [B] ordinal -> stream (E0)
   int32_t* count;          // [1] flagged streams (E0)
-  double* rows;            // the plan's z: [ordinal][n] (f_mark, f_space), then (env_mark, env_space)
+  double* rows;            // the plan's z: (f_mark, f_space), then (env_mark, env_space) (see live)
   double* slots;           // [n_slots][slot_doubles] envelope scratch (E2)
   int64_t slot_doubles;
   int n_slots;
@@ -25,6 +25,12 @@ struct FskExact {
   uint8_t* xbits;          // [B][bits_stride] exact compare bits, F3 reads them for flagged streams
   int fuse;                // LDS-fused transforms (pf_fuse_on)
   int lean;                // ... and every radix hard-coded: k_exact_env_lean
+  // live (the plan's keep_z): rows is z itself, stream-indexed in the [L | D]
+  // layout lc, whole after F2 -- no F1 re-run; the envelopes go back into z's
+  // live samples, E3 reads them there.  Otherwise rows holds the F1 re-run's
+  // output by ordinal, natural layout.
+  int live;
+  LiveCols lc;
 };
 
 // E0: F2's flags -> X.list / X.count.  Then F1 in list mode (fsk_api.cpp),

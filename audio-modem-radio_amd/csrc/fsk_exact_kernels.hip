@@ -135,19 +135,35 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
 }
 
 // E2, lean: plans with only hard-coded radices, every transform fused (no
-// fallback code in the kernel, so a smaller register budget than k_exact_env)
-// two workgroups per CU (4 waves per SIMD: <= 128 VGPRs)
+// fallback code in the kernel, so a smaller register budget than k_exact_env).
+// LIVE: row r = tone r & 1 of stream list[r >> 1], read from z's [L | D]
+// layout; only the live samples' envelopes are written back (E3 reads no
+// others).  Two workgroups per CU (4 waves per SIMD: <= 128 VGPRs).
+template <bool LIVE>
 __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_env_lean(FskParams p,
                                                                                                          FskExact X) {
   __shared__ pf::Cx lds[2 * kPfTileElems];
   const int64_t cnt = *X.count;
   const int64_t n = p.n;
+  const LiveCols lc = X.lc;
   double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
-    double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
-    auto src = [=](int i) { return zr[2 * i]; };
-    auto fin = [=](int i, double e) { zr[2 * i] = e; };
-    pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
+    const int64_t s = LIVE ? (int64_t)X.list[r >> 1] : (r >> 1);
+    double* zr = X.rows + (size_t)s * 2 * n + (r & 1);
+    if (LIVE) {
+      auto src = [=](int i) { return zr[2 * lc_zoff(lc, i)]; };
+      auto fin = [=](int i, double e) {
+        const int j2 = lc_div(i, lc.inv_n1);
+        bool live;
+        const int pos = lc_col_pos(lc, i - j2 * lc.n1, live);
+        if (live) zr[2 * ((int64_t)j2 * lc.nl + pos)] = e;
+      };
+      pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
+    } else {
+      auto src = [=](int i) { return zr[2 * i]; };
+      auto fin = [=](int i, double e) { zr[2 * i] = e; };
+      pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
+    }
   }
 }
 
@@ -162,8 +178,11 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
   const int64_t n2 = p.rn2, n1 = p.lc.on ? p.lc.n1 : p.rn1;
   const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
   for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {
-    const double2* e = reinterpret_cast<const double2*>(X.rows) + (size_t)q * n;   // (env_mark, env_space)
-    uint8_t* ob = X.xbits + (size_t)X.list[q] * p.bits_stride;
+    const int64_t st = X.list[q];
+    // (env_mark, env_space): z of stream st ([L | D]: live column c, row kk at
+    // kk * nl + c), or the ordinal row q (natural layout)
+    const double2* e = reinterpret_cast<const double2*>(X.rows) + (size_t)(X.live ? st : q) * n;
+    uint8_t* ob = X.xbits + (size_t)st * p.bits_stride;
     for (int64_t qb = threadIdx.x; qb < nbytes; qb += blockDim.x) {
       const int64_t cb = qb / n2, kk = qb - cb * n2;
       unsigned byte = 0;
@@ -172,7 +191,8 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
         if (c >= ncol) break;
         const int64_t col = p.lc.on ? lc_live_col(p.lc, c) : c;
         const int64_t i = col + n1 * kk;
-        if (i < n && e[i].x > e[i].y) byte |= 1u << t;
+        const int64_t o = X.live ? kk * p.lc.nl + c : i;
+        if (i < n && e[o].x > e[o].y) byte |= 1u << t;
       }
       ob[qb] = (uint8_t)byte;
     }
@@ -198,10 +218,14 @@ hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X
       return 256;
     return std::max(1, per_cu * cus);
   };
-  static const int res_full = resident((const void*)k_exact_env), res_lean = resident((const void*)k_exact_env_lean);
-  if (X.lean)
-    hipLaunchKernelGGL(k_exact_env_lean, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0, st, p,
-                       X);
+  static const int res_full = resident((const void*)k_exact_env),
+                   res_lean = resident((const void*)k_exact_env_lean<false>);
+  if (X.live)   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
+    hipLaunchKernelGGL(k_exact_env_lean<true>, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0,
+                       st, p, X);
+  else if (X.lean)
+    hipLaunchKernelGGL(k_exact_env_lean<false>, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0,
+                       st, p, X);
   else
     hipLaunchKernelGGL(k_exact_env, dim3((unsigned)std::min(X.n_slots, res_full)), dim3(kEnvThreads), 0, st, p, X);
   hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 2048)), dim3(kBitsThreads), 0, st, p, X);

@@ -384,7 +384,9 @@ __device__ void cfftp_passes(const PfPasses& P, const double* pool, Cx* c, Cx* c
 }
 
 // ------------------------- LDS-fused executor -------------------------------
-constexpr int kPfLoadU = 8;   // tile loads a thread issues before it writes any to LDS
+constexpr int kPfThreadsPre = 512;                      // workgroup size of the prefetching tile loop
+constexpr int kPfPreC = kPfTileElems / kPfThreadsPre;    // complex elements per thread of a tile
+constexpr int kPfPreR = kPfTileDoubles / kPfThreadsPre;  // real elements per thread of a tile
 // One tile pass: radix IP over the tile's Q columns, local sizes idol = ido / D,
 // l1l = l1 / L; column uu holds residue i = i0 + uu % Qi of the group's
 // global index (the butterfly's twiddle index is i + D * i_loc).
@@ -414,33 +416,57 @@ template <bool FWD, class Rd, class Wr>
 __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, const double* pool, Rd rd, Wr wr, Cx* lds) {
   const int D = G.D, L = G.L, P = G.P;
   const int Q = G.Q, Qi = G.Qi, Qk = G.Qk;
-  const int nti = (D + Qi - 1) / Qi, ntk = (L + Qk - 1) / Qk;
-  for (int tile = 0; tile < nti * ntk; ++tile) {
+  const int nti = (D + Qi - 1) / Qi, ntk = (L + Qk - 1) / Qk, nt = nti * ntk;
+  // a 512-thread workgroup holds a whole tile in registers (kPfPreC per
+  // thread): the next tile's loads are issued before this tile's passes, so
+  // their latency hides behind the LDS work and the stores
+  const bool pre = blockDim.x == kPfThreadsPre;
+  Cx pv[kPfPreC];
+  auto geom = [&](int tile, int& i0, int& k0, int& qi, int& qk) {
     const int tk = tile / nti, ti = tile - tk * nti;
-    const int i0 = ti * Qi, k0 = tk * Qk;
-    const int qi = (int)(D - i0 < Qi ? D - i0 : Qi), qk = (int)(L - k0 < Qk ? L - k0 : Qk);
+    i0 = ti * Qi;
+    k0 = tk * Qk;
+    qi = D - i0 < Qi ? D - i0 : Qi;
+    qk = L - k0 < Qk ? L - k0 : Qk;
+  };
+  auto issue = [&](int tile) {
+    int i0, k0, qi, qk;
+    geom(tile, i0, k0, qi, qk);
+    const int ne = qk * P * qi;
+#pragma unroll
+    for (int u = 0; u < kPfPreC; ++u) {
+      const int e = (int)threadIdx.x + u * kPfThreadsPre;
+      if (e < ne) {
+        const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+        pv[u] = rd(i0 + ii + D * (j + P * (k0 + kk)));
+      }
+    }
+  };
+  if (pre) issue(0);
+  for (int tile = 0; tile < nt; ++tile) {
+    int i0, k0, qi, qk;
+    geom(tile, i0, k0, qi, qk);
     Cx* cur = lds;
     Cx* nxt = lds + kPfTileElems;
-    // load in memory order (k, j, i), kPfLoadU independent loads in flight per thread
-    const int ne = (int)qk * P * qi;
-    for (int e0 = threadIdx.x; e0 < ne; e0 += kPfLoadU * blockDim.x) {
-      Cx v[kPfLoadU];
-      int li[kPfLoadU];
+    // load in memory order (k, j, i)
+    const int ne = qk * P * qi;
+    if (pre) {
 #pragma unroll
-      for (int u = 0; u < kPfLoadU; ++u) {
-        const int e = e0 + u * (int)blockDim.x;
-        li[u] = -1;
+      for (int u = 0; u < kPfPreC; ++u) {
+        const int e = (int)threadIdx.x + u * kPfThreadsPre;
         if (e < ne) {
           const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
-          li[u] = j * Q + kk * Qi + ii;
-          v[u] = rd(i0 + ii + D * (j + P * (k0 + kk)));
+          cur[j * Q + kk * Qi + ii] = pv[u];
         }
       }
-#pragma unroll
-      for (int u = 0; u < kPfLoadU; ++u)
-        if (li[u] >= 0) cur[li[u]] = v[u];
+    } else {
+      for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+        const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+        cur[j * Q + kk * Qi + ii] = rd(i0 + ii + D * (j + P * (k0 + kk)));
+      }
     }
     __syncthreads();
+    if (pre && tile + 1 < nt) issue(tile + 1);
     for (int q = G.f0; q < G.f0 + G.nf; ++q) {
       const PfFact F = Pl.f[q];
       const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
@@ -461,8 +487,7 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     }
     // store in memory order (j, k, i)
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-      const int ii = (int)(e % qi);
-      const int r = e / qi, kk = r % qk, j = r / qk;
+      const int ii = e % qi, r = e / qi, kk = r % qk, j = r / qk;
       wr(i0 + ii + D * (k0 + kk + L * j), cur[j * Q + kk * Qi + ii]);
     }
     __syncthreads();
@@ -1176,31 +1201,45 @@ __device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, 
     }
     const int D = Gr.D, Pp = Gr.P, Lr = Gr.L, DP = D * Pp;
     const int Qk = Gr.Qk;
+    const bool pre = blockDim.x == kPfThreadsPre;
+    double pv[kPfPreR];
+    // global a + D (k + Lr w) -> local k DP + a + D w, in memory order (w, k, a)
+    auto issue = [&](int k0) {
+      const int qk = Lr - k0 < Qk ? Lr - k0 : Qk, ne = qk * DP;
+#pragma unroll
+      for (int u = 0; u < kPfPreR; ++u) {
+        const int e = (int)threadIdx.x + u * kPfThreadsPre;
+        if (e < ne) {
+          const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+          const int pos = a + D * (k0 + kk) + D * Lr * w;
+          pv[u] = g == 0 ? src(pos) : in[pos];
+        }
+      }
+    };
+    if (pre) issue(0);
     for (int k0 = 0; k0 < Lr; k0 += Qk) {
       const int qk = Lr - k0 < Qk ? Lr - k0 : Qk;
       double* cur = lds;
       double* nxt = lds + kPfTileDoubles;
-      // load in memory order (w, k, a): global a + D (k + Lr w) -> local k DP + a + D w
       const int ne = qk * DP;
-      for (int e0 = threadIdx.x; e0 < ne; e0 += kPfLoadU * blockDim.x) {
-        double v[kPfLoadU];
-        int li[kPfLoadU];
+      if (pre) {
 #pragma unroll
-        for (int u = 0; u < kPfLoadU; ++u) {
-          const int e = e0 + u * (int)blockDim.x;
-          li[u] = -1;
+        for (int u = 0; u < kPfPreR; ++u) {
+          const int e = (int)threadIdx.x + u * kPfThreadsPre;
           if (e < ne) {
             const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
-            const int pos = a + D * (k0 + kk) + D * Lr * w;
-            li[u] = kk * DP + a + D * w;
-            v[u] = g == 0 ? src(pos) : in[pos];
+            cur[kk * DP + a + D * w] = pv[u];
           }
         }
-#pragma unroll
-        for (int u = 0; u < kPfLoadU; ++u)
-          if (li[u] >= 0) cur[li[u]] = v[u];
+      } else {
+        for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+          const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+          const int pos = a + D * (k0 + kk) + D * Lr * w;
+          cur[kk * DP + a + D * w] = g == 0 ? src(pos) : in[pos];
+        }
       }
       __syncthreads();
+      if (pre && k0 + Qk < Lr) issue(k0 + Qk);
       for (int q = Gr.f0; q > Gr.f0 - Gr.nf; --q) {
         const PfFact F = P.f[q];
         const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
