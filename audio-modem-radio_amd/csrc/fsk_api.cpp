@@ -645,7 +645,7 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
   g.exact = exact_env && p.n_bits > 0;
   if (g.exact) {
-    g.slot_doubles = n + pf_scratch_doubles_n(n);    // the row, then its transforms' scratch
+    g.slot_doubles = pf_even(n) + pf_scratch_doubles_n(n);   // the row, then its transforms' scratch
     // one persistent workgroup per slot: up to 2 per stream and 512 (2 per
     // CU; the launch takes no more than are resident at once, E2's register
     // budget allows one per CU), within 2 GiB of slots
@@ -1112,7 +1112,7 @@ int amr_resample_host(const double* x, int64_t nx, int64_t num, int64_t batch, d
   double *xd = nullptr, *yd = nullptr, *slots = nullptr;
   const int n_slots = (int)std::min<int64_t>(batch, 64);
   // scratch for the slots, and for pf_finish's transform before that
-  const int64_t sd = std::max(pf_scratch_doubles_n(nx), pf_scratch_doubles_n(num)) + std::max(nx, num);
+  const int64_t sd = std::max(pf_scratch_doubles_n(nx), pf_scratch_doubles_n(num)) + pf_even(std::max(nx, num));
   int rc = AMR_OK;
   hipError_t e = hipMalloc(&slots, (size_t)(n_slots * sd * 8));
   if (e == hipSuccess) e = hipMalloc(&xd, (size_t)(batch * nx * 8));
@@ -1146,8 +1146,9 @@ int amr_hilbert_env_exact_host(const double* x, int64_t n, int64_t batch, double
   HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   PfDev D;
   double *xd = nullptr, *slots = nullptr;
-  const int n_slots = (int)std::min<int64_t>(batch, 128);
-  const int64_t sd = n + pf_scratch_doubles_n(n);   // the fused envelope keeps the spectrum in its slot
+  const int64_t sd = pf_even(n) + pf_scratch_doubles_n(n);   // the fused envelope keeps the spectrum in its slot
+  // as the FSK exact path: up to 512 persistent workgroups within 2 GiB
+  const int n_slots = (int)std::max<int64_t>(1, std::min<int64_t>({batch, 512, ((int64_t)1 << 31) / (sd * 8)}));
   int rc = AMR_OK;
   hipError_t e = hipMalloc(&slots, (size_t)(n_slots * sd * 8));
   if (e == hipSuccess) e = hipMalloc(&xd, (size_t)(batch * n * 8));

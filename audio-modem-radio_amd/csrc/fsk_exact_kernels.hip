@@ -128,41 +128,67 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
     double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = zr[2 * i];
     __syncthreads();
-    pf::pf_hilbert_env(*X.L, X.pool, c, c, c + n, X.fct, X.fuse ? lds : nullptr);
+    pf::pf_hilbert_env(*X.L, X.pool, c, c, c + pf_even(n), X.fct, X.fuse ? lds : nullptr);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) zr[2 * i] = c[i];
     __syncthreads();
   }
 }
 
-// E2, lean: plans with only hard-coded radices, every transform fused (no
-// fallback code in the kernel, so a smaller register budget than k_exact_env).
-// LIVE: row r = tone r & 1 of stream list[r >> 1], read from z's [L | D]
-// layout; only the live samples' envelopes are written back (E3 reads no
-// others).  Two workgroups per CU (4 waves per SIMD: <= 128 VGPRs).
+// E2, lean plans (pf_hilbert_lean), as two kernels (one holding both halves
+// spills registers): E2a the real transform of row r = tone r & 1 of stream
+// s into its halfcomplex spectrum, parked in the row's own z elements; E2b the
+// spectrum times h, the inverse transform and the envelope, back into z.
+// LIVE: s = list[r >> 1], z in the [L | D] layout (element i of the row at
+// lc_zoff(i); only live samples' envelopes written -- E3 reads no others);
+// otherwise s = r >> 1, the F1 re-run's natural rows.  Two workgroups per CU
+// (4 waves per SIMD: <= 128 VGPRs).
 template <bool LIVE>
-__global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_env_lean(FskParams p,
-                                                                                                         FskExact X) {
+struct ZRow {
+  double* zr;
+  LiveCols lc;
+  __device__ int64_t at(int i) const { return LIVE ? 2 * lc_zoff(lc, i) : 2 * (int64_t)i; }
+};
+template <bool LIVE>
+__device__ inline ZRow<LIVE> zrow(const FskParams& p, const FskExact& X, int64_t r) {
+  const int64_t s = LIVE ? (int64_t)X.list[r >> 1] : (r >> 1);
+  return ZRow<LIVE>{X.rows + (size_t)s * 2 * p.n + (r & 1), X.lc};
+}
+
+template <bool LIVE>
+__global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_rfft(FskParams p,
+                                                                                                     FskExact X) {
   __shared__ pf::Cx lds[2 * kPfTileElems];
   const int64_t cnt = *X.count;
-  const int64_t n = p.n;
-  const LiveCols lc = X.lc;
-  double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
+  double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
-    const int64_t s = LIVE ? (int64_t)X.list[r >> 1] : (r >> 1);
-    double* zr = X.rows + (size_t)s * 2 * n + (r & 1);
+    const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
+    pf::pf_rfft_row(
+        *X.L, X.pool, [=](int i) { return z.zr[z.at(i)]; }, [=](int i, double v) { z.zr[z.at(i)] = v; }, slot, lds);
+  }
+}
+
+template <bool LIVE>
+__global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_cenv(FskParams p,
+                                                                                                     FskExact X) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  const int64_t cnt = *X.count;
+  double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
+  for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+    const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
+    auto fget = [=](int j) { return z.zr[z.at(j)]; };
     if (LIVE) {
-      auto src = [=](int i) { return zr[2 * lc_zoff(lc, i)]; };
-      auto fin = [=](int i, double e) {
-        const int j2 = lc_div(i, lc.inv_n1);
-        bool live;
-        const int pos = lc_col_pos(lc, i - j2 * lc.n1, live);
-        if (live) zr[2 * ((int64_t)j2 * lc.nl + pos)] = e;
-      };
-      pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
+      const LiveCols lc = z.lc;
+      pf::pf_env_row(
+          *X.L, X.pool, fget,
+          [=](int i, double e) {
+            const int j2 = lc_div(i, lc.inv_n1);
+            bool live;
+            const int pos = lc_col_pos(lc, i - j2 * lc.n1, live);
+            if (live) z.zr[2 * ((int64_t)j2 * lc.nl + pos)] = e;
+          },
+          slot, X.fct, lds);
     } else {
-      auto src = [=](int i) { return zr[2 * i]; };
-      auto fin = [=](int i, double e) { zr[2 * i] = e; };
-      pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*X.L, X.pool, src, fin, c, X.fct, lds);
+      pf::pf_env_row(*X.L, X.pool, fget, [=](int i, double e) { z.zr[2 * (int64_t)i] = e; }, slot, X.fct, lds);
     }
   }
 }
@@ -219,14 +245,15 @@ hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X
     return std::max(1, per_cu * cus);
   };
   static const int res_full = resident((const void*)k_exact_env),
-                   res_lean = resident((const void*)k_exact_env_lean<false>);
-  if (X.live)   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
-    hipLaunchKernelGGL(k_exact_env_lean<true>, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0,
-                       st, p, X);
-  else if (X.lean)
-    hipLaunchKernelGGL(k_exact_env_lean<false>, dim3((unsigned)std::min(X.n_slots, res_lean)), dim3(kEnvThreads), 0,
-                       st, p, X);
-  else
+                   res_lean = std::min(resident((const void*)k_exact_rfft<true>), resident((const void*)k_exact_cenv<true>));
+  const dim3 gl((unsigned)std::min(X.n_slots, res_lean));
+  if (X.live) {   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
+    hipLaunchKernelGGL(k_exact_rfft<true>, gl, dim3(kEnvThreads), 0, st, p, X);
+    hipLaunchKernelGGL(k_exact_cenv<true>, gl, dim3(kEnvThreads), 0, st, p, X);
+  } else if (X.lean) {
+    hipLaunchKernelGGL(k_exact_rfft<false>, gl, dim3(kEnvThreads), 0, st, p, X);
+    hipLaunchKernelGGL(k_exact_cenv<false>, gl, dim3(kEnvThreads), 0, st, p, X);
+  } else
     hipLaunchKernelGGL(k_exact_env, dim3((unsigned)std::min(X.n_slots, res_full)), dim3(kEnvThreads), 0, st, p, X);
   hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 2048)), dim3(kBitsThreads), 0, st, p, X);
   return hipGetLastError();

@@ -17,7 +17,10 @@
 namespace amr {
 
 constexpr int kPfMaxF = 32;
-constexpr int64_t kPfMaxLen = (int64_t)1 << 27;   // longest row the device transforms take   // factors of one plan (a length < 2^31 has at most 30)
+constexpr int64_t kPfMaxLen = (int64_t)1 << 27;   // longest row the device transforms take
+// a real row's doubles rounded up to even: complex scratch placed after a row
+// stays 16-byte aligned (pocketfft_dev.h Cx is loaded and stored as one b128)
+__host__ __device__ inline int64_t pf_even(int64_t n) { return (n + 1) & ~(int64_t)1; }   // factors of one plan (a length < 2^31 has at most 30)
 
 // one factor of a plan: radix ip, l1 = product of the factors before it,
 // ido = len / (l1 * ip); tw / tws: offsets (in doubles) of its twiddles and of
@@ -40,7 +43,10 @@ constexpr int kPfMaxGroupP = 512;    // radix product of a group (>= 4 columns p
 // a multi-pass group couples every residue mod D, so a tile is Qk whole
 // blocks k of D * P reals (read at a + D (k + L w), written to k D P + ...).
 // Q = 0 marks a pass run unfused over the whole array (too large a block, or
-// a generic radix).
+// a generic radix).  Q = 2: a "pair" group -- the trailing passes from an
+// even ido D on (radf4 / radf2 only), L = 1, P = len / D; a tile is Qk pair
+// classes {p, D/2 - p} (residues 2p - 1, 2p and their mirrors) or the class
+// {0, D - 1}, times all P blocks: reads and writes a + D w.
 constexpr int kPfTileDoubles = 2 * kPfTileElems;
 constexpr int kPfMinRun = 16;        // doubles a tile reads contiguously, at least
 struct PfGroup {

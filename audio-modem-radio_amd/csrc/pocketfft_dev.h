@@ -14,12 +14,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pocketfft.h"
 
 namespace amr {
 namespace pf {
 
-struct Cx {
+// 16-byte aligned: LDS and global accesses as one b128 / dwordx4 each (every
+// complex array the routines touch starts on a 16-byte boundary: pf_even)
+struct alignas(16) Cx {
   double r, i;
 };
 __device__ __forceinline__ Cx add(Cx a, Cx b) { return {a.r + b.r, a.i + b.i}; }
@@ -52,6 +56,22 @@ __device__ __forceinline__ Cx rot135(Cx a) {
 }
 
 #define PF_FOR(t, N) for (int t = (int)threadIdx.x; t < (int)(N); t += (int)blockDim.x)
+
+// x / d and x % d for 0 <= x < 2^31 by a uniform divisor d >= 1 (round-up
+// multiply-high: m = floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d), then
+// x / d = (umulhi(x, m) + x) >> l, exact for every such x).  The tile loops'
+// index splits run on these instead of ~30-instruction integer divisions.
+struct FDiv {
+  unsigned m;
+  int l, d;
+  __device__ explicit FDiv(int dd) : d(dd) {
+    l = 0;
+    while ((1 << l) < dd) ++l;
+    m = (unsigned)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - (uint64_t)dd)) / (uint64_t)dd + 1);
+  }
+  __device__ __forceinline__ int div(int x) const { return (int)((__umulhi((unsigned)x, m) + (unsigned)x) >> l); }
+  __device__ __forceinline__ int mod(int x) const { return x - div(x) * d; }
+};
 
 // ======================= complex passes (cfftp) =============================
 // One butterfly of pocketfft's pass of radix IP at index i of a pass with ido:
@@ -391,14 +411,15 @@ constexpr int kPfPreR = kPfTileDoubles / kPfThreadsPre;  // real elements per th
 // l1l = l1 / L; column uu holds residue i = i0 + uu % Qi of the group's
 // global index (the butterfly's twiddle index is i + D * i_loc).
 template <bool FWD, int IP>
-__device__ __forceinline__ void tile_pass(const Cx* cur, Cx* nxt, int Q, int Qi, int qi, int qk, int i0, int D,
-                          int idol, int l1l, const Cx* wa, int ido) {
-  const int nb = (int)Q * idol * l1l;
+__device__ __forceinline__ void tile_pass(const Cx* cur, Cx* nxt, const FDiv& fQ, const FDiv& fQi, int qi, int qk,
+                                          int i0, int D, int idol, int l1l, const Cx* wa, int ido) {
+  const int Q = fQ.d, nb = Q * idol * l1l;
+  const FDiv fid(idol);
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    const int uu = (int)(b % Q);
-    const int ii = uu % Qi, kk = uu / Qi;
+    const int r = fQ.div(b), uu = b - r * Q;
+    const int kk = fQi.div(uu), ii = uu - kk * fQi.d;
     if (ii >= qi || kk >= qk) continue;
-    const int r = b / Q, i_loc = r % idol, k_loc = r / idol;
+    const int k_loc = fid.div(r), i_loc = r - k_loc * idol;
     Cx v[IP];
 #pragma unroll
     for (int m = 0; m < IP; ++m) v[m] = cur[(i_loc + idol * (m + IP * k_loc)) * Q + uu];
@@ -421,6 +442,7 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
   // thread): the next tile's loads are issued before this tile's passes, so
   // their latency hides behind the LDS work and the stores
   const bool pre = blockDim.x == kPfThreadsPre;
+  const FDiv fP(P), fQ(Q), fQi(Qi);
   Cx pv[kPfPreC];
   auto geom = [&](int tile, int& i0, int& k0, int& qi, int& qk) {
     const int tk = tile / nti, ti = tile - tk * nti;
@@ -433,11 +455,12 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     int i0, k0, qi, qk;
     geom(tile, i0, k0, qi, qk);
     const int ne = qk * P * qi;
+    const FDiv fqi(qi);
 #pragma unroll
     for (int u = 0; u < kPfPreC; ++u) {
       const int e = (int)threadIdx.x + u * kPfThreadsPre;
       if (e < ne) {
-        const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+        const int r = fqi.div(e), ii = e - r * qi, kk = fP.div(r), j = r - kk * P;
         pv[u] = rd(i0 + ii + D * (j + P * (k0 + kk)));
       }
     }
@@ -450,18 +473,19 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     Cx* nxt = lds + kPfTileElems;
     // load in memory order (k, j, i)
     const int ne = qk * P * qi;
+    const FDiv fqi(qi), fqk(qk);
     if (pre) {
 #pragma unroll
       for (int u = 0; u < kPfPreC; ++u) {
         const int e = (int)threadIdx.x + u * kPfThreadsPre;
         if (e < ne) {
-          const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+          const int r = fqi.div(e), ii = e - r * qi, kk = fP.div(r), j = r - kk * P;
           cur[j * Q + kk * Qi + ii] = pv[u];
         }
       }
     } else {
       for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-        const int ii = e % qi, r = e / qi, j = r % P, kk = r / P;
+        const int r = fqi.div(e), ii = e - r * qi, kk = fP.div(r), j = r - kk * P;
         cur[j * Q + kk * Qi + ii] = rd(i0 + ii + D * (j + P * (k0 + kk)));
       }
     }
@@ -472,13 +496,13 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
       const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
       const int idol = F.ido / D, l1l = F.l1 / L;
       switch (F.ip) {
-        case 4: tile_pass<FWD, 4>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 8: tile_pass<FWD, 8>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 2: tile_pass<FWD, 2>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 3: tile_pass<FWD, 3>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 5: tile_pass<FWD, 5>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 7: tile_pass<FWD, 7>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        default: tile_pass<FWD, 11>(cur, nxt, Q, Qi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 4: tile_pass<FWD, 4>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 8: tile_pass<FWD, 8>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 2: tile_pass<FWD, 2>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 3: tile_pass<FWD, 3>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 5: tile_pass<FWD, 5>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 7: tile_pass<FWD, 7>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        default: tile_pass<FWD, 11>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
       }
       __syncthreads();
       Cx* t = cur;
@@ -487,7 +511,7 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     }
     // store in memory order (j, k, i)
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-      const int ii = e % qi, r = e / qi, kk = r % qk, j = r / qk;
+      const int r = fqi.div(e), ii = e - r * qi, j = fqk.div(r), kk = r - j * qk;
       wr(i0 + ii + D * (k0 + kk + L * j), cur[j * Q + kk * Qi + ii]);
     }
     __syncthreads();
@@ -497,6 +521,10 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
 struct RdBuf {
   const Cx* p;
   __device__ Cx operator()(int i) const { return p[i]; }
+};
+struct WrD {
+  double* p;
+  __device__ void operator()(int i, double v) const { p[i] = v; }
 };
 struct RdD {
   const double* p;
@@ -513,7 +541,7 @@ struct WrBuf {
 // (the last one reads B); others materialise src into A, run the passes and
 // hand A's entries to fin.
 template <bool FWD, class Src, class Fin, bool LEAN = false>
-__device__ void cfftp_x(const PfPasses& P, const double* pool, Src src, Cx* A, Cx* B, Fin fin, Cx* lds) {
+__device__ __forceinline__ void cfftp_x(const PfPasses& P, const double* pool, Src src, Cx* A, Cx* B, Fin fin, Cx* lds) {
   const int len = P.len;
   if (!LEAN && (!P.fused || lds == nullptr)) {
     PF_FOR(i, len) A[i] = src(i);
@@ -556,8 +584,9 @@ __device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, doub
 __device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
                       int bs = 0) {
 #define CH(a, b, c) ch[(a) + ido * ((b) + 2 * (c))]
+  const FDiv fl1(l1);
   PF_FOR(tb, nb * l1) {
-    const int b = tb / l1, k = tb - b * l1;
+    const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     CH(0, 0, k) = CC(0, k, 0) + CC(0, k, 1);
@@ -569,9 +598,10 @@ __device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido <= 2) return;
   const int hi = (ido - 1) / 2;
+  const FDiv flh(l1 * hi), fhi(hi);
   PF_FOR(tb, nb * l1 * hi) {
-    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
-    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int b = flh.div(tb), t = tb - b * (l1 * hi);
+    const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double tr2 = wa[i - 2] * CC(i - 1, k, 1) + wa[i - 1] * CC(i, k, 1);
@@ -590,8 +620,9 @@ __device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* _
                       int bs = 0) {
   const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 3 * (c))]
+  const FDiv fl1(l1);
   PF_FOR(tb, nb * l1) {
-    const int b = tb / l1, k = tb - b * l1;
+    const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double cr2 = CC(0, k, 1) + CC(0, k, 2);
@@ -601,9 +632,10 @@ __device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido == 1) return;
   const int hi = (ido - 1) / 2;
+  const FDiv flh(l1 * hi), fhi(hi);
   PF_FOR(tb, nb * l1 * hi) {
-    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
-    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int b = flh.div(tb), t = tb - b * (l1 * hi);
+    const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
@@ -629,8 +661,9 @@ __device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* _
                       int bs = 0) {
   const double hsqt2 = 0.707106781186547524400844362104849;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 4 * (c))]
+  const FDiv fl1(l1);
   PF_FOR(tb, nb * l1) {
-    const int b = tb / l1, k = tb - b * l1;
+    const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double tr1 = CC(0, k, 3) + CC(0, k, 1);
@@ -650,9 +683,10 @@ __device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido <= 2) return;
   const int hi = (ido - 1) / 2;
+  const FDiv flh(l1 * hi), fhi(hi);
   PF_FOR(tb, nb * l1 * hi) {
-    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
-    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int b = flh.div(tb), t = tb - b * (l1 * hi);
+    const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double cr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
@@ -684,8 +718,9 @@ __device__ void radf5(int ido, int l1, const double* __restrict__ cc0, double* _
   const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
   const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 5 * (c))]
+  const FDiv fl1(l1);
   PF_FOR(tb, nb * l1) {
-    const int b = tb / l1, k = tb - b * l1;
+    const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double cr2 = CC(0, k, 4) + CC(0, k, 1), ci5 = CC(0, k, 4) - CC(0, k, 1);
@@ -698,9 +733,10 @@ __device__ void radf5(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido == 1) return;
   const int hi = (ido - 1) / 2;
+  const FDiv flh(l1 * hi), fhi(hi);
   PF_FOR(tb, nb * l1 * hi) {
-    const int b = tb / (l1 * hi), t = tb - b * (l1 * hi);
-    const int k = t / hi, i = 2 + 2 * (t - k * hi), ic = ido - i;
+    const int b = flh.div(tb), t = tb - b * (l1 * hi);
+    const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
     const double* cc = cc0 + b * bs;
     double* ch = ch0 + b * bs;
     const double dr2 = WA(0, i - 2) * CC(i - 1, k, 1) + WA(0, i - 1) * CC(i, k, 1);
@@ -1165,19 +1201,249 @@ __device__ inline void radf_whole(const PfPasses& P, const PfFact& F, const doub
   __syncthreads();
 }
 
+// ---- "pair" groups: the trailing radf4 / radf2 passes from an even ido D ----
+// (pocketfft.h, Q = 2).  A tile holds two runs of residues mod D -- run A
+// (slots 0 .. na-1) and run B (slots na .. na+nb-1) -- times all P = n / D
+// blocks w, at lds[w * R + slot]; element (a, w) is position a + D w.  Within
+// a pass of ido = D B, position a' = res + D blk; the butterflies below are
+// radf4 / radf2's own expressions on explicit (residue, block) references.
+struct PairTile {
+  int a0, na, b0, nb, R;
+  __device__ int slot(int res) const { return (res >= a0 && res < a0 + na) ? res - a0 : na + (res - b0); }
+};
+__device__ inline PairTile pair_tile(int tile, int D, int T) {
+  PairTile t;
+  if (tile == 0) {   // the class {0, D - 1}
+    t.a0 = 0;
+    t.na = 1;
+    t.b0 = D - 1;
+    t.nb = 1;
+  } else {
+    const int H = D / 2, pmax = H / 2;
+    const int p0 = 1 + (tile - 1) * T, p1 = min(p0 + T, pmax + 1);
+    const int pe = (2 * (p1 - 1) == H) ? p1 - 1 : p1;   // p = H / 2 pairs with itself
+    t.a0 = 2 * p0 - 1;
+    t.na = 2 * (p1 - p0);
+    t.b0 = 2 * (H - pe) + 1;
+    t.nb = 2 * (pe - p0);
+  }
+  t.R = t.na + t.nb;
+  return t;
+}
+__device__ inline int pair_tiles(int D, int T) { return 1 + ((D / 2) / 2 + T - 1) / T; }
+
+// radf4's butterflies: x[m] = CC(i-1, k, m), y[m] = CC(i, k, m) in; lo[b] =
+// CH(i-1, b, k) for b = 0, 2 and CH(ic-1, b, k) for b = 1, 3; hi[b] likewise
+// at i / ic
+__device__ __forceinline__ void radf4_bf(const double* x, const double* y, int i, int ido, const double* wa,
+                                         double* lo, double* hi) {
+#define WA(q, j) wa[(j) + (q) * (ido - 1)]
+  const double cr2 = WA(0, i - 2) * x[1] + WA(0, i - 1) * y[1];
+  const double ci2 = WA(0, i - 2) * y[1] - WA(0, i - 1) * x[1];
+  const double cr3 = WA(1, i - 2) * x[2] + WA(1, i - 1) * y[2];
+  const double ci3 = WA(1, i - 2) * y[2] - WA(1, i - 1) * x[2];
+  const double cr4 = WA(2, i - 2) * x[3] + WA(2, i - 1) * y[3];
+  const double ci4 = WA(2, i - 2) * y[3] - WA(2, i - 1) * x[3];
+#undef WA
+  const double tr1 = cr4 + cr2, tr4 = cr4 - cr2;
+  const double ti1 = ci2 + ci4, ti4 = ci2 - ci4;
+  const double tr2 = x[0] + cr3, tr3 = x[0] - cr3;
+  const double ti2 = y[0] + ci3, ti3 = y[0] - ci3;
+  lo[0] = tr2 + tr1;
+  lo[3] = tr2 - tr1;
+  hi[0] = ti1 + ti2;
+  hi[3] = ti1 - ti2;
+  lo[2] = tr3 + ti4;
+  lo[1] = tr3 - ti4;
+  hi[2] = tr4 + ti3;
+  hi[1] = tr4 - ti3;
+}
+// column 0 (c[m] = CC(0, k, m)): z0[b] = CH(0, b, k) for b = 0, 2; zl[b] = CH(ido-1, b, k) for b = 1, 3
+__device__ __forceinline__ void radf4_c0(const double* c, double* z0, double* zl) {
+  const double tr1 = c[3] + c[1];
+  z0[2] = c[3] - c[1];
+  const double tr2 = c[0] + c[2];
+  zl[1] = c[0] - c[2];
+  z0[0] = tr2 + tr1;
+  zl[3] = tr2 - tr1;
+}
+// column ido - 1 (c[m] = CC(ido-1, k, m)): zl[b] = CH(ido-1, b, k) for b = 0, 2; z0[b] = CH(0, b, k) for b = 1, 3
+__device__ __forceinline__ void radf4_cl(const double* c, double* z0, double* zl) {
+  const double hsqt2 = 0.707106781186547524400844362104849;
+  const double ti1 = -hsqt2 * (c[1] + c[3]);
+  const double tr1b = hsqt2 * (c[1] - c[3]);
+  zl[0] = c[0] + tr1b;
+  zl[2] = c[0] - tr1b;
+  z0[3] = ti1 + c[2];
+  z0[1] = ti1 - c[2];
+}
+// radf2's: lo[0] = CH(i-1, 0, k), lo[1] = CH(ic-1, 1, k); hi likewise
+__device__ __forceinline__ void radf2_bf(const double* x, const double* y, int i, const double* wa, double* lo,
+                                         double* hi) {
+  const double tr2 = wa[i - 2] * x[1] + wa[i - 1] * y[1];
+  const double ti2 = wa[i - 2] * y[1] - wa[i - 1] * x[1];
+  lo[0] = x[0] + tr2;
+  lo[1] = x[0] - tr2;
+  hi[0] = ti2 + y[0];
+  hi[1] = ti2 - y[0];
+}
+__device__ __forceinline__ void radf2_c0(const double* c, double* z0, double* zl) {
+  z0[0] = c[0] + c[1];
+  zl[1] = c[0] - c[1];
+}
+__device__ __forceinline__ void radf2_cl(const double* c, double* z0, double* zl) {
+  z0[1] = -c[1];
+  zl[0] = c[0];
+}
+
+// one radf<IP> pass (ido = D B, l1) over a pair tile: cur -> nxt
+template <int IP>
+__device__ __forceinline__ void rpair_pass(const double* cur, double* nxt, const PairTile& T, bool special, int D, int B, int l1,
+                           const double* wa) {
+  const int ido = D * B, R = T.R;
+  // input CC(res + D blk, k, m) at w = blk + B (k + l1 m); output CH(res + D blk, b, k) at w = blk + B (b + IP k)
+  auto ldx = [&](int res, int blk, int k, int m) { return cur[(blk + B * (k + l1 * m)) * R + T.slot(res)]; };
+  auto stx = [&](int res, int blk, int b, int k, double v) { nxt[(blk + B * (b + IP * k)) * R + T.slot(res)] = v; };
+  if (!special) {
+    const int np = R / 2, nbf = l1 * B * np;
+    const FDiv fnp(np), fB(B);
+    for (int t = threadIdx.x; t < nbf; t += blockDim.x) {
+      const int r = fnp.div(t), u = t - r * np, k = fB.div(r), blk = r - k * B;
+      const int ae = u < T.na / 2 ? T.a0 + 1 + 2 * u : T.b0 + 1 + 2 * (u - T.na / 2);   // residue of i (even)
+      const int i = ae + D * blk, rc = D - ae, bc = B - 1 - blk;                        // ic = rc + D bc
+      double x[IP], y[IP], lo[IP], hi[IP];
+#pragma unroll
+      for (int m = 0; m < IP; ++m) {
+        x[m] = ldx(ae - 1, blk, k, m);
+        y[m] = ldx(ae, blk, k, m);
+      }
+      if constexpr (IP == 4) radf4_bf(x, y, i, ido, wa, lo, hi);
+      else radf2_bf(x, y, i, wa, lo, hi);
+#pragma unroll
+      for (int b = 0; b < IP; ++b) {
+        if ((b & 1) == 0) {
+          stx(ae - 1, blk, b, k, lo[b]);
+          stx(ae, blk, b, k, hi[b]);
+        } else {
+          stx(rc - 1, bc, b, k, lo[b]);
+          stx(rc, bc, b, k, hi[b]);
+        }
+      }
+    }
+  } else {
+    // columns 0 and ido - 1, and the pairs (i - 1, i) = (D - 1 of block c - 1, 0 of block c), c = 1 .. B - 1
+    const int nbf = l1 * (B + 1);
+    const FDiv fB1(B + 1);
+    for (int t = threadIdx.x; t < nbf; t += blockDim.x) {
+      const int k = fB1.div(t), c = t - k * (B + 1);
+      double x[IP], y[IP], lo[IP], hi[IP];
+      if (c == 0 || c == B) {
+        double z0[IP], zl[IP];
+#pragma unroll
+        for (int m = 0; m < IP; ++m) x[m] = c == 0 ? ldx(0, 0, k, m) : ldx(D - 1, B - 1, k, m);
+        if (c == 0) {
+          if constexpr (IP == 4) radf4_c0(x, z0, zl);
+          else radf2_c0(x, z0, zl);
+        } else {
+          if constexpr (IP == 4) radf4_cl(x, z0, zl);
+          else radf2_cl(x, z0, zl);
+        }
+        // column 0 fills CH(0, even b) and CH(ido-1, odd b); column ido-1 the others
+#pragma unroll
+        for (int b = 0; b < IP; ++b) {
+          const bool to0 = ((b & 1) == 0) == (c == 0);
+          if (to0) stx(0, 0, b, k, z0[b]);
+          else stx(D - 1, B - 1, b, k, zl[b]);
+        }
+      } else {
+        const int i = D * c;   // ic = D (B - c): residue 0 of block B - c, ic - 1 = D - 1 of block B - c - 1
+#pragma unroll
+        for (int m = 0; m < IP; ++m) {
+          x[m] = ldx(D - 1, c - 1, k, m);
+          y[m] = ldx(0, c, k, m);
+        }
+        if constexpr (IP == 4) radf4_bf(x, y, i, ido, wa, lo, hi);
+        else radf2_bf(x, y, i, wa, lo, hi);
+#pragma unroll
+        for (int b = 0; b < IP; ++b) {
+          if ((b & 1) == 0) {
+            stx(D - 1, c - 1, b, k, lo[b]);
+            stx(0, c, b, k, hi[b]);
+          } else {
+            stx(D - 1, B - c - 1, b, k, lo[b]);
+            stx(0, B - c, b, k, hi[b]);
+          }
+        }
+      }
+    }
+  }
+}
+
+// a pair group over the whole array: in (or src, first group) -> out
+template <class Src, class Wr>
+__device__ __forceinline__ void rgroup_pairs(const PfPasses& P, const PfGroup& Gr, const double* pool, Src src,
+                                             bool first, const double* in, Wr wr, double* lds) {
+  const int D = Gr.D, Pp = Gr.P, Tn = Gr.Qk;
+  const int ntiles = pair_tiles(D, Tn);
+  for (int tile = 0; tile < ntiles; ++tile) {
+    const PairTile T = pair_tile(tile, D, Tn);
+    const int R = T.R, ne = R * Pp;
+    double* cur = lds;
+    double* nxt = lds + kPfTileDoubles;
+    const FDiv fR(R);
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) {   // (w, slot): runs A and B of each block
+      const int w = fR.div(e), sl = e - w * R;
+      const int res = sl < T.na ? T.a0 + sl : T.b0 + (sl - T.na);
+      const int pos = res + D * w;
+      cur[e] = first ? src(pos) : in[pos];
+    }
+    __syncthreads();
+    int B = 1;
+    for (int q = Gr.f0; q > Gr.f0 - Gr.nf; --q) {
+      const PfFact F = P.f[q];
+      const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
+      if (F.ip == 4) rpair_pass<4>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa);
+      else rpair_pass<2>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa);
+      __syncthreads();
+      double* t = cur;
+      cur = nxt;
+      nxt = t;
+      B *= (int)F.ip;
+    }
+    for (int e = threadIdx.x; e < ne; e += blockDim.x) {
+      const int w = fR.div(e), sl = e - w * R;
+      const int res = sl < T.na ? T.a0 + sl : T.b0 + (sl - T.na);
+      wr(res + D * w, cur[e]);
+    }
+    __syncthreads();
+  }
+}
+
 // pocketfft's rfftp forward (r2hc, fct 1) of the sequence src(0 .. n-1) into
 // f (halfcomplex); tmp: n doubles of scratch; src must read neither f nor
 // tmp.  Groups in executed order (pocketfft.h), the last one writing f;
 // lds: 2 * kPfTileDoubles doubles.
-template <class Src, bool LEAN = false>
-__device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, double* f, double* tmp,
-                                double* lds) {
+// fin(i, v): where the halfcomplex result goes (WrD{f}: into f).  A fin
+// other than f may alias src's storage element for element: src is read by
+// the first group only, fin written by the last (one group: a single tile, or
+// pair tiles, each of which reads and writes the same positions).
+template <class Src, bool LEAN = false, class Fin = WrD>
+__device__ __forceinline__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, double* f, double* tmp,
+                                                double* lds, Fin fin = Fin{nullptr}) {
   const int G = P.ng;
+  if constexpr (std::is_same<Fin, WrD>::value)
+    if (fin.p == nullptr) fin.p = f;
   auto outbuf = [&](int g) { return ((G - 1 - g) & 1) == 0 ? f : tmp; };
   for (int g = 0; g < G; ++g) {
     const PfGroup& Gr = P.g[g];
+    const bool last = g == G - 1;
     double* out = outbuf(g);
     double* in = g == 0 ? nullptr : outbuf(g - 1);
+    if (Gr.Q == 2) {
+      if (last) rgroup_pairs(P, Gr, pool, src, g == 0, in, fin, lds);
+      else rgroup_pairs(P, Gr, pool, src, g == 0, in, WrD{out}, lds);
+      continue;
+    }
     if (Gr.Q == 0) {
       if (g == 0) {   // materialise the source in the other buffer
         in = out == f ? tmp : f;
@@ -1197,20 +1463,30 @@ __device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, 
       } else {
         radf_whole(P, P.f[Gr.f0], pool, in, out);
       }
+      if (last) {
+        bool direct = false;
+        if constexpr (std::is_same<Fin, WrD>::value) direct = fin.p == out;
+        if (!direct) {
+          PF_FOR(i, P.len) fin(i, out[i]);
+          __syncthreads();
+        }
+      }
       continue;
     }
     const int D = Gr.D, Pp = Gr.P, Lr = Gr.L, DP = D * Pp;
     const int Qk = Gr.Qk;
     const bool pre = blockDim.x == kPfThreadsPre;
+    const FDiv fD(D);
     double pv[kPfPreR];
     // global a + D (k + Lr w) -> local k DP + a + D w, in memory order (w, k, a)
     auto issue = [&](int k0) {
       const int qk = Lr - k0 < Qk ? Lr - k0 : Qk, ne = qk * DP;
+      const FDiv fqk(qk);
 #pragma unroll
       for (int u = 0; u < kPfPreR; ++u) {
         const int e = (int)threadIdx.x + u * kPfThreadsPre;
         if (e < ne) {
-          const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+          const int r = fD.div(e), a = e - r * D, w = fqk.div(r), kk = r - w * qk;
           const int pos = a + D * (k0 + kk) + D * Lr * w;
           pv[u] = g == 0 ? src(pos) : in[pos];
         }
@@ -1222,18 +1498,19 @@ __device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, 
       double* cur = lds;
       double* nxt = lds + kPfTileDoubles;
       const int ne = qk * DP;
+      const FDiv fqk(qk);
       if (pre) {
 #pragma unroll
         for (int u = 0; u < kPfPreR; ++u) {
           const int e = (int)threadIdx.x + u * kPfThreadsPre;
           if (e < ne) {
-            const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+            const int r = fD.div(e), a = e - r * D, w = fqk.div(r), kk = r - w * qk;
             cur[kk * DP + a + D * w] = pv[u];
           }
         }
       } else {
         for (int e = threadIdx.x; e < ne; e += blockDim.x) {
-          const int a = e % D, r = e / D, kk = r % qk, w = r / qk;
+          const int r = fD.div(e), a = e - r * D, w = fqk.div(r), kk = r - w * qk;
           const int pos = a + D * (k0 + kk) + D * Lr * w;
           cur[kk * DP + a + D * w] = g == 0 ? src(pos) : in[pos];
         }
@@ -1256,7 +1533,10 @@ __device__ void rfftp_fwd_fused(const PfPasses& P, const double* pool, Src src, 
         nxt = t;
       }
       // blocks k0 .. k0 + qk - 1 are contiguous in the output
-      for (int e = threadIdx.x; e < ne; e += blockDim.x) out[k0 * DP + e] = cur[e];
+      if (last)
+        for (int e = threadIdx.x; e < ne; e += blockDim.x) fin(k0 * DP + e, cur[e]);
+      else
+        for (int e = threadIdx.x; e < ne; e += blockDim.x) out[k0 * DP + e] = cur[e];
       __syncthreads();
     }
   }
@@ -1396,12 +1676,26 @@ __device__ inline void pf_hilbert_env(const PfLen& L, const double* pool, double
 // pf_hilbert_fusable(L); slot as pf_hilbert_env's (f = slot, then the
 // scratch); src is read before fin is first called.
 template <class Src, class Fin, bool LEAN = false>
-__device__ void pf_hilbert_env_x(const PfLen& L, const double* pool, Src src, Fin fin, double* slot, double fct,
-                                 Cx* lds) {
+__device__ __forceinline__ void pf_hilbert_env_x(const PfLen& L, const double* pool, Src src, Fin fin, double* slot, double fct,
+                                 Cx* lds, int stage = 0) {
   const int n = (int)L.n;
   double* f = slot;
-  const PfScratch s = pf_scratch(L, slot + n, lds);
-  rfftp_fwd_fused<Src, LEAN>(L.r, pool, src, f, s.a, reinterpret_cast<double*>(lds));
+  const PfScratch s = pf_scratch(L, slot + pf_even(n), lds);
+  // stage (diagnostic timing only, AMR_PF_STAGE): 1 the real transform alone
+  // (its halfcomplex output handed to fin), 2 the complex half alone (src
+  // taken as the halfcomplex spectrum)
+  if (stage == 1) {
+    rfftp_fwd_fused<Src, LEAN>(L.r, pool, src, f, s.a, reinterpret_cast<double*>(lds));
+    for (int i = threadIdx.x; i < n; i += blockDim.x) fin(i, f[i]);
+    __syncthreads();
+    return;
+  }
+  if (stage == 2) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) f[i] = src(i);
+    __syncthreads();
+  } else {
+    rfftp_fwd_fused<Src, LEAN>(L.r, pool, src, f, s.a, reinterpret_cast<double*>(lds));
+  }
   auto spec = [=](int i) -> Cx {
     double xr, xi;
     if (i == 0) { xr = f[0]; xi = -0.0; }
@@ -1418,6 +1712,40 @@ __device__ void pf_hilbert_env_x(const PfLen& L, const double* pool, Src src, Fi
     fin(i, h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0)));
   };
   cfftp_x<false, decltype(spec), decltype(envf), LEAN>(L.c, pool, spec, s.x, reinterpret_cast<Cx*>(s.a), envf, lds);
+}
+
+// The two halves of pf_hilbert_env_x as the bodies of two lean kernels (one
+// kernel holding both spills registers): pf_rfft_row -- pocketfft_r forward
+// of src into fin (halfcomplex; fin may be src's own storage), scratch slot
+// (2n); pf_env_row -- the spectrum read back through fget(j) (halfcomplex
+// element j), times h, pocketfft_c backward, 1/n, numpy's abs into fin(i, e),
+// scratch slot (4n).  Lean plans only (pf_hilbert_lean).
+template <class Src, class Fin>
+__device__ __forceinline__ void pf_rfft_row(const PfLen& L, const double* pool, Src src, Fin fin, double* slot,
+                                            Cx* lds) {
+  rfftp_fwd_fused<Src, true, Fin>(L.r, pool, src, slot, slot + L.n, reinterpret_cast<double*>(lds), fin);
+}
+template <class Fget, class Fin>
+__device__ __forceinline__ void pf_env_row(const PfLen& L, const double* pool, Fget fget, Fin fin, double* slot,
+                                           double fct, Cx* lds) {
+  const int n = (int)L.n;
+  auto spec = [=](int i) -> Cx {
+    double xr, xi;
+    if (i == 0) { xr = fget(0); xi = -0.0; }
+    else if (2 * i == n) { xr = fget(n - 1); xi = -0.0; }
+    else if (2 * i < n) { xr = fget(2 * i - 1); xi = fget(2 * i); }
+    else { xr = fget(2 * (n - i) - 1); xi = -fget(2 * (n - i)); }
+    const double hr = (i == 0 || 2 * i == n) ? 1.0 : (2 * i < n ? 2.0 : 0.0), hi = 0.0;
+    return {__builtin_fma(xr, hr, -(xi * hi)), __builtin_fma(xr, hi, xi * hr)};
+  };
+  auto envf = [=](int i, Cx v) {
+    if (fct != 1.0) v = scale(v, fct);
+    const double ar = fabs(v.r), ai = fabs(v.i);
+    const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
+    fin(i, h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0)));
+  };
+  cfftp_x<false, decltype(spec), decltype(envf), true>(L.c, pool, spec, reinterpret_cast<Cx*>(slot),
+                                                       reinterpret_cast<Cx*>(slot + 2 * (size_t)n), envf, lds);
 }
 
 #undef PF_FOR

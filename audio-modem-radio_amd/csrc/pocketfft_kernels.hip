@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_resample(const PfLen* __restr
   __shared__ pf::Cx lds[2 * kPfTileElems];
   pf::Cx* tl = fuse ? lds : nullptr;
   double* c = slots + (size_t)blockIdx.x * slot_doubles;
-  double* scr = c + std::max(nx, num);
+  double* scr = c + pf_even(std::max(nx, num));
   const int64_t N = std::min(num, nx), nyq = N / 2 + 1;
   for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
     const double* xr = x + (size_t)b * nx;
@@ -130,18 +130,27 @@ __global__ __launch_bounds__(kPfThreads) void k_pf_hilbert_env(const PfLen* __re
   }
 }
 
-// the lean instantiation (pf_hilbert_lean plans; the FSK exact path's E2 runs
-// the same code, fsk_exact_kernels.hip k_exact_env_lean)
-__global__ __launch_bounds__(kPfThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_hilbert_env_lean(
+// lean plans (pf_hilbert_lean): the envelope as two kernels, the real
+// transform's halfcomplex output parked in the row itself (the FSK exact
+// path's E2a / E2b run the same bodies, fsk_exact_kernels.hip)
+__global__ __launch_bounds__(kPfThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_rfft_lean(
+    const PfLen* __restrict__ L, const double* pool, double* x, int64_t n, int64_t batch, double* slots,
+    int64_t slot_doubles) {
+  __shared__ pf::Cx lds[2 * kPfTileElems];
+  double* slot = slots + (size_t)blockIdx.x * slot_doubles;
+  for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
+    double* f = x + (size_t)b * n;
+    pf::pf_rfft_row(*L, pool, pf::RdD{f}, pf::WrD{f}, slot, lds);
+  }
+}
+__global__ __launch_bounds__(kPfThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_pf_env_lean(
     const PfLen* __restrict__ L, const double* pool, double* x, int64_t n, int64_t batch, double* slots,
     int64_t slot_doubles, double fct) {
   __shared__ pf::Cx lds[2 * kPfTileElems];
   double* slot = slots + (size_t)blockIdx.x * slot_doubles;
   for (int64_t b = blockIdx.x; b < batch; b += gridDim.x) {
     double* f = x + (size_t)b * n;
-    auto src = [=](int i) { return f[i]; };
-    auto fin = [=](int i, double e) { f[i] = e; };
-    pf::pf_hilbert_env_x<decltype(src), decltype(fin), true>(*L, pool, src, fin, slot, fct, lds);
+    pf::pf_env_row(*L, pool, pf::RdD{f}, pf::WrD{f}, slot, fct, lds);
   }
 }
 
@@ -157,9 +166,12 @@ hipError_t launch_pf_hilbert_env(const PfLen* dL, const double* pool, double* x,
     return (unsigned)(v >= 64 && v <= kPfThreads ? v : kPfThreads);
   }();
   static const int stage = [] { const char* e = getenv("AMR_PF_STAGE"); return e ? atoi(e) : 0; }();
-  if (lean && stage == 0 && nt == kPfThreads && pf_fuse_on()) {
-    hipLaunchKernelGGL(k_pf_hilbert_env_lean, dim3(g), dim3(kPfThreads), 0, st, dL, pool, x, n, batch, slots,
-                       slot_doubles, fct);
+  if (lean && nt == kPfThreads && pf_fuse_on()) {   // (stage 1 / 2: one half alone, for timing)
+    if (stage != 2)
+      hipLaunchKernelGGL(k_pf_rfft_lean, dim3(g), dim3(kPfThreads), 0, st, dL, pool, x, n, batch, slots, slot_doubles);
+    if (stage != 1)
+      hipLaunchKernelGGL(k_pf_env_lean, dim3(g), dim3(kPfThreads), 0, st, dL, pool, x, n, batch, slots, slot_doubles,
+                         fct);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_pf_hilbert_env, dim3(g), dim3(nt), 0, st, dL, pool, x, n, batch, slots, slot_doubles, fct,

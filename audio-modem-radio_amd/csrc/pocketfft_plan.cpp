@@ -258,6 +258,21 @@ void build_rgroups(PfPasses& P) {
     PfGroup& G = P.g[P.ng++];
     G.f0 = k;
     const int64_t D = P.f[k].ido;
+    // an even ido: every pass left is radf4 / radf2 (pocketfft executes its
+    // 4s and 2 last), and they couple only residue pairs {p, D/2 - p} and
+    // {0, D - 1} mod D -- one "pair" group to the end, tiles of T pair
+    // classes times all n / D blocks (pocketfft_dev.h rgroup_pairs)
+    if (D % 2 == 0 && P.len / D <= kPfTileDoubles / 4) {
+      G.nf = k + 1;
+      G.D = D;
+      G.P = P.len / D;
+      G.L = 1;
+      G.Q = 2;
+      G.Qi = 0;
+      G.Qk = (int)(kPfTileDoubles / (4 * G.P));   // T: pair classes per tile (<= 4 T residues)
+      k = -1;
+      break;
+    }
     const int64_t qmin = std::max<int64_t>(1, (kPfMinRun + D - 1) / D);
     G.D = D;
     G.P = P.f[k].ip;
@@ -425,7 +440,7 @@ int64_t pf_pool_doubles_bound(int64_t n) {
 
 int64_t pf_resample_slot_doubles(const PfLen& Lx, const PfLen& Ly) {
   // the row (max n) + one transform's scratch at a time
-  return std::max(Lx.n, Ly.n) + std::max(pf_scratch_doubles(Lx), pf_scratch_doubles(Ly));
+  return pf_even(std::max(Lx.n, Ly.n)) + std::max(pf_scratch_doubles(Lx), pf_scratch_doubles(Ly));
 }
 
 }  // namespace amr
