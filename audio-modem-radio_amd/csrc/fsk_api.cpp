@@ -438,6 +438,11 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
 // left it whole), otherwise F1 again over their input x (still resident).
 int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride) {
   if (!pl->exact_on || pl->exact_mode == 0) return AMR_OK;
+  // AMR_FSK_EXACT_LAUNCH=0 (diagnostic A/B only, decisions then NOT exact):
+  // F1 / F2 keep their margin work, the E0-E3 launches are skipped
+  // (=2: E0 and E3 only, E2 skipped)
+  static const int launch = [] { const char* e = std::getenv("AMR_FSK_EXACT_LAUNCH"); return e ? atoi(e) : 1; }();
+  if (launch == 0) return AMR_OK;
   FskExact X{};
   X.flags = pl->xflags;
   X.list = pl->xlist;
@@ -467,7 +472,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f,
                                 pl->stream));
   }
-  HIP_TRY(launch_fsk_exact_env(B, pl->p, X, pl->stream));
+  HIP_TRY(launch_fsk_exact_env(B, pl->p, X, pl->stream, launch != 2));
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1));
   return AMR_OK;
 }

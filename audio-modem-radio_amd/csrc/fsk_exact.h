@@ -37,6 +37,7 @@ struct FskExact {
 // then E2 + E3: the flagged streams' exact compare bits in X.xbits.  Every
 // kernel exits at once when nothing is flagged.
 hipError_t launch_fsk_exact_list(int64_t B, const FskExact& X, hipStream_t st);
-hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st);
+hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st,
+                                bool env = true);
 
 }  // namespace amr

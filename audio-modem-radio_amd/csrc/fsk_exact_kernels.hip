@@ -231,7 +231,7 @@ hipError_t launch_fsk_exact_list(int64_t B, const FskExact& X, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st) {
+hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X, hipStream_t st, bool env) {
   if (B < 1) return hipSuccess;
   // a persistent grid no larger than what is resident at once: a workgroup
   // beyond that would start its rows only after a resident one finished all of
@@ -247,7 +247,9 @@ hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X
   static const int res_full = resident((const void*)k_exact_env),
                    res_lean = std::min(resident((const void*)k_exact_rfft<true>), resident((const void*)k_exact_cenv<true>));
   const dim3 gl((unsigned)std::min(X.n_slots, res_lean));
-  if (X.live) {   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
+  if (!env) {
+    // (diagnostic: the envelope kernels skipped)
+  } else if (X.live) {   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
     hipLaunchKernelGGL(k_exact_rfft<true>, gl, dim3(kEnvThreads), 0, st, p, X);
     hipLaunchKernelGGL(k_exact_cenv<true>, gl, dim3(kEnvThreads), 0, st, p, X);
   } else if (X.lean) {
@@ -255,7 +257,7 @@ hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X
     hipLaunchKernelGGL(k_exact_cenv<false>, gl, dim3(kEnvThreads), 0, st, p, X);
   } else
     hipLaunchKernelGGL(k_exact_env, dim3((unsigned)std::min(X.n_slots, res_full)), dim3(kEnvThreads), 0, st, p, X);
-  hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 2048)), dim3(kBitsThreads), 0, st, p, X);
+  hipLaunchKernelGGL(k_exact_bits, dim3((unsigned)std::min<int64_t>(B, 256)), dim3(kBitsThreads), 0, st, p, X);
   return hipGetLastError();
 }
 

@@ -664,6 +664,8 @@ def fsk_exact_probe(N, baud, mark, space, dev, B=2048):
     pl = _fsk.FskPlan(N, baud, mark, space, FS, max_streams=B, device=dev)
     pl.enable_timing(True)
     res = {"streams": B, "samples": N, "unit": "ms"}
+    if os.environ.get("AMR_FSK_EXACT", "1") == "0":   # (an A/B run with the exact path off)
+        return {**res, "skipped": "AMR_FSK_EXACT=0"}
     for label, xx, mode in (("silent_padded", x, 1), ("all_exact", x, 2),
                             ("noise_floor", x + rng.normal(0, 0.01, x.shape).astype(np.float32), 1)):
         pl.set_exact_mode(mode)
