@@ -425,8 +425,27 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   HIP_TRY(mark_fsk(pl, AMR_TF_HILBERT, 0));
   if (pl->p.lc.on) {
     if (env_out) return fail(AMR_E_INVALID, "live-column plan: envelopes go through a natural-layout plan");
-    HIP_TRY(launch_fft_hilbert_live(pl->z, pl->u, pl->keep_z ? pl->dd : nullptr, pl->fft.d, B, pl->p.lc, env,
-                                    pl->stream));
+    // AMR_FSK_SUBBATCH=S (an A/B experiment): the three
+    // passes per sub-batch of S streams (a multiple of 32: the flag words),
+    // so a sub-batch's intermediates could stay in the Infinity Cache
+    static const int64_t sub = [] {
+      const char* e = std::getenv("AMR_FSK_SUBBATCH");
+      const int64_t v = e ? atoll(e) : 0;
+      return v >= 32 ? v / 32 * 32 : 0;
+    }();
+    const LiveCols& lc = pl->p.lc;
+    const int64_t step = sub > 0 ? sub : B;
+    for (int64_t b0 = 0; b0 < B; b0 += step) {
+      const int64_t nb = std::min(step, B - b0);
+      FftEpi e = env;
+      e.z = env.z + b0 * pl->p.n;
+      e.bits = env.bits + b0 * env.bits_stride;
+      if (e.amb) e.amb += b0;
+      if (e.xflags) e.xflags += b0 / 32;
+      HIP_TRY(launch_fft_hilbert_live(pl->z + b0 * pl->p.n, pl->u + b0 * (int64_t)lc.nl * lc.n2,
+                                      pl->keep_z ? pl->dd + b0 * (int64_t)lc.nd * lc.n2 : nullptr, pl->fft.d, nb, lc,
+                                      e, pl->stream));
+    }
   } else {
     HIP_TRY(fft_hilbert(pl->fft, pl->z, pl->u, pl->v, B, env, pl->stream));
   }
