@@ -136,12 +136,13 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
 
 // E2, lean plans (pf_hilbert_lean), as two kernels (one holding both halves
 // spills registers): E2a the real transform of row r = tone r & 1 of stream
-// s into its halfcomplex spectrum, parked in the row's own z elements; E2b the
-// spectrum times h, the inverse transform and the envelope, back into z.
-// LIVE: s = list[r >> 1], z in the [L | D] layout (element i of the row at
-// lc_zoff(i); only live samples' envelopes written -- E3 reads no others);
-// otherwise s = r >> 1, the F1 re-run's natural rows.  Two workgroups per CU
-// (4 waves per SIMD: <= 128 VGPRs).
+// s into its halfcomplex spectrum, parked in the row's own z elements in
+// natural order (element j at 2 j); E2b the spectrum times h, the inverse
+// transform and the envelope, back into z in natural order.  LIVE: s =
+// list[r >> 1], f read from z's [L | D] layout (sample i at lc_zoff(i)), only
+// live samples' envelopes written (E3 reads no others); otherwise s = r >> 1,
+// the F1 re-run's natural rows.  Two workgroups per CU (4 waves per SIMD:
+// <= 128 VGPRs).
 template <bool LIVE>
 struct ZRow {
   double* zr;
@@ -162,8 +163,11 @@ __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))
   double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
     const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
+    // the halfcomplex spectrum parked in natural order (the row's z elements
+    // are free once the first group has read them)
     pf::pf_rfft_row(
-        *X.L, X.pool, [=](int i) { return z.zr[z.at(i)]; }, [=](int i, double v) { z.zr[z.at(i)] = v; }, slot, lds);
+        *X.L, X.pool, [=](int i) { return z.zr[z.at(i)]; }, [=](int i, double v) { z.zr[2 * (int64_t)i] = v; }, slot,
+        lds);
   }
 }
 
@@ -175,16 +179,16 @@ __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))
   double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
     const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
-    auto fget = [=](int j) { return z.zr[z.at(j)]; };
-    if (LIVE) {
+    auto fget = [=](int j) { return z.zr[2 * (int64_t)j]; };
+    if (LIVE) {   // envelopes in natural order too, the live samples only (E3 reads no others)
       const LiveCols lc = z.lc;
       pf::pf_env_row(
           *X.L, X.pool, fget,
           [=](int i, double e) {
             const int j2 = lc_div(i, lc.inv_n1);
             bool live;
-            const int pos = lc_col_pos(lc, i - j2 * lc.n1, live);
-            if (live) z.zr[2 * ((int64_t)j2 * lc.nl + pos)] = e;
+            (void)lc_col_pos(lc, i - j2 * lc.n1, live);
+            if (live) z.zr[2 * (int64_t)i] = e;
           },
           slot, X.fct, lds);
     } else {
@@ -205,8 +209,8 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
   const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
   for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {
     const int64_t st = X.list[q];
-    // (env_mark, env_space): z of stream st ([L | D]: live column c, row kk at
-    // kk * nl + c), or the ordinal row q (natural layout)
+    // (env_mark, env_space) in natural sample order: z of stream st (live
+    // layout, E2 parked them so), or the ordinal row q (natural layout)
     const double2* e = reinterpret_cast<const double2*>(X.rows) + (size_t)(X.live ? st : q) * n;
     uint8_t* ob = X.xbits + (size_t)st * p.bits_stride;
     for (int64_t qb = threadIdx.x; qb < nbytes; qb += blockDim.x) {
@@ -217,8 +221,7 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
         if (c >= ncol) break;
         const int64_t col = p.lc.on ? lc_live_col(p.lc, c) : c;
         const int64_t i = col + n1 * kk;
-        const int64_t o = X.live ? kk * p.lc.nl + c : i;
-        if (i < n && e[o].x > e[o].y) byte |= 1u << t;
+        if (i < n && e[i].x > e[i].y) byte |= 1u << t;
       }
       ob[qb] = (uint8_t)byte;
     }

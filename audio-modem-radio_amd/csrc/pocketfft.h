@@ -25,8 +25,29 @@ __host__ __device__ inline int64_t pf_even(int64_t n) { return (n + 1) & ~(int64
 // one factor of a plan: radix ip, l1 = product of the factors before it,
 // ido = len / (l1 * ip); tw / tws: offsets (in doubles) of its twiddles and of
 // the generic passes' extra table in the plan's pool, -1 when absent
+// x / d for 0 <= x < 2^31 by multiply-high (pocketfft_dev.h FDiv): m =
+// floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d); built on the host for every
+// divisor the fused tile loops use, so no division is emulated on the device
+struct PfDiv {
+  uint32_t m;
+  int32_t l, d;
+};
+inline PfDiv pf_div(int64_t d) {
+  PfDiv r{};
+  r.d = (int32_t)(d < 1 ? 1 : d);
+  r.l = 0;
+  while (((int64_t)1 << r.l) < r.d) ++r.l;
+  r.m = (uint32_t)(((((uint64_t)1 << 32) * (((uint64_t)1 << r.l) - (uint64_t)r.d)) / (uint64_t)r.d) + 1);
+  return r;
+}
+
+// dv: the pass's divisors inside its fused group -- complex: [0] ido / D;
+// real blocks: [0] l1 / L, [1] (ido - 1) / 2, [2] their product; real pair
+// tiles: [0] B = ido / D, [1] B + 1
 struct PfFact {
   int64_t ip, l1, ido, tw, tws;
+  PfDiv dv[3];
+  int32_t l1l;   // l1 / L inside its fused group (complex, real blocks)
 };
 
 // LDS-fused execution of consecutive complex passes (pocketfft_dev.h
@@ -49,10 +70,15 @@ constexpr int kPfMaxGroupP = 512;    // radix product of a group (>= 4 columns p
 // {0, D - 1}, times all P blocks: reads and writes a + D w.
 constexpr int kPfTileDoubles = 2 * kPfTileElems;
 constexpr int kPfMinRun = 16;        // doubles a tile reads contiguously, at least
+// dv (host-built divisors of the group's tile loops) -- complex: P, Q, Qi,
+// the last i-tile's qi, Qk, the last k-tile's qk; real blocks: D, Qk, the
+// last tile's qk; pair tiles: R and R / 2 of the special tile, a full tile
+// and the last tile
 struct PfGroup {
   int f0, nf;
   int64_t P, D, L;
   int Q, Qi, Qk;
+  PfDiv dv[7];   // (complex: [6] the i-tile count, for the tile index split)
 };
 
 // an FFTPACK-style plan (pocketfft's cfftp or rfftp); fused: the passes are

@@ -64,6 +64,7 @@ __device__ __forceinline__ Cx rot135(Cx a) {
 struct FDiv {
   unsigned m;
   int l, d;
+  __device__ FDiv(const PfDiv& v) : m(v.m), l(v.l), d(v.d) {}   // host-built (pocketfft.h pf_div)
   __device__ explicit FDiv(int dd) : d(dd) {
     l = 0;
     while ((1 << l) < dd) ++l;
@@ -412,9 +413,8 @@ constexpr int kPfPreR = kPfTileDoubles / kPfThreadsPre;  // real elements per th
 // global index (the butterfly's twiddle index is i + D * i_loc).
 template <bool FWD, int IP>
 __device__ __forceinline__ void tile_pass(const Cx* cur, Cx* nxt, const FDiv& fQ, const FDiv& fQi, int qi, int qk,
-                                          int i0, int D, int idol, int l1l, const Cx* wa, int ido) {
-  const int Q = fQ.d, nb = Q * idol * l1l;
-  const FDiv fid(idol);
+                                          int i0, int D, const FDiv& fid, int l1l, const Cx* wa, int ido) {
+  const int Q = fQ.d, idol = fid.d, nb = Q * idol * l1l;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     const int r = fQ.div(b), uu = b - r * Q;
     const int kk = fQi.div(uu), ii = uu - kk * fQi.d;
@@ -442,10 +442,11 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
   // thread): the next tile's loads are issued before this tile's passes, so
   // their latency hides behind the LDS work and the stores
   const bool pre = blockDim.x == kPfThreadsPre;
-  const FDiv fP(P), fQ(Q), fQi(Qi);
+  const FDiv fP(G.dv[0]), fQ(G.dv[1]), fQi(G.dv[2]);
   Cx pv[kPfPreC];
+  const FDiv fnti(G.dv[6]);
   auto geom = [&](int tile, int& i0, int& k0, int& qi, int& qk) {
-    const int tk = tile / nti, ti = tile - tk * nti;
+    const int tk = fnti.div(tile), ti = tile - tk * nti;
     i0 = ti * Qi;
     k0 = tk * Qk;
     qi = D - i0 < Qi ? D - i0 : Qi;
@@ -455,7 +456,7 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     int i0, k0, qi, qk;
     geom(tile, i0, k0, qi, qk);
     const int ne = qk * P * qi;
-    const FDiv fqi(qi);
+    const FDiv fqi(qi == Qi ? G.dv[2] : G.dv[3]);
 #pragma unroll
     for (int u = 0; u < kPfPreC; ++u) {
       const int e = (int)threadIdx.x + u * kPfThreadsPre;
@@ -473,7 +474,7 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     Cx* nxt = lds + kPfTileElems;
     // load in memory order (k, j, i)
     const int ne = qk * P * qi;
-    const FDiv fqi(qi), fqk(qk);
+    const FDiv fqi(qi == Qi ? G.dv[2] : G.dv[3]), fqk(qk == Qk ? G.dv[4] : G.dv[5]);
     if (pre) {
 #pragma unroll
       for (int u = 0; u < kPfPreC; ++u) {
@@ -494,15 +495,16 @@ __device__ __forceinline__ void cgroup(const PfPasses& Pl, const PfGroup& G, con
     for (int q = G.f0; q < G.f0 + G.nf; ++q) {
       const PfFact F = Pl.f[q];
       const Cx* wa = reinterpret_cast<const Cx*>(pool + F.tw);
-      const int idol = F.ido / D, l1l = F.l1 / L;
+      const FDiv fid(F.dv[0]);
+      const int l1l = F.l1l;
       switch (F.ip) {
-        case 4: tile_pass<FWD, 4>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 8: tile_pass<FWD, 8>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 2: tile_pass<FWD, 2>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 3: tile_pass<FWD, 3>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 5: tile_pass<FWD, 5>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        case 7: tile_pass<FWD, 7>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
-        default: tile_pass<FWD, 11>(cur, nxt, fQ, fQi, qi, qk, i0, D, idol, l1l, wa, F.ido); break;
+        case 4: tile_pass<FWD, 4>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        case 8: tile_pass<FWD, 8>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        case 2: tile_pass<FWD, 2>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        case 3: tile_pass<FWD, 3>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        case 5: tile_pass<FWD, 5>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        case 7: tile_pass<FWD, 7>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
+        default: tile_pass<FWD, 11>(cur, nxt, fQ, fQi, qi, qk, i0, D, fid, l1l, wa, F.ido); break;
       }
       __syncthreads();
       Cx* t = cur;
@@ -582,9 +584,9 @@ __device__ void cfftp(const PfPasses& P, const double* pool, Cx* c, Cx* ch, doub
 // nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
 // whole-array pass)
 __device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
-                      int bs = 0) {
+                      int bs = 0, const PfDiv* dv = nullptr) {
 #define CH(a, b, c) ch[(a) + ido * ((b) + 2 * (c))]
-  const FDiv fl1(l1);
+  const FDiv fl1 = dv ? FDiv(dv[0]) : FDiv(l1);
   PF_FOR(tb, nb * l1) {
     const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
@@ -598,7 +600,7 @@ __device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido <= 2) return;
   const int hi = (ido - 1) / 2;
-  const FDiv flh(l1 * hi), fhi(hi);
+  const FDiv flh = dv ? FDiv(dv[2]) : FDiv(l1 * hi), fhi = dv ? FDiv(dv[1]) : FDiv(hi);
   PF_FOR(tb, nb * l1 * hi) {
     const int b = flh.div(tb), t = tb - b * (l1 * hi);
     const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
@@ -617,10 +619,10 @@ __device__ void radf2(int ido, int l1, const double* __restrict__ cc0, double* _
 // nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
 // whole-array pass)
 __device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
-                      int bs = 0) {
+                      int bs = 0, const PfDiv* dv = nullptr) {
   const double taur = -0.5, taui = 0.8660254037844386467637231707529362;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 3 * (c))]
-  const FDiv fl1(l1);
+  const FDiv fl1 = dv ? FDiv(dv[0]) : FDiv(l1);
   PF_FOR(tb, nb * l1) {
     const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
@@ -632,7 +634,7 @@ __device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido == 1) return;
   const int hi = (ido - 1) / 2;
-  const FDiv flh(l1 * hi), fhi(hi);
+  const FDiv flh = dv ? FDiv(dv[2]) : FDiv(l1 * hi), fhi = dv ? FDiv(dv[1]) : FDiv(hi);
   PF_FOR(tb, nb * l1 * hi) {
     const int b = flh.div(tb), t = tb - b * (l1 * hi);
     const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
@@ -658,10 +660,10 @@ __device__ void radf3(int ido, int l1, const double* __restrict__ cc0, double* _
 // nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
 // whole-array pass)
 __device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
-                      int bs = 0) {
+                      int bs = 0, const PfDiv* dv = nullptr) {
   const double hsqt2 = 0.707106781186547524400844362104849;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 4 * (c))]
-  const FDiv fl1(l1);
+  const FDiv fl1 = dv ? FDiv(dv[0]) : FDiv(l1);
   PF_FOR(tb, nb * l1) {
     const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
@@ -683,7 +685,7 @@ __device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido <= 2) return;
   const int hi = (ido - 1) / 2;
-  const FDiv flh(l1 * hi), fhi(hi);
+  const FDiv flh = dv ? FDiv(dv[2]) : FDiv(l1 * hi), fhi = dv ? FDiv(dv[1]) : FDiv(hi);
   PF_FOR(tb, nb * l1 * hi) {
     const int b = flh.div(tb), t = tb - b * (l1 * hi);
     const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
@@ -714,11 +716,11 @@ __device__ void radf4(int ido, int l1, const double* __restrict__ cc0, double* _
 // nb sub-arrays at stride bs (the fused executor's tile columns; 1 / 0 for a
 // whole-array pass)
 __device__ void radf5(int ido, int l1, const double* __restrict__ cc0, double* __restrict__ ch0, const double* wa, int nb = 1,
-                      int bs = 0) {
+                      int bs = 0, const PfDiv* dv = nullptr) {
   const double tr11 = 0.3090169943749474241022934171828191, ti11 = 0.9510565162951535721164393333793821;
   const double tr12 = -0.8090169943749474241022934171828191, ti12 = 0.5877852522924731291687059546390728;
 #define CH(a, b, c) ch[(a) + ido * ((b) + 5 * (c))]
-  const FDiv fl1(l1);
+  const FDiv fl1 = dv ? FDiv(dv[0]) : FDiv(l1);
   PF_FOR(tb, nb * l1) {
     const int b = fl1.div(tb), k = tb - b * l1;
     const double* cc = cc0 + b * bs;
@@ -733,7 +735,7 @@ __device__ void radf5(int ido, int l1, const double* __restrict__ cc0, double* _
   }
   if (ido == 1) return;
   const int hi = (ido - 1) / 2;
-  const FDiv flh(l1 * hi), fhi(hi);
+  const FDiv flh = dv ? FDiv(dv[2]) : FDiv(l1 * hi), fhi = dv ? FDiv(dv[1]) : FDiv(hi);
   PF_FOR(tb, nb * l1 * hi) {
     const int b = flh.div(tb), t = tb - b * (l1 * hi);
     const int k = fhi.div(t), i = 2 + 2 * (t - k * hi), ic = ido - i;
@@ -1298,15 +1300,15 @@ __device__ __forceinline__ void radf2_cl(const double* c, double* z0, double* zl
 
 // one radf<IP> pass (ido = D B, l1) over a pair tile: cur -> nxt
 template <int IP>
-__device__ __forceinline__ void rpair_pass(const double* cur, double* nxt, const PairTile& T, bool special, int D, int B, int l1,
-                           const double* wa) {
+__device__ __forceinline__ void rpair_pass(const double* cur, double* nxt, const PairTile& T, bool special, int D,
+                                           int B, int l1, const double* wa, const FDiv& fnp, const PfDiv* dvp) {
   const int ido = D * B, R = T.R;
   // input CC(res + D blk, k, m) at w = blk + B (k + l1 m); output CH(res + D blk, b, k) at w = blk + B (b + IP k)
   auto ldx = [&](int res, int blk, int k, int m) { return cur[(blk + B * (k + l1 * m)) * R + T.slot(res)]; };
   auto stx = [&](int res, int blk, int b, int k, double v) { nxt[(blk + B * (b + IP * k)) * R + T.slot(res)] = v; };
   if (!special) {
     const int np = R / 2, nbf = l1 * B * np;
-    const FDiv fnp(np), fB(B);
+    const FDiv fB(dvp[0]);
     for (int t = threadIdx.x; t < nbf; t += blockDim.x) {
       const int r = fnp.div(t), u = t - r * np, k = fB.div(r), blk = r - k * B;
       const int ae = u < T.na / 2 ? T.a0 + 1 + 2 * u : T.b0 + 1 + 2 * (u - T.na / 2);   // residue of i (even)
@@ -1333,7 +1335,7 @@ __device__ __forceinline__ void rpair_pass(const double* cur, double* nxt, const
   } else {
     // columns 0 and ido - 1, and the pairs (i - 1, i) = (D - 1 of block c - 1, 0 of block c), c = 1 .. B - 1
     const int nbf = l1 * (B + 1);
-    const FDiv fB1(B + 1);
+    const FDiv fB1(dvp[1]);
     for (int t = threadIdx.x; t < nbf; t += blockDim.x) {
       const int k = fB1.div(t), c = t - k * (B + 1);
       double x[IP], y[IP], lo[IP], hi[IP];
@@ -1390,7 +1392,8 @@ __device__ __forceinline__ void rgroup_pairs(const PfPasses& P, const PfGroup& G
     const int R = T.R, ne = R * Pp;
     double* cur = lds;
     double* nxt = lds + kPfTileDoubles;
-    const FDiv fR(R);
+    const int kind = tile == 0 ? 0 : (tile == ntiles - 1 ? 4 : 2);   // Gr.dv: R, R / 2 of this tile's kind
+    const FDiv fR(Gr.dv[kind]), fnp(Gr.dv[kind + 1]);
     for (int e = threadIdx.x; e < ne; e += blockDim.x) {   // (w, slot): runs A and B of each block
       const int w = fR.div(e), sl = e - w * R;
       const int res = sl < T.na ? T.a0 + sl : T.b0 + (sl - T.na);
@@ -1402,8 +1405,8 @@ __device__ __forceinline__ void rgroup_pairs(const PfPasses& P, const PfGroup& G
     for (int q = Gr.f0; q > Gr.f0 - Gr.nf; --q) {
       const PfFact F = P.f[q];
       const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
-      if (F.ip == 4) rpair_pass<4>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa);
-      else rpair_pass<2>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa);
+      if (F.ip == 4) rpair_pass<4>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa, fnp, F.dv);
+      else rpair_pass<2>(cur, nxt, T, tile == 0, D, B, (int)F.l1, wa, fnp, F.dv);
       __syncthreads();
       double* t = cur;
       cur = nxt;
@@ -1476,12 +1479,12 @@ __device__ __forceinline__ void rfftp_fwd_fused(const PfPasses& P, const double*
     const int D = Gr.D, Pp = Gr.P, Lr = Gr.L, DP = D * Pp;
     const int Qk = Gr.Qk;
     const bool pre = blockDim.x == kPfThreadsPre;
-    const FDiv fD(D);
+    const FDiv fD(Gr.dv[0]);
     double pv[kPfPreR];
     // global a + D (k + Lr w) -> local k DP + a + D w, in memory order (w, k, a)
     auto issue = [&](int k0) {
       const int qk = Lr - k0 < Qk ? Lr - k0 : Qk, ne = qk * DP;
-      const FDiv fqk(qk);
+      const FDiv fqk(qk == Qk ? Gr.dv[1] : Gr.dv[2]);
 #pragma unroll
       for (int u = 0; u < kPfPreR; ++u) {
         const int e = (int)threadIdx.x + u * kPfThreadsPre;
@@ -1498,7 +1501,7 @@ __device__ __forceinline__ void rfftp_fwd_fused(const PfPasses& P, const double*
       double* cur = lds;
       double* nxt = lds + kPfTileDoubles;
       const int ne = qk * DP;
-      const FDiv fqk(qk);
+      const FDiv fqk(qk == Qk ? Gr.dv[1] : Gr.dv[2]);
       if (pre) {
 #pragma unroll
         for (int u = 0; u < kPfPreR; ++u) {
@@ -1520,12 +1523,12 @@ __device__ __forceinline__ void rfftp_fwd_fused(const PfPasses& P, const double*
       for (int q = Gr.f0; q > Gr.f0 - Gr.nf; --q) {
         const PfFact F = P.f[q];
         const double* wa = pool + (F.tw >= 0 ? F.tw : 0);
-        const int l1l = F.l1 / Lr;
+        const int l1l = F.l1l;
         switch (F.ip) {
-          case 4: radf4(F.ido, l1l, cur, nxt, wa, qk, DP); break;
-          case 2: radf2(F.ido, l1l, cur, nxt, wa, qk, DP); break;
-          case 3: radf3(F.ido, l1l, cur, nxt, wa, qk, DP); break;
-          default: radf5(F.ido, l1l, cur, nxt, wa, qk, DP); break;
+          case 4: radf4(F.ido, l1l, cur, nxt, wa, qk, DP, F.dv); break;
+          case 2: radf2(F.ido, l1l, cur, nxt, wa, qk, DP, F.dv); break;
+          case 3: radf3(F.ido, l1l, cur, nxt, wa, qk, DP, F.dv); break;
+          default: radf5(F.ido, l1l, cur, nxt, wa, qk, DP, F.dv); break;
         }
         __syncthreads();
         double* t = cur;

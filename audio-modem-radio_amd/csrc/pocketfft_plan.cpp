@@ -203,6 +203,18 @@ void build_groups(PfPasses& P) {
       G.Qi = (int)G.D;
       G.Qk = (int)(G.Q / G.D);
     }
+    const int64_t nti = (G.D + G.Qi - 1) / G.Qi, ntk = (G.L + G.Qk - 1) / G.Qk;
+    G.dv[0] = pf_div(G.P);
+    G.dv[1] = pf_div(G.Q);
+    G.dv[2] = pf_div(G.Qi);
+    G.dv[3] = pf_div(G.D - (nti - 1) * G.Qi);
+    G.dv[4] = pf_div(G.Qk);
+    G.dv[5] = pf_div(G.L - (ntk - 1) * G.Qk);
+    G.dv[6] = pf_div(nti);
+    for (int q = G.f0; q < G.f0 + G.nf; ++q) {
+      P.f[q].dv[0] = pf_div(P.f[q].ido / G.D);
+      P.f[q].l1l = (int32_t)(P.f[q].l1 / G.L);
+    }
   }
   P.fused = 1;
 }
@@ -270,6 +282,29 @@ void build_rgroups(PfPasses& P) {
       G.Q = 2;
       G.Qi = 0;
       G.Qk = (int)(kPfTileDoubles / (4 * G.P));   // T: pair classes per tile (<= 4 T residues)
+      {
+        // R (and R / 2) of the special tile {0, D - 1}, a full tile (4 T
+        // residues, or 4 T - 2 when it ends on the self-paired p = D / 4) and
+        // the last tile
+        const int64_t H = D / 2, pmax = H / 2, T = G.Qk, nt = (pmax + T - 1) / T;
+        auto rtile = [&](int64_t tile) {
+          const int64_t p0 = 1 + (tile - 1) * T, p1 = std::min(p0 + T, pmax + 1);
+          const int64_t pe = (2 * (p1 - 1) == H) ? p1 - 1 : p1;
+          return 2 * (p1 - p0) + 2 * (pe - p0);
+        };
+        G.dv[0] = pf_div(2);
+        G.dv[1] = pf_div(1);
+        G.dv[2] = pf_div(nt >= 1 ? rtile(1) : 2);
+        G.dv[3] = pf_div(nt >= 1 ? rtile(1) / 2 : 1);
+        G.dv[4] = pf_div(nt >= 1 ? rtile(nt) : 2);
+        G.dv[5] = pf_div(nt >= 1 ? rtile(nt) / 2 : 1);
+        int64_t B = 1;
+        for (int q = k; q >= 0; --q) {
+          P.f[q].dv[0] = pf_div(B);
+          P.f[q].dv[1] = pf_div(B + 1);
+          B *= P.f[q].ip;
+        }
+      }
       k = -1;
       break;
     }
@@ -286,6 +321,17 @@ void build_rgroups(PfPasses& P) {
     if (hard && D * G.P * qmin <= kPfTileDoubles) {
       G.Q = 1;
       G.Qk = (int)std::min<int64_t>(G.L, kPfTileDoubles / (D * G.P));
+      const int64_t ntk = (G.L + G.Qk - 1) / G.Qk;
+      G.dv[0] = pf_div(D);
+      G.dv[1] = pf_div(G.Qk);
+      G.dv[2] = pf_div(G.L - (ntk - 1) * G.Qk);
+      for (int q = G.f0; q > G.f0 - G.nf; --q) {
+        const int64_t l1l = P.f[q].l1 / G.L, hi = (P.f[q].ido - 1) / 2;
+        P.f[q].dv[0] = pf_div(l1l);
+        P.f[q].dv[1] = pf_div(hi);
+        P.f[q].dv[2] = pf_div(l1l * hi);
+        P.f[q].l1l = (int32_t)l1l;
+      }
     } else {
       G.Q = 0;
       G.Qk = 0;
