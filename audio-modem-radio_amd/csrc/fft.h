@@ -100,10 +100,6 @@ hipError_t fft_configure_smem();
 // six-step transpose (+ twiddle W_M^(r c) from tw_lo/tw_hi, conjugated when inverse)
 hipError_t launch_transpose(const double2* in, double2* out, int64_t R, int64_t C, int64_t batch,
                             const double2* tw_lo, const double2* tw_hi, bool inverse, hipStream_t st);
-// scipy.signal.resample's spectrum surgery and final scaling (fsk_api.cpp amr_resample_host)
-hipError_t launch_resample_spec(const double2* X, double2* Yf, int64_t nx, int64_t num, int64_t batch,
-                                hipStream_t st);
-hipError_t launch_real_scale(const double2* Y, double* y, int64_t tot, double scale, hipStream_t st);
 
 // Compare bits of a length-n filter output: sample k = r + rn1*kk (r < rn1,
 // kk < rn2) is bit (r & 7) of byte (r >> 3)*rn2 + kk -- the order in which a

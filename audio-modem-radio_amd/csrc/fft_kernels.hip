@@ -962,52 +962,6 @@ hipError_t launch_transpose(const double2* in, double2* out, int64_t R, int64_t 
   return hipGetLastError();
 }
 
-// ---- scipy.signal.resample (real input, axis 0), signaltools.py ------------
-// X = FFT_nx(x) -> the full Hermitian spectrum of irfft(Y, num): Y[k] = X[k]
-// for k < nyq = min(num, nx)//2 + 1, zero above; the Nyquist bin of an even
-// N = min(num, nx) doubled (down) / halved (up); the imaginary parts irfft
-// ignores (k = 0, k = num/2) dropped; Yf[num - k] = conj(Yf[k]).
-__global__ __launch_bounds__(256) void k_resample_spec(const double2* __restrict__ X, double2* __restrict__ Yf,
-                                                       int64_t nx, int64_t num, int64_t batch) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= batch * num) return;
-  const int64_t b = i / num, k = i - b * num;
-  const int64_t h = k <= num / 2 ? k : num - k;                 // the rfft bin this output bin mirrors
-  const int64_t N = num < nx ? num : nx;
-  const int64_t nyq = N / 2 + 1;
-  double2 v = make_double2(0.0, 0.0);
-  if (h < nyq) {
-    v = X[(size_t)b * nx + h];
-    if ((N & 1) == 0 && h == N / 2) {
-      if (num < nx) v = make_double2(v.x * 2.0, v.y * 2.0);
-      else if (nx < num) v = make_double2(v.x * 0.5, v.y * 0.5);
-    }
-  }
-  if (h == 0 || 2 * h == num) v.y = 0.0;
-  if (k != h) v.y = -v.y;
-  Yf[i] = v;
-}
-
-// y = Re(IFFT_num(Yf)) * (num / nx)   (y *= float(num) / float(Nx))
-__global__ __launch_bounds__(256) void k_real_scale(const double2* __restrict__ Y, double* __restrict__ y, int64_t tot,
-                                                    double scale) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < tot) y[i] = Y[i].x * scale;
-}
-
-hipError_t launch_resample_spec(const double2* X, double2* Yf, int64_t nx, int64_t num, int64_t batch,
-                                hipStream_t st) {
-  const int64_t tot = batch * num;
-  if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_resample_spec, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, X, Yf, nx, num, batch);
-  return hipGetLastError();
-}
-
-hipError_t launch_real_scale(const double2* Y, double* y, int64_t tot, double scale, hipStream_t st) {
-  if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_real_scale, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, Y, y, tot, scale);
-  return hipGetLastError();
-}
 
 template <int P, int Q>
 static hipError_t fft_set_smem(int bytes) {
