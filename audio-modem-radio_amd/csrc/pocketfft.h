@@ -7,7 +7,8 @@
 // The algorithm is the one oracle/amr_pocketfft.c restates and pins bit for bit
 // against scipy on every length 1..2000 (tests/test_oracle_golden.py); the
 // plans here are built on the host by the same rules (pocketfft_plan.cpp) and
-// executed by pocketfft_dev.h, one workgroup per transform.
+// executed by pocketfft_dev.h, one workgroup per transform, consecutive passes
+// fused through LDS tiles where the plan's groups allow.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,15 +17,12 @@
 
 namespace amr {
 
-constexpr int kPfMaxF = 32;
+constexpr int kPfMaxF = 32;   // factors of one plan (a length < 2^31 has at most 30)
 constexpr int64_t kPfMaxLen = (int64_t)1 << 27;   // longest row the device transforms take
 // a real row's doubles rounded up to even: complex scratch placed after a row
 // stays 16-byte aligned (pocketfft_dev.h Cx is loaded and stored as one b128)
-__host__ __device__ inline int64_t pf_even(int64_t n) { return (n + 1) & ~(int64_t)1; }   // factors of one plan (a length < 2^31 has at most 30)
+__host__ __device__ inline int64_t pf_even(int64_t n) { return (n + 1) & ~(int64_t)1; }
 
-// one factor of a plan: radix ip, l1 = product of the factors before it,
-// ido = len / (l1 * ip); tw / tws: offsets (in doubles) of its twiddles and of
-// the generic passes' extra table in the plan's pool, -1 when absent
 // x / d for 0 <= x < 2^31 by multiply-high (pocketfft_dev.h FDiv): m =
 // floor(2^32 (2^l - d) / d) + 1, l = ceil(log2 d); built on the host for every
 // divisor the fused tile loops use, so no division is emulated on the device
@@ -41,6 +39,9 @@ inline PfDiv pf_div(int64_t d) {
   return r;
 }
 
+// one factor of a plan: radix ip, l1 = product of the factors before it,
+// ido = len / (l1 * ip); tw / tws: offsets (in doubles) of its twiddles and of
+// the generic passes' extra table in the plan's pool, -1 when absent.
 // dv: the pass's divisors inside its fused group -- complex: [0] ido / D;
 // real blocks: [0] l1 / L, [1] (ido - 1) / 2, [2] their product; real pair
 // tiles: [0] B = ido / D, [1] B + 1

@@ -4,12 +4,17 @@
 // scipy.fft's (oracle/amr_pocketfft.c is the CPU statement of the same
 // algorithm, pinned against scipy; tests/test_gpu_pocketfft.py pins these).
 //
-// Each routine is run by ONE whole workgroup over global scratch: a pass
-// spreads its independent butterflies (pocketfft's (k, i) loop nests) over
-// the workgroup's threads, passes are separated by barriers, and the generic
-// passes (radfg / radbg / passg) run their phases between barriers, each
-// thread owning the accumulation chains of its outputs (so their order is
-// pocketfft's).  Every thread of the workgroup must call these.
+// Each routine is run by ONE whole workgroup.  Pass by pass over global
+// scratch: a pass spreads its independent butterflies (pocketfft's (k, i)
+// loop nests) over the workgroup's threads, passes are separated by barriers,
+// and the generic passes (radfg / radbg / passg) run their phases between
+// barriers, each thread owning the accumulation chains of its outputs (so
+// their order is pocketfft's).  Fused (the plans' groups, pocketfft.h): runs
+// of consecutive passes go through LDS tiles that are closed under those
+// passes' data flow -- cgroup (complex), rfftp_fwd_fused's blocks and
+// rgroup_pairs' residue-pair tiles (real forward) -- calling the same
+// butterflies, so every value is computed by the same operations.  Every
+// thread of the workgroup must call these.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
