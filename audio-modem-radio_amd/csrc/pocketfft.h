@@ -60,6 +60,9 @@ struct PfFact {
 // order, as the passes run one by one over the whole array.
 constexpr int kPfTileElems = 2048;   // complex elements per LDS buffer (32 KiB; two buffers)
 constexpr int kPfMaxGroupP = 512;    // radix product of a group (>= 4 columns per tile)
+// a two-group complex plan's hand-off rows (D >= kPfPadMinD complex) padded to
+// whole kPfPadC-complex (128-byte) lines where the caller has the room
+constexpr int kPfPadC = 8, kPfPadMinD = 64;
 // rfftp forward (r2hc) groups, in executed order (ido growing): passes
 // f0, f0 - 1, ..., f0 - nf + 1; D = the first one's ido, L = the last one's l1;
 // a multi-pass group couples every residue mod D, so a tile is Qk whole
@@ -79,7 +82,7 @@ struct PfGroup {
   int f0, nf;
   int64_t P, D, L;
   int Q, Qi, Qk;
-  PfDiv dv[7];   // (complex: [6] the i-tile count, for the tile index split)
+  PfDiv dv[8];   // (complex: [6] the i-tile count, for the tile index split; [7] D)
 };
 
 // an FFTPACK-style plan (pocketfft's cfftp or rfftp); fused: the passes are

@@ -546,8 +546,10 @@ struct WrBuf {
 // handed to fin(pos, v) (unscaled); A, B: len complex of scratch each.  src
 // may read A (not B); fin must not write B.  Fused plans run group by group
 // (the last one reads B); others materialise src into A, run the passes and
-// hand A's entries to fin.
-template <bool FWD, class Src, class Fin, bool LEAN = false>
+// hand A's entries to fin.  PADB: a two-group plan whose src does not read A
+// may run B past len (up to len + len / 8, over A's start): its hand-off rows
+// are then padded to whole 128-byte lines.
+template <bool FWD, class Src, class Fin, bool LEAN = false, bool PADB = false>
 __device__ __forceinline__ void cfftp_x(const PfPasses& P, const double* pool, Src src, Cx* A, Cx* B, Fin fin, Cx* lds) {
   const int len = P.len;
   if (!LEAN && (!P.fused || lds == nullptr)) {
@@ -561,6 +563,16 @@ __device__ __forceinline__ void cfftp_x(const PfPasses& P, const double* pool, S
   const int G = P.ng;
   if (G == 1) {   // one group of one tile: every load precedes every store
     cgroup<FWD>(P, P.g[0], pool, src, fin, lds);
+    return;
+  }
+  if (PADB && G == 2 && P.g[0].D >= kPfPadMinD) {
+    // group 0's output rows (position p = i + D j, i < D) at i + Dp j, Dp =
+    // D rounded up to whole lines: its tiles store line-aligned runs, and
+    // group 1 (D = 1) still reads each row as one contiguous run
+    const FDiv fD(P.g[0].dv[7]);
+    const int pad = (kPfPadC - fD.d % kPfPadC) % kPfPadC;
+    cgroup<FWD>(P, P.g[0], pool, src, [=](int p, Cx v) { B[p + fD.div(p) * pad] = v; }, lds);
+    cgroup<FWD>(P, P.g[1], pool, [=](int p) { return B[p + fD.div(p) * pad]; }, fin, lds);
     return;
   }
   // outputs: group G-2 -> B, G-3 -> A, ...
@@ -1719,7 +1731,9 @@ __device__ __forceinline__ void pf_hilbert_env_x(const PfLen& L, const double* p
     const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
     fin(i, h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0)));
   };
-  cfftp_x<false, decltype(spec), decltype(envf), LEAN>(L.c, pool, spec, s.x, reinterpret_cast<Cx*>(s.a), envf, lds);
+  // (spec reads f only: B = s.a may pad over s.x)
+  cfftp_x<false, decltype(spec), decltype(envf), LEAN, true>(L.c, pool, spec, s.x, reinterpret_cast<Cx*>(s.a), envf,
+                                                             lds);
 }
 
 // The two halves of pf_hilbert_env_x as the bodies of two lean kernels (one
@@ -1752,8 +1766,9 @@ __device__ __forceinline__ void pf_env_row(const PfLen& L, const double* pool, F
     const double h = ar > ai ? ar : ai, l = ar > ai ? ai : ar;
     fin(i, h == 0.0 ? 0.0 : h * __builtin_sqrt(__builtin_fma(l / h, l / h, 1.0)));
   };
-  cfftp_x<false, decltype(spec), decltype(envf), true>(L.c, pool, spec, reinterpret_cast<Cx*>(slot),
-                                                       reinterpret_cast<Cx*>(slot + 2 * (size_t)n), envf, lds);
+  // (B = slot + 2n pads into the slot's tail, >= n doubles past 4n)
+  cfftp_x<false, decltype(spec), decltype(envf), true, true>(L.c, pool, spec, reinterpret_cast<Cx*>(slot),
+                                                             reinterpret_cast<Cx*>(slot + 2 * (size_t)n), envf, lds);
 }
 
 #undef PF_FOR

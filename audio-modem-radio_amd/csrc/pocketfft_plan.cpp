@@ -211,6 +211,7 @@ void build_groups(PfPasses& P) {
     G.dv[4] = pf_div(G.Qk);
     G.dv[5] = pf_div(G.L - (ntk - 1) * G.Qk);
     G.dv[6] = pf_div(nti);
+    G.dv[7] = pf_div(G.D);
     for (int q = G.f0; q < G.f0 + G.nf; ++q) {
       P.f[q].dv[0] = pf_div(P.f[q].ido / G.D);
       P.f[q].l1l = (int32_t)(P.f[q].l1 / G.L);
