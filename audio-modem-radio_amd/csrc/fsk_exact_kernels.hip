@@ -155,13 +155,23 @@ __device__ inline ZRow<LIVE> zrow(const FskParams& p, const FskExact& X, int64_t
   return ZRow<LIVE>{X.rows + (size_t)s * 2 * p.n + (r & 1), X.lc};
 }
 
+// the first row of workgroup b: with a grid of whole XCD rounds (workgroup b
+// on XCD b % 8), rows 2q and 2q + 1 -- the two tones of one stream, each 8
+// bytes of every 16-byte z element -- go to workgroups b and b + 8 of the
+// same XCD, so both halves of z's lines meet in one L2
+__device__ inline int64_t exact_row0(const FskExact& X) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (!X.xcd_pair || G % 16 != 0) return b;
+  return (int64_t)(b % 8) * (G / 8) + b / 8;
+}
+
 template <bool LIVE>
 __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_exact_rfft(FskParams p,
                                                                                                      FskExact X) {
   __shared__ pf::Cx lds[2 * kPfTileElems];
   const int64_t cnt = *X.count;
   double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
-  for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+  for (int64_t r = exact_row0(X); r < 2 * cnt; r += gridDim.x) {
     const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
     // the halfcomplex spectrum parked in natural order (the row's z elements
     // are free once the first group has read them)
@@ -177,7 +187,7 @@ __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ pf::Cx lds[2 * kPfTileElems];
   const int64_t cnt = *X.count;
   double* slot = X.slots + (size_t)blockIdx.x * X.slot_doubles;
-  for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+  for (int64_t r = exact_row0(X); r < 2 * cnt; r += gridDim.x) {
     const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
     auto fget = [=](int j) { return z.zr[2 * (int64_t)j]; };
     if (LIVE) {   // envelopes in natural order too, the live samples only (E3 reads no others)
