@@ -480,6 +480,8 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.lean = X.fuse && pl->x_lean;
   static const int xcd_pair = [] { const char* e = std::getenv("AMR_FSK_XCDPAIR"); return !(e && e[0] == '0'); }();
   X.xcd_pair = xcd_pair;
+  static const int live_only = [] { const char* e = std::getenv("AMR_FSK_LIVEONLY"); return !(e && e[0] == '0'); }();
+  X.live_only = live_only;
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
   pl->ran_exact = true;
   HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));

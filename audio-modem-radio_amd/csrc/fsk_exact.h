@@ -25,6 +25,7 @@ struct FskExact {
   uint8_t* xbits;          // [B][bits_stride] exact compare bits, F3 reads them for flagged streams
   int fuse;                // LDS-fused transforms (pf_fuse_on)
   int lean;                // ... and every radix hard-coded: k_exact_env_lean
+  int live_only;           // E2b stores only the live samples' envelopes (AMR_FSK_LIVEONLY=0: every sample, A/B)
   int xcd_pair;            // E2 rows of one stream on one XCD (AMR_FSK_XCDPAIR=0: off, A/B)
   // live (the plan's keep_z): rows is z itself, stream-indexed in the [L | D]
   // layout lc, whole after F2 -- no F1 re-run; the envelopes go back into z's

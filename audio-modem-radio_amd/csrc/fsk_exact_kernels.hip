@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kEnvThreads) __attribute__((amdgpu_waves_per_eu(4))
   for (int64_t r = exact_row0(X); r < 2 * cnt; r += gridDim.x) {
     const ZRow<LIVE> z = zrow<LIVE>(p, X, r);
     auto fget = [=](int j) { return z.zr[2 * (int64_t)j]; };
-    if (LIVE) {   // envelopes in natural order too, the live samples only (E3 reads no others)
+    if (LIVE && X.live_only) {   // envelopes in natural order too, the live samples only (E3 reads no others)
       const LiveCols lc = z.lc;
       pf::pf_env_row(
           *X.L, X.pool, fget,
