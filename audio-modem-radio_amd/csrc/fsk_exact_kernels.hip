@@ -106,6 +106,16 @@ __global__ __launch_bounds__(kListThreads) void k_exact_list(const uint32_t* __r
   if (threadIdx.x == kListThreads - 1) *count = part[threadIdx.x];
 }
 
+// the first row of workgroup b: with a grid of whole XCD rounds (workgroup b
+// on XCD b % 8), rows 2q and 2q + 1 -- the two tones of one stream, each 8
+// bytes of every 16-byte z element -- go to workgroups b and b + 8 of the
+// same XCD, so both halves of z's lines meet in one L2
+__device__ inline int64_t exact_row0(const FskExact& X) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (!X.xcd_pair || G % 16 != 0) return b;
+  return (int64_t)(b % 8) * (G / 8) + b / 8;
+}
+
 // E2: workgroup = row r = 2q + tone: the tone's band-pass output (F1 in list
 // mode left ordinal q's z row = f_mark + i f_space) -> the slot, |hilbert| of
 // it, back into the same interleaved positions of z
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
   const int64_t n = p.n;
   double* c = X.slots + (size_t)blockIdx.x * X.slot_doubles;
   if (X.fuse && pf_hilbert_fusable(*X.L)) {   // straight from z and back, every transform in LDS tiles
-    for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+    for (int64_t r = exact_row0(X); r < 2 * cnt; r += gridDim.x) {
       double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
       pf::pf_hilbert_env_x(
           *X.L, X.pool, [=](int64_t i) { return zr[2 * i]; }, [=](int64_t i, double e) { zr[2 * i] = e; }, c, X.fct,
@@ -124,7 +134,7 @@ __global__ __launch_bounds__(kEnvThreads) void k_exact_env(FskParams p, FskExact
     }
     return;
   }
-  for (int64_t r = blockIdx.x; r < 2 * cnt; r += gridDim.x) {
+  for (int64_t r = exact_row0(X); r < 2 * cnt; r += gridDim.x) {
     double* zr = X.rows + (size_t)(r >> 1) * 2 * n + (r & 1);
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) c[i] = zr[2 * i];
     __syncthreads();
@@ -153,16 +163,6 @@ template <bool LIVE>
 __device__ inline ZRow<LIVE> zrow(const FskParams& p, const FskExact& X, int64_t r) {
   const int64_t s = LIVE ? (int64_t)X.list[r >> 1] : (r >> 1);
   return ZRow<LIVE>{X.rows + (size_t)s * 2 * p.n + (r & 1), X.lc};
-}
-
-// the first row of workgroup b: with a grid of whole XCD rounds (workgroup b
-// on XCD b % 8), rows 2q and 2q + 1 -- the two tones of one stream, each 8
-// bytes of every 16-byte z element -- go to workgroups b and b + 8 of the
-// same XCD, so both halves of z's lines meet in one L2
-__device__ inline int64_t exact_row0(const FskExact& X) {
-  const int G = gridDim.x, b = blockIdx.x;
-  if (!X.xcd_pair || G % 16 != 0) return b;
-  return (int64_t)(b % 8) * (G / 8) + b / 8;
 }
 
 template <bool LIVE>
