@@ -349,6 +349,8 @@ struct amr_fsk_plan {
   uint32_t* xflags = nullptr;  // [B / 32] F2's flags, bit s of word s / 32 (cleared by F1 every batch)
   double* amb = nullptr;       // [B] F1's ambiguity scale per stream
   int32_t* xlist = nullptr;    // [B] flagged ordinal -> stream, then [1] the count
+  int32_t* xcount_host = nullptr;   // host-mapped: the count E3 last saw (FskExact count_hint)
+  int32_t* xcount_dev = nullptr;    // its device pointer
   double* xslots = nullptr;    // [n_slots][slot_doubles] envelope scratch
   uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
   double* xpool = nullptr;     // pocketfft's twiddle / chirp tables of length n
@@ -378,6 +380,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   (void)hipSetDevice(pl->device);
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
+  if (pl->xcount_host) (void)hipHostFree(pl->xcount_host);
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
                   (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL})
@@ -482,6 +485,8 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.xcd_pair = xcd_pair;
   static const int live_only = [] { const char* e = std::getenv("AMR_FSK_LIVEONLY"); return !(e && e[0] == '0'); }();
   X.live_only = live_only;
+  X.count_host = pl->xcount_dev;
+  X.count_hint = pl->xcount_host ? (int64_t)*reinterpret_cast<volatile int32_t*>(pl->xcount_host) : B;
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
   pl->ran_exact = true;
   HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));
@@ -786,6 +791,16 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->scratch_bytes += a.bytes;
   }
   if (geo.exact) {
+    // E2's grid hint (FskExact count_hint): none yet, so the full grid
+    e = hipHostMalloc((void**)&pl->xcount_host, sizeof(int32_t), hipHostMallocMapped);
+    if (e == hipSuccess) {
+      *pl->xcount_host = (int32_t)max_streams;
+      e = hipHostGetDevicePointer((void**)&pl->xcount_dev, pl->xcount_host, 0);
+    }
+    if (e != hipSuccess) {
+      fsk_plan_free(pl);
+      return fail(AMR_E_NOMEM, std::string("hipHostMalloc (exact-path count hint): ") + hipGetErrorString(e));
+    }
     // pocketfft's plans of length n: tables to the device, then the Bluestein
     // tables that need a device transform (into the envelope slots' scratch)
     std::vector<double> pool;

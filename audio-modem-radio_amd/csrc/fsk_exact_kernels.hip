@@ -217,6 +217,7 @@ __global__ __launch_bounds__(kBitsThreads) void k_exact_bits(FskParams p, FskExa
   const int ncol = p.lc.on ? p.lc.nl : (int)p.rn1;
   const int64_t n2 = p.rn2, n1 = p.lc.on ? p.lc.n1 : p.rn1;
   const int64_t nbytes = (int64_t)((ncol + 7) >> 3) * n2;
+  if (X.count_host && blockIdx.x == 0 && threadIdx.x == 0) *X.count_host = (int32_t)cnt;
   for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {
     const int64_t st = X.list[q];
     // (env_mark, env_space) in natural sample order: z of stream st (live
@@ -259,7 +260,12 @@ hipError_t launch_fsk_exact_env(int64_t B, const FskParams& p, const FskExact& X
   };
   static const int res_full = resident((const void*)k_exact_env),
                    res_lean = std::min(resident((const void*)k_exact_rfft<true>), resident((const void*)k_exact_cenv<true>));
-  const dim3 gl((unsigned)std::min(X.n_slots, res_lean));
+  // (FskExact count_hint) two rows per stream, whole XCD rounds of 16, at
+  // least kIdleGrid; AMR_FSK_E2_GRID=G (A/B): at most G workgroups
+  static const int e2_grid = [] { const char* e = std::getenv("AMR_FSK_E2_GRID"); return e ? std::max(1, atoi(e)) : 1 << 30; }();
+  constexpr int64_t kIdleGrid = 16;
+  const int64_t want = std::max(kIdleGrid, (2 * std::max<int64_t>(X.count_hint, 0) + 15) / 16 * 16);
+  const dim3 gl((unsigned)std::min<int64_t>({X.n_slots, res_lean, e2_grid, want}));
   if (!env) {
     // (diagnostic: the envelope kernels skipped)
   } else if (X.live) {   // the plan guarantees a lean plan (fsk_api.cpp keep_z)
