@@ -351,6 +351,21 @@ struct amr_fsk_plan {
   int32_t* xlist = nullptr;    // [B] flagged ordinal -> stream, then [1] the count
   int32_t* xcount_host = nullptr;   // host-mapped: the count E3 last saw (FskExact count_hint)
   int32_t* xcount_dev = nullptr;    // its device pointer
+  // E0-E3 on a stream of their own at the device's highest priority, ordered
+  // by events after F2 and before F3 (AMR_FSK_XSTREAM=0: on the plan's
+  // stream): an exact-path workgroup needs 64 KiB of LDS, and from a
+  // high-priority queue it takes the next CU that frees that much ahead of
+  // the other launches in flight, so the full resident grid can be launched
+  // every batch (a burst of flagged streams after clean batches gets all of
+  // it) without the idle launches waiting behind the FFT passes
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_f2 = nullptr, ev_x = nullptr;
+  // the counts E3 reported before the last kHintDepth launches:
+  // E2's grid follows their maximum, so one clean batch between flagged ones
+  // does not shrink the grid of the next flagged batch to kIdleGrid
+  static constexpr int kHintDepth = 8;
+  int32_t hint_hist[kHintDepth]{};
+  int hint_pos = 0;
   double* xslots = nullptr;    // [n_slots][slot_doubles] envelope scratch
   uint8_t* xbits = nullptr;    // [B][bits_stride] the flagged streams' exact compare bits
   double* xpool = nullptr;     // pocketfft's twiddle / chirp tables of length n
@@ -389,14 +404,18 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   for (auto& e : pl->ev)
     for (auto& h : e)
       if (h) (void)hipEventDestroy(h);
+  if (pl->xstream) (void)hipStreamSynchronize(pl->xstream);
+  if (pl->ev_f2) (void)hipEventDestroy(pl->ev_f2);
+  if (pl->ev_x) (void)hipEventDestroy(pl->ev_x);
+  if (pl->xstream) (void)hipStreamDestroy(pl->xstream);
   if (pl->stream) (void)hipStreamDestroy(pl->stream);
   delete pl;
 }
 
-hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which) {
+hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which, hipStream_t st = nullptr) {
   if (!pl->timing) return hipSuccess;
   pl->ev_used[slot] = true;
-  return hipEventRecord(pl->ev[slot][which], pl->stream);
+  return hipEventRecord(pl->ev[slot][which], st ? st : pl->stream);
 }
 
 // F1 over the B streams of x -> z (and, with the exact path on, each
@@ -456,14 +475,20 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
   return AMR_OK;
 }
 
+// AMR_FSK_EXACT_LAUNCH=0 (diagnostic A/B only, decisions then NOT exact):
+// F1 / F2 keep their margin work, the E0-E3 launches are skipped (=2: E0 and
+// E3 only, E2 skipped).  Either way F3 then takes every stream's bits from the
+// fast path (run_fsk_back), not from an xbits buffer E2 / E3 never filled.
+int exact_launch_mode() {
+  static const int launch = [] { const char* e = std::getenv("AMR_FSK_EXACT_LAUNCH"); return e ? atoi(e) : 1; }();
+  return launch;
+}
+
 // The exact path over F2's flagged streams: with keep_z straight from z (F2
 // left it whole), otherwise F1 again over their input x (still resident).
 int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride) {
   if (!pl->exact_on || pl->exact_mode == 0) return AMR_OK;
-  // AMR_FSK_EXACT_LAUNCH=0 (diagnostic A/B only, decisions then NOT exact):
-  // F1 / F2 keep their margin work, the E0-E3 launches are skipped
-  // (=2: E0 and E3 only, E2 skipped)
-  static const int launch = [] { const char* e = std::getenv("AMR_FSK_EXACT_LAUNCH"); return e ? atoi(e) : 1; }();
+  const int launch = exact_launch_mode();
   if (launch == 0) return AMR_OK;
   FskExact X{};
   X.flags = pl->xflags;
@@ -486,10 +511,24 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   static const int live_only = [] { const char* e = std::getenv("AMR_FSK_LIVEONLY"); return !(e && e[0] == '0'); }();
   X.live_only = live_only;
   X.count_host = pl->xcount_dev;
-  X.count_hint = pl->xcount_host ? (int64_t)*reinterpret_cast<volatile int32_t*>(pl->xcount_host) : B;
-  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0));
+  if (pl->xstream) {
+    X.count_hint = B;                                   // the full resident grid (see xstream)
+  } else if (pl->xcount_host) {
+    pl->hint_hist[pl->hint_pos] = *reinterpret_cast<volatile int32_t*>(pl->xcount_host);
+    pl->hint_pos = (pl->hint_pos + 1) % amr_fsk_plan::kHintDepth;
+    X.count_hint = *std::max_element(pl->hint_hist, pl->hint_hist + amr_fsk_plan::kHintDepth);
+  } else {
+    X.count_hint = B;
+  }
+  hipStream_t st = pl->stream;
+  if (pl->xstream) {
+    HIP_TRY(hipEventRecord(pl->ev_f2, pl->stream));
+    HIP_TRY(hipStreamWaitEvent(pl->xstream, pl->ev_f2, 0));
+    st = pl->xstream;
+  }
+  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0, st));
   pl->ran_exact = true;
-  HIP_TRY(launch_fsk_exact_list(B, X, pl->stream));
+  HIP_TRY(launch_fsk_exact_list(B, X, st));
   if (!pl->keep_z) {
     // E1: F1 again over the flagged streams only (list mode), natural z layout
     FskParams p1 = pl->p;
@@ -497,11 +536,14 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     p1.lc = LiveCols{};
     p1.xlist = X.list;
     p1.xcount = X.count;
-    HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f,
-                                pl->stream));
+    HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f, st));
   }
-  HIP_TRY(launch_fsk_exact_env(B, pl->p, X, pl->stream, launch != 2));
-  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1));
+  HIP_TRY(launch_fsk_exact_env(B, pl->p, X, st, launch != 2));
+  HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1, st));
+  if (pl->xstream) {
+    HIP_TRY(hipEventRecord(pl->ev_x, pl->xstream));
+    HIP_TRY(hipStreamWaitEvent(pl->stream, pl->ev_x, 0));
+  }
   return AMR_OK;
 }
 
@@ -535,7 +577,12 @@ int fsk_empty_outputs(amr_fsk_plan* pl, int64_t B, int64_t* d_len, int64_t* d_sy
 int run_fsk_back(amr_fsk_plan* pl, int64_t B, uint8_t* d_out, int64_t out_stride, int64_t* d_len, int64_t* d_sync) {
   hipStream_t st = pl->stream;
   HIP_TRY(mark_fsk(pl, AMR_TF_DECIDE, 0));
-  HIP_TRY(launch_fsk_decide(pl->cmp, pl->words, B, pl->p, st));
+  // a flagged stream's bits come from xbits only when this call's E0-E3 wrote
+  // them (exact mode 0 leaves the flag words of an earlier call untouched;
+  // the diagnostic launch modes leave xbits unwritten)
+  FskParams p = pl->p;
+  if (!pl->ran_exact || exact_launch_mode() != 1) p.xflags = nullptr;
+  HIP_TRY(launch_fsk_decide(pl->cmp, pl->words, B, p, st));
   HIP_TRY(gate_wait(pl->gate, st));             // the outputs: after any gather still reading them
   HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
   HIP_TRY(mark_fsk(pl, AMR_TF_DECIDE, 1));
@@ -694,7 +741,13 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
     // live layout: keep all of z through F2 (the exact path then needs no F1
     // re-run); the dead tiles' transform and the staged input go to dd
     // (AMR_FSK_KEEPZ=0, an A/B switch: dead tiles in place, the F1 re-run)
-    static const bool keepz_env = [] { const char* e = std::getenv("AMR_FSK_KEEPZ"); return !(e && e[0] == '0'); }();
+    // (AMR_FSK_F1_FMA=1 makes F1 the contracted form, not scipy's order: the
+    // exact path must then re-run F1 in scipy's order, so no keep_z)
+    static const bool keepz_env = [] {
+      const char* e = std::getenv("AMR_FSK_KEEPZ");
+      const char* f = std::getenv("AMR_FSK_F1_FMA");
+      return !(e && e[0] == '0') && !(f && f[0] == '1');
+    }();
     g.keep_z = keepz_env && p.lc.on && (int64_t)p.lc.nd * p.lc.n2 * 2 >= n;
     if (g.keep_z) {
       g.dd = max_streams * (int64_t)p.lc.nd * p.lc.n2 * 16;
@@ -795,6 +848,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     e = hipHostMalloc((void**)&pl->xcount_host, sizeof(int32_t), hipHostMallocMapped);
     if (e == hipSuccess) {
       *pl->xcount_host = (int32_t)max_streams;
+      for (int32_t& h : pl->hint_hist) h = (int32_t)max_streams;
       e = hipHostGetDevicePointer((void**)&pl->xcount_dev, pl->xcount_host, 0);
     }
     if (e != hipSuccess) {
@@ -831,6 +885,18 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->p.xbits = pl->xbits;
     pl->n_slots = geo.n_slots;
     pl->slot_doubles = geo.slot_doubles;
+    static const bool xstream_on = [] { const char* e = std::getenv("AMR_FSK_XSTREAM"); return !(e && e[0] == '0'); }();
+    if (xstream_on) {
+      int least = 0, greatest = 0;
+      e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+      if (e == hipSuccess) e = hipStreamCreateWithPriority(&pl->xstream, hipStreamNonBlocking, greatest);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&pl->ev_f2, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&pl->ev_x, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        fsk_plan_free(pl);
+        return fail(AMR_E_HIP, std::string("exact-path stream: ") + hipGetErrorString(e));
+      }
+    }
   }
   *out = pl;
   return AMR_OK;

@@ -28,10 +28,11 @@ struct FskExact {
   int live_only;           // E2b stores only the live samples' envelopes (AMR_FSK_LIVEONLY=0: every sample, A/B)
   int xcd_pair;            // E2 rows of one stream on one XCD (AMR_FSK_XCDPAIR=0: off, A/B)
   // E2's grid: the persistent loops are correct at any size, so it is sized
-  // from the count an earlier launch on this plan saw (count_hint, which E3
-  // writes to count_host, host-mapped) -- a few workgroups when nothing was
-  // flagged, which then dispatch and exit without waiting for room beside the
-  // other launches in flight; the full resident grid otherwise
+  // from the counts the plan's last 8 launches saw (count_hint = their
+  // maximum; E3 writes each to count_host, host-mapped) -- a few workgroups
+  // after a run of clean batches, which then dispatch and exit without
+  // waiting for room beside the other launches in flight; the full resident
+  // grid while flagged batches keep coming
   int32_t* count_host;     // device pointer of a host-mapped int, or nullptr
   int64_t count_hint;
   // live (the plan's keep_z): rows is z itself, stream-indexed in the [L | D]

@@ -10,13 +10,17 @@
 // recomputes the flagged streams' compare bits the reference's own way, bit
 // for bit, at any length:
 //   E0 k_exact_list      flag words -> list of flagged streams (ordinals)
-//   E1 F1 in list mode   the flagged streams' band-pass filtfilt again
-//                        (fsk_kernels.hip k_fsk_bandpass2: scipy's order, so
-//                        f is the reference's), z row q = ordinal q's
-//                        f_mark + i f_space -- F2 has consumed z by now
-//   E2 k_exact_env       workgroup = row (q, tone): |scipy.signal.hilbert(f)|
-//                        as pocketfft + numpy evaluate it (pocketfft_dev.h,
-//                        every radix and Bluestein), back into z
+//   E1 F1 in list mode   only on plans without keep_z (the natural layout, or
+//                        AMR_FSK_KEEPZ=0): the flagged streams' band-pass
+//                        filtfilt again (fsk_kernels.hip k_fsk_bandpass2,
+//                        scipy's order), z row q = ordinal q's f_mark + i
+//                        f_space, because F2 transformed z's dead tiles in
+//                        place.  With keep_z (the default on live-layout
+//                        plans) F2 left z -- F1's output, already scipy's
+//                        filtfilt bit for bit -- whole, and E2 reads it there.
+//   E2 k_exact_rfft +    workgroup = row (stream, tone): |scipy.signal.hilbert(f)|
+//      k_exact_cenv      as pocketfft + numpy evaluate it (pocketfft_dev.h,
+//      (k_exact_env)     every radix and Bluestein), back into z
 //   E3 k_exact_bits      bit = env_mark > env_space in the final pass's byte
 //                        layout -> xbits, which F3 (k_fsk_decide) reads for a
 //                        flagged stream instead of the fast path's bytes

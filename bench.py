@@ -58,7 +58,17 @@ import synth  # noqa: E402
 FS = 96000
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MIXED_GBS = 5200.0         # measured streaming rate at 1:1..2:1 read:write (tools/hbm_mix_probe.hip, profiles/)
-PROFILE_ROUND = "r03"           # profiles/<round>_pmc.json holds the PMC traffic per timing slot
+def _newest_pmc_round():
+    """The newest profiles/r<NN>_pmc.json (the PMC traffic per timing slot of
+    the latest profiled round; profiles/<round>_summary.md folds it)."""
+    import glob
+    import re
+    rounds = [m.group(1) for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
+              if (m := re.fullmatch(r"(r\d+)_pmc\.json", os.path.basename(f)))]
+    return max(rounds, key=lambda r: int(r[1:])) if rounds else None
+
+
+PROFILE_ROUND = _newest_pmc_round()
 FP64_PEAK_TOPS = 39.3          # non-fused FP64 vector ops/s (78.6 TFLOP/s counts an FMA as 2)
 
 # BASELINE.json configs[1..4], 0-based (configs[0] is the reference's CPU plumbing case)
@@ -180,7 +190,8 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
     # launch holds >= 4096 streams (what one batch of the headline holds); the
     # timed region is still exactly K steps (the last launch may be partial)
     C, BL, n_launch, launch_sizes = launch_plan(K, B, strong, args.coalesce)
-    # fsk9600: 4 in flight (35.4 GB of plan scratch each; K = 64, one MI355X: P = 2 34.4 ms/step, 3 33.7, 4 33.1)
+    # fsk9600: 4 in flight (amr_fsk_plan_bytes_estimate per 16384-stream plan; K = 64,
+    # one MI355X, round 3: P = 2 34.4 ms/step, 3 33.7, 4 33.1)
     P = args.inflight or (min(4, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
@@ -509,7 +520,7 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
         # on how many launches are in flight or on the rank count)
         traffic, step_traffic, traffic_src = None, None, None
         pmc_file = os.path.join(ROOT, "profiles", f"{PROFILE_ROUND}_pmc.json")
-        if os.path.exists(pmc_file) and N == 96000 and BL == W["batch"]:
+        if PROFILE_ROUND and os.path.exists(pmc_file) and N == 96000 and BL == W["batch"]:
             with open(pmc_file) as f:
                 pm = json.load(f).get(name, {})
             if pm.get("layout", layout) == layout:
@@ -524,7 +535,13 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
         ach_if = alg_bytes / (kavg[dom] / 1e3) / 1e9 if dom in kavg else None
         roofline = {
             "bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": int(traffic) if traffic else None,
+            "frac": round(ach / HBM_PEAK_GBS, 5),
+            "frac_throughput": round(step_bytes / ms_per_step / 1e6 / HBM_PEAK_GBS, 5),
+            "frac_note": (f"frac = one launch's algorithmic bytes / the dominant kernel's duration as ONE launch alone "
+                          f"on the GPU ({dom_ms:.3f} ms, longer than the {ms_per_step:.3f} ms step because {P} launches "
+                          "overlap in the timed region); frac_throughput = the algorithmic bytes of a step / the step "
+                          "time, the figure consistent with `value` (= pipeline.frac)"),
+            "traffic": int(traffic) if traffic else None,
             "traffic_ratio": round(traffic / alg_bytes, 2) if traffic else None, "traffic_source": traffic_src,
             "alg_bytes_per_launch": int(alg_bytes),
             "alg_bytes_def": "SURVEY 8(d): per stream N x 4 B float32 samples in + decided bits / 8 out "
@@ -979,7 +996,7 @@ def main():
                 subs[name] = {k: r[k] for k in ("metric", "value", "unit", "steps", "ms_per_step", "scaling", "parity",
                                                 "latency_ms_one_batch", "latency_ms_per_global_batch", "kernel_ms",
                                                 "kernel_ms_solo", "cpu_baseline", "config")}
-                subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "kernel_ms_used", "inflight", "pipeline",
+                subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "frac_throughput", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
                 for k in ("gather_check", "exact_path_streams", "exact_probe"):
                     if k in r:

@@ -18,8 +18,11 @@ rounding decides.  Round 4 appends 16 more (their own
 seed, so the first 84 cases are unchanged) at lengths with a prime factor
 above 5 -- Bluestein and generic-radix plans in pocketfft -- with digital
 silence, a DC (constant) stretch or a stretch 1e-17 below the signal
-(params.quiet).  The oracle and the GPU (through its exact path) must match
-all of them.
+(params.quiet).  Round 5 appends 7 long captures (params.long, their own
+seed): 10-s (960 000 samples, what decode_wav_file makes of a 10-s WAV) and
+20-s streams and the non-5-smooth long lengths 441 000 and 400 001, signal
+between digital silence, DC or 1e-17 stretches.  The oracle and the GPU
+(through its exact path) must match all of them.
 
 Run:  python tests/golden/make_sweep_golden.py   (needs /root/reference)
 """
@@ -132,12 +135,50 @@ def draw_quiet(rng, i):
     return "fsk", dict(baud=baud, f0=f0, f1=f1, samp_rate=fs, silence=True, quiet=quiet), x
 
 
+# Round 5: long captures -- decode_wav_file makes a 10-s
+# recording 960 000 samples (decoder.py:385-387), past the fast path's
+# two-pass limit (six-step FFTs), and a non-5-smooth long length runs
+# Bluestein over a six-step convolution.  Signal between quiet stretches
+# (digital silence, a DC lead-in, a 1e-17 stretch) at valid tones: these
+# pin the margin premise (F2's tau) where the fast FFT has the most rounding
+# stages.  (n, baud, quiet, dtype); tones drawn like draw_quiet's.
+LONG_CASES = [(960000, 9600, "silence", "int16"), (960000, 1200, "dc", "float32"),
+              (960000, 4800, "tiny", "float32"), (960000, 2400, "silence", "float64"),
+              (441000, 2400, "silence", "int16"), (400001, 9600, "dc", "float32"),
+              (1920000, 1200, "silence", "int16")]
+
+
+def draw_long(rng, i):
+    fs = 96000.0
+    n, baud, quiet, dt = LONG_CASES[i]
+    f0, f1 = sorted(round(float(v), 3) for v in rng.uniform(baud * 1.1, fs / 2 - baud * 1.1, 2))
+    if i == 0:
+        f0, f1 = 12000.0, 24000.0                        # the benchmark's tones
+    fr = synth.random_frame(rng, int(rng.integers(200, 1200)))
+    w = synth.fsk_waveform(fr, baud, f0, f1, fs)
+    off = int(rng.integers(n // 5, n // 2))              # seconds of quiet before the frame
+    x = np.zeros(n)
+    seg = w[:max(0, n - off)]
+    x[off:off + seg.size] = seg
+    if quiet == "dc":
+        x[:off] = float(rng.choice([0.25, -3.0 / 32768, 1e-3]))
+    elif quiet == "tiny":
+        x[:off] = rng.normal(0, 1e-17, off)
+    if i == 3:
+        g = off + seg.size // 2                          # and a gap of digital silence inside the frame
+        x[g:g + 5000] = 0.0
+    x = np.round(np.clip(x, -1, 1) * 32767).astype(np.int16) if dt == "int16" else x.astype(dt)
+    return "fsk", dict(baud=baud, f0=f0, f1=f1, samp_rate=fs, silence=True, quiet=quiet, long=True), x
+
+
 def main():
     rng = np.random.default_rng(20261017)
     draws = [draw(rng, c) for c in range(N_CASES)]
     draws += [draw_silence(rng) for _ in range(N_SILENCE)]
     rng_q = np.random.default_rng(20261018)
     draws += [draw_quiet(rng_q, i) for i in range(N_QUIET)]
+    rng_l = np.random.default_rng(20261019)
+    draws += [draw_long(rng_l, i) for i in range(len(LONG_CASES))]
     scratch = tempfile.mkdtemp(prefix="amr_sweep_golden_")
     cwd = os.getcwd()
     try:

@@ -189,17 +189,24 @@ def test_fsk_batch_past_2g_samples():
 
 
 @pytest.mark.parametrize("n,baud,mark,space", [(77880, 2400, 11229.28, 29833.37), (96000, 9600, 12000.0, 24000.0),
-                                                (24001, 1200, 2400.0, 4800.0), (30000, 300, 1200.0, 2200.0)])
+                                                (24001, 1200, 2400.0, 4800.0), (30000, 300, 1200.0, 2200.0),
+                                                (96001, 9600, 12000.0, 24000.0),     # Bluestein over a six-step M
+                                                (960000, 9600, 12000.0, 24000.0),    # six-step: a 10-s WAV
+                                                (1920000, 1200, 2400.0, 4800.0),     # six-step, 20 s
+                                                (400001, 4800, 8000.0, 16000.0),     # Bluestein over six-step
+                                                (441000, 2400, 7000.0, 19000.0)])    # 44.1 kHz x 10 s: 2^3 3^2 5^3 7^2
 def test_envelope_error_is_far_below_the_margin(n, baud, mark, space):
     """F2 flags a stream for the exact path when some compare has
     |env_mark - env_space| <= 2 tau peak|x| (tau = 2^-36, amr_internal.h
     kAmbTau); unflagged compares are then bit-exact only if the fast path's
     envelopes are within tau peak|x| of the reference's.  F1 computes scipy's
     filtfilt bit for bit, so the difference is the FFTs' rounding alone --
-    two-pass (96000, 30000), Bluestein (24001, 77880).  Measure it (GPU
+    two-pass (96000, 30000), Bluestein over a two-pass M (24001, 77880),
+    six-step (960000, 1920000: more rounding stages) and
+    Bluestein over a six-step M (96001, 400001, 441000).  Measure it (GPU
     natural-layout envelopes vs the reference's |hilbert(filtfilt(.))|, the
     oracle's restatement) on noise, signal, digital silence and quiet
-    stretches: it must stay below tau / 100."""
+    stretches: it must stay below tau / 100.  The ratio per length is printed."""
     import _fsk
     import synth
     from oracle import oracle
@@ -258,6 +265,10 @@ def _silence_batch(rng, B, n, baud, mark, space, dtype):
     (24001, 4800, 7000.0, 19000.0, np.float32),      # Bluestein
     (30011, 1200, 2400.0, 4800.0, np.int16),         # Bluestein
     (96001, 9600, 12000.0, 24000.0, np.float64),     # Bluestein, six-step fast path
+    (960000, 9600, 12000.0, 24000.0, np.int16),      # a 10-s WAV's length: six-step
+    (960000, 1200, 2400.0, 4800.0, np.float32),
+    (400001, 4800, 7000.0, 19000.0, np.float32),     # Bluestein over a six-step M
+    (441000, 2400, 7000.0, 19000.0, np.float64),
 ])
 def test_fsk_digital_silence_exact(n, baud, mark, space, dtype):
     """Digital silence next to signal, at 5-smooth, generic-radix and
@@ -269,7 +280,7 @@ def test_fsk_digital_silence_exact(n, baud, mark, space, dtype):
     import _fsk
     from oracle import oracle
     rng = np.random.default_rng(n + baud)
-    B = 12
+    B = 12 if n < 200000 else 6
     x = _silence_batch(rng, B, n, baud, mark, space, dtype)
     pl = _fsk.FskPlan(n, baud, mark, space, max_streams=B)
     got, _ = pl.demod_host(x)
@@ -281,7 +292,7 @@ def test_fsk_digital_silence_exact(n, baud, mark, space, dtype):
 
 
 @pytest.mark.parametrize("kind", ["dc", "tiny", "zero"])
-@pytest.mark.parametrize("n", [30000, 77880, 24001])
+@pytest.mark.parametrize("n", [30000, 77880, 24001, 960000, 400001])
 def test_fsk_quiet_stretches_exact(kind, n):
     """Stretches where both envelopes sink to rounding level without being
     exact zeros: a constant (DC) offset -- butter(3, band)'s
@@ -296,7 +307,7 @@ def test_fsk_quiet_stretches_exact(kind, n):
     from oracle import oracle
     rng = np.random.default_rng(n + len(kind))
     baud, mark, space = 2400, 7000.0, 19000.0
-    B = 6
+    B = 6 if n < 200000 else 3
     rows = []
     q = n // 3                      # a quiet lead-in long enough for the band-pass tails to die out
     for i in range(B):

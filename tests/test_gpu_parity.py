@@ -281,9 +281,11 @@ def test_decode_wav_file_44k_qpsk_through_gpu_resample(tmp_path, monkeypatch):
     """A 44.1 kHz QPSK@1000 WAV: decode_wav_file (GPU resample + GPU demod) ==
     scipy.signal.resample + the oracle demod + the host frame parse, i.e. the
     reference's decode_wav_file pipeline (decoder.py:380-389) restated on the CPU.
-    The resample itself is within 1e-11 of scipy's (test_gpu_fsk.py); the
-    decoded bytes are compared exactly ("parity unpinned" at the float64 ulp:
-    no reference fixture holds a resampled 44.1 kHz PSK decode)."""
+    The GPU resample is scipy's bit for bit (test_gpu_fsk.py::test_resample_matches_scipy),
+    and here equal to the oracle's pocketfft restatement (oracle.resample) and
+    to scipy's on the recording itself; the decoded bytes and saved files are
+    compared exactly (the reference's own decode_wav_file outputs at 44.1 / 48
+    / 22.05 kHz are pinned by tests/test_gpu_wav.py)."""
     import decoder
     import synth
     from oracle import oracle
@@ -300,7 +302,11 @@ def test_decode_wav_file_44k_qpsk_through_gpu_resample(tmp_path, monkeypatch):
     with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
         saved = decoder.decode_wav_file(str(p), "QPSK", 1000)
     data, sr = decoder._read_wav(str(p))
-    y = signal.resample(data, int(round(len(data) * 96000.0 / sr)))
+    import _amr
+    num = int(round(len(data) * 96000.0 / sr))
+    y = signal.resample(data, num)
+    assert np.array_equal(oracle.resample(data, num), y)
+    assert np.array_equal(_amr.resample(data, num), y)
     raw = oracle.qpsk_demodulate(y, baud=1000)
     with contextlib.redirect_stdout(io.StringIO()):
         frames = decoder.parse_fbp_stream_enhanced(raw)

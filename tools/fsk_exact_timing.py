@@ -2,7 +2,8 @@
 """How long the FSK exact path takes: zero-padded captures (F2 flags the
 streams whose compares fall inside the margin), every
 stream forced through it (exact mode 2), against the same batch with a noise
-floor (nothing flagged).  GPU box:  python tools/fsk_exact_timing.py"""
+floor (nothing flagged).  GPU box:  python tools/fsk_exact_timing.py [B ...]
+(`burst`: the first all-flagged batch after 0 / 1 / 8 / 20 clean ones)"""
 import os
 import sys
 import time
@@ -52,5 +53,29 @@ def main():
                   flush=True)
 
 
+def burst(B=2048, clean_runs=(0, 1, 8, 20)):
+    """E2's grid follows the counts of the plan's last 8 launches.
+    A fresh plan per row: `c` clean (noise-floor) batches, then one
+    silent-padded batch whose every stream is flagged, with no warm-up of that
+    input -- the first flagged batch after a run of clean ones."""
+    n = 96000
+    noisy, silent = batch(B, n, 0.01), batch(B, n, 0.0)
+    for c in clean_runs:
+        pl = _fsk.FskPlan(n, 9600, 12000.0, 24000.0, max_streams=B)
+        pl.enable_timing(True)
+        for _ in range(c):
+            pl.demod_host(noisy)
+        t = time.perf_counter()
+        pl.demod_host(silent)
+        ms = (time.perf_counter() - t) * 1e3
+        tm = pl.timings()
+        print(f"B={B} after {c:2d} clean batches: all-flagged batch {ms:9.2f} ms (host entry); flagged "
+              f"{pl.exact_streams():4d}; exact stage {tm.get('exact', -1):8.2f} ms", flush=True)
+        del pl
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:2] == ["burst"]:
+        burst()
+    else:
+        main()
