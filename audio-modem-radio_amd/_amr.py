@@ -52,7 +52,8 @@ EXPORTS = [
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather", "amr_fsk_allgather",
     "amr_comm_synchronize", "amr_comm_allgather_host", "amr_comm_allreduce_max", "amr_comm_world", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
     "amr_resample_host", "amr_hilbert_env_exact_host", "amr_fsk_plan_exact_streams",
-    "amr_fsk_plan_set_exact_mode",
+    "amr_fsk_plan_set_exact_mode", "amr_psk_plan_set_layout", "amr_psk_plan_split_info", "amr_psk_split_design",
+    "amr_psk_split_symbols_host",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -207,6 +208,10 @@ def lib():
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
             "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
             "amr_psk_plan_last_layout": (I32, [P]),
+            "amr_psk_plan_set_layout": (I32, [P, I32]),
+            "amr_psk_plan_split_info": (I32, [P, P, P, P, P, P]),
+            "amr_psk_split_design": (I32, [P, P, I32, P, P, I32, I64, I64, P, P, P]),
+            "amr_psk_split_symbols_host": (I32, [P, P, I32, I64, I64, I64, P]),
             "amr_psk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_fsk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_host_register": (I32, [P, I64]),
@@ -314,6 +319,18 @@ def design_psk(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
     return sps, first, bp, lp, lo_table(n, carrier, samp_rate)
 
 
+def split_design(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
+    """The time-split design (host arithmetic in libamr.so, no device): dict of
+    warmup_bp, warmup_lp, kappa, or None when the filters do not allow it."""
+    sps, first, bp, lp, _ = design_psk(kind, n, baud, carrier, samp_rate)
+    S = max(0, (n - first + sps - 1) // sps)
+    w1, w2 = ctypes.c_int64(), ctypes.c_int64()
+    k = ctypes.c_double()
+    rc = lib().amr_psk_split_design(ptr(bp[0]), ptr(bp[1]), len(bp[0]), ptr(lp[0]), ptr(lp[1]), len(lp[0]), n, S,
+                                    ctypes.byref(w1), ctypes.byref(w2), ctypes.byref(k))
+    return None if rc != 0 else {"warmup_bp": w1.value, "warmup_lp": w2.value, "kappa": k.value}
+
+
 def lo_table(n: int, carrier, samp_rate) -> np.ndarray:
     """[n][4]: lo_re, lo_im, -(0*lo_im), 0*lo_re with lo = exp(-1j*2*pi*fc*t) (modem.py:200-201).
 
@@ -395,9 +412,37 @@ class PskPlan:
         check(lib().amr_psk_plan_timings(self.handle, ms, len(T_NAMES)))
         return {k: float(v) for k, v in zip(T_NAMES, ms) if v >= 0}
 
+    LAYOUTS = {"row": 0, "lane": 1, "split": 2}
+
     def last_layout(self) -> str:
-        """'row' (state-per-lane kernels) or 'lane' (one stream per lane) for the last call."""
-        return {0: "row", 1: "lane"}.get(int(lib().amr_psk_plan_last_layout(self.handle)), "?")
+        """'row' (state-per-lane kernels), 'lane' (one stream per lane) or 'split'
+        (time-split passes, margin-checked, serial fallback) for the last call."""
+        return {v: k for k, v in self.LAYOUTS.items()}.get(int(lib().amr_psk_plan_last_layout(self.handle)), "?")
+
+    def set_layout(self, layout):
+        """Force 'row' / 'lane' / 'split' for this plan's calls; None: by streams in flight."""
+        check(lib().amr_psk_plan_set_layout(self.handle, -1 if layout is None else self.LAYOUTS[layout]))
+
+    def split_symbols(self, x: np.ndarray, chunk: int = 0) -> np.ndarray:
+        """Diagnostic: the time-split passes' symbol samples [B][S] complex (not bit-exact)."""
+        x = np.ascontiguousarray(np.atleast_2d(x))
+        B = x.shape[0]
+        S = max(0, (self.n - self.first + self.sps - 1) // self.sps)
+        sym = np.zeros((B, S, 2))
+        with self.lock:
+            check(lib().amr_psk_split_symbols_host(self.handle, ptr(x), DTYPES[x.dtype], B, x.shape[1], int(chunk),
+                                                    ptr(sym)))
+        return sym[..., 0] + 1j * sym[..., 1]
+
+    def split_info(self) -> dict:
+        """The time-split layout: streams the last call flagged for the serial path
+        (-1: that call ran another layout), warm-ups, chunk length, error bound kappa."""
+        fl, w1, w2, L = (ctypes.c_int64() for _ in range(4))
+        k = ctypes.c_double()
+        check(lib().amr_psk_plan_split_info(self.handle, ctypes.byref(fl), ctypes.byref(w1), ctypes.byref(w2),
+                                            ctypes.byref(L), ctypes.byref(k)))
+        return {"flagged": fl.value, "warmup_bp": w1.value, "warmup_lp": w2.value, "chunk": L.value,
+                "kappa": k.value}
 
     def exact_streams(self) -> int:
         c = ctypes.c_int64(0)

@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libamr.so")
-SOURCES = ["psk_kernels.hip", "psk_lane_kernels.hip", "util_kernels.hip", "fft_kernels.hip", "fsk_kernels.hip", "fsk_exact_kernels.hip", "pocketfft_kernels.hip", "frame_kernels.hip", "tx_kernels.hip",
+SOURCES = ["psk_kernels.hip", "psk_lane_kernels.hip", "psk_split_kernels.hip", "util_kernels.hip", "fft_kernels.hip", "fsk_kernels.hip", "fsk_exact_kernels.hip", "pocketfft_kernels.hip", "frame_kernels.hip", "tx_kernels.hip",
            "api.cpp", "tx_api.cpp",
            "fsk_api.cpp", "pocketfft_plan.cpp"]
 HEADERS = ["amr_internal.h", "psk_common.h", "fft.h", "api_common.h", "fsk_exact.h", "pocketfft.h", "pocketfft_dev.h", os.path.join(INCLUDE, "amr.h")]

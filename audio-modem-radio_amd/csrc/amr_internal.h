@@ -63,6 +63,26 @@ struct PskBuffers {
   int64_t out_stride;
   int64_t* out_len;       // [B]
   int64_t* sync_idx;      // [B]
+  const int32_t* gate;    // non-null: every kernel of the launch exits at once while *gate == 0
+                          // (the time-split layout's serial fallback, api.cpp run_psk)
+};
+
+// PSK time-split layout (psk_split_kernels.hip): each filtfilt
+// pass cut into chunks of L outputs, one lane per chunk, each started w
+// samples early from a zero state; decisions kept where the symbols' error
+// bound kappa * peak|x| cannot move them, the rest flagged for the serial path.
+struct PskSplit {
+  int64_t L;              // outputs per chunk, every pass
+  int64_t w1, w2;         // warm-up samples: band-pass, low-pass passes
+  int64_t c1, c2;         // chunks per stream: ceil(m1 / L), ceil(m2 / L)
+  double kappa;           // |symbol error| <= kappa * peak|ext x| (api.cpp split_design)
+  double* y1;             // [B][m1] band-pass forward output (the plan's s1)
+  double* f;              // [B][n] band-pass output (s2)
+  double* y3;             // [B][2][m2] low-pass forward outputs, re then im (s3)
+  double* sym;            // [B][S][re, im] symbol samples (s1, after the band-pass)
+  unsigned long long* peak;   // [B] bits of max |ext x| (cleared per launch)
+  int32_t* flag;          // [B] 1: a decision inside the margin (cleared per launch)
+  int32_t* count;         // [1] flagged streams: the serial fallback's gate
 };
 
 // FSK live-column layout.  A four-step length n = n1 * n2

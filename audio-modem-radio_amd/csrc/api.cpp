@@ -31,6 +31,11 @@ hipError_t launch_synth_tile_noise(const float*, int64_t, int64_t, float*, int64
                                    hipStream_t);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
                             hipStream_t);
+hipError_t launch_sync_pack_gated(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
+                                  const int32_t*, hipStream_t);
+hipError_t launch_psk_split_bp(const PskBuffers&, const PskParams&, const Iir&, const PskSplit&, hipStream_t);
+hipError_t launch_psk_split_lp(const PskBuffers&, const PskParams&, const Iir&, const PskSplit&, hipStream_t);
+hipError_t launch_psk_split_slice(const PskBuffers&, const PskParams&, const PskSplit&, hipStream_t);
 hipError_t launch_fec_decode(const uint8_t*, int64_t, const int64_t*, int64_t, uint8_t*, int64_t, int64_t*,
                              int32_t*, const uint32_t*, const uint32_t*, hipStream_t);
 hipError_t launch_frame_parse(const uint8_t*, int64_t, const int64_t*, int64_t, int64_t, int32_t*, amr_frame_rec*,
@@ -190,6 +195,15 @@ constexpr int64_t kFrontSlack = 8192;
 // streams in flight (batch x amr_psk_plan_set_inflight) from which the
 // lane-per-stream layout runs
 constexpr int64_t kLaneMinLiveStreams = 16384;
+// time-split layout: picked for at most this many streams in
+// flight (a flagged stream re-runs its batch serially, so the batch stays
+// small enough that most batches have none); its error bound is kSplitSafety
+// times the filters' L1 noise gain (split_design); chunks are at least
+// kSplitMinL outputs, and longer once a batch would exceed kSplitLanes lanes
+constexpr int64_t kSplitMaxLiveStreams = 16;
+constexpr double kSplitSafety = 64.0;
+constexpr int64_t kSplitMinL = 64;
+constexpr int64_t kSplitLanes = 65536;
 
 struct amr_psk_plan {
   std::mutex mu;
@@ -230,6 +244,14 @@ struct amr_psk_plan {
   bool ev_used[AMR_T_COUNT]{};
   int64_t last_exact = 0;
   GatherGate gate;              // an all-gather still reading this plan's outputs
+  // time-split layout (psk_split_kernels.hip): designed on first use
+  int forced_layout = -1;       // amr_psk_plan_set_layout (-1: by streams in flight)
+  bool split_designed = false, split_ok = false;
+  int64_t split_w1 = 0, split_w2 = 0, split_L = 0;
+  double split_kappa = 0.0;
+  unsigned long long* split_peak = nullptr;   // [max_streams], then flags [max_streams] and the count
+  int32_t* split_flag = nullptr;
+  int32_t* split_count = nullptr;
 };
 
 struct amr_comm {
@@ -297,7 +319,8 @@ std::vector<PskAlloc> psk_allocs(const amr_psk_plan* pl) {
           {3, g * 2 * ((n + 1) / 2) * 32 * 16 + (1 << 16)},
           {4, kFrontSlack * 8 + lane_s3_bytes(pl)},
           {5, g * kWave * pl->p.n_words * 4},
-          {6, 2 * g * kWave * 4}};     // low-pass flags, then band-pass flags
+          {6, 2 * g * kWave * 4},      // low-pass flags, then band-pass flags
+          {7, pl->max_streams * 12 + 64}};   // time-split: input peaks, flags, the flagged count
 }
 
 // the most the plan can hold: `allocated` with s1 / s3 grown to the row
@@ -381,6 +404,14 @@ int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
 }
 }  // namespace amr
 
+namespace {
+void split_design(amr_psk_plan* pl);   // below, with run_psk
+bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, int64_t* w1, int64_t* w2,
+                       double* kappa);
+int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L);
+int ensure(void** p, int64_t* have, int64_t need);
+}  // namespace
+
 extern "C" {
 
 int amr_abi_version(void) { return AMR_ABI_VERSION; }
@@ -438,6 +469,7 @@ static void plan_free(amr_psk_plan* pl) {
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
   for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
+                  (void*)pl->split_peak,
                   pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
     if (p) (void)hipFree(p);
@@ -497,7 +529,7 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
     if (f[0] == '1') pl->lp_exact_only = true;
 
   void** ptrs[] = {(void**)&pl->lo, (void**)&pl->lo2, (void**)&pl->s1_base, (void**)&pl->s2, (void**)&pl->s3_base,
-                   (void**)&pl->words, (void**)&pl->flags};
+                   (void**)&pl->words, (void**)&pl->flags, (void**)&pl->split_peak};
   struct A { void** ptr; int64_t bytes; };
   std::vector<A> allocs;
   for (const PskAlloc& a : psk_allocs(pl)) allocs.push_back({ptrs[a.which], a.bytes});
@@ -511,6 +543,8 @@ int amr_psk_plan_create(amr_psk_plan** out, int device, int kind, int64_t n, int
   }
   pl->s1 = pl->s1_base + kFrontSlack;
   pl->s3 = pl->s3_base + kFrontSlack;
+  pl->split_flag = reinterpret_cast<int32_t*>(pl->split_peak + max_streams);
+  pl->split_count = pl->split_flag + max_streams;
   pl->s1_bytes = kFrontSlack * 8 + lane_s1_bytes(pl);
   pl->s3_bytes = kFrontSlack * 8 + lane_s3_bytes(pl);
   {
@@ -607,6 +641,78 @@ int amr_psk_plan_timings(amr_psk_plan* plan, float* ms, int count) {
 
 int amr_psk_plan_last_layout(const amr_psk_plan* plan) { return plan ? plan->last_layout : -1; }
 
+int amr_psk_plan_set_layout(amr_psk_plan* plan, int layout) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  if (layout != -1 && layout != AMR_LAYOUT_ROW && layout != AMR_LAYOUT_LANE && layout != AMR_LAYOUT_SPLIT)
+    return fail(AMR_E_INVALID, "unknown layout");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  plan->forced_layout = layout;
+  return AMR_OK;
+}
+
+int amr_psk_split_design(const double* bp_b, const double* bp_a, int bp_nt, const double* lp_b, const double* lp_a,
+                         int lp_nt, int64_t n, int64_t n_sym, int64_t* warmup_bp, int64_t* warmup_lp, double* kappa) {
+  if (!bp_b || !bp_a || !lp_b || !lp_a || !warmup_bp || !warmup_lp || !kappa || bp_nt < 2 || bp_nt > kMaxTaps ||
+      lp_nt < 2 || lp_nt > kMaxTaps || n < 1 || n_sym < 0)
+    return fail(AMR_E_INVALID, "amr_psk_split_design: bad argument");
+  Iir bp{}, lp{};
+  bp.nt = bp_nt;
+  lp.nt = lp_nt;
+  for (int i = 0; i < bp_nt; ++i) { bp.b[i] = bp_b[i]; bp.a[i] = bp_a[i]; }
+  for (int i = 0; i < lp_nt; ++i) { lp.b[i] = lp_b[i]; lp.a[i] = lp_a[i]; }
+  *warmup_bp = *warmup_lp = -1;
+  *kappa = -1.0;
+  if (!split_design_core(bp, lp, n, n_sym, warmup_bp, warmup_lp, kappa)) {
+    *warmup_bp = *warmup_lp = -1;
+    *kappa = -1.0;
+    return fail(AMR_E_INVALID, "these filters do not allow the time-split layout");
+  }
+  return AMR_OK;
+}
+
+int amr_psk_split_symbols_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                               int64_t chunk, double* sym) {
+  if (!plan || !x || !sym || B < 1) return fail(AMR_E_INVALID, "amr_psk_split_symbols_host: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (dtype_size(dtype) == 0 || x_stride < plan->p.n) return fail(AMR_E_INVALID, "bad dtype / x_stride");
+  if (!plan->split_designed) split_design(plan);
+  if (!plan->split_ok || plan->p.n_sym < 2) return fail(AMR_E_INVALID, "no time-split layout for this plan");
+  const int64_t n = plan->p.n, es = dtype_size(dtype);
+  int64_t have = plan->d_x_bytes;
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  if (int rc = ensure(&plan->d_x, &have, B * n * es)) return rc;
+  plan->d_x_bytes = have;
+  if (int rc = copy_batch_h2d(plan->d_x, x, n * es, x_stride * es, B, plan->stream)) return rc;
+  if (int rc = run_psk_split_front(plan, plan->d_x, dtype, B, n, chunk)) return rc;
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  HIP_TRY(hipMemcpy(sym, plan->s1, (size_t)(B * plan->p.n_sym * 2 * 8), hipMemcpyDeviceToHost));
+  return AMR_OK;
+}
+
+int amr_psk_plan_split_info(amr_psk_plan* plan, int64_t* flagged, int64_t* warmup_bp, int64_t* warmup_lp,
+                            int64_t* chunk, double* kappa) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (!plan->split_designed) split_design(plan);
+  if (flagged) {
+    *flagged = -1;
+    if (plan->last_layout == AMR_LAYOUT_SPLIT) {
+      int32_t c = 0;
+      HIP_TRY(hipStreamSynchronize(plan->stream));
+      HIP_TRY(hipMemcpy(&c, plan->split_count, 4, hipMemcpyDeviceToHost));
+      *flagged = c;
+    }
+  }
+  if (warmup_bp) *warmup_bp = plan->split_ok ? plan->split_w1 : -1;
+  if (warmup_lp) *warmup_lp = plan->split_ok ? plan->split_w2 : -1;
+  if (chunk) *chunk = plan->split_L;
+  if (kappa) *kappa = plan->split_ok ? plan->split_kappa : -1.0;
+  return AMR_OK;
+}
+
 int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
   if (!plan || !count) return fail(AMR_E_INVALID, "NULL argument");
   std::lock_guard<std::mutex> lk(plan->mu);
@@ -623,6 +729,120 @@ int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
 }  // extern "C"
 
 namespace {
+
+// ---- time-split layout design ------------------------------
+// The DF-II-T's responses with zero input (scipy's recursion, a[0] = 1):
+//   g_i  the output after a unit error in state i -- how one step's rounding
+//        in state i reaches the output; g1 = sum_i sum_m |g_i(m)|, and
+//        tail(m) = sup_{m' >= m} sum_i |g_i(m')| (what a state error left m
+//        steps back still contributes);
+//   h    the output and states after a unit input sample: h1 = ||h||_1 (the
+//        L1 gain), zmax = max_i ||h_{x -> z_i}||_1 (a state per unit input peak).
+struct IirGains {
+  double g1 = 0.0, h1 = 0.0, zmax = 0.0;
+  std::vector<double> tail;
+  bool ok = false;
+};
+IirGains iir_gains(const Iir& f) {
+  IirGains r;
+  const int N = f.nt - 1;
+  constexpr int64_t kMaxSteps = 4000000;
+  std::vector<double> zs((size_t)N * N, 0.0);
+  for (int i = 0; i < N; ++i) zs[(size_t)i * N + i] = 1.0;
+  bool decayed = false;
+  for (int64_t m = 0; m < kMaxSteps && !decayed; ++m) {
+    double t = 0.0, live = 0.0;
+    for (int i = 0; i < N; ++i) {
+      double* z = &zs[(size_t)i * N];
+      const double y = z[0];
+      for (int j = 0; j < N - 1; ++j) z[j] = z[j + 1] - f.a[j + 1] * y;
+      z[N - 1] = -f.a[N] * y;
+      t += std::fabs(y);
+      for (int j = 0; j < N; ++j) live = std::max(live, std::fabs(z[j]));
+    }
+    r.g1 += t;
+    r.tail.push_back(t);
+    decayed = live < 1e-40 && m > 4 * N;
+  }
+  if (!decayed || !std::isfinite(r.g1)) return r;
+  for (int64_t m = (int64_t)r.tail.size() - 2; m >= 0; --m) r.tail[(size_t)m] = std::max(r.tail[(size_t)m], r.tail[(size_t)m + 1]);
+  std::vector<double> z(N, 0.0), zsum(N, 0.0);
+  double x = 1.0;
+  decayed = false;
+  for (int64_t m = 0; m < kMaxSteps && !decayed; ++m) {
+    const double y = z[0] + f.b[0] * x;
+    for (int j = 0; j < N - 1; ++j) z[j] = z[j + 1] + f.b[j + 1] * x - f.a[j + 1] * y;
+    z[N - 1] = f.b[N] * x - f.a[N] * y;
+    r.h1 += std::fabs(y);
+    double live = 0.0;
+    for (int j = 0; j < N; ++j) {
+      zsum[j] += std::fabs(z[j]);
+      live = std::max(live, std::fabs(z[j]));
+    }
+    x = 0.0;
+    decayed = live < 1e-40 && m > 4 * N;
+  }
+  r.zmax = *std::max_element(zsum.begin(), zsum.end());
+  r.ok = decayed && std::isfinite(r.h1) && std::isfinite(r.zmax);
+  return r;
+}
+// the first m with tail(m) * scale <= tol (-1: none within the response)
+int64_t warmup_for(const IirGains& g, double scale, double tol) {
+  for (size_t m = 0; m < g.tail.size(); ++m)
+    if (g.tail[m] * scale <= tol) return (int64_t)m;
+  return -1;
+}
+// A chunked pass differs from the serial one by (1) the zero start state,
+// decayed after w samples to at most tail(w) * zmax * (the pass's input peak)
+// at the pass's output, then amplified by the later passes' L1 gains -- w is
+// chosen to bring that below 1/16 of u * G, G = g1(band-pass) + g1(low-pass);
+// and (2) a different rounding trajectory: measured <= 1.4 u G over tones,
+// square waves, noise and modulated inputs at 10 filter sets
+// (tests/test_gpu_split.py), so |symbol error| <= kappa * peak|x| with kappa =
+// 64 u G plus the transients.  Input peaks per unit peak|x|: the band-pass
+// forward pass 3 (odd extension), backward 3 h1_bp; the low-pass (f * lo,
+// odd extension) 9 h1_bp^2, backward 9 h1_bp^2 h1_lp.
+bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, int64_t* w1o, int64_t* w2o,
+                       double* kappa) {
+  if (bp.nt != 9 || lp.nt != 5 || 2 * n_sym > n + 6 * bp.nt) return false;
+  const IirGains gb = iir_gains(bp), gl = iir_gains(lp);
+  if (!gb.ok || !gl.ok) return false;
+  const double u = 0x1p-53;
+  const double G = gb.g1 + gl.g1;
+  const double tol = 0x1p-4 * u * G;
+  const int64_t w1 = warmup_for(gb, gb.zmax * 3.0 * gb.h1 * gl.h1 * gl.h1, tol);
+  const int64_t w2 = warmup_for(gl, gl.zmax * 9.0 * gb.h1 * gb.h1 * gl.h1, tol);
+  if (w1 < 0 || w2 < 0 || w1 > n / 4 || w2 > n / 4) return false;
+  *w1o = w1;
+  *w2o = w2;
+  *kappa = (kSplitSafety + 0.25) * u * G;
+  return std::isfinite(*kappa) && *kappa > 0.0;
+}
+// the launch's chunking: L (0: the plan's rule -- at least kSplitMinL
+// outputs, and long enough to keep a batch within kSplitLanes lanes)
+PskSplit split_params(amr_psk_plan* pl, int64_t B, int64_t L) {
+  PskSplit sp{};
+  sp.L = L > 0 ? L : std::max<int64_t>(kSplitMinL, (B * pl->p.m1 + kSplitLanes - 1) / kSplitLanes);
+  sp.w1 = pl->split_w1;
+  sp.w2 = pl->split_w2;
+  sp.c1 = (pl->p.m1 + sp.L - 1) / sp.L;
+  sp.c2 = (pl->p.m2 + sp.L - 1) / sp.L;
+  sp.kappa = pl->split_kappa;
+  sp.y1 = pl->s1;
+  sp.f = pl->s2;
+  sp.y3 = pl->s3;
+  sp.sym = pl->s1;
+  sp.peak = pl->split_peak;
+  sp.flag = pl->split_flag;
+  sp.count = pl->split_count;
+  pl->split_L = sp.L;
+  return sp;
+}
+void split_design(amr_psk_plan* pl) {
+  pl->split_designed = true;
+  pl->split_ok = split_design_core(pl->bp, pl->lp, pl->p.n, pl->p.n_sym, &pl->split_w1, &pl->split_w2,
+                                   &pl->split_kappa);
+}
 
 // Launch the whole PSK pipeline on plan->stream.  Caller holds plan->mu.
 int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, uint8_t* d_out,
@@ -644,20 +864,41 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   // enough streams are in flight on the device to give it waves -- it does
   // a third of the arithmetic per stream -- else the state-per-lane kernels
   // (more waves per stream, lower latency).  AMR_PSK_LANE=0/1 forces either.
+  // The time-split layout (psk_split_kernels.hip, §3.3) for one capture or a
+  // few: chunk-parallel passes, margin-checked decisions, the serial row
+  // kernels behind them for a flagged batch.  AMR_PSK_SPLIT=0/1 (and
+  // amr_psk_plan_set_layout, which overrides every switch) force it off / on.
   static const int lane_force = [] {
     const char* e = std::getenv("AMR_PSK_LANE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  static const int split_force = [] {
+    const char* e = std::getenv("AMR_PSK_SPLIT");
     return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
   const int64_t live = B * (pl->inflight > 1 ? pl->inflight : 1);
   // the lane kernels are written for butter(4) band-pass / low-pass
   // coefficient shapes: 9 taps and a palindromic 5-tap low-pass
   const bool lane_ok = pl->bp.nt == 9 && pl->p.lp_sym;
-  const bool lane = lane_ok && (lane_force >= 0 ? lane_force == 1 : live >= kLaneMinLiveStreams);
-  pl->last_layout = lane ? AMR_LAYOUT_LANE : AMR_LAYOUT_ROW;
+  int layout;
+  if (pl->forced_layout >= 0) layout = pl->forced_layout;
+  else if (lane_force >= 0) layout = lane_force == 1 ? AMR_LAYOUT_LANE : AMR_LAYOUT_ROW;
+  else if (split_force == 1) layout = AMR_LAYOUT_SPLIT;
+  else if (live >= kLaneMinLiveStreams) layout = AMR_LAYOUT_LANE;
+  else layout = split_force != 0 && live <= kSplitMaxLiveStreams ? AMR_LAYOUT_SPLIT : AMR_LAYOUT_ROW;
+  if (layout == AMR_LAYOUT_LANE && !lane_ok) layout = AMR_LAYOUT_ROW;
+  if (layout == AMR_LAYOUT_SPLIT) {
+    if (!pl->split_designed) split_design(pl);
+    if (!pl->split_ok || B > 65535 || pl->p.n_sym < 2) layout = AMR_LAYOUT_ROW;
+  }
+  const bool lane = layout == AMR_LAYOUT_LANE;
+  pl->last_layout = layout;
   if (pl->p.n_sym >= 2) {
     // the sizes this layout's kernels assume (the row layout's full-length
-    // intermediates are allocated on its first call); a plan whose earlier
-    // grow failed re-tries here and fails cleanly if it still cannot
+    // intermediates are allocated on its first call; the time-split layout
+    // keeps its passes' outputs in the same buffers and runs the row kernels
+    // behind them); a plan whose earlier grow failed re-tries here and fails
+    // cleanly if it still cannot
     const int64_t b1 = kFrontSlack * 8 + (lane ? lane_s1_bytes(pl) : row_s1_bytes(pl));
     const int64_t b3 = kFrontSlack * 8 + (lane ? lane_s3_bytes(pl) : row_s3_bytes(pl));
     if (int rc = ensure_scratch(pl, b1, b3)) return rc;
@@ -703,6 +944,37 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(gate_wait(pl->gate, st));
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
+  } else if (layout == AMR_LAYOUT_SPLIT) {
+    const PskSplit sp = split_params(pl, B, 0);
+    HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, st));   // peaks, flags, count
+    HIP_TRY(mark(AMR_T_BANDPASS, 0));
+    HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, st));
+    HIP_TRY(mark(AMR_T_BANDPASS, 1));
+    HIP_TRY(mark(AMR_T_LOWPASS_FWD, 0));
+    HIP_TRY(launch_psk_split_lp(b, pl->p, pl->lp, sp, st));
+    HIP_TRY(mark(AMR_T_LOWPASS_FWD, 1));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 0));
+    HIP_TRY(launch_psk_split_slice(b, pl->p, sp, st));
+    HIP_TRY(gate_wait(pl->gate, st));                  // the outputs: after any gather still reading them
+    HIP_TRY(launch_sync_pack(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync, st));
+    HIP_TRY(mark(AMR_T_SYNC_PACK, 1));
+    // the serial row kernels over the whole batch, each exiting at once while
+    // no stream was flagged (the count on the device; no host round trip)
+    PskBuffers g = b;
+    g.gate = pl->split_count;
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 0));
+    HIP_TRY(launch_psk_bandpass(g, pl->p, pl->bp, st));
+    if (pl->lp_exact_only) {
+      HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)pl->flags, 1, (size_t)B, st));
+    } else {
+      HIP_TRY(launch_psk_lowpass_fwd(g, pl->p, pl->lp, st));
+      HIP_TRY(launch_psk_lowpass_bwd(g, pl->p, pl->lp, st));
+    }
+    HIP_TRY(launch_psk_lowpass_exact(g, pl->p, pl->lp, st));
+    HIP_TRY(launch_psk_slice(g, pl->p, st));
+    HIP_TRY(launch_sync_pack_gated(pl->words, pl->p.n_words, pl->p.n_bits, B, d_out, out_stride, d_len, d_sync,
+                                   pl->split_count, st));
+    HIP_TRY(mark(AMR_T_LOWPASS_EXACT, 1));
   } else if (lane) {
     HIP_TRY(mark(AMR_T_BANDPASS, 0));
     HIP_TRY(launch_psk_bandpass_lane(b, pl->p, pl->bp, st));
@@ -757,6 +1029,24 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(mark(AMR_T_FEC, 1));
   }
   if (pl->timing) HIP_TRY(hipEventRecord(pl->ev[AMR_T_LAUNCH][1], st));
+  return AMR_OK;
+}
+
+// the time-split passes alone (KS1-KS4) with chunk length L: the symbol
+// samples in s1 [B][S][2] (amr_psk_split_symbols_host).  Caller holds mu.
+int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L) {
+  if (int rc = ensure_scratch(pl, kFrontSlack * 8 + row_s1_bytes(pl), kFrontSlack * 8 + row_s3_bytes(pl))) return rc;
+  PskBuffers b{};
+  b.x = d_x;
+  b.x_stride = x_stride;
+  b.dtype = dtype;
+  b.n_streams = B;
+  b.lo = pl->lo;
+  b.lo2 = pl->lo2;
+  const PskSplit sp = split_params(pl, B, L);
+  HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, pl->stream));
+  HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, pl->stream));
+  HIP_TRY(launch_psk_split_lp(b, pl->p, pl->lp, sp, pl->stream));
   return AMR_OK;
 }
 

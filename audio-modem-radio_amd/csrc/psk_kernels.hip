@@ -171,6 +171,7 @@ __device__ __forceinline__ size_t row_pair_index(int64_t w, int64_t m_pairs, int
 
 template <typename T, int WPB>
 __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams p, Iir f) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   __shared__ __attribute__((aligned(16))) uint8_t tiles[WPB][2][kRowStreams][kTilePitch];
   __shared__ __attribute__((aligned(16))) uint8_t bwd_ring[WPB][kBpRing][1024];   // s1 chunks (LDS-DMA)
   __shared__ __attribute__((aligned(16))) BwdStage bwd_st[WPB];
@@ -425,6 +426,7 @@ __device__ __forceinline__ double g8_step(const RowIir& c, double& z, bool top, 
 
 template <typename T, int WPB>
 __global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p, Iir f) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   __shared__ __attribute__((aligned(16))) uint8_t tiles[WPB][2][kG8Streams][kG8Pitch];
   __shared__ __attribute__((aligned(1024))) uint8_t ring[WPB][kG8Ring][1024];   // s1 chunks (LDS-DMA)
   __shared__ __attribute__((aligned(1024))) G8Stage st8[WPB];
@@ -682,6 +684,7 @@ __device__ __forceinline__ void quad_flag(PskBuffers& buf, int64_t s, int j, boo
 }
 
 __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams p, Iir f) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   const int lane = threadIdx.x;
   const int j = lane & 3, sq = lane >> 2;
   // blocks b and b+8 land on the same XCD (blocks are dealt to the 8 XCDs
@@ -860,6 +863,7 @@ __global__ __launch_bounds__(64) void k_lowpass_fwd_q(PskBuffers buf, PskParams 
 // K3q: SPS > 0 as K3 (static symbol offsets inside CH-sample chunks)
 template <int SPS>
 __global__ __launch_bounds__(64) void k_lowpass_bwd_q(PskBuffers buf, PskParams p, Iir f) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   constexpr int CH = SPS > 0 ? 20 : kLpChunk;
   static_assert(SPS == 0 || CH % SPS == 0, "chunk must be a multiple of SPS");
   const int lane = threadIdx.x;
@@ -1017,6 +1021,7 @@ int64_t psk_exact_scratch_bytes(int64_t n_streams, int64_t m2) {
 
 template <int NT>
 __global__ __launch_bounds__(64) void k_lowpass_exact(PskBuffers buf, PskParams p, Iir f) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   static_assert(NT == 5, "checkpoint layout holds 2 x 4 states");
   const int lane = threadIdx.x;
   const int64_t n_groups = (buf.n_streams + kWave - 1) / kWave;
@@ -1129,6 +1134,7 @@ constexpr int kSliceWords = 32;
 // (k_lp_lane FUSE); only the streams K3x recomputed get their words here.
 template <int WV>
 __global__ __launch_bounds__(64 * WV) void k_slice(PskBuffers buf, PskParams p, int only_flagged) {
+  if (buf.gate && *buf.gate == 0) return;   // a gated launch (PskBuffers::gate): whole grid
   constexpr int WPW = kSliceWords / WV;         // words per wave
   __shared__ uint32_t wl[kWave][kSliceWords + 1];
   const int lane = threadIdx.x & 63;

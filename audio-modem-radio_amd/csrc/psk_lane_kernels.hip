@@ -45,59 +45,7 @@ constexpr int kBpT = 32;     // band-pass checkpoint tile (samples)
 constexpr int kLpT = 40;     // low-pass checkpoint tile: a multiple of sps 5 / 10 / 20 (static symbol slots)
 constexpr int kLpT2 = 20;    // the same for the role-split low-pass (LDS: 2 components x 2 buffers x tile)
 
-// scipy lfilter's DF-II-T step with all states of one stream in one lane:
-//   y = z0 + b0*x ;  z[j] = (z[j+1] + x*b[j+1]) - y*a[j+1] ;  z[last] = x*b[last] - y*a[last]
-// (z[last] of the row kernels is (-0.0 + x*b) - y*a: -0.0 is the additive
-// identity for every double, NaN included, so the forms agree bit for bit)
-template <int NS>
-__device__ __forceinline__ double df2t_step(double (&z)[NS], const Iir& f, double x) {
-  const double y = z[0] + f.b[0] * x;
-#pragma unroll
-  for (int j = 0; j < NS - 1; ++j) z[j] = (z[j + 1] + x * f.b[j + 1]) - y * f.a[j + 1];
-  z[NS - 1] = x * f.b[NS] - y * f.a[NS];
-  return y;
-}
-
-// The band-pass's odd taps b1, b3, b5, b7 are exactly +0.0 (butter(4, band);
-// the plan checks, PskParams::bp_zero_odd).  The step without them --
-// z[i] = z[i+1] - y*a[i+1] for even i -- is scipy's bit for bit whenever
-// z[i+1] + x*(+0.0) == z[i+1], i.e. unless z[i+1] is -0.0 (or x is inf / NaN,
-// which makes the final states non-finite).  The detector keeps the minimum
-// |hi word| (as float) of z1, z3, z5, z7 before every step: >= FLT_MIN means
-// |z| >= 2^-1015, never a zero; a stream that fails, or ends non-finite, is
-// flagged and its group re-run with every tap (k_bp_lane2's FIXUP form).
-// 26 instead of 34 FP64 per step, + 2 v_min3_f32.
-// The numerator is also palindromic (b8 == b0, b6 == b2 bit for bit,
-// PskParams::bp_sym), so x*b8 IS x*b0 and x*b6 IS x*b2: 3 products, not 5.
-// 23 FP64 per step instead of 34.
-__device__ __forceinline__ double df2t_step_zo(double (&z)[8], const Iir& f, double x, float& acc) {
-  acc = tiny_min3(acc, z[1], z[3]);
-  acc = tiny_min3(acc, z[5], z[7]);
-  const double p0 = f.b[0] * x, p2 = x * f.b[2], p4 = x * f.b[4];
-  const double y = z[0] + p0;
-  z[0] = z[1] - y * f.a[1];
-  z[1] = (z[2] + p2) - y * f.a[2];
-  z[2] = z[3] - y * f.a[3];
-  z[3] = (z[4] + p4) - y * f.a[4];
-  z[4] = z[5] - y * f.a[5];
-  z[5] = (z[6] + p2) - y * f.a[6];
-  z[6] = z[7] - y * f.a[7];
-  z[7] = p0 - y * f.a[8];
-  return y;
-}
-
-// The low-pass numerator k*[1,4,6,4,1] is palindromic (PskParams::lp_sym,
-// required for the lane layout): x*b4 IS x*b0 and x*b3 IS x*b1.  15 FP64
-// per step instead of 17, each result identical to df2t_step<4>.
-__device__ __forceinline__ double lp_step(double (&z)[4], const Iir& f, double x) {
-  const double p0 = f.b[0] * x, p1 = x * f.b[1], p2 = x * f.b[2];
-  const double y = z[0] + p0;
-  z[0] = (z[1] + p1) - y * f.a[1];
-  z[1] = (z[2] + p2) - y * f.a[2];
-  z[2] = (z[3] + p1) - y * f.a[3];
-  z[3] = p0 - y * f.a[4];
-  return y;
-}
+// (the DF-II-T step functions df2t_step / df2t_step_zo / lp_step: psk_common.h)
 
 template <bool ZO>
 __device__ __forceinline__ double bp_step(double (&z)[8], const Iir& f, double x, float& acc) {

@@ -33,10 +33,11 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
 __global__ __launch_bounds__(64) void k_sync_pack(const uint32_t* __restrict__ words_all, int64_t n_words,
                                                   int64_t n_bits, int64_t n_streams,
                                                   uint8_t* __restrict__ out, int64_t out_stride,
-                                                  int64_t* __restrict__ out_len, int64_t* __restrict__ sync_idx) {
+                                                  int64_t* __restrict__ out_len, int64_t* __restrict__ sync_idx,
+                                                  const int32_t* __restrict__ gate) {
   const int lane = threadIdx.x;
   const int64_t s = blockIdx.x;
-  if (s >= n_streams) return;
+  if (s >= n_streams || (gate && *gate == 0)) return;
   const uint32_t* __restrict__ w = words_all + (size_t)s * n_words;
   const int64_t L = n_bits;
   const int64_t nw = (L + 31) >> 5;
@@ -178,7 +179,15 @@ hipError_t launch_sync_pack(const uint32_t* words, int64_t n_words, int64_t n_bi
                             uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx,
                             hipStream_t st) {
   hipLaunchKernelGGL(k_sync_pack, dim3((unsigned)n_streams), dim3(kWave), 0, st, words, n_words, n_bits,
-                     n_streams, out, out_stride, out_len, sync_idx);
+                     n_streams, out, out_stride, out_len, sync_idx, (const int32_t*)nullptr);
+  return hipGetLastError();
+}
+// the same, exiting at once while *gate == 0 (the time-split layout's serial fallback)
+hipError_t launch_sync_pack_gated(const uint32_t* words, int64_t n_words, int64_t n_bits, int64_t n_streams,
+                                  uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx,
+                                  const int32_t* gate, hipStream_t st) {
+  hipLaunchKernelGGL(k_sync_pack, dim3((unsigned)n_streams), dim3(kWave), 0, st, words, n_words, n_bits,
+                     n_streams, out, out_stride, out_len, sync_idx, gate);
   return hipGetLastError();
 }
 

@@ -57,8 +57,9 @@
 extern "C" {
 #endif
 
-#define AMR_ABI_VERSION 2   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
-                                 amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT */
+#define AMR_ABI_VERSION 3   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
+                                 amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT
+                               3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -145,10 +146,42 @@ int amr_psk_plan_set_inflight(amr_psk_plan *plan, int batches);
 int amr_psk_plan_timings(amr_psk_plan *plan, float *ms, int count);
 /* kernel layout of the last call: AMR_LAYOUT_ROW = states spread over lanes
  * (psk_kernels.hip), AMR_LAYOUT_LANE = one stream per lane
- * (psk_lane_kernels.hip); picked by streams in flight */
+ * (psk_lane_kernels.hip), AMR_LAYOUT_SPLIT = each filtfilt pass cut in time
+ * into chunks, decisions kept where a margin proves them the reference's and
+ * a batch with any other stream re-run by the row kernels
+ * (psk_split_kernels.hip).  Picked by streams in flight
+ * (DESIGN.md §3): split for <= 16 (one capture at a time, as the reference's
+ * own callers decode -- filebeep_advanced_v2.py:324, 1112), row up to
+ * 16383, lane from 16384. */
 #define AMR_LAYOUT_ROW 0
 #define AMR_LAYOUT_LANE 1
+#define AMR_LAYOUT_SPLIT 2
 int amr_psk_plan_last_layout(const amr_psk_plan *plan);
+/* force a layout for this plan's calls (-1: by streams in flight, the
+ * default).  No reference counterpart: a test / tuning knob; the bytes are
+ * the reference's in every layout. */
+int amr_psk_plan_set_layout(amr_psk_plan *plan, int layout);
+/* the time-split layout of this plan: streams its last call flagged for the
+ * serial path (-1 when that call ran another layout; synchronises the plan's
+ * stream), the band-pass / low-pass warm-up samples and the symbols' error
+ * bound per unit input peak (-1 when the plan's filters do not allow the
+ * layout), and the last call's chunk length (0 before any).  Any pointer may
+ * be NULL. */
+int amr_psk_plan_split_info(amr_psk_plan *plan, int64_t *flagged, int64_t *warmup_bp, int64_t *warmup_lp,
+                            int64_t *chunk, double *kappa);
+/* The time-split design of a band-pass / low-pass pair (host arithmetic, no
+ * device): warm-up samples per filter and kappa, the bound on a symbol
+ * sample's error per unit input peak; AMR_E_INVALID when the
+ * filters do not allow the layout (warm-ups over n / 4, not 9 + 5 taps). */
+int amr_psk_split_design(const double *bp_b, const double *bp_a, int bp_ntaps, const double *lp_b,
+                         const double *lp_a, int lp_ntaps, int64_t n_samples, int64_t n_sym, int64_t *warmup_bp,
+                         int64_t *warmup_lp, double *kappa);
+/* Diagnostic (tests): the time-split passes alone over a host batch, chunk
+ * outputs per lane (0: the plan's rule) -> the symbol samples
+ * sym [n_streams][n_sym][re, im] (baseband[first::sps], modem.py:92, 209, as
+ * the time-split layout computes them -- not bit-exact). */
+int amr_psk_split_symbols_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                               int64_t chunk, double *sym);
 /* number of streams the exact complex low-pass path re-ran in the last call */
 int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
 

@@ -302,6 +302,92 @@ done:
     return result;
 }
 
+/* ---- the time-split layout, restated (psk_split_kernels.hip) -----------------
+ * NOT a reference function: the GPU's chunk-parallel approximation of the
+ * four filtfilt passes, so tests can check the device computes exactly what
+ * DESIGN.md §3.3 says (symbols equal to these up to the sign of a zero) and
+ * measure its error against the serial (reference) symbols.  Every pass is cut
+ * into chunks of L outputs; a chunk runs the recursion from w samples before
+ * its first output from a zero state, or from the pass's start with scipy's
+ * zi * first-sample state when that is within w.  The low-pass runs its two
+ * components as separate real recursions (the GPU's form; scipy's complex
+ * lfilter differs only in signed zeros).  sym: [S][2]. Returns S (0: < 2). */
+static void chunked_pass(const double *b, const double *a, int nt, const double *zi,
+                         const double *in, double *out, int64_t m, int64_t L, int64_t w)
+{
+    double z[32];
+    for (int64_t o0 = 0; o0 < m; o0 += L) {
+        const int64_t o1 = o0 + L < m ? o0 + L : m;
+        int64_t j = o0 - w;
+        if (j <= 0) { j = 0; for (int i = 0; i < nt - 1; ++i) z[i] = zi[i] * in[0]; }
+        else for (int i = 0; i < nt - 1; ++i) z[i] = 0.0;
+        for (; j < o1; ++j) {
+            double y;
+            df2t(b, a, nt, z, in + j, &y, 1, 1);
+            if (j >= o0) out[j] = y;
+        }
+    }
+}
+
+int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
+                                 const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                                 const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                                 const double *lo, int64_t L, int64_t w1, int64_t w2, double *sym)
+{
+    const int pad1 = 3 * bp_nt, pad2 = 3 * lp_nt;
+    if (n <= pad1 || n <= pad2 || L < 1) return -1;
+    const int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
+    if (S < 2) return 0;
+    const int64_t m1 = n + 2 * (int64_t)pad1, m2 = n + 2 * (int64_t)pad2;
+    double *e = (double *)malloc(sizeof(double) * (size_t)(m1 > 2 * m2 ? m1 : 2 * m2));
+    double *y = (double *)malloc(sizeof(double) * (size_t)m1);
+    double *r = (double *)malloc(sizeof(double) * (size_t)m1);
+    double *g = (double *)malloc(sizeof(double) * 2 * (size_t)n);
+    for (int64_t j = 0; j < m1; ++j) e[j] = ext_sample(x, dtype, n, pad1, j);
+    chunked_pass(bp_b, bp_a, bp_nt, bp_zi, e, y, m1, L, w1);
+    for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
+    chunked_pass(bp_b, bp_a, bp_nt, bp_zi, r, y, m1, L, w1);
+    for (int64_t i = 0; i < n; ++i)                      /* f[i] = y[m1 - 1 - pad1 - i]; (f + 0j) * lo */
+        cmul_np(y[m1 - 1 - pad1 - i], 0.0, lo[2 * i], lo[2 * i + 1], &g[2 * i], &g[2 * i + 1]);
+    for (int c = 0; c < 2; ++c) {
+        double *ec = e + (size_t)c * m2;
+        const double x0 = g[c], xl = g[2 * (n - 1) + c];
+        for (int j = 0; j < pad2; ++j) ec[j] = 2.0 * x0 - g[2 * (pad2 - j) + c];
+        for (int64_t i = 0; i < n; ++i) ec[pad2 + i] = g[2 * i + c];
+        for (int j = 0; j < pad2; ++j) ec[pad2 + n + j] = 2.0 * xl - g[2 * (n - 2 - j) + c];
+        chunked_pass(lp_b, lp_a, lp_nt, lp_zi, ec, y, m2, L, w2);
+        for (int64_t k = 0; k < m2; ++k) r[k] = y[m2 - 1 - k];
+        chunked_pass(lp_b, lp_a, lp_nt, lp_zi, r, y, m2, L, w2);
+        for (int64_t q = 0; q < S; ++q) sym[2 * q + c] = y[m2 - 1 - pad2 - (first + q * sps)];
+    }
+    free(e); free(y); free(r); free(g);
+    return S;
+}
+
+/* The serial (reference) symbol samples baseband[first::sps] of the same
+ * stream: scipy's filtfilt, the mixer, scipy's complex filtfilt.  sym [S][2]. */
+int64_t oracle_psk_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
+                           const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                           const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                           const double *lo, double *sym)
+{
+    const int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
+    int64_t m = n + 2 * 3 * (int64_t)(bp_nt > lp_nt ? bp_nt : lp_nt);
+    double *filt = (double *)malloc(sizeof(double) * n);
+    double *re = (double *)malloc(sizeof(double) * n);
+    double *im = (double *)malloc(sizeof(double) * n);
+    double *work = (double *)malloc(sizeof(double) * 2 * m);
+    int64_t rc = S;
+    if (oracle_filtfilt(bp_b, bp_a, bp_nt, bp_zi, x, dtype, n, filt, work)) rc = -1;
+    else {
+        for (int64_t i = 0; i < n; ++i) cmul_np(filt[i], 0.0, lo[2 * i], lo[2 * i + 1], &re[i], &im[i]);
+        if (filtfilt_complex(lp_b, lp_a, lp_nt, lp_zi, re, im, n, work)) rc = -2;
+        else for (int64_t q = 0; q < S; ++q) { sym[2 * q] = re[first + q * sps]; sym[2 * q + 1] = im[first + q * sps]; }
+    }
+    free(filt); free(re); free(im); free(work);
+    return rc;
+}
+
 /* Batch driver (the CPU baseline): streams are independent; parallelised with
  * OpenMP across streams when built with -fopenmp. */
 int64_t oracle_psk_demod_batch(int kind, const void *x, int dtype, int64_t n_streams, int64_t n,
