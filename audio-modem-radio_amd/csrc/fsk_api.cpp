@@ -351,15 +351,24 @@ struct amr_fsk_plan {
   int32_t* xlist = nullptr;    // [B] flagged ordinal -> stream, then [1] the count
   int32_t* xcount_host = nullptr;   // host-mapped: the count E3 last saw (FskExact count_hint)
   int32_t* xcount_dev = nullptr;    // its device pointer
-  // E0-E3 on a stream of their own at the device's highest priority, ordered
-  // by events after F2 and before F3 (AMR_FSK_XSTREAM=0: on the plan's
-  // stream): an exact-path workgroup needs 64 KiB of LDS, and from a
-  // high-priority queue it takes the next CU that frees that much ahead of
-  // the other launches in flight, so the full resident grid can be launched
-  // every batch (a burst of flagged streams after clean batches gets all of
-  // it) without the idle launches waiting behind the FFT passes
+  // AMR_FSK_XSTREAM=1 (an A/B, off by default): E0-E3 on a stream of their
+  // own at the device's highest priority, ordered by events after F2 and
+  // before F3, with the full resident grid every batch.  An exact-path
+  // workgroup needs 64 KiB of LDS; from a high-priority queue it takes the
+  // next CU that frees that much ahead of the launches in flight.  Measured
+  // (profiles/r05_fsk_exact_xstream.txt): alone, fsk9600 36.5-36.8 vs
+  // 37.1-37.5 ms/step and a burst of 2048 flagged streams after clean batches
+  // 21.8 vs 393 ms of exact stage; but in the default bench process (the
+  // PSK headline's 21 streams created first) 39.2-39.9 vs 37.3-37.4 ms/step,
+  // two interleaved pairs -- so the plan's own stream stays the default, and
+  // the synchronous host entry sizes the grid from the batch's own count
+  // (count_sync)
   hipStream_t xstream = nullptr;
   hipEvent_t ev_f2 = nullptr, ev_x = nullptr;
+  // the synchronous host entry (amr_fsk_demod_host) reads E0's count on the
+  // host before the envelope kernels: none flagged -> E1-E3 are not launched
+  // at all; else E2's grid is sized from this batch's own count
+  bool count_sync = false;
   // the counts E3 reported before the last kHintDepth launches:
   // E2's grid follows their maximum, so one clean batch between flagged ones
   // does not shrink the grid of the next flagged batch to kIdleGrid
@@ -511,7 +520,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   static const int live_only = [] { const char* e = std::getenv("AMR_FSK_LIVEONLY"); return !(e && e[0] == '0'); }();
   X.live_only = live_only;
   X.count_host = pl->xcount_dev;
-  if (pl->xstream) {
+  if (pl->xstream && !pl->count_sync) {
     X.count_hint = B;                                   // the full resident grid (see xstream)
   } else if (pl->xcount_host) {
     pl->hint_hist[pl->hint_pos] = *reinterpret_cast<volatile int32_t*>(pl->xcount_host);
@@ -521,7 +530,8 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     X.count_hint = B;
   }
   hipStream_t st = pl->stream;
-  if (pl->xstream) {
+  const bool xs = pl->xstream && !pl->count_sync;
+  if (xs) {
     HIP_TRY(hipEventRecord(pl->ev_f2, pl->stream));
     HIP_TRY(hipStreamWaitEvent(pl->xstream, pl->ev_f2, 0));
     st = pl->xstream;
@@ -529,6 +539,18 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 0, st));
   pl->ran_exact = true;
   HIP_TRY(launch_fsk_exact_list(B, X, st));
+  if (pl->count_sync) {
+    int32_t c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, X.count, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (c == 0) {                            // nothing flagged: F3 takes every stream's fast-path bits
+      pl->ran_exact = false;
+      *pl->xcount_host = 0;
+      HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1, st));
+      return AMR_OK;
+    }
+    X.count_hint = c;
+  }
   if (!pl->keep_z) {
     // E1: F1 again over the flagged streams only (list mode), natural z layout
     FskParams p1 = pl->p;
@@ -540,7 +562,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   }
   HIP_TRY(launch_fsk_exact_env(B, pl->p, X, st, launch != 2));
   HIP_TRY(mark_fsk(pl, AMR_TF_EXACT, 1, st));
-  if (pl->xstream) {
+  if (xs) {
     HIP_TRY(hipEventRecord(pl->ev_x, pl->xstream));
     HIP_TRY(hipStreamWaitEvent(pl->stream, pl->ev_x, 0));
   }
@@ -885,7 +907,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->p.xbits = pl->xbits;
     pl->n_slots = geo.n_slots;
     pl->slot_doubles = geo.slot_doubles;
-    static const bool xstream_on = [] { const char* e = std::getenv("AMR_FSK_XSTREAM"); return !(e && e[0] == '0'); }();
+    static const bool xstream_on = [] { const char* e = std::getenv("AMR_FSK_XSTREAM"); return e && e[0] == '1'; }();
     if (xstream_on) {
       int least = 0, greatest = 0;
       e = hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -1009,7 +1031,10 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   } else {
     void* xs = nullptr;
     if (int rc = stage_input(plan, x, dtype, B, x_stride, &xs)) return rc;
-    if (int rc = run_fsk(plan, xs, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync)) return rc;
+    plan->count_sync = true;                 // this call waits anyway: the exact path sized by its own count
+    const int rc = run_fsk(plan, xs, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync);
+    plan->count_sync = false;
+    if (rc) return rc;
   }
   if (int rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B,
                               plan->stream))
