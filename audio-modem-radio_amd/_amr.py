@@ -53,7 +53,7 @@ EXPORTS = [
     "amr_comm_synchronize", "amr_comm_allgather_host", "amr_comm_allreduce_max", "amr_comm_world", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
     "amr_resample_host", "amr_hilbert_env_exact_host", "amr_fsk_plan_exact_streams",
     "amr_fsk_plan_set_exact_mode", "amr_psk_plan_set_layout", "amr_psk_plan_split_info", "amr_psk_split_design",
-    "amr_psk_split_symbols_host",
+    "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -212,6 +212,8 @@ def lib():
             "amr_psk_plan_split_info": (I32, [P, P, P, P, P, P]),
             "amr_psk_split_design": (I32, [P, P, I32, P, P, I32, I64, I64, P, P, P]),
             "amr_psk_split_symbols_host": (I32, [P, P, I32, I64, I64, I64, P]),
+            "amr_psk_f32_margin": (D, [P, P, I32]),
+            "amr_psk_plan_last_f32f": (I32, [P]),
             "amr_psk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_fsk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_host_register": (I32, [P, I64]),
@@ -331,6 +333,12 @@ def split_design(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
     return None if rc != 0 else {"warmup_bp": w1.value, "warmup_lp": w2.value, "kappa": k.value}
 
 
+def f32_margin(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000) -> float:
+    """The float32 hand-off's symbol error bound per unit max |f| (libamr.so, host arithmetic)."""
+    _, _, _, lp, _ = design_psk(kind, n, baud, carrier, samp_rate)
+    return float(lib().amr_psk_f32_margin(ptr(lp[0]), ptr(lp[1]), len(lp[0])))
+
+
 def lo_table(n: int, carrier, samp_rate) -> np.ndarray:
     """[n][4]: lo_re, lo_im, -(0*lo_im), 0*lo_re with lo = exp(-1j*2*pi*fc*t) (modem.py:200-201).
 
@@ -433,6 +441,10 @@ class PskPlan:
             check(lib().amr_psk_split_symbols_host(self.handle, ptr(x), DTYPES[x.dtype], B, x.shape[1], int(chunk),
                                                     ptr(sym)))
         return sym[..., 0] + 1j * sym[..., 1]
+
+    def last_f32f(self) -> bool:
+        """The last call handed the band-pass output to the low-pass in float32."""
+        return int(lib().amr_psk_plan_last_f32f(self.handle)) == 1
 
     def split_info(self) -> dict:
         """The time-split layout: streams the last call flagged for the serial path

@@ -42,6 +42,10 @@ struct PskParams {
   int bp_zero_odd;        // 1: b[1], b[3], ... are all +0.0 (band-pass symmetry)
   int bp_sym;             // 1: 9 taps with b[8] == b[0] and b[6] == b[2] bit for bit
   int lp_sym;             // 1: 5 taps with b[4] == b[0] and b[3] == b[1] bit for bit
+  // the lane layout's float32 hand-off (PskBuffers::f32f):
+  // |symbol error| <= f32_margin * (the stream's max |f|) + 2^-120 when the
+  // low-pass reads f rounded to float32 (api.cpp f32_design; 0: not allowed)
+  double f32_margin;
 };
 
 // Pointers of one batch launch (device memory).
@@ -65,6 +69,13 @@ struct PskBuffers {
   int64_t* sync_idx;      // [B]
   const int32_t* gate;    // non-null: every kernel of the launch exits at once while *gate == 0
                           // (the time-split layout's serial fallback, api.cpp run_psk)
+  // lane layout, float32 hand-off: the band-pass stores f rounded to float32
+  // (half of each group's s2 slot) and its per-stream max |f| in fpeak; the
+  // fused low-pass slicer flags (flags and bp_flags) every stream with a
+  // decision inside the rounding's margin, whose group the band-pass fix-up
+  // then recomputes in float64 for K3x / K4a
+  int f32f;
+  double* fpeak;          // [B]
 };
 
 // PSK time-split layout (psk_split_kernels.hip): each filtfilt

@@ -36,6 +36,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "amr_internal.h"
 #include "psk_common.h"
 
@@ -271,9 +273,13 @@ __global__ __launch_bounds__(256) void k_bp_fwd(PskBuffers buf, PskParams p, Iir
 // reaches the second tile of a pair by first re-running the pair's first
 // tile without outputs (1.5x its steps), holding the pair's inputs in
 // registers (one more tile of them) -- bit for bit the same outputs.
-template <typename T, int GPB, bool ZO, bool FIXUP = false, bool PRE = false, int CK = 1>
+// F32F (PskBuffers::f32f): f is stored rounded to float32 into the first half
+// of the group's s2 slot (the f64 layout's element order, float elements),
+// and each stream's max |f| (bits: NaN / inf dominate) into buf.fpeak.
+template <typename T, int GPB, bool ZO, bool FIXUP = false, bool PRE = false, int CK = 1, bool F32F = false>
 __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParams p, Iir f) {
   static_assert(!(FIXUP && PRE), "the fix-up pass runs its own forward pass");
+  static_assert(!(F32F && FIXUP), "the fix-up pass writes float64 f");
   static_assert(CK == 1 || (CK == 2 && !PRE), "64-sample checkpoints: the kernel's own forward pass");
   constexpr int TB = kBpT;
   constexpr int PER = 16 / (int)sizeof(T);
@@ -304,6 +310,8 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
   double* __restrict__ ck = buf.s1 + (size_t)w * nt * 8 * 64 + lane;
   double* __restrict__ eb = buf.s1 + (size_t)G * nt * 8 * 64 + (size_t)w * ecap * 64 + lane;
   double* __restrict__ fo = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+  [[maybe_unused]] float* __restrict__ fo32 =
+      reinterpret_cast<float*>(buf.s2 + (size_t)w * 2 * n2 * 64) + (size_t)(lane >> 5) * n2 * 64 + (lane & 31) * 2;
 
   auto load_tile = [&](int64_t t, v4u (&r)[NL]) {
 #pragma unroll
@@ -443,6 +451,13 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
     // ---- backward pass: the tail edge, then the tiles out of LDS -------------
     double zb[8];
     float acc = __builtin_inff();
+    unsigned long long pk = 0;                  // F32F: max |f| as bits
+    auto pk_acc = [&](double y) {
+      if constexpr (F32F) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(y) & 0x7fffffffffffffffULL;
+        pk = b > pk ? b : pk;
+      }
+    };
     if (active) {
       const double ylast = eb[(ne - 1) * 64];
 #pragma unroll
@@ -450,7 +465,14 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
       for (int e = ne - 1; e >= 0; --e) {
         const double y = bp_step<ZO>(zb, f, eb[e * 64], acc);
         const int64_t i = i_tail + e;
-        if (i < n) fo[(i >> 1) * 64 + (i & 1)] = y;
+        if (i < n) {
+          if constexpr (F32F) {
+            fo32[(i >> 1) * 64 + (i & 1)] = (float)y;
+            pk_acc(y);
+          } else {
+            fo[(i >> 1) * 64 + (i & 1)] = y;
+          }
+        }
       }
     }
     __syncthreads();                            // tile nt-1 is in buffer 0
@@ -459,17 +481,27 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
       if (active) {
         const double2 (*ybuf)[64] = yb[gi][(it - 1) & 1];
         double* const fp = fo + (size_t)(t * (TB / 2)) * 64;
+        float* const fp32 = fo32 + (size_t)(t * (TB / 2)) * 64;
 #pragma unroll
         for (int k = TB / 2 - 1; k >= 0; --k) {
           const double2 yy = ybuf[k][lane];
           const double y1 = bp_step<ZO>(zb, f, yy.y, acc);
           const double y0 = bp_step<ZO>(zb, f, yy.x, acc);
-          *reinterpret_cast<double2*>(fp + k * 64) = make_double2(y0, y1);
+          if constexpr (F32F) {
+            *reinterpret_cast<float2*>(fp32 + k * 64) = make_float2((float)y0, (float)y1);
+            pk_acc(y0);
+            pk_acc(y1);
+          } else {
+            *reinterpret_cast<double2*>(fp + k * 64) = make_double2(y0, y1);
+          }
         }
       }
       __syncthreads();
     }
     if (active && bp_bad<ZO>(acc, zb) && s <= last) atomicOr(&buf.bp_flags[s], 1);
+    if constexpr (F32F) {
+      if (active && s <= last) buf.fpeak[s] = __longlong_as_double((long long)pk);
+    }
   }
 }
 
@@ -516,9 +548,18 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
 // each word as it completes.  No symbol leaves the chip (0.63 GB written and
 // read back per 4096-stream batch before); streams the detector flags get
 // their symbols from K3x and their words from K4a afterwards.
-template <int SPS, int FM, int WPB, bool FUSE = false>
+// F32F (with FUSE; PskBuffers::f32f): f arrives rounded to float32 (k_bp_lane2
+// F32F), so the symbols differ from the reference's by at most
+// E = p.f32_margin * fpeak[s] + 2^-120 (the rounding through the low-pass's L1
+// gain, api.cpp f32_design); the re wave flags every decision within E of its
+// boundary -- QPSK ||di| - |dr||, BPSK |dr| against sqrt2 E (|s0|_1 + |s1|_1 +
+// E) -- into flags and bp_flags, and the fix-up band-pass, K3x and K4a redo
+// those streams exactly.
+template <int SPS, int FM, int WPB, bool FUSE = false, bool F32F = false>
 __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lane(PskBuffers buf, PskParams p, Iir f) {
   static_assert(!FUSE || (SPS > 0 && WPB >= 2), "fused slicing: static slots, both components in one workgroup");
+  static_assert(!F32F || FUSE, "the float32 hand-off's margin check runs in the fused slicer");
+  using FV = typename std::conditional<F32F, float2, double2>::type;
   constexpr int TL = kLpT;
   constexpr int CH = AMR_LP_CH;                 // samples per f chunk (CH / 2 x 16 B per lane)
   constexpr int NCH = TL / CH, HC = CH / 2;
@@ -564,29 +605,40 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   double* __restrict__ eh = buf.s3 + (size_t)2 * G * nt * 4 * 64 + (size_t)wc * ecap * 64 + lane;
   double* __restrict__ et = eh + (size_t)(pad + TL) * 64;
   const double* __restrict__ fl = buf.s2 + (size_t)(w * 2 + (lane >> 5)) * n2 * 64 + (lane & 31) * 2;
+  const float* __restrict__ fl32 =
+      reinterpret_cast<const float*>(buf.s2 + (size_t)w * 2 * n2 * 64) + (size_t)(lane >> 5) * n2 * 64 + (lane & 31) * 2;
   const double* __restrict__ lov = buf.lo2 + (size_t)comp * n;                   // lo_c[i], vector loads
   CDouble* const loc = (CDouble*)(buf.lo2 + (size_t)comp * n);                   // the same, scalar loads
   CDouble* const lo4 = (CDouble*)(buf.lo) + 2 * comp;                            // (mult, addend) at [4i]
-  auto F = [&](int64_t i) { return fl[(i >> 1) * 64 + (i & 1)]; };
+  auto F = [&](int64_t i) -> double {
+    if constexpr (F32F) return (double)fl32[(i >> 1) * 64 + (i & 1)];
+    else return fl[(i >> 1) * 64 + (i & 1)];
+  };
   auto Xm = [&](int64_t i) { return F(i) * loc[i]; };
-  // f pairs of tile t, chunk c: this lane's 16 B at fl + (t*TL/2 + c*HC + k) * 64
-  auto load_chunk = [&](int64_t t, int c, double2 (&r)[HC]) {
-    const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2) + c * HC) * 64);
+  // f pairs of tile t, chunk c: this lane's 16 B (F32F: 8 B) at pair t*TL/2 + c*HC + k
+  auto load_chunk = [&](int64_t t, int c, FV (&r)[HC]) {
+    if constexpr (F32F) {
+      const float2* fp = reinterpret_cast<const float2*>(fl32 + (size_t)(t * (TL / 2) + c * HC) * 64);
 #pragma unroll
-    for (int k = 0; k < HC; ++k) r[k] = fp[k * 32];
+      for (int k = 0; k < HC; ++k) r[k] = fp[k * 32];
+    } else {
+      const double2* fp = reinterpret_cast<const double2*>(fl + (size_t)(t * (TL / 2) + c * HC) * 64);
+#pragma unroll
+      for (int k = 0; k < HC; ++k) r[k] = fp[k * 32];
+    }
   };
   auto load_lo = [&](int64_t t) -> double { return lov[t * TL + (lane < TL ? lane : 0)]; };
   auto put_lo = [&](int64_t t, double v) {
     if (lane < TL) lo_lds[wv][t & 1][lane] = v;
   };
   // mixer inputs of chunk c from the chunk's f pairs and the tile's LDS multipliers
-  auto chunk_e = [&](int64_t t, int c, const double2 (&fv)[HC], double (&e)[CH]) {
+  auto chunk_e = [&](int64_t t, int c, const FV (&fv)[HC], double (&e)[CH]) {
     const double2* lp = reinterpret_cast<const double2*>(&lo_lds[wv][t & 1][c * CH]);
 #pragma unroll
     for (int k = 0; k < HC; ++k) {
       const double2 l = lp[k];
-      e[2 * k] = fv[k].x * l.x;
-      e[2 * k + 1] = fv[k].y * l.y;
+      e[2 * k] = (double)fv[k].x * l.x;
+      e[2 * k + 1] = (double)fv[k].y * l.y;
     }
   };
 
@@ -614,7 +666,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
     acc = tiny_min3(acc, i == 0 ? y : e, y);
     eh[(pad + i) * 64] = y;
   }
-  double2 ring[R][HC];
+  FV ring[R][HC];
   if (nt > 1) {
 #pragma unroll
     for (int c = 0; c < R; ++c) load_chunk(1, c, ring[c]);
@@ -627,7 +679,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
     for (int j = 0; j < 4; ++j) ck[(t * 4 + j) * 64] = z[j];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      double2 fv[HC];
+      FV fv[HC];
 #pragma unroll
       for (int k = 0; k < HC; ++k) fv[k] = ring[c % R][k];
       if (c + R < NCH) load_chunk(t, c + R, ring[c % R]);
@@ -680,6 +732,9 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   double pr = 0.0, pim = 0.0;                   // s[k+1]
   uint32_t wacc = 0;
   const bool qpsk = p.kind == kQpsk;
+  // F32F: this stream's symbol error bound, and whether a decision fell inside it
+  const double Em = F32F && s < buf.n_streams ? p.f32_margin * buf.fpeak[s] + 0x1p-120 : 0.0;
+  bool mflag = false;
   auto region_done = [&](int64_t i_lo, int64_t i_hi) {
     if constexpr (FUSE) {
       __syncthreads();
@@ -692,8 +747,18 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
           if (k <= S - 2) {
             const double br = sr, bi = -si;
             const double dr = __builtin_fma(pr, br, -(pim * bi));
+            double md = 0.0;                    // F32F: the decision's margin (d's error bound)
+            if constexpr (F32F) {
+              const double a0 = fabs(br) + fabs(bi), a1 = fabs(pr) + fabs(pim);
+              md = 0x1.6a09e667f3bcdp+0 * Em * (a0 + a1 + Em) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
+              if (!qpsk && !(fabs(dr) > md)) mflag = true;
+            }
             if (qpsk) {
               const double di = __builtin_fma(pr, bi, pim * br);
+              if constexpr (F32F) {
+                const double adr = fabs(dr), adi = fabs(di);
+                if (!(fabs(adi - adr) > md + 0x1p-29 * (adr + adi))) mflag = true;
+              }
               wacc |= qpsk_dibit(dr, di) << (30 - 2 * (int)(k & 15));
               if ((k & 15) == 0) {
                 if (s < buf.n_streams) buf.words[(size_t)s * p.n_words + (k >> 4)] = wacc;
@@ -744,7 +809,7 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
       double yt[TL];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        double2 fv[HC];
+        FV fv[HC];
 #pragma unroll
         for (int k = 0; k < HC; ++k) fv[k] = ring[c % R][k];
         if (c + R < NCH) load_chunk(t, c + R, ring[c % R]);
@@ -784,7 +849,11 @@ __global__ __launch_bounds__(64 * WPB, SPS > 0 ? AMR_LP_WAVES : 1) void k_lp_lan
   bad |= !(accb >= kTinyHi);
 #pragma unroll
   for (int j = 0; j < 4; ++j) bad |= !__builtin_isfinite(zb[j]);
-  if (bad && s < buf.n_streams) atomicOr(&buf.flags[s], 1);
+  if constexpr (F32F) bad |= mflag;
+  if (bad && s < buf.n_streams) {
+    atomicOr(&buf.flags[s], 1);
+    if constexpr (F32F) atomicOr(&buf.bp_flags[s], 1);   // float64 f for K3x: the fix-up re-runs the group
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1057,6 +1126,19 @@ static int bp_zero_taps(const PskParams& p) {
 template <typename T>
 static hipError_t launch_bp(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
   const int64_t g = (b.n_streams + 63) / 64;
+  if (b.f32f) {
+    // the float32 hand-off (the default throughput configuration only: split
+    // roles, 4-wave workgroups, 32-sample checkpoints); its fix-up launch
+    // comes after the low-pass, which flags streams too
+    // (launch_psk_bandpass_fixup)
+    if (!(bp_split() && lane_wpb() >= 2 && !bp_prefwd() && bp_ck() == 1)) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(b.bp_flags, 0, (size_t)b.n_streams * 4, st);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)((g + 1) / 2)), block(256);
+    if (bp_zero_taps(p)) hipLaunchKernelGGL((k_bp_lane2<T, 2, true, false, false, 1, true>), grid, block, 0, st, b, p, f);
+    else hipLaunchKernelGGL((k_bp_lane2<T, 2, false, false, false, 1, true>), grid, block, 0, st, b, p, f);
+    return hipGetLastError();
+  }
   if (bp_split()) {
     const bool zo = bp_zero_taps(p);
     if (zo) {
@@ -1105,6 +1187,20 @@ hipError_t launch_psk_bandpass_lane(const PskBuffers& b, const PskParams& p, con
   }
 }
 
+// the float32 hand-off's fix-up: every tap, float64 f, for the groups holding
+// a stream the band-pass detector or the low-pass margin flagged (bp_flags)
+hipError_t launch_psk_bandpass_fixup(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st) {
+  if (f.nt != 9) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((b.n_streams + 63) / 64)), block(128);
+  switch (b.dtype) {
+    case kF32: hipLaunchKernelGGL((k_bp_lane2<float, 1, false, true>), grid, block, 0, st, b, p, f); break;
+    case kF64: hipLaunchKernelGGL((k_bp_lane2<double, 1, false, true>), grid, block, 0, st, b, p, f); break;
+    case kI16: hipLaunchKernelGGL((k_bp_lane2<int16_t, 1, false, true>), grid, block, 0, st, b, p, f); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 static int lp_split() {
   // role-split low-pass (k_lp_lane2): AMR_LP_SPLIT=1 turns it on (off by
   // default: its 20-sample tiles double the checkpoint traffic and leave its
@@ -1132,6 +1228,12 @@ static bool launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hip
   }();
   const int64_t live = b.n_streams * (b.inflight > 1 ? b.inflight : 1);
   const bool fuse = S_ > 0 && lane_wpb() >= 2 && (fuse_env >= 0 ? fuse_env == 1 : live >= 32768);
+  if (b.f32f) {
+    // the float32 hand-off needs the fused slicer (api.cpp asks psk_lane_fused first)
+    if (!(fuse && S_ != 0 && lane_wpb() == 4)) return false;
+    hipLaunchKernelGGL((k_lp_lane<S_, F_, 4, S_ != 0, S_ != 0>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
+    return true;
+  }
   switch (lane_wpb()) {
     case 4:
       if (fuse) hipLaunchKernelGGL((k_lp_lane<S_, F_, 4, S_ != 0>), dim3((unsigned)((g + 1) / 2)), dim3(256), 0, st, b, p, f);
@@ -1146,6 +1248,20 @@ static bool launch_lp(const PskBuffers& b, const PskParams& p, const Iir& f, hip
       hipLaunchKernelGGL((k_lp_lane<S_, F_, 1>), dim3((unsigned)((2 * g + 15) / 16 * 16)), dim3(64), 0, st, b, p, f);
   }
   return fuse;
+}
+
+// whether launch_psk_lowpass_lane will run the fused slicer for this batch
+// (the float32 hand-off's precondition, api.cpp)
+bool psk_lane_fused(const PskBuffers& b, const PskParams& p) {
+  const int fm = (int)(p.first % (p.sps > 0 ? p.sps : 1));
+  const bool stat = p.first <= kLpT2 && ((p.sps == 10 && (fm == 5 || fm == 0)) || (p.sps == 5 && (fm == 2 || fm == 0)) ||
+                                         (p.sps == 20 && (fm == 10 || fm == 0)));
+  static const int fuse_env = [] {
+    const char* e = getenv("AMR_FUSED_SLICE");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  const int64_t live = b.n_streams * (b.inflight > 1 ? b.inflight : 1);
+  return stat && !lp_split() && lane_wpb() == 4 && (fuse_env >= 0 ? fuse_env == 1 : live >= 32768);
 }
 
 hipError_t launch_psk_lowpass_lane(const PskBuffers& b, const PskParams& p, const Iir& f, hipStream_t st,

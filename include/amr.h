@@ -59,7 +59,9 @@ extern "C" {
 
 #define AMR_ABI_VERSION 3   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
                                  amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT
-                               3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info */
+                               3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info,
+                                  amr_psk_split_design, amr_psk_split_symbols_host, the float32 hand-off
+                                  (amr_psk_f32_margin, amr_psk_plan_last_f32f) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -176,6 +178,13 @@ int amr_psk_plan_split_info(amr_psk_plan *plan, int64_t *flagged, int64_t *warmu
 int amr_psk_split_design(const double *bp_b, const double *bp_a, int bp_ntaps, const double *lp_b,
                          const double *lp_a, int lp_ntaps, int64_t n_samples, int64_t n_sym, int64_t *warmup_bp,
                          int64_t *warmup_lp, double *kappa);
+/* The lane layout's float32 hand-off: the bound on a symbol
+ * sample's error per unit of the stream's max |band-pass output| when the
+ * low-pass reads that output rounded to float32 (host arithmetic on the
+ * low-pass b, a; 0: no hand-off for these coefficients), and whether the
+ * plan's last call used the hand-off (1) or float64 (0). */
+double amr_psk_f32_margin(const double *lp_b, const double *lp_a, int lp_ntaps);
+int amr_psk_plan_last_f32f(const amr_psk_plan *plan);
 /* Diagnostic (tests): the time-split passes alone over a host batch, chunk
  * outputs per lane (0: the plan's rule) -> the symbol samples
  * sym [n_streams][n_sym][re, im] (baseband[first::sps], modem.py:92, 209, as

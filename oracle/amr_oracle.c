@@ -365,11 +365,39 @@ int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sp
 }
 
 /* The serial (reference) symbol samples baseband[first::sps] of the same
- * stream: scipy's filtfilt, the mixer, scipy's complex filtfilt.  sym [S][2]. */
+ * stream: scipy's filtfilt, the mixer, scipy's complex filtfilt.  sym [S][2].
+ * f32f: the band-pass output rounded to float32 before the mixer -- NOT the
+ * reference: the lane layout's float32 hand-off, restated. */
+static int64_t psk_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
+                           const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                           const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                           const double *lo, double *sym, int f32f);
 int64_t oracle_psk_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
                            const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
                            const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
                            const double *lo, double *sym)
+{
+    return psk_symbols(x, dtype, n, sps, first, bp_b, bp_a, bp_nt, bp_zi, lp_b, lp_a, lp_nt, lp_zi, lo, sym, 0);
+}
+int64_t oracle_psk_symbols_f32f(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
+                                const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                                const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                                const double *lo, double *sym, double *fpeak)
+{
+    /* fpeak: max |f| (the kernel's per-stream scale of the margin) */
+    int64_t m = n + 2 * 3 * (int64_t)(bp_nt > lp_nt ? bp_nt : lp_nt);
+    double *filt = (double *)malloc(sizeof(double) * n);
+    double *work = (double *)malloc(sizeof(double) * 2 * m);
+    *fpeak = 0.0;
+    if (oracle_filtfilt(bp_b, bp_a, bp_nt, bp_zi, x, dtype, n, filt, work) == 0)
+        for (int64_t i = 0; i < n; ++i) if (fabs(filt[i]) > *fpeak) *fpeak = fabs(filt[i]);
+    free(filt); free(work);
+    return psk_symbols(x, dtype, n, sps, first, bp_b, bp_a, bp_nt, bp_zi, lp_b, lp_a, lp_nt, lp_zi, lo, sym, 1);
+}
+static int64_t psk_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
+                           const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
+                           const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
+                           const double *lo, double *sym, int f32f)
 {
     const int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
     int64_t m = n + 2 * 3 * (int64_t)(bp_nt > lp_nt ? bp_nt : lp_nt);
@@ -380,6 +408,7 @@ int64_t oracle_psk_symbols(const void *x, int dtype, int64_t n, int64_t sps, int
     int64_t rc = S;
     if (oracle_filtfilt(bp_b, bp_a, bp_nt, bp_zi, x, dtype, n, filt, work)) rc = -1;
     else {
+        if (f32f) for (int64_t i = 0; i < n; ++i) filt[i] = (double)(float)filt[i];
         for (int64_t i = 0; i < n; ++i) cmul_np(filt[i], 0.0, lo[2 * i], lo[2 * i + 1], &re[i], &im[i]);
         if (filtfilt_complex(lp_b, lp_a, lp_nt, lp_zi, re, im, n, work)) rc = -2;
         else for (int64_t q = 0; q < S; ++q) { sym[2 * q] = re[first + q * sps]; sym[2 * q + 1] = im[first + q * sps]; }

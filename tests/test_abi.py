@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_symbols():
     with open(os.path.join(ROOT, "include", "amr.h")) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*\*?\s*(amr_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|double|const char \*)\s*\*?\s*(amr_\w+)\(", txt, re.M)))
 
 
 def test_header_and_binding_agree():

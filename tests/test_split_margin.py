@@ -85,3 +85,29 @@ def test_split_restatement_with_unbounded_warmup_is_the_reference(built_lib):
     ref = oracle.psk_symbols("qpsk", x, 9600)
     sp = oracle.psk_split_symbols("qpsk", x, 9600, 3000.0, 96000.0, 97, 10 ** 6, 10 ** 6)
     assert np.array_equal(sp, ref)
+
+
+F32F_CONFIGS = [("qpsk", 9600, 3000.0, 96000.0), ("qpsk", 19200, 3000.0, 96000.0), ("qpsk", 1200, 3000.0, 96000.0),
+                ("qpsk", 300, 3000.0, 96000.0), ("bpsk", 1200, 3000.0, 96000.0), ("qpsk", 2400, 1800.0, 44100.0)]
+
+
+@pytest.mark.parametrize("kind,baud,fc,fs", F32F_CONFIGS, ids=lambda v: str(v))
+def test_f32_handoff_error_below_its_bound(kind, baud, fc, fs, built_lib):
+    """The lane layout's float32 hand-off: the exact
+    band-pass output rounded to float32 before the low-pass moves the symbols
+    by at most f32_margin * max|f| (libamr.so's amr_psk_f32_margin: the
+    rounding through the low-pass's L1 gain -- a bound, not a fit).  Measured
+    on the same inputs as the time-split test; the ratio is printed."""
+    import _amr
+    from oracle import oracle
+    n = 48000
+    c = _amr.f32_margin(kind, n, baud, fc, fs)
+    assert c > 0
+    rng = np.random.default_rng(baud + 7)
+    worst = 0.0
+    for name, x in _inputs(kind, baud, fc, fs, n, rng).items():
+        ref = oracle.psk_symbols(kind, x, baud, fc, fs)
+        got, fpeak = oracle.psk_symbols_f32f(kind, x, baud, fc, fs)
+        worst = max(worst, np.abs(got - ref).max() / (c * fpeak + 2.0 ** -120))
+    print(f"{kind}@{baud} fc {fc:g}: f32 margin {c:.3e} x max|f|; worst error / bound {worst:.3f}")
+    assert worst <= 0.5
