@@ -328,14 +328,24 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 // 1024 waves fill the 1024 SIMDs at B = 16384 (the one-wave form: 512), and
 // phase 2 costs one recursion per sample instead of two.  Arithmetic and
 // order per recursion are those of k_fsk_bandpass (same outputs).
-constexpr int kFsk2Tile = 64;
-__host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n) { return (n / kFsk2Tile) * 6 * 64; }
+// AMR_FSK_TILE=64 (an A/B; default 32): samples per tile.  A tile of 64 held
+// 77 KB of LDS per workgroup (two re-run buffers of 64 samples x 64 lanes),
+// so two F1 workgroups filled a CU's LDS and no FFT-pass workgroup could sit
+// beside them; 32 halves that at twice the checkpoints (3 B per sample):
+// fsk9600 37.03-37.16 -> 34.68-34.79 ms/step, and 16 (four times the
+// checkpoints) measured 35.75-35.77 against 32's 35.38-35.60 on another box
+// (profiles/r05_fsk_f1_tile.txt)
+constexpr int kFsk2Tile = 32;
+constexpr int kFsk2TileMin = 32;
+__host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n, int tl = kFsk2Tile) {
+  return (n / tl) * 6 * 64;
+}
 
-template <typename T, int ZO, bool LIVE, bool W1S, bool AMB = false>
+template <typename T, int ZO, bool LIVE, bool W1S, bool AMB = false, int TLT = kFsk2Tile>
 __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x_stride, int64_t n_streams,
                                                        double* __restrict__ scratch, double2* __restrict__ z,
                                                        FskParams p, FskIir f) {
-  constexpr int TL = kFsk2Tile;
+  constexpr int TL = TLT;
   constexpr int RB = TL * (int)sizeof(T);           // bytes per stream row per tile
   constexpr int PITCH = RB + 16;
   constexpr int LPR = RB / 16;                      // lanes per row in a load
@@ -343,7 +353,9 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   constexpr int NI = 32 / RPI;                      // load instructions per tile
   constexpr int YP = 66;                            // yb pitch (doubles)
   __shared__ __attribute__((aligned(16))) uint8_t tin[1][32][PITCH];
-  __shared__ __attribute__((aligned(16))) double yb[2 * TL][YP];   // two tile buffers, or the tail (<= 2*TL rows)
+  // two tile buffers, or the tail's forward outputs (n % TL + pad <= TL - 1 + 21 rows)
+  constexpr int YR = 2 * TL > TL + 20 ? 2 * TL : TL + 20;
+  __shared__ __attribute__((aligned(16))) double yb[YR][YP];
   __shared__ double ylast_sh[64];
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -369,8 +381,8 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   const int pad = p.pad;
   const int64_t n_tiles = n / TL;
   const int64_t n_main = n_tiles * TL;
-  const int64_t ntail = n - n_main + pad;            // <= TL - 1 + 21 < 2 * TL
-  double* __restrict__ ck = scratch + (size_t)w * fsk2_scratch_doubles_per_group(n) + lane;
+  const int64_t ntail = n - n_main + pad;            // <= TL - 1 + 21 <= YR
+  double* __restrict__ ck = scratch + (size_t)w * fsk2_scratch_doubles_per_group(n, TL) + lane;
   double b[7], a[7], zs[6];
 #pragma unroll
   for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
@@ -601,7 +613,7 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
 }
 
 int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad) {
-  const int64_t per = std::max(fsk_scratch_doubles_per_wave(n, pad), fsk2_scratch_doubles_per_group(n));
+  const int64_t per = std::max(fsk_scratch_doubles_per_wave(n, pad), fsk2_scratch_doubles_per_group(n, kFsk2TileMin));
   return ((n_streams + 31) / 32) * per * (int64_t)sizeof(double);
 }
 
@@ -633,7 +645,16 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
   if (!fsk_one_wave() || p.xlist) {
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
-#define BP2(T, S, D) hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams, s1, z, p, f)
+    static const bool t64 = [] { const char* e = getenv("AMR_FSK_TILE"); return e && atoi(e) == 64; }();
+#define BP2(T, S, D)                                                                                                 \
+  do {                                                                                                               \
+    if (t64)                                                                                                         \
+      hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D, 64>), dim3(grid), dim3(128), 0, st, x, x_stride,         \
+                         n_streams, s1, z, p, f);                                                                    \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams,  \
+                         s1, z, p, f);                                                                               \
+  } while (0)
 #define BP2D(T) do { if (p.amb) { if (w1s) BP2(T, true, true); else BP2(T, false, true); } else if (w1s) BP2(T, true, false); else BP2(T, false, false); } while (0)
     switch (dtype) {
       case kF32: BP2D(float); break;
