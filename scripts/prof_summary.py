@@ -155,6 +155,9 @@ def main():
                                   "kernel_ms_hip_events": rl.get("kernel_ms_used"),
                                   "kernel_ms_hip_events_inflight": (rl.get("inflight") or {}).get("kernel_ms"),
                                   "ms_per_step": bench.get("ms_per_step"),
+                                  "streams_per_step": cfg.get("global_batch"),
+                                  "streams_per_launch": cfg.get("streams_per_launch"),
+                                  "frac": rl.get("frac"), "frac_throughput": rl.get("frac_throughput"),
                                   "value": bench.get("value"), "unit": bench.get("unit")}}
     with open(pmc_path, "w") as f:
         json.dump(allres, f, indent=1)
@@ -188,6 +191,15 @@ def main():
                         f"(timed launches): rocprofv3 {sl.get('avg_ns_timed_steps', 0) / 1e6:.3f} ms, HIP events "
                         f"{b.get('kernel_ms_hip_events_inflight')} ms; step {b.get('ms_per_step')} ms, "
                         f"{b.get('value')} {b.get('unit')}.\n")
+                spl, sps_ = b.get("streams_per_launch"), b.get("streams_per_step")
+                if b.get("ms_per_step") and spl and sps_:
+                    step_bytes = b["alg_bytes_per_launch"] / spl * sps_
+                    f.write(f"Throughput-consistent fraction (`frac_throughput`): the algorithmic bytes of a step "
+                            f"({step_bytes:,.0f} B) / the step time {b['ms_per_step']} ms = "
+                            f"{step_bytes / b['ms_per_step'] / 1e6:.2f} GB/s = "
+                            f"{step_bytes / b['ms_per_step'] / 1e6 / 8000:.5f} of 8000 GB/s (the bench line: "
+                            f"frac {b.get('frac')}, frac_throughput {b.get('frac_throughput')}); the solo duration "
+                            f"exceeds the step because {r.get('inflight')} launches overlap in the timed region.\n")
                 if sl.get("hbm_bytes_per_launch"):
                     f.write(f"HBM traffic of that slot per launch (FETCH_SIZE x2 + WRITE_SIZE): "
                             f"{sl['hbm_bytes_per_launch'] / 1e6:.1f} MB = "
