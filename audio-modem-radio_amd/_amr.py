@@ -47,6 +47,7 @@ EXPORTS = [
     "amr_psk_demod_host_async", "amr_fsk_demod_host_async", "amr_host_register", "amr_host_unregister",
     "amr_host_alloc", "amr_host_free",
     "amr_fsk_plan_create", "amr_fsk_plan_destroy", "amr_fsk_plan_out_capacity", "amr_fsk_plan_scratch_bytes",
+    "amr_fsk_plan_resident_bytes",
     "amr_fsk_plan_fft_length", "amr_fsk_plan_live_columns", "amr_fsk_plan_synchronize", "amr_fsk_plan_enable_timing", "amr_fsk_plan_timings",
     "amr_fsk_demod_host", "amr_fsk_demod_device", "amr_fsk_envelopes_host", "amr_fft_c2c_host", "amr_hilbert_host",
     "amr_fec_decode_host", "amr_frame_parse_host", "amr_frame_parse_device", "amr_comm_unique_id", "amr_comm_create", "amr_comm_destroy", "amr_allgather", "amr_fsk_allgather",
@@ -225,6 +226,7 @@ def lib():
             "amr_fsk_plan_destroy": (I32, [P]),
             "amr_fsk_plan_out_capacity": (I64, [P]),
             "amr_fsk_plan_scratch_bytes": (I64, [P]),
+            "amr_fsk_plan_resident_bytes": (I64, [P]),
             "amr_fsk_plan_fft_length": (I64, [P]),
             "amr_fsk_plan_live_columns": (I32, [P]),
             "amr_fsk_plan_synchronize": (I32, [P]),

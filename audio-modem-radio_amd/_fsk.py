@@ -111,6 +111,10 @@ class FskPlan:
         """Device bytes this plan holds (scratch + host-API staging)."""
         return int(lib().amr_fsk_plan_scratch_bytes(self.handle)) if self.handle else 0
 
+    def resident_bytes(self) -> int:
+        """Device bytes allocated now (a device-entry-only plan holds no host staging)."""
+        return int(lib().amr_fsk_plan_resident_bytes(self.handle)) if self.handle else 0
+
     def enable_timing(self, on=True):
         check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
 

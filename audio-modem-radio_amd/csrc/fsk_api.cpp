@@ -337,9 +337,15 @@ struct amr_fsk_plan {
   // keep_z (live layout with the exact path): the column pass writes the dead
   // tiles' transform to dd [B][nd * n2] instead of over z's dead columns, so
   // all of z (the band-pass output) survives F2 for the exact path; dd also
-  // takes the host entries' staged input (>= 8 B per sample: nd >= n1 / 2)
+  // takes the host entries' staged input (>= 8 B per sample: nd >= n1 / 2).
+  // dd (9.6 B per sample at FSK9600) is allocated by the first host entry,
+  // which needs a staging buffer anyway; until then the device entries run
+  // lean -- dead tiles in place, a flagged stream's F1 re-run from the
+  // caller's x (E1) -- so a device-entry plan holds z + C only
+  // (AMR_FSK_KEEPZ=1: dd at creation, every call keeps z; =0: never)
   double2* dd = nullptr;
-  bool keep_z = false;
+  bool keep_z = false;         // the plan can keep z (dd sized); a call does when dd is allocated
+  int64_t dd_bytes = 0;
   int64_t staging_bytes = 0;   // d_x of the host entries (0 with keep_z)
   int64_t u_bytes = 0;
   uint8_t* cmp = nullptr;      // [B][bits_stride] packed compare bits (fft.h fft_bits_stride)
@@ -421,6 +427,9 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   delete pl;
 }
 
+// this call keeps z whole through F2 (dd allocated: see amr_fsk_plan::dd)
+bool keeps_z(const amr_fsk_plan* pl) { return pl->keep_z && pl->dd != nullptr; }
+
 hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which, hipStream_t st = nullptr) {
   if (!pl->timing) return hipSuccess;
   pl->ev_used[slot] = true;
@@ -474,7 +483,7 @@ int run_fsk_f2(amr_fsk_plan* pl, int64_t B, bool env_out) {
       if (e.amb) e.amb += b0;
       if (e.xflags) e.xflags += b0 / 32;
       HIP_TRY(launch_fft_hilbert_live(pl->z + b0 * pl->p.n, pl->u + b0 * (int64_t)lc.nl * lc.n2,
-                                      pl->keep_z ? pl->dd + b0 * (int64_t)lc.nd * lc.n2 : nullptr, pl->fft.d, nb, lc,
+                                      keeps_z(pl) ? pl->dd + b0 * (int64_t)lc.nd * lc.n2 : nullptr, pl->fft.d, nb, lc,
                                       e, pl->stream));
     }
   } else {
@@ -504,7 +513,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
   X.list = pl->xlist;
   X.count = pl->xlist + pl->max_streams;
   X.rows = reinterpret_cast<double*>(pl->z);
-  X.live = pl->keep_z ? 1 : 0;
+  X.live = keeps_z(pl) ? 1 : 0;
   X.lc = pl->p.lc;
   X.slots = pl->xslots;
   X.slot_doubles = pl->slot_doubles;
@@ -551,7 +560,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     }
     X.count_hint = c;
   }
-  if (!pl->keep_z) {
+  if (!X.live) {
     // E1: F1 again over the flagged streams only (list mode), natural z layout
     FskParams p1 = pl->p;
     p1.amb = nullptr;
@@ -630,6 +639,10 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
 // else d_x, where it stays for the exact path's F1 re-run after F2.
 int staging_buffer(amr_fsk_plan* pl, void** buf) {
   if (pl->keep_z) {
+    if (!pl->dd) {
+      HIP_TRY(hipMalloc(&pl->dd, (size_t)pl->dd_bytes));
+      pl->scratch_bytes += pl->dd_bytes;
+    }
     *buf = pl->dd;
     return AMR_OK;
   }
@@ -702,6 +715,7 @@ struct FskGeom {
   FftShape sh;
   int64_t z = 0, u = 0, v = 0, dd = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
   bool keep_z = false;
+  bool dd_eager = false;   // AMR_FSK_KEEPZ=1: dd at creation (else on the first host entry)
   // the exact path: flags, scales, list, slots, exact bits, pocketfft tables
   bool exact = false;
   int n_slots = 0;
@@ -770,9 +784,11 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
       const char* f = std::getenv("AMR_FSK_F1_FMA");
       return !(e && e[0] == '0') && !(f && f[0] == '1');
     }();
+    static const bool eager_env = [] { const char* e = std::getenv("AMR_FSK_KEEPZ"); return e && e[0] == '1'; }();
     g.keep_z = keepz_env && p.lc.on && (int64_t)p.lc.nd * p.lc.n2 * 2 >= n;
     if (g.keep_z) {
-      g.dd = max_streams * (int64_t)p.lc.nd * p.lc.n2 * 16;
+      g.dd = max_streams * (int64_t)p.lc.nd * p.lc.n2 * 16;   // counted: a host entry allocates it
+      g.dd_eager = eager_env;
       g.staging = 0;
     }
   }
@@ -840,12 +856,13 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   if (pl->fft.six) pl->scratch_bytes += geo.six;
   pl->u_bytes = geo.u;
   pl->staging_bytes = geo.staging;
+  pl->dd_bytes = geo.dd;
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, geo.z},
       {(void**)&pl->u, geo.u},
       {(void**)&pl->v, geo.v},
-      {(void**)&pl->dd, geo.dd},
+      {(void**)&pl->dd, geo.dd_eager ? geo.dd : 0},
       {(void**)&pl->cmp, geo.cmp},
       {(void**)&pl->words, geo.words},
       {(void**)&pl->xflags, geo.xflags},
@@ -931,9 +948,17 @@ int amr_fsk_plan_destroy(amr_fsk_plan* plan) {
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan* plan) { return plan ? plan->out_cap : -1; }
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
-  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host)
-  return plan->scratch_bytes + plan->staging_bytes +
+  // scratch + the host-API staging (allocated on the first amr_fsk_demod_host:
+  // d_x, or dd on a plan that keeps z)
+  return plan->scratch_bytes + plan->staging_bytes + (plan->dd ? 0 : plan->dd_bytes) +
          plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
+}
+int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
+  if (!plan) return -1;
+  // what is allocated now: a plan that only ever ran the device entry holds
+  // no staging (no d_x, no dd, no output staging)
+  return plan->scratch_bytes + (plan->d_x ? plan->staging_bytes : 0) +
+         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }

@@ -190,8 +190,8 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
     # launch holds >= 4096 streams (what one batch of the headline holds); the
     # timed region is still exactly K steps (the last launch may be partial)
     C, BL, n_launch, launch_sizes = launch_plan(K, B, strong, args.coalesce)
-    # fsk9600: 4 in flight (amr_fsk_plan_bytes_estimate per 16384-stream plan; K = 64,
-    # one MI355X, round 3: P = 2 34.4 ms/step, 3 33.7, 4 33.1)
+    # fsk9600: 4 in flight (a device-entry 16384-stream plan holds ~37 GB, `plan_bytes` in the line,
+    # DESIGN.md §3b; round 5, one MI355X: P = 3 35.85 ms/step, 4 35.30, 5 35.22)
     P = args.inflight or (min(4, max(1, n_launch // 2)) if fsk else default_inflight(n_launch, 20 if BL <= 4096 else 16))
 
     # ---- inputs: clean frames on the host, one noisy batch per slot in HBM ----
@@ -634,6 +634,12 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
         if gather_check is not None:
             result["gather_check"] = gather_check
         result["exact_path_streams"] = sum(pl.exact_streams() for pl in plans)
+        if fsk:
+            # device memory per plan: what the device entry holds (no dd, no
+            # staging) beside what a host-entry plan of this shape takes
+            result["plan_bytes"] = {"resident_per_plan": plans[0].resident_bytes(),
+                                    "host_entry_plan": plans[0].scratch_bytes(), "plans": P,
+                                    "resident_all_plans": sum(pl.resident_bytes() for pl in plans)}
 
         # PCIe-inclusive rate (never `value`): the host API on the
         # same batch from host memory, H2D + demod + D2H, one batch at a time
@@ -1034,7 +1040,7 @@ def main():
                                                 "kernel_ms_solo", "cpu_baseline", "config")}
                 subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "frac_throughput", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
-                for k in ("gather_check", "exact_path_streams", "exact_probe"):
+                for k in ("gather_check", "exact_path_streams", "exact_probe", "plan_bytes"):
                     if k in r:
                         subs[name][k] = r[k]
         if rank == 0 and result is not None:

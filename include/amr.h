@@ -61,7 +61,7 @@ extern "C" {
                                  amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT
                                3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info,
                                   amr_psk_split_design, amr_psk_split_symbols_host, the float32 hand-off
-                                  (amr_psk_f32_margin, amr_psk_plan_last_f32f) */
+                                  (amr_psk_f32_margin, amr_psk_plan_last_f32f), amr_fsk_plan_resident_bytes */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -263,6 +263,10 @@ int amr_fsk_plan_create(amr_fsk_plan **plan, int device, int64_t n_samples, int6
 int amr_fsk_plan_destroy(amr_fsk_plan *plan);
 int64_t amr_fsk_plan_out_capacity(const amr_fsk_plan *plan);
 int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan *plan);
+/* device bytes the plan holds now: scratch_bytes less what the host entries
+   allocate on their first call (input / output staging; on a live-layout plan
+   the buffer that keeps z through F2) -- a device-entry-only plan's footprint */
+int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan *plan);
 /* the amr_fsk_plan_scratch_bytes a plan of this shape would report, without creating it */
 int64_t amr_fsk_plan_bytes_estimate(int64_t n_samples, int64_t sps, int ntaps, int64_t max_streams);
 /* FFT length actually run: n_samples, or the Bluestein length when n is not 5-smooth */

@@ -333,6 +333,62 @@ def test_fsk_quiet_stretches_exact(kind, n):
     print(f"n={n} {kind}: {pl.exact_streams()} of {B} flagged")
 
 
+def _fsk_device_demod(pl, x):
+    """amr_fsk_demod_device on x copied to device memory: (bytes list, sync)."""
+    import ctypes
+    import _amr
+    L = _amr.lib()
+    B, n = x.shape
+    cap = max(pl.out_cap, 1)
+    ptrs = {}
+    for name, nbytes in (("x", x.nbytes), ("out", B * cap), ("len", B * 8), ("sync", B * 8)):
+        p = ctypes.c_void_p()
+        _amr.check(L.amr_malloc(ctypes.byref(p), nbytes))
+        ptrs[name] = p
+    try:
+        _amr.check(L.amr_memcpy_h2d(ptrs["x"], _amr.ptr(x), x.nbytes))
+        _amr.check(L.amr_fsk_demod_device(pl.handle, ptrs["x"], _amr.DTYPES[x.dtype], B, n, ptrs["out"], cap,
+                                          ptrs["len"], ptrs["sync"]))
+        _amr.check(L.amr_fsk_plan_synchronize(pl.handle))
+        out, ln, sy = np.empty((B, cap), np.uint8), np.empty(B, np.int64), np.empty(B, np.int64)
+        for name, h in (("out", out), ("len", ln), ("sync", sy)):
+            _amr.check(L.amr_memcpy_d2h(_amr.ptr(h), ptrs[name], h.nbytes))
+    finally:
+        for p in ptrs.values():
+            L.amr_free(p)
+    return [out[i, :ln[i]].tobytes() for i in range(B)], sy
+
+
+def test_fsk_device_entry_lean_plan():
+    """A live-layout plan that only ran the device entry holds z and C, not
+    the buffer that keeps z through F2 (dd: 9.6 B per sample at FSK9600) --
+    its flagged streams re-run F1 from the caller's x (E1) instead.  The
+    first host entry allocates dd (it is also that entry's staging) and every
+    later call keeps z.  Bytes == the oracle's in both modes, on a batch with
+    digital silence (flagged streams)."""
+    import _fsk
+    from oracle import oracle
+    n, baud, mark, space, B = 96000, 9600, 12000.0, 24000.0, 8
+    x = _silence_batch(np.random.default_rng(7), B, n, baud, mark, space, np.float32)
+    want = [oracle.fsk_demodulate(r, baud, mark, space) for r in x]
+    pl = _fsk.FskPlan(n, baud, mark, space, max_streams=B)
+    assert pl.live_columns
+    total = pl.scratch_bytes()
+    lean = pl.resident_bytes()
+    dd = B * n * 6 // 10 * 16            # the dead columns' transform: nd / n1 = 6 / 10 at sps 10
+    assert total - lean >= dd, (total, lean, dd)
+    got, _ = _fsk_device_demod(pl, x)
+    assert pl.exact_streams() > 0
+    assert got == want
+    assert pl.resident_bytes() == lean               # the device entry allocated nothing
+    got_h, _ = pl.demod_host(x)
+    assert got_h == want and pl.exact_streams() > 0
+    assert pl.resident_bytes() == total == pl.scratch_bytes()
+    got2, _ = _fsk_device_demod(pl, x)               # now keeping z
+    assert got2 == want
+    print(f"plan bytes: device entry only {lean / 1e6:.1f} MB, after a host entry {total / 1e6:.1f} MB")
+
+
 def test_fsk_every_stream_exact_on_golden(golden):
     """The exact path alone (exact mode 2: every stream recomputed) on every
     golden FSK case through a plan: bytes == the reference's -- the exact
@@ -453,9 +509,10 @@ sys.exit(1 if bad else 0)
 
 
 def test_fsk_live_async_host_entry():
-    """amr_fsk_demod_host_async on a live-column plan: the input is staged in
-    C in chunks on the plan's stream (float64: 2 chunks for 64 streams) while
-    nothing waits on the host; == the synchronous entry == oracle."""
+    """amr_fsk_demod_host_async on a live-column plan: the input is staged on
+    the plan's stream (into dd, the buffer that keeps z through F2, allocated
+    by this first host entry) while nothing waits on the host; == the
+    synchronous entry == oracle."""
     import _amr
     import _fsk
     import synth
