@@ -55,6 +55,7 @@ EXPORTS = [
     "amr_resample_host", "amr_hilbert_env_exact_host", "amr_fsk_plan_exact_streams",
     "amr_fsk_plan_set_exact_mode", "amr_psk_plan_set_layout", "amr_psk_plan_split_info", "amr_psk_split_design",
     "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f",
+    "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -254,6 +255,10 @@ def lib():
             "amr_hilbert_env_exact_host": (I32, [P, I64, I64, P, I32]),
             "amr_fsk_plan_exact_streams": (I32, [P, P]),
             "amr_fsk_plan_set_exact_mode": (I32, [P, I32]),
+            "amr_fsk_plan_set_layout": (I32, [P, I32]),
+            "amr_fsk_plan_split_info": (I32, [P, P, P, P, P, P]),
+            "amr_fsk_split_design": (I32, [I64, P, P, P, P, I32, P, P, P]),
+            "amr_fsk_split_bandpass_host": (I32, [P, P, I32, I64, I64, I64, P]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
             "amr_modulate_host": (I32, [I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64]),
             "amr_modulate_device": (I32, [P, I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64, P, I64]),

@@ -35,6 +35,22 @@ def design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
     return sps, out
 
 
+FSK_LAYOUTS = {"auto": 0, "serial": 1, "split": 2}
+
+
+def split_design(n: int, baud, mark_freq, space_freq, samp_rate=96000):
+    """The FSK time-split design (host arithmetic in libamr.so, no device):
+    dict of warmup, kappa, hilbert_l1, tau (F2's margin scale for split calls),
+    or None when the filters cannot be split at this length."""
+    _, ((mb, ma, _), (sb, sa, _)) = design_fsk(n, baud, mark_freq, space_freq, samp_rate)
+    w, k, h = ctypes.c_int64(0), ctypes.c_double(0.0), ctypes.c_double(0.0)
+    rc = lib().amr_fsk_split_design(int(n), ptr(mb), ptr(ma), ptr(sb), ptr(sa), len(mb), ctypes.byref(w),
+                                    ctypes.byref(k), ctypes.byref(h))
+    if rc != 0:
+        return None
+    return {"warmup": w.value, "kappa": k.value, "hilbert_l1": h.value, "tau": 2.0 ** -36 + k.value * h.value}
+
+
 class FskPlan:
     """A device plan: both tones' coefficients, the FFT tables and HBM scratch."""
 
@@ -117,6 +133,29 @@ class FskPlan:
 
     def enable_timing(self, on=True):
         check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
+
+    def set_layout(self, layout: str):
+        """F1 per call: "auto" (split for <= 16 streams), "serial", "split" (include/amr.h)."""
+        check(lib().amr_fsk_plan_set_layout(self.handle, FSK_LAYOUTS[layout]))
+
+    def split_info(self) -> dict:
+        """The last call's F1 layout and the plan's split design."""
+        ls, w, L = ctypes.c_int(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        k, t = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        check(lib().amr_fsk_plan_split_info(self.handle, ctypes.byref(ls), ctypes.byref(w), ctypes.byref(L),
+                                            ctypes.byref(k), ctypes.byref(t)))
+        return {"last_split": bool(ls.value), "warmup": w.value, "chunk": L.value, "kappa": k.value, "tau": t.value}
+
+    def split_bandpass(self, x: np.ndarray, chunk: int = 0) -> np.ndarray:
+        """The split F1's output [B][n][2] (mark, space): a diagnostic."""
+        x = np.ascontiguousarray(x)
+        if x.dtype not in _amr.DTYPES:
+            x = np.ascontiguousarray(x, np.float64)
+        out = np.empty((x.shape[0], self.n, 2))
+        with self.lock:
+            check(lib().amr_fsk_split_bandpass_host(self.handle, ptr(x), _amr.DTYPES[x.dtype], x.shape[0], x.shape[1],
+                                                    int(chunk), ptr(out)))
+        return out
 
     def set_exact_mode(self, mode: int):
         """0 off, 1 the streams F2 flags (default), 2 every stream (include/amr.h)."""

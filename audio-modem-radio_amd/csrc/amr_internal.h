@@ -179,12 +179,28 @@ constexpr double kAmbTau = 0x1p-36;
 // c = 8 (tau peak)^2 (fft_kernels.hip env_ambiguous compares squares);
 // -1 for a stream of exact zeros (both paths' envelopes are exact zeros),
 // +inf for tiny / huge / non-finite input (every compare goes exact)
-__host__ __device__ inline double amb_scale(double peak) {
+__host__ __device__ inline double amb_scale(double peak, double tau = kAmbTau) {
   if (peak == 0.0) return -1.0;
   if (!(peak >= 0x1p-400 && peak <= 0x1p400)) return __builtin_inf();
-  const double d = kAmbTau * peak;
+  const double d = tau * peak;
   return 8.0 * d * d;
 }
+
+// FSK time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3b "time-split F1"):
+// each filtfilt pass of both tones cut into chunks of L outputs, one lane per
+// (chunk, tone), every chunk started w samples early from a zero state.  Its
+// band-pass output is within kappa * peak|ext x| of scipy's, so each envelope
+// is within (kAmbTau + tau_env) * peak of the reference's, tau_env = kappa *
+// ||ifft(h)||_1 (scipy.signal.hilbert's kernel), and F2 flags with that
+// margin instead of kAmbTau's; flagged streams re-run the serial F1 (E1).
+struct FskSplit {
+  int64_t L;                  // outputs per chunk
+  int64_t w;                  // warm-up samples (both passes, both tones)
+  int64_t c;                  // chunks per pass: ceil(m1 / L), m1 = n + 2 pad
+  double tau;                 // kAmbTau + tau_env: F2's margin scale for these streams
+  double* y1;                 // [B][2][m1] forward outputs (tone-major per stream)
+  unsigned long long* peak;   // [B] bits of max |ext x| (cleared per launch)
+};
 
 struct FskIir {            // [tone][tap], tone 0 = mark
   double b[2][8];

@@ -15,6 +15,7 @@
 
 #include "amr_internal.h"
 #include "api_common.h"
+#include "iir_design.h"
 
 namespace amr {
 hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
@@ -745,68 +746,7 @@ int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
 
 namespace {
 
-// ---- time-split layout design ------------------------------
-// The DF-II-T's responses with zero input (scipy's recursion, a[0] = 1):
-//   g_i  the output after a unit error in state i -- how one step's rounding
-//        in state i reaches the output; g1 = sum_i sum_m |g_i(m)|, and
-//        tail(m) = sup_{m' >= m} sum_i |g_i(m')| (what a state error left m
-//        steps back still contributes);
-//   h    the output and states after a unit input sample: h1 = ||h||_1 (the
-//        L1 gain), zmax = max_i ||h_{x -> z_i}||_1 (a state per unit input peak).
-struct IirGains {
-  double g1 = 0.0, h1 = 0.0, zmax = 0.0;
-  std::vector<double> tail;
-  bool ok = false;
-};
-IirGains iir_gains(const Iir& f) {
-  IirGains r;
-  const int N = f.nt - 1;
-  constexpr int64_t kMaxSteps = 4000000;
-  std::vector<double> zs((size_t)N * N, 0.0);
-  for (int i = 0; i < N; ++i) zs[(size_t)i * N + i] = 1.0;
-  bool decayed = false;
-  for (int64_t m = 0; m < kMaxSteps && !decayed; ++m) {
-    double t = 0.0, live = 0.0;
-    for (int i = 0; i < N; ++i) {
-      double* z = &zs[(size_t)i * N];
-      const double y = z[0];
-      for (int j = 0; j < N - 1; ++j) z[j] = z[j + 1] - f.a[j + 1] * y;
-      z[N - 1] = -f.a[N] * y;
-      t += std::fabs(y);
-      for (int j = 0; j < N; ++j) live = std::max(live, std::fabs(z[j]));
-    }
-    r.g1 += t;
-    r.tail.push_back(t);
-    decayed = live < 1e-40 && m > 4 * N;
-  }
-  if (!decayed || !std::isfinite(r.g1)) return r;
-  for (int64_t m = (int64_t)r.tail.size() - 2; m >= 0; --m) r.tail[(size_t)m] = std::max(r.tail[(size_t)m], r.tail[(size_t)m + 1]);
-  std::vector<double> z(N, 0.0), zsum(N, 0.0);
-  double x = 1.0;
-  decayed = false;
-  for (int64_t m = 0; m < kMaxSteps && !decayed; ++m) {
-    const double y = z[0] + f.b[0] * x;
-    for (int j = 0; j < N - 1; ++j) z[j] = z[j + 1] + f.b[j + 1] * x - f.a[j + 1] * y;
-    z[N - 1] = f.b[N] * x - f.a[N] * y;
-    r.h1 += std::fabs(y);
-    double live = 0.0;
-    for (int j = 0; j < N; ++j) {
-      zsum[j] += std::fabs(z[j]);
-      live = std::max(live, std::fabs(z[j]));
-    }
-    x = 0.0;
-    decayed = live < 1e-40 && m > 4 * N;
-  }
-  r.zmax = *std::max_element(zsum.begin(), zsum.end());
-  r.ok = decayed && std::isfinite(r.h1) && std::isfinite(r.zmax);
-  return r;
-}
-// the first m with tail(m) * scale <= tol (-1: none within the response)
-int64_t warmup_for(const IirGains& g, double scale, double tol) {
-  for (size_t m = 0; m < g.tail.size(); ++m)
-    if (g.tail[m] * scale <= tol) return (int64_t)m;
-  return -1;
-}
+// ---- time-split layout design (the filters' responses: iir_design.h)
 // A chunked pass differs from the serial one by (1) the zero start state,
 // decayed after w samples to at most tail(w) * zmax * (the pass's input peak)
 // at the pass's output, then amplified by the later passes' L1 gains -- w is

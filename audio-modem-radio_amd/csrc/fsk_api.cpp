@@ -22,11 +22,14 @@
 #include "api_common.h"
 #include "fsk_exact.h"
 #include "fft.h"
+#include "iir_design.h"
 
 namespace amr {
 hipError_t launch_fsk_bandpass(int, const void*, int64_t, int64_t, double*, double2*, const FskParams&,
                                const FskIir&, hipStream_t);
 hipError_t launch_fsk_decide(const uint8_t*, uint32_t*, int64_t, const FskParams&, hipStream_t);
+hipError_t launch_fsk_split(int, const void*, int64_t, int64_t, double2*, const FskParams&, const FskIir&,
+                            const FskSplit&, hipStream_t);
 int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad);
 hipError_t launch_sync_pack(const uint32_t*, int64_t, int64_t, int64_t, uint8_t*, int64_t, int64_t*, int64_t*,
                             hipStream_t);
@@ -391,6 +394,22 @@ struct amr_fsk_plan {
   bool ran_exact = false;      // the last call ran the exact path (its count is in xlist[max_streams])
   int exact_mode = 1;          // amr_fsk_plan_set_exact_mode: 0 off, 1 F2's flags, 2 every stream
   int64_t scratch_bytes = 0;
+  // the time-split F1 (fsk_kernels.hip FS1-FS3): designed
+  // with the plan; used for calls of at most kFskSplitMaxStreams streams
+  // (amr_fsk_plan_set_layout overrides); its forward outputs and peaks in
+  // split_y1 / split_peak, allocated on the first split call
+  bool split_ok = false;
+  int64_t split_w = 0;
+  double split_kappa = 0.0, split_hl1 = 0.0, split_tau = 0.0;
+  int split_mode = AMR_FSK_LAYOUT_AUTO;
+  bool split_now = false;      // this call runs the split F1 (z approximate: no keep_z, E1 re-runs F1)
+  bool last_split = false;
+  int64_t split_L = 0;
+  double* split_y1 = nullptr;
+  unsigned long long* split_peak = nullptr;
+  int64_t split_cap = 0;       // streams split_y1 / split_peak hold
+  int64_t split_alloc = 0;     // their bytes (not in scratch_bytes)
+  int64_t split_reserved = 0;  // what amr_fsk_plan_bytes_estimate counts for them (<= 16 streams)
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
   void* d_x = nullptr;
@@ -413,7 +432,8 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   if (pl->xcount_host) (void)hipHostFree(pl->xcount_host);
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
-                  (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL})
+                  (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL,
+                  (void*)pl->split_y1, (void*)pl->split_peak})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -427,8 +447,9 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   delete pl;
 }
 
-// this call keeps z whole through F2 (dd allocated: see amr_fsk_plan::dd)
-bool keeps_z(const amr_fsk_plan* pl) { return pl->keep_z && pl->dd != nullptr; }
+// this call keeps z whole through F2 (dd allocated: see amr_fsk_plan::dd;
+// a split call's z is not scipy's, so the exact path re-runs F1 instead)
+bool keeps_z(const amr_fsk_plan* pl) { return pl->keep_z && pl->dd != nullptr && !pl->split_now; }
 
 hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which, hipStream_t st = nullptr) {
   if (!pl->timing) return hipSuccess;
@@ -438,10 +459,61 @@ hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which, hipStream_t st = null
 
 // F1 over the B streams of x -> z (and, with the exact path on, each
 // stream's ambiguity scale; the flag words cleared).  Caller holds mu.
+constexpr int64_t kFskSplitMaxStreams = 16;   // AUTO: calls of at most this many streams split
+
+// The split F1's launch geometry: L outputs per chunk (at least
+// kFskSplitMinL and w / 4, so warm-ups are at most 4x the useful work, and
+// long enough to keep a launch within kFskSplitLanes lanes)
+constexpr int64_t kFskSplitMinL = 64;
+constexpr int64_t kFskSplitLanes = 65536;
+FskSplit fsk_split_params(amr_fsk_plan* pl, int64_t B, int64_t L) {
+  FskSplit sp{};
+  const int64_t m1 = pl->p.n + 2 * (int64_t)pl->p.pad;
+  sp.L = L > 0 ? L : std::max({kFskSplitMinL, pl->split_w / 4, (2 * B * m1 + kFskSplitLanes - 1) / kFskSplitLanes});
+  sp.w = pl->split_w;
+  sp.c = (m1 + sp.L - 1) / sp.L;
+  sp.tau = pl->split_tau;
+  sp.y1 = pl->split_y1;
+  sp.peak = pl->split_peak;
+  pl->split_L = sp.L;
+  return sp;
+}
+int ensure_split_buffers(amr_fsk_plan* pl, int64_t B) {
+  if (B <= pl->split_cap) return AMR_OK;
+  const int64_t m1 = pl->p.n + 2 * (int64_t)pl->p.pad;
+  if (pl->split_y1 || pl->split_peak) {
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    (void)hipFree(pl->split_y1);
+    (void)hipFree(pl->split_peak);
+    pl->split_y1 = nullptr;
+    pl->split_peak = nullptr;
+    pl->split_alloc = 0;
+    pl->split_cap = 0;
+  }
+  HIP_TRY(hipMalloc(&pl->split_y1, (size_t)(B * 2 * m1 * 8)));
+  HIP_TRY(hipMalloc(&pl->split_peak, (size_t)(B * 8)));
+  pl->split_cap = B;
+  pl->split_alloc = B * (2 * m1 * 8 + 8);
+  return AMR_OK;
+}
+// does this call run the split F1?  Only with the exact path on (it is what
+// makes the split's decisions exact)
+bool use_split(const amr_fsk_plan* pl, int64_t B) {
+  static const bool env_off = [] { const char* e = std::getenv("AMR_FSK_SPLIT"); return e && e[0] == '0'; }();
+  if (!pl->split_ok || !pl->exact_on || pl->exact_mode == 0 || pl->p.n_bits == 0 || B < 1 || B > 65535) return false;
+  if (pl->split_mode == AMR_FSK_LAYOUT_SPLIT) return true;
+  return pl->split_mode == AMR_FSK_LAYOUT_AUTO && !env_off && B <= kFskSplitMaxStreams;
+}
+
 int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool exact) {
   FskParams p = pl->p;
   if (!(exact && pl->exact_on && pl->exact_mode != 0)) p.amb = nullptr;
   p.force_exact = pl->exact_mode == 2 ? 1 : 0;
+  if (pl->split_now) {
+    if (int rc = ensure_split_buffers(pl, B)) return rc;
+    HIP_TRY(launch_fsk_split(dtype, d_x, x_stride, B, pl->z, p, pl->f, fsk_split_params(pl, B, 0), pl->stream));
+    return AMR_OK;
+  }
   HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p, pl->f,
                               pl->stream));
   return AMR_OK;
@@ -580,6 +652,7 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
 
 // F1, F2 (and the exact path) on a device-resident batch: x -> cmp (or the envelopes).  Caller holds mu.
 int run_fsk_front(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, bool env_out) {
+  if (env_out) pl->split_now = false;        // the envelopes themselves: scipy's F1
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 0));
   if (int rc = run_fsk_f1(pl, d_x, dtype, B, x_stride, !env_out)) return rc;
   HIP_TRY(mark_fsk(pl, AMR_TF_BANDPASS, 1));
@@ -625,6 +698,8 @@ int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   if (int rc = check_fsk_args(pl, dtype, B, x_stride, out_stride)) return rc;
   for (bool& u : pl->ev_used) u = false;
   pl->ran_exact = false;
+  pl->split_now = use_split(pl, B);
+  pl->last_split = pl->split_now;
   if (B == 0) return AMR_OK;
   if (pl->p.n_bits == 0) return fsk_empty_outputs(pl, B, d_len, d_sync);
   HIP_TRY(mark_fsk(pl, AMR_TF_LAUNCH, 0));
@@ -714,6 +789,7 @@ struct FskGeom {
   FskParams p{};
   FftShape sh;
   int64_t z = 0, u = 0, v = 0, dd = 0, cmp = 0, words = 0, six = 0, staging = 0, out = 0, out_cap = 0;
+  int64_t split = 0;       // the split F1's buffers for up to kFskSplitMaxStreams streams (allocated on use)
   bool keep_z = false;
   bool dd_eager = false;   // AMR_FSK_KEEPZ=1: dd at creation (else on the first host entry)
   // the exact path: flags, scales, list, slots, exact bits, pocketfft tables
@@ -721,7 +797,8 @@ struct FskGeom {
   int n_slots = 0;
   int64_t slot_doubles = 0, xflags = 0, amb = 0, xlist = 0, xslots = 0, xbits = 0, xpool = 0, xplan = 0;
   int64_t total() const {
-    return z + u + v + dd + cmp + words + six + staging + out + xflags + amb + xlist + xslots + xbits + xpool + xplan;
+    return z + u + v + dd + cmp + words + six + staging + out + xflags + amb + xlist + xslots + xbits + xpool + xplan +
+           split;
   }
 };
 bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& g) {
@@ -757,6 +834,7 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
   g.out = max_streams * (g.out_cap + 16);            // host-API output staging
+  g.split = std::min<int64_t>(max_streams, kFskSplitMaxStreams) * (2 * (n + 2 * (int64_t)p.pad) * 8 + 8);
   // the exact path (AMR_FSK_EXACT=0: off), at every length with decisions to make
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
   g.exact = exact_env && p.n_bits > 0;
@@ -795,9 +873,72 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   return true;
 }
 
+// The split F1's design (the PSK layout's rule, iir_design.h):
+// per tone, a chunk's outputs differ from scipy's by (1) the zero start,
+// decayed after w samples to tail(w) * zmax * 3 peak (the odd extension
+// triples the input peak) and carried through the backward pass (its L1 gain
+// h1) -- w is chosen to bring that below u G / 16 -- and (2) a different
+// rounding trajectory, G = g1 (1 + h1): the forward pass's rounding (noise
+// gain g1) filtered backward, plus the backward pass's own.  kappa = 64.25 u
+// G over the tones (measured >= 30x above the worst error,
+// tests/test_split_margin.py); an envelope then moves by at most kappa *
+// ||ifft(h)||_1 * peak|ext x|, the margin F2 adds for split calls.  Refused
+// when a warm-up exceeds n / 4 or the margin would pass 2^-24 of the peak.
+constexpr double kFskSplitSafety = 64.0;
+bool fsk_split_design(const FskIir& f, int nt, int64_t n, int64_t* w_out, double* kappa_out, double* hl1_out) {
+  if (nt != 7 || n < 64) return false;
+  const double u = 0x1p-53;
+  IirGains g[2];
+  double G = 0.0;
+  for (int t = 0; t < 2; ++t) {
+    Iir fi{};
+    fi.nt = nt;
+    for (int i = 0; i < nt; ++i) {
+      fi.b[i] = f.b[t][i];
+      fi.a[i] = f.a[t][i];
+    }
+    g[t] = iir_gains(fi);
+    if (!g[t].ok) return false;
+    G = std::max(G, g[t].g1 * (1.0 + g[t].h1));
+  }
+  const double tol = 0x1p-4 * u * G;
+  int64_t w = 0;
+  for (int t = 0; t < 2; ++t) {
+    const int64_t wt = warmup_for(g[t], g[t].zmax * 3.0 * g[t].h1, tol);
+    if (wt < 0) return false;
+    w = std::max(w, wt);
+  }
+  const double kappa = (kFskSplitSafety + 0.25) * u * G;
+  const double hl1 = hilbert_l1(n) * (1.0 + 0x1p-20);
+  if (w > n / 4 || !(kappa * hl1 <= 0x1p-16)) return false;
+  *w_out = w;
+  *kappa_out = kappa;
+  *hl1_out = hl1;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+int amr_fsk_split_design(int64_t n, const double* mb, const double* ma, const double* sb, const double* sa, int nt,
+                         int64_t* warmup, double* kappa, double* hilbert_l1_out) {
+  if (!mb || !ma || !sb || !sa || nt != 7) return fail(AMR_E_INVALID, "amr_fsk_split_design: bad argument");
+  FskIir f{};
+  for (int i = 0; i < nt; ++i) {
+    f.b[0][i] = mb[i];
+    f.a[0][i] = ma[i];
+    f.b[1][i] = sb[i];
+    f.a[1][i] = sa[i];
+  }
+  int64_t w = 0;
+  double k = 0.0, h = 0.0;
+  if (!fsk_split_design(f, nt, n, &w, &k, &h)) return fail(AMR_E_INVALID, "no time-split design for these filters at n");
+  if (warmup) *warmup = w;
+  if (kappa) *kappa = k;
+  if (hilbert_l1_out) *hilbert_l1_out = h;
+  return AMR_OK;
+}
 
 int64_t amr_fsk_plan_bytes_estimate(int64_t n, int64_t sps, int ntaps, int64_t max_streams) {
   if (n < 1 || sps < 1 || ntaps < 1 || max_streams < 1)
@@ -857,6 +998,7 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
   pl->u_bytes = geo.u;
   pl->staging_bytes = geo.staging;
   pl->dd_bytes = geo.dd;
+  pl->split_reserved = geo.split;
   struct A { void** ptr; int64_t bytes; };
   const A allocs[] = {
       {(void**)&pl->z, geo.z},
@@ -937,6 +1079,13 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
       }
     }
   }
+  {
+    double kappa = 0.0, hl1 = 0.0;
+    pl->split_ok = fsk_split_design(pl->f, nt, n, &pl->split_w, &kappa, &hl1);
+    pl->split_kappa = kappa;
+    pl->split_hl1 = hl1;
+    pl->split_tau = kAmbTau + kappa * hl1;
+  }
   *out = pl;
   return AMR_OK;
 }
@@ -951,17 +1100,61 @@ int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   // scratch + the host-API staging (allocated on the first amr_fsk_demod_host:
   // d_x, or dd on a plan that keeps z)
   return plan->scratch_bytes + plan->staging_bytes + (plan->dd ? 0 : plan->dd_bytes) +
-         plan->max_streams * (plan->out_cap + 16);   // == fsk_geometry().total()
+         plan->max_streams * (plan->out_cap + 16) +
+         std::max(plan->split_reserved, plan->split_alloc);   // == fsk_geometry().total() (split calls <= 16 streams)
 }
 int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;
   // what is allocated now: a plan that only ever ran the device entry holds
   // no staging (no d_x, no dd, no output staging)
   return plan->scratch_bytes + (plan->d_x ? plan->staging_bytes : 0) +
-         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0);
+         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0) + plan->split_alloc;
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
+
+int amr_fsk_plan_set_layout(amr_fsk_plan* plan, int layout) {
+  if (!plan || layout < AMR_FSK_LAYOUT_AUTO || layout > AMR_FSK_LAYOUT_SPLIT)
+    return fail(AMR_E_INVALID, "amr_fsk_plan_set_layout: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  plan->split_mode = layout;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_split_info(const amr_fsk_plan* plan, int* last_split, int64_t* warmup, int64_t* chunk, double* kappa,
+                            double* tau) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  if (last_split) *last_split = plan->last_split ? 1 : 0;
+  if (warmup) *warmup = plan->split_ok ? plan->split_w : -1;
+  if (chunk) *chunk = plan->split_L;
+  if (kappa) *kappa = plan->split_kappa;
+  if (tau) *tau = plan->split_tau;
+  return AMR_OK;
+}
+
+int amr_fsk_split_bandpass_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                                int64_t chunk, double* out) {
+  if (!plan || (B && (!x || !out))) return fail(AMR_E_INVALID, "amr_fsk_split_bandpass_host: NULL argument");
+  if (!dtype_size(dtype)) return fail(AMR_E_INVALID, "unknown dtype");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (!plan->split_ok) return fail(AMR_E_INVALID, "the plan's filters have no time-split design");
+  if (B > plan->max_streams || B > 65535) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  if (chunk < 0) return fail(AMR_E_INVALID, "chunk < 0");
+  if (B == 0) return AMR_OK;
+  const int64_t n = plan->p.n;
+  void* xs = nullptr;
+  if (int rc = stage_input(plan, x, dtype, B, x_stride, &xs)) return rc;
+  if (int rc = ensure_split_buffers(plan, B)) return rc;
+  FskParams p = plan->p;
+  p.lc = LiveCols{};                         // natural order for the caller
+  p.amb = nullptr;
+  HIP_TRY(launch_fsk_split(dtype, xs, n, B, plan->z, p, plan->f, fsk_split_params(plan, B, chunk), plan->stream));
+  HIP_TRY(hipMemcpyAsync(out, plan->z, (size_t)(B * n * 16), hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  return AMR_OK;
+}
 
 int amr_fsk_plan_synchronize(amr_fsk_plan* plan) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");

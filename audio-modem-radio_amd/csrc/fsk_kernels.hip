@@ -612,6 +612,161 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
   }
 }
 
+// ---- time-split F1 (one capture or a few: the reference's own call pattern,
+// filebeep_advanced_v2.py:324 -> modem.fsk_demodulate, modem.py:307-308) ----
+// The serial F1 is two dependent recursions of n + 2 pad steps per tone (9-10
+// ms for a 1-s capture, whatever the batch).  Here each pass is cut into
+// chunks of L outputs, lane = (chunk, tone), and a chunk starts w samples
+// early from a zero state -- or, the chunk holding the pass's first sample,
+// from scipy's zi * first-sample state.  The filters are stable, so the zero
+// start has decayed below the rounding level after w samples (fsk_api.cpp
+// fsk_split_design); what remains is a different rounding trajectory, within
+// kappa * peak|ext x| of scipy's output (tests/test_split_margin.py measures
+// it).  F2 then flags with the wider margin FskSplit::tau and the exact path
+// re-runs the serial F1 for the flagged streams, so decisions stay the
+// reference's.  Each step is F1's own (fsk_step<MODE>, scipy's order), so a
+// chunk is scipy's lfilter operation for operation from its start state
+// (oracle/amr_oracle.c oracle_fsk_split_bandpass restates it).
+constexpr int kFskSplitK = 16;   // samples loaded ahead of the recursion
+
+template <typename Ld, typename Body>
+__device__ __forceinline__ void fsk_split_chain(int64_t j0, int64_t j1, Ld ld, Body body) {
+  constexpr int K = kFskSplitK;
+  int64_t j = j0;
+  if (j1 - j0 >= K) {
+    double cur[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) cur[k] = ld(j + k);
+    for (; j + 2 * K <= j1; j += K) {
+      double nxt[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) nxt[k] = ld(j + K + k);
+#pragma unroll
+      for (int k = 0; k < K; ++k) body(j + k, cur[k]);
+#pragma unroll
+      for (int k = 0; k < K; ++k) cur[k] = nxt[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) body(j + k, cur[k]);
+    j += K;
+  }
+  for (; j < j1; ++j) body(j, ld(j));
+}
+
+// FS1: forward pass over ext(x) (odd extension in the input's precision, as
+// F1), outputs [o0, o1) of chunk c for tone q & 1 -> y1; tone-0 lanes keep
+// the stream's max |ext x|
+template <typename T, int MODE>
+__global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_stride, FskParams p, FskIir f,
+                                                      FskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (q >= 2 * sp.c) return;
+  const int tone = (int)(q & 1);
+  const int64_t c = q >> 1;
+  const T* __restrict__ x = reinterpret_cast<const T*>(xv) + s * x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad;
+  const int64_t m1 = n + 2 * (int64_t)pad;
+  const int64_t o0 = c * sp.L, o1 = o0 + sp.L < m1 ? o0 + sp.L : m1;
+  double b[7], a[7], z[6];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
+  const T x0 = x[0], xl = x[n - 1];
+  int64_t j = o0 - sp.w;
+  if (j <= 0) {
+    j = 0;
+    const double e0 = FIn<T>::ext(x0, x[pad]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * e0;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = 0.0;
+  }
+  double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
+  unsigned long long pk = 0;
+  auto body = [&](int64_t jj, double e) {
+    const double y = fsk_step<MODE>(z, b, a, e);
+    if (jj >= o0) {
+      y1[jj] = y;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
+      pk = bits > pk ? bits : pk;
+    }
+  };
+  for (; j < o1 && j < pad; ++j) body(j, FIn<T>::ext(x0, x[pad - j]));
+  const int64_t jm = o1 < pad + n ? o1 : pad + n;
+  if (j < jm) {
+    fsk_split_chain(j, jm, [&](int64_t jj) { return FIn<T>::cvt(x[jj - pad]); }, body);
+    j = jm;
+  }
+  for (; j < o1; ++j) body(j, FIn<T>::ext(xl, x[n - 2 - (j - pad - n)]));
+  if (tone == 0) atomicMax(&sp.peak[s], pk);
+}
+
+// FS2: backward pass (scipy: lfilter over y1 reversed from zi * y1[-1]);
+// chunk c covers reversed positions [o0, o1): f[i], i = m1 - 1 - k - pad, into
+// z at F1's offsets (the live-column layout when the plan has it)
+template <int MODE, bool LIVE>
+__global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, FskParams p, FskIir f, FskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (q >= 2 * sp.c) return;
+  const int tone = (int)(q & 1);
+  const int64_t c = q >> 1;
+  const int64_t n = p.n;
+  const int pad = p.pad;
+  const int64_t m1 = n + 2 * (int64_t)pad;
+  const int64_t o0 = c * sp.L, o1 = o0 + sp.L < m1 ? o0 + sp.L : m1;
+  double b[7], a[7], z[6];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
+  const double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
+  int64_t k = o0 - sp.w;
+  if (k <= 0) {
+    k = 0;
+    const double yl = y1[m1 - 1];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * yl;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = 0.0;
+  }
+  fsk_split_chain(
+      k, o1, [&](int64_t kk) { return y1[m1 - 1 - kk]; },
+      [&](int64_t kk, double v) {
+        const double y = fsk_step<MODE>(z, b, a, v);
+        const int64_t i = m1 - 1 - kk - pad;
+        if (kk >= o0 && i >= 0 && i < n) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
+      });
+}
+
+// FS3: per stream, F2's margin scale from the input peak with the split's
+// tau (exact mode 2: +inf, every stream exact), and its flag word cleared
+__global__ __launch_bounds__(64) void k_fsk_split_amb(int64_t n_streams, FskParams p, FskSplit sp) {
+  const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (s >= n_streams) return;
+  const double peak = __longlong_as_double((long long)sp.peak[s]);
+  p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(peak, sp.tau);
+  if ((s & 31) == 0) p.xflags[s >> 5] = 0u;
+}
+
+template <int MODE>
+static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride, int64_t B, double2* z,
+                                     const FskParams& p, const FskIir& f, const FskSplit& sp, hipStream_t st) {
+  const dim3 blk(64), g((unsigned)((2 * sp.c + 63) / 64), (unsigned)B);
+  switch (dtype) {
+    case kF32: hipLaunchKernelGGL((k_fsk_split_fwd<float, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    case kF64: hipLaunchKernelGGL((k_fsk_split_fwd<double, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    case kI16: hipLaunchKernelGGL((k_fsk_split_fwd<int16_t, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    default: return hipErrorInvalidValue;
+  }
+  double* zd = reinterpret_cast<double*>(z);
+  if (p.lc.on) hipLaunchKernelGGL((k_fsk_split_bwd<MODE, true>), g, blk, 0, st, zd, p, f, sp);
+  else hipLaunchKernelGGL((k_fsk_split_bwd<MODE, false>), g, blk, 0, st, zd, p, f, sp);
+  if (p.amb) hipLaunchKernelGGL(k_fsk_split_amb, dim3((unsigned)((B + 63) / 64)), blk, 0, st, B, p, sp);
+  return hipGetLastError();
+}
+
 int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad) {
   const int64_t per = std::max(fsk_scratch_doubles_per_wave(n, pad), fsk2_scratch_doubles_per_group(n, kFsk2TileMin));
   return ((n_streams + 31) / 32) * per * (int64_t)sizeof(double);
@@ -690,6 +845,20 @@ hipError_t launch_fsk_bandpass(int dtype, const void* x, int64_t x_stride, int64
   if (mode == 2) return BPM(2);
   return mode == 1 ? BPM(1) : BPM(0);
 #undef BPM
+}
+
+// FS1-FS3 over B streams of x (B <= 65535: grid.y); z in the plan's layout.
+// sp.peak is cleared here; p.amb non-null: FS3 sets the margin scales.
+hipError_t launch_fsk_split(int dtype, const void* x, int64_t x_stride, int64_t B, double2* z, const FskParams& p,
+                            const FskIir& f, const FskSplit& sp, hipStream_t st) {
+  if (B < 1) return hipSuccess;
+  if (B > 65535 || p.nt != 7 || sp.L < 1 || sp.c < 1) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(sp.peak, 0, (size_t)B * sizeof(unsigned long long), st);
+  if (e != hipSuccess) return e;
+  const int mode = fsk_step_mode(f, false);
+  if (mode == 3) return launch_fsk_split_t<3>(dtype, x, x_stride, B, z, p, f, sp, st);
+  return mode == 1 ? launch_fsk_split_t<1>(dtype, x, x_stride, B, z, p, f, sp, st)
+                   : launch_fsk_split_t<0>(dtype, x, x_stride, B, z, p, f, sp, st);
 }
 
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,

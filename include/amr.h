@@ -61,7 +61,9 @@ extern "C" {
                                  amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT
                                3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info,
                                   amr_psk_split_design, amr_psk_split_symbols_host, the float32 hand-off
-                                  (amr_psk_f32_margin, amr_psk_plan_last_f32f), amr_fsk_plan_resident_bytes */
+                                  (amr_psk_f32_margin, amr_psk_plan_last_f32f), amr_fsk_plan_resident_bytes,
+                                  the FSK time-split F1 (AMR_FSK_LAYOUT_*, amr_fsk_plan_set_layout,
+                                  amr_fsk_plan_split_info, amr_fsk_split_design, amr_fsk_split_bandpass_host) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -298,6 +300,34 @@ int amr_fsk_demod_host_async(amr_fsk_plan *plan, const void *x, int dtype, int64
  * of each tone (modem.py:308-309) -- the intermediate the tolerance tests read. */
 int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                            double *mark_env, double *space_env);
+/* F1's layout per call.  SERIAL: scipy's filtfilt, one recursion per (stream,
+ * tone).  SPLIT: each filtfilt pass cut in time into chunks started early from
+ * a zero state (the latency path of one capture): its band-pass
+ * output is within kappa * peak|ext x| of scipy's, F2 flags every compare
+ * within (2^-36 + kappa * ||hilbert kernel||_1) * peak of a tie, and the exact
+ * path re-runs the serial F1 for those streams -- decided bytes unchanged.
+ * AUTO (the default): SPLIT for calls of at most 16 streams when the plan's
+ * filters allow it (warm-up <= n / 4) and the exact path is on. */
+#define AMR_FSK_LAYOUT_AUTO 0
+#define AMR_FSK_LAYOUT_SERIAL 1
+#define AMR_FSK_LAYOUT_SPLIT 2
+int amr_fsk_plan_set_layout(amr_fsk_plan *plan, int layout);
+/* the last call's F1 (*last_split 1: split) and the plan's split design:
+ * warm-up samples, chunk length of the last split call, kappa, and tau (F2's
+ * margin scale for split calls).  Any pointer may be NULL; *warmup = -1 when
+ * the plan cannot split. */
+int amr_fsk_plan_split_info(const amr_fsk_plan *plan, int *last_split, int64_t *warmup, int64_t *chunk,
+                            double *kappa, double *tau);
+/* the split design from the filters alone (host arithmetic; no device):
+ * warm-up, kappa and ||ifft(h)||_1 of scipy.signal.hilbert's multiplier h at
+ * length n.  Returns AMR_E_INVALID when the filters cannot be split at n. */
+int amr_fsk_split_design(int64_t n_samples, const double *mark_b, const double *mark_a, const double *space_b,
+                         const double *space_a, int ntaps, int64_t *warmup, double *kappa, double *hilbert_l1);
+/* the split F1's band-pass output itself (a diagnostic the tests compare with
+ * the oracle's restatement): out [n_streams][n_samples][2] (mark, space);
+ * chunk 0 = the plan's rule.  Synchronous. */
+int amr_fsk_split_bandpass_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                                int64_t chunk, double *out);
 
 /* ---- FFT / Hilbert (the transforms under scipy.signal.hilbert) --------------
  * in/out: [batch][n] interleaved complex doubles; inverse scales by 1/n

@@ -329,6 +329,29 @@ static void chunked_pass(const double *b, const double *a, int nt, const double 
     }
 }
 
+/* The FSK time-split F1 (fsk_kernels.hip FS1 / FS2), restated per tone: the
+ * chunked forward pass over the odd-extended input, the chunked backward pass
+ * over its reversal, f[i] = y[m - 1 - pad - i].  Same chunk rule as
+ * chunked_pass (zero start w samples early, scipy's zi state for the chunk
+ * at the pass's start).  out: n doubles.  Returns -1 if n <= pad. */
+int oracle_split_filtfilt(const double *b, const double *a, int nt, const double *zi, const void *x, int dtype,
+                          int64_t n, int64_t L, int64_t w, double *out)
+{
+    const int pad = 3 * nt;
+    if (n <= pad || L < 1) return -1;
+    const int64_t m = n + 2 * (int64_t)pad;
+    double *e = (double *)malloc(sizeof(double) * (size_t)m);
+    double *y = (double *)malloc(sizeof(double) * (size_t)m);
+    double *r = (double *)malloc(sizeof(double) * (size_t)m);
+    for (int64_t j = 0; j < m; ++j) e[j] = ext_sample(x, dtype, n, pad, j);
+    chunked_pass(b, a, nt, zi, e, y, m, L, w);
+    for (int64_t k = 0; k < m; ++k) r[k] = y[m - 1 - k];
+    chunked_pass(b, a, nt, zi, r, y, m, L, w);
+    for (int64_t i = 0; i < n; ++i) out[i] = y[m - 1 - pad - i];
+    free(e); free(y); free(r);
+    return 0;
+}
+
 int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
                                  const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
                                  const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,

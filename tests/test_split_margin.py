@@ -111,3 +111,81 @@ def test_f32_handoff_error_below_its_bound(kind, baud, fc, fs, built_lib):
         worst = max(worst, np.abs(got - ref).max() / (c * fpeak + 2.0 ** -120))
     print(f"{kind}@{baud} fc {fc:g}: f32 margin {c:.3e} x max|f|; worst error / bound {worst:.3f}")
     assert worst <= 0.5
+
+
+# ---- the FSK time-split F1 (fsk_kernels.hip FS1-FS3) ----------
+FSK_CONFIGS = [(9600, 12000.0, 24000.0, 96000), (4800, 7000.0, 19000.0, 96000), (2400, 11229.28, 29833.37, 96000),
+               (1200, 2400.0, 4800.0, 96000), (19200, 21000.0, 27000.0, 96000), (1200, 2400.0, 4800.0, 48000)]
+
+
+def _fsk_inputs(baud, mark, space, fs, n, rng):
+    import synth
+    t = np.arange(n) / fs
+    ins = {"noise": rng.normal(0, 0.3, n), "mark": np.sin(2 * np.pi * mark * t), "space": np.sin(2 * np.pi * space * t),
+           "edge": np.sin(2 * np.pi * (mark + baud) * t), "square": np.sign(np.sin(2 * np.pi * mark * t)),
+           "noise_dc": rng.normal(0.5, 0.1, n)}
+    w = synth.fsk_waveform(synth.random_frame(rng, 40), baud, mark, space, float(fs))
+    x = np.zeros(n)
+    x[n // 5:n // 5 + min(w.size, n - n // 5)] = w[:n - n // 5]
+    x[n // 2:n // 2 + 3000] = 0.0
+    ins["signal_gap"] = x + np.where(x != 0, rng.normal(0, 0.02, n), 0.0)
+    return ins
+
+
+@pytest.mark.parametrize("baud,mark,space,fs", FSK_CONFIGS, ids=lambda v: str(v))
+def test_fsk_split_error_far_below_kappa(baud, mark, space, fs, built_lib):
+    """The split F1's band-pass output against scipy's filtfilt (the oracle's
+    restatements of both): max |split - serial| / peak|x| <= kappa / 16 over
+    tones at mark / space / a band edge, a square wave, noise, DC and an FSK
+    frame with a silence gap, three chunk lengths.  The envelope error that
+    implies is kappa * ||hilbert kernel||_1 (the margin F2 adds); measured
+    here too, through the oracle's exact |hilbert|."""
+    import _fsk
+    from oracle import oracle
+    n = 48000
+    d = _fsk.split_design(n, baud, mark, space, fs)
+    assert d is not None and 0 < d["warmup"] <= n // 4 and d["kappa"] > 0
+    _, ((mb, ma, _), (sb, sa, _)) = _fsk.design_fsk(n, baud, mark, space, fs)
+    rng = np.random.default_rng(baud + int(mark))
+    worst, where, worst_env = 0.0, None, 0.0
+    for name, x in _fsk_inputs(baud, mark, space, fs, n, rng).items():
+        peak = np.abs(x).max()
+        for b, a in ((mb, ma), (sb, sa)):
+            ref = oracle.filtfilt(b, a, x)
+            for L in (64, 97, 5000):
+                sp = oracle.split_filtfilt(b, a, x, L, d["warmup"])
+                err = np.abs(sp - ref).max() / peak
+                if err > worst:
+                    worst, where = err, (name, L)
+                if L == 97 and name in ("signal_gap", "noise"):
+                    de = np.abs(oracle.hilbert_env(sp) - oracle.hilbert_env(ref)).max() / peak
+                    worst_env = max(worst_env, de)
+    env_bound = d["kappa"] * d["hilbert_l1"]
+    print(f"fsk@{baud} {mark:g}/{space:g} fs {fs}: warm-up {d['warmup']}, kappa {d['kappa']:.3e}, worst |split - "
+          f"serial| / peak {worst:.3e} ({where}), kappa / worst = {d['kappa'] / worst:.1f}; envelope bound "
+          f"{env_bound:.3e}, worst {worst_env:.3e}")
+    assert worst <= d["kappa"] / 16
+    assert worst_env <= env_bound / 16
+
+
+def test_fsk_split_refused_for_narrow_bands(built_lib):
+    """300 Bd at 96 kHz (a 600 Hz band): the rounding noise gain makes the
+    margin wider than 2^-16 of the peak, so those plans keep the serial F1."""
+    import _fsk
+    assert _fsk.split_design(96000, 300, 1200.0, 2200.0, 96000) is None
+    assert _fsk.split_design(96000, 9600, 12000.0, 24000.0, 96000) is not None
+
+
+@pytest.mark.parametrize("n", [2400, 2401, 24001, 96000, 96001])
+def test_fsk_split_hilbert_gain(n, built_lib):
+    """The design's ||ifft(h)||_1 (scipy.signal.hilbert's kernel, iir_design.h
+    hilbert_l1) equals sum |hilbert(unit impulse)| and is not below it, at
+    even and odd lengths."""
+    import _fsk
+    from scipy.signal import hilbert
+    d = _fsk.split_design(n, 9600, 12000.0, 24000.0, 96000)
+    assert d is not None
+    e = np.zeros(n)
+    e[0] = 1.0
+    want = np.abs(hilbert(e)).sum()
+    assert want <= d["hilbert_l1"] <= want * (1 + 1e-5)
