@@ -649,6 +649,12 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
             host_res = (xh, o0, ln0)
     elif gather_check is not None and "MISMATCH" in gather_check:
         log(f"[rank {rank}] {name}: {gather_check}")
+    fsk_one = None
+    if result is not None and fsk and world == 1 and not args.no_dropin:
+        n1 = min(BL, 8)
+        x8 = np.empty((n1, N), np.float32)
+        _amr.check(L.amr_memcpy_d2h(_amr.ptr(x8), ctx[0]["x"], x8.nbytes))
+        fsk_one = (x8, outs[0][0][:n1].copy(), outs[0][1][:n1].copy())
     for c in ctx:
         c.clear()
     del plans, ctx
@@ -662,7 +668,54 @@ def run_workload(name, args, tp, world, rank, dev, comm, headline):
             result["dropin"] = dropin_path(host_res[0], baud, sym_per_stream, host_res[1], host_res[2])
     if result is not None and fsk and world == 1 and not args.no_cpu:
         result["exact_probe"] = fsk_exact_probe(N, baud, mark, space, dev)
+    if result is not None and fsk_one is not None:
+        result["dropin"] = fsk_dropin_path(*fsk_one, baud, mark, space)
     return result
+
+
+def fsk_dropin_path(xh, out_dev, len_dev, baud, mark, space):
+    """modem.fsk_demodulate(x) on one 1-s capture at a time -- the reference's
+    own call pattern (filebeep_advanced_v2.py:324) -- which runs the FSK
+    time-split F1, beside the serial F1 on the same captures
+    and the C port on one host core; bytes checked against the device path's.
+    Never `value`."""
+    import _fsk
+    import modem
+    args = dict(baud=baud, mark_freq=mark, space_freq=space)
+    n1, N = xh.shape
+    modem.fsk_demodulate(xh[0], **args)                    # plan and scratch
+    plan1 = _fsk.get_fsk_plan(N, baud, mark, space, FS, 1)
+    ts, flagged, same = [], 0, True
+    for i in range(n1):
+        t1 = time.perf_counter()
+        r = modem.fsk_demodulate(xh[i], **args)
+        ts.append(time.perf_counter() - t1)
+        same &= r == out_dev[i, :len_dev[i]].tobytes()
+        flagged += plan1.exact_streams()
+    ser = _fsk.FskPlan(N, baud, mark, space, FS, max_streams=1)
+    ser.set_layout("serial")
+    ser.demod_host(xh[:1])
+    tr = []
+    for i in range(n1):
+        t1 = time.perf_counter()
+        ser.demod_host(xh[i:i + 1])
+        tr.append(time.perf_counter() - t1)
+    del ser
+    from oracle import oracle
+    tc = []
+    for i in range(3):
+        t1 = time.perf_counter()
+        oracle.fsk_demodulate(xh[i], **args)
+        tc.append(time.perf_counter() - t1)
+    info = plan1.split_info()
+    return {"one_capture": {"ms": round(float(np.median(ts)) * 1e3, 3), "ms_min": round(min(ts) * 1e3, 3),
+                            "split": info, "flagged_of": f"{flagged}/{n1}",
+                            "serial_f1_ms": round(float(np.median(tr)) * 1e3, 3),
+                            "c_port_1core_ms": round(float(np.median(tc)) * 1e3, 3), "bytes_equal": bool(same),
+                            "what": f"modem.fsk_demodulate(x, baud={int(baud)}) on one {N}-sample float32 capture "
+                                    f"(H2D + demod + D2H, cached plan), median over {n1} distinct captures of the "
+                                    "benchmark batch; serial_f1_ms: the same calls with the serial F1; "
+                                    "c_port_1core_ms: the oracle's C restatement (filtfilt + pocketfft) on one core"}}
 
 
 def fsk_exact_probe(N, baud, mark, space, dev, B=2048):
@@ -1040,7 +1093,7 @@ def main():
                                                 "kernel_ms_solo", "cpu_baseline", "config")}
                 subs[name]["roofline"] = {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "frac_throughput", "kernel_ms_used", "inflight", "pipeline",
                                                                           "fp64_valu")}
-                for k in ("gather_check", "exact_path_streams", "exact_probe", "plan_bytes"):
+                for k in ("gather_check", "exact_path_streams", "exact_probe", "plan_bytes", "dropin"):
                     if k in r:
                         subs[name][k] = r[k]
         if rank == 0 and result is not None:
