@@ -708,8 +708,22 @@ def fsk_dropin_path(xh, out_dev, len_dev, baud, mark, space):
         oracle.fsk_demodulate(xh[i], **args)
         tc.append(time.perf_counter() - t1)
     info = plan1.split_info()
+    # a capture that opens with digital silence (as a padded WAV does): its
+    # compares there sit inside the margin, so the call also runs the exact
+    # path (the serial F1 again, then pocketfft's envelopes)
+    xs = xh[0].copy()
+    xs[:N // 5] = 0.0
+    want = oracle.fsk_demodulate(xs, **args)
+    tf, fl_s = [], 0
+    for _ in range(3):
+        t1 = time.perf_counter()
+        r = modem.fsk_demodulate(xs, **args)
+        tf.append(time.perf_counter() - t1)
+        fl_s = plan1.exact_streams()
+    flagged_capture = {"ms": round(float(np.median(tf)) * 1e3, 3), "flagged": int(fl_s), "bytes_equal": r == want,
+                       "what": "the same call on capture 0 with its first fifth set to digital silence"}
     return {"one_capture": {"ms": round(float(np.median(ts)) * 1e3, 3), "ms_min": round(min(ts) * 1e3, 3),
-                            "split": info, "flagged_of": f"{flagged}/{n1}",
+                            "split": info, "flagged_of": f"{flagged}/{n1}", "flagged_capture": flagged_capture,
                             "serial_f1_ms": round(float(np.median(tr)) * 1e3, 3),
                             "c_port_1core_ms": round(float(np.median(tc)) * 1e3, 3), "bytes_equal": bool(same),
                             "what": f"modem.fsk_demodulate(x, baud={int(baud)}) on one {N}-sample float32 capture "
@@ -757,6 +771,13 @@ def fsk_exact_probe(N, baud, mark, space, dev, B=2048):
     del pl
     gc.collect()
     return res
+
+
+def row_bytes(x, baud):
+    """One capture through a plan forced to the serial row layout."""
+    pl = _amr.PskPlan("qpsk", x.size, baud, max_streams=1)
+    pl.set_layout("row")
+    return pl.demod_host(np.ascontiguousarray(x)[None])[0][0]
 
 
 def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
@@ -812,6 +833,20 @@ def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
                                   f"(H2D + demod + D2H, cached plan), median over {n1} distinct captures of the "
                                   "benchmark batch; row_layout_ms: the same calls on the serial row layout",
                           "bytes_equal": bool(one == out_dev[0, :len_dev[0]].tobytes() and same)}
+    # a capture that opens with digital silence: exact zero products are
+    # flagged, so the call also runs the gated serial kernels
+    xs = x1.copy()
+    xs[:x1.size // 5] = 0.0
+    want_s = modem.qpsk_demodulate(xs, baud=baud)
+    tf = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        r = modem.qpsk_demodulate(xs, baud=baud)
+        tf.append(time.perf_counter() - t1)
+    res["one_capture"]["flagged_capture"] = {
+        "ms": round(float(np.median(tf)) * 1e3, 3), "flagged": int(plan1.split_info()["flagged"]),
+        "bytes_equal_row_layout": r == want_s and r == row_bytes(xs, baud),
+        "what": "the same call on capture 0 with its first fifth set to digital silence"}
     # how many single captures the margin sends to the serial path: the first
     # 1024 streams of the benchmark batch, 16 per call, time-split layout forced
     nsp = min(B, 1024)
