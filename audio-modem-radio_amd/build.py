@@ -22,7 +22,8 @@ LIB = os.path.join(HERE, "libamr.so")
 SOURCES = ["psk_kernels.hip", "psk_lane_kernels.hip", "psk_split_kernels.hip", "util_kernels.hip", "fft_kernels.hip", "fsk_kernels.hip", "fsk_exact_kernels.hip", "pocketfft_kernels.hip", "frame_kernels.hip", "tx_kernels.hip",
            "api.cpp", "tx_api.cpp",
            "fsk_api.cpp", "pocketfft_plan.cpp"]
-HEADERS = ["amr_internal.h", "psk_common.h", "fft.h", "api_common.h", "fsk_exact.h", "pocketfft.h", "pocketfft_dev.h", os.path.join(INCLUDE, "amr.h")]
+HEADERS = ["amr_internal.h", "psk_common.h", "fft.h", "api_common.h", "fsk_exact.h", "pocketfft.h", "pocketfft_dev.h",
+           "iir_design.h", "split_chain.h", os.path.join(INCLUDE, "amr.h")]
 ARCH = os.environ.get("AMR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",

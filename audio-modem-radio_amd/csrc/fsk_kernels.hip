@@ -29,6 +29,7 @@
 #include <cstdlib>
 
 #include "amr_internal.h"
+#include "split_chain.h"
 
 namespace amr {
 
@@ -627,32 +628,6 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
 // reference's.  Each step is F1's own (fsk_step<MODE>, scipy's order), so a
 // chunk is scipy's lfilter operation for operation from its start state
 // (oracle/amr_oracle.c oracle_fsk_split_bandpass restates it).
-constexpr int kFskSplitK = 16;   // samples loaded ahead of the recursion
-
-template <typename Ld, typename Body>
-__device__ __forceinline__ void fsk_split_chain(int64_t j0, int64_t j1, Ld ld, Body body) {
-  constexpr int K = kFskSplitK;
-  int64_t j = j0;
-  if (j1 - j0 >= K) {
-    double cur[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) cur[k] = ld(j + k);
-    for (; j + 2 * K <= j1; j += K) {
-      double nxt[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) nxt[k] = ld(j + K + k);
-#pragma unroll
-      for (int k = 0; k < K; ++k) body(j + k, cur[k]);
-#pragma unroll
-      for (int k = 0; k < K; ++k) cur[k] = nxt[k];
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) body(j + k, cur[k]);
-    j += K;
-  }
-  for (; j < j1; ++j) body(j, ld(j));
-}
-
 // FS1: forward pass over ext(x) (odd extension in the input's precision, as
 // F1), outputs [o0, o1) of chunk c for tone q & 1 -> y1; tone-0 lanes keep
 // the stream's max |ext x|
@@ -696,7 +671,15 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
   for (; j < o1 && j < pad; ++j) body(j, FIn<T>::ext(x0, x[pad - j]));
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
   if (j < jm) {
-    fsk_split_chain(j, jm, [&](int64_t jj) { return FIn<T>::cvt(x[jj - pad]); }, body);
+    split_chain_2(
+        j, o0, jm, fwd_blocks(x - pad, [](T v) { return FIn<T>::cvt(v); }),
+        [&](int64_t jj) { return FIn<T>::cvt(x[jj - pad]); },
+        [&](int64_t, double e) { (void)fsk_step<MODE>(z, b, a, e); },
+        [&](int64_t jj, double e) {
+          y1[jj] = fsk_step<MODE>(z, b, a, e);
+          const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
+          pk = bits > pk ? bits : pk;
+        });
     j = jm;
   }
   for (; j < o1; ++j) body(j, FIn<T>::ext(xl, x[n - 2 - (j - pad - n)]));
@@ -731,12 +714,13 @@ __global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, F
 #pragma unroll
     for (int i = 0; i < 6; ++i) z[i] = 0.0;
   }
-  fsk_split_chain(
-      k, o1, [&](int64_t kk) { return y1[m1 - 1 - kk]; },
+  split_chain_2(
+      k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
+      [&](int64_t, double v) { (void)fsk_step<MODE>(z, b, a, v); },
       [&](int64_t kk, double v) {
         const double y = fsk_step<MODE>(z, b, a, v);
         const int64_t i = m1 - 1 - kk - pad;
-        if (kk >= o0 && i >= 0 && i < n) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
+        if (i >= 0 && i < n) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
       });
 }
 

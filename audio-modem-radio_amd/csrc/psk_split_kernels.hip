@@ -47,35 +47,9 @@
 
 #include "amr_internal.h"
 #include "psk_common.h"
+#include "split_chain.h"
 
 namespace amr {
-
-constexpr int kSplitK = 16;   // samples loaded ahead of the recursion
-
-// for j in [j0, j1): body(j, ld(j)), the loads kSplitK steps ahead of use
-template <typename Ld, typename Body>
-__device__ __forceinline__ void split_chain(int64_t j0, int64_t j1, Ld ld, Body body) {
-  constexpr int K = kSplitK;
-  int64_t j = j0;
-  if (j1 - j0 >= K) {
-    double cur[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) cur[k] = ld(j + k);
-    for (; j + 2 * K <= j1; j += K) {
-      double nxt[K];
-#pragma unroll
-      for (int k = 0; k < K; ++k) nxt[k] = ld(j + K + k);
-#pragma unroll
-      for (int k = 0; k < K; ++k) body(j + k, cur[k]);
-#pragma unroll
-      for (int k = 0; k < K; ++k) cur[k] = nxt[k];
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) body(j + k, cur[k]);
-    j += K;
-  }
-  for (; j < j1; ++j) body(j, ld(j));
-}
 
 template <bool ZO>
 __device__ __forceinline__ double split_bp_step(double (&z)[8], const Iir& f, double x) {
@@ -130,7 +104,15 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
   for (; j < o1 && j < pad; ++j) body(j, In<T>::ext(x0, x[pad - j]));
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
   if (j < jm) {
-    split_chain(j, jm, [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); }, body);
+    split_chain_2(
+        j, o0, jm, fwd_blocks(x - pad, [](T v) { return In<T>::cvt(v); }),
+        [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); },
+        [&](int64_t, double e) { (void)split_bp_step<ZO>(z, f, e); },
+        [&](int64_t jj, double e) {
+          y1[jj] = split_bp_step<ZO>(z, f, e);
+          const unsigned long long b = abs_bits(e);
+          pk = b > pk ? b : pk;
+        });
     j = jm;
   }
   for (; j < o1; ++j) body(j, In<T>::ext(xl, x[n - 2 - (j - pad - n)]));
@@ -161,12 +143,13 @@ __global__ __launch_bounds__(64) void k_split_bp_bwd(PskBuffers buf, PskParams p
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] = 0.0;
   }
-  split_chain(
-      k, o1, [&](int64_t kk) { return y1[m1 - 1 - kk]; },
+  split_chain_2(
+      k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
+      [&](int64_t, double v) { (void)split_bp_step<ZO>(z, f, v); },
       [&](int64_t kk, double v) {
         const double y = split_bp_step<ZO>(z, f, v);
         const int64_t i = m1 - 1 - kk - pad;
-        if (kk >= o0 && i >= 0 && i < n) fo[i] = y;
+        if (i >= 0 && i < n) fo[i] = y;
       });
 }
 
@@ -209,7 +192,18 @@ __global__ __launch_bounds__(64) void k_split_lp_fwd(PskBuffers buf, PskParams p
   for (; j < o1 && j <= pad; ++j) body(j, j < pad ? 2.0 * x0 - Xm(pad - j) : x0);
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
   if (j < jm) {
-    split_chain(j, jm, [&](int64_t jj) { return Xm(jj - pad); }, body);
+    split_chain_2(
+        j, o0, jm,
+        [&](int64_t jj, double (&v)[kSplitRun]) {
+          double a[kSplitRun], l[kSplitRun];
+          run_load<kSplitRun>(fi + (jj - pad), a);
+          run_load<kSplitRun>(loc + (jj - pad), l);
+#pragma unroll
+          for (int q = 0; q < kSplitRun; ++q) v[q] = a[q] * l[q];
+        },
+        [&](int64_t jj) { return Xm(jj - pad); },
+        [&](int64_t, double e) { (void)split_lp_step<SYM>(z, f, e); },
+        [&](int64_t jj, double e) { y3[jj] = split_lp_step<SYM>(z, f, e); });
     j = jm;
   }
   for (; j < o1; ++j) body(j, 2.0 * xl - Xm(n - 2 - (j - pad - n)));
@@ -240,16 +234,17 @@ __global__ __launch_bounds__(64) void k_split_lp_bwd(PskBuffers buf, PskParams p
 #pragma unroll
     for (int i = 0; i < 4; ++i) z[i] = 0.0;
   }
-  // sample i = m2 - 1 - k - pad falls by one per step: r = (i - first) mod sps
-  // counts down to the next symbol sample
-  const int64_t i0 = m2 - 1 - k - pad;
+  // over the outputs, sample i = m2 - 1 - k - pad falls by one per step:
+  // r = (i - first) mod sps counts down to the next symbol sample
+  const int64_t i0 = m2 - 1 - (k > o0 ? k : o0) - pad;
   int64_t r = ((i0 - first) % sps + sps) % sps;
-  split_chain(
-      k, o1, [&](int64_t kk) { return y3[m2 - 1 - kk]; },
+  split_chain_2(
+      k, o0, o1, bwd_blocks(y3, m2 - 1), [&](int64_t kk) { return y3[m2 - 1 - kk]; },
+      [&](int64_t, double v) { (void)split_lp_step<SYM>(z, f, v); },
       [&](int64_t kk, double v) {
         const double y = split_lp_step<SYM>(z, f, v);
         const int64_t i = m2 - 1 - kk - pad;
-        if (r == 0 && kk >= o0 && i >= first && i < n) so[(i - first) / sps * 2] = y;
+        if (r == 0 && i >= first && i < n) so[(i - first) / sps * 2] = y;
         r = r == 0 ? sps - 1 : r - 1;
       });
 }
