@@ -628,6 +628,16 @@ __global__ __launch_bounds__(kDecideThreads) void k_fsk_decide(const uint8_t* __
 // reference's.  Each step is F1's own (fsk_step<MODE>, scipy's order), so a
 // chunk is scipy's lfilter operation for operation from its start state
 // (oracle/amr_oracle.c oracle_fsk_split_bandpass restates it).
+// a split chunk's warm-up step (before its first output): one FMA per tap
+// (fsk_split_warm), as the PSK split's (psk_common.h bp_warm) -- only the
+// state it leaves matters; oracle/amr_oracle.c chunked_pass_w restates it
+__device__ __forceinline__ void fsk_split_warm(double (&z)[6], const double (&b)[7], const double (&a)[7], double x) {
+  const double y = __builtin_fma(b[0], x, z[0]);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) z[i] = __builtin_fma(-a[i + 1], y, __builtin_fma(b[i + 1], x, z[i + 1]));
+  z[5] = __builtin_fma(-a[6], y, b[6] * x);
+}
+
 // FS1: forward pass over ext(x) (odd extension in the input's precision, as
 // F1), outputs [o0, o1) of chunk c for tone q & 1 -> y1; tone-0 lanes keep
 // the stream's max |ext x|
@@ -661,9 +671,10 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
   double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
   unsigned long long pk = 0;
   auto body = [&](int64_t jj, double e) {
-    const double y = fsk_step<MODE>(z, b, a, e);
-    if (jj >= o0) {
-      y1[jj] = y;
+    if (jj < o0) {
+      fsk_split_warm(z, b, a, e);
+    } else {
+      y1[jj] = fsk_step<MODE>(z, b, a, e);
       const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
       pk = bits > pk ? bits : pk;
     }
@@ -674,7 +685,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
     split_chain_2(
         j, o0, jm, fwd_blocks(x - pad, [](T v) { return FIn<T>::cvt(v); }),
         [&](int64_t jj) { return FIn<T>::cvt(x[jj - pad]); },
-        [&](int64_t, double e) { (void)fsk_step<MODE>(z, b, a, e); },
+        [&](int64_t, double e) { fsk_split_warm(z, b, a, e); },
         [&](int64_t jj, double e) {
           y1[jj] = fsk_step<MODE>(z, b, a, e);
           const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
@@ -716,7 +727,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, F
   }
   split_chain_2(
       k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
-      [&](int64_t, double v) { (void)fsk_step<MODE>(z, b, a, v); },
+      [&](int64_t, double v) { fsk_split_warm(z, b, a, v); },
       [&](int64_t kk, double v) {
         const double y = fsk_step<MODE>(z, b, a, v);
         const int64_t i = m1 - 1 - kk - pad;

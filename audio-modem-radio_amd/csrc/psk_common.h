@@ -123,6 +123,33 @@ __device__ __forceinline__ double lp_step(double (&z)[4], const Iir& f, double x
 // df2t_step_zo without the zero-state detector: the time-split kernels
 // (psk_split_kernels.hip) decide by margins, where the sign of an exact zero
 // state -- all the skipped +0.0 taps can change -- moves no decision
+// The time-split band-pass's WARM-UP steps (psk_split_kernels.hip: a chunk's
+// recursion before its first output): not scipy's order -- only the state
+// they leave matters, and it differs from the serial one by rounding either
+// way -- so each tap is one FMA, 13 operations per step with
+// the zero odd taps (bp_warm_zo) or 17 (bp_warm), against 23 / 33.
+// oracle/amr_oracle.c chunked_pass restates it (its generic form, with
+// fma(0, x, z) = z for the zero taps).
+__device__ __forceinline__ double bp_warm_zo(double (&z)[8], const Iir& f, double x) {
+  const double y = __builtin_fma(f.b[0], x, z[0]);
+  z[0] = __builtin_fma(-f.a[1], y, z[1]);
+  z[1] = __builtin_fma(-f.a[2], y, __builtin_fma(f.b[2], x, z[2]));
+  z[2] = __builtin_fma(-f.a[3], y, z[3]);
+  z[3] = __builtin_fma(-f.a[4], y, __builtin_fma(f.b[4], x, z[4]));
+  z[4] = __builtin_fma(-f.a[5], y, z[5]);
+  z[5] = __builtin_fma(-f.a[6], y, __builtin_fma(f.b[6], x, z[6]));
+  z[6] = __builtin_fma(-f.a[7], y, z[7]);
+  z[7] = __builtin_fma(-f.a[8], y, f.b[8] * x);
+  return y;
+}
+__device__ __forceinline__ double bp_warm(double (&z)[8], const Iir& f, double x) {
+  const double y = __builtin_fma(f.b[0], x, z[0]);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) z[i] = __builtin_fma(-f.a[i + 1], y, __builtin_fma(f.b[i + 1], x, z[i + 1]));
+  z[7] = __builtin_fma(-f.a[8], y, f.b[8] * x);
+  return y;
+}
+
 __device__ __forceinline__ double bp_step_zo(double (&z)[8], const Iir& f, double x) {
   const double p0 = f.b[0] * x, p2 = x * f.b[2], p4 = x * f.b[4];
   const double y = z[0] + p0;

@@ -56,6 +56,11 @@ __device__ __forceinline__ double split_bp_step(double (&z)[8], const Iir& f, do
   if constexpr (ZO) return bp_step_zo(z, f, x);
   else return df2t_step<8>(z, f, x);
 }
+template <bool ZO>
+__device__ __forceinline__ void split_bp_warm(double (&z)[8], const Iir& f, double x) {
+  if constexpr (ZO) (void)bp_warm_zo(z, f, x);
+  else (void)bp_warm(z, f, x);
+}
 template <bool SYM>
 __device__ __forceinline__ double split_lp_step(double (&z)[4], const Iir& f, double x) {
   if constexpr (SYM) return lp_step(z, f, x);
@@ -93,9 +98,10 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
   double* __restrict__ y1 = sp.y1 + s * m1;
   unsigned long long pk = 0;
   auto body = [&](int64_t jj, double e) {
-    const double y = split_bp_step<ZO>(z, f, e);
-    if (jj >= o0) {
-      y1[jj] = y;
+    if (jj < o0) {
+      split_bp_warm<ZO>(z, f, e);
+    } else {
+      y1[jj] = split_bp_step<ZO>(z, f, e);
       const unsigned long long b = abs_bits(e);
       pk = b > pk ? b : pk;
     }
@@ -107,7 +113,7 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
     split_chain_2(
         j, o0, jm, fwd_blocks(x - pad, [](T v) { return In<T>::cvt(v); }),
         [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); },
-        [&](int64_t, double e) { (void)split_bp_step<ZO>(z, f, e); },
+        [&](int64_t, double e) { split_bp_warm<ZO>(z, f, e); },
         [&](int64_t jj, double e) {
           y1[jj] = split_bp_step<ZO>(z, f, e);
           const unsigned long long b = abs_bits(e);
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(64) void k_split_bp_bwd(PskBuffers buf, PskParams p
   }
   split_chain_2(
       k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
-      [&](int64_t, double v) { (void)split_bp_step<ZO>(z, f, v); },
+      [&](int64_t, double v) { split_bp_warm<ZO>(z, f, v); },
       [&](int64_t kk, double v) {
         const double y = split_bp_step<ZO>(z, f, v);
         const int64_t i = m1 - 1 - kk - pad;

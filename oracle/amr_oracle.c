@@ -312,8 +312,11 @@ done:
  * zi * first-sample state when that is within w.  The low-pass runs its two
  * components as separate real recursions (the GPU's form; scipy's complex
  * lfilter differs only in signed zeros).  sym: [S][2]. Returns S (0: < 2). */
-static void chunked_pass(const double *b, const double *a, int nt, const double *zi,
-                         const double *in, double *out, int64_t m, int64_t L, int64_t w)
+/* warm_fma: a chunk's steps before its first output (the warm-up) in the
+ * GPU's FMA form (psk_common.h bp_warm): y = fma(b0, x, z0),
+ * z[i] = fma(-a[i+1], y, fma(b[i+1], x, z[i+1])), z[last] = fma(-a[nt-1], y, b[nt-1] x). */
+static void chunked_pass_w(const double *b, const double *a, int nt, const double *zi,
+                           const double *in, double *out, int64_t m, int64_t L, int64_t w, int warm_fma)
 {
     double z[32];
     for (int64_t o0 = 0; o0 < m; o0 += L) {
@@ -322,18 +325,30 @@ static void chunked_pass(const double *b, const double *a, int nt, const double 
         if (j <= 0) { j = 0; for (int i = 0; i < nt - 1; ++i) z[i] = zi[i] * in[0]; }
         else for (int i = 0; i < nt - 1; ++i) z[i] = 0.0;
         for (; j < o1; ++j) {
+            if (warm_fma && j < o0) {
+                const double x = in[j], y = fma(b[0], x, z[0]);
+                for (int i = 0; i < nt - 2; ++i) z[i] = fma(-a[i + 1], y, fma(b[i + 1], x, z[i + 1]));
+                z[nt - 2] = fma(-a[nt - 1], y, b[nt - 1] * x);
+                continue;
+            }
             double y;
             df2t(b, a, nt, z, in + j, &y, 1, 1);
             if (j >= o0) out[j] = y;
         }
     }
 }
+static void chunked_pass(const double *b, const double *a, int nt, const double *zi,
+                         const double *in, double *out, int64_t m, int64_t L, int64_t w)
+{
+    chunked_pass_w(b, a, nt, zi, in, out, m, L, w, 0);
+}
 
 /* The FSK time-split F1 (fsk_kernels.hip FS1 / FS2), restated per tone: the
  * chunked forward pass over the odd-extended input, the chunked backward pass
  * over its reversal, f[i] = y[m - 1 - pad - i].  Same chunk rule as
  * chunked_pass (zero start w samples early, scipy's zi state for the chunk
- * at the pass's start).  out: n doubles.  Returns -1 if n <= pad. */
+ * at the pass's start, warm-up steps in FMA form).  out: n doubles.
+ * Returns -1 if n <= pad. */
 int oracle_split_filtfilt(const double *b, const double *a, int nt, const double *zi, const void *x, int dtype,
                           int64_t n, int64_t L, int64_t w, double *out)
 {
@@ -344,9 +359,9 @@ int oracle_split_filtfilt(const double *b, const double *a, int nt, const double
     double *y = (double *)malloc(sizeof(double) * (size_t)m);
     double *r = (double *)malloc(sizeof(double) * (size_t)m);
     for (int64_t j = 0; j < m; ++j) e[j] = ext_sample(x, dtype, n, pad, j);
-    chunked_pass(b, a, nt, zi, e, y, m, L, w);
+    chunked_pass_w(b, a, nt, zi, e, y, m, L, w, 1);
     for (int64_t k = 0; k < m; ++k) r[k] = y[m - 1 - k];
-    chunked_pass(b, a, nt, zi, r, y, m, L, w);
+    chunked_pass_w(b, a, nt, zi, r, y, m, L, w, 1);
     for (int64_t i = 0; i < n; ++i) out[i] = y[m - 1 - pad - i];
     free(e); free(y); free(r);
     return 0;
@@ -367,9 +382,9 @@ int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sp
     double *r = (double *)malloc(sizeof(double) * (size_t)m1);
     double *g = (double *)malloc(sizeof(double) * 2 * (size_t)n);
     for (int64_t j = 0; j < m1; ++j) e[j] = ext_sample(x, dtype, n, pad1, j);
-    chunked_pass(bp_b, bp_a, bp_nt, bp_zi, e, y, m1, L, w1);
+    chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, e, y, m1, L, w1, 1);
     for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
-    chunked_pass(bp_b, bp_a, bp_nt, bp_zi, r, y, m1, L, w1);
+    chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, r, y, m1, L, w1, 1);
     for (int64_t i = 0; i < n; ++i)                      /* f[i] = y[m1 - 1 - pad1 - i]; (f + 0j) * lo */
         cmul_np(y[m1 - 1 - pad1 - i], 0.0, lo[2 * i], lo[2 * i + 1], &g[2 * i], &g[2 * i + 1]);
     for (int c = 0; c < 2; ++c) {
