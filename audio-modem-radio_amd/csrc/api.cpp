@@ -203,7 +203,7 @@ constexpr int64_t kLaneMinLiveStreams = 16384;
 // small enough that most batches have none); its error bound is kSplitSafety
 // times the filters' L1 noise gain (split_design); chunks are at least
 // kSplitMinL outputs, and longer once a batch would exceed kSplitLanes lanes
-constexpr int64_t kSplitMaxLiveStreams = 16;
+constexpr int64_t kSplitMaxLiveStreams = 64;
 constexpr double kSplitSafety = 64.0;
 constexpr int64_t kSplitMinL = 64;
 constexpr int64_t kSplitLanes = 65536;

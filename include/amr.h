@@ -154,7 +154,7 @@ int amr_psk_plan_timings(amr_psk_plan *plan, float *ms, int count);
  * into chunks, decisions kept where a margin proves them the reference's and
  * a batch with any other stream re-run by the row kernels
  * (psk_split_kernels.hip).  Picked by streams in flight
- * (DESIGN.md §3): split for <= 16 (one capture at a time, as the reference's
+ * (DESIGN.md §3): split for <= 64 (one capture at a time, as the reference's
  * own callers decode -- filebeep_advanced_v2.py:324, 1112), row up to
  * 16383, lane from 16384. */
 #define AMR_LAYOUT_ROW 0
@@ -306,7 +306,7 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
  * output is within kappa * peak|ext x| of scipy's, F2 flags every compare
  * within (2^-36 + kappa * ||hilbert kernel||_1) * peak of a tie, and the exact
  * path re-runs the serial F1 for those streams -- decided bytes unchanged.
- * AUTO (the default): SPLIT for calls of at most 16 streams when the plan's
+ * AUTO (the default): SPLIT for calls of at most 64 streams when the plan's
  * filters allow it (warm-up <= n / 4) and the exact path is on. */
 #define AMR_FSK_LAYOUT_AUTO 0
 #define AMR_FSK_LAYOUT_SERIAL 1

@@ -333,32 +333,6 @@ def test_fsk_quiet_stretches_exact(kind, n):
     print(f"n={n} {kind}: {pl.exact_streams()} of {B} flagged")
 
 
-def _fsk_device_demod(pl, x):
-    """amr_fsk_demod_device on x copied to device memory: (bytes list, sync)."""
-    import ctypes
-    import _amr
-    L = _amr.lib()
-    B, n = x.shape
-    cap = max(pl.out_cap, 1)
-    ptrs = {}
-    for name, nbytes in (("x", x.nbytes), ("out", B * cap), ("len", B * 8), ("sync", B * 8)):
-        p = ctypes.c_void_p()
-        _amr.check(L.amr_malloc(ctypes.byref(p), nbytes))
-        ptrs[name] = p
-    try:
-        _amr.check(L.amr_memcpy_h2d(ptrs["x"], _amr.ptr(x), x.nbytes))
-        _amr.check(L.amr_fsk_demod_device(pl.handle, ptrs["x"], _amr.DTYPES[x.dtype], B, n, ptrs["out"], cap,
-                                          ptrs["len"], ptrs["sync"]))
-        _amr.check(L.amr_fsk_plan_synchronize(pl.handle))
-        out, ln, sy = np.empty((B, cap), np.uint8), np.empty(B, np.int64), np.empty(B, np.int64)
-        for name, h in (("out", out), ("len", ln), ("sync", sy)):
-            _amr.check(L.amr_memcpy_d2h(_amr.ptr(h), ptrs[name], h.nbytes))
-    finally:
-        for p in ptrs.values():
-            L.amr_free(p)
-    return [out[i, :ln[i]].tobytes() for i in range(B)], sy
-
-
 def test_fsk_device_entry_lean_plan():
     """A live-layout plan that only ran the device entry holds z and C, not
     the buffer that keeps z through F2 (dd: 9.6 B per sample at FSK9600) --
@@ -368,6 +342,7 @@ def test_fsk_device_entry_lean_plan():
     digital silence (flagged streams)."""
     import _fsk
     from oracle import oracle
+    from _util import fsk_device_demod
     n, baud, mark, space, B = 96000, 9600, 12000.0, 24000.0, 8
     x = _silence_batch(np.random.default_rng(7), B, n, baud, mark, space, np.float32)
     want = [oracle.fsk_demodulate(r, baud, mark, space) for r in x]
@@ -376,17 +351,17 @@ def test_fsk_device_entry_lean_plan():
     assert pl.live_columns
     total = pl.scratch_bytes()
     lean = pl.resident_bytes()
-    split_reserved = min(B, 16) * (2 * (n + 42) * 8 + 8)    # counted, allocated by the first split call
+    split_reserved = min(B, 64) * (2 * (n + 42) * 8 + 8)    # counted, allocated by the first split call
     dd = B * n * 6 // 10 * 16            # the dead columns' transform: nd / n1 = 6 / 10 at sps 10
     assert total - lean >= dd, (total, lean, dd)
-    got, _ = _fsk_device_demod(pl, x)
+    got, _ = fsk_device_demod(pl, x)
     assert pl.exact_streams() > 0
     assert got == want
     assert pl.resident_bytes() == lean               # the device entry allocated nothing
     got_h, _ = pl.demod_host(x)
     assert got_h == want and pl.exact_streams() > 0
     assert pl.resident_bytes() + split_reserved == total == pl.scratch_bytes()
-    got2, _ = _fsk_device_demod(pl, x)               # now keeping z
+    got2, _ = fsk_device_demod(pl, x)               # now keeping z
     assert got2 == want
     print(f"plan bytes: device entry only {lean / 1e6:.1f} MB, after a host entry {total / 1e6:.1f} MB")
 

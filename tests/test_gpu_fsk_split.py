@@ -138,6 +138,25 @@ def test_split_silence_and_special_values(layout):
         assert got == [oracle.fsk_demodulate(r, baud, mark, space) for r in clean]
 
 
+def test_split_device_entry():
+    """amr_fsk_demod_device with <= 64 streams runs the split F1 too; its
+    flagged streams' serial F1 re-run reads the caller's device x.  Bytes ==
+    the oracle's on a batch with silence, NaN and clean streams."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    from _util import fsk_device_demod
+    n, baud, mark, space, B = 96000, 9600, 12000.0, 24000.0, 6
+    x = synth.fsk_batch(B, n, baud, mark, space, seed=21, distinct=B, noise=0.05).astype(np.float64)
+    x[0, :30000] = 0.0
+    x[1, 5000] = np.nan
+    x[2] *= 1e-310
+    pl = _fsk.FskPlan(n, baud, mark, space, max_streams=B)
+    got, _ = fsk_device_demod(pl, x)
+    assert pl.split_info()["last_split"] and pl.exact_streams() >= 2
+    assert got == [oracle.fsk_demodulate(r, baud, mark, space) for r in x]
+
+
 def test_split_flag_rate_on_benchmark_captures():
     """The benchmark's inputs (clean FSK9600 frames + N(0, 0.05^2) noise): what
     fraction of single captures the split's wider margin sends to the exact

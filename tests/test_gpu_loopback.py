@@ -52,7 +52,7 @@ def _want_payload(frame):
 
 
 @pytest.mark.parametrize("baud", [600, 1000, 1500, 3000])
-@pytest.mark.parametrize("layout", ["row", "lane"])
+@pytest.mark.parametrize("layout", ["row", "lane", "split"])
 def test_qpsk_loopback(baud, layout):
     import _amr
     import modem
@@ -61,8 +61,10 @@ def test_qpsk_loopback(baud, layout):
     plan = _amr.PskPlan("qpsk", x.shape[1], baud, max_streams=x.shape[0])
     if layout == "lane":
         plan.set_inflight(1024)
+    else:
+        plan.set_layout(layout)
     raws, _ = plan.demod_host(x)
-    assert plan.last_layout() == layout
+    assert plan.last_layout() == layout or (layout == "split" and plan.last_layout() == "row")
     got = _payloads(raws)
     for i, fr in enumerate(frames):
         assert got[i] == [_want_payload(fr)], (baud, layout, i)

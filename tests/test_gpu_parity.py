@@ -202,7 +202,7 @@ def test_fec_gpu_matches_reference(golden):
     assert ("Aviso: CRC" in buf.getvalue()) == manifest["fec"][-1]["crc_warn"]
 
 
-@pytest.mark.parametrize("B,layout", [(64, "row"), (8192, "row"), (8192, "lane")])
+@pytest.mark.parametrize("B,layout", [(64, "row"), (64, "split"), (8192, "row"), (8192, "lane")])
 def test_fec_fused_after_8psk_demod(B, layout):
     """Config 5: 8PSK@19200 demod + FEC decode fused on the device == oracle
     chain (psk_demod_batch then fec_decode, fec.py:34-69), every stream's
@@ -217,6 +217,8 @@ def test_fec_fused_after_8psk_demod(B, layout):
     plan = _amr.PskPlan("qpsk", N, 19200, max_streams=B)
     if layout == "lane":
         plan.set_inflight(16)
+    elif B <= 64:
+        plan.set_layout(layout)     # up to 64 streams the default is the time-split layout
     L = _amr.lib()
     cap = plan.out_cap
     ptrs = {}
@@ -265,15 +267,23 @@ def test_decode_wav_file_end_to_end(golden, tmp_path, monkeypatch):
         assert got == case["files"], case["id"]
 
 
-def test_timing_hooks():
+@pytest.mark.parametrize("layout", ["row", "split"])
+def test_timing_hooks(layout):
+    """Per-stage HIP-event times of a call; the time-split layout times its
+    two low-pass passes in the lowpass_fwd slot and its gated serial fallback
+    in lowpass_exact."""
     import _amr
     import synth
     x = synth.qpsk_batch(64, 20000, 9600, seed=1, distinct=2)
     plan = _amr.PskPlan("qpsk", 20000, 9600, max_streams=64)
+    plan.set_layout(layout)
     plan.enable_timing(True)
     plan.demod_host(x)
+    assert plan.last_layout() == layout
     t = plan.timings()
-    assert set(t) >= {"bandpass", "lowpass_fwd", "lowpass_bwd", "sync_pack"}
+    want = {"bandpass", "lowpass_fwd", "lowpass_bwd", "sync_pack"} if layout == "row" else \
+        {"bandpass", "lowpass_fwd", "lowpass_exact", "sync_pack"}
+    assert set(t) >= want
     assert all(v > 0 for v in t.values())
 
 

@@ -3,7 +3,7 @@ draw of configurations across the space the reference's signatures accept
 (modem.py:68, :189, :298 -- baud, carrier / tones, sample rate, stream
 length, input dtype, batch size) rather than the benchmark's few, each
 through the GPU in the layout drawn (PSK: row = one batch alone, every other
-one of them by batch size -- the time-split layout up to 16 streams -- lane =
+one of them by batch size -- the time-split layout up to 64 streams -- lane =
 the plan told many batches are in flight), every stream's bytes and sync index
 bit-exact with the oracle -- or the same ValueError text, where the
 reference's scipy design raises.  Input: a framed, modulated signal at the
@@ -85,7 +85,7 @@ def test_psk_sweep():
             if layout == "lane":
                 plan.set_inflight(max(1, 16384 // B + 1))
             elif c % 2 == 0:
-                plan.set_layout("row")       # else by batch size: the time-split layout up to 16 streams
+                plan.set_layout("row")       # else by batch size: the time-split layout up to 64 streams
             out = plan.demod_host(x)
             assert plan.last_layout() in (layout, "row", "split"), plan.last_layout()
             return out[0], [int(s) for s in out[1]]
