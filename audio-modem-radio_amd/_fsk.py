@@ -9,6 +9,7 @@ after the filter design runs in libamr.so (fsk_kernels.hip, fft_kernels.hip).
 from __future__ import annotations
 
 import ctypes
+import functools
 import threading
 
 import numpy as np
@@ -19,7 +20,15 @@ from _amr import check, lib, ptr
 
 def design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
     """Return (sps, [(b, a, zi) mark, (b, a, zi) space]); raise exactly where
-    the reference raises, in the reference's order (modem.py:301-320)."""
+    the reference raises, in the reference's order (modem.py:301-320).
+    Memoised per parameter set (scipy's butter + lfilter_zi for both tones
+    took ~0.3-0.6 ms of every one-capture call); the arrays are read-only,
+    and a raising design is not cached (it raises again on every call)."""
+    return _design_fsk(int(n), baud, mark_freq, space_freq, samp_rate)
+
+
+@functools.lru_cache(maxsize=256)
+def _design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
     from scipy import signal
     sps = int(samp_rate / baud)            # modem.py:301 (ZeroDivisionError for baud == 0)
     nyq = samp_rate / 2
@@ -29,7 +38,10 @@ def design_fsk(n: int, baud, mark_freq, space_freq, samp_rate):
         nt = max(len(a), len(b))
         if n <= 3 * nt:
             raise ValueError("The length of the input vector x must be greater than padlen, which is %d." % (3 * nt))
-        out.append(tuple(np.ascontiguousarray(v, np.float64) for v in (b, a, signal.lfilter_zi(b, a))))
+        arrs = tuple(np.ascontiguousarray(v, np.float64) for v in (b, a, signal.lfilter_zi(b, a)))
+        for v in arrs:
+            v.setflags(write=False)
+        out.append(arrs)
     if sps == 0:
         raise ValueError("range() arg 3 must not be zero")   # modem.py:320
     return sps, out
