@@ -762,6 +762,53 @@ static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride,
   return hipGetLastError();
 }
 
+// F3 for a few streams (a one-capture call): one workgroup per stream leaves
+// the decisions of a 1-s capture on 256 threads (~32 us); here thread = bit,
+// the window's compare bits read straight from global memory (L2), and a
+// wave's 64 bits packed by ballot into two MSB-first words -- the same
+// majority as k_fsk_decide (np.mean(chunk) > 0.5, modem.py:320-323).
+// grid = (ceil(n_bits / 256), streams)
+__global__ __launch_bounds__(256) void k_fsk_decide_bits(const uint8_t* __restrict__ bits,
+                                                         uint32_t* __restrict__ words, FskParams p) {
+  const int64_t s = blockIdx.y;
+  const int64_t bi = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool exact = p.xflags && ((p.xflags[s >> 5] >> (s & 31)) & 1u);
+  const uint8_t* __restrict__ sb = (exact ? p.xbits : bits) + (size_t)s * p.bits_stride;
+  bool one = false;
+  if (bi < p.n_bits) {
+    const int64_t q = p.sps / 4, half = p.sps / 2;
+    const int64_t i = half + bi * p.sps;
+    const int64_t lo = i - q, hi = (i + q < p.n) ? i + q : p.n;
+    int64_t kk = (int64_t)(((float)lo + 0.5f) * p.inv_rn1);
+    int64_t r = lo - kk * p.rn1;
+    int64_t ones = 0;
+    if (p.lc.on) {
+      bool lv;
+      const int l0 = lc_col_pos(p.lc, (int)r, lv);
+      for (int64_t k = 0; k < hi - lo; ++k) {
+        const int64_t l = l0 + k;
+        ones += (sb[(l >> 3) * p.rn2 + kk] >> (l & 7)) & 1;
+      }
+    } else {
+      for (int64_t k = lo; k < hi; ++k) {
+        ones += (sb[(r >> 3) * p.rn2 + kk] >> (r & 7)) & 1;
+        if (++r == p.rn1) {
+          r = 0;
+          ++kk;
+        }
+      }
+    }
+    one = 2 * ones > hi - lo;
+  }
+  const unsigned long long m = __ballot(one);
+  const int lane = threadIdx.x & 63;
+  if (lane == 0 || lane == 32) {
+    const int64_t w = bi >> 5;
+    const uint32_t half_mask = (uint32_t)(lane == 0 ? m : m >> 32);
+    if (w < p.n_words) words[(size_t)s * p.n_words + w] = __brev(half_mask);
+  }
+}
+
 int64_t fsk_bandpass_scratch_bytes(int64_t n_streams, int64_t n, int pad) {
   const int64_t per = std::max(fsk_scratch_doubles_per_wave(n, pad), fsk2_scratch_doubles_per_group(n, kFsk2TileMin));
   return ((n_streams + 31) / 32) * per * (int64_t)sizeof(double);
@@ -861,6 +908,13 @@ hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_stre
   if (p.n_words < 1 || p.n_bits < 1) return hipSuccess;
   // AMR_FSK_DECIDE_GLOBAL=1: the global-memory form at every length (tests)
   static const bool force_global = [] { const char* e = getenv("AMR_FSK_DECIDE_GLOBAL"); return e && e[0] == '1'; }();
+  // a few streams: thread per bit (k_fsk_decide_bits); AMR_FSK_DECIDE_BITS=0 keeps the per-stream form
+  static const bool bits_off = [] { const char* e = getenv("AMR_FSK_DECIDE_BITS"); return e && e[0] == '0'; }();
+  if (n_streams <= 64 && !bits_off && !force_global) {
+    hipLaunchKernelGGL(k_fsk_decide_bits, dim3((unsigned)((p.n_bits + 255) / 256), (unsigned)n_streams), dim3(256), 0,
+                       st, cmp, words, p);
+    return hipGetLastError();
+  }
   if (p.bits_stride <= kDecideLdsMax && !force_global)
     hipLaunchKernelGGL(k_fsk_decide<true>, dim3((unsigned)n_streams), dim3(kDecideThreads), (size_t)p.bits_stride,
                        st, cmp, words, n_streams, p);
