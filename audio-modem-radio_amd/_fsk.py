@@ -147,7 +147,7 @@ class FskPlan:
         check(lib().amr_fsk_plan_enable_timing(self.handle, 1 if on else 0))
 
     def set_layout(self, layout: str):
-        """F1 per call: "auto" (split for <= 64 streams), "serial", "split" (include/amr.h)."""
+        """F1 per call: "auto" (split for <= 1024 streams), "serial", "split" (include/amr.h)."""
         check(lib().amr_fsk_plan_set_layout(self.handle, FSK_LAYOUTS[layout]))
 
     def split_info(self) -> dict:

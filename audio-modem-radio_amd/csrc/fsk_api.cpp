@@ -397,7 +397,7 @@ struct amr_fsk_plan {
   // the time-split F1 (fsk_kernels.hip FS1-FS3): designed
   // with the plan; used for calls of at most kFskSplitMaxStreams streams
   // (amr_fsk_plan_set_layout overrides); its forward outputs and peaks in
-  // split_y1 / split_peak, allocated on the first split call (<= 64 streams)
+  // split_y1 / split_peak, allocated on the first split call (<= 1024 streams)
   bool split_ok = false;
   int64_t split_w = 0;
   double split_kappa = 0.0, split_hl1 = 0.0, split_tau = 0.0;
@@ -409,7 +409,7 @@ struct amr_fsk_plan {
   unsigned long long* split_peak = nullptr;
   int64_t split_cap = 0;       // streams split_y1 / split_peak hold
   int64_t split_alloc = 0;     // their bytes (not in scratch_bytes)
-  int64_t split_reserved = 0;  // what amr_fsk_plan_bytes_estimate counts for them (<= 64 streams)
+  int64_t split_reserved = 0;  // what amr_fsk_plan_bytes_estimate counts for them (<= 1024 streams)
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
   void* d_x = nullptr;
@@ -459,7 +459,7 @@ hipError_t mark_fsk(amr_fsk_plan* pl, int slot, int which, hipStream_t st = null
 
 // F1 over the B streams of x -> z (and, with the exact path on, each
 // stream's ambiguity scale; the flag words cleared).  Caller holds mu.
-constexpr int64_t kFskSplitMaxStreams = 64;   // AUTO: calls of at most this many streams split
+constexpr int64_t kFskSplitMaxStreams = 1024;   // AUTO: calls of at most this many streams split
 
 // The split F1's launch geometry: L outputs per chunk (at least
 // kFskSplitMinL and w / 4, so warm-ups are at most 4x the useful work, and
@@ -1101,7 +1101,7 @@ int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   // d_x, or dd on a plan that keeps z)
   return plan->scratch_bytes + plan->staging_bytes + (plan->dd ? 0 : plan->dd_bytes) +
          plan->max_streams * (plan->out_cap + 16) +
-         std::max(plan->split_reserved, plan->split_alloc);   // == fsk_geometry().total() (split calls <= 64 streams)
+         std::max(plan->split_reserved, plan->split_alloc);   // == fsk_geometry().total() (split calls <= 1024 streams)
 }
 int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;

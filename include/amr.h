@@ -306,7 +306,7 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
  * output is within kappa * peak|ext x| of scipy's, F2 flags every compare
  * within (2^-36 + kappa * ||hilbert kernel||_1) * peak of a tie, and the exact
  * path re-runs the serial F1 for those streams -- decided bytes unchanged.
- * AUTO (the default): SPLIT for calls of at most 64 streams when the plan's
+ * AUTO (the default): SPLIT for calls of at most 1024 streams when the plan's
  * filters allow it (warm-up <= n / 4) and the exact path is on. */
 #define AMR_FSK_LAYOUT_AUTO 0
 #define AMR_FSK_LAYOUT_SERIAL 1

@@ -351,7 +351,7 @@ def test_fsk_device_entry_lean_plan():
     assert pl.live_columns
     total = pl.scratch_bytes()
     lean = pl.resident_bytes()
-    split_reserved = min(B, 64) * (2 * (n + 42) * 8 + 8)    # counted, allocated by the first split call
+    split_reserved = min(B, 1024) * (2 * (n + 42) * 8 + 8)    # counted, allocated by the first split call
     dd = B * n * 6 // 10 * 16            # the dead columns' transform: nd / n1 = 6 / 10 at sps 10
     assert total - lean >= dd, (total, lean, dd)
     got, _ = fsk_device_demod(pl, x)

@@ -139,7 +139,7 @@ def test_split_silence_and_special_values(layout):
 
 
 def test_split_device_entry():
-    """amr_fsk_demod_device with <= 64 streams runs the split F1 too; its
+    """amr_fsk_demod_device with <= 1024 streams runs the split F1 too; its
     flagged streams' serial F1 re-run reads the caller's device x.  Bytes ==
     the oracle's on a batch with silence, NaN and clean streams."""
     import _fsk
