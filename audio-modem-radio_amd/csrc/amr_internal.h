@@ -186,7 +186,7 @@ __host__ __device__ inline double amb_scale(double peak, double tau = kAmbTau) {
   return 8.0 * d * d;
 }
 
-// FSK time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3b "time-split F1"):
+// FSK time-split F1 (fsk_kernels.hip FS1-FS3):
 // each filtfilt pass of both tones cut into chunks of L outputs, one lane per
 // (chunk, tone), every chunk started w samples early from a zero state.  Its
 // band-pass output is within kappa * peak|ext x| of scipy's, so each envelope

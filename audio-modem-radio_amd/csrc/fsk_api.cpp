@@ -394,7 +394,7 @@ struct amr_fsk_plan {
   bool ran_exact = false;      // the last call ran the exact path (its count is in xlist[max_streams])
   int exact_mode = 1;          // amr_fsk_plan_set_exact_mode: 0 off, 1 F2's flags, 2 every stream
   int64_t scratch_bytes = 0;
-  // the time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3b): designed
+  // the time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3d): designed
   // with the plan; used for calls of at most kFskSplitMaxStreams streams
   // (amr_fsk_plan_set_layout overrides); its forward outputs and peaks in
   // split_y1 / split_peak, allocated on the first split call (<= 1024 streams)
@@ -873,7 +873,7 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   return true;
 }
 
-// The split F1's design (DESIGN.md §3b, the PSK layout's rule, iir_design.h):
+// The split F1's design (DESIGN.md §3d, the PSK layout's rule, iir_design.h):
 // per tone, a chunk's outputs differ from scipy's by (1) the zero start,
 // decayed after w samples to tail(w) * zmax * 3 peak (the odd extension
 // triples the input peak) and carried through the backward pass (its L1 gain

@@ -1,6 +1,6 @@
 // iir_design.h -- host-side analysis of a DF-II-T recursion for the
 // time-split layouts (PSK: api.cpp split_design; FSK:
-// fsk_api.cpp fsk_split_design, §3b): how far a chunk's zero start and its
+// fsk_api.cpp fsk_split_design, §3d): how far a chunk's zero start and its
 // rounding trajectory can move the outputs.
 #pragma once
 #include <algorithm>

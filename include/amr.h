@@ -302,7 +302,7 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
                            double *mark_env, double *space_env);
 /* F1's layout per call.  SERIAL: scipy's filtfilt, one recursion per (stream,
  * tone).  SPLIT: each filtfilt pass cut in time into chunks started early from
- * a zero state (the latency path of one capture, DESIGN.md §3b): its band-pass
+ * a zero state (the latency path of one capture, DESIGN.md §3d): its band-pass
  * output is within kappa * peak|ext x| of scipy's, F2 flags every compare
  * within (2^-36 + kappa * ||hilbert kernel||_1) * peak of a tie, and the exact
  * path re-runs the serial F1 for those streams -- decided bytes unchanged.

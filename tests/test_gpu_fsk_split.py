@@ -1,4 +1,4 @@
-"""GPU tests of the FSK time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3b):
+"""GPU tests of the FSK time-split F1 (fsk_kernels.hip FS1-FS3, DESIGN.md §3d):
 the latency path of one capture at a time, the reference's own call pattern
 (filebeep_advanced_v2.py:324 -> modem.fsk_demodulate, modem.py:298-341).
 

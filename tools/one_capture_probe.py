@@ -1,5 +1,5 @@
 """Where one capture's time goes: modem.qpsk_demodulate / modem.fsk_demodulate
-on one 96000-sample stream (the time-split layouts, DESIGN.md §3.3 / §3c),
+on one 96000-sample stream (the time-split layouts, DESIGN.md §3.3 / §3d),
 wall time per call and, under rocprofv3 --kernel-trace, the kernels' own
 durations (their sum against the wall time is the host side's share).
     rocprofv3 --kernel-trace --stats -d gpurun_out/oc -o run --output-format csv -- python3 tools/one_capture_probe.py
