@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 N_PSK = int(os.environ.get("AMR_SWEEP_PSK", "140"))
 N_FSK = int(os.environ.get("AMR_SWEEP_FSK", "36"))
 SEED = int(os.environ.get("AMR_SWEEP_SEED", "0"))
+FSK_BMAX = int(os.environ.get("AMR_SWEEP_FSK_BMAX", "6"))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -126,7 +127,7 @@ def test_fsk_sweep():
             else:
                 mark, space = sorted(float(v) for v in rng.uniform(lo, hi, 2))
         n = int(rng.choice([int(rng.integers(22, 3000)), int(rng.integers(3000, 100000))]))
-        B = int(rng.integers(1, 6))
+        B = int(rng.integers(1, FSK_BMAX))
         x = _signal(rng, "fsk", B, n, baud, mark, space, fs)
         g = _outcome(lambda: modem.fsk_demodulate_batch(x, baud=baud, mark_freq=mark, space_freq=space, samp_rate=fs))
         # the public drop-in takes integer samples as raw values (as the
