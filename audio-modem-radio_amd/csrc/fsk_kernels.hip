@@ -335,7 +335,8 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
 // beside them; 32 halves that at twice the checkpoints (3 B per sample):
 // fsk9600 37.03-37.16 -> 34.68-34.79 ms/step, and 16 (four times the
 // checkpoints) measured 35.75-35.77 against 32's 35.38-35.60 on another box
-// (profiles/r05_fsk_f1_tile.txt)
+// (profiles/r05_fsk_f1_tile.txt); AMR_FSK_TILE=40 (f32 / f64; the generic
+// load / store mapping below) measured 35.11-35.29 vs 34.55-34.61 ms/step
 constexpr int kFsk2Tile = 32;
 constexpr int kFsk2TileMin = 32;
 __host__ __device__ inline int64_t fsk2_scratch_doubles_per_group(int64_t n, int tl = kFsk2Tile) {
@@ -349,9 +350,10 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   constexpr int TL = TLT;
   constexpr int RB = TL * (int)sizeof(T);           // bytes per stream row per tile
   constexpr int PITCH = RB + 16;
-  constexpr int LPR = RB / 16;                      // lanes per row in a load
-  constexpr int RPI = 64 / LPR;                     // rows per load instruction
-  constexpr int NI = 32 / RPI;                      // load instructions per tile
+  constexpr int LPR = RB / 16;                      // 16-B segments per stream row
+  constexpr int SEG = 32 * LPR;                     // segments per tile (32 rows)
+  constexpr int NI = (SEG + 63) / 64;               // load instructions per tile
+  static_assert(RB % 16 == 0 && SEG % 64 == 0, "a tile's rows must split into whole 64-lane loads");
   constexpr int YP = 66;                            // yb pitch (doubles)
   __shared__ __attribute__((aligned(16))) uint8_t tin[1][32][PITCH];
   // two tile buffers, or the tail's forward outputs (n % TL + pad <= TL - 1 + 21 rows)
@@ -391,12 +393,16 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
 
   // wave 0's input path: 16 B per lane per row segment, two register sets so
   // every load has two tiles of work to land behind (tin is this wave's own)
-  const int rsub = lane / LPR, cb = (lane % LPR) * 16;
+  // instruction i, lane l: segment g = 64 i + l of the tile = row g / LPR,
+  // bytes 16 (g % LPR) (for LPR | 64: rows 64 / LPR per instruction)
   const uint8_t* rowp[NI];
+  int lrow[NI], lcb[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int64_t rs = w * 32 + RPI * i + rsub;
-    rowp[i] = reinterpret_cast<const uint8_t*>(xrow(rs)) + cb;
+    const int g = 64 * i + lane;
+    lrow[i] = g / LPR;
+    lcb[i] = (g % LPR) * 16;
+    rowp[i] = reinterpret_cast<const uint8_t*>(xrow(w * 32 + lrow[i])) + lcb[i];
   }
   v4u r0[NI], r1[NI];
   auto fetch = [&](v4u (&r)[NI], int64_t t) {
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   };
   auto deposit = [&](const v4u (&r)[NI]) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][RPI * i + rsub][cb]) = r[i];
+    for (int i = 0; i < NI; ++i) *reinterpret_cast<v4u*>(&tin[0][lrow[i]][lcb[i]]) = r[i];
   };
   uint32_t pk_hi = 0, pk_lo = 0;   // AMB: the input peak (PeakT), first forward pass
   auto run_tile = [&](auto emit, bool det) {
@@ -486,16 +492,28 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   // tile tz's 32 rows of z from yb buffer bb, after wave 1 has run it backward:
   // RPS rows per 1-KiB store instruction, lane -> (row, sample)
   auto store_tile = [&](int bb, int64_t tz) {
-    constexpr int RPS = 64 / TL;
     const double (*buf)[YP] = &yb[bb * TL];
-    const int sub = lane / TL, k = lane % TL;
-    const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
+    if constexpr (64 % TL == 0) {
+      constexpr int RPS = 64 / TL;
+      const int sub = lane / TL, k = lane % TL;
+      const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
 #pragma unroll 4
-    for (int row = 0; row < 32; row += RPS) {
-      const int rr = row + sub;
-      const int64_t so = w * 32 + rr;
-      const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
-      if (so < ns) z[(size_t)so * n + zo] = v;
+      for (int row = 0; row < 32; row += RPS) {
+        const int rr = row + sub;
+        const int64_t so = w * 32 + rr;
+        const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * rr]);
+        if (so < ns) z[(size_t)so * n + zo] = v;
+      }
+    } else {
+      // lanes k < TL, one row of TL samples per store instruction
+      const int k = lane < TL ? lane : TL - 1;
+      const int64_t zo = fsk_zoff<LIVE>(p, tz * TL + k);
+#pragma unroll 4
+      for (int row = 0; row < 32; ++row) {
+        const int64_t so = w * 32 + row;
+        const double2 v = *reinterpret_cast<const double2*>(&buf[k][2 * row]);
+        if (lane < TL && so < ns) z[(size_t)so * n + zo] = v;
+      }
     }
   };
   // ---- phase 2: wave 0 re-forwards tile T-1-i while wave 1 runs tile T-i backward
@@ -842,12 +860,16 @@ static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stri
   if (!fsk_one_wave() || p.xlist) {
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
-    static const bool t64 = [] { const char* e = getenv("AMR_FSK_TILE"); return e && atoi(e) == 64; }();
+    static const int tile_env = [] { const char* e = getenv("AMR_FSK_TILE"); return e ? atoi(e) : 0; }();
+    const bool t64 = tile_env == 64, t40 = tile_env == 40 && dtype != kI16;
 #define BP2(T, S, D)                                                                                                 \
   do {                                                                                                               \
     if (t64)                                                                                                         \
       hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D, 64>), dim3(grid), dim3(128), 0, st, x, x_stride,         \
                          n_streams, s1, z, p, f);                                                                    \
+    else if (t40 && sizeof(T) != 2)                                                                                  \
+      hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D, (sizeof(T) == 2 ? 32 : 40)>), dim3(grid), dim3(128), 0,  \
+                         st, x, x_stride, n_streams, s1, z, p, f);                                                   \
     else                                                                                                             \
       hipLaunchKernelGGL((k_fsk_bandpass2<T, ZO, LIVE, S, D>), dim3(grid), dim3(128), 0, st, x, x_stride, n_streams,  \
                          s1, z, p, f);                                                                               \
