@@ -204,3 +204,28 @@ def test_one_capture_drop_in_latency():
         tr.append(time.perf_counter() - t)
     print(f"one FSK9600 capture: split {np.median(ts) * 1e3:.3f} ms (min {min(ts) * 1e3:.3f}), "
           f"serial {np.median(tr) * 1e3:.3f} ms")
+
+
+def test_flagged_burst_after_clean_batches_device_entry():
+    """The exact path's serial F1 re-run (E1, list mode) takes its grid from
+    the plan's recent flagged counts and strides over the flagged streams
+    (fsk_kernels.hip k_fsk_bandpass2): after 8 clean device-entry batches the
+    grid is one workgroup, and a batch with 100 flagged streams (a NaN each:
+    every compare goes exact) must still have all 100 recomputed.  Bytes ==
+    the oracle's."""
+    import _fsk
+    import synth
+    from oracle import oracle
+    from _util import fsk_device_demod
+    n, baud, mark, space, B = 24000, 9600, 12000.0, 24000.0, 128
+    clean = synth.fsk_batch(B, n, baud, mark, space, seed=31, distinct=8, noise=0.05).astype(np.float64)
+    pl = _fsk.FskPlan(n, baud, mark, space, max_streams=B)
+    for _ in range(8):
+        fsk_device_demod(pl, clean)
+        assert pl.exact_streams() == 0
+    x = clean.copy()
+    x[:100, 777] = np.nan
+    got, _ = fsk_device_demod(pl, x)
+    assert pl.exact_streams() == 100
+    want = [oracle.fsk_demodulate(r, baud, mark, space) for r in x]
+    assert got == want
