@@ -167,7 +167,6 @@ struct FskParams {
   int force_exact;  // exact mode 2 (amr_fsk_plan_set_exact_mode): every stream's scale +inf, all go exact
   const int32_t* xlist;   // F1 list mode (the exact path): z row r <- x row xlist[r], r < *xcount
   const int32_t* xcount;
-  int32_t xgrid;          // F1 list mode: workgroups to launch (0: one per 32 streams); the kernel strides
 };
 
 // F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within

@@ -639,10 +639,6 @@ int run_fsk_exact(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64
     p1.lc = LiveCols{};
     p1.xlist = X.list;
     p1.xcount = X.count;
-    // the grid from the same count hint as E2 (one workgroup per 32 flagged
-    // streams, at least one): a clean batch's E1 is one workgroup that reads
-    // the count and exits, not B / 32 of them queueing for LDS
-    p1.xgrid = (int32_t)std::max<int64_t>(1, (std::max<int64_t>(X.count_hint, 0) + 31) / 32);
     HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p1, pl->f, st));
   }
   HIP_TRY(launch_fsk_exact_env(B, pl->p, X, st, launch != 2));

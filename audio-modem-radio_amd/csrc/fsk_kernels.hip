@@ -363,17 +363,16 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   const int role = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int tone = lane & 1, sl = lane >> 1;
+  const int64_t w = blockIdx.x;
+  const int64_t s = w * 32 + sl;
   // list mode (p.xlist, the exact path): the streams F2 flagged, by ordinal
-  // (row r of z is ordinal r's, x row p.xlist[r]); the count is read here, and
-  // the groups of 32 ordinals are taken grid-stride (the launch sizes its grid
-  // from the plan's recent counts, FskParams::xgrid: correct at any grid)
+  // (row r of z is ordinal r's, x row p.xlist[r]); the count is read here
   int64_t ns = n_streams;
   if (p.xlist) {
     const int64_t c = *p.xcount;
     ns = c < n_streams ? c : n_streams;
+    if (w * 32 >= ns) return;              // whole workgroup, before any barrier
   }
-  auto group = [&](const int64_t w) {
-  const int64_t s = w * 32 + sl;
   const int64_t last = ns - 1;
   const T* __restrict__ xall = reinterpret_cast<const T*>(xv);
   auto xrow = [&](int64_t r) -> const T* {
@@ -566,15 +565,6 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       }
       __syncthreads();
     }
-  }
-  };
-  if (!p.xlist) {
-    group((int64_t)blockIdx.x);
-    return;
-  }
-  for (int64_t w = blockIdx.x; w * 32 < ns; w += gridDim.x) {   // whole workgroup: w is uniform
-    group(w);
-    __syncthreads();                                    // LDS reused by the next group
   }
 }
 
@@ -866,8 +856,7 @@ static int fsk_step_mode(const FskIir& f, bool allow_fma) {
 template <int ZO, bool LIVE>
 static hipError_t launch_fsk_bandpass_t(int dtype, const void* x, int64_t x_stride, int64_t n_streams, double* s1,
                                         double2* z, const FskParams& p, const FskIir& f, hipStream_t st) {
-  const int64_t groups = (n_streams + 31) / 32;
-  const unsigned grid = (unsigned)(p.xlist && p.xgrid > 0 && p.xgrid < groups ? p.xgrid : groups);
+  const unsigned grid = (unsigned)((n_streams + 31) / 32);
   if (!fsk_one_wave() || p.xlist) {
     // AMR_FSK_W1S=0: wave 0 stores z (the round-2 schedule)
     static const bool w1s = [] { const char* e = getenv("AMR_FSK_W1S"); return !(e && e[0] == '0'); }();
