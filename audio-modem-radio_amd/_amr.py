@@ -54,7 +54,8 @@ EXPORTS = [
     "amr_comm_synchronize", "amr_comm_allgather_host", "amr_comm_allreduce_max", "amr_comm_world", "amr_tx_samples", "amr_tx_work_bytes", "amr_modulate_host", "amr_modulate_device",
     "amr_resample_host", "amr_hilbert_env_exact_host", "amr_fsk_plan_exact_streams",
     "amr_fsk_plan_set_exact_mode", "amr_psk_plan_set_layout", "amr_psk_plan_split_info", "amr_psk_split_design",
-    "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f",
+    "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f", "amr_split_state_tables",
+    "amr_psk_plan_split_conv",
     "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
 ]
 
@@ -214,6 +215,8 @@ def lib():
             "amr_psk_plan_split_info": (I32, [P, P, P, P, P, P]),
             "amr_psk_split_design": (I32, [P, P, I32, P, P, I32, I64, I64, P, P, P]),
             "amr_psk_split_symbols_host": (I32, [P, P, I32, I64, I64, I64, P]),
+            "amr_split_state_tables": (I32, [P, P, P, I32, I64, P, P]),
+            "amr_psk_plan_split_conv": (I32, [P]),
             "amr_psk_f32_margin": (D, [P, P, I32]),
             "amr_psk_plan_last_f32f": (I32, [P]),
             "amr_psk_demod_host_async": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
@@ -340,6 +343,20 @@ def split_design(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
     return None if rc != 0 else {"warmup_bp": w1.value, "warmup_lp": w2.value, "kappa": k.value}
 
 
+def split_state_tables(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
+    """The time-split band-pass's convolution tables (K [w1][8], Z0 [w1 + 1][8];
+    libamr.so host arithmetic, amr_split_state_tables), or None without a design."""
+    d = split_design(kind, n, baud, carrier, samp_rate)
+    if d is None:
+        return None
+    _, _, bp, _, _ = design_psk(kind, n, baud, carrier, samp_rate)
+    w = d["warmup_bp"]
+    ns = len(bp[0]) - 1
+    K, Z0 = np.zeros((w, ns)), np.zeros((w + 1, ns))
+    check(lib().amr_split_state_tables(ptr(bp[0]), ptr(bp[1]), ptr(bp[2]), len(bp[0]), w, ptr(K), ptr(Z0)))
+    return K, Z0
+
+
 def f32_margin(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000) -> float:
     """The float32 hand-off's symbol error bound per unit max |f| (libamr.so, host arithmetic)."""
     _, _, _, lp, _ = design_psk(kind, n, baud, carrier, samp_rate)
@@ -452,6 +469,11 @@ class PskPlan:
     def last_f32f(self) -> bool:
         """The last call handed the band-pass output to the low-pass in float32."""
         return int(lib().amr_psk_plan_last_f32f(self.handle)) == 1
+
+    def split_conv(self) -> bool:
+        """The time-split layout starts its band-pass chunks from convolution
+        states (KS0) rather than warm-ups (AMR_PSK_SPLIT_CONV=0)."""
+        return int(lib().amr_psk_plan_split_conv(self.handle)) == 1
 
     def split_info(self) -> dict:
         """The time-split layout: streams the last call flagged for the serial path

@@ -94,6 +94,12 @@ struct PskSplit {
   unsigned long long* peak;   // [B] bits of max |ext x| (cleared per launch)
   int32_t* flag;          // [B] 1: a decision inside the margin (cleared per launch)
   int32_t* count;         // [1] flagged streams: the serial fallback's gate
+  // band-pass chunk start states by convolution (KS0) instead
+  // of w1-step warm-ups: conv = 1 uses them
+  int conv;
+  const double* ktab;     // [w1][8] state weights of past inputs (api.cpp split_state_tables)
+  const double* z0tab;    // [w1 + 1][8] scipy's zi state after t zero inputs
+  double* zs;             // [B][c1][8] start states, KS0 -> KS1 (then reused for KS2)
 };
 
 // FSK live-column layout.  A four-step length n = n1 * n2

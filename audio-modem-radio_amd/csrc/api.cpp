@@ -207,6 +207,12 @@ constexpr int64_t kSplitMaxLiveStreams = 64;
 constexpr double kSplitSafety = 64.0;
 constexpr int64_t kSplitMinL = 64;
 constexpr int64_t kSplitLanes = 65536;
+// with KS0's convolution start states: chunks of kSplitConvMinL..MaxL outputs,
+// about kSplitConvChunks per call (the wall-time optimum at 1-64 captures of
+// 96000 samples, tools/split_batch_probe.py)
+constexpr int64_t kSplitConvMinL = 128;
+constexpr int64_t kSplitConvMaxL = 1024;
+constexpr int64_t kSplitConvChunks = 3072;
 
 struct amr_psk_plan {
   std::mutex mu;
@@ -255,6 +261,9 @@ struct amr_psk_plan {
   unsigned long long* split_peak = nullptr;   // [max_streams], then flags [max_streams] and the count
   int32_t* split_flag = nullptr;
   int32_t* split_count = nullptr;
+  double* split_tab = nullptr;    // [w1][8] K, then [w1 + 1][8] Z0 (split_state_tables), with the design
+  double* split_zs = nullptr;     // [B][c1][8] chunk start states (grown per launch)
+  int64_t split_zs_bytes = 0;
   bool last_f32f = false;       // the last lane-layout call handed f over in float32
 };
 
@@ -410,6 +419,8 @@ int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
 
 namespace {
 void split_design(amr_psk_plan* pl);   // below, with run_psk
+void split_state_tables(const Iir& f, int64_t w, double* K, double* Z0);
+bool split_conv_on(const amr_psk_plan* pl);
 bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, int64_t* w1, int64_t* w2,
                        double* kappa);
 double f32_design(const Iir& lp);
@@ -474,7 +485,7 @@ static void plan_free(amr_psk_plan* pl) {
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
   for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
-                  (void*)pl->split_peak,
+                  (void*)pl->split_peak, (void*)pl->split_tab, (void*)pl->split_zs,
                   pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
     if (p) (void)hipFree(p);
@@ -707,6 +718,28 @@ int amr_psk_split_symbols_host(amr_psk_plan* plan, const void* x, int dtype, int
 
 int amr_psk_plan_last_f32f(const amr_psk_plan* plan) { return plan ? (plan->last_f32f ? 1 : 0) : -1; }
 
+int amr_split_state_tables(const double* b, const double* a, const double* zi, int nt, int64_t w, double* K,
+                           double* Z0) {
+  if (!b || !a || !zi || !K || !Z0 || nt < 2 || nt > kMaxTaps || w < 0)
+    return fail(AMR_E_INVALID, "amr_split_state_tables: bad argument");
+  Iir f{};
+  f.nt = nt;
+  for (int i = 0; i < nt; ++i) { f.b[i] = b[i]; f.a[i] = a[i]; }
+  for (int i = 0; i < nt - 1; ++i) f.zi[i] = zi[i];
+  split_state_tables(f, w, K, Z0);
+  return AMR_OK;
+}
+
+int amr_psk_plan_split_conv(amr_psk_plan* plan) {
+  if (!plan) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  if (!plan->split_designed) {
+    if (hipSetDevice(plan->device) != hipSuccess) return 0;
+    split_design(plan);
+  }
+  return split_conv_on(plan) ? 1 : 0;
+}
+
 int amr_psk_plan_split_info(amr_psk_plan* plan, int64_t* flagged, int64_t* warmup_bp, int64_t* warmup_lp,
                             int64_t* chunk, double* kappa) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
@@ -775,9 +808,27 @@ bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, i
 }
 // the launch's chunking: L (0: the plan's rule -- at least kSplitMinL
 // outputs, and long enough to keep a batch within kSplitLanes lanes)
+// AMR_PSK_SPLIT_CONV=0: the w1-step warm-ups instead of KS0's convolution
+bool split_conv_on(const amr_psk_plan* pl) {
+  static const bool conv_env = [] { const char* e = std::getenv("AMR_PSK_SPLIT_CONV"); return !(e && e[0] == '0'); }();
+  return conv_env && pl->split_tab && pl->bp.nt == 9;
+}
 PskSplit split_params(amr_psk_plan* pl, int64_t B, int64_t L) {
   PskSplit sp{};
-  sp.L = L > 0 ? L : std::max<int64_t>(kSplitMinL, (B * pl->p.m1 + kSplitLanes - 1) / kSplitLanes);
+  // AMR_PSK_SPLIT_MINL: a fixed minimum chunk length instead of the rules (an A/B knob)
+  static const int64_t min_l = [] {
+    const char* e = std::getenv("AMR_PSK_SPLIT_MINL");
+    const long v = e ? std::atol(e) : 0;
+    return v >= 8 && v <= 65536 ? (int64_t)v : 0;
+  }();
+  sp.conv = split_conv_on(pl) ? 1 : 0;
+  const int64_t lanes = (B * pl->p.m1 + kSplitLanes - 1) / kSplitLanes;
+  if (L > 0) sp.L = L;
+  else if (min_l > 0) sp.L = std::max<int64_t>(min_l, lanes);
+  else if (sp.conv)   // KS0's work grows with the chunk count, KS1-KS4's serial steps with L
+    sp.L = std::max<int64_t>(lanes, std::min<int64_t>(kSplitConvMaxL, std::max<int64_t>(
+                                        kSplitConvMinL, (B * pl->p.m1 + kSplitConvChunks - 1) / kSplitConvChunks)));
+  else sp.L = std::max<int64_t>(kSplitMinL, lanes);
   sp.w1 = pl->split_w1;
   sp.w2 = pl->split_w2;
   sp.c1 = (pl->p.m1 + sp.L - 1) / sp.L;
@@ -790,6 +841,9 @@ PskSplit split_params(amr_psk_plan* pl, int64_t B, int64_t L) {
   sp.peak = pl->split_peak;
   sp.flag = pl->split_flag;
   sp.count = pl->split_count;
+  sp.ktab = pl->split_tab;
+  sp.z0tab = pl->split_tab ? pl->split_tab + (size_t)sp.w1 * 8 : nullptr;
+  sp.zs = pl->split_zs;
   pl->split_L = sp.L;
   return sp;
 }
@@ -813,6 +867,55 @@ void split_design(amr_psk_plan* pl) {
   pl->split_designed = true;
   pl->split_ok = split_design_core(pl->bp, pl->lp, pl->p.n, pl->p.n_sym, &pl->split_w1, &pl->split_w2,
                                    &pl->split_kappa);
+  if (!pl->split_ok) return;
+  // the band-pass's convolution tables (KS0); without them the plan keeps the warm-ups
+  const int64_t w = pl->split_w1;
+  std::vector<double> tab((size_t)(2 * w + 1) * 8);
+  split_state_tables(pl->bp, w, tab.data(), tab.data() + (size_t)w * 8);
+  if (hipMalloc((void**)&pl->split_tab, tab.size() * 8) != hipSuccess ||
+      hipMemcpy(pl->split_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+    if (pl->split_tab) (void)hipFree(pl->split_tab);
+    pl->split_tab = nullptr;
+    (void)hipGetLastError();
+  }
+}
+// KS0's tables for a filter f (nt - 1 states, DF-II-T, a[0] = 1) in long
+// double, rounded once: K[m] = the state after a unit input and m zero inputs
+// (m < w), Z0[t] = scipy's zi after t zero inputs (t <= w; Z0[0] = zi
+// exactly).  The state before input t0 of a run that started at 0 from zi v0
+// is Z0[t0] v0 + sum_{m < t0} K[m] v(t0 - 1 - m); a run's warm-up computes
+// the same map truncated at m < w (rows of nt - 1 doubles)
+void split_state_tables(const Iir& f, int64_t w, double* K, double* Z0) {
+  const int ns = f.nt - 1;
+  long double z[kMaxTaps], y;
+  auto zero_step = [&]() {
+    y = z[0];
+    for (int i = 0; i < ns - 1; ++i) z[i] = z[i + 1] - (long double)f.a[i + 1] * y;
+    z[ns - 1] = -(long double)f.a[ns] * y;
+  };
+  for (int i = 0; i < ns; ++i)
+    z[i] = (long double)f.b[i + 1] - (long double)f.a[i + 1] * (long double)f.b[0];
+  for (int64_t m = 0; m < w; ++m) {
+    for (int i = 0; i < ns; ++i) K[m * ns + i] = (double)z[i];
+    zero_step();
+  }
+  for (int i = 0; i < ns; ++i) { z[i] = f.zi[i]; Z0[i] = f.zi[i]; }
+  for (int64_t t = 1; t <= w; ++t) {
+    zero_step();
+    for (int i = 0; i < ns; ++i) Z0[t * ns + i] = (double)z[i];
+  }
+}
+int ensure_split_zs(amr_psk_plan* pl, const PskSplit& sp, int64_t B) {
+  if (!sp.conv) return AMR_OK;
+  const int64_t need = B * sp.c1 * 8 * 8;
+  if (pl->split_zs_bytes >= need && pl->split_zs) return AMR_OK;
+  HIP_TRY(hipStreamSynchronize(pl->stream));
+  if (pl->split_zs) HIP_TRY(hipFree(pl->split_zs));
+  pl->split_zs = nullptr;
+  pl->split_zs_bytes = 0;
+  HIP_TRY(hipMalloc((void**)&pl->split_zs, (size_t)need));
+  pl->split_zs_bytes = need;
+  return AMR_OK;
 }
 
 // Launch the whole PSK pipeline on plan->stream.  Caller holds plan->mu.
@@ -916,7 +1019,9 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
   } else if (layout == AMR_LAYOUT_SPLIT) {
-    const PskSplit sp = split_params(pl, B, 0);
+    PskSplit sp = split_params(pl, B, 0);
+    if (int rc = ensure_split_zs(pl, sp, B)) return rc;
+    sp.zs = pl->split_zs;
     HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, st));   // peaks, flags, count
     HIP_TRY(mark(AMR_T_BANDPASS, 0));
     HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, st));
@@ -1027,7 +1132,9 @@ int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B,
   b.n_streams = B;
   b.lo = pl->lo;
   b.lo2 = pl->lo2;
-  const PskSplit sp = split_params(pl, B, L);
+  PskSplit sp = split_params(pl, B, L);
+  if (int rc = ensure_split_zs(pl, sp, B)) return rc;
+  sp.zs = pl->split_zs;
   HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, pl->stream));
   HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, pl->stream));
   HIP_TRY(launch_psk_split_lp(b, pl->p, pl->lp, sp, pl->stream));

@@ -30,6 +30,10 @@
 // Unflagged decisions are therefore the reference's, bit for bit.
 //
 // Kernels (grid.y = stream, lanes = chunks; no LDS, no barriers):
+//   KS0 k_split_bp_state_fwd / _bwd (default; AMR_PSK_SPLIT_CONV=0: off): a
+//                        wave per chunk computes its band-pass start state by
+//                        convolution -> zs [B][c1][8], KS1 / KS2 then run only
+//                        their L outputs (no w1-step warm-up)
 //   KS1 k_split_bp_fwd   ext(x) -> y1 [B][m1]   (+ the stream's input peak)
 //   KS2 k_split_bp_bwd   y1 reversed -> f [B][n]
 //   KS3 k_split_lp_fwd   lane = (chunk, component): f * lo, odd ext -> y3 [B][2][m2]
@@ -72,6 +76,96 @@ __device__ __forceinline__ unsigned long long abs_bits(double v) {
   return (unsigned long long)__double_as_longlong(v) & 0x7fffffffffffffffULL;
 }
 
+// KS0 (sp.conv): a band-pass chunk's start state without a warm-up.  The
+// state before output o0 of a pass that starts at 0 from zi v0 is
+//   Z0[o0] v0 + sum_{m < o0} K[m] v(o0 - 1 - m)
+// (K, Z0: the filter's state responses, api.cpp split_state_tables); the
+// w1-step warm-up computes the same map truncated at m < w1 (the zero start),
+// in w1 dependent steps of one lane.  Here it is a dot product over a whole
+// wave: lane l takes m = l (mod 64) in ascending order (FMA), then a
+// butterfly sum over the lanes (lane 0's order: ((p0 + p1) + (p2 + p3)) ...;
+// oracle/amr_oracle.c conv_state restates it), the Z0 term while o0 <= w1.
+// Chunk 0 keeps scipy's zi * v0.  One wave per chunk, four per workgroup.
+template <typename Val>
+__device__ __forceinline__ void split_conv_state(const PskSplit& sp, int64_t o0, double v0, Val val,
+                                                 double* __restrict__ zo) {
+  const int lane = (int)(threadIdx.x & 63);
+  double acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.0;
+  const int64_t M = o0 < sp.w1 ? o0 : sp.w1;
+  // four terms' loads in flight per lane, then their FMAs in ascending m
+  typedef double V2 __attribute__((ext_vector_type(2)));
+  constexpr int U = 4;
+  for (int64_t m0 = lane; m0 < M; m0 += 64 * U) {
+    double v[U];
+    V2 k[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + 64 * u < M ? m0 + 64 * u : M - 1;   // clamped: loaded, not used
+      v[u] = val(o0 - 1 - m);
+      const V2* kp = reinterpret_cast<const V2*>(sp.ktab + m * 8);
+#pragma unroll
+      for (int h = 0; h < 4; ++h) k[u][h] = kp[h];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (m0 + 64 * u < M) {
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          acc[2 * h] = __builtin_fma(k[u][h][0], v[u], acc[2 * h]);
+          acc[2 * h + 1] = __builtin_fma(k[u][h][1], v[u], acc[2 * h + 1]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = acc[i] + __shfl_xor(acc[i], d, 64);
+  if (lane == 0) {
+    if (o0 == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zo[i] = sp.z0tab[i] * v0;
+    } else if (o0 <= sp.w1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zo[i] = __builtin_fma(sp.z0tab[o0 * 8 + i], v0, acc[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) zo[i] = acc[i];
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= sp.c1) return;   // whole waves
+  const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + s * buf.x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad1;
+  const T x0 = x[0], xl = x[n - 1];
+  split_conv_state(
+      sp, c * sp.L, In<T>::ext(x0, x[pad]),
+      [&](int64_t j) -> double {
+        if (j < pad) return In<T>::ext(x0, x[pad - j]);
+        if (j < pad + n) return In<T>::cvt(x[j - pad]);
+        return In<T>::ext(xl, x[n - 2 - (j - pad - n)]);
+      },
+      sp.zs + (s * sp.c1 + c) * 8);
+}
+
+__global__ __launch_bounds__(256) void k_split_bp_state_bwd(PskBuffers buf, PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= sp.c1) return;
+  const int64_t m1 = p.m1;
+  const double* __restrict__ y1 = sp.y1 + s * m1;
+  split_conv_state(
+      sp, c * sp.L, y1[m1 - 1], [&](int64_t k) { return y1[m1 - 1 - k]; }, sp.zs + (s * sp.c1 + c) * 8);
+}
+
 // KS1: the band-pass's forward pass over ext(x) (odd extension in the input's
 // precision, In<T>), outputs [o0, o1) of chunk c
 template <typename T, bool ZO>
@@ -86,7 +180,12 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
   const T x0 = x[0], xl = x[n - 1];
   double z[8];
   int64_t j = o0 - sp.w1;
-  if (j <= 0) {
+  if (sp.conv) {   // KS0's start state
+    j = o0;
+    const double* zs = sp.zs + (s * sp.c1 + c) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = zs[i];
+  } else if (j <= 0) {
     j = 0;
     const double e0 = In<T>::ext(x0, x[pad]);
 #pragma unroll
@@ -140,7 +239,12 @@ __global__ __launch_bounds__(64) void k_split_bp_bwd(PskBuffers buf, PskParams p
   const int64_t o0 = c * sp.L, o1 = o0 + sp.L < m1 ? o0 + sp.L : m1;
   double z[8];
   int64_t k = o0 - sp.w1;
-  if (k <= 0) {
+  if (sp.conv) {   // KS0's start state
+    k = o0;
+    const double* zs = sp.zs + (s * sp.c1 + c) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = zs[i];
+  } else if (k <= 0) {
     k = 0;
     const double yl = y1[m1 - 1];
 #pragma unroll
@@ -299,14 +403,24 @@ __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p,
   if (flag && atomicOr(&sp.flag[s], 1) == 0) atomicAdd(sp.count, 1);
 }
 
-// KS1 + KS2
+// (KS0 +) KS1 + (KS0 +) KS2
 hipError_t launch_psk_split_bp(const PskBuffers& b, const PskParams& p, const Iir& bp, const PskSplit& sp,
                                hipStream_t st) {
   const int64_t B = b.n_streams;
   if (B < 1) return hipSuccess;
   if (B > 65535 || bp.nt != 9) return hipErrorInvalidValue;
   const dim3 blk(64), g1((unsigned)((sp.c1 + 63) / 64), (unsigned)B);
+  const dim3 blk0(256), g0((unsigned)((sp.c1 + 3) / 4), (unsigned)B);
   const bool zo = p.bp_zero_odd && p.bp_sym;
+  if (sp.conv && (!sp.ktab || !sp.z0tab || !sp.zs)) return hipErrorInvalidValue;
+  if (sp.conv) {
+    switch (b.dtype) {
+      case kF32: hipLaunchKernelGGL(k_split_bp_state_fwd<float>, g0, blk0, 0, st, b, p, sp); break;
+      case kF64: hipLaunchKernelGGL(k_split_bp_state_fwd<double>, g0, blk0, 0, st, b, p, sp); break;
+      case kI16: hipLaunchKernelGGL(k_split_bp_state_fwd<int16_t>, g0, blk0, 0, st, b, p, sp); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (b.dtype) {
     case kF32:
       if (zo) hipLaunchKernelGGL((k_split_bp_fwd<float, true>), g1, blk, 0, st, b, p, bp, sp);
@@ -323,6 +437,7 @@ hipError_t launch_psk_split_bp(const PskBuffers& b, const PskParams& p, const Ii
     default:
       return hipErrorInvalidValue;
   }
+  if (sp.conv) hipLaunchKernelGGL(k_split_bp_state_bwd, g0, blk0, 0, st, b, p, sp);
   if (zo) hipLaunchKernelGGL((k_split_bp_bwd<true>), g1, blk, 0, st, b, p, bp, sp);
   else hipLaunchKernelGGL((k_split_bp_bwd<false>), g1, blk, 0, st, b, p, bp, sp);
   return hipGetLastError();

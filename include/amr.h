@@ -57,13 +57,15 @@
 extern "C" {
 #endif
 
-#define AMR_ABI_VERSION 3   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
+#define AMR_ABI_VERSION 4   /* 2: AMR_TF_EXACT (AMR_TF_COUNT 5), amr_fsk_plan_exact_streams / _set_exact_mode,
                                  amr_resample_host bit-exact; size timing arrays from AMR_*_COUNT
                                3: AMR_LAYOUT_SPLIT, amr_psk_plan_set_layout, amr_psk_plan_split_info,
                                   amr_psk_split_design, amr_psk_split_symbols_host, the float32 hand-off
                                   (amr_psk_f32_margin, amr_psk_plan_last_f32f), amr_fsk_plan_resident_bytes,
                                   the FSK time-split F1 (AMR_FSK_LAYOUT_*, amr_fsk_plan_set_layout,
-                                  amr_fsk_plan_split_info, amr_fsk_split_design, amr_fsk_split_bandpass_host) */
+                                  amr_fsk_plan_split_info, amr_fsk_split_design, amr_fsk_split_bandpass_host)
+                               4: the time-split band-pass's chunk start states by convolution
+                                  (amr_split_state_tables, amr_psk_plan_split_conv) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -193,6 +195,20 @@ int amr_psk_plan_last_f32f(const amr_psk_plan *plan);
  * the time-split layout computes them -- not bit-exact). */
 int amr_psk_split_symbols_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                                int64_t chunk, double *sym);
+/* The time-split band-pass's chunk start states: instead of
+ * running w samples of recursion from a zero state, a chunk starting at
+ * output t0 takes Z0[t0] v0 + sum_{m < min(t0, w)} K[m] v(t0 - 1 - m) (the
+ * Z0 term while t0 <= w), a dot product the GPU spreads over a wave.  Host
+ * arithmetic (long double, rounded once) for a DF-II-T filter b, a (a[0] = 1,
+ * ntaps - 1 states) and scipy's zi: K [w][ntaps - 1] = the state after a unit
+ * input and m zero inputs, Z0 [w + 1][ntaps - 1] = zi after t zero inputs.
+ * amr_psk_plan_split_conv: 1 when the plan's time-split layout uses them (its
+ * tables are built with the design; AMR_PSK_SPLIT_CONV=0 selects the
+ * warm-ups), 0 when not, -1 for NULL.  Both replace no reference function
+ * (modem.py:194-199's filtfilt is what they approximate). */
+int amr_split_state_tables(const double *b, const double *a, const double *zi, int ntaps, int64_t w, double *K,
+                           double *Z0);
+int amr_psk_plan_split_conv(amr_psk_plan *plan);
 /* number of streams the exact complex low-pass path re-ran in the last call */
 int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
 

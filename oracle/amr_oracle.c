@@ -337,6 +337,38 @@ static void chunked_pass_w(const double *b, const double *a, int nt, const doubl
         }
     }
 }
+/* conv_state: psk_split_kernels.hip KS0 restated -- a chunk's start state as
+ * Z0[o0] in[0] + sum_{m < min(o0, w)} K[m] in[o0 - 1 - m] (the Z0 term while
+ * o0 <= w; zi * in[0] for o0 = 0), summed as the wave does: 64 partial sums,
+ * lane l over m = l (mod 64) ascending with fma, then the butterfly
+ * p[l] + p[l ^ d] for d = 1, 2, ..., 32, lane 0's value.  K [w][ns], Z0
+ * [w + 1][ns] (amr_split_state_tables). */
+static void conv_state(const double *K, const double *Z0, int ns, const double *in, int64_t o0, int64_t w,
+                       double *z)
+{
+    double p[64][16], q[64][16];
+    if (o0 == 0) { for (int i = 0; i < ns; ++i) z[i] = Z0[i] * in[0]; return; }
+    for (int l = 0; l < 64; ++l) for (int i = 0; i < ns; ++i) p[l][i] = 0.0;
+    const int64_t M = o0 < w ? o0 : w;
+    for (int64_t m = 0; m < M; ++m)
+        for (int i = 0; i < ns; ++i) p[m & 63][i] = fma(K[m * ns + i], in[o0 - 1 - m], p[m & 63][i]);
+    for (int d = 1; d < 64; d <<= 1) {
+        for (int l = 0; l < 64; ++l) for (int i = 0; i < ns; ++i) q[l][i] = p[l][i] + p[l ^ d][i];
+        memcpy(p, q, sizeof(p));
+    }
+    for (int i = 0; i < ns; ++i) z[i] = o0 <= w ? fma(Z0[o0 * ns + i], in[0], p[0][i]) : p[0][i];
+}
+/* a chunked pass whose chunks start from conv_state (no warm-up steps) */
+static void chunked_pass_conv(const double *b, const double *a, int nt, const double *in, double *out, int64_t m,
+                              int64_t L, int64_t w, const double *K, const double *Z0)
+{
+    double z[32];
+    for (int64_t o0 = 0; o0 < m; o0 += L) {
+        const int64_t o1 = o0 + L < m ? o0 + L : m;
+        conv_state(K, Z0, nt - 1, in, o0, w, z);
+        for (int64_t j = o0; j < o1; ++j) df2t(b, a, nt, z, in + j, &out[j], 1, 1);
+    }
+}
 static void chunked_pass(const double *b, const double *a, int nt, const double *zi,
                          const double *in, double *out, int64_t m, int64_t L, int64_t w)
 {
@@ -370,8 +402,11 @@ int oracle_split_filtfilt(const double *b, const double *a, int nt, const double
 int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sps, int64_t first,
                                  const double *bp_b, const double *bp_a, int bp_nt, const double *bp_zi,
                                  const double *lp_b, const double *lp_a, int lp_nt, const double *lp_zi,
-                                 const double *lo, int64_t L, int64_t w1, int64_t w2, double *sym)
+                                 const double *lo, int64_t L, int64_t w1, int64_t w2, const double *K,
+                                 const double *Z0, double *sym)
 {
+    /* K, Z0 (both or neither): the band-pass chunks start from conv_state
+     * (the GPU's default), else from w1-step FMA-form warm-ups */
     const int pad1 = 3 * bp_nt, pad2 = 3 * lp_nt;
     if (n <= pad1 || n <= pad2 || L < 1) return -1;
     const int64_t S = (n > first) ? (n - first + sps - 1) / sps : 0;
@@ -382,9 +417,15 @@ int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sp
     double *r = (double *)malloc(sizeof(double) * (size_t)m1);
     double *g = (double *)malloc(sizeof(double) * 2 * (size_t)n);
     for (int64_t j = 0; j < m1; ++j) e[j] = ext_sample(x, dtype, n, pad1, j);
-    chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, e, y, m1, L, w1, 1);
-    for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
-    chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, r, y, m1, L, w1, 1);
+    if (K && Z0 && bp_nt <= 17) {
+        chunked_pass_conv(bp_b, bp_a, bp_nt, e, y, m1, L, w1, K, Z0);
+        for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
+        chunked_pass_conv(bp_b, bp_a, bp_nt, r, y, m1, L, w1, K, Z0);
+    } else {
+        chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, e, y, m1, L, w1, 1);
+        for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
+        chunked_pass_w(bp_b, bp_a, bp_nt, bp_zi, r, y, m1, L, w1, 1);
+    }
     for (int64_t i = 0; i < n; ++i)                      /* f[i] = y[m1 - 1 - pad1 - i]; (f + 0j) * lo */
         cmul_np(y[m1 - 1 - pad1 - i], 0.0, lo[2 * i], lo[2 * i + 1], &g[2 * i], &g[2 * i + 1]);
     for (int c = 0; c < 2; ++c) {

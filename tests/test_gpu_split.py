@@ -64,9 +64,53 @@ def test_split_symbols_are_the_restatement(kind, baud, fc, fs, n, dtype, chunk):
     got = pl.split_symbols(x, chunk)
     info = pl.split_info()
     assert info["warmup_bp"] > 0 and info["chunk"] == (chunk or info["chunk"])
+    # the default start states: KS0's convolution (AMR_PSK_SPLIT_CONV=0: warm-ups,
+    # test_split_warmup_variant)
+    tables = _amr.split_state_tables(kind, n, baud, fc, fs) if pl.split_conv() else None
+    assert tables is not None or os.environ.get("AMR_PSK_SPLIT_CONV") == "0"
     for i in range(B):
-        want = oracle.psk_split_symbols(kind, x[i], baud, fc, fs, info["chunk"], info["warmup_bp"], info["warmup_lp"])
+        want = oracle.psk_split_symbols(kind, x[i], baud, fc, fs, info["chunk"], info["warmup_bp"], info["warmup_lp"],
+                                        tables=tables)
         assert np.array_equal(got[i], want), (i, np.abs(got[i] - want).max())
+
+
+def test_split_warmup_variant(tmp_path):
+    """AMR_PSK_SPLIT_CONV=0 (a subprocess: the switch is read once): the band-pass
+    chunks start from w1-step warm-ups instead of KS0's convolution states --
+    the restatement without tables, and bytes == the oracle on a seeded batch."""
+    import subprocess
+    import sys
+    script = tmp_path / "warm.py"
+    script.write_text(f'''
+import sys
+sys.path[:0] = {[os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."),
+                 os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "audio-modem-radio_amd"),
+                 os.path.dirname(os.path.abspath(__file__))]!r}
+import numpy as np
+import _amr, synth
+from oracle import oracle
+bad = []
+for kind, baud, n, B in (("qpsk", 9600, 96000, 3), ("bpsk", 1200, 48000, 2)):
+    x = synth.qpsk_batch(B, n, baud, seed=B, distinct=B, noise=0.1)
+    pl = _amr.PskPlan(kind, n, baud, 3000.0, 96000, max_streams=B)
+    assert not pl.split_conv()
+    got = pl.split_symbols(x, 0)
+    info = pl.split_info()
+    for i in range(B):
+        want = oracle.psk_split_symbols(kind, x[i], baud, 3000.0, 96000, info["chunk"], info["warmup_bp"], info["warmup_lp"])
+        if not np.array_equal(got[i], want):
+            bad.append((kind, "sym", i))
+    pl.set_layout("split")
+    o, s = pl.demod_host(x)
+    wo, ws = oracle.psk_demod_batch(kind, x, baud, 3000.0, 96000)
+    if list(o) != list(wo) or [int(v) for v in s] != [int(v) for v in ws]:
+        bad.append((kind, "bytes"))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+''')
+    env = dict(os.environ, AMR_PSK_SPLIT_CONV="0")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
 
 def _split_plan(kind, n, baud, fc=3000.0, fs=96000, B=1):

@@ -52,16 +52,18 @@ def test_split_error_far_below_kappa(kind, baud, fc, fs, built_lib):
     n = 48000 if baud >= 1200 else 96000
     d = _amr.split_design(kind, n, baud, fc, fs)
     assert d is not None and d["kappa"] > 0 and 0 < d["warmup_bp"] <= n // 4
+    T = _amr.split_state_tables(kind, n, baud, fc, fs)
     rng = np.random.default_rng(baud + int(fc))
     worst, where = 0.0, None
     for name, x in _inputs(kind, baud, fc, fs, n, rng).items():
         ref = oracle.psk_symbols(kind, x, baud, fc, fs)
         peak = np.abs(x).max()
         for L in (64, 97, 5000):
-            sp = oracle.psk_split_symbols(kind, x, baud, fc, fs, L, d["warmup_bp"], d["warmup_lp"])
-            err = np.abs(sp - ref).max() / peak
-            if err > worst:
-                worst, where = err, (name, L)
+            for tables in (None, T):     # the w1-step warm-ups, KS0's convolution start states
+                sp = oracle.psk_split_symbols(kind, x, baud, fc, fs, L, d["warmup_bp"], d["warmup_lp"], tables=tables)
+                err = np.abs(sp - ref).max() / peak
+                if err > worst:
+                    worst, where = err, (name, L, "warm" if tables is None else "conv")
     print(f"{kind}@{baud} fc {fc:g} fs {fs:g}: kappa {d['kappa']:.3e}, worst |split - serial| / peak {worst:.3e} "
           f"({where}), kappa / worst = {d['kappa'] / worst:.1f}")
     assert worst <= d["kappa"] / 16
