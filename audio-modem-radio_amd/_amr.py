@@ -57,6 +57,7 @@ EXPORTS = [
     "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f", "amr_split_state_tables",
     "amr_psk_plan_split_conv",
     "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
+    "amr_fsk_plan_split_conv",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -262,6 +263,7 @@ def lib():
             "amr_fsk_plan_split_info": (I32, [P, P, P, P, P, P]),
             "amr_fsk_split_design": (I32, [I64, P, P, P, P, I32, P, P, P]),
             "amr_fsk_split_bandpass_host": (I32, [P, P, I32, I64, I64, I64, P]),
+            "amr_fsk_plan_split_conv": (I32, [P]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),
             "amr_modulate_host": (I32, [I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64]),
             "amr_modulate_device": (I32, [P, I32, D, D, D, D, P, I64, P, I64, P, I64, I64, P, I64, P, I64]),
@@ -341,6 +343,14 @@ def split_design(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
     rc = lib().amr_psk_split_design(ptr(bp[0]), ptr(bp[1]), len(bp[0]), ptr(lp[0]), ptr(lp[1]), len(lp[0]), n, S,
                                     ctypes.byref(w1), ctypes.byref(w2), ctypes.byref(k))
     return None if rc != 0 else {"warmup_bp": w1.value, "warmup_lp": w2.value, "kappa": k.value}
+
+
+def state_tables(b, a, zi, w: int):
+    """amr_split_state_tables for one DF-II-T filter: (K [w][nt-1], Z0 [w+1][nt-1])."""
+    b, a, zi = (np.ascontiguousarray(v, np.float64) for v in (b, a, zi))
+    K, Z0 = np.zeros((w, len(b) - 1)), np.zeros((w + 1, len(b) - 1))
+    check(lib().amr_split_state_tables(ptr(b), ptr(a), ptr(zi), len(b), int(w), ptr(K), ptr(Z0)))
+    return K, Z0
 
 
 def split_state_tables(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):

@@ -150,6 +150,11 @@ class FskPlan:
         """F1 per call: "auto" (split for <= 1024 streams), "serial", "split" (include/amr.h)."""
         check(lib().amr_fsk_plan_set_layout(self.handle, FSK_LAYOUTS[layout]))
 
+    def split_conv(self) -> bool:
+        """The time-split F1 starts its chunks from convolution states (FS0)
+        rather than warm-ups (AMR_FSK_SPLIT_CONV=0)."""
+        return int(lib().amr_fsk_plan_split_conv(self.handle)) == 1
+
     def split_info(self) -> dict:
         """The last call's F1 layout and the plan's split design."""
         ls, w, L = ctypes.c_int(0), ctypes.c_int64(0), ctypes.c_int64(0)

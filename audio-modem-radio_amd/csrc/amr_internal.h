@@ -97,7 +97,7 @@ struct PskSplit {
   // band-pass chunk start states by convolution (KS0) instead
   // of w1-step warm-ups: conv = 1 uses them
   int conv;
-  const double* ktab;     // [w1][8] state weights of past inputs (api.cpp split_state_tables)
+  const double* ktab;     // [w1][8] state weights of past inputs (iir_design.h split_state_tables)
   const double* z0tab;    // [w1 + 1][8] scipy's zi state after t zero inputs
   double* zs;             // [B][c1][8] start states, KS0 -> KS1 (then reused for KS2)
 };
@@ -206,6 +206,11 @@ struct FskSplit {
   double tau;                 // kAmbTau + tau_env: F2's margin scale for these streams
   double* y1;                 // [B][2][m1] forward outputs (tone-major per stream)
   unsigned long long* peak;   // [B] bits of max |ext x| (cleared per launch)
+  // chunk start states by convolution (FS0, as the PSK split's KS0): conv = 1 uses them
+  int conv;
+  const double* ktab;         // [2 tones][w][6] (iir_design.h split_state_tables)
+  const double* z0tab;        // [2 tones][w + 1][6]
+  double* zs;                 // [B][2][c][6] start states, FS0 -> FS1 (then reused for FS2)
 };
 
 struct FskIir {            // [tone][tap], tone 0 = mark

@@ -419,7 +419,6 @@ int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
 
 namespace {
 void split_design(amr_psk_plan* pl);   // below, with run_psk
-void split_state_tables(const Iir& f, int64_t w, double* K, double* Z0);
 bool split_conv_on(const amr_psk_plan* pl);
 bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, int64_t* w1, int64_t* w2,
                        double* kappa);
@@ -877,32 +876,6 @@ void split_design(amr_psk_plan* pl) {
     if (pl->split_tab) (void)hipFree(pl->split_tab);
     pl->split_tab = nullptr;
     (void)hipGetLastError();
-  }
-}
-// KS0's tables for a filter f (nt - 1 states, DF-II-T, a[0] = 1) in long
-// double, rounded once: K[m] = the state after a unit input and m zero inputs
-// (m < w), Z0[t] = scipy's zi after t zero inputs (t <= w; Z0[0] = zi
-// exactly).  The state before input t0 of a run that started at 0 from zi v0
-// is Z0[t0] v0 + sum_{m < t0} K[m] v(t0 - 1 - m); a run's warm-up computes
-// the same map truncated at m < w (rows of nt - 1 doubles)
-void split_state_tables(const Iir& f, int64_t w, double* K, double* Z0) {
-  const int ns = f.nt - 1;
-  long double z[kMaxTaps], y;
-  auto zero_step = [&]() {
-    y = z[0];
-    for (int i = 0; i < ns - 1; ++i) z[i] = z[i + 1] - (long double)f.a[i + 1] * y;
-    z[ns - 1] = -(long double)f.a[ns] * y;
-  };
-  for (int i = 0; i < ns; ++i)
-    z[i] = (long double)f.b[i + 1] - (long double)f.a[i + 1] * (long double)f.b[0];
-  for (int64_t m = 0; m < w; ++m) {
-    for (int i = 0; i < ns; ++i) K[m * ns + i] = (double)z[i];
-    zero_step();
-  }
-  for (int i = 0; i < ns; ++i) { z[i] = f.zi[i]; Z0[i] = f.zi[i]; }
-  for (int64_t t = 1; t <= w; ++t) {
-    zero_step();
-    for (int i = 0; i < ns; ++i) Z0[t * ns + i] = (double)z[i];
   }
 }
 int ensure_split_zs(amr_psk_plan* pl, const PskSplit& sp, int64_t B) {

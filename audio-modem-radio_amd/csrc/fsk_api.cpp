@@ -410,6 +410,11 @@ struct amr_fsk_plan {
   int64_t split_cap = 0;       // streams split_y1 / split_peak hold
   int64_t split_alloc = 0;     // their bytes (not in scratch_bytes)
   int64_t split_reserved = 0;  // what amr_fsk_plan_bytes_estimate counts for them (<= 1024 streams)
+  // FS0's convolution start states: tables [2][w][6] + [2][w + 1][6] (host
+  // copy made with the design), on the device with the zs states in split_cz
+  std::vector<double> split_tab_host;
+  double* split_cz = nullptr;
+  int64_t split_cz_bytes = 0;
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
   void* d_x = nullptr;
@@ -433,7 +438,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
                   (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL,
-                  (void*)pl->split_y1, (void*)pl->split_peak})
+                  (void*)pl->split_y1, (void*)pl->split_peak, (void*)pl->split_cz})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -466,10 +471,27 @@ constexpr int64_t kFskSplitMaxStreams = 1024;   // AUTO: calls of at most this m
 // long enough to keep a launch within kFskSplitLanes lanes)
 constexpr int64_t kFskSplitMinL = 64;
 constexpr int64_t kFskSplitLanes = 65536;
+// with FS0's convolution start states (AMR_FSK_SPLIT_CONV=0: the warm-ups):
+// chunks of kFskSplitConvMinL..MaxL outputs, about kFskSplitConvChunks (chunk,
+// tone) waves per call -- the PSK split's rule (api.cpp kSplitConv*)
+constexpr int64_t kFskSplitConvMinL = 128;
+constexpr int64_t kFskSplitConvMaxL = 1024;
+constexpr int64_t kFskSplitConvChunks = 3072;
+bool fsk_split_conv_on(const amr_fsk_plan* pl) {
+  static const bool env = [] { const char* e = std::getenv("AMR_FSK_SPLIT_CONV"); return !(e && e[0] == '0'); }();
+  return env && pl->split_ok && !pl->split_tab_host.empty();
+}
 FskSplit fsk_split_params(amr_fsk_plan* pl, int64_t B, int64_t L) {
   FskSplit sp{};
   const int64_t m1 = pl->p.n + 2 * (int64_t)pl->p.pad;
-  sp.L = L > 0 ? L : std::max({kFskSplitMinL, pl->split_w / 4, (2 * B * m1 + kFskSplitLanes - 1) / kFskSplitLanes});
+  sp.conv = fsk_split_conv_on(pl) ? 1 : 0;
+  const int64_t lanes = (2 * B * m1 + kFskSplitLanes - 1) / kFskSplitLanes;
+  if (L > 0) sp.L = L;
+  else if (sp.conv)
+    sp.L = std::max(lanes, std::min(kFskSplitConvMaxL, std::max(kFskSplitConvMinL,
+                                                                  (2 * B * m1 + kFskSplitConvChunks - 1) /
+                                                                      kFskSplitConvChunks)));
+  else sp.L = std::max({kFskSplitMinL, pl->split_w / 4, lanes});
   sp.w = pl->split_w;
   sp.c = (m1 + sp.L - 1) / sp.L;
   sp.tau = pl->split_tau;
@@ -477,6 +499,30 @@ FskSplit fsk_split_params(amr_fsk_plan* pl, int64_t B, int64_t L) {
   sp.peak = pl->split_peak;
   pl->split_L = sp.L;
   return sp;
+}
+// the tables and this call's zs in split_cz (grown as needed; counted in
+// split_alloc), then sp's pointers into it
+int ensure_split_conv(amr_fsk_plan* pl, FskSplit& sp, int64_t B) {
+  if (!sp.conv) return AMR_OK;
+  const int64_t tab = (int64_t)pl->split_tab_host.size() * 8;
+  const int64_t need = tab + B * 2 * sp.c * 6 * 8;
+  if (pl->split_cz_bytes < need || !pl->split_cz) {
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    if (pl->split_cz) {
+      (void)hipFree(pl->split_cz);
+      pl->split_alloc -= pl->split_cz_bytes;
+    }
+    pl->split_cz = nullptr;
+    pl->split_cz_bytes = 0;
+    HIP_TRY(hipMalloc((void**)&pl->split_cz, (size_t)need));
+    HIP_TRY(hipMemcpy(pl->split_cz, pl->split_tab_host.data(), (size_t)tab, hipMemcpyHostToDevice));
+    pl->split_cz_bytes = need;
+    pl->split_alloc += need;
+  }
+  sp.ktab = pl->split_cz;
+  sp.z0tab = pl->split_cz + 2 * sp.w * 6;
+  sp.zs = pl->split_cz + tab / 8;
+  return AMR_OK;
 }
 int ensure_split_buffers(amr_fsk_plan* pl, int64_t B) {
   if (B <= pl->split_cap) return AMR_OK;
@@ -487,13 +533,13 @@ int ensure_split_buffers(amr_fsk_plan* pl, int64_t B) {
     (void)hipFree(pl->split_peak);
     pl->split_y1 = nullptr;
     pl->split_peak = nullptr;
-    pl->split_alloc = 0;
+    pl->split_alloc = pl->split_cz_bytes;
     pl->split_cap = 0;
   }
   HIP_TRY(hipMalloc(&pl->split_y1, (size_t)(B * 2 * m1 * 8)));
   HIP_TRY(hipMalloc(&pl->split_peak, (size_t)(B * 8)));
   pl->split_cap = B;
-  pl->split_alloc = B * (2 * m1 * 8 + 8);
+  pl->split_alloc = B * (2 * m1 * 8 + 8) + pl->split_cz_bytes;
   return AMR_OK;
 }
 // does this call run the split F1?  Only with the exact path on (it is what
@@ -511,7 +557,9 @@ int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t 
   p.force_exact = pl->exact_mode == 2 ? 1 : 0;
   if (pl->split_now) {
     if (int rc = ensure_split_buffers(pl, B)) return rc;
-    HIP_TRY(launch_fsk_split(dtype, d_x, x_stride, B, pl->z, p, pl->f, fsk_split_params(pl, B, 0), pl->stream));
+    FskSplit sp = fsk_split_params(pl, B, 0);
+    if (int rc = ensure_split_conv(pl, sp, B)) return rc;
+    HIP_TRY(launch_fsk_split(dtype, d_x, x_stride, B, pl->z, p, pl->f, sp, pl->stream));
     return AMR_OK;
   }
   HIP_TRY(launch_fsk_bandpass(dtype, d_x, x_stride, B, reinterpret_cast<double*>(pl->u), pl->z, p, pl->f,
@@ -834,7 +882,10 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
   g.out = max_streams * (g.out_cap + 16);            // host-API output staging
-  g.split = std::min<int64_t>(max_streams, kFskSplitMaxStreams) * (2 * (n + 2 * (int64_t)p.pad) * 8 + 8);
+  // (+ FS0's tables, w <= n / 4, and start states at L >= kFskSplitConvMinL)
+  g.split = std::min<int64_t>(max_streams, kFskSplitMaxStreams) *
+                (2 * (n + 2 * (int64_t)p.pad) * 8 + 8 + 96 * ((n + 2 * (int64_t)p.pad) / kFskSplitConvMinL + 2)) +
+            2 * (2 * (n / 4) + 1) * 48;
   // the exact path (AMR_FSK_EXACT=0: off), at every length with decisions to make
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
   g.exact = exact_env && p.n_bits > 0;
@@ -1085,6 +1136,17 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     pl->split_kappa = kappa;
     pl->split_hl1 = hl1;
     pl->split_tau = kAmbTau + kappa * hl1;
+    if (pl->split_ok) {   // FS0's tables, per tone: K [w][6], then Z0 [w + 1][6]
+      const int64_t w = pl->split_w;
+      pl->split_tab_host.assign((size_t)(2 * w + 2 * (w + 1)) * 6, 0.0);
+      for (int t = 0; t < 2; ++t) {
+        Iir fi{};
+        fi.nt = nt;
+        for (int i = 0; i < nt; ++i) { fi.b[i] = pl->f.b[t][i]; fi.a[i] = pl->f.a[t][i]; fi.zi[i] = pl->f.zi[t][i]; }
+        split_state_tables(fi, w, pl->split_tab_host.data() + (size_t)t * w * 6,
+                           pl->split_tab_host.data() + (size_t)(2 * w + t * (w + 1)) * 6);
+      }
+    }
   }
   *out = pl;
   return AMR_OK;
@@ -1112,6 +1174,8 @@ int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
+
+int amr_fsk_plan_split_conv(const amr_fsk_plan* plan) { return plan ? (fsk_split_conv_on(plan) ? 1 : 0) : -1; }
 
 int amr_fsk_plan_set_layout(amr_fsk_plan* plan, int layout) {
   if (!plan || layout < AMR_FSK_LAYOUT_AUTO || layout > AMR_FSK_LAYOUT_SPLIT)
@@ -1150,7 +1214,9 @@ int amr_fsk_split_bandpass_host(amr_fsk_plan* plan, const void* x, int dtype, in
   FskParams p = plan->p;
   p.lc = LiveCols{};                         // natural order for the caller
   p.amb = nullptr;
-  HIP_TRY(launch_fsk_split(dtype, xs, n, B, plan->z, p, plan->f, fsk_split_params(plan, B, chunk), plan->stream));
+  FskSplit sp = fsk_split_params(plan, B, chunk);
+  if (int rc = ensure_split_conv(plan, sp, B)) return rc;
+  HIP_TRY(launch_fsk_split(dtype, xs, n, B, plan->z, p, plan->f, sp, plan->stream));
   HIP_TRY(hipMemcpyAsync(out, plan->z, (size_t)(B * n * 16), hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipStreamSynchronize(plan->stream));
   return AMR_OK;

@@ -656,6 +656,45 @@ __device__ __forceinline__ void fsk_split_warm(double (&z)[6], const double (&b)
   z[5] = __builtin_fma(-a[6], y, b[6] * x);
 }
 
+// FS0 (sp.conv): a chunk's start state by convolution instead of a w-step
+// warm-up (split_chain.h split_conv_state; the PSK split's KS0): one wave
+// per (chunk, tone), four per workgroup, -> zs; before FS1 over ext(x) and
+// again before FS2 over y1 reversed
+template <typename T>
+__global__ __launch_bounds__(256) void k_fsk_split_state_fwd(const void* xv, int64_t x_stride, FskParams p,
+                                                             FskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= 2 * sp.c) return;   // whole waves
+  const int tone = (int)(q & 1);
+  const int64_t c = q >> 1;
+  const T* __restrict__ x = reinterpret_cast<const T*>(xv) + s * x_stride;
+  const int64_t n = p.n;
+  const int pad = p.pad;
+  const T x0 = x[0], xl = x[n - 1];
+  split_conv_state<6>(
+      sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L,
+      FIn<T>::ext(x0, x[pad]),
+      [&](int64_t j) -> double {
+        if (j < pad) return FIn<T>::ext(x0, x[pad - j]);
+        if (j < pad + n) return FIn<T>::cvt(x[j - pad]);
+        return FIn<T>::ext(xl, x[n - 2 - (j - pad - n)]);
+      },
+      sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6);
+}
+__global__ __launch_bounds__(256) void k_fsk_split_state_bwd(FskParams p, FskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= 2 * sp.c) return;
+  const int tone = (int)(q & 1);
+  const int64_t c = q >> 1;
+  const int64_t m1 = p.n + 2 * (int64_t)p.pad;
+  const double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
+  split_conv_state<6>(
+      sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L, y1[m1 - 1],
+      [&](int64_t k) { return y1[m1 - 1 - k]; }, sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6);
+}
+
 // FS1: forward pass over ext(x) (odd extension in the input's precision, as
 // F1), outputs [o0, o1) of chunk c for tone q & 1 -> y1; tone-0 lanes keep
 // the stream's max |ext x|
@@ -677,7 +716,12 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
   for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
   const T x0 = x[0], xl = x[n - 1];
   int64_t j = o0 - sp.w;
-  if (j <= 0) {
+  if (sp.conv) {   // FS0's start state
+    j = o0;
+    const double* zs = sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = zs[i];
+  } else if (j <= 0) {
     j = 0;
     const double e0 = FIn<T>::ext(x0, x[pad]);
 #pragma unroll
@@ -734,7 +778,12 @@ __global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, F
   for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
   const double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
   int64_t k = o0 - sp.w;
-  if (k <= 0) {
+  if (sp.conv) {   // FS0's start state
+    k = o0;
+    const double* zs = sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) z[i] = zs[i];
+  } else if (k <= 0) {
     k = 0;
     const double yl = y1[m1 - 1];
 #pragma unroll
@@ -767,6 +816,16 @@ template <int MODE>
 static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride, int64_t B, double2* z,
                                      const FskParams& p, const FskIir& f, const FskSplit& sp, hipStream_t st) {
   const dim3 blk(64), g((unsigned)((2 * sp.c + 63) / 64), (unsigned)B);
+  const dim3 blk0(256), g0((unsigned)((2 * sp.c + 3) / 4), (unsigned)B);
+  if (sp.conv && (!sp.ktab || !sp.z0tab || !sp.zs)) return hipErrorInvalidValue;
+  if (sp.conv) {
+    switch (dtype) {
+      case kF32: hipLaunchKernelGGL(k_fsk_split_state_fwd<float>, g0, blk0, 0, st, x, x_stride, p, sp); break;
+      case kF64: hipLaunchKernelGGL(k_fsk_split_state_fwd<double>, g0, blk0, 0, st, x, x_stride, p, sp); break;
+      case kI16: hipLaunchKernelGGL(k_fsk_split_state_fwd<int16_t>, g0, blk0, 0, st, x, x_stride, p, sp); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (dtype) {
     case kF32: hipLaunchKernelGGL((k_fsk_split_fwd<float, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
     case kF64: hipLaunchKernelGGL((k_fsk_split_fwd<double, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
@@ -774,6 +833,7 @@ static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride,
     default: return hipErrorInvalidValue;
   }
   double* zd = reinterpret_cast<double*>(z);
+  if (sp.conv) hipLaunchKernelGGL(k_fsk_split_state_bwd, g0, blk0, 0, st, p, sp);
   if (p.lc.on) hipLaunchKernelGGL((k_fsk_split_bwd<MODE, true>), g, blk, 0, st, zd, p, f, sp);
   else hipLaunchKernelGGL((k_fsk_split_bwd<MODE, false>), g, blk, 0, st, zd, p, f, sp);
   if (p.amb) hipLaunchKernelGGL(k_fsk_split_amb, dim3((unsigned)((B + 63) / 64)), blk, 0, st, B, p, sp);

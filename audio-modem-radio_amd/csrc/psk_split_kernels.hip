@@ -85,58 +85,8 @@ __device__ __forceinline__ unsigned long long abs_bits(double v) {
 // wave: lane l takes m = l (mod 64) in ascending order (FMA), then a
 // butterfly sum over the lanes (lane 0's order: ((p0 + p1) + (p2 + p3)) ...;
 // oracle/amr_oracle.c conv_state restates it), the Z0 term while o0 <= w1.
-// Chunk 0 keeps scipy's zi * v0.  One wave per chunk, four per workgroup.
-template <typename Val>
-__device__ __forceinline__ void split_conv_state(const PskSplit& sp, int64_t o0, double v0, Val val,
-                                                 double* __restrict__ zo) {
-  const int lane = (int)(threadIdx.x & 63);
-  double acc[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = 0.0;
-  const int64_t M = o0 < sp.w1 ? o0 : sp.w1;
-  // four terms' loads in flight per lane, then their FMAs in ascending m
-  typedef double V2 __attribute__((ext_vector_type(2)));
-  constexpr int U = 4;
-  for (int64_t m0 = lane; m0 < M; m0 += 64 * U) {
-    double v[U];
-    V2 k[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t m = m0 + 64 * u < M ? m0 + 64 * u : M - 1;   // clamped: loaded, not used
-      v[u] = val(o0 - 1 - m);
-      const V2* kp = reinterpret_cast<const V2*>(sp.ktab + m * 8);
-#pragma unroll
-      for (int h = 0; h < 4; ++h) k[u][h] = kp[h];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (m0 + 64 * u < M) {
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          acc[2 * h] = __builtin_fma(k[u][h][0], v[u], acc[2 * h]);
-          acc[2 * h + 1] = __builtin_fma(k[u][h][1], v[u], acc[2 * h + 1]);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = acc[i] + __shfl_xor(acc[i], d, 64);
-  if (lane == 0) {
-    if (o0 == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) zo[i] = sp.z0tab[i] * v0;
-    } else if (o0 <= sp.w1) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) zo[i] = __builtin_fma(sp.z0tab[o0 * 8 + i], v0, acc[i]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) zo[i] = acc[i];
-    }
-  }
-}
-
+// Chunk 0 keeps scipy's zi * v0.  One wave per chunk, four per workgroup
+// (split_chain.h split_conv_state).
 template <typename T>
 __global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskParams p, PskSplit sp) {
   const int64_t s = blockIdx.y;
@@ -146,8 +96,8 @@ __global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskP
   const int64_t n = p.n;
   const int pad = p.pad1;
   const T x0 = x[0], xl = x[n - 1];
-  split_conv_state(
-      sp, c * sp.L, In<T>::ext(x0, x[pad]),
+  split_conv_state<8>(
+      sp.ktab, sp.z0tab, sp.w1, c * sp.L, In<T>::ext(x0, x[pad]),
       [&](int64_t j) -> double {
         if (j < pad) return In<T>::ext(x0, x[pad - j]);
         if (j < pad + n) return In<T>::cvt(x[j - pad]);
@@ -162,8 +112,9 @@ __global__ __launch_bounds__(256) void k_split_bp_state_bwd(PskBuffers buf, PskP
   if (c >= sp.c1) return;
   const int64_t m1 = p.m1;
   const double* __restrict__ y1 = sp.y1 + s * m1;
-  split_conv_state(
-      sp, c * sp.L, y1[m1 - 1], [&](int64_t k) { return y1[m1 - 1 - k]; }, sp.zs + (s * sp.c1 + c) * 8);
+  split_conv_state<8>(
+      sp.ktab, sp.z0tab, sp.w1, c * sp.L, y1[m1 - 1], [&](int64_t k) { return y1[m1 - 1 - k]; },
+      sp.zs + (s * sp.c1 + c) * 8);
 }
 
 // KS1: the band-pass's forward pass over ext(x) (odd extension in the input's

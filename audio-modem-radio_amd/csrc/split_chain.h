@@ -89,4 +89,59 @@ __device__ __forceinline__ auto bwd_blocks(const double* a, int64_t top) {
   };
 }
 
+// A chunk's start state by convolution (psk_split_kernels.hip KS0,
+// fsk_kernels.hip FS0): NS states, K [w][NS] and Z0 [w + 1][NS]
+// (iir_design.h split_state_tables), one wave per chunk; lane 0 writes zo.
+template <int NS, typename Val>
+__device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab, const double* __restrict__ z0tab,
+                                                 int64_t w, int64_t o0, double v0, Val val, double* __restrict__ zo) {
+  static_assert(NS % 2 == 0, "pairs of states per 16-byte load");
+  const int lane = (int)(threadIdx.x & 63);
+  double acc[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) acc[i] = 0.0;
+  const int64_t M = o0 < w ? o0 : w;
+  // four terms' loads in flight per lane, then their FMAs in ascending m
+  typedef double V2 __attribute__((ext_vector_type(2)));
+  constexpr int U = 4;
+  for (int64_t m0 = lane; m0 < M; m0 += 64 * U) {
+    double v[U];
+    V2 k[U][NS / 2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + 64 * u < M ? m0 + 64 * u : M - 1;   // clamped: loaded, not used
+      v[u] = val(o0 - 1 - m);
+      const V2* kp = reinterpret_cast<const V2*>(ktab + m * NS);
+#pragma unroll
+      for (int h = 0; h < NS / 2; ++h) k[u][h] = kp[h];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (m0 + 64 * u < M) {
+#pragma unroll
+        for (int h = 0; h < NS / 2; ++h) {
+          acc[2 * h] = __builtin_fma(k[u][h][0], v[u], acc[2 * h]);
+          acc[2 * h + 1] = __builtin_fma(k[u][h][1], v[u], acc[2 * h + 1]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1)
+#pragma unroll
+    for (int i = 0; i < NS; ++i) acc[i] = acc[i] + __shfl_xor(acc[i], d, 64);
+  if (lane == 0) {
+    if (o0 == 0) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) zo[i] = z0tab[i] * v0;
+    } else if (o0 <= w) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) zo[i] = __builtin_fma(z0tab[o0 * NS + i], v0, acc[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) zo[i] = acc[i];
+    }
+  }
+}
+
 }  // namespace amr

@@ -64,8 +64,8 @@ extern "C" {
                                   (amr_psk_f32_margin, amr_psk_plan_last_f32f), amr_fsk_plan_resident_bytes,
                                   the FSK time-split F1 (AMR_FSK_LAYOUT_*, amr_fsk_plan_set_layout,
                                   amr_fsk_plan_split_info, amr_fsk_split_design, amr_fsk_split_bandpass_host)
-                               4: the time-split band-pass's chunk start states by convolution
-                                  (amr_split_state_tables, amr_psk_plan_split_conv) */
+                               4: the time-split passes' chunk start states by convolution
+                                  (amr_split_state_tables, amr_psk_plan_split_conv, amr_fsk_plan_split_conv) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -327,6 +327,10 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
 #define AMR_FSK_LAYOUT_AUTO 0
 #define AMR_FSK_LAYOUT_SERIAL 1
 #define AMR_FSK_LAYOUT_SPLIT 2
+/* 1 when the plan's time-split F1 starts its chunks from convolution states
+ * (FS0, amr_split_state_tables per tone) rather than warm-ups
+ * (AMR_FSK_SPLIT_CONV=0), 0 when not (or no split design), -1 for NULL. */
+int amr_fsk_plan_split_conv(const amr_fsk_plan *plan);
 int amr_fsk_plan_set_layout(amr_fsk_plan *plan, int layout);
 /* the last call's F1 (*last_split 1: split) and the plan's split design:
  * warm-up samples, chunk length of the last split call, kappa, and tau (F2's

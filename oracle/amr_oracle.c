@@ -382,8 +382,10 @@ static void chunked_pass(const double *b, const double *a, int nt, const double 
  * at the pass's start, warm-up steps in FMA form).  out: n doubles.
  * Returns -1 if n <= pad. */
 int oracle_split_filtfilt(const double *b, const double *a, int nt, const double *zi, const void *x, int dtype,
-                          int64_t n, int64_t L, int64_t w, double *out)
+                          int64_t n, int64_t L, int64_t w, const double *K, const double *Z0, double *out)
 {
+    /* K, Z0 (both or neither): chunks start from conv_state (FS0, the GPU's
+     * default), else from w-step FMA-form warm-ups */
     const int pad = 3 * nt;
     if (n <= pad || L < 1) return -1;
     const int64_t m = n + 2 * (int64_t)pad;
@@ -391,9 +393,15 @@ int oracle_split_filtfilt(const double *b, const double *a, int nt, const double
     double *y = (double *)malloc(sizeof(double) * (size_t)m);
     double *r = (double *)malloc(sizeof(double) * (size_t)m);
     for (int64_t j = 0; j < m; ++j) e[j] = ext_sample(x, dtype, n, pad, j);
-    chunked_pass_w(b, a, nt, zi, e, y, m, L, w, 1);
-    for (int64_t k = 0; k < m; ++k) r[k] = y[m - 1 - k];
-    chunked_pass_w(b, a, nt, zi, r, y, m, L, w, 1);
+    if (K && Z0 && nt <= 17) {
+        chunked_pass_conv(b, a, nt, e, y, m, L, w, K, Z0);
+        for (int64_t k = 0; k < m; ++k) r[k] = y[m - 1 - k];
+        chunked_pass_conv(b, a, nt, r, y, m, L, w, K, Z0);
+    } else {
+        chunked_pass_w(b, a, nt, zi, e, y, m, L, w, 1);
+        for (int64_t k = 0; k < m; ++k) r[k] = y[m - 1 - k];
+        chunked_pass_w(b, a, nt, zi, r, y, m, L, w, 1);
+    }
     for (int64_t i = 0; i < n; ++i) out[i] = y[m - 1 - pad - i];
     free(e); free(y); free(r);
     return 0;

@@ -513,7 +513,7 @@ def test_fsk_live_async_host_entry():
 @pytest.mark.parametrize("env", [{"AMR_FFT_MID_TWG": "0"}, {"AMR_FFT_PRUNE": "0"}, {"AMR_FSK_W1S": "0"},
                                  {"AMR_FSK_BP1": "1"}, {"AMR_FFT_MID_NT": "256"}, {"AMR_FSK_DECIDE_BITS": "0"},
                                  {"AMR_FSK_SPLIT": "1"}, {"AMR_FSK_TILE": "40"}, {"AMR_FSK_TILE": "64"},
-                                 {"AMR_FSK_KEEPZ": "0"}],
+                                 {"AMR_FSK_KEEPZ": "0"}, {"AMR_FSK_SPLIT": "1", "AMR_FSK_SPLIT_CONV": "0"}],
                          ids=lambda e: ",".join(f"{k}={v}" for k, v in e.items()))
 def test_fsk_live_kernel_variants(tmp_path, env):
     """Every kernel variant of the live-column path, forced through its switch

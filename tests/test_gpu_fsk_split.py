@@ -42,6 +42,7 @@ def _cast(x, dtype):
     (960000, 9600, 12000.0, 24000.0, np.float32, 0),   # a 10-s capture
 ])
 def test_split_bandpass_is_the_restatement(n, baud, mark, space, dtype, chunk):
+    import _amr
     import _fsk
     import synth
     from oracle import oracle
@@ -51,10 +52,13 @@ def test_split_bandpass_is_the_restatement(n, baud, mark, space, dtype, chunk):
     got = pl.split_bandpass(x, chunk)
     info = pl.split_info()
     assert info["warmup"] > 0 and info["chunk"] == (chunk or info["chunk"])
-    _, ((mb, ma, _), (sb, sa, _)) = _fsk.design_fsk(n, baud, mark, space, 96000)
+    _, ((mb, ma, mzi), (sb, sa, szi)) = _fsk.design_fsk(n, baud, mark, space, 96000)
+    conv = pl.split_conv()      # FS0's convolution start states (AMR_FSK_SPLIT_CONV=0: warm-ups)
+    assert conv or os.environ.get("AMR_FSK_SPLIT_CONV") == "0"
     for i in range(B):
-        for t, (b, a) in enumerate(((mb, ma), (sb, sa))):
-            want = oracle.split_filtfilt(b, a, x[i], info["chunk"], info["warmup"])
+        for t, (b, a, zi) in enumerate(((mb, ma, mzi), (sb, sa, szi))):
+            tables = _amr.state_tables(b, a, zi, info["warmup"]) if conv else None
+            want = oracle.split_filtfilt(b, a, x[i], info["chunk"], info["warmup"], tables=tables)
             assert np.array_equal(got[i, :, t], want), (i, t, np.abs(got[i, :, t] - want).max())
 
 

@@ -142,24 +142,28 @@ def test_fsk_split_error_far_below_kappa(baud, mark, space, fs, built_lib):
     tones at mark / space / a band edge, a square wave, noise, DC and an FSK
     frame with a silence gap, three chunk lengths.  The envelope error that
     implies is kappa * ||hilbert kernel||_1 (the margin F2 adds); measured
-    here too, through the oracle's exact |hilbert|."""
+    here too, through the oracle's exact |hilbert|.  Both chunk starts: the
+    warm-ups and FS0's convolution states."""
+    import _amr
     import _fsk
     from oracle import oracle
     n = 48000
     d = _fsk.split_design(n, baud, mark, space, fs)
     assert d is not None and 0 < d["warmup"] <= n // 4 and d["kappa"] > 0
-    _, ((mb, ma, _), (sb, sa, _)) = _fsk.design_fsk(n, baud, mark, space, fs)
+    _, ((mb, ma, mzi), (sb, sa, szi)) = _fsk.design_fsk(n, baud, mark, space, fs)
     rng = np.random.default_rng(baud + int(mark))
     worst, where, worst_env = 0.0, None, 0.0
     for name, x in _fsk_inputs(baud, mark, space, fs, n, rng).items():
         peak = np.abs(x).max()
-        for b, a in ((mb, ma), (sb, sa)):
+        for b, a, zi in ((mb, ma, mzi), (sb, sa, szi)):
             ref = oracle.filtfilt(b, a, x)
+            T = _amr.state_tables(b, a, zi, d["warmup"])
             for L in (64, 97, 5000):
-                sp = oracle.split_filtfilt(b, a, x, L, d["warmup"])
-                err = np.abs(sp - ref).max() / peak
-                if err > worst:
-                    worst, where = err, (name, L)
+                for tables in (None, T):     # w-step warm-ups, FS0's convolution start states
+                    sp = oracle.split_filtfilt(b, a, x, L, d["warmup"], tables=tables)
+                    err = np.abs(sp - ref).max() / peak
+                    if err > worst:
+                        worst, where = err, (name, L, "warm" if tables is None else "conv")
                 if L == 97 and name in ("signal_gap", "noise"):
                     de = np.abs(oracle.hilbert_env(sp) - oracle.hilbert_env(ref)).max() / peak
                     worst_env = max(worst_env, de)
