@@ -351,7 +351,10 @@ def test_fsk_device_entry_lean_plan():
     assert pl.live_columns
     total = pl.scratch_bytes()
     lean = pl.resident_bytes()
-    split_reserved = min(B, 1024) * (2 * (n + 42) * 8 + 8)    # counted, allocated by the first split call
+    # counted, allocated by the first split call: the forward outputs, peaks,
+    # FS0's start states (chunks >= 128) and tables (w <= n / 4)
+    m1 = n + 42
+    split_reserved = min(B, 1024) * (2 * m1 * 8 + 8 + 96 * (m1 // 128 + 2)) + 2 * (2 * (n // 4) + 1) * 48
     dd = B * n * 6 // 10 * 16            # the dead columns' transform: nd / n1 = 6 / 10 at sps 10
     assert total - lean >= dd, (total, lean, dd)
     got, _ = fsk_device_demod(pl, x)
