@@ -58,6 +58,7 @@ EXPORTS = [
     "amr_psk_plan_split_conv",
     "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
     "amr_fsk_plan_split_conv",
+    "amr_psk_demod_host_edges", "amr_psk_demod_device_edges", "amr_fsk_demod_host_edges", "amr_fsk_demod_device_edges",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -209,6 +210,10 @@ def lib():
             "amr_psk_plan_exact_streams": (I32, [P, P]),
             "amr_psk_demod_host": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
             "amr_psk_demod_device": (I32, [P, P, I32, I64, I64, P, I64, P, P]),
+            "amr_psk_demod_host_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
+            "amr_psk_demod_device_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
+            "amr_fsk_demod_host_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
+            "amr_fsk_demod_device_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
             "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
             "amr_psk_plan_last_layout": (I32, [P]),
@@ -284,6 +289,33 @@ def check(rc: int):
 
 def ptr(a) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def is_kernel_dtype(dt) -> bool:
+    """float32 / float64: the dtypes the kernels read and extend themselves."""
+    return np.dtype(dt) in (np.dtype(np.float32), np.dtype(np.float64))
+
+
+def raw_input(x: np.ndarray, pad: int):
+    """A raw capture [B][n] of any other real dtype -- integers of every width
+    (int16 as its values, not PCM), bool, float16, longdouble -- as the
+    reference's filtfilt sees it (modem.py:77, 198, 308; scipy
+    _arraytools.odd_ext): (xk, edges).  xk: the samples as float32 (exact for
+    integers of <= 16 bits, bool, float16) or float64 (numpy's cast, which is
+    lfilter's own); edges [B][2 pad] float64: the odd extension 2*x[0] - x[k]
+    computed by numpy IN x's dtype -- integer wraparound, bool -> int64,
+    float16 rounding -- the left pad then the right (include/amr.h
+    amr_psk_demod_host_edges).  n > pad (the plan's design checked it)."""
+    x = np.ascontiguousarray(x)
+    if not x.dtype.isnative:
+        x = np.ascontiguousarray(x.astype(x.dtype.newbyteorder("=")))
+    pad = int(pad)
+    with np.errstate(all="ignore"):                      # numpy warns where scipy would, e.g. float16 overflow
+        left = 2 * x[:, :1] - x[:, pad:0:-1]             # ext index j < pad: 2 x[0] - x[pad - j]
+        right = 2 * x[:, -1:] - x[:, -2:-(pad + 2):-1]    # ext index pad + n + r: 2 x[n-1] - x[n-2-r]
+        edges = np.ascontiguousarray(np.concatenate([left, right], axis=1), np.float64)
+    narrow = x.dtype.kind == "b" or (x.dtype.kind in "iu" and x.dtype.itemsize <= 2) or x.dtype == np.float16
+    return np.ascontiguousarray(x, np.float32 if narrow else np.float64), edges
 
 
 def device_count() -> int:
@@ -434,6 +466,26 @@ class PskPlan:
             with self.lock:
                 check(lib().amr_psk_demod_host(self.handle, ptr(xb), dt[xb.dtype], nb, xb.shape[1], ptr(out), cap,
                                                ptr(ln), ptr(sy)))
+            outs += [out[i, :ln[i]].tobytes() for i in range(nb)]
+            syncs[s0:s0 + nb] = sy
+        return outs, syncs
+
+    def demod_host_raw(self, x: np.ndarray):
+        """x [B][N] of a dtype the kernels do not store (raw_input): the
+        reference's semantics for that array.  Returns (list[bytes], sync)."""
+        xk, edges = raw_input(np.atleast_2d(x), 3 * len(self.bp[0]))
+        B = xk.shape[0]
+        outs, syncs = [], np.empty(B, np.int64)
+        cap = max(self.out_cap, 1)
+        for s0 in range(0, B, self.max_streams):
+            xb, eb = xk[s0:s0 + self.max_streams], edges[s0:s0 + self.max_streams]
+            nb = xb.shape[0]
+            out = np.empty((nb, cap), np.uint8)
+            ln = np.empty(nb, np.int64)
+            sy = np.empty(nb, np.int64)
+            with self.lock:
+                check(lib().amr_psk_demod_host_edges(self.handle, ptr(xb), DTYPES[xb.dtype], nb, xb.shape[1],
+                                                     ptr(eb), ptr(out), cap, ptr(ln), ptr(sy)))
             outs += [out[i, :ln[i]].tobytes() for i in range(nb)]
             syncs[s0:s0 + nb] = sy
         return outs, syncs

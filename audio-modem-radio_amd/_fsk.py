@@ -121,6 +121,29 @@ class FskPlan:
             syncs[s0:s0 + nb] = sy
         return outs, syncs
 
+    def demod_host_raw(self, x: np.ndarray):
+        """x [B][N] of a dtype the kernels do not store (_amr.raw_input): the
+        reference's semantics for that array (both tones' filtfilt see the
+        same odd extension).  Returns (list[bytes], sync[B])."""
+        B = x.shape[0]
+        if self.handle is None:
+            return [b""] * B, np.full(B, -1, np.int64)
+        xk, edges = _amr.raw_input(x, 3 * len(self.coef[0]))
+        outs, syncs = [], np.empty(B, np.int64)
+        cap = max(self.out_cap, 1)
+        for s0 in range(0, B, self.max_streams):
+            xb, eb = xk[s0:s0 + self.max_streams], edges[s0:s0 + self.max_streams]
+            nb = xb.shape[0]
+            out = np.empty((nb, cap), np.uint8)
+            ln = np.empty(nb, np.int64)
+            sy = np.empty(nb, np.int64)
+            with self.lock:
+                check(lib().amr_fsk_demod_host_edges(self.handle, ptr(xb), _amr.DTYPES[xb.dtype], nb, xb.shape[1],
+                                                     ptr(eb), ptr(out), cap, ptr(ln), ptr(sy)))
+            outs += [out[i, :ln[i]].tobytes() for i in range(nb)]
+            syncs[s0:s0 + nb] = sy
+        return outs, syncs
+
     def envelopes(self, x: np.ndarray):
         """(mark_env, space_env) [B][N]: |hilbert(filtfilt(.))| per tone (modem.py:308-309)."""
         if self.handle is None:
@@ -206,11 +229,17 @@ def get_fsk_plan(n, baud, mark_freq, space_freq, samp_rate, batch) -> FskPlan:
                                                             device=dev), estimate if sps >= 1 else None)
 
 
-def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate) -> list:
+def fsk_demodulate_batch(x: np.ndarray, baud, mark_freq, space_freq, samp_rate, raw=False) -> list:
+    """raw: x is the caller's array as the reference gets it (any real dtype;
+    int16 as values) -- otherwise the plans' convention (int16 = PCM / 32768,
+    decode_wav_file's path)."""
     if x.ndim != 2:
         raise ValueError("batch input must be a 2-D [streams, samples] array")
     design_fsk(x.shape[1], baud, mark_freq, space_freq, samp_rate)
     _amr.require_gpu()
     if x.shape[0] == 0:
         return []
-    return get_fsk_plan(x.shape[1], baud, mark_freq, space_freq, samp_rate, x.shape[0]).demod_host(x)[0]
+    plan = get_fsk_plan(x.shape[1], baud, mark_freq, space_freq, samp_rate, x.shape[0])
+    if raw and not _amr.is_kernel_dtype(x.dtype):
+        return plan.demod_host_raw(x)[0]
+    return plan.demod_host(x)[0]

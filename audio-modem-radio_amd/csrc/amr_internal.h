@@ -76,6 +76,9 @@ struct PskBuffers {
   // then recomputes in float64 for K3x / K4a
   int f32f;
   double* fpeak;          // [B]
+  // the band-pass input's odd extension as the caller's dtype formed it
+  // (odd_ext.h): [B][2 * pad1] (the left pad, then the right), or null
+  const double* edge;
 };
 
 // PSK time-split layout (psk_split_kernels.hip): each filtfilt
@@ -173,6 +176,7 @@ struct FskParams {
   int force_exact;  // exact mode 2 (amr_fsk_plan_set_exact_mode): every stream's scale +inf, all go exact
   const int32_t* xlist;   // F1 list mode (the exact path): z row r <- x row xlist[r], r < *xcount
   const int32_t* xcount;
+  const double* edge;     // the odd extension as the caller's dtype formed it (odd_ext.h): [B][2 * pad] or null
 };
 
 // F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within

@@ -242,6 +242,8 @@ struct amr_psk_plan {
   uint8_t* d_out = nullptr;
   int64_t* d_len = nullptr;
   int64_t* d_sync = nullptr;
+  double* d_edge = nullptr;   // amr_psk_demod_host_edges' table [max_streams][2 pad1]
+  int64_t d_edge_bytes = 0;
   uint8_t* d_fec = nullptr;   // FEC host API staging
   int64_t* d_fec_len = nullptr;
   int32_t* d_crc = nullptr;
@@ -344,7 +346,9 @@ int64_t psk_max_bytes(const amr_psk_plan* pl, int64_t allocated) {
   const int64_t have3 = pl->s3_bytes ? pl->s3_bytes : kFrontSlack * 8 + lane_s3_bytes(pl);
   const int64_t grow = std::max<int64_t>(0, kFrontSlack * 8 + row_s1_bytes(pl) - have1) +
                        std::max<int64_t>(0, kFrontSlack * 8 + row_s3_bytes(pl) - have3);
-  return allocated + grow + pl->max_streams * pl->p.n * 8 + pl->max_streams * (pl->out_cap + 16);
+  // + the host entries' staging: x (8 B per sample), outputs, the edge table
+  return allocated + grow + pl->max_streams * pl->p.n * 8 + pl->max_streams * (pl->out_cap + 16) +
+         pl->max_streams * 2 * pl->p.pad1 * 8;
 }
 
 // Grow one scratch buffer to `want` bytes.  The new block is allocated before
@@ -425,6 +429,8 @@ bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, i
 double f32_design(const Iir& lp);
 int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L);
 int ensure(void** p, int64_t* have, int64_t need);
+int psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, const double* edges,
+                   uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx);
 }  // namespace
 
 extern "C" {
@@ -485,7 +491,7 @@ static void plan_free(amr_psk_plan* pl) {
   gate_free(pl->gate);
   for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
                   (void*)pl->split_peak, (void*)pl->split_tab, (void*)pl->split_zs,
-                  pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_fec,
+                  pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_edge, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
     if (p) (void)hipFree(p);
   for (auto& e : pl->ev)
@@ -892,9 +898,11 @@ int ensure_split_zs(amr_psk_plan* pl, const PskSplit& sp, int64_t B) {
 }
 
 // Launch the whole PSK pipeline on plan->stream.  Caller holds plan->mu.
+// d_edge: the band-pass's odd-extension table [B][2 pad1] of a raw-integer
+// capture (odd_ext.h), or null
 int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, uint8_t* d_out,
             int64_t out_stride, int64_t* d_len, int64_t* d_sync, uint8_t* d_fec, int64_t fec_stride,
-            int64_t* d_fec_len, int32_t* d_crc) {
+            int64_t* d_fec_len, int32_t* d_crc, const double* d_edge = nullptr) {
   if (B < 0 || B > pl->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
   if (dtype_size(dtype) == 0) return fail(AMR_E_INVALID, "unknown dtype");
   if (x_stride < pl->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
@@ -968,6 +976,7 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
   b.out_stride = out_stride;
   b.out_len = d_len;
   b.sync_idx = d_sync;
+  b.edge = d_edge;
   // AMR_SYNC_EACH_KERNEL=1: synchronise after every launch so a fault names its kernel
   static const bool sync_each = [] {
     const char* e = std::getenv("AMR_SYNC_EACH_KERNEL");
@@ -1150,8 +1159,34 @@ int amr_psk_demod_fec_device(amr_psk_plan* plan, const void* d_x, int dtype, int
                  fec_stride, d_fec_len, d_crc_ok);
 }
 
+int amr_psk_demod_device_edges(amr_psk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,
+                               const double* d_edges, uint8_t* d_out, int64_t out_stride, int64_t* d_out_len,
+                               int64_t* d_sync_idx) {
+  if (!plan || (n_streams && (!d_x || !d_edges || !d_out || !d_out_len || !d_sync_idx)))
+    return fail(AMR_E_INVALID, "amr_psk_demod_device_edges: NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  return run_psk(plan, d_x, dtype, n_streams, x_stride, d_out, out_stride, d_out_len, d_sync_idx, nullptr, 0,
+                 nullptr, nullptr, d_edges);
+}
+
 int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
                        uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+  return psk_demod_host(plan, x, dtype, B, x_stride, nullptr, out, out_stride, out_len, sync_idx);
+}
+
+int amr_psk_demod_host_edges(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                             const double* edges, uint8_t* out, int64_t out_stride, int64_t* out_len,
+                             int64_t* sync_idx) {
+  if (B && !edges) return fail(AMR_E_INVALID, "amr_psk_demod_host_edges: NULL edges");
+  return psk_demod_host(plan, x, dtype, B, x_stride, edges, out, out_stride, out_len, sync_idx);
+}
+
+}  // extern "C"
+
+namespace {
+int psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, const double* edges,
+                   uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
   if (!plan || (B && (!x || !out || !out_len || !sync_idx)))
     return fail(AMR_E_INVALID, "amr_psk_demod_host: NULL argument");
   const int64_t es = dtype_size(dtype);
@@ -1176,8 +1211,15 @@ int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, 
   }
   rc = copy_batch_h2d(plan->d_x, x, n * es, x_stride * es, B, plan->stream);
   if (rc) return rc;
+  const double* d_edge = nullptr;
+  if (edges) {
+    const int64_t eb = B * 2 * plan->p.pad1 * 8;
+    if ((rc = ensure((void**)&plan->d_edge, &plan->d_edge_bytes, plan->max_streams * 2 * plan->p.pad1 * 8))) return rc;
+    HIP_TRY(hipMemcpyAsync(plan->d_edge, edges, (size_t)eb, hipMemcpyHostToDevice, plan->stream));
+    d_edge = plan->d_edge;
+  }
   rc = run_psk(plan, plan->d_x, dtype, B, n, plan->d_out, cap, plan->d_len, plan->d_sync, nullptr, 0, nullptr,
-               nullptr);
+               nullptr, d_edge);
   if (rc) return rc;
   rc = copy_batch_d2h(out, out_stride, plan->d_out, cap, out_stride < cap ? out_stride : cap, B, plan->stream);
   if (rc) return rc;
@@ -1186,6 +1228,9 @@ int amr_psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, 
   HIP_TRY(hipStreamSynchronize(plan->stream));
   return AMR_OK;
 }
+}  // namespace
+
+extern "C" {
 
 // Queued host entry: upload, demod and download on the plan's stream, no
 // wait.  With two or more plans used in turn, batch k+1's upload (PCIe) runs

@@ -421,6 +421,7 @@ struct amr_fsk_plan {
   uint8_t* d_out = nullptr;
   int64_t* d_len = nullptr;
   int64_t* d_sync = nullptr;
+  double* d_edge = nullptr;    // amr_fsk_demod_host_edges' table [max_streams][2 pad] (with d_out)
   // timing
   bool timing = false;
   hipEvent_t ev[AMR_TF_COUNT][2]{};
@@ -438,7 +439,7 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
                   (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL,
-                  (void*)pl->split_y1, (void*)pl->split_peak, (void*)pl->split_cz})
+                  (void*)pl->split_y1, (void*)pl->split_peak, (void*)pl->split_cz, (void*)pl->d_edge})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -741,9 +742,21 @@ int run_fsk_back(amr_fsk_plan* pl, int64_t B, uint8_t* d_out, int64_t out_stride
   return AMR_OK;
 }
 
+// the call's odd-extension table (odd_ext.h) in the plan's FskParams for the
+// launches of one call (F1, its split form and the exact path's F1 re-run
+// copy pl->p); cleared when the call returns.  Caller holds mu.
+struct EdgeScope {
+  FskParams& p;
+  EdgeScope(FskParams& q, const double* e) : p(q) { p.edge = e; }
+  ~EdgeScope() { p.edge = nullptr; }
+};
+
+// d_edge: [B][2 pad] for a raw-integer capture (include/amr.h
+// amr_fsk_demod_host_edges), or null
 int run_fsk(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, uint8_t* d_out,
-            int64_t out_stride, int64_t* d_len, int64_t* d_sync) {
+            int64_t out_stride, int64_t* d_len, int64_t* d_sync, const double* d_edge = nullptr) {
   if (int rc = check_fsk_args(pl, dtype, B, x_stride, out_stride)) return rc;
+  EdgeScope edge_scope(pl->p, d_edge);
   for (bool& u : pl->ev_used) u = false;
   pl->ran_exact = false;
   pl->split_now = use_split(pl, B);
@@ -780,11 +793,13 @@ int stage_input(amr_fsk_plan* pl, const void* x, int dtype, int64_t B, int64_t x
   return copy_batch_h2d(*staged, x, n * es, x_stride * es, B, pl->stream);
 }
 
+// the host entries' output staging and the edge table (amr_fsk_demod_host_edges)
 int ensure_out_staging(amr_fsk_plan* pl) {
   if (pl->d_out) return AMR_OK;
   HIP_TRY(hipMalloc(&pl->d_out, (size_t)(pl->max_streams * pl->out_cap)));
   HIP_TRY(hipMalloc(&pl->d_len, (size_t)pl->max_streams * 8));
   HIP_TRY(hipMalloc(&pl->d_sync, (size_t)pl->max_streams * 8));
+  HIP_TRY(hipMalloc((void**)&pl->d_edge, (size_t)(pl->max_streams * 2 * (int64_t)pl->p.pad * 8)));
   return AMR_OK;
 }
 
@@ -881,7 +896,7 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.cmp = max_streams * p.bits_stride;
   g.words = max_streams * p.n_words * 4;
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
-  g.out = max_streams * (g.out_cap + 16);            // host-API output staging
+  g.out = max_streams * (g.out_cap + 16 + 2 * (int64_t)p.pad * 8);   // host-API output staging + edge table
   // (+ FS0's tables, w <= n / 4, and start states at L >= kFskSplitConvMinL)
   g.split = std::min<int64_t>(max_streams, kFskSplitMaxStreams) *
                 (2 * (n + 2 * (int64_t)p.pad) * 8 + 8 + 96 * ((n + 2 * (int64_t)p.pad) / kFskSplitConvMinL + 2)) +
@@ -1162,7 +1177,7 @@ int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   // scratch + the host-API staging (allocated on the first amr_fsk_demod_host:
   // d_x, or dd on a plan that keeps z)
   return plan->scratch_bytes + plan->staging_bytes + (plan->dd ? 0 : plan->dd_bytes) +
-         plan->max_streams * (plan->out_cap + 16) +
+         plan->max_streams * (plan->out_cap + 16 + 2 * (int64_t)plan->p.pad * 8) +
          std::max(plan->split_reserved, plan->split_alloc);   // == fsk_geometry().total() (split calls <= 1024 streams)
 }
 int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
@@ -1170,7 +1185,8 @@ int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
   // what is allocated now: a plan that only ever ran the device entry holds
   // no staging (no d_x, no dd, no output staging)
   return plan->scratch_bytes + (plan->d_x ? plan->staging_bytes : 0) +
-         (plan->d_out ? plan->max_streams * (plan->out_cap + 16) : 0) + plan->split_alloc;
+         (plan->d_out ? plan->max_streams * (plan->out_cap + 16 + 2 * (int64_t)plan->p.pad * 8) : 0) +
+         plan->split_alloc;
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
@@ -1296,8 +1312,21 @@ int amr_fsk_demod_device(amr_fsk_plan* plan, const void* d_x, int dtype, int64_t
   return run_fsk(plan, d_x, dtype, n_streams, x_stride, d_out, out_stride, d_out_len, d_sync_idx);
 }
 
-int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, uint8_t* out,
-                       int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+int amr_fsk_demod_device_edges(amr_fsk_plan* plan, const void* d_x, int dtype, int64_t n_streams, int64_t x_stride,
+                               const double* d_edges, uint8_t* d_out, int64_t out_stride, int64_t* d_out_len,
+                               int64_t* d_sync_idx) {
+  if (!plan || (n_streams && (!d_x || !d_edges || !d_out || !d_out_len || !d_sync_idx)))
+    return fail(AMR_E_INVALID, "amr_fsk_demod_device_edges: NULL argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  return run_fsk(plan, d_x, dtype, n_streams, x_stride, d_out, out_stride, d_out_len, d_sync_idx, d_edges);
+}
+
+}  // extern "C"
+
+namespace {
+int fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, const double* edges,
+                   uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
   if (!plan || (B && (!x || !out || !out_len || !sync_idx)))
     return fail(AMR_E_INVALID, "amr_fsk_demod_host: NULL argument");
   if (!dtype_size(dtype)) return fail(AMR_E_INVALID, "unknown dtype");
@@ -1315,8 +1344,14 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   } else {
     void* xs = nullptr;
     if (int rc = stage_input(plan, x, dtype, B, x_stride, &xs)) return rc;
+    const double* d_edge = nullptr;
+    if (edges) {
+      HIP_TRY(hipMemcpyAsync(plan->d_edge, edges, (size_t)(B * 2 * (int64_t)plan->p.pad * 8), hipMemcpyHostToDevice,
+                             plan->stream));
+      d_edge = plan->d_edge;
+    }
     plan->count_sync = true;                 // this call waits anyway: the exact path sized by its own count
-    const int rc = run_fsk(plan, xs, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync);
+    const int rc = run_fsk(plan, xs, dtype, B, plan->p.n, plan->d_out, cap, plan->d_len, plan->d_sync, d_edge);
     plan->count_sync = false;
     if (rc) return rc;
   }
@@ -1327,6 +1362,21 @@ int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, 
   HIP_TRY(hipMemcpyAsync(sync_idx, plan->d_sync, (size_t)B * 8, hipMemcpyDeviceToHost, plan->stream));
   HIP_TRY(hipStreamSynchronize(plan->stream));
   return AMR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int amr_fsk_demod_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, uint8_t* out,
+                       int64_t out_stride, int64_t* out_len, int64_t* sync_idx) {
+  return fsk_demod_host(plan, x, dtype, B, x_stride, nullptr, out, out_stride, out_len, sync_idx);
+}
+
+int amr_fsk_demod_host_edges(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                             const double* edges, uint8_t* out, int64_t out_stride, int64_t* out_len,
+                             int64_t* sync_idx) {
+  if (B && !edges) return fail(AMR_E_INVALID, "amr_fsk_demod_host_edges: NULL edges");
+  return fsk_demod_host(plan, x, dtype, B, x_stride, edges, out, out_stride, out_len, sync_idx);
 }
 
 // Queued host entry (as amr_psk_demod_host_async): upload, demod, download on

@@ -34,52 +34,6 @@
 
 namespace amr {
 
-template <typename T> struct XIn;
-template <> struct XIn<float> {
-  static __device__ double cvt(const float* x, int64_t i) { return (double)x[i]; }
-  static __device__ double ext(const float* x, int64_t e, int64_t k) { return (double)(2.0f * x[e] - x[k]); }
-};
-template <> struct XIn<double> {
-  static __device__ double cvt(const double* x, int64_t i) { return x[i]; }
-  static __device__ double ext(const double* x, int64_t e, int64_t k) { return 2.0 * x[e] - x[k]; }
-};
-template <> struct XIn<int16_t> {
-  static __device__ double cvt(const int16_t* x, int64_t i) { return (double)x[i] / 32768.0; }
-  static __device__ double ext(const int16_t* x, int64_t e, int64_t k) { return 2.0 * cvt(x, e) - cvt(x, k); }
-};
-
-// ---- the serial filtfilt, scipy's order (one lane per tone) ----------------
-// y (m samples, step +-1, in global scratch) is filtered in place.  Blocks of
-// kDfBlock samples: the next block's loads are issued before this block's
-// recursion, so the serial chain waits on FP64 latency, not on memory.
-constexpr int kDfBlock = 16;
-__device__ __forceinline__ double df2t_step(const double* b, const double* a, double* z, double xn) {
-  const double yn = z[0] + b[0] * xn;
-  for (int i = 0; i < 5; ++i) z[i] = z[i + 1] + xn * b[i + 1] - yn * a[i + 1];
-  z[5] = xn * b[6] - yn * a[6];
-  return yn;
-}
-__device__ void df2t_exact(const double* b, const double* a, double* z, double* y, int64_t m, int64_t step) {
-  const int64_t nblk = m / kDfBlock;
-  double cur[kDfBlock], nxt[kDfBlock];
-  if (nblk > 0)
-#pragma unroll
-    for (int j = 0; j < kDfBlock; ++j) cur[j] = y[j * step];
-  for (int64_t blk = 0; blk < nblk; ++blk) {
-    const int64_t k0 = blk * kDfBlock;
-    if (blk + 1 < nblk)
-#pragma unroll
-      for (int j = 0; j < kDfBlock; ++j) nxt[j] = y[(k0 + kDfBlock + j) * step];
-#pragma unroll
-    for (int j = 0; j < kDfBlock; ++j) cur[j] = df2t_step(b, a, z, cur[j]);
-#pragma unroll
-    for (int j = 0; j < kDfBlock; ++j) y[(k0 + j) * step] = cur[j];
-#pragma unroll
-    for (int j = 0; j < kDfBlock; ++j) cur[j] = nxt[j];
-  }
-  for (int64_t k = nblk * kDfBlock; k < m; ++k) y[k * step] = df2t_step(b, a, z, y[k * step]);
-}
-
 constexpr int kListThreads = 1024;
 
 // E0: the flagged streams in stream order (ordinal q -> stream), and their count

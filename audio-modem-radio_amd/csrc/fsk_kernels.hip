@@ -29,23 +29,12 @@
 #include <cstdlib>
 
 #include "amr_internal.h"
+#include "odd_ext.h"
 #include "split_chain.h"
 
 namespace amr {
 
-template <typename T> struct FIn;
-template <> struct FIn<float> {
-  static __device__ __forceinline__ double cvt(float v) { return (double)v; }
-  static __device__ __forceinline__ double ext(float e, float v) { return (double)(2.0f * e - v); }
-};
-template <> struct FIn<double> {
-  static __device__ __forceinline__ double cvt(double v) { return v; }
-  static __device__ __forceinline__ double ext(double e, double v) { return 2.0 * e - v; }
-};
-template <> struct FIn<int16_t> {
-  static __device__ __forceinline__ double cvt(int16_t v) { return (double)v / 32768.0; }
-  static __device__ __forceinline__ double ext(int16_t e, int16_t v) { return 2.0 * cvt(e) - cvt(v); }
-};
+// the input's conversion and odd extension: In<T> / OddExt<T> (odd_ext.h)
 
 // lfilter step (DF-II-T), 7 taps, per-lane coefficients, in scipy's own
 // operation order (scipy.signal.lfilter's real DF-II-T loop, no contraction):
@@ -226,16 +215,16 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
       T xs[PER];
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
-      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step<ZO>(zs, b, a, FIn<T>::cvt(xs[u])));
+      for (int u = 0; u < PER; ++u) emit(k + u, fsk_step<ZO>(zs, b, a, In<T>::cvt(xs[u])));
     }
   };
 
   // ---- forward pass: checkpoints only ------------------------------------
-  const T x0 = x[0], xl = x[n - 1];
-  const double e0 = FIn<T>::ext(x0, x[pad]);
+  const OddExt<T> ox(x, p.edge, s < last ? s : last, n, pad);
+  const double e0 = ox.left(0);
 #pragma unroll
   for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
-  for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
+  for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, ox.left(j));   // trimmed later
   if (n_tiles > 0) {
     fetch(0);
     deposit(0);
@@ -254,15 +243,16 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   }
   for (int64_t i = n_main; i < n; ++i) {
     if constexpr (AMB) PeakT<T>::one(x[i], pk_hi, pk_lo);
-    tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, FIn<T>::cvt(x[i]));
+    tl[(size_t)(i - n_main) * 64] = fsk_step<ZO>(zs, b, a, In<T>::cvt(x[i]));
   }
   if constexpr (AMB) {
-    if (tone == 0 && s < n_streams) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+    if (tone == 0 && s < n_streams)
+      p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)));
     if (lane == 0) p.xflags[w] = 0u;
   }
   double ylast = 0.0;
   for (int j = 0; j < pad; ++j) {
-    ylast = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
+    ylast = fsk_step<ZO>(zs, b, a, ox.right(j));
     tl[(size_t)(n - n_main + j) * 64] = ylast;
   }
   __threadfence();
@@ -375,10 +365,11 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
   }
   const int64_t last = ns - 1;
   const T* __restrict__ xall = reinterpret_cast<const T*>(xv);
-  auto xrow = [&](int64_t r) -> const T* {
+  auto xrow_index = [&](int64_t r) -> int64_t {   // the x row (and edge row) of z row r
     const int64_t rr = r < last ? r : last;
-    return xall + (p.xlist ? (int64_t)p.xlist[rr] : rr) * x_stride;
+    return p.xlist ? (int64_t)p.xlist[rr] : rr;
   };
+  auto xrow = [&](int64_t r) -> const T* { return xall + xrow_index(r) * x_stride; };
   const T* __restrict__ x = xrow(s);
   const int64_t n = p.n;
   const int pad = p.pad;
@@ -425,18 +416,18 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
       __builtin_memcpy(xs, &v, 16);
 #pragma unroll
       for (int u = 0; u < PER; ++u) {
-        const double xv = FIn<T>::cvt(xs[u]);
+        const double xv = In<T>::cvt(xs[u]);
         emit(k + u, fsk_step<ZO>(zs, b, a, xv));
       }
     }
   };
   if (role == 0) {
     // ---- phase 1: forward pass, checkpoints only
-    const T x0 = x[0], xl = x[n - 1];
-    const double e0 = FIn<T>::ext(x0, x[pad]);
+    const OddExt<T> ox(x, p.edge, xrow_index(s), n, pad);
+    const double e0 = ox.left(0);
 #pragma unroll
     for (int i = 0; i < 6; ++i) zs[i] = f.zi[tone][i] * e0;
-    for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, FIn<T>::ext(x0, x[pad - j]));   // trimmed later
+    for (int j = 0; j < pad; ++j) (void)fsk_step<ZO>(zs, b, a, ox.left(j));   // trimmed later
     if (n_tiles > 0) {
       fetch(r0, 0);
       fetch(r1, 1);
@@ -460,17 +451,18 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     for (int64_t i = n_main; i < n; ++i) {
       const T xi = x[i];
       if constexpr (AMB) PeakT<T>::one(xi, pk_hi, pk_lo);
-      const double xv = FIn<T>::cvt(xi);
+      const double xv = In<T>::cvt(xi);
       (&yb[0][0])[(size_t)(i - n_main) * YP + lane] = fsk_step<ZO>(zs, b, a, xv);
     }
     if constexpr (AMB) {
       // this batch's margin scale, and the group's flag word cleared for F2
-      if (tone == 0 && s < ns) p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(PeakT<T>::peak(pk_hi, pk_lo));
+      if (tone == 0 && s < ns)
+        p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)));
       if (lane == 0) p.xflags[w] = 0u;
     }
     double yl = 0.0;
     for (int j = 0; j < pad; ++j) {
-      yl = fsk_step<ZO>(zs, b, a, FIn<T>::ext(xl, x[n - 2 - j]));
+      yl = fsk_step<ZO>(zs, b, a, ox.right(j));
       (&yb[0][0])[(size_t)(n - n_main + j) * YP + lane] = yl;
     }
     ylast_sh[lane] = yl;
@@ -671,14 +663,13 @@ __global__ __launch_bounds__(256) void k_fsk_split_state_fwd(const void* xv, int
   const T* __restrict__ x = reinterpret_cast<const T*>(xv) + s * x_stride;
   const int64_t n = p.n;
   const int pad = p.pad;
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, p.edge, s, n, pad);
   split_conv_state<6>(
-      sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L,
-      FIn<T>::ext(x0, x[pad]),
+      sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L, ox.left(0),
       [&](int64_t j) -> double {
-        if (j < pad) return FIn<T>::ext(x0, x[pad - j]);
-        if (j < pad + n) return FIn<T>::cvt(x[j - pad]);
-        return FIn<T>::ext(xl, x[n - 2 - (j - pad - n)]);
+        if (j < pad) return ox.left(j);
+        if (j < pad + n) return In<T>::cvt(x[j - pad]);
+        return ox.right(j - pad - n);
       },
       sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6);
 }
@@ -714,7 +705,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
   double b[7], a[7], z[6];
 #pragma unroll
   for (int i = 0; i < 7; ++i) { b[i] = f.b[tone][i]; a[i] = f.a[tone][i]; }
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, p.edge, s, n, pad);
   int64_t j = o0 - sp.w;
   if (sp.conv) {   // FS0's start state
     j = o0;
@@ -723,7 +714,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
     for (int i = 0; i < 6; ++i) z[i] = zs[i];
   } else if (j <= 0) {
     j = 0;
-    const double e0 = FIn<T>::ext(x0, x[pad]);
+    const double e0 = ox.left(0);
 #pragma unroll
     for (int i = 0; i < 6; ++i) z[i] = f.zi[tone][i] * e0;
   } else {
@@ -741,12 +732,12 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
       pk = bits > pk ? bits : pk;
     }
   };
-  for (; j < o1 && j < pad; ++j) body(j, FIn<T>::ext(x0, x[pad - j]));
+  for (; j < o1 && j < pad; ++j) body(j, ox.left(j));
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
   if (j < jm) {
     split_chain_2(
-        j, o0, jm, fwd_blocks(x - pad, [](T v) { return FIn<T>::cvt(v); }),
-        [&](int64_t jj) { return FIn<T>::cvt(x[jj - pad]); },
+        j, o0, jm, fwd_blocks(x - pad, [](T v) { return In<T>::cvt(v); }),
+        [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); },
         [&](int64_t, double e) { fsk_split_warm(z, b, a, e); },
         [&](int64_t jj, double e) {
           y1[jj] = fsk_step<MODE>(z, b, a, e);
@@ -755,7 +746,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
         });
     j = jm;
   }
-  for (; j < o1; ++j) body(j, FIn<T>::ext(xl, x[n - 2 - (j - pad - n)]));
+  for (; j < o1; ++j) body(j, ox.right(j - pad - n));
   if (tone == 0) atomicMax(&sp.peak[s], pk);
 }
 

@@ -8,25 +8,11 @@
 #include <stdint.h>
 
 #include "amr_internal.h"
+#include "odd_ext.h"
 
 namespace amr {
 
-// ---------------------------------------------------------------------------
-// input conversion + odd extension in the INPUT's precision
-// (scipy _arraytools.odd_ext: 2*x[0] - x[k] on the caller's dtype)
-template <typename T> struct In;
-template <> struct In<float> {
-  static __device__ __forceinline__ double cvt(float v) { return (double)v; }
-  static __device__ __forceinline__ double ext(float e, float v) { return (double)(2.0f * e - v); }
-};
-template <> struct In<double> {
-  static __device__ __forceinline__ double cvt(double v) { return v; }
-  static __device__ __forceinline__ double ext(double e, double v) { return 2.0 * e - v; }
-};
-template <> struct In<int16_t> {   // decode_wav_file: float64 = int16 / 32768 (exact)
-  static __device__ __forceinline__ double cvt(int16_t v) { return (double)v / 32768.0; }
-  static __device__ __forceinline__ double ext(int16_t e, int16_t v) { return 2.0 * cvt(e) - cvt(v); }
-};
+// input conversion + odd extension (In<T>, OddExt<T>): odd_ext.h
 
 // class masks for __builtin_amdgcn_class (v_cmp_class_f64)
 // bit: 0 sNaN 1 qNaN 2 -inf 3 -norm 4 -denorm 5 -0 6 +0 7 +denorm 8 +norm 9 +inf

@@ -203,10 +203,10 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
   int hk = (int)0x80000000;
 
   // ---- forward pass -------------------------------------------------------
-  const T x0 = x[0], xl = x[n - 1];
-  z = zi * In<T>::ext(x0, x[pad]);
+  const OddExt<T> ox(x, buf.edge, s < last ? s : last, n, pad);
+  z = zi * ox.left(0);
   for (int jj = 0; jj < pad; ++jj) {
-    const double y = row_step(c, z, hk, In<T>::ext(x0, x[pad - jj]));
+    const double y = row_step(c, z, hk, ox.left(jj));
     s1[row_pair_index(w, m1_pairs, jj + qs, r)] = y;
   }
   const int64_t n_tiles = n / TS;
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void k_bandpass_row(PskBuffers buf, PskParams 
   }
   double ylast = 0.0;
   for (int jj = 0; jj < pad; ++jj) {
-    ylast = row_step(c, z, hk, In<T>::ext(xl, x[n - 2 - jj]));
+    ylast = row_step(c, z, hk, ox.right(jj));
     s1[row_pair_index(w, m1_pairs, pad + n + jj + qs, r)] = ylast;
   }
   __threadfence();
@@ -467,10 +467,10 @@ __global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p
   };
 
   // ---- forward pass -------------------------------------------------------
-  const T x0 = x[0], xl = x[n - 1];
-  z = zi * In<T>::ext(x0, x[pad]);
+  const OddExt<T> ox(x, buf.edge, s < last ? s : last, n, pad);
+  z = zi * ox.left(0);
   for (int jj = 0; jj < pad; ++jj) {
-    const double y = g8_step(c, z, top, In<T>::ext(x0, x[pad - jj]));
+    const double y = g8_step(c, z, top, ox.left(jj));
     s1[g8_pair_index(w, m1_pairs, jj + qs, g)] = y;
   }
   const int64_t n_tiles = n / TS;
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256) void k_bandpass_g8(PskBuffers buf, PskParams p
   }
   double ylast = 0.0;
   for (int jj = 0; jj < pad; ++jj) {
-    ylast = g8_step(c, z, top, In<T>::ext(xl, x[n - 2 - jj]));
+    ylast = g8_step(c, z, top, ox.right(jj));
     s1[g8_pair_index(w, m1_pairs, pad + n + jj + qs, g)] = ylast;
   }
   __threadfence();

@@ -115,13 +115,13 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
 
   // ---- forward pass: pads + tiles (checkpoints only) + tail (edge) --------
   double z[8];
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, buf.edge, s < last ? s : last, n, pad);
   {
-    const double e0 = In<T>::ext(x0, x[pad]);
+    const double e0 = ox.left(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
   }
-  for (int jj = 0; jj < pad; ++jj) (void)df2t_step<8>(z, f, In<T>::ext(x0, x[pad - jj]));
+  for (int jj = 0; jj < pad; ++jj) (void)df2t_step<8>(z, f, ox.left(jj));
   v4u xr[NL];
   if (nt > 0) load_tile(0, xr);
   for (int64_t t = 0; t < nt; ++t) {
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64 * WPB) void k_bp_lane(PskBuffers buf, PskParams 
   for (int64_t i = i_tail; i < n; ++i) eb[(ne++) * 64] = df2t_step<8>(z, f, In<T>::cvt(x[i]));
   double ylast = 0.0;
   for (int jj = 0; jj < pad; ++jj) {
-    ylast = df2t_step<8>(z, f, In<T>::ext(xl, x[n - 2 - jj]));
+    ylast = df2t_step<8>(z, f, ox.right(jj));
     eb[(ne++) * 64] = ylast;
   }
   __threadfence();                              // checkpoints / edge re-read below
@@ -217,13 +217,13 @@ __device__ __forceinline__ void bp_forward_pass(const PskBuffers& buf, const Psk
   };
   double z[8];
   float acc = __builtin_inff();
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, buf.edge, s < last ? s : last, n, pad);
   {
-    const double e0 = In<T>::ext(x0, x[pad]);
+    const double e0 = ox.left(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
   }
-  for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, In<T>::ext(x0, x[pad - jj]), acc);
+  for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, ox.left(jj), acc);
   v4u xr[NL];
   if (nt > 0) load_tile(0, xr);
   for (int64_t t = 0; t < nt; ++t) {
@@ -238,7 +238,7 @@ __device__ __forceinline__ void bp_forward_pass(const PskBuffers& buf, const Psk
   }
   int e = 0;
   for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::cvt(x[i]), acc);
-  for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::ext(xl, x[n - 2 - jj]), acc);
+  for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, ox.right(jj), acc);
   if (bp_bad<ZO>(acc, z) && s <= last) atomicOr(&buf.bp_flags[s], 1);
 }
 
@@ -329,13 +329,13 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
     // function the compiler kept 238 VGPRs live here against 113)
     double z[8];
     float acc = __builtin_inff();
-    const T x0 = x[0], xl = x[n - 1];
+    const OddExt<T> ox(x, buf.edge, s < last ? s : last, n, pad);
     {
-      const double e0 = In<T>::ext(x0, x[pad]);
+      const double e0 = ox.left(0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) z[j] = f.zi[j] * e0;
     }
-    for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, In<T>::ext(x0, x[pad - jj]), acc);
+    for (int jj = 0; jj < pad; ++jj) (void)bp_step<ZO>(z, f, ox.left(jj), acc);
     v4u xr[NL];
     if (nt > 0) load_tile(0, xr);
     for (int64_t t = 0; t < nt; ++t) {
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(128 * GPB) void k_bp_lane2(PskBuffers buf, PskParam
     }
     int e = 0;
     for (int64_t i = i_tail; i < n; ++i) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::cvt(x[i]), acc);
-    for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, In<T>::ext(xl, x[n - 2 - jj]), acc);
+    for (int jj = 0; jj < pad; ++jj) eb[(e++) * 64] = bp_step<ZO>(z, f, ox.right(jj), acc);
     if (bp_bad<ZO>(acc, z) && s <= last) atomicOr(&buf.bp_flags[s], 1);
     __threadfence();                            // checkpoints + edge: read by this wave and the backward wave
   }

@@ -34,7 +34,9 @@
 //                        wave per chunk computes its band-pass start state by
 //                        convolution -> zs [B][c1][8], KS1 / KS2 then run only
 //                        their L outputs (no w1-step warm-up)
-//   KS1 k_split_bp_fwd   ext(x) -> y1 [B][m1]   (+ the stream's input peak)
+//   KS1 k_split_bp_fwd   ext(x) -> y1 [B][m1]   (+ the stream's peak |ext x|, the
+//                        extension -- from the host's edge table for a raw
+//                        integer capture (odd_ext.h) -- included)
 //   KS2 k_split_bp_bwd   y1 reversed -> f [B][n]
 //   KS3 k_split_lp_fwd   lane = (chunk, component): f * lo, odd ext -> y3 [B][2][m2]
 //   KS4 k_split_lp_bwd   y3 reversed -> symbol samples sym [B][S][2]
@@ -95,13 +97,13 @@ __global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskP
   const T* __restrict__ x = reinterpret_cast<const T*>(buf.x) + s * buf.x_stride;
   const int64_t n = p.n;
   const int pad = p.pad1;
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, buf.edge, s, n, pad);
   split_conv_state<8>(
-      sp.ktab, sp.z0tab, sp.w1, c * sp.L, In<T>::ext(x0, x[pad]),
+      sp.ktab, sp.z0tab, sp.w1, c * sp.L, ox.left(0),
       [&](int64_t j) -> double {
-        if (j < pad) return In<T>::ext(x0, x[pad - j]);
+        if (j < pad) return ox.left(j);
         if (j < pad + n) return In<T>::cvt(x[j - pad]);
-        return In<T>::ext(xl, x[n - 2 - (j - pad - n)]);
+        return ox.right(j - pad - n);
       },
       sp.zs + (s * sp.c1 + c) * 8);
 }
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
   const int64_t n = p.n, m1 = p.m1;
   const int pad = p.pad1;
   const int64_t o0 = c * sp.L, o1 = o0 + sp.L < m1 ? o0 + sp.L : m1;
-  const T x0 = x[0], xl = x[n - 1];
+  const OddExt<T> ox(x, buf.edge, s, n, pad);
   double z[8];
   int64_t j = o0 - sp.w1;
   if (sp.conv) {   // KS0's start state
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
     for (int i = 0; i < 8; ++i) z[i] = zs[i];
   } else if (j <= 0) {
     j = 0;
-    const double e0 = In<T>::ext(x0, x[pad]);
+    const double e0 = ox.left(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] = f.zi[i] * e0;
   } else {
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
     }
   };
   // head extension, the samples themselves, tail extension
-  for (; j < o1 && j < pad; ++j) body(j, In<T>::ext(x0, x[pad - j]));
+  for (; j < o1 && j < pad; ++j) body(j, ox.left(j));
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
   if (j < jm) {
     split_chain_2(
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
         });
     j = jm;
   }
-  for (; j < o1; ++j) body(j, In<T>::ext(xl, x[n - 2 - (j - pad - n)]));
+  for (; j < o1; ++j) body(j, ox.right(j - pad - n));
   atomicMax(&sp.peak[s], pk);
 }
 

@@ -45,11 +45,15 @@ class AdvancedModem:
 # ---------------------------------------------------------------------------
 # input normalisation
 def _as_batch(samples) -> np.ndarray:
+    """The caller's samples as an array, in THEIR dtype: the reference hands
+    them to filtfilt as they are (modem.py:77, 198, 308), which forms its odd
+    extension 2*x[0] - x[k] in that dtype -- a full-scale int16 capture's
+    extension wraps.  float32 / float64 go to the kernels as they are; other
+    real dtypes (integers of every width, bool, float16) go with the extension
+    numpy forms in their own dtype (_amr.raw_input, DESIGN.md §2 item 7);
+    anything else as float64."""
     x = np.asarray(samples)
-    if x.dtype not in (np.float32, np.float64):
-        # The reference would form its odd extension in this dtype; for every
-        # integer value range that cannot overflow there (and for bool) the
-        # float64 conversion is exact and identical.  DESIGN.md §Inputs.
+    if not _amr.is_kernel_dtype(x.dtype) and x.dtype.kind not in "biuf":
         x = x.astype(np.float64)
     return x
 
@@ -62,14 +66,15 @@ def _psk_batch(kind: str, x2d: np.ndarray, baud, carrier, samp_rate):
     if B == 0:
         return []
     plan = _amr.get_psk_plan(kind, n, baud, carrier, samp_rate, B)
-    outs, _ = plan.demod_host(x2d)
+    outs, _ = plan.demod_host(x2d) if _amr.is_kernel_dtype(x2d.dtype) else plan.demod_host_raw(x2d)
     return outs
 
 
 # 16-bit WAV samples straight from the file (decoder.decode_wav_file): the
 # plans take int16 as pcm / 32768 -- exactly the float64 libsndfile gives the
 # reference -- so a quarter of the float64 bytes cross PCIe.  Internal: the
-# public functions treat integer input as raw values, as the reference does.
+# public functions treat integer input as raw values, as the reference does
+# (its odd extension wrapping in the integer dtype included).
 def _pcm16_psk(kind: str, pcm: np.ndarray, baud, carrier=3000.0, samp_rate=96000) -> bytes:
     x = np.ascontiguousarray(pcm, np.int16)[None, :]
     plan = _amr.get_psk_plan(kind, x.shape[1], baud, carrier, samp_rate, 1)
@@ -135,7 +140,7 @@ def fsk_demodulate(samples: np.ndarray, baud=1200, mark_freq=1200.0, space_freq=
 def fsk_demodulate_batch(samples: np.ndarray, baud=1200, mark_freq=1200.0, space_freq=2200.0,
                          samp_rate=96000) -> list:
     import _fsk
-    return _fsk.fsk_demodulate_batch(_as_batch(np.asarray(samples)), baud, mark_freq, space_freq, samp_rate)
+    return _fsk.fsk_demodulate_batch(_as_batch(np.asarray(samples)), baud, mark_freq, space_freq, samp_rate, raw=True)
 
 
 # ---------------------------------------------------------------------------

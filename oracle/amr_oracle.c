@@ -51,7 +51,64 @@
 
 #define AMR_DT_F32 0
 #define AMR_DT_F64 1
-#define AMR_DT_I16 2
+#define AMR_DT_I16 2      /* int16 PCM read as int16 / 32768 (decode_wav_file's libsndfile data) */
+/* Raw samples of the caller's own dtype, as the reference's public functions
+ * take them (modem.py:77, 198, 308 hand `samples` straight to filtfilt): the
+ * values are the samples themselves, and scipy's odd extension 2*x[0] - x[k]
+ * (_arraytools.py odd_ext) is evaluated in THAT dtype's numpy arithmetic --
+ * integers wrap modulo 2^bits (2 * an int16 array stays int16 under NEP 50),
+ * bool promotes to int64, float16 rounds each operation to half. */
+#define AMR_DT_RAW_I8 3
+#define AMR_DT_RAW_U8 4
+#define AMR_DT_RAW_I16 5
+#define AMR_DT_RAW_U16 6
+#define AMR_DT_RAW_I32 7
+#define AMR_DT_RAW_U32 8
+#define AMR_DT_RAW_I64 9
+#define AMR_DT_RAW_U64 10
+#define AMR_DT_RAW_BOOL 11
+#define AMR_DT_F16 12
+
+static size_t dt_size(int dtype)
+{
+    switch (dtype) {
+    case AMR_DT_F32: case AMR_DT_RAW_I32: case AMR_DT_RAW_U32: return 4;
+    case AMR_DT_I16: case AMR_DT_RAW_I16: case AMR_DT_RAW_U16: case AMR_DT_F16: return 2;
+    case AMR_DT_RAW_I8: case AMR_DT_RAW_U8: case AMR_DT_RAW_BOOL: return 1;
+    default: return 8;
+    }
+}
+
+/* IEEE binary16 <-> binary32, round to nearest even (numpy's npy_half_to_float /
+ * npy_float_to_half; numpy's float16 ufuncs compute in float32 and round the
+ * result to half, which equals a correctly rounded half operation: 24 >= 2*11+2) */
+static float f16_to_f32(uint16_t h)
+{
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    uint32_t b;
+    float f;
+    if (e == 0) { f = ldexpf((float)m, -24); return s ? -f : f; }
+    b = e == 31 ? (s | 0x7f800000u | (m << 13)) : (s | ((e + 112u) << 23) | (m << 13));
+    memcpy(&f, &b, 4);
+    return f;
+}
+static uint16_t f32_to_f16(float f)
+{
+    uint32_t b;
+    memcpy(&b, &f, 4);
+    const uint16_t s = (uint16_t)((b >> 16) & 0x8000u);
+    const uint32_t a = b & 0x7fffffffu;
+    if (a > 0x7f800000u) return (uint16_t)(s | 0x7e00u | ((a >> 13) & 0x3ffu));   /* NaN */
+    if (a >= 0x477ff000u) return (uint16_t)(s | 0x7c00u);         /* >= 65520 (a tie to even: inf) or inf */
+    if (a < 0x38800000u) {                                         /* below 2^-14: a subnormal half */
+        float v;
+        memcpy(&v, &a, 4);
+        return (uint16_t)(s | (uint16_t)rintf(v * 16777216.0f)); /* units of 2^-24, exact scaling, RNE */
+    }
+    uint32_t r = a - 0x38000000u, h = r >> 13, rem = r & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+    return (uint16_t)(s | h);
+}
 
 /* ---- lfilter (DF-II-T) ----------------------------------------------------
  * scipy/signal lfilter inner loop, real double case.  x and y may alias.   */
@@ -68,26 +125,75 @@ static void df2t(const double *b, const double *a, int nt, double *z,
     }
 }
 
+/* sample i as lfilter sees it: numpy's cast of the array to float64 */
 static double load_x(const void *x, int dtype, int64_t i)
 {
-    if (dtype == AMR_DT_F32) return (double)((const float *)x)[i];
-    if (dtype == AMR_DT_I16) return (double)((const int16_t *)x)[i] / 32768.0;
-    return ((const double *)x)[i];
+    switch (dtype) {
+    case AMR_DT_F32: return (double)((const float *)x)[i];
+    case AMR_DT_I16: return (double)((const int16_t *)x)[i] / 32768.0;
+    case AMR_DT_RAW_I8: return (double)((const int8_t *)x)[i];
+    case AMR_DT_RAW_U8: return (double)((const uint8_t *)x)[i];
+    case AMR_DT_RAW_I16: return (double)((const int16_t *)x)[i];
+    case AMR_DT_RAW_U16: return (double)((const uint16_t *)x)[i];
+    case AMR_DT_RAW_I32: return (double)((const int32_t *)x)[i];
+    case AMR_DT_RAW_U32: return (double)((const uint32_t *)x)[i];
+    case AMR_DT_RAW_I64: return (double)((const int64_t *)x)[i];
+    case AMR_DT_RAW_U64: return (double)((const uint64_t *)x)[i];
+    case AMR_DT_RAW_BOOL: return ((const uint8_t *)x)[i] ? 1.0 : 0.0;
+    case AMR_DT_F16: return (double)f16_to_f32(((const uint16_t *)x)[i]);
+    default: return ((const double *)x)[i];
+    }
+}
+
+/* 2*x[e] - x[k] in the dtype's own arithmetic (_arraytools.py:103), then as float64 */
+static double odd_pair(const void *x, int dtype, int64_t e, int64_t k)
+{
+    switch (dtype) {
+    case AMR_DT_F32: { const float *v = (const float *)x; return (double)(2.0f * v[e] - v[k]); }
+    case AMR_DT_RAW_I8: { const uint8_t *v = (const uint8_t *)x; return (double)(int8_t)(uint8_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_U8: { const uint8_t *v = (const uint8_t *)x; return (double)(uint8_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_I16: {
+        const uint16_t *v = (const uint16_t *)x;
+        return (double)(int16_t)(uint16_t)(2u * v[e] - v[k]);
+    }
+    case AMR_DT_RAW_U16: { const uint16_t *v = (const uint16_t *)x; return (double)(uint16_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_I32: { const uint32_t *v = (const uint32_t *)x; return (double)(int32_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_U32: { const uint32_t *v = (const uint32_t *)x; return (double)(uint32_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_I64: { const uint64_t *v = (const uint64_t *)x; return (double)(int64_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_U64: { const uint64_t *v = (const uint64_t *)x; return (double)(uint64_t)(2u * v[e] - v[k]); }
+    case AMR_DT_RAW_BOOL: {   /* 2 * bool -> int64 (numpy's default integer), no wrap */
+        const uint8_t *v = (const uint8_t *)x;
+        return (double)(2 * (int64_t)(v[e] != 0) - (int64_t)(v[k] != 0));
+    }
+    case AMR_DT_F16: {
+        const uint16_t *v = (const uint16_t *)x;
+        const uint16_t t = f32_to_f16(2.0f * f16_to_f32(v[e]));
+        return (double)f16_to_f32(f32_to_f16(f16_to_f32(t) - f16_to_f32(v[k])));
+    }
+    default:   /* f64 and the i16 PCM (decode_wav_file hands the demod float64 = i16/32768) */
+        return 2.0 * load_x(x, dtype, e) - load_x(x, dtype, k);
+    }
 }
 
 /* odd extension sample j of the padded sequence (0 <= j < n + 2*pad),
- * evaluated in the input's own precision as numpy does (_arraytools.py:103). */
+ * evaluated in the input's own dtype as numpy does (_arraytools.py:103). */
 static double ext_sample(const void *x, int dtype, int64_t n, int pad, int64_t j)
 {
     if (j >= pad && j < pad + n) return load_x(x, dtype, j - pad);
-    if (dtype == AMR_DT_F32) {
-        const float *xf = (const float *)x;
-        if (j < pad) return (double)(2.0f * xf[0] - xf[pad - j]);
-        return (double)(2.0f * xf[n - 1] - xf[n - 2 - (j - pad - n)]);
-    }
-    /* f64 and i16 (decode_wav_file hands the demod float64 = i16/32768) */
-    if (j < pad) return 2.0 * load_x(x, dtype, 0) - load_x(x, dtype, pad - j);
-    return 2.0 * load_x(x, dtype, n - 1) - load_x(x, dtype, n - 2 - (j - pad - n));
+    if (j < pad) return odd_pair(x, dtype, 0, pad - j);
+    return odd_pair(x, dtype, n - 1, n - 2 - (j - pad - n));
+}
+
+/* The 2*pad extension samples of one stream in libamr.so's edge-table order
+ * (include/amr.h amr_psk_demod_host_edges): out[j] = ext index j (the left
+ * pad), out[pad + r] = ext index pad + n + r (the right).  The product builds
+ * this table with numpy itself; tests check it against this C restatement. */
+int oracle_odd_edges(const void *x, int dtype, int64_t n, int pad, double *out)
+{
+    if (pad < 1 || n <= pad) return -1;
+    for (int j = 0; j < pad; ++j) out[j] = ext_sample(x, dtype, n, pad, j);
+    for (int r = 0; r < pad; ++r) out[pad + r] = ext_sample(x, dtype, n, pad, pad + n + r);
+    return 0;
 }
 
 /* scipy.signal.filtfilt(b, a, x) with default odd padding, padlen = 3*nt.
@@ -513,7 +619,7 @@ int64_t oracle_psk_demod_batch(int kind, const void *x, int dtype, int64_t n_str
                                const double *lo, uint8_t *out, int64_t out_stride,
                                int64_t *out_len, int64_t *sync_idx, int n_threads)
 {
-    const size_t esz = dtype == AMR_DT_F32 ? 4 : dtype == AMR_DT_I16 ? 2 : 8;
+    const size_t esz = dt_size(dtype);
     int64_t worst = 0;
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads) reduction(min:worst)

@@ -40,6 +40,19 @@ def sweep_golden():
 
 
 @pytest.fixture(scope="session")
+def rawint_golden():
+    """The reference's outputs on raw integer / bool / float16 captures, whose
+    odd extension scipy forms in the array's dtype (tests/golden/make_rawint_golden.py)."""
+    import json
+
+    import numpy as np
+    g = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(g, "rawint_manifest.json")) as f:
+        manifest = json.load(f)
+    return manifest, np.load(os.path.join(g, "rawint.npz"))
+
+
+@pytest.fixture(scope="session")
 def wav_golden():
     """The reference's decode_wav_file on 44.1 / 48 / 22.05 kHz WAVs
     (tests/golden/make_wav_golden.py)."""

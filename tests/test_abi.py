@@ -39,7 +39,7 @@ def test_library_has_gfx950_code_object(built_lib):
 def test_library_loads_and_reports_version(built_lib):
     import _amr
     L = _amr.lib()
-    assert L.amr_abi_version() == 4
+    assert L.amr_abi_version() == 5
 
 
 def test_demod_fails_loudly_without_gpu(built_lib):

@@ -86,6 +86,10 @@ def test_psk_sweep():
         B = int(rng.integers(1, 40))
         layout = "lane" if rng.random() < 0.5 else "row"
         x = _signal(rng, kind, B, n, baud, carrier, 0.0, fs)
+        # int16 batches: the plans' PCM path (int16 / 32768), or every third
+        # configuration the reference's raw semantics (the odd extension in
+        # int16, wrapping -- the drop-in's public path, _amr.raw_input)
+        raw = x.dtype == np.int16 and c % 3 == 0
 
         def gpu_run():
             plan = _amr.PskPlan(kind, n, baud, carrier, fs, max_streams=B)
@@ -93,12 +97,13 @@ def test_psk_sweep():
                 plan.set_inflight(max(1, 16384 // B + 1))
             elif c % 2 == 0:
                 plan.set_layout("row")       # else by batch size: the time-split layout up to 64 streams
-            out = plan.demod_host(x)
+            out = plan.demod_host_raw(x) if raw else plan.demod_host(x)
             assert plan.last_layout() in (layout, "row", "split"), plan.last_layout()
             return out[0], [int(s) for s in out[1]]
 
         def cpu_run():
-            o, s = oracle.psk_demod_batch(kind, x, baud, carrier, fs, n_threads=min(16, os.cpu_count() or 1))
+            o, s = oracle.psk_demod_batch(kind, x, baud, carrier, fs, n_threads=min(16, os.cpu_count() or 1),
+                                          raw_int16=raw)
             return o, [int(v) for v in s]
         g, w = _outcome(gpu_run), _outcome(cpu_run)
         if g != w:
@@ -130,12 +135,10 @@ def test_fsk_sweep():
         B = int(rng.integers(1, FSK_BMAX))
         x = _signal(rng, "fsk", B, n, baud, mark, space, fs)
         g = _outcome(lambda: modem.fsk_demodulate_batch(x, baud=baud, mark_freq=mark, space_freq=space, samp_rate=fs))
-        # the public drop-in takes integer samples as raw values (as the
-        # reference would); the oracle's int16 path is pcm / 32768 (the WAV
-        # entry's), which underflows differently in silent stretches -- so the
-        # oracle gets the same float64 values the drop-in computes on
-        xr = x.astype(np.float64) if x.dtype.kind in "iu" else x
-        w = _outcome(lambda: [oracle.fsk_demodulate(r, baud, mark, space, fs) for r in xr])
+        # the public drop-in takes an int16 capture as the reference does: raw
+        # values, the odd extension formed (and wrapping) in int16 -- the
+        # oracle's raw int16 (amr_oracle.c AMR_DT_RAW_I16), not its PCM path
+        w = _outcome(lambda: [oracle.fsk_demodulate(r, baud, mark, space, fs, raw_int16=True) for r in x])
         if g != w:
             bad.append((c, baud, mark, space, fs, n, B, str(x.dtype), g[0], w[0], str(g[1])[:80], str(w[1])[:80]))
     assert not bad, f"{len(bad)} of {N_FSK} configurations differ: {bad[:5]}"

@@ -100,6 +100,80 @@ def test_oracle_matches_reference_sweep(sweep_golden):
     assert not bad, f"oracle differs from the reference on {bad}"
 
 
+def test_oracle_matches_reference_rawint(rawint_golden):
+    """Raw integer (int8 / uint8 / int16 / uint16 / int32 / int64), bool and
+    float16 captures: the reference hands the caller's array to filtfilt as
+    it is (modem.py:77, 198, 308), so its odd extension wraps / rounds in the
+    array's dtype -- the oracle's AMR_DT_RAW_* restate that arithmetic in C
+    (amr_oracle.c odd_pair).  Bytes equal the reference's on all 24 fixtures
+    (tests/golden/make_rawint_golden.py), 13 of them cases where the wrap
+    decides the bytes (the reference's float64 bytes differ)."""
+    manifest, inputs = rawint_golden
+    assert sum(c["differs_from_float64"] for c in manifest["cases"]) >= 10
+    bad = []
+    for c in manifest["cases"]:
+        x, p = inputs[c["id"]], c["params"]
+        if c["fn"] == "fsk":
+            got = outcome(lambda: oracle.fsk_demodulate(x, p["baud"], p["f0"], p["f1"], p["samp_rate"], raw_int16=True))
+        else:
+            f = oracle.qpsk_demodulate if c["fn"] == "qpsk" else oracle.bpsk_demodulate
+            got = outcome(lambda: f(x, p["baud"], p["f0"], p["samp_rate"], raw_int16=True))
+        if got != expected(c):
+            bad.append((c["id"], c["fn"], c["dtype"]))
+    assert not bad, f"oracle differs from the reference on {bad}"
+
+
+def test_oracle_raw_filtfilt_is_scipys():
+    """oracle.filtfilt on raw arrays of every integer width, bool and
+    float16 == scipy.signal.filtfilt on the same array, bit for bit
+    (full-scale values: the odd extension wraps / overflows)."""
+    from scipy import signal
+    rng = np.random.default_rng(5)
+    b, a = signal.butter(4, [0.05, 0.2], btype="band")
+    bad = []
+    for dt in (np.int8, np.uint8, np.int16, np.uint16, np.int32, np.uint32, np.int64, np.uint64, np.bool_, np.float16):
+        for t in range(40):
+            n = int(rng.integers(28, 300))
+            if dt == np.bool_:
+                x = rng.integers(0, 2, n).astype(bool)
+            elif dt == np.float16:
+                x = (rng.standard_normal(n) * float(rng.choice([1e-6, 1.0, 3e4, 6e4]))).astype(np.float16)
+            else:
+                info = np.iinfo(dt)
+                x = rng.integers(int(info.min), int(info.max), n, dtype=dt, endpoint=True)
+            with np.errstate(all="ignore"):
+                want = signal.filtfilt(b, a, x)
+            got = oracle.filtfilt(b, a, x, raw_int16=True)
+            if not np.array_equal(np.nan_to_num(got).view(np.uint64), np.nan_to_num(want).view(np.uint64)):
+                bad.append((np.dtype(dt).name, t))
+    assert not bad, bad
+
+
+def test_drop_in_raw_edges_are_the_oracles(rawint_golden):
+    """The product's host half of a raw capture (_amr.raw_input: numpy's own
+    odd extension in the caller's dtype, the samples' exact float copy) ==
+    the oracle's C restatement of the extension (oracle_odd_edges) and of the
+    samples' float64 cast, on every fixture and a random draw of each dtype."""
+    import _amr
+    manifest, inputs = rawint_golden
+    rng = np.random.default_rng(6)
+    arrays = [inputs[c["id"]] for c in manifest["cases"]]
+    for dt in (np.int8, np.uint8, np.int16, np.uint16, np.int32, np.uint32, np.int64, np.uint64):
+        info = np.iinfo(dt)
+        arrays.append(rng.integers(int(info.min), int(info.max), 500, dtype=dt, endpoint=True))
+    with np.errstate(over="ignore"):
+        arrays.append((rng.standard_normal(500) * 5e4).astype(np.float16))
+    arrays.append(rng.integers(0, 2, 500).astype(bool))
+    arrays.append(rng.integers(-30000, 30000, 500).astype(">i2"))      # non-native byte order
+    for pad in (21, 27):
+        for x in arrays:
+            xk, edges = _amr.raw_input(x[None, :], pad)
+            assert xk.dtype in (np.float32, np.float64) and xk.shape == (1, x.size)
+            assert np.array_equal(xk[0].astype(np.float64), x.astype(np.float64)), x.dtype
+            want = oracle.odd_edges(x, pad)
+            assert np.array_equal(np.nan_to_num(edges[0]), np.nan_to_num(want)), (x.dtype, pad)
+
+
 def _host_numpy_is_modelled():
     """The restatement models numpy's complex multiply (FMA) and complex abs
     (AVX-512 hypot form) as the fixtures' host runs them; on a host whose
