@@ -59,6 +59,8 @@ EXPORTS = [
     "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
     "amr_fsk_plan_split_conv",
     "amr_psk_demod_host_edges", "amr_psk_demod_device_edges", "amr_fsk_demod_host_edges", "amr_fsk_demod_device_edges",
+    "amr_psk_split_bounds_host", "amr_psk_plan_set_split_strict", "amr_psk_plan_split_strict",
+    "amr_psk_plan_last_strict", "amr_psk_split_strict_design",
 ]
 
 TX_BPSK, TX_QPSK, TX_FSK = 0, 1, 2
@@ -214,6 +216,11 @@ def lib():
             "amr_psk_demod_device_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
             "amr_fsk_demod_host_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
             "amr_fsk_demod_device_edges": (I32, [P, P, I32, I64, I64, P, P, I64, P, P]),
+            "amr_psk_split_bounds_host": (I32, [P, P, I32, I64, I64, P, P, P]),
+            "amr_psk_plan_set_split_strict": (I32, [P, I32]),
+            "amr_psk_plan_split_strict": (I32, [P]),
+            "amr_psk_plan_last_strict": (I32, [P]),
+            "amr_psk_split_strict_design": (I32, [P, P, P, I32, P, P, P, I32, I64, I64, I64, P, P]),
             "amr_psk_demod_fec_device": (I32, [P, P, I32, I64, I64, P, I64, P, P, P, I64, P, P]),
             "amr_psk_slice_host": (I32, [I32, P, I64, I64, P]),
             "amr_psk_plan_last_layout": (I32, [P]),
@@ -399,6 +406,33 @@ def split_state_tables(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000)
     return K, Z0
 
 
+STRICT_CONSTS = ["g1x", "gmax", "hz", "tk", "zi_sum", "zb", "kx", "ky", "u2", "gam", "c3", "w1", "w2", "n_sym", "nw",
+                 "nk", "nh", "ng", "nz", "k12_off", "w_tail", "k12_tail", "hs_tail", "tz_tail", "lp_tail", "lp_rad",
+                 "ok", "kappa"]
+
+
+def split_strict_design(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000):
+    """The strict bound's design (libamr.so host arithmetic, amr_psk_split_strict_design):
+    dict of the constants and the tables kabs, z0abs, lpc, W, K12, HS, GS, TZ; None
+    when the plan has no strict bound."""
+    sps, first, bp, lp, _ = design_psk(kind, n, baud, carrier, samp_rate)
+    c = np.zeros(32)
+    args = [ptr(bp[0]), ptr(bp[1]), ptr(bp[2]), len(bp[0]), ptr(lp[0]), ptr(lp[1]), ptr(lp[2]), len(lp[0]), n, first,
+            sps, ptr(c)]
+    if lib().amr_psk_split_strict_design(*args, None) != 0:
+        return None
+    d = dict(zip(STRICT_CONSTS, c[:len(STRICT_CONSTS)].tolist()))
+    sizes = [("kabs", int(d["w1"])), ("z0abs", int(d["w1"]) + 1), ("lpc", int(d["n_sym"])), ("W", int(d["nw"])),
+             ("K12", int(d["nk"])), ("HS", int(d["nh"])), ("GS", int(d["ng"])), ("TZ", int(d["nz"]))]
+    tabs = np.zeros(sum(k for _, k in sizes))
+    check(lib().amr_psk_split_strict_design(*args, ptr(tabs)))
+    o = 0
+    for name, k in sizes:
+        d[name] = tabs[o:o + k]
+        o += k
+    return d
+
+
 def f32_margin(kind: str, n: int, baud, carrier=3000.0, samp_rate=96000) -> float:
     """The float32 hand-off's symbol error bound per unit max |f| (libamr.so, host arithmetic)."""
     _, _, _, lp, _ = design_psk(kind, n, baud, carrier, samp_rate)
@@ -527,6 +561,31 @@ class PskPlan:
             check(lib().amr_psk_split_symbols_host(self.handle, ptr(x), DTYPES[x.dtype], B, x.shape[1], int(chunk),
                                                     ptr(sym)))
         return sym[..., 0] + 1j * sym[..., 1]
+
+    def set_split_strict(self, on):
+        """The time-split layout's strict bound for this plan: True / False, None = the
+        process default (AMR_PSK_SPLIT_STRICT=1)."""
+        check(lib().amr_psk_plan_set_split_strict(self.handle, -1 if on is None else (1 if on else 0)))
+
+    def split_strict(self) -> bool:
+        return int(lib().amr_psk_plan_split_strict(self.handle)) == 1
+
+    def last_strict(self) -> bool:
+        return int(lib().amr_psk_plan_last_strict(self.handle)) == 1
+
+    def split_bounds(self, x: np.ndarray):
+        """Diagnostic: the strict passes' symbols [B][S] complex, the bound e [B][S] on each
+        component's |split - reference|, and per stream (E1, F, X, P3) (P3 < 0: caps failed)."""
+        x = np.ascontiguousarray(np.atleast_2d(x))
+        B = x.shape[0]
+        S = max(0, (self.n - self.first + self.sps - 1) // self.sps)
+        sym = np.zeros((B, S, 2))
+        eb = np.zeros((B, S))
+        sc = np.zeros((B, 4))
+        with self.lock:
+            check(lib().amr_psk_split_bounds_host(self.handle, ptr(x), DTYPES[x.dtype], B, x.shape[1], ptr(sym),
+                                                  ptr(eb), ptr(sc)))
+        return sym[..., 0] + 1j * sym[..., 1], eb, sc
 
     def last_f32f(self) -> bool:
         """The last call handed the band-pass output to the low-pass in float32."""

@@ -81,6 +81,9 @@ struct PskBuffers {
   const double* edge;
 };
 
+// the time-split strict bound's block of outputs (split_strict.h, psk_split_kernels.hip KB)
+constexpr int kStrictBlk = 16;
+
 // PSK time-split layout (psk_split_kernels.hip): each filtfilt
 // pass cut into chunks of L outputs, one lane per chunk, each started w
 // samples early from a zero state; decisions kept where the symbols' error
@@ -103,7 +106,44 @@ struct PskSplit {
   const double* ktab;     // [w1][8] state weights of past inputs (iir_design.h split_state_tables)
   const double* z0tab;    // [w1 + 1][8] scipy's zi state after t zero inputs
   double* zs;             // [B][c1][8] start states, KS0 -> KS1 (then reused for KS2)
+  // STRICT mode (split_strict.h): the decisions' margin from a
+  // bound that holds for every input instead of kappa * peak.  KS0 adds each
+  // chunk start's error bound, KS1 / KS2 each step's rounding bound
+  //   D = u2 sum_{i>=1} |z_i| + kx |x| + ky |y|
+  // and their maxima per stream to bnd; KS5 turns them into a bound per symbol
+  int strict;
+  unsigned long long* bnd;   // [B][8] bits (cleared per launch): D1max, -, max|y1|, D2max, -, max|f|
+  const double* kabs;        // [w1] sum_i |K_i[m]|
+  const double* z0abs;       // [w1 + 1] sum_i |Z0_i[t]|
+  const double* lpc;         // [n_sym] the band-pass error's reach to symbol k (the low-pass stage)
+  double gam;                // KS0's dot-product rounding factor (gamma_n + the tables' 2u)
+  double u2, kx, ky;         // the step bound's constants
+  double g1x, gmax;          // 1 + sum_m max_j |g_j(m)|, its max
+  double hz, tk, zi_sum, zb; // ||h||_1 + max|tz|; truncation per unit peak; sum|zi|; state sum per unit peak
+  double c3;                 // the low-pass's own rounding, truncation, extension rounding per unit P3
+  // the block bound (KB; split_strict.h kStrictBlk): kernels and their cut remainders
+  const double *kW, *kK12, *kHS, *kGS, *kTZ;
+  int nw, nk, k12_off, nh, nz;
+  double w_tail, k12_tail, hs_tail, tz_tail, lp_tail;
+  int64_t lp_rad;
+  // per-stream scratch (stride sstride doubles): D1 blocks [nb1] | D2 blocks [nb1] | chunk start bounds
+  // pass 1 [c1] | pass 2 [c1] | E1 blocks [nb1] | S1 blocks [nb1] | E2 blocks [nb1] | X blocks [nbs] |
+  // e(k) [n_sym] | scalars [4]: E1max, Fmax, Xmax, P3 (negative: the caps failed, the stream is flagged)
+  double* sc;
+  int64_t sstride, nb1, nbs;
+  double* ebound;            // diagnostic (amr_psk_split_bounds_host): copy e(k) and the scalars out
 };
+
+// offsets into PskSplit::sc
+__host__ __device__ inline int64_t strict_off_d1(const PskSplit&) { return 0; }
+__host__ __device__ inline int64_t strict_off_d2(const PskSplit& s) { return s.nb1; }
+__host__ __device__ inline int64_t strict_off_ds1(const PskSplit& s) { return 2 * s.nb1; }
+__host__ __device__ inline int64_t strict_off_ds2(const PskSplit& s) { return 2 * s.nb1 + s.c1; }
+__host__ __device__ inline int64_t strict_off_e1(const PskSplit& s) { return 2 * s.nb1 + 2 * s.c1; }
+__host__ __device__ inline int64_t strict_off_s1(const PskSplit& s) { return 3 * s.nb1 + 2 * s.c1; }
+__host__ __device__ inline int64_t strict_off_e2(const PskSplit& s) { return 4 * s.nb1 + 2 * s.c1; }
+__host__ __device__ inline int64_t strict_off_x(const PskSplit& s) { return 5 * s.nb1 + 2 * s.c1; }
+__host__ __device__ inline int64_t strict_off_e(const PskSplit& s) { return 5 * s.nb1 + 2 * s.c1 + s.nbs; }
 
 // FSK live-column layout.  A four-step length n = n1 * n2
 // (sample i = j1 + n1 * j2) with n1 % sps == 0: every decision window of

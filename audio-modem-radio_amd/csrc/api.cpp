@@ -16,6 +16,7 @@
 #include "amr_internal.h"
 #include "api_common.h"
 #include "iir_design.h"
+#include "split_strict.h"
 
 namespace amr {
 hipError_t launch_psk_bandpass(const PskBuffers&, const PskParams&, const Iir&, hipStream_t);
@@ -266,7 +267,19 @@ struct amr_psk_plan {
   double* split_tab = nullptr;    // [w1][8] K, then [w1 + 1][8] Z0 (split_state_tables), with the design
   double* split_zs = nullptr;     // [B][c1][8] chunk start states (grown per launch)
   int64_t split_zs_bytes = 0;
+  // the split layout's STRICT bound (split_strict.h): -1 = the process default
+  // (AMR_PSK_SPLIT_STRICT=1), else amr_psk_plan_set_split_strict; designed on
+  // the first strict call (the device tables kabs | z0abs | lpc in strict_tab,
+  // the per-stream maxima in strict_bnd)
+  int strict_mode = -1;
+  bool strict_designed = false;
+  StrictDesign sdes;
+  double* strict_tab = nullptr;
+  unsigned long long* strict_bnd = nullptr;
+  double* strict_sc = nullptr;    // the per-stream scratch of the block bound (PskSplit::sc), grown per call
+  int64_t strict_sc_bytes = 0;
   bool last_f32f = false;       // the last lane-layout call handed f over in float32
+  bool last_strict = false;     // the last split call decided with the strict bound
 };
 
 struct amr_comm {
@@ -424,10 +437,13 @@ int plan_stream(amr_psk_plan* plan, int* dev, hipStream_t* st) {
 namespace {
 void split_design(amr_psk_plan* pl);   // below, with run_psk
 bool split_conv_on(const amr_psk_plan* pl);
+bool split_strict_on(const amr_psk_plan* pl);
+int strict_prepare(amr_psk_plan* pl);
 bool split_design_core(const Iir& bp, const Iir& lp, int64_t n, int64_t n_sym, int64_t* w1, int64_t* w2,
                        double* kappa);
 double f32_design(const Iir& lp);
-int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L);
+int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L,
+                        double* ebound = nullptr);
 int ensure(void** p, int64_t* have, int64_t need);
 int psk_demod_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride, const double* edges,
                    uint8_t* out, int64_t out_stride, int64_t* out_len, int64_t* sync_idx);
@@ -490,7 +506,8 @@ static void plan_free(amr_psk_plan* pl) {
   if (pl->stream) (void)hipStreamSynchronize(pl->stream);
   gate_free(pl->gate);
   for (auto* p : {(void*)pl->lo, (void*)pl->lo2, (void*)pl->s1_base, (void*)pl->s2, (void*)pl->s3_base, (void*)pl->words, (void*)pl->flags,
-                  (void*)pl->split_peak, (void*)pl->split_tab, (void*)pl->split_zs,
+                  (void*)pl->split_peak, (void*)pl->split_tab, (void*)pl->split_zs, (void*)pl->strict_tab,
+                  (void*)pl->strict_bnd, (void*)pl->strict_sc,
                   pl->d_x, (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->d_edge, (void*)pl->d_fec,
                   (void*)pl->d_fec_len, (void*)pl->d_crc})
     if (p) (void)hipFree(p);
@@ -721,6 +738,95 @@ int amr_psk_split_symbols_host(amr_psk_plan* plan, const void* x, int dtype, int
   return AMR_OK;
 }
 
+int amr_psk_split_bounds_host(amr_psk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                              double* sym, double* ebound, double* scalars) {
+  if (!plan || !x || !sym || !ebound || !scalars || B < 1)
+    return fail(AMR_E_INVALID, "amr_psk_split_bounds_host: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (B > plan->max_streams) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (dtype_size(dtype) == 0 || x_stride < plan->p.n) return fail(AMR_E_INVALID, "bad dtype / x_stride");
+  if (!plan->split_designed) split_design(plan);
+  if (!plan->split_ok || plan->p.n_sym < 2) return fail(AMR_E_INVALID, "no time-split layout for this plan");
+  const int64_t n = plan->p.n, es = dtype_size(dtype), S = plan->p.n_sym;
+  int64_t have = plan->d_x_bytes;
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  if (int rc = ensure(&plan->d_x, &have, B * n * es)) return rc;
+  plan->d_x_bytes = have;
+  double* stage = nullptr;
+  HIP_TRY(hipMalloc((void**)&stage, (size_t)(B * (S + 4) * 8)));
+  int rc = copy_batch_h2d(plan->d_x, x, n * es, x_stride * es, B, plan->stream);
+  if (!rc) rc = run_psk_split_front(plan, plan->d_x, dtype, B, n, 0, stage);
+  if (!rc) {
+    std::vector<double> h((size_t)(B * (S + 4)));
+    if (hipStreamSynchronize(plan->stream) != hipSuccess ||
+        hipMemcpy(sym, plan->s1, (size_t)(B * S * 2 * 8), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(h.data(), stage, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = fail(AMR_E_HIP, "amr_psk_split_bounds_host: copy failed");
+    } else {
+      for (int64_t i = 0; i < B; ++i) {
+        std::memcpy(ebound + i * S, h.data() + i * (S + 4), (size_t)S * 8);
+        std::memcpy(scalars + i * 4, h.data() + i * (S + 4) + S, 32);
+      }
+    }
+  }
+  (void)hipFree(stage);
+  return rc;
+}
+
+int amr_psk_plan_set_split_strict(amr_psk_plan* plan, int mode) {
+  if (!plan || mode < -1 || mode > 1) return fail(AMR_E_INVALID, "amr_psk_plan_set_split_strict: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  plan->strict_mode = mode;
+  return AMR_OK;
+}
+
+int amr_psk_plan_split_strict(amr_psk_plan* plan) {
+  if (!plan) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return split_strict_on(plan) ? 1 : 0;
+}
+
+int amr_psk_plan_last_strict(const amr_psk_plan* plan) { return plan ? (plan->last_strict ? 1 : 0) : -1; }
+
+int amr_psk_split_strict_design(const double* bp_b, const double* bp_a, const double* bp_zi, int bp_nt,
+                                const double* lp_b, const double* lp_a, const double* lp_zi, int lp_nt, int64_t n,
+                                int64_t first, int64_t sps, double* consts, double* tabs) {
+  if (!bp_b || !bp_a || !bp_zi || !lp_b || !lp_a || !lp_zi || !consts || bp_nt != 9 || lp_nt != 5 || n < 1 ||
+      sps < 1 || first < 0)
+    return fail(AMR_E_INVALID, "amr_psk_split_strict_design: bad argument");
+  Iir bp{}, lp{};
+  bp.nt = bp_nt;
+  lp.nt = lp_nt;
+  for (int i = 0; i < bp_nt; ++i) { bp.b[i] = bp_b[i]; bp.a[i] = bp_a[i]; }
+  for (int i = 0; i < bp_nt - 1; ++i) bp.zi[i] = bp_zi[i];
+  for (int i = 0; i < lp_nt; ++i) { lp.b[i] = lp_b[i]; lp.a[i] = lp_a[i]; }
+  for (int i = 0; i < lp_nt - 1; ++i) lp.zi[i] = lp_zi[i];
+  const int64_t n_sym = n > first ? (n - first + sps - 1) / sps : 0;
+  int64_t w1 = 0, w2 = 0;
+  double kappa = 0.0;
+  for (int i = 0; i < 32; ++i) consts[i] = 0.0;
+  if (!split_design_core(bp, lp, n, n_sym, &w1, &w2, &kappa)) return fail(AMR_E_INVALID, "no time-split layout");
+  std::vector<double> tab((size_t)(2 * w1 + 1) * 8);
+  split_state_tables(bp, w1, tab.data(), tab.data() + (size_t)w1 * 8);
+  const StrictDesign d = strict_design(bp, lp, tab.data(), tab.data() + (size_t)w1 * 8, w1, w2, n, first, sps, n_sym);
+  // the device table's layout: kabs | z0abs | lpc | W | K12 | HS | GS | TZ
+  const double v[32] = {d.g1x, d.gmax, d.hz, d.tk, d.zi_sum, d.zb, d.kx, d.ky, 2.0 * 0x1p-53 * (1.0 + 0x1p-50),
+                        d.gam, d.c3, (double)w1, (double)w2, (double)n_sym, (double)d.W.size(), (double)d.K12.size(),
+                        (double)d.HS.size(), (double)d.GS.size(), (double)d.TZ.size(), (double)d.k12_off, d.w_tail,
+                        d.k12_tail, d.hs_tail, d.tz_tail, d.lp_tail, (double)d.lp_rad, d.ok ? 1.0 : 0.0, kappa};
+  for (int i = 0; i < 32; ++i) consts[i] = v[i];
+  if (!d.ok) return fail(AMR_E_INVALID, "no strict bound for these filters");
+  if (tabs) {
+    double* o = tabs;
+    for (const std::vector<double>* t : {&d.kabs, &d.z0abs, &d.lpc, &d.W, &d.K12, &d.HS, &d.GS, &d.TZ}) {
+      std::memcpy(o, t->data(), t->size() * 8);
+      o += t->size();
+    }
+  }
+  return AMR_OK;
+}
+
 int amr_psk_plan_last_f32f(const amr_psk_plan* plan) { return plan ? (plan->last_f32f ? 1 : 0) : -1; }
 
 int amr_split_state_tables(const double* b, const double* a, const double* zi, int nt, int64_t w, double* K,
@@ -818,6 +924,12 @@ bool split_conv_on(const amr_psk_plan* pl) {
   static const bool conv_env = [] { const char* e = std::getenv("AMR_PSK_SPLIT_CONV"); return !(e && e[0] == '0'); }();
   return conv_env && pl->split_tab && pl->bp.nt == 9;
 }
+// the strict bound for this plan's split calls: amr_psk_plan_set_split_strict,
+// else AMR_PSK_SPLIT_STRICT=1 (off by default: DESIGN.md §3.3)
+bool split_strict_on(const amr_psk_plan* pl) {
+  static const bool env = [] { const char* e = std::getenv("AMR_PSK_SPLIT_STRICT"); return e && e[0] == '1'; }();
+  return pl->strict_mode >= 0 ? pl->strict_mode == 1 : env;
+}
 PskSplit split_params(amr_psk_plan* pl, int64_t B, int64_t L) {
   PskSplit sp{};
   // AMR_PSK_SPLIT_MINL: a fixed minimum chunk length instead of the rules (an A/B knob)
@@ -850,7 +962,87 @@ PskSplit split_params(amr_psk_plan* pl, int64_t B, int64_t L) {
   sp.z0tab = pl->split_tab ? pl->split_tab + (size_t)sp.w1 * 8 : nullptr;
   sp.zs = pl->split_zs;
   pl->split_L = sp.L;
+  if (pl->strict_designed && pl->sdes.ok && split_strict_on(pl) && sp.conv) {
+    const StrictDesign& d = pl->sdes;
+    // chunks on block boundaries (the per-block step bounds stay within a lane)
+    sp.L = (sp.L + kStrictBlk - 1) / kStrictBlk * kStrictBlk;
+    sp.c1 = (pl->p.m1 + sp.L - 1) / sp.L;
+    sp.c2 = (pl->p.m2 + sp.L - 1) / sp.L;
+    pl->split_L = sp.L;
+    sp.strict = 1;
+    sp.bnd = pl->strict_bnd;
+    const double* t = pl->strict_tab;
+    sp.kabs = t;
+    sp.z0abs = t + sp.w1;
+    sp.lpc = t + 2 * sp.w1 + 1;
+    const double* k = sp.lpc + pl->p.n_sym;
+    sp.kW = k;
+    sp.kK12 = sp.kW + d.W.size();
+    sp.kHS = sp.kK12 + d.K12.size();
+    sp.kGS = sp.kHS + d.HS.size();
+    sp.kTZ = sp.kGS + d.GS.size();
+    sp.nw = (int)d.W.size();
+    sp.nk = (int)d.K12.size();
+    sp.k12_off = d.k12_off;
+    sp.nh = (int)d.HS.size();
+    sp.nz = (int)d.TZ.size();
+    sp.w_tail = d.w_tail;
+    sp.k12_tail = d.k12_tail;
+    sp.hs_tail = d.hs_tail;
+    sp.tz_tail = d.tz_tail;
+    sp.lp_tail = d.lp_tail;
+    sp.lp_rad = d.lp_rad;
+    sp.gam = d.gam;
+    sp.u2 = 2.0 * 0x1p-53 * (1.0 + 0x1p-50);
+    sp.kx = d.kx;
+    sp.ky = d.ky;
+    sp.g1x = d.g1x;
+    sp.gmax = d.gmax;
+    sp.hz = d.hz;
+    sp.tk = d.tk;
+    sp.zi_sum = d.zi_sum;
+    sp.zb = d.zb;
+    sp.c3 = d.c3;
+    sp.nb1 = (pl->p.m1 + kStrictBlk - 1) / kStrictBlk;
+    sp.nbs = (pl->p.n + kStrictBlk - 1) / kStrictBlk;
+    sp.sstride = 5 * sp.nb1 + 2 * sp.c1 + sp.nbs + pl->p.n_sym + 4;
+  }
   return sp;
+}
+// the strict scratch for B streams of this call's geometry
+int ensure_strict_sc(amr_psk_plan* pl, PskSplit& sp, int64_t B) {
+  if (!sp.strict) return AMR_OK;
+  const int64_t need = B * sp.sstride * 8;
+  if (pl->strict_sc_bytes < need || !pl->strict_sc) {
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    if (pl->strict_sc) HIP_TRY(hipFree(pl->strict_sc));
+    pl->strict_sc = nullptr;
+    pl->strict_sc_bytes = 0;
+    HIP_TRY(hipMalloc((void**)&pl->strict_sc, (size_t)need));
+    pl->strict_sc_bytes = need;
+  }
+  sp.sc = pl->strict_sc;
+  return AMR_OK;
+}
+// the strict mode's design and device tables, on the first strict call
+int strict_prepare(amr_psk_plan* pl) {
+  if (pl->strict_designed) return AMR_OK;
+  pl->strict_designed = true;
+  if (!pl->split_ok || !pl->split_tab) return AMR_OK;
+  const int64_t w = pl->split_w1;
+  std::vector<double> tab((size_t)(2 * w + 1) * 8);
+  split_state_tables(pl->bp, w, tab.data(), tab.data() + (size_t)w * 8);
+  pl->sdes = strict_design(pl->bp, pl->lp, tab.data(), tab.data() + (size_t)w * 8, w, pl->split_w2, pl->p.n,
+                           pl->p.first, pl->p.sps, pl->p.n_sym);
+  if (!pl->sdes.ok) return AMR_OK;
+  std::vector<double> dev(pl->sdes.kabs);
+  for (const std::vector<double>* v : {&pl->sdes.z0abs, &pl->sdes.lpc, &pl->sdes.W, &pl->sdes.K12, &pl->sdes.HS,
+                                       &pl->sdes.GS, &pl->sdes.TZ})
+    dev.insert(dev.end(), v->begin(), v->end());
+  HIP_TRY(hipMalloc((void**)&pl->strict_tab, dev.size() * 8));
+  HIP_TRY(hipMemcpy(pl->strict_tab, dev.data(), dev.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMalloc((void**)&pl->strict_bnd, (size_t)pl->max_streams * 64));
+  return AMR_OK;
 }
 // The lane layout's float32 hand-off: the band-pass output f
 // is exact (scipy's filtfilt) and rounded to float32 for the low-pass, so
@@ -1001,10 +1193,15 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
     HIP_TRY(hipMemsetAsync(d_len, 0, (size_t)B * 8, st));
     HIP_TRY(hipMemsetAsync(d_sync, 0xFF, (size_t)B * 8, st));
   } else if (layout == AMR_LAYOUT_SPLIT) {
+    if (split_strict_on(pl))
+      if (int rc = strict_prepare(pl)) return rc;
     PskSplit sp = split_params(pl, B, 0);
     if (int rc = ensure_split_zs(pl, sp, B)) return rc;
+    if (int rc = ensure_strict_sc(pl, sp, B)) return rc;
     sp.zs = pl->split_zs;
     HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, st));   // peaks, flags, count
+    if (sp.strict) HIP_TRY(hipMemsetAsync(sp.bnd, 0, (size_t)B * 64, st));
+    pl->last_strict = sp.strict != 0;
     HIP_TRY(mark(AMR_T_BANDPASS, 0));
     HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, st));
     HIP_TRY(mark(AMR_T_BANDPASS, 1));
@@ -1104,8 +1301,11 @@ int run_psk(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_s
 }
 
 // the time-split passes alone (KS1-KS4) with chunk length L: the symbol
-// samples in s1 [B][S][2] (amr_psk_split_symbols_host).  Caller holds mu.
-int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L) {
+// samples in s1 [B][S][2] (amr_psk_split_symbols_host); with ebound (device,
+// [B][S] + [B][4]) the strict bound too, KS5 writing it there
+// (amr_psk_split_bounds_host).  Caller holds mu.
+int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t x_stride, int64_t L,
+                        double* ebound) {
   if (int rc = ensure_scratch(pl, kFrontSlack * 8 + row_s1_bytes(pl), kFrontSlack * 8 + row_s3_bytes(pl))) return rc;
   PskBuffers b{};
   b.x = d_x;
@@ -1114,12 +1314,29 @@ int run_psk_split_front(amr_psk_plan* pl, const void* d_x, int dtype, int64_t B,
   b.n_streams = B;
   b.lo = pl->lo;
   b.lo2 = pl->lo2;
+  const int saved = pl->strict_mode;
+  if (ebound) {
+    pl->strict_mode = 1;
+    if (int rc = strict_prepare(pl)) { pl->strict_mode = saved; return rc; }
+  }
   PskSplit sp = split_params(pl, B, L);
+  pl->strict_mode = saved;
+  if (ebound && !sp.strict) return fail(AMR_E_INVALID, "no strict bound for this plan (no convolution starts or design)");
   if (int rc = ensure_split_zs(pl, sp, B)) return rc;
+  if (int rc = ensure_strict_sc(pl, sp, B)) return rc;
   sp.zs = pl->split_zs;
   HIP_TRY(hipMemsetAsync(pl->split_peak, 0, (size_t)pl->max_streams * 12 + 4, pl->stream));
+  if (sp.strict) HIP_TRY(hipMemsetAsync(sp.bnd, 0, (size_t)B * 64, pl->stream));
   HIP_TRY(launch_psk_split_bp(b, pl->p, pl->bp, sp, pl->stream));
   HIP_TRY(launch_psk_split_lp(b, pl->p, pl->lp, sp, pl->stream));
+  if (ebound) {
+    b.words = pl->words;
+    HIP_TRY(launch_psk_split_slice(b, pl->p, sp, pl->stream));
+    // e(k) and the scalars of every stream, packed [B][S + 4]
+    const int64_t S = pl->p.n_sym;
+    HIP_TRY(hipMemcpy2DAsync(ebound, (size_t)(S + 4) * 8, sp.sc + strict_off_e(sp), (size_t)sp.sstride * 8,
+                             (size_t)(S + 4) * 8, (size_t)B, hipMemcpyDeviceToDevice, pl->stream));
+  }
   return AMR_OK;
 }
 

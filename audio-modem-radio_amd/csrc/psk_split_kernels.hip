@@ -73,6 +73,16 @@ __device__ __forceinline__ double split_lp_step(double (&z)[4], const Iir& f, do
   else return df2t_step<4>(z, f, x);
 }
 
+// STRICT (split_strict.h): the rounding one DF-II-T step of scipy's order
+// commits, summed over states, bounded from its pre-step states z1..z7, its
+// input and its output: u2 sum_{i>=1} |z_i| + kx |x| + ky |y|
+__device__ __forceinline__ double step_bound_pre(const double (&z)[8]) {
+  return ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) + ((fabs(z[5]) + fabs(z[6])) + fabs(z[7]));
+}
+__device__ __forceinline__ double step_bound(const PskSplit& sp, double sz, double x, double y) {
+  return __builtin_fma(sp.u2, sz, __builtin_fma(sp.kx, fabs(x), sp.ky * fabs(y)));
+}
+
 // |v| as ordered bits (NaN above inf above every finite value)
 __device__ __forceinline__ unsigned long long abs_bits(double v) {
   return (unsigned long long)__double_as_longlong(v) & 0x7fffffffffffffffULL;
@@ -89,7 +99,7 @@ __device__ __forceinline__ unsigned long long abs_bits(double v) {
 // oracle/amr_oracle.c conv_state restates it), the Z0 term while o0 <= w1.
 // Chunk 0 keeps scipy's zi * v0.  One wave per chunk, four per workgroup
 // (split_chain.h split_conv_state).
-template <typename T>
+template <typename T, bool ST>
 __global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskParams p, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -98,30 +108,33 @@ __global__ __launch_bounds__(256) void k_split_bp_state_fwd(PskBuffers buf, PskP
   const int64_t n = p.n;
   const int pad = p.pad1;
   const OddExt<T> ox(x, buf.edge, s, n, pad);
-  split_conv_state<8>(
+  split_conv_state<8, ST>(
       sp.ktab, sp.z0tab, sp.w1, c * sp.L, ox.left(0),
       [&](int64_t j) -> double {
         if (j < pad) return ox.left(j);
         if (j < pad + n) return In<T>::cvt(x[j - pad]);
         return ox.right(j - pad - n);
       },
-      sp.zs + (s * sp.c1 + c) * 8);
+      sp.zs + (s * sp.c1 + c) * 8,
+      ConvBound{sp.kabs, sp.z0abs, sp.gam, ST ? sp.sc + s * sp.sstride + strict_off_ds1(sp) + c : nullptr});
 }
 
+template <bool ST>
 __global__ __launch_bounds__(256) void k_split_bp_state_bwd(PskBuffers buf, PskParams p, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= sp.c1) return;
   const int64_t m1 = p.m1;
   const double* __restrict__ y1 = sp.y1 + s * m1;
-  split_conv_state<8>(
+  split_conv_state<8, ST>(
       sp.ktab, sp.z0tab, sp.w1, c * sp.L, y1[m1 - 1], [&](int64_t k) { return y1[m1 - 1 - k]; },
-      sp.zs + (s * sp.c1 + c) * 8);
+      sp.zs + (s * sp.c1 + c) * 8,
+      ConvBound{sp.kabs, sp.z0abs, sp.gam, ST ? sp.sc + s * sp.sstride + strict_off_ds2(sp) + c : nullptr});
 }
 
 // KS1: the band-pass's forward pass over ext(x) (odd extension in the input's
 // precision, In<T>), outputs [o0, o1) of chunk c
-template <typename T, bool ZO>
+template <typename T, bool ZO, bool ST>
 __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p, Iir f, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t c = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -149,14 +162,34 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
   }
   double* __restrict__ y1 = sp.y1 + s * m1;
   unsigned long long pk = 0;
-  auto body = [&](int64_t jj, double e) {
-    if (jj < o0) {
-      split_bp_warm<ZO>(z, f, e);
+  // ST: this chunk's largest step bound and |y1|, and the step bounds summed
+  // per block of kStrictBlk outputs (chunks start on block boundaries)
+  [[maybe_unused]] double dmax = 0.0, ymax = 0.0, dsum = 0.0;
+  [[maybe_unused]] int dcnt = 0;
+  [[maybe_unused]] double* dblk = ST ? sp.sc + s * sp.sstride + strict_off_d1(sp) : nullptr;
+  auto out = [&](int64_t jj, double e) {
+    if constexpr (ST) {
+      const double sz = step_bound_pre(z);
+      const double y = split_bp_step<ZO>(z, f, e);
+      y1[jj] = y;
+      const double dd = step_bound(sp, sz, e, y);
+      dmax = fmax(dmax, dd);
+      dsum += dd;
+      if (++dcnt == kStrictBlk) {
+        dblk[jj / kStrictBlk] = dsum;
+        dsum = 0.0;
+        dcnt = 0;
+      }
+      ymax = fmax(ymax, fabs(y));                 // (NaN / inf input: the peak test flags the stream)
     } else {
       y1[jj] = split_bp_step<ZO>(z, f, e);
-      const unsigned long long b = abs_bits(e);
-      pk = b > pk ? b : pk;
     }
+    const unsigned long long b = abs_bits(e);
+    pk = b > pk ? b : pk;
+  };
+  auto body = [&](int64_t jj, double e) {
+    if (jj < o0) split_bp_warm<ZO>(z, f, e);
+    else out(jj, e);
   };
   // head extension, the samples themselves, tail extension
   for (; j < o1 && j < pad; ++j) body(j, ox.left(j));
@@ -165,22 +198,22 @@ __global__ __launch_bounds__(64) void k_split_bp_fwd(PskBuffers buf, PskParams p
     split_chain_2(
         j, o0, jm, fwd_blocks(x - pad, [](T v) { return In<T>::cvt(v); }),
         [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); },
-        [&](int64_t, double e) { split_bp_warm<ZO>(z, f, e); },
-        [&](int64_t jj, double e) {
-          y1[jj] = split_bp_step<ZO>(z, f, e);
-          const unsigned long long b = abs_bits(e);
-          pk = b > pk ? b : pk;
-        });
+        [&](int64_t, double e) { split_bp_warm<ZO>(z, f, e); }, out);
     j = jm;
   }
   for (; j < o1; ++j) body(j, ox.right(j - pad - n));
   atomicMax(&sp.peak[s], pk);
+  if constexpr (ST) {
+    if (dcnt > 0) dblk[(o1 - 1) / kStrictBlk] = dsum;   // the pass's last, partial block
+    atomicMax(sp.bnd + s * 8 + 0, abs_bits(dmax));
+    atomicMax(sp.bnd + s * 8 + 2, abs_bits(ymax));
+  }
 }
 
 // KS2: the band-pass's backward pass (scipy runs lfilter over y1 reversed,
 // from zi * y1[-1]); chunk c covers reversed positions [o0, o1), i.e. f[i] for
 // i = m1 - 1 - k - pad
-template <bool ZO>
+template <bool ZO, bool ST>
 __global__ __launch_bounds__(64) void k_split_bp_bwd(PskBuffers buf, PskParams p, Iir f, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t c = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -206,14 +239,37 @@ __global__ __launch_bounds__(64) void k_split_bp_bwd(PskBuffers buf, PskParams p
 #pragma unroll
     for (int i = 0; i < 8; ++i) z[i] = 0.0;
   }
+  [[maybe_unused]] double dmax = 0.0, fmx = 0.0, dsum = 0.0;   // ST: the largest step bound and |f|, block sums
+  [[maybe_unused]] int dcnt = 0;
+  [[maybe_unused]] double* dblk = ST ? sp.sc + s * sp.sstride + strict_off_d2(sp) : nullptr;
   split_chain_2(
       k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
       [&](int64_t, double v) { split_bp_warm<ZO>(z, f, v); },
       [&](int64_t kk, double v) {
+        [[maybe_unused]] double sz = 0.0;
+        if constexpr (ST) sz = step_bound_pre(z);
         const double y = split_bp_step<ZO>(z, f, v);
         const int64_t i = m1 - 1 - kk - pad;
-        if (i >= 0 && i < n) fo[i] = y;
+        if (i >= 0 && i < n) {
+          fo[i] = y;
+          if constexpr (ST) fmx = fmax(fmx, fabs(y));
+        }
+        if constexpr (ST) {
+          const double dd = step_bound(sp, sz, v, y);
+          dmax = fmax(dmax, dd);
+          dsum += dd;
+          if (++dcnt == kStrictBlk) {
+            dblk[kk / kStrictBlk] = dsum;
+            dsum = 0.0;
+            dcnt = 0;
+          }
+        }
       });
+  if constexpr (ST) {
+    if (dcnt > 0) dblk[(o1 - 1) / kStrictBlk] = dsum;
+    atomicMax(sp.bnd + s * 8 + 3, abs_bits(dmax));
+    atomicMax(sp.bnd + s * 8 + 5, abs_bits(fmx));
+  }
 }
 
 // KS3: the low-pass's forward pass of one component of the baseband
@@ -312,6 +368,134 @@ __global__ __launch_bounds__(64) void k_split_lp_bwd(PskBuffers buf, PskParams p
       });
 }
 
+// KB (STRICT; split_strict.h): one workgroup per stream turns KS0-KS2's
+// per-block step bounds and per-chunk start bounds into a bound e(k) on each
+// symbol component's |split - reference|:
+//   E1[J]  the forward pass, output block J: the split's and the serial's
+//          rounding (block sums of D through W, the cut remainder at max D),
+//          the chunk starts' errors (+ truncation tk * peak) through GS
+//   E2[J]  the backward pass at forward block J: the forward rounding through
+//          the backward pass (K12, exact at block resolution), the start
+//          errors through |h| (HS), the last input's error through the zi
+//          start (TZ), its own rounding and starts (in its own block index)
+//   X[fb]  the mixer's output error over sample block fb
+//   e(k)   lpc[k] x the largest X within the low-pass's reach of symbol k (and
+//          the extension's source blocks), + the cut remainder, + c3 P3
+// The serial's rounding is the split's within the a-posteriori caps (each
+// pass's difference <= 2^-10 of its input peak; a stream past them gets e =
+// inf: flagged).  Every sum is of non-negative terms; the final factor
+// 1 + 2^-30 covers their own rounding.
+__device__ __forceinline__ double bnd_get(const unsigned long long* b, int i) {
+  return __longlong_as_double((long long)b[i]);
+}
+__device__ __forceinline__ void lds_max(unsigned long long* m, double v) {
+  atomicMax(m, (unsigned long long)__double_as_longlong(fabs(v)));
+}
+constexpr int kKbThreads = 256;
+__global__ __launch_bounds__(kKbThreads) void k_split_strict_bound(PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.x;
+  double* __restrict__ sc = sp.sc + s * sp.sstride;
+  const double* d1 = sc + strict_off_d1(sp);
+  const double* d2 = sc + strict_off_d2(sp);
+  const double* ds1 = sc + strict_off_ds1(sp);
+  const double* ds2 = sc + strict_off_ds2(sp);
+  double* e1 = sc + strict_off_e1(sp);
+  double* s1 = sc + strict_off_s1(sp);
+  double* e2 = sc + strict_off_e2(sp);
+  double* xb = sc + strict_off_x(sp);
+  double* eo = sc + strict_off_e(sp);
+  __shared__ unsigned long long red[4];   // max E1, max S1, max E2 (F), max X
+  if (threadIdx.x < 4) red[threadIdx.x] = 0ull;
+  const unsigned long long* b = sp.bnd + s * 8;
+  const double D1m = bnd_get(b, 0), y1m = bnd_get(b, 2), D2m = bnd_get(b, 3), fm0 = bnd_get(b, 5);
+  const double peak1 = __longlong_as_double((long long)sp.peak[s]);
+  const double u = 0x1p-53, eta = 0x1p-1060, two = 2.0 + 0x1p-20;
+  const int64_t nb1 = sp.nb1, nbs = sp.nbs, m1 = p.m1, n = p.n, LB = sp.L / kStrictBlk;
+  const int pad1 = p.pad1, pad2 = p.pad2;
+  const double cap1 = 0x1p-10 * peak1, p2 = y1m + cap1, cap2 = 0x1p-10 * p2;
+  const double sec1 = sp.u2 * sp.zb * cap1 + sp.ky * cap1;
+  // the forward pass's per-stream terms (besides the block sums)
+  const double c1 = sp.g1x * (sec1 + 2 * eta) + sp.gmax * u * sp.zi_sum * peak1;
+  __syncthreads();
+  for (int64_t J = threadIdx.x; J < nb1; J += kKbThreads) {
+    double r = sp.w_tail * D1m;
+    const int64_t dn = J + 1 < sp.nw ? J + 1 : sp.nw;
+    for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d1[J - dl], r);
+    const int64_t c = J / LB;
+    const int64_t q = J - c * LB;
+    const double st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds1[c] + sp.tk * peak1) : 0.0;
+    s1[J] = st;
+    e1[J] = two * r + c1 + st;
+    lds_max(&red[0], e1[J]);
+    lds_max(&red[1], st);
+  }
+  __syncthreads();
+  const double E1max = __longlong_as_double((long long)red[0]), S1max = __longlong_as_double((long long)red[1]);
+  const double E1last = fmax(e1[nb1 - 1], nb1 > 1 ? e1[nb1 - 2] : 0.0);
+  const double sec2 = sp.u2 * sp.zb * cap2 + sp.kx * E1max + sp.ky * cap2;
+  const double c2 = sp.hz * c1 + sp.g1x * (sec2 + 2 * eta) + 2.0 * sp.gmax * u * sp.zi_sum * p2;
+  // the backward pass's own rounding and starts at its block K (its own index)
+  auto own2 = [&](int64_t K) {
+    if (K < 0 || K >= nb1) return 0.0;
+    double r = sp.w_tail * D2m;
+    const int64_t dn = K + 1 < sp.nw ? K + 1 : sp.nw;
+    for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d2[K - dl], r);
+    const int64_t c = K / LB;
+    const int64_t q = K - c * LB;
+    const double st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds2[c] + sp.tk * p2) : 0.0;
+    return two * r + st;
+  };
+  auto tzw = [&](int64_t q) { return q < sp.nz ? sp.kTZ[q] : sp.tz_tail; };
+  for (int64_t J = threadIdx.x; J < nb1; J += kKbThreads) {
+    // forward block J: j in [16 J, 16 J + 15] <-> backward index k2 = m1 - 1 - j
+    double a = sp.k12_tail * D1m;
+    for (int64_t kq = 0; kq < sp.nk; ++kq) {
+      const int64_t bb = J + kq - sp.k12_off;
+      if (bb >= 0 && bb < nb1) a = __builtin_fma(sp.kK12[kq], d1[bb], a);
+    }
+    double h = sp.hs_tail * S1max;
+    for (int64_t db = 0; db < sp.nh && J + db < nb1; ++db) h = __builtin_fma(sp.kHS[db], s1[J + db], h);
+    const int64_t jhi = 16 * J + 15 < m1 - 1 ? 16 * J + 15 : m1 - 1;
+    const int64_t k2lo = m1 - 1 - jhi, k2hi = m1 - 1 - 16 * J;
+    const int64_t Ka = k2lo / kStrictBlk, Kb = k2hi / kStrictBlk;
+    const double tz = fmax(tzw(Ka), tzw(Kb)) * E1last;
+    const double o2 = fmax(own2(Ka), own2(Kb));
+    e2[J] = two * a + h + tz + o2 + c2;
+    lds_max(&red[2], e2[J]);
+  }
+  __syncthreads();
+  const double Fmax = __longlong_as_double((long long)red[2]);
+  const double fm = fm0 + Fmax;
+  for (int64_t fb = threadIdx.x; fb < nbs; fb += kKbThreads) {
+    const int64_t ilo = 16 * fb, ihi = 16 * fb + 15 < n - 1 ? 16 * fb + 15 : n - 1;
+    const double F = fmax(e2[(ilo + pad1) / kStrictBlk], e2[(ihi + pad1) / kStrictBlk]);
+    xb[fb] = F * (1.0 + 0x1p-50) + 0x1.02p-52 * fm;
+    lds_max(&red[3], xb[fb]);
+  }
+  __syncthreads();
+  const double Xmax = __longlong_as_double((long long)red[3]);
+  const double P3 = 3.0 * (fm + Xmax);
+  const bool ok = E1max <= cap1 && Fmax <= cap2;      // false for NaN
+  const int64_t S = p.n_sym;
+  const double tailc = sp.lp_tail * Xmax + sp.c3 * P3;
+  for (int64_t k = threadIdx.x; k < S; k += kKbThreads) {
+    const int64_t t = p.first + k * p.sps;
+    const int64_t lo = t - sp.lp_rad - pad2, hi = t + sp.lp_rad + pad2;
+    const int64_t flo = lo > 0 ? lo / kStrictBlk : 0, fhi = (hi < n - 1 ? hi : n - 1) / kStrictBlk;
+    double xw = fmax(xb[0], xb[nbs - 1]);
+    for (int64_t fb = flo; fb <= fhi; ++fb) xw = fmax(xw, xb[fb]);
+    const double e = (1.0 + 0x1p-30) * __builtin_fma(sp.lpc[k], xw, tailc);
+    eo[k] = ok ? e : __builtin_inf();
+  }
+  if (threadIdx.x == 0) {
+    double* scal = eo + S;
+    scal[0] = E1max;
+    scal[1] = Fmax;
+    scal[2] = Xmax;
+    scal[3] = ok ? P3 : -P3;
+  }
+}
+
 // KS5: one thread per (stream, 32-bit word): the differential products of the
 // word's symbols in numpy's fma form, the reference's decision (qpsk_dibit /
 // real < 0, as K4a), and the margin: |s| <= |s|_1, a symbol's error <= E, so
@@ -331,15 +515,25 @@ __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p,
   const double E = sp.kappa * peak;
   // tiny / huge / non-finite input: every decision goes the serial way
   bool flag = !(peak >= 0x1p-400 && peak <= 0x1p400);
+  // STRICT: |symbol error|_2 <= sqrt2 e(k), both components within e(k) (KB;
+  // inf when the stream's caps failed); else kappa * peak for every symbol
+  const double sq2 = 0x1.6a09e667f3bcdp+0;
+  const double* eo = sp.strict ? sp.sc + s * sp.sstride + strict_off_e(sp) : nullptr;
+  auto esym = [&](int64_t k) { return sq2 * eo[k]; };
   const double* __restrict__ sy = sp.sym + (size_t)s * S * 2;
   uint32_t word = 0;
   double br = sy[2 * k0], bi0 = sy[2 * k0 + 1];
+  double e0 = sp.strict ? esym(k0) : E;
   for (int64_t k = k0; k < k1; ++k) {
     const double pr = sy[2 * (k + 1)], pim = sy[2 * (k + 1) + 1];
     const double bi = -bi0;
     const double dr = __builtin_fma(pr, br, -(pim * bi));
     const double a0 = fabs(br) + fabs(bi), a1 = fabs(pr) + fabs(pim);
-    const double md = 0x1.6a09e667f3bcdp+0 * E * (a0 + a1 + E) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
+    const double e1 = sp.strict ? esym(k + 1) : E;
+    // |d error|_1 <= sqrt2 (e1 |s0|_2 + e0 |s1|_2 + e0 e1), |s|_2 <= |s|_1
+    const double md = sp.strict ? sq2 * ((e1 * a0 + e0 * a1) + e0 * e1) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1)
+                                : sq2 * E * (a0 + a1 + E) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
+    e0 = e1;
     if (qpsk) {
       const double di = __builtin_fma(pr, bi, pim * br);
       const double adr = fabs(dr), adi = fabs(di);
@@ -366,33 +560,51 @@ hipError_t launch_psk_split_bp(const PskBuffers& b, const PskParams& p, const Ii
   const dim3 blk0(256), g0((unsigned)((sp.c1 + 3) / 4), (unsigned)B);
   const bool zo = p.bp_zero_odd && p.bp_sym;
   if (sp.conv && (!sp.ktab || !sp.z0tab || !sp.zs)) return hipErrorInvalidValue;
+  // the strict bound covers the convolution starts only (no FMA warm-ups)
+  if (sp.strict && (!sp.conv || !sp.bnd || !sp.kabs || !sp.z0abs || !sp.lpc)) return hipErrorInvalidValue;
+  const bool stv = sp.strict != 0;
+#define KS0F(T) \
+  do { \
+    if (stv) hipLaunchKernelGGL((k_split_bp_state_fwd<T, true>), g0, blk0, 0, st, b, p, sp); \
+    else hipLaunchKernelGGL((k_split_bp_state_fwd<T, false>), g0, blk0, 0, st, b, p, sp); \
+  } while (0)
+#define KS1F(T) \
+  do { \
+    if (zo) { \
+      if (stv) hipLaunchKernelGGL((k_split_bp_fwd<T, true, true>), g1, blk, 0, st, b, p, bp, sp); \
+      else hipLaunchKernelGGL((k_split_bp_fwd<T, true, false>), g1, blk, 0, st, b, p, bp, sp); \
+    } else { \
+      if (stv) hipLaunchKernelGGL((k_split_bp_fwd<T, false, true>), g1, blk, 0, st, b, p, bp, sp); \
+      else hipLaunchKernelGGL((k_split_bp_fwd<T, false, false>), g1, blk, 0, st, b, p, bp, sp); \
+    } \
+  } while (0)
   if (sp.conv) {
     switch (b.dtype) {
-      case kF32: hipLaunchKernelGGL(k_split_bp_state_fwd<float>, g0, blk0, 0, st, b, p, sp); break;
-      case kF64: hipLaunchKernelGGL(k_split_bp_state_fwd<double>, g0, blk0, 0, st, b, p, sp); break;
-      case kI16: hipLaunchKernelGGL(k_split_bp_state_fwd<int16_t>, g0, blk0, 0, st, b, p, sp); break;
+      case kF32: KS0F(float); break;
+      case kF64: KS0F(double); break;
+      case kI16: KS0F(int16_t); break;
       default: return hipErrorInvalidValue;
     }
   }
   switch (b.dtype) {
-    case kF32:
-      if (zo) hipLaunchKernelGGL((k_split_bp_fwd<float, true>), g1, blk, 0, st, b, p, bp, sp);
-      else hipLaunchKernelGGL((k_split_bp_fwd<float, false>), g1, blk, 0, st, b, p, bp, sp);
-      break;
-    case kF64:
-      if (zo) hipLaunchKernelGGL((k_split_bp_fwd<double, true>), g1, blk, 0, st, b, p, bp, sp);
-      else hipLaunchKernelGGL((k_split_bp_fwd<double, false>), g1, blk, 0, st, b, p, bp, sp);
-      break;
-    case kI16:
-      if (zo) hipLaunchKernelGGL((k_split_bp_fwd<int16_t, true>), g1, blk, 0, st, b, p, bp, sp);
-      else hipLaunchKernelGGL((k_split_bp_fwd<int16_t, false>), g1, blk, 0, st, b, p, bp, sp);
-      break;
-    default:
-      return hipErrorInvalidValue;
+    case kF32: KS1F(float); break;
+    case kF64: KS1F(double); break;
+    case kI16: KS1F(int16_t); break;
+    default: return hipErrorInvalidValue;
   }
-  if (sp.conv) hipLaunchKernelGGL(k_split_bp_state_bwd, g0, blk0, 0, st, b, p, sp);
-  if (zo) hipLaunchKernelGGL((k_split_bp_bwd<true>), g1, blk, 0, st, b, p, bp, sp);
-  else hipLaunchKernelGGL((k_split_bp_bwd<false>), g1, blk, 0, st, b, p, bp, sp);
+#undef KS1F
+#undef KS0F
+  if (sp.conv) {
+    if (stv) hipLaunchKernelGGL(k_split_bp_state_bwd<true>, g0, blk0, 0, st, b, p, sp);
+    else hipLaunchKernelGGL(k_split_bp_state_bwd<false>, g0, blk0, 0, st, b, p, sp);
+  }
+  if (zo) {
+    if (stv) hipLaunchKernelGGL((k_split_bp_bwd<true, true>), g1, blk, 0, st, b, p, bp, sp);
+    else hipLaunchKernelGGL((k_split_bp_bwd<true, false>), g1, blk, 0, st, b, p, bp, sp);
+  } else {
+    if (stv) hipLaunchKernelGGL((k_split_bp_bwd<false, true>), g1, blk, 0, st, b, p, bp, sp);
+    else hipLaunchKernelGGL((k_split_bp_bwd<false, false>), g1, blk, 0, st, b, p, bp, sp);
+  }
   return hipGetLastError();
 }
 
@@ -419,6 +631,10 @@ hipError_t launch_psk_split_slice(const PskBuffers& b, const PskParams& p, const
   if (B < 1 || p.n_words < 1 || p.n_bits < 1) return hipSuccess;
   if (B > 65535) return hipErrorInvalidValue;
   const dim3 blk(64), g5((unsigned)((p.n_words + 63) / 64), (unsigned)B);
+  if (sp.strict) {
+    if (!sp.sc || sp.L % kStrictBlk != 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_strict_bound, dim3((unsigned)B), dim3(kKbThreads), 0, st, p, sp);
+  }
   hipLaunchKernelGGL(k_split_slice, g5, blk, 0, st, b, p, sp);
   return hipGetLastError();
 }

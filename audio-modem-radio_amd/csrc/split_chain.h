@@ -89,15 +89,29 @@ __device__ __forceinline__ auto bwd_blocks(const double* a, int64_t top) {
   };
 }
 
+// The strict mode's bound on a start state's error (split_strict.h): the sum
+// over states of |computed - exact| <= gam (sum_m kabs[m] |v(o0 - 1 - m)| +
+// z0abs[o0] |v0|) -- the FMA chains, the butterfly and the tables' rounding;
+// lane 0 stores it to *dst (0 for the chunk at the pass's start: scipy's own
+// zi * v0).  Off when dst is null.
+struct ConvBound {
+  const double* kabs;
+  const double* z0abs;
+  double gam;
+  double* dst;
+};
+
 // A chunk's start state by convolution (psk_split_kernels.hip KS0,
 // fsk_kernels.hip FS0): NS states, K [w][NS] and Z0 [w + 1][NS]
 // (iir_design.h split_state_tables), one wave per chunk; lane 0 writes zo.
-template <int NS, typename Val>
+template <int NS, bool ST = false, typename Val>
 __device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab, const double* __restrict__ z0tab,
-                                                 int64_t w, int64_t o0, double v0, Val val, double* __restrict__ zo) {
+                                                 int64_t w, int64_t o0, double v0, Val val, double* __restrict__ zo,
+                                                 ConvBound cb = ConvBound{}) {
   static_assert(NS % 2 == 0, "pairs of states per 16-byte load");
   const int lane = (int)(threadIdx.x & 63);
   double acc[NS];
+  [[maybe_unused]] double sa = 0.0;   // ST: sum kabs[m] |v|
 #pragma unroll
   for (int i = 0; i < NS; ++i) acc[i] = 0.0;
   const int64_t M = o0 < w ? o0 : w;
@@ -123,13 +137,22 @@ __device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab
           acc[2 * h] = __builtin_fma(k[u][h][0], v[u], acc[2 * h]);
           acc[2 * h + 1] = __builtin_fma(k[u][h][1], v[u], acc[2 * h + 1]);
         }
+        if constexpr (ST) sa = __builtin_fma(cb.kabs[m0 + 64 * u], fabs(v[u]), sa);
       }
     }
   }
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1)
+  for (int d = 1; d < 64; d <<= 1) {
 #pragma unroll
     for (int i = 0; i < NS; ++i) acc[i] = acc[i] + __shfl_xor(acc[i], d, 64);
+    if constexpr (ST) sa = sa + __shfl_xor(sa, d, 64);
+  }
+  if constexpr (ST) {
+    if (lane == 0) {
+      const double z0t = o0 <= w ? cb.z0abs[o0] * fabs(v0) : 0.0;
+      *cb.dst = o0 > 0 ? cb.gam * (sa + z0t) : 0.0;
+    }
+  }
   if (lane == 0) {
     if (o0 == 0) {
 #pragma unroll

@@ -214,6 +214,40 @@ int amr_psk_split_symbols_host(amr_psk_plan *plan, const void *x, int dtype, int
 int amr_split_state_tables(const double *b, const double *a, const double *zi, int ntaps, int64_t w, double *K,
                            double *Z0);
 int amr_psk_plan_split_conv(amr_psk_plan *plan);
+/* The time-split layout's STRICT mode (csrc/split_strict.h).
+ * By default a split decision is kept when it clears kappa * peak|x| -- a
+ * measured premise (the worst error over the test signal classes and the
+ * adversarial search is >= 54x below it), not a bound.  Strict mode keeps it
+ * only when it clears a bound that holds for every input: per-step rounding
+ * bounds and chunk-start error bounds the kernels measure on the stream itself,
+ * carried through the filters' L1 response gains to a bound per symbol; a
+ * decision inside it goes to the serial row kernels as before.  Bytes are the
+ * reference's in both modes wherever the premise holds; strict mode makes
+ * that unconditional at the cost of more flagged captures.
+ * amr_psk_plan_set_split_strict: 1 on, 0 off, -1 the process default
+ * (AMR_PSK_SPLIT_STRICT=1 turns it on); amr_psk_plan_split_strict: whether this
+ * plan's split calls use it; amr_psk_plan_last_strict: whether the last split
+ * call did.  No reference counterpart (modem.py:197-214 is what is bounded). */
+int amr_psk_plan_set_split_strict(amr_psk_plan *plan, int mode);
+int amr_psk_plan_split_strict(amr_psk_plan *plan);
+int amr_psk_plan_last_strict(const amr_psk_plan *plan);
+/* Diagnostic (tests): the strict passes over a host batch -> the symbol
+ * samples sym [n_streams][n_sym][re, im], the bound e [n_streams][n_sym] on
+ * each symbol component's |split - reference| and, per stream, scalars
+ * [n_streams][4]: E1 (band-pass forward), F (band-pass output), X (mixer
+ * output) and P3 (low-pass input peak; negative when the a-posteriori caps
+ * failed and the stream would be flagged). */
+int amr_psk_split_bounds_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                              double *sym, double *ebound, double *scalars);
+/* The strict design from the filters alone (host arithmetic; the tests'
+ * restatement of the bound uses it): consts[32] = g1x, gmax, hz, tk, zi_sum,
+ * zb, kx, ky, u2, gam, c3, w1, w2, n_sym, and the sizes nw, nk, nh, ng, nz,
+ * k12_off, the cut remainders w_tail, k12_tail, hs_tail, tz_tail, lp_tail,
+ * lp_rad, ok, kappa; tabs (NULL: not written) = kabs [w1] | z0abs [w1 + 1] |
+ * lpc [n_sym] | W [nw] | K12 [nk] | HS [nh] | GS [ng] | TZ [nz]. */
+int amr_psk_split_strict_design(const double *bp_b, const double *bp_a, const double *bp_zi, int bp_ntaps,
+                                const double *lp_b, const double *lp_a, const double *lp_zi, int lp_ntaps,
+                                int64_t n_samples, int64_t first, int64_t sps, double *consts, double *tabs);
 /* number of streams the exact complex low-pass path re-ran in the last call */
 int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
 

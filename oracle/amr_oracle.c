@@ -475,6 +475,53 @@ static void chunked_pass_conv(const double *b, const double *a, int nt, const do
         for (int64_t j = o0; j < o1; ++j) df2t(b, a, nt, z, in + j, &out[j], 1, 1);
     }
 }
+/* The strict mode's statistics of one convolution-started chunked pass
+ * (psk_split_kernels.hip KS0 + KS1 / KS2 with PskSplit::strict, restated):
+ * per chunk c the start-state bound ds[c] = gam (sum_m kabs[m] |in[o0-1-m]|
+ * + z0abs[o0] |in[0]|) (0 for c = 0) summed as the wave does (lane l over m =
+ * l mod 64 with fma, then the butterfly); per output step the rounding bound
+ * fma(u2, sz, fma(kx, |x|, ky |y|)), sz the pre-step |z1..z7| in the
+ * kernel's pairing, summed per block of 16 outputs in step order (dblk) and
+ * maximised (*dmax); *ymax: max |out| over [olo, ohi).  cst: u2, kx, ky, gam.
+ * L must be a multiple of 16. */
+static void chunked_pass_conv_stats(const double *b, const double *a, int nt, const double *in, double *out,
+                                    int64_t m, int64_t L, int64_t w, const double *K, const double *Z0,
+                                    const double *kabs, const double *z0abs, const double *cst, int64_t olo,
+                                    int64_t ohi, double *dblk, double *ds, double *dmax, double *ymax)
+{
+    double z[32];
+    for (int64_t o0 = 0, c = 0; o0 < m; o0 += L, ++c) {
+        const int64_t o1 = o0 + L < m ? o0 + L : m;
+        conv_state(K, Z0, nt - 1, in, o0, w, z);
+        ds[c] = 0.0;
+        if (o0 > 0) {
+            double p[64], q[64];
+            for (int l = 0; l < 64; ++l) p[l] = 0.0;
+            const int64_t M = o0 < w ? o0 : w;
+            for (int64_t mm = 0; mm < M; ++mm) p[mm & 63] = fma(kabs[mm], fabs(in[o0 - 1 - mm]), p[mm & 63]);
+            for (int d = 1; d < 64; d <<= 1) {
+                for (int l = 0; l < 64; ++l) q[l] = p[l] + p[l ^ d];
+                memcpy(p, q, sizeof(p));
+            }
+            const double z0t = o0 <= w ? z0abs[o0] * fabs(in[0]) : 0.0;
+            ds[c] = cst[3] * (p[0] + z0t);
+        }
+        double dsum = 0.0;
+        int cnt = 0;
+        for (int64_t j = o0; j < o1; ++j) {
+            const double sz = ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) +
+                              ((fabs(z[5]) + fabs(z[6])) + fabs(z[7]));
+            df2t(b, a, nt, z, in + j, &out[j], 1, 1);
+            const double dd = fma(cst[0], sz, fma(cst[1], fabs(in[j]), cst[2] * fabs(out[j])));
+            if (dd > *dmax) *dmax = dd;
+            dsum += dd;
+            if (++cnt == 16) { dblk[j / 16] = dsum; dsum = 0.0; cnt = 0; }
+            if (j >= olo && j < ohi && fabs(out[j]) > *ymax) *ymax = fabs(out[j]);
+        }
+        if (cnt > 0) dblk[(o1 - 1) / 16] = dsum;
+    }
+}
+
 static void chunked_pass(const double *b, const double *a, int nt, const double *zi,
                          const double *in, double *out, int64_t m, int64_t L, int64_t w)
 {
@@ -555,6 +602,35 @@ int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sp
     }
     free(e); free(y); free(r); free(g);
     return S;
+}
+
+/* The strict mode's per-stream statistics of the split band-pass passes
+ * (restating the device's; tests compute the bound from them): d1, d2 [nb1]
+ * the passes' per-block step bound sums (nb1 = ceil(m1 / 16)), ds1, ds2 [c1]
+ * their chunk-start bounds (c1 = ceil(m1 / L)), stats[4] = D1max, max|y1|,
+ * D2max, max|f|.  Returns 0, or -1 for bad arguments (bp_nt must be 9: the
+ * kernels' 8 states; L a multiple of 16). */
+int oracle_psk_split_stats(const void *x, int dtype, int64_t n, const double *bp_b, const double *bp_a, int bp_nt,
+                           int64_t L, int64_t w1, const double *K, const double *Z0, const double *kabs,
+                           const double *z0abs, const double *cst, double *d1, double *d2, double *ds1, double *ds2,
+                           double *stats)
+{
+    const int pad1 = 3 * bp_nt;
+    if (bp_nt != 9 || n <= pad1 || L < 16 || L % 16 || !K || !Z0) return -1;
+    const int64_t m1 = n + 2 * (int64_t)pad1;
+    double *e = (double *)malloc(sizeof(double) * (size_t)m1);
+    double *y = (double *)malloc(sizeof(double) * (size_t)m1);
+    double *r = (double *)malloc(sizeof(double) * (size_t)m1);
+    for (int i = 0; i < 4; ++i) stats[i] = 0.0;
+    for (int64_t j = 0; j < m1; ++j) e[j] = ext_sample(x, dtype, n, pad1, j);
+    chunked_pass_conv_stats(bp_b, bp_a, bp_nt, e, y, m1, L, w1, K, Z0, kabs, z0abs, cst, 0, m1, d1, ds1, &stats[0],
+                            &stats[1]);
+    for (int64_t k = 0; k < m1; ++k) r[k] = y[m1 - 1 - k];
+    /* f[i] = y[m1 - 1 - pad1 - i], i in [0, n) <-> pass-2 index k in [pad1, pad1 + n) */
+    chunked_pass_conv_stats(bp_b, bp_a, bp_nt, r, y, m1, L, w1, K, Z0, kabs, z0abs, cst, pad1, pad1 + n, d2, ds2,
+                            &stats[2], &stats[3]);
+    free(e); free(y); free(r);
+    return 0;
 }
 
 /* The serial (reference) symbol samples baseband[first::sps] of the same

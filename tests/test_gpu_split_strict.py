@@ -1,0 +1,131 @@
+"""The PSK time-split layout's STRICT mode on the MI355X.
+
+By default a split decision is kept when it clears kappa * peak|x| -- a
+measured premise.  Strict mode (AMR_PSK_SPLIT_STRICT=1 /
+amr_psk_plan_set_split_strict) keeps it only when it clears a bound that holds
+for every input (csrc/split_strict.h, psk_split_kernels.hip KB).  Checked
+here: the device's bound is the restatement's (tests/_util.py
+strict_symbol_bounds over oracle.psk_split_stats -- the CPU tests prove that
+restatement >= the measured error), it is >= the device's own |split -
+reference| on every symbol component, and strict calls decide the reference's
+bytes (flagged captures through the serial kernels)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("qpsk", 9600, 3000.0, 96000.0, 96000), ("qpsk", 1200, 3000.0, 96000.0, 48000),
+         ("bpsk", 1200, 3000.0, 96000.0, 48000), ("qpsk", 2400, 1800.0, 44100.0, 44100)]
+
+
+def _signals(kind, baud, fc, fs, n, seed):
+    import synth
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / fs
+    out = [rng.normal(0, 0.3, n), np.sign(np.sin(2 * np.pi * fc * t)), np.sin(2 * np.pi * fc * t)]
+    if fs / baud >= 10:
+        for _ in range(3):
+            w = synth.qpsk_waveform(synth.random_frame(rng, 200), baud, fc, fs) if kind == "qpsk" else \
+                synth.bpsk_waveform(synth.random_frame(rng, 200), baud, fc, fs)
+            x = np.zeros(n)
+            x[:min(n, w.size)] = w[:n]
+            out.append(x + rng.normal(0, 0.05, n))
+        out.append(np.clip(4 * out[-1], -1, 1))
+    return np.stack(out).astype(np.float32)
+
+
+@pytest.mark.parametrize("kind,baud,fc,fs,n", CASES, ids=lambda v: str(v))
+def test_device_bound_is_the_restatement_and_holds(kind, baud, fc, fs, n):
+    import _amr
+    from oracle import oracle
+    from _util import strict_symbol_bounds
+    x = _signals(kind, baud, fc, fs, n, baud)
+    d = _amr.split_strict_design(kind, n, baud, fc, fs)
+    assert d is not None
+    sd = _amr.split_design(kind, n, baud, fc, fs)
+    T = _amr.split_state_tables(kind, n, baud, fc, fs)
+    pl = _amr.PskPlan(kind, n, baud, fc, fs, max_streams=x.shape[0])
+    sym, eb, sc = pl.split_bounds(x)
+    L = pl.split_info()["chunk"]
+    assert L % 16 == 0
+    op = oracle.PskPlan(kind, n, baud, fc, fs)
+    bad, ratio = [], []
+    for i in range(x.shape[0]):
+        want_sym = oracle.psk_split_symbols(kind, x[i], baud, fc, fs, L, sd["warmup_bp"], sd["warmup_lp"], tables=T)
+        assert np.array_equal(sym[i], want_sym), i
+        st = oracle.psk_split_stats(kind, x[i], baud, fc, fs, L, sd["warmup_bp"], T, d)
+        e, scal = strict_symbol_bounds(st, d, float(np.abs(x[i]).max()), n, op.first, op.sps, L)
+        assert (sc[i, 3] > 0) == scal[4], i
+        if not scal[4]:
+            continue
+        assert np.allclose(eb[i], e, rtol=1e-9, atol=0), (i, np.abs(eb[i] / e - 1).max())
+        ref = oracle.psk_symbols(kind, x[i], baud, fc, fs)
+        act = np.maximum(np.abs(sym[i].real - ref.real), np.abs(sym[i].imag - ref.imag))
+        if (act > eb[i]).any():
+            bad.append(i)
+        ratio.append(float((eb[i] / np.maximum(act, 1e-300)).min()))
+    print(f"{kind}@{baud}: device bound / measured >= {min(ratio):.1f} over {len(ratio)} streams")
+    assert not bad, bad
+
+
+def test_strict_mode_bytes_and_flag_rate():
+    """Strict calls on 96 noisy one-capture calls (QPSK@9600, the benchmark's
+    captures): bytes == the oracle's, the strict mode reported, and the
+    flagged count printed next to the default mode's."""
+    import _amr
+    import modem
+    import synth
+    from oracle import oracle
+    x = synth.qpsk_batch(96, 96000, 9600, seed=21, distinct=96)
+    want, _ = oracle.psk_demod_batch("qpsk", x, 9600, n_threads=min(16, os.cpu_count() or 1))
+    pl = _amr.get_psk_plan("qpsk", 96000, 9600, 3000.0, 96000, 1)
+    flagged = {}
+    for strict in (False, True):
+        pl.set_split_strict(strict)
+        f = 0
+        for i in range(x.shape[0]):
+            got = modem.qpsk_demodulate(x[i], baud=9600)
+            assert got == want[i], (strict, i)
+            assert pl.last_layout() == "split" and pl.last_strict() == strict
+            f += pl.split_info()["flagged"]
+        flagged[strict] = f
+    pl.set_split_strict(None)
+    print(f"flagged of 96 captures: default {flagged[False]}, strict {flagged[True]}")
+    assert flagged[True] >= flagged[False]
+
+
+def test_strict_mode_golden_and_sweep(golden, sweep_golden):
+    """Every golden and reference-sweep PSK case through the drop-in with the
+    strict mode on for every plan (AMR_PSK_SPLIT_STRICT=1 in a subprocess: the
+    switch is read once per process): bytes == the reference's."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = f'''
+import sys, json, numpy as np
+sys.path[:0] = [{os.path.join(root, "audio-modem-radio_amd")!r}, {root!r}, {here!r}]
+import modem, _amr
+from _util import call_case, call_sweep_case, expected, outcome
+g = {os.path.join(here, "golden")!r}
+m = json.load(open(g + "/manifest.json")); inp = np.load(g + "/inputs.npz")
+bad = [c["id"] for c in m["cases"] if not c["fn"].startswith("fsk")
+       and outcome(lambda: call_case(modem, c, inp[c["id"]])) != expected(c)]
+m = json.load(open(g + "/sweep_manifest.json")); inp = np.load(g + "/sweep.npz")
+for c in m["cases"]:
+    if c["fn"] == "fsk":
+        continue
+    x = inp[c["id"]]
+    x = x.astype(np.float64) / 32768.0 if x.dtype == np.int16 else x
+    if outcome(lambda: call_sweep_case(modem, c, x)) != expected(c):
+        bad.append(c["id"])
+strict = [p.split_strict() for p in _amr.plan_cache._d.values() if isinstance(p, _amr.PskPlan)]
+print("BAD", bad, "STRICT", all(strict), len(strict))
+'''
+    env = dict(os.environ, AMR_PSK_SPLIT_STRICT="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("BAD")][-1]
+    assert line.startswith("BAD [] STRICT True"), line

@@ -196,3 +196,89 @@ def test_fsk_split_hilbert_gain(n, built_lib):
     e[0] = 1.0
     want = np.abs(hilbert(e)).sum()
     assert want <= d["hilbert_l1"] <= want * (1 + 1e-5)
+
+
+# ---- the strict mode's bound (split_strict.h, psk_split_kernels.hip KB) -----
+def _adversarial(kind, baud, fc, fs, n, rng):
+    """Inputs aimed at the split's weak spots: square waves
+    resonant at each band-pass pole's frequency, the sign pattern of the
+    slowest state response (the input that maximises a state's accumulated
+    error), clipped full-scale PCM, chirps across the band edges, and a
+    full-scale capture that opens with a wrapped (+/- full scale) click."""
+    import _amr
+    import synth
+    _, _, bp, lp, _ = _amr.design_psk(kind, n, baud, fc, fs)
+    b, a, _ = bp
+    t = np.arange(n) / fs
+    ins = {}
+    poles = np.roots(a)
+    for i, p in enumerate(sorted({round(abs(float(np.angle(q))), 9) for q in poles if np.angle(q) > 0})):
+        ins[f"pole_sq{i}"] = np.sign(np.sin(p * np.arange(n) + 0.3))
+    # sign pattern of the zero-input response from state 0 (the slowest decay), repeated
+    z = np.zeros(len(a) - 1)
+    z[0] = 1.0
+    g = []
+    for _ in range(4096):
+        y = z[0]
+        g.append(y)
+        z = np.append(z[1:], 0.0) - a[1:] * y
+    pat = np.sign(np.array(g[::-1]))
+    pat[pat == 0] = 1.0
+    ins["g_sign"] = np.resize(pat, n)
+    if fs / baud >= 10:
+        w = synth.qpsk_waveform(synth.random_frame(rng, 300), baud, fc, fs) if kind == "qpsk" else \
+            synth.bpsk_waveform(synth.random_frame(rng, 300), baud, fc, fs)
+        x = np.zeros(n)
+        x[:min(n, w.size)] = w[:n]
+        ins["clipped"] = np.clip(4.0 * x + rng.normal(0, 0.05, n), -1, 1)
+        xc = x.copy()
+        xc[0], xc[-1] = 1.0, -1.0
+        ins["edge_clicks"] = xc
+    nyq = fs / 2
+    lo, hi = max(0.01 * nyq, fc - 1.5 * baud), min(0.99 * nyq, fc + 1.5 * baud)
+    ins["chirp"] = np.sin(2 * np.pi * (0.7 * lo * t + (1.3 * hi - 0.7 * lo) * t * t / (2 * t[-1])))
+    return ins
+
+
+@pytest.mark.parametrize("kind,baud,fc,fs", CONFIGS, ids=lambda v: str(v))
+def test_strict_bound_holds(kind, baud, fc, fs, built_lib):
+    """The strict mode's bound (KB restated: tests/_util.py strict_symbol_bounds,
+    from the oracle's restatement of KS0-KS2's statistics and libamr.so's
+    strict design) is at least the measured |split - serial| on every symbol
+    component, over the signal classes above and the adversarial inputs, at
+    every filter set; the bound's size against kappa * peak is printed (the
+    flag rate scales with it).  The adversarial inputs' measured error is
+    also held against the default kappa: kappa / worst >= 16."""
+    import _amr
+    from oracle import oracle
+    from _util import strict_symbol_bounds
+    n = 48000 if baud >= 1200 else 96000
+    d = _amr.split_strict_design(kind, n, baud, fc, fs)
+    assert d is not None and d["ok"] == 1.0
+    sd = _amr.split_design(kind, n, baud, fc, fs)
+    T = _amr.split_state_tables(kind, n, baud, fc, fs)
+    pl = oracle.PskPlan(kind, n, baud, fc, fs)
+    rng = np.random.default_rng(baud + 3 * int(fc))
+    ins = _inputs(kind, baud, fc, fs, n, rng)
+    ins.update(_adversarial(kind, baud, fc, fs, n, rng))
+    worst_ratio, bound_ratio, adv_worst, bad = np.inf, [], 0.0, []
+    for name, x in ins.items():
+        ref = oracle.psk_symbols(kind, x, baud, fc, fs)
+        peak = np.abs(x).max()
+        for L in (128, 1024):
+            st = oracle.psk_split_stats(kind, x, baud, fc, fs, L, sd["warmup_bp"], T, d)
+            e, sc = strict_symbol_bounds(st, d, peak, n, pl.first, pl.sps, L)
+            sp = oracle.psk_split_symbols(kind, x, baud, fc, fs, L, sd["warmup_bp"], sd["warmup_lp"], tables=T)
+            act = np.maximum(np.abs(sp.real - ref.real), np.abs(sp.imag - ref.imag))
+            if sc[4] and (act > e).any():
+                bad.append((name, L, int((act > e).sum())))
+            if sc[4]:
+                worst_ratio = min(worst_ratio, float((e / np.maximum(act, 1e-300)).min()))
+            bound_ratio.append(float(np.median(e)) * np.sqrt(2) / (sd["kappa"] * peak))
+            if name in ("g_sign", "clipped", "edge_clicks", "chirp") or name.startswith("pole_sq"):
+                adv_worst = max(adv_worst, float(np.abs(sp - ref).max() / peak))
+    print(f"{kind}@{baud} fc {fc:g} fs {fs:g}: strict bound / measured >= {worst_ratio:.1f}; median bound "
+          f"{np.median(bound_ratio):.2f}x kappa peak; adversarial worst |split - serial| / peak {adv_worst:.3e} "
+          f"(kappa / worst = {sd['kappa'] / max(adv_worst, 1e-300):.1f})")
+    assert not bad, bad
+    assert adv_worst <= sd["kappa"] / 16
