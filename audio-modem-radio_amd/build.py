@@ -23,7 +23,7 @@ SOURCES = ["psk_kernels.hip", "psk_lane_kernels.hip", "psk_split_kernels.hip", "
            "api.cpp", "tx_api.cpp",
            "fsk_api.cpp", "pocketfft_plan.cpp"]
 HEADERS = ["amr_internal.h", "psk_common.h", "fft.h", "api_common.h", "fsk_exact.h", "pocketfft.h", "pocketfft_dev.h",
-           "iir_design.h", "split_chain.h", "odd_ext.h", os.path.join(INCLUDE, "amr.h")]
+           "iir_design.h", "split_chain.h", "odd_ext.h", "split_strict.h", os.path.join(INCLUDE, "amr.h")]
 ARCH = os.environ.get("AMR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", f"--offload-arch={ARCH}",

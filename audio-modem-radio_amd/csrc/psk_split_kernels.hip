@@ -16,18 +16,30 @@
 // the chunked values differ from the serial ones by rounding noise amplified
 // by the filter (a DF-II-T with poles at |z| = 0.989 amplifies its rounding
 // by ~1e7).  So the symbols are NOT bit-exact, and the decisions are made
-// exact by a margin instead:
-//   * every symbol sample's error is below E = kappa * peak|x| (kappa per plan:
-//     64 x the L1 noise gain u * sum_i ||g_i||_1 of both filters, which bounds
-//     the measured worst error within 1.4x over tones, square waves, noise and
-//     modulated signals at 10 parameter sets -- tests/test_gpu_split.py);
-//   * a differential product whose decision could move by that much -- QPSK
-//     ||di| - |dr|| or BPSK |dr| within sqrt2 E (|s0| + |s1| + E) -- flags its
-//     stream (so does exact silence: every zero product is flagged);
+// exact by a margin instead, in one of two modes:
+//   * DEFAULT (a measured premise, not a proof): the symbol error is taken to
+//     be below E = kappa * peak|x| (kappa per plan: 64 x the L1 noise gain
+//     u * sum_i ||g_i||_1 of both filters).  Measured, not derived: the
+//     worst error over tones, square waves, noise, modulated, clipped, chirp
+//     and adversarially searched inputs at 10+ parameter sets stays >= 16x
+//     (tests: >= 56x) below kappa * peak (tests/test_split_margin.py,
+//     tests/test_gpu_split.py).  An input outside that evidence could in
+//     principle exceed E, and an unflagged decision could then differ.
+//   * STRICT (AMR_PSK_SPLIT_STRICT=1 / amr_psk_plan_set_split_strict): KS1 /
+//     KS2 also accumulate per-block rounding bounds of every step, and KB
+//     (k_split_strict_bound) turns them into a per-symbol bound e(k) that
+//     holds for every input (a forward error analysis of the DF-II-T chain,
+//     csrc/split_strict.h; a pass whose error exceeds 2^-10 of its input's
+//     peak flags the stream instead).  E = e(k) then, and the margin below is
+//     a proof.
+//   * either way a differential product whose decision could move by E --
+//     QPSK ||di| - |dr|| or BPSK |dr| within sqrt2 E (|s0| + |s1| + E) --
+//     flags its stream (so does exact silence: every zero product is flagged);
 //   * a flagged stream's batch is recomputed by the serial row-layout kernels
 //     (psk_kernels.hip: bit-exact), launched behind these ones and gated on
 //     the flag count on the device (they exit at once when it is zero).
-// Unflagged decisions are therefore the reference's, bit for bit.
+// Unflagged decisions are the reference's bit for bit under strict mode; under
+// the default they are whenever the measured premise holds for the input.
 //
 // Kernels (grid.y = stream, lanes = chunks; no LDS, no barriers):
 //   KS0 k_split_bp_state_fwd / _bwd (default; AMR_PSK_SPLIT_CONV=0: off): a
@@ -40,6 +52,8 @@
 //   KS2 k_split_bp_bwd   y1 reversed -> f [B][n]
 //   KS3 k_split_lp_fwd   lane = (chunk, component): f * lo, odd ext -> y3 [B][2][m2]
 //   KS4 k_split_lp_bwd   y3 reversed -> symbol samples sym [B][S][2]
+//   KB  k_split_strict_bound (strict mode only) workgroup = stream: the
+//                        block step bounds -> per-symbol bound e [B][S]
 //   KS5 k_split_slice    thread = (stream, word): numpy's fma differential
 //                        product, the sector / sign decision, the margin
 //                        check -> words, flag, count

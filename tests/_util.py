@@ -70,11 +70,20 @@ def fsk_device_demod(pl, x):
     return [out[i, :ln[i]].tobytes() for i in range(B)], sy
 
 
+def pass1_peak(x, pad1=27) -> float:
+    """The band-pass pass-1 input's peak: max |x| over the capture and its
+    odd extension (formed in x's dtype, oracle.odd_edges) -- the peak the
+    device's strict bound scales its caps by (an edge can reach 3 peak|x|)."""
+    import numpy as np
+    from oracle import oracle
+    return float(max(np.abs(np.asarray(x, dtype=np.float64)).max(), np.abs(oracle.odd_edges(x, pad1)).max()))
+
+
 def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
     """The strict mode's per-symbol bound e(k) on each symbol component's
     |split - reference| (psk_split_kernels.hip KB, restated in numpy) from a
     stream's split statistics st (oracle.psk_split_stats / the device's) and
-    the design d (_amr.split_strict_design).  Returns (e [S], (E1max, Fmax,
+    the design d (_amr.split_strict_design); peak1 = pass1_peak(x).  Returns (e [S], (E1max, Fmax,
     Xmax, P3, ok))."""
     import numpy as np
     u, eta, two = 2.0 ** -53, 2.0 ** -1060, 2.0 + 2.0 ** -20

@@ -40,7 +40,7 @@ def _signals(kind, baud, fc, fs, n, seed):
 def test_device_bound_is_the_restatement_and_holds(kind, baud, fc, fs, n):
     import _amr
     from oracle import oracle
-    from _util import strict_symbol_bounds
+    from _util import pass1_peak, strict_symbol_bounds
     x = _signals(kind, baud, fc, fs, n, baud)
     d = _amr.split_strict_design(kind, n, baud, fc, fs)
     assert d is not None
@@ -56,7 +56,7 @@ def test_device_bound_is_the_restatement_and_holds(kind, baud, fc, fs, n):
         want_sym = oracle.psk_split_symbols(kind, x[i], baud, fc, fs, L, sd["warmup_bp"], sd["warmup_lp"], tables=T)
         assert np.array_equal(sym[i], want_sym), i
         st = oracle.psk_split_stats(kind, x[i], baud, fc, fs, L, sd["warmup_bp"], T, d)
-        e, scal = strict_symbol_bounds(st, d, float(np.abs(x[i]).max()), n, op.first, op.sps, L)
+        e, scal = strict_symbol_bounds(st, d, pass1_peak(x[i]), n, op.first, op.sps, L)
         assert (sc[i, 3] > 0) == scal[4], i
         if not scal[4]:
             continue

@@ -251,7 +251,7 @@ def test_strict_bound_holds(kind, baud, fc, fs, built_lib):
     also held against the default kappa: kappa / worst >= 16."""
     import _amr
     from oracle import oracle
-    from _util import strict_symbol_bounds
+    from _util import pass1_peak, strict_symbol_bounds
     n = 48000 if baud >= 1200 else 96000
     d = _amr.split_strict_design(kind, n, baud, fc, fs)
     assert d is not None and d["ok"] == 1.0
@@ -267,7 +267,7 @@ def test_strict_bound_holds(kind, baud, fc, fs, built_lib):
         peak = np.abs(x).max()
         for L in (128, 1024):
             st = oracle.psk_split_stats(kind, x, baud, fc, fs, L, sd["warmup_bp"], T, d)
-            e, sc = strict_symbol_bounds(st, d, peak, n, pl.first, pl.sps, L)
+            e, sc = strict_symbol_bounds(st, d, pass1_peak(x), n, pl.first, pl.sps, L)
             sp = oracle.psk_split_symbols(kind, x, baud, fc, fs, L, sd["warmup_bp"], sd["warmup_lp"], tables=T)
             act = np.maximum(np.abs(sp.real - ref.real), np.abs(sp.imag - ref.imag))
             if sc[4] and (act > e).any():
