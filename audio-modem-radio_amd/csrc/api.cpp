@@ -726,6 +726,10 @@ int amr_psk_split_symbols_host(amr_psk_plan* plan, const void* x, int dtype, int
   if (dtype_size(dtype) == 0 || x_stride < plan->p.n) return fail(AMR_E_INVALID, "bad dtype / x_stride");
   if (!plan->split_designed) split_design(plan);
   if (!plan->split_ok || plan->p.n_sym < 2) return fail(AMR_E_INVALID, "no time-split layout for this plan");
+  // KS0's start states are B x ceil(m1 / L) x 64 B (and as many waves): a
+  // chunk below the layout's own minimum is refused rather than allocated
+  if (chunk < 0 || (chunk > 0 && chunk < kSplitConvMinL && split_conv_on(plan)))
+    return fail(AMR_E_INVALID, "amr_psk_split_symbols_host: chunk must be 0 (the plan's) or >= 128 with the convolution starts");
   const int64_t n = plan->p.n, es = dtype_size(dtype);
   int64_t have = plan->d_x_bytes;
   HIP_TRY(hipStreamSynchronize(plan->stream));
@@ -878,6 +882,16 @@ int amr_psk_plan_exact_streams(amr_psk_plan* plan, int64_t* count) {
   std::lock_guard<std::mutex> lk(plan->mu);
   HIP_TRY(hipSetDevice(plan->device));
   HIP_TRY(hipStreamSynchronize(plan->stream));
+  if (plan->last_layout == AMR_LAYOUT_SPLIT) {
+    // the flag memsets behind the gate run whatever the count; the row
+    // fallback (and its exact low-pass) ran only when a stream was flagged
+    int32_t sc = 0;
+    HIP_TRY(hipMemcpy(&sc, plan->split_count, 4, hipMemcpyDeviceToHost));
+    if (sc == 0) {
+      *count = 0;
+      return AMR_OK;
+    }
+  }
   std::vector<int32_t> fl((size_t)plan->groups * kWave);
   HIP_TRY(hipMemcpy(fl.data(), plan->flags, fl.size() * 4, hipMemcpyDeviceToHost));
   int64_t c = 0;

@@ -1191,7 +1191,11 @@ int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
 
-int amr_fsk_plan_split_conv(const amr_fsk_plan* plan) { return plan ? (fsk_split_conv_on(plan) ? 1 : 0) : -1; }
+int amr_fsk_plan_split_conv(amr_fsk_plan* plan) {
+  if (!plan) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return fsk_split_conv_on(plan) ? 1 : 0;
+}
 
 int amr_fsk_plan_set_layout(amr_fsk_plan* plan, int layout) {
   if (!plan || layout < AMR_FSK_LAYOUT_AUTO || layout > AMR_FSK_LAYOUT_SPLIT)
@@ -1201,9 +1205,10 @@ int amr_fsk_plan_set_layout(amr_fsk_plan* plan, int layout) {
   return AMR_OK;
 }
 
-int amr_fsk_plan_split_info(const amr_fsk_plan* plan, int* last_split, int64_t* warmup, int64_t* chunk, double* kappa,
+int amr_fsk_plan_split_info(amr_fsk_plan* plan, int* last_split, int64_t* warmup, int64_t* chunk, double* kappa,
                             double* tau) {
   if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);   // run_fsk / fsk_split_params write these under it
   if (last_split) *last_split = plan->last_split ? 1 : 0;
   if (warmup) *warmup = plan->split_ok ? plan->split_w : -1;
   if (chunk) *chunk = plan->split_L;
@@ -1221,7 +1226,10 @@ int amr_fsk_split_bandpass_host(amr_fsk_plan* plan, const void* x, int dtype, in
   if (!plan->split_ok) return fail(AMR_E_INVALID, "the plan's filters have no time-split design");
   if (B > plan->max_streams || B > 65535) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
   if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
-  if (chunk < 0) return fail(AMR_E_INVALID, "chunk < 0");
+  // FS0's start states are B x 2 x ceil(m1 / L) x 48 B (outside split_reserved's
+  // L >= kFskSplitConvMinL estimate): a smaller chunk is refused
+  if (chunk < 0 || (chunk > 0 && chunk < kFskSplitConvMinL && fsk_split_conv_on(plan)))
+    return fail(AMR_E_INVALID, "amr_fsk_split_bandpass_host: chunk must be 0 (the plan's) or >= 128 with the convolution starts");
   if (B == 0) return AMR_OK;
   const int64_t n = plan->p.n;
   void* xs = nullptr;

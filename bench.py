@@ -861,7 +861,34 @@ def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
                               "kappa": sp.split_info()["kappa"],
                               "what": "time-split layout over the benchmark's noisy captures (16 per call): streams "
                                       "with a decision inside the error margin, re-run by the serial kernels"}
+    # the same with the strict margin (a per-symbol rounding bound that holds
+    # for every input) in place of kappa's measured premise
+    sp.set_split_strict(True)
+    fl, eq = 0, True
+    for s0 in range(0, nsp, 16):
+        g, _ = sp.demod_host(np.ascontiguousarray(xh[s0:s0 + 16]))
+        fl += sp.split_info()["flagged"]
+        eq &= all(g[j] == out_dev[s0 + j, :len_dev[s0 + j]].tobytes() for j in range(len(g)))
+    res["split_flag_rate"]["strict"] = {"flagged": fl, "fraction": round(fl / nsp, 5), "bytes_equal": bool(eq),
+                                        "last_strict": sp.last_strict()}
     del sp
+    # one capture at a time with the strict margin: latency and how many of
+    # the captures went to the serial kernels
+    plan1.set_split_strict(True)
+    ts, flagged, same = [], 0, True
+    for i in range(n1):
+        xi = np.ascontiguousarray(xh[i])
+        t1 = time.perf_counter()
+        r = modem.qpsk_demodulate(xi, baud=baud)
+        ts.append(time.perf_counter() - t1)
+        same &= r == out_dev[i, :len_dev[i]].tobytes()
+        flagged += max(0, plan1.split_info()["flagged"])
+    res["one_capture"]["strict"] = {"ms": round(float(np.median(ts)) * 1e3, 3), "ms_max": round(max(ts) * 1e3, 3),
+                                    "flagged_of": f"{flagged}/{n1}", "bytes_equal": bool(same),
+                                    "last_strict": plan1.last_strict(),
+                                    "what": "the same calls with AMR_PSK_SPLIT_STRICT's margin on this plan "
+                                            "(amr_psk_plan_set_split_strict): median and worst call"}
+    plan1.set_split_strict(None)
     # the same capture through the C port on one host core (the CPU side of
     # the single-capture call pattern, filebeep_advanced_v2.py:324), and where
     # the GPU drop-in overtakes one core / all host cores as the batch grows

@@ -197,7 +197,9 @@ int amr_psk_plan_last_f32f(const amr_psk_plan *plan);
 /* Diagnostic (tests): the time-split passes alone over a host batch, chunk
  * outputs per lane (0: the plan's rule) -> the symbol samples
  * sym [n_streams][n_sym][re, im] (baseband[first::sps], modem.py:92, 209, as
- * the time-split layout computes them -- not bit-exact). */
+ * the time-split layout computes them -- not bit-exact).
+ * With the convolution chunk starts on, a chunk in 1..127 is refused
+ * (AMR_E_INVALID): the start states take n_streams x m1 / chunk x 64 B. */
 int amr_psk_split_symbols_host(amr_psk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                                int64_t chunk, double *sym);
 /* The time-split band-pass's chunk start states: instead of
@@ -248,7 +250,9 @@ int amr_psk_split_bounds_host(amr_psk_plan *plan, const void *x, int dtype, int6
 int amr_psk_split_strict_design(const double *bp_b, const double *bp_a, const double *bp_zi, int bp_ntaps,
                                 const double *lp_b, const double *lp_a, const double *lp_zi, int lp_ntaps,
                                 int64_t n_samples, int64_t first, int64_t sps, double *consts, double *tabs);
-/* number of streams the exact complex low-pass path re-ran in the last call */
+/* number of streams the exact complex low-pass path re-ran in the last call
+ * (time-split layout: 0 when no stream was flagged -- the gated row kernels
+ * did not run -- else the flagged streams of the row fallback's low-pass) */
 int amr_psk_plan_exact_streams(amr_psk_plan *plan, int64_t *count);
 
 /* x: [n_streams][x_stride] samples of `dtype`; out: [n_streams][out_stride]
@@ -399,13 +403,13 @@ int amr_fsk_envelopes_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t
 /* 1 when the plan's time-split F1 starts its chunks from convolution states
  * (FS0, amr_split_state_tables per tone) rather than warm-ups
  * (AMR_FSK_SPLIT_CONV=0), 0 when not (or no split design), -1 for NULL. */
-int amr_fsk_plan_split_conv(const amr_fsk_plan *plan);
+int amr_fsk_plan_split_conv(amr_fsk_plan *plan);
 int amr_fsk_plan_set_layout(amr_fsk_plan *plan, int layout);
 /* the last call's F1 (*last_split 1: split) and the plan's split design:
  * warm-up samples, chunk length of the last split call, kappa, and tau (F2's
  * margin scale for split calls).  Any pointer may be NULL; *warmup = -1 when
  * the plan cannot split. */
-int amr_fsk_plan_split_info(const amr_fsk_plan *plan, int *last_split, int64_t *warmup, int64_t *chunk,
+int amr_fsk_plan_split_info(amr_fsk_plan *plan, int *last_split, int64_t *warmup, int64_t *chunk,
                             double *kappa, double *tau);
 /* the split design from the filters alone (host arithmetic; no device):
  * warm-up, kappa and ||ifft(h)||_1 of scipy.signal.hilbert's multiplier h at
@@ -414,7 +418,8 @@ int amr_fsk_split_design(int64_t n_samples, const double *mark_b, const double *
                          const double *space_a, int ntaps, int64_t *warmup, double *kappa, double *hilbert_l1);
 /* the split F1's band-pass output itself (a diagnostic the tests compare with
  * the oracle's restatement): out [n_streams][n_samples][2] (mark, space);
- * chunk 0 = the plan's rule.  Synchronous. */
+ * chunk 0 = the plan's rule (1..127 refused with the convolution starts on,
+ * as amr_psk_split_symbols_host).  Synchronous. */
 int amr_fsk_split_bandpass_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
                                 int64_t chunk, double *out);
 

@@ -35,7 +35,7 @@ def _cast(x, dtype):
 
 @pytest.mark.parametrize("n,baud,mark,space,dtype,chunk", [
     (96000, 9600, 12000.0, 24000.0, np.float32, 0),
-    (96000, 9600, 12000.0, 24000.0, np.float64, 97),
+    (96000, 9600, 12000.0, 24000.0, np.float64, 193),
     (50001, 4800, 7000.0, 19000.0, np.float64, 0),     # Bluestein length
     (30000, 2400, 11229.28, 29833.37, np.int16, 333),
     (96000, 1200, 2400.0, 4800.0, np.float64, 0),

@@ -47,7 +47,7 @@ def gpu(built_lib):
 
 @pytest.mark.parametrize("kind,baud,fc,fs,n,dtype,chunk", [
     ("qpsk", 9600, 3000.0, 96000, 96000, np.float32, 0),
-    ("qpsk", 9600, 3000.0, 96000, 96000, np.float64, 97),
+    ("qpsk", 9600, 3000.0, 96000, 96000, np.float64, 193),
     ("qpsk", 19200, 3000.0, 96000, 50001, np.int16, 0),
     ("bpsk", 1200, 3000.0, 96000, 48000, np.float32, 333),
     ("qpsk", 1000, 3000.0, 48000, 40000, np.float64, 0),
@@ -219,9 +219,34 @@ def test_split_flags_silence_and_special_values():
     want, ws = oracle.psk_demod_batch("qpsk", x, 9600)
     assert got == want and np.array_equal(gs, ws)
     assert pl.split_info()["flagged"] >= 5
+    assert pl.exact_streams() >= 0
     clean = synth.qpsk_batch(B, n, 9600, seed=9, distinct=B, noise=0.05)
     pl.demod_host(clean)
     assert pl.split_info()["flagged"] == 0
+    # nothing flagged: the gated row fallback (and its exact low-pass) did not run
+    assert pl.exact_streams() == 0
+
+
+def test_split_diagnostics_refuse_tiny_chunks():
+    """With the convolution chunk starts on, a diagnostic chunk of 1..127
+    outputs is refused (its start states would take B m1 / L x 64 B); 0 and
+    >= 128 run."""
+    import _amr
+    import _fsk
+    import synth
+    n = 48000
+    x = synth.qpsk_batch(2, n, 9600, seed=4, distinct=2)
+    pl = _amr.PskPlan("qpsk", n, 9600, max_streams=2)
+    if pl.split_conv():
+        with pytest.raises(_amr.AmrError):
+            pl.split_symbols(x, 1)
+    assert pl.split_symbols(x, 128).shape[0] == 2
+    xf = synth.fsk_batch(2, n, 9600, 12000.0, 24000.0, seed=4, distinct=2)
+    fp = _fsk.FskPlan(n, 9600, 12000.0, 24000.0, max_streams=2)
+    if fp.split_conv():
+        with pytest.raises(_amr.AmrError):
+            fp.split_bandpass(xf, 64)
+    assert fp.split_bandpass(xf, 128).shape[0] == 2
 
 
 def test_split_flag_rate_on_benchmark_captures():
