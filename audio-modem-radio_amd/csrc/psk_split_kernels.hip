@@ -27,7 +27,7 @@
 //     principle exceed E, and an unflagged decision could then differ.
 //   * STRICT (AMR_PSK_SPLIT_STRICT=1 / amr_psk_plan_set_split_strict): KS1 /
 //     KS2 also accumulate per-block rounding bounds of every step, and KB
-//     (k_split_strict_bound) turns them into a per-symbol bound e(k) that
+//     (KB1-KB4, k_split_strict_*) turn them into a per-symbol bound e(k) that
 //     holds for every input (a forward error analysis of the DF-II-T chain,
 //     csrc/split_strict.h; a pass whose error exceeds 2^-10 of its input's
 //     peak flags the stream instead).  E = e(k) then, and the margin below is
@@ -52,8 +52,9 @@
 //   KS2 k_split_bp_bwd   y1 reversed -> f [B][n]
 //   KS3 k_split_lp_fwd   lane = (chunk, component): f * lo, odd ext -> y3 [B][2][m2]
 //   KS4 k_split_lp_bwd   y3 reversed -> symbol samples sym [B][S][2]
-//   KB  k_split_strict_bound (strict mode only) workgroup = stream: the
-//                        block step bounds -> per-symbol bound e [B][S]
+//   KB1-KB4 k_split_strict_e1 / _e2 / _x / _e (strict mode only; thread =
+//                        (block or symbol, stream)): the block step bounds ->
+//                        per-symbol bound e [B][S]
 //   KS5 k_split_slice    thread = (stream, word): numpy's fma differential
 //                        product, the sector / sign decision, the margin
 //                        check -> words, flag, count
@@ -382,87 +383,123 @@ __global__ __launch_bounds__(64) void k_split_lp_bwd(PskBuffers buf, PskParams p
       });
 }
 
-// KB (STRICT; split_strict.h): one workgroup per stream turns KS0-KS2's
-// per-block step bounds and per-chunk start bounds into a bound e(k) on each
-// symbol component's |split - reference|:
-//   E1[J]  the forward pass, output block J: the split's and the serial's
-//          rounding (block sums of D through W, the cut remainder at max D),
-//          the chunk starts' errors (+ truncation tk * peak) through GS
-//   E2[J]  the backward pass at forward block J: the forward rounding through
-//          the backward pass (K12, exact at block resolution), the start
-//          errors through |h| (HS), the last input's error through the zi
-//          start (TZ), its own rounding and starts (in its own block index)
-//   X[fb]  the mixer's output error over sample block fb
-//   e(k)   lpc[k] x the largest X within the low-pass's reach of symbol k (and
-//          the extension's source blocks), + the cut remainder, + c3 P3
+// KB (STRICT; split_strict.h): four grid-wide stages (grid = block tiles x
+// streams; the per-stream maxima meet in bnd's free slots by atomicMax) turn
+// KS0-KS2's per-block step bounds and per-chunk start bounds into a bound e(k)
+// on each symbol component's |split - reference|:
+//   KB1 E1[J]  the forward pass, output block J: the split's and the serial's
+//              rounding (block sums of D through W, the cut remainder at max D),
+//              the chunk starts' errors (+ truncation tk * peak) through GS
+//   KB2 E2[J]  the backward pass at forward block J: the forward rounding
+//              through the backward pass (K12, exact at block resolution), the
+//              start errors through |h| (HS), the last input's error through the
+//              zi start (TZ), its own rounding and starts (in its own block index)
+//   KB3 X[fb]  the mixer's output error over sample block fb
+//   KB4 e(k)   lpc[k] x the largest X within the low-pass's reach of symbol k
+//              (and the extension's source blocks), + the cut remainder, + c3 P3
 // The serial's rounding is the split's within the a-posteriori caps (each
 // pass's difference <= 2^-10 of its input peak; a stream past them gets e =
 // inf: flagged).  Every sum is of non-negative terms; the final factor
-// 1 + 2^-30 covers their own rounding.
+// 1 + 2^-30 covers their own rounding.  (Round 6's first cut ran all four in
+// one workgroup per stream: 1.05 ms of a 1.4 ms strict one-capture call.)
 __device__ __forceinline__ double bnd_get(const unsigned long long* b, int i) {
   return __longlong_as_double((long long)b[i]);
 }
-__device__ __forceinline__ void lds_max(unsigned long long* m, double v) {
-  atomicMax(m, (unsigned long long)__double_as_longlong(fabs(v)));
-}
 constexpr int kKbThreads = 256;
-__global__ __launch_bounds__(kKbThreads) void k_split_strict_bound(PskParams p, PskSplit sp) {
-  const int64_t s = blockIdx.x;
-  double* __restrict__ sc = sp.sc + s * sp.sstride;
-  const double* d1 = sc + strict_off_d1(sp);
-  const double* d2 = sc + strict_off_d2(sp);
-  const double* ds1 = sc + strict_off_ds1(sp);
-  const double* ds2 = sc + strict_off_ds2(sp);
-  double* e1 = sc + strict_off_e1(sp);
-  double* s1 = sc + strict_off_s1(sp);
-  double* e2 = sc + strict_off_e2(sp);
-  double* xb = sc + strict_off_x(sp);
-  double* eo = sc + strict_off_e(sp);
-  __shared__ unsigned long long red[4];   // max E1, max S1, max E2 (F), max X
-  if (threadIdx.x < 4) red[threadIdx.x] = 0ull;
-  const unsigned long long* b = sp.bnd + s * 8;
-  const double D1m = bnd_get(b, 0), y1m = bnd_get(b, 2), D2m = bnd_get(b, 3), fm0 = bnd_get(b, 5);
-  const double peak1 = __longlong_as_double((long long)sp.peak[s]);
-  const double u = 0x1p-53, eta = 0x1p-1060, two = 2.0 + 0x1p-20;
-  const int64_t nb1 = sp.nb1, nbs = sp.nbs, m1 = p.m1, n = p.n, LB = sp.L / kStrictBlk;
-  const int pad1 = p.pad1, pad2 = p.pad2;
-  const double cap1 = 0x1p-10 * peak1, p2 = y1m + cap1, cap2 = 0x1p-10 * p2;
-  const double sec1 = sp.u2 * sp.zb * cap1 + sp.ky * cap1;
+// bnd slots: 0 D1max, 1 E1max (KB1), 2 max|y1|, 3 D2max, 4 S1max (KB1),
+// 5 max|f|, 6 Fmax (KB2), 7 Xmax (KB3)
+struct KbStream {
+  double* sc;
+  const unsigned long long* b;
+  unsigned long long* bw;
+  double D1m, y1m, D2m, fm0, peak1, cap1, p2, cap2, c1;
+};
+__device__ __forceinline__ KbStream kb_stream(const PskSplit& sp, int64_t s) {
+  KbStream k;
+  k.sc = sp.sc + s * sp.sstride;
+  k.bw = sp.bnd + s * 8;
+  k.b = k.bw;
+  k.D1m = bnd_get(k.b, 0);
+  k.y1m = bnd_get(k.b, 2);
+  k.D2m = bnd_get(k.b, 3);
+  k.fm0 = bnd_get(k.b, 5);
+  k.peak1 = __longlong_as_double((long long)sp.peak[s]);
+  k.cap1 = 0x1p-10 * k.peak1;
+  k.p2 = k.y1m + k.cap1;
+  k.cap2 = 0x1p-10 * k.p2;
+  const double sec1 = sp.u2 * sp.zb * k.cap1 + sp.ky * k.cap1;
   // the forward pass's per-stream terms (besides the block sums)
-  const double c1 = sp.g1x * (sec1 + 2 * eta) + sp.gmax * u * sp.zi_sum * peak1;
-  __syncthreads();
-  for (int64_t J = threadIdx.x; J < nb1; J += kKbThreads) {
-    double r = sp.w_tail * D1m;
+  k.c1 = sp.g1x * (sec1 + 2 * 0x1p-1060) + sp.gmax * 0x1p-53 * sp.zi_sum * k.peak1;
+  return k;
+}
+// a wave's maximum of non-negative v into *m (one atomic per wave)
+__device__ __forceinline__ void wave_max_to(unsigned long long* m, double v, bool live) {
+  unsigned long long x = live ? (unsigned long long)__double_as_longlong(fabs(v)) : 0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(x, o);
+    x = y > x ? y : x;
+  }
+  if ((threadIdx.x & 63) == 0 && x != 0ull) atomicMax(m, x);
+}
+constexpr double kKbTwo = 2.0 + 0x1p-20;
+
+__global__ __launch_bounds__(kKbThreads) void k_split_strict_e1(PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t J = (int64_t)blockIdx.x * kKbThreads + threadIdx.x;
+  const KbStream k = kb_stream(sp, s);
+  const int64_t nb1 = sp.nb1, LB = sp.L / kStrictBlk;
+  const double* d1 = k.sc + strict_off_d1(sp);
+  const double* ds1 = k.sc + strict_off_ds1(sp);
+  double e = 0.0, st = 0.0;
+  const bool live = J < nb1;
+  if (live) {
+    double r = sp.w_tail * k.D1m;
     const int64_t dn = J + 1 < sp.nw ? J + 1 : sp.nw;
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d1[J - dl], r);
     const int64_t c = J / LB;
     const int64_t q = J - c * LB;
-    const double st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds1[c] + sp.tk * peak1) : 0.0;
-    s1[J] = st;
-    e1[J] = two * r + c1 + st;
-    lds_max(&red[0], e1[J]);
-    lds_max(&red[1], st);
+    st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds1[c] + sp.tk * k.peak1) : 0.0;
+    e = kKbTwo * r + k.c1 + st;
+    k.sc[strict_off_s1(sp) + J] = st;
+    k.sc[strict_off_e1(sp) + J] = e;
   }
-  __syncthreads();
-  const double E1max = __longlong_as_double((long long)red[0]), S1max = __longlong_as_double((long long)red[1]);
+  (void)p;
+  wave_max_to(k.bw + 1, e, live);
+  wave_max_to(k.bw + 4, st, live);
+}
+
+__global__ __launch_bounds__(kKbThreads) void k_split_strict_e2(PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t J = (int64_t)blockIdx.x * kKbThreads + threadIdx.x;
+  const KbStream k = kb_stream(sp, s);
+  const int64_t nb1 = sp.nb1, m1 = p.m1, LB = sp.L / kStrictBlk;
+  const double* d1 = k.sc + strict_off_d1(sp);
+  const double* d2 = k.sc + strict_off_d2(sp);
+  const double* ds2 = k.sc + strict_off_ds2(sp);
+  const double* e1 = k.sc + strict_off_e1(sp);
+  const double* s1 = k.sc + strict_off_s1(sp);
+  const double E1max = bnd_get(k.b, 1), S1max = bnd_get(k.b, 4);
   const double E1last = fmax(e1[nb1 - 1], nb1 > 1 ? e1[nb1 - 2] : 0.0);
-  const double sec2 = sp.u2 * sp.zb * cap2 + sp.kx * E1max + sp.ky * cap2;
-  const double c2 = sp.hz * c1 + sp.g1x * (sec2 + 2 * eta) + 2.0 * sp.gmax * u * sp.zi_sum * p2;
+  const double sec2 = sp.u2 * sp.zb * k.cap2 + sp.kx * E1max + sp.ky * k.cap2;
+  const double c2 = sp.hz * k.c1 + sp.g1x * (sec2 + 2 * 0x1p-1060) + 2.0 * sp.gmax * 0x1p-53 * sp.zi_sum * k.p2;
   // the backward pass's own rounding and starts at its block K (its own index)
   auto own2 = [&](int64_t K) {
     if (K < 0 || K >= nb1) return 0.0;
-    double r = sp.w_tail * D2m;
+    double r = sp.w_tail * k.D2m;
     const int64_t dn = K + 1 < sp.nw ? K + 1 : sp.nw;
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d2[K - dl], r);
     const int64_t c = K / LB;
     const int64_t q = K - c * LB;
-    const double st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds2[c] + sp.tk * p2) : 0.0;
-    return two * r + st;
+    const double st = c > 0 ? (q < 64 ? sp.kGS[q] : sp.gmax) * (ds2[c] + sp.tk * k.p2) : 0.0;
+    return kKbTwo * r + st;
   };
   auto tzw = [&](int64_t q) { return q < sp.nz ? sp.kTZ[q] : sp.tz_tail; };
-  for (int64_t J = threadIdx.x; J < nb1; J += kKbThreads) {
+  double e = 0.0;
+  const bool live = J < nb1;
+  if (live) {
     // forward block J: j in [16 J, 16 J + 15] <-> backward index k2 = m1 - 1 - j
-    double a = sp.k12_tail * D1m;
+    double a = sp.k12_tail * k.D1m;
     for (int64_t kq = 0; kq < sp.nk; ++kq) {
       const int64_t bb = J + kq - sp.k12_off;
       if (bb >= 0 && bb < nb1) a = __builtin_fma(sp.kK12[kq], d1[bb], a);
@@ -474,34 +511,52 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_bound(PskParams p, 
     const int64_t Ka = k2lo / kStrictBlk, Kb = k2hi / kStrictBlk;
     const double tz = fmax(tzw(Ka), tzw(Kb)) * E1last;
     const double o2 = fmax(own2(Ka), own2(Kb));
-    e2[J] = two * a + h + tz + o2 + c2;
-    lds_max(&red[2], e2[J]);
+    e = kKbTwo * a + h + tz + o2 + c2;
+    k.sc[strict_off_e2(sp) + J] = e;
   }
-  __syncthreads();
-  const double Fmax = __longlong_as_double((long long)red[2]);
-  const double fm = fm0 + Fmax;
-  for (int64_t fb = threadIdx.x; fb < nbs; fb += kKbThreads) {
+  wave_max_to(k.bw + 6, e, live);
+}
+
+__global__ __launch_bounds__(kKbThreads) void k_split_strict_x(PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t fb = (int64_t)blockIdx.x * kKbThreads + threadIdx.x;
+  const KbStream k = kb_stream(sp, s);
+  const int64_t n = p.n;
+  const double* e2 = k.sc + strict_off_e2(sp);
+  const double fm = k.fm0 + bnd_get(k.b, 6);
+  double x = 0.0;
+  const bool live = fb < sp.nbs;
+  if (live) {
     const int64_t ilo = 16 * fb, ihi = 16 * fb + 15 < n - 1 ? 16 * fb + 15 : n - 1;
-    const double F = fmax(e2[(ilo + pad1) / kStrictBlk], e2[(ihi + pad1) / kStrictBlk]);
-    xb[fb] = F * (1.0 + 0x1p-50) + 0x1.02p-52 * fm;
-    lds_max(&red[3], xb[fb]);
+    const double F = fmax(e2[(ilo + p.pad1) / kStrictBlk], e2[(ihi + p.pad1) / kStrictBlk]);
+    x = F * (1.0 + 0x1p-50) + 0x1.02p-52 * fm;
+    k.sc[strict_off_x(sp) + fb] = x;
   }
-  __syncthreads();
-  const double Xmax = __longlong_as_double((long long)red[3]);
+  wave_max_to(k.bw + 7, x, live);
+}
+
+__global__ __launch_bounds__(kKbThreads) void k_split_strict_e(PskParams p, PskSplit sp) {
+  const int64_t s = blockIdx.y;
+  const int64_t kk = (int64_t)blockIdx.x * kKbThreads + threadIdx.x;
+  const KbStream k = kb_stream(sp, s);
+  const int64_t n = p.n, nbs = sp.nbs, S = p.n_sym;
+  const double* xb = k.sc + strict_off_x(sp);
+  double* eo = k.sc + strict_off_e(sp);
+  const double E1max = bnd_get(k.b, 1), Fmax = bnd_get(k.b, 6), Xmax = bnd_get(k.b, 7);
+  const double fm = k.fm0 + Fmax;
   const double P3 = 3.0 * (fm + Xmax);
-  const bool ok = E1max <= cap1 && Fmax <= cap2;      // false for NaN
-  const int64_t S = p.n_sym;
-  const double tailc = sp.lp_tail * Xmax + sp.c3 * P3;
-  for (int64_t k = threadIdx.x; k < S; k += kKbThreads) {
-    const int64_t t = p.first + k * p.sps;
-    const int64_t lo = t - sp.lp_rad - pad2, hi = t + sp.lp_rad + pad2;
+  const bool ok = E1max <= k.cap1 && Fmax <= k.cap2;      // false for NaN
+  if (kk < S) {
+    const double tailc = sp.lp_tail * Xmax + sp.c3 * P3;
+    const int64_t t = p.first + kk * p.sps;
+    const int64_t lo = t - sp.lp_rad - p.pad2, hi = t + sp.lp_rad + p.pad2;
     const int64_t flo = lo > 0 ? lo / kStrictBlk : 0, fhi = (hi < n - 1 ? hi : n - 1) / kStrictBlk;
     double xw = fmax(xb[0], xb[nbs - 1]);
     for (int64_t fb = flo; fb <= fhi; ++fb) xw = fmax(xw, xb[fb]);
-    const double e = (1.0 + 0x1p-30) * __builtin_fma(sp.lpc[k], xw, tailc);
-    eo[k] = ok ? e : __builtin_inf();
+    const double e = (1.0 + 0x1p-30) * __builtin_fma(sp.lpc[kk], xw, tailc);
+    eo[kk] = ok ? e : __builtin_inf();
   }
-  if (threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     double* scal = eo + S;
     scal[0] = E1max;
     scal[1] = Fmax;
@@ -647,7 +702,11 @@ hipError_t launch_psk_split_slice(const PskBuffers& b, const PskParams& p, const
   const dim3 blk(64), g5((unsigned)((p.n_words + 63) / 64), (unsigned)B);
   if (sp.strict) {
     if (!sp.sc || sp.L % kStrictBlk != 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_strict_bound, dim3((unsigned)B), dim3(kKbThreads), 0, st, p, sp);
+    auto g = [&](int64_t units) { return dim3((unsigned)((units + kKbThreads - 1) / kKbThreads), (unsigned)B); };
+    hipLaunchKernelGGL(k_split_strict_e1, g(sp.nb1), dim3(kKbThreads), 0, st, p, sp);
+    hipLaunchKernelGGL(k_split_strict_e2, g(sp.nb1), dim3(kKbThreads), 0, st, p, sp);
+    hipLaunchKernelGGL(k_split_strict_x, g(sp.nbs), dim3(kKbThreads), 0, st, p, sp);
+    hipLaunchKernelGGL(k_split_strict_e, g(p.n_sym), dim3(kKbThreads), 0, st, p, sp);
   }
   hipLaunchKernelGGL(k_split_slice, g5, blk, 0, st, b, p, sp);
   return hipGetLastError();
