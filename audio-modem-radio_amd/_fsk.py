@@ -60,7 +60,20 @@ def split_design(n: int, baud, mark_freq, space_freq, samp_rate=96000):
                                     ctypes.byref(k), ctypes.byref(h))
     if rc != 0:
         return None
-    return {"warmup": w.value, "kappa": k.value, "hilbert_l1": h.value, "tau": 2.0 ** -36 + k.value * h.value}
+    m = fft_margin(n, baud, mark_freq, space_freq, samp_rate)
+    return {"warmup": w.value, "kappa": k.value, "hilbert_l1": h.value, "tau": m["tau"] + k.value * h.value}
+
+
+def fft_margin(n: int, baud, mark_freq, space_freq, samp_rate=96000):
+    """F2's margin scale from a standard FFT rounding bound (host arithmetic
+    in libamr.so, no device; include/amr.h amr_fsk_fft_margin): dict of tau,
+    eps_fast, eps_ref, zmax (the bound on max_t ||z_t||_2 / peak|ext x|),
+    fast_blue, fast_M, ref_blue, ref_M."""
+    _, ((mb, ma, mz), (sb, sa, sz)) = design_fsk(n, baud, mark_freq, space_freq, samp_rate)
+    out = np.zeros(8)
+    check(lib().amr_fsk_fft_margin(int(n), ptr(mb), ptr(ma), ptr(mz), ptr(sb), ptr(sa), ptr(sz), len(mb), ptr(out)))
+    return {"tau": out[0], "eps_fast": out[1], "eps_ref": out[2], "zmax": out[3], "fast_blue": bool(out[4]),
+            "fast_M": int(out[5]), "ref_blue": bool(out[6]), "ref_M": int(out[7])}
 
 
 class FskPlan:
@@ -185,6 +198,12 @@ class FskPlan:
         check(lib().amr_fsk_plan_split_info(self.handle, ctypes.byref(ls), ctypes.byref(w), ctypes.byref(L),
                                             ctypes.byref(k), ctypes.byref(t)))
         return {"last_split": bool(ls.value), "warmup": w.value, "chunk": L.value, "kappa": k.value, "tau": t.value}
+
+    def margin(self) -> dict:
+        """F2's margin scales of this plan: tau (serial F1) and tau_split."""
+        t, ts = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        check(lib().amr_fsk_plan_margin(self.handle, ctypes.byref(t), ctypes.byref(ts)))
+        return {"tau": t.value, "tau_split": ts.value}
 
     def split_bandpass(self, x: np.ndarray, chunk: int = 0) -> np.ndarray:
         """The split F1's output [B][n][2] (mark, space): a diagnostic."""

@@ -217,14 +217,17 @@ struct FskParams {
   const int32_t* xlist;   // F1 list mode (the exact path): z row r <- x row xlist[r], r < *xcount
   const int32_t* xcount;
   const double* edge;     // the odd extension as the caller's dtype formed it (odd_ext.h): [B][2 * pad] or null
+  double tau;             // F2's margin scale (fsk_api.cpp fsk_fft_bound: >= kAmbTau, a standard FFT bound)
 };
 
 // F2's ambiguity margin: |env_mark - env_space| <= 2 tau peak|x| is within
 // reach of the fast path's and pocketfft's rounding.
 // F1 computes scipy's filtfilt bit for bit, so the envelopes differ from the
 // reference's by the two FFTs' rounding alone: measured <= 4.3e-15 peak|x|
-// (two-pass and Bluestein lengths, 300-9600 Bd); tau = 2^-36 ~ 1.5e-11 is
-// >= 3000 times that (tests/test_gpu_fsk.py::test_envelope_error_is_far_below_the_margin)
+// (two-pass and Bluestein lengths, 300-9600 Bd).  A plan's tau (FskParams::tau)
+// is the larger of kAmbTau = 2^-36 (>= 3000 times the measured difference)
+// and a standard FFT rounding bound for its length and filters (fsk_api.cpp
+// fsk_fft_bound, round 6: ~13 x 2^-36 at n = 96000)
 constexpr double kAmbTau = 0x1p-36;
 // c = 8 (tau peak)^2 (fft_kernels.hip env_ambiguous compares squares);
 // -1 for a stream of exact zeros (both paths' envelopes are exact zeros),

@@ -983,9 +983,126 @@ bool fsk_split_design(const FskIir& f, int nt, int64_t n, int64_t* w_out, double
   return true;
 }
 
+// F2's margin scale tau from a standard FFT rounding bound (round 6, DESIGN.md
+// §2 item 6).  F2 keeps a compare only when |env_mark - env_space| > 2 tau
+// peak|ext x|; the fast path's and pocketfft's envelopes each differ from
+// |hilbert(z)| in exact arithmetic by at most (4 eps + 4u) ||z||_2 per tone,
+// eps the transform's relative 2-norm error:
+//   direct (FFTPACK-style / two-pass / six-step) length M, widest radix p:
+//     eps = L eta / (1 - L eta), L = ceil(log2 M), eta = max(8.5u, sqrt(p)
+//     gamma_{p+4} / log2 p) + 2u (a radix-p pass's 2-norm error per binary
+//     level -- Higham's radix-2 eta = mu + gamma_4 (sqrt2 + mu) generalised --
+//     plus twiddles within 2u);
+//   Bluestein (n, M): (2n - 1) / sqrt(n) (3 eps_M + 2 gc) + gc, gc = sqrt2
+//     gamma_2 + 2u (the chirp products; 2n - 1 = ||chirp||_1 bounds its
+//     spectrum's peak);
+// and ||z||_2 <= (G^2 sqrt(m1) + 2 G R + R^2) peak|ext x| per tone (G the
+// band-pass's L1 gain, R the L2 norm of its zi-start transient: both
+// filtfilt passes).  tau = max(2^-36, (4 eps_fast + 4 eps_ref + 8u) max
+// ||z||_2 / peak): a compare F2 keeps cannot differ between the two paths.
+// ~13 x 2^-36 at n = 96000 (the measured difference stays ~1e-15 of the
+// peak, tests/test_gpu_fsk.py); the flag rate of real signals is unchanged.
+struct FskFftBound {
+  double tau = 0.0, eps_fast = 0.0, eps_ref = 0.0, zmax = 0.0;
+  bool fast_blue = false, ref_blue = false;
+  int64_t fast_M = 0, ref_M = 0;
+};
+int64_t lpf_of(int64_t n) {
+  int64_t r = 1;
+  for (int64_t q = 2; q * q <= n; ++q)
+    while (n % q == 0) {
+      r = q;
+      n /= q;
+    }
+  return n > 1 ? std::max(r, n) : r;
+}
+bool fsk_fft_bound(const FskIir& f, int nt, int64_t n, int pad, FskFftBound& o) {
+  const double u = 0x1p-53;
+  auto gam = [&](double k) { return k * u / (1.0 - k * u); };
+  auto eta_of = [&](int64_t p) {
+    const double r = (double)std::max<int64_t>(p, 2);
+    return std::max(8.5 * u, std::sqrt(r) * gam(r + 4.0) / std::max(1.0, std::log2(r))) + 2.0 * u;
+  };
+  auto eps_direct = [&](int64_t M, int64_t p) {
+    const double e = std::ceil(std::log2((double)std::max<int64_t>(M, 2))) * eta_of(p);
+    return e / (1.0 - e);
+  };
+  const double gc = std::sqrt(2.0) * gam(2.0) + 2.0 * u;
+  auto eps_blue = [&](int64_t M) {
+    return (2.0 * (double)n - 1.0) / std::sqrt((double)n) * (3.0 * eps_direct(M, lpf_of(M)) + 2.0 * gc) + gc;
+  };
+  FftShape sh;
+  if (!fft_shape(n, sh)) return false;
+  bool rb = false;
+  int64_t rn2 = n, rp = 1;
+  pf_hilbert_shape(n, &rb, &rn2, &rp);
+  o.fast_blue = sh.bluestein;
+  o.fast_M = sh.M;
+  o.ref_blue = rb;
+  o.ref_M = rn2;
+  o.eps_fast = sh.bluestein ? eps_blue(sh.M) : eps_direct(n, lpf_of(n));
+  o.eps_ref = rb ? eps_blue(rn2) : eps_direct(n, rp);
+  const double m1 = (double)(n + 2 * (int64_t)pad);
+  double zb = 0.0;
+  for (int t = 0; t < 2; ++t) {
+    Iir fi{};
+    fi.nt = nt;
+    for (int i = 0; i < nt; ++i) {
+      fi.b[i] = f.b[t][i];
+      fi.a[i] = f.a[t][i];
+    }
+    for (int i = 0; i < nt - 1; ++i) fi.zi[i] = f.zi[t][i];
+    const IirGains g = iir_gains(fi);
+    const double R = zi_response_l2(fi);
+    if (!g.ok || !(R >= 0.0)) return false;
+    const double G = g.h1 * (1.0 + 0x1p-20);
+    zb = std::max(zb, G * G * std::sqrt(m1) + 2.0 * G * R + R * R);
+  }
+  o.zmax = zb;
+  const double tau = (4.0 * o.eps_fast + 4.0 * o.eps_ref + 8.0 * u) * zb * (1.0 + 0x1p-20);
+  o.tau = std::max(kAmbTau, tau);
+  return std::isfinite(o.tau);
+}
+
 }  // namespace
 
 extern "C" {
+
+int amr_fsk_fft_margin(int64_t n, const double* mb, const double* ma, const double* mzi, const double* sb,
+                       const double* sa, const double* szi, int nt, double* out) {
+  if (!mb || !ma || !mzi || !sb || !sa || !szi || !out || nt < 2 || nt > 8 || n <= 3 * nt)
+    return fail(AMR_E_INVALID, "amr_fsk_fft_margin: bad argument");
+  FskIir f{};
+  for (int i = 0; i < nt; ++i) {
+    f.b[0][i] = mb[i];
+    f.a[0][i] = ma[i];
+    f.b[1][i] = sb[i];
+    f.a[1][i] = sa[i];
+  }
+  for (int i = 0; i < nt - 1; ++i) {
+    f.zi[0][i] = mzi[i];
+    f.zi[1][i] = szi[i];
+  }
+  FskFftBound o;
+  if (!fsk_fft_bound(f, nt, n, 3 * nt, o)) return fail(AMR_E_INVALID, "amr_fsk_fft_margin: no bound for these filters at n");
+  out[0] = o.tau;
+  out[1] = o.eps_fast;
+  out[2] = o.eps_ref;
+  out[3] = o.zmax;
+  out[4] = o.fast_blue ? 1.0 : 0.0;
+  out[5] = (double)o.fast_M;
+  out[6] = o.ref_blue ? 1.0 : 0.0;
+  out[7] = (double)o.ref_M;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_margin(amr_fsk_plan* plan, double* tau, double* tau_split) {
+  if (!plan) return fail(AMR_E_INVALID, "plan is NULL");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  if (tau) *tau = plan->p.tau;
+  if (tau_split) *tau_split = plan->split_tau;
+  return AMR_OK;
+}
 
 int amr_fsk_split_design(int64_t n, const double* mb, const double* ma, const double* sb, const double* sa, int nt,
                          int64_t* warmup, double* kappa, double* hilbert_l1_out) {
@@ -1146,11 +1263,17 @@ int amr_fsk_plan_create(amr_fsk_plan** out, int device, int64_t n, int64_t sps, 
     }
   }
   {
+    FskFftBound fb;
+    if (!fsk_fft_bound(pl->f, nt, n, p.pad, fb)) {
+      fsk_plan_free(pl);
+      return fail(AMR_E_INVALID, "no FFT rounding bound for these filters at length " + std::to_string(n));
+    }
+    p.tau = fb.tau;
     double kappa = 0.0, hl1 = 0.0;
     pl->split_ok = fsk_split_design(pl->f, nt, n, &pl->split_w, &kappa, &hl1);
     pl->split_kappa = kappa;
     pl->split_hl1 = hl1;
-    pl->split_tau = kAmbTau + kappa * hl1;
+    pl->split_tau = p.tau + kappa * hl1;
     if (pl->split_ok) {   // FS0's tables, per tone: K [w][6], then Z0 [w + 1][6]
       const int64_t w = pl->split_w;
       pl->split_tab_host.assign((size_t)(2 * w + 2 * (w + 1)) * 6, 0.0);

@@ -247,7 +247,7 @@ __global__ __launch_bounds__(64) void k_fsk_bandpass(const void* xv, int64_t x_s
   }
   if constexpr (AMB) {
     if (tone == 0 && s < n_streams)
-      p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)));
+      p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)), p.tau);
     if (lane == 0) p.xflags[w] = 0u;
   }
   double ylast = 0.0;
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(128) void k_fsk_bandpass2(const void* xv, int64_t x
     if constexpr (AMB) {
       // this batch's margin scale, and the group's flag word cleared for F2
       if (tone == 0 && s < ns)
-        p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)));
+        p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(ox.peak_with_tab(PeakT<T>::peak(pk_hi, pk_lo)), p.tau);
       if (lane == 0) p.xflags[w] = 0u;
     }
     double yl = 0.0;

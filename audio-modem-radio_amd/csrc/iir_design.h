@@ -67,6 +67,25 @@ inline IirGains iir_gains(const Iir& f) {
   r.ok = decayed && std::isfinite(r.h1) && std::isfinite(r.zmax);
   return r;
 }
+// ||y||_2 of the DF-II-T's output with zero input from scipy's zi state (the
+// transient a filtfilt pass's zi * x0 start adds per unit x0), in long
+// double; -1 if it has not decayed within the step limit
+inline double zi_response_l2(const Iir& f) {
+  const int N = f.nt - 1;
+  long double z[8] = {0};
+  for (int i = 0; i < N; ++i) z[i] = f.zi[i];
+  long double s2 = 0.0L;
+  for (int64_t m = 0; m < 4000000; ++m) {
+    const long double y = z[0];
+    for (int j = 0; j < N - 1; ++j) z[j] = z[j + 1] - (long double)f.a[j + 1] * y;
+    z[N - 1] = -(long double)f.a[N] * y;
+    s2 += y * y;
+    long double live = 0.0L;
+    for (int j = 0; j < N; ++j) live = std::max(live, std::fabs(z[j]));
+    if (live < 1e-40L && m > 4 * N) return (double)std::sqrt(s2) * (1.0 + 0x1p-30);
+  }
+  return -1.0;
+}
 // the first m with tail(m) * scale <= tol (-1: none within the response)
 inline int64_t warmup_for(const IirGains& g, double scale, double tol) {
   for (size_t m = 0; m < g.tail.size(); ++m)

@@ -143,6 +143,12 @@ struct PfLen {
   PfBlue bl;
 };
 
+// the shape of pocketfft's transforms for scipy.signal.hilbert at length n
+// (its real forward and complex inverse FFT): whether either runs Bluestein,
+// the length it then transforms (n otherwise) and that length's largest
+// prime factor (the widest radix pass) -- for F2's FFT rounding bound
+void pf_hilbert_shape(int64_t n, bool* blue, int64_t* n2, int64_t* maxp);
+
 // AMR_PF_FUSE=0 (A/B switch): run the complex transforms pass by pass
 // instead of through the LDS-fused groups; default on
 bool pf_fuse_on();

@@ -446,6 +446,14 @@ bool build_blue(int64_t n, PfBlue& B, std::vector<double>& pool) {
 
 }  // namespace
 
+void pf_hilbert_shape(int64_t n, bool* blue, int64_t* n2, int64_t* maxp) {
+  const bool b = use_bluestein(n, true) || use_bluestein(n, false);
+  const int64_t m = b ? good_size_cmplx(2 * n - 1) : n;
+  if (blue) *blue = b;
+  if (n2) *n2 = m;
+  if (maxp) *maxp = m > 1 ? largest_prime_factor(m) : 1;
+}
+
 bool pf_fuse_on() {
   static const bool on = [] {
     const char* e = getenv("AMR_PF_FUSE");

@@ -70,7 +70,9 @@ extern "C" {
                                   (amr_split_state_tables, amr_psk_plan_split_conv, amr_fsk_plan_split_conv)
                                5: raw-integer captures: amr_psk_demod_host_edges / _device_edges,
                                   amr_fsk_demod_host_edges / _device_edges (the odd extension as the
-                                  caller's dtype forms it) */
+                                  caller's dtype forms it); the PSK split's strict mode
+                                  (amr_psk_plan_set_split_strict ...); F2's margin from a standard
+                                  FFT rounding bound (amr_fsk_fft_margin, amr_fsk_plan_margin) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -411,6 +413,17 @@ int amr_fsk_plan_set_layout(amr_fsk_plan *plan, int layout);
  * the plan cannot split. */
 int amr_fsk_plan_split_info(amr_fsk_plan *plan, int *last_split, int64_t *warmup, int64_t *chunk,
                             double *kappa, double *tau);
+/* F2's margin scale tau from a standard FFT rounding bound (DESIGN.md §2 item
+ * 6; host arithmetic, no device): out[8] = tau (max(2^-36, the bound)), the
+ * fast path's and pocketfft's relative 2-norm transform errors eps_fast /
+ * eps_ref, the bound on max ||z||_2 / peak|ext x| over both tones, whether
+ * the fast path runs Bluestein and its length, whether pocketfft does and its
+ * length.  The filters as amr_fsk_plan_create takes them. */
+int amr_fsk_fft_margin(int64_t n_samples, const double *mark_b, const double *mark_a, const double *mark_zi,
+                       const double *space_b, const double *space_a, const double *space_zi, int ntaps, double *out);
+/* a plan's F2 margin scales: tau (serial F1) and tau_split (time-split F1:
+ * tau + kappa ||ifft(h)||_1) */
+int amr_fsk_plan_margin(amr_fsk_plan *plan, double *tau, double *tau_split);
 /* the split design from the filters alone (host arithmetic; no device):
  * warm-up, kappa and ||ifft(h)||_1 of scipy.signal.hilbert's multiplier h at
  * length n.  Returns AMR_E_INVALID when the filters cannot be split at n. */

@@ -197,8 +197,8 @@ def test_fsk_batch_past_2g_samples():
                                                 (441000, 2400, 7000.0, 19000.0)])    # 44.1 kHz x 10 s: 2^3 3^2 5^3 7^2
 def test_envelope_error_is_far_below_the_margin(n, baud, mark, space):
     """F2 flags a stream for the exact path when some compare has
-    |env_mark - env_space| <= 2 tau peak|x| (tau = 2^-36, amr_internal.h
-    kAmbTau); unflagged compares are then bit-exact only if the fast path's
+    |env_mark - env_space| <= 2 tau peak|x| (the plan's tau: max(2^-36 =
+    kAmbTau, a standard FFT rounding bound, fsk_api.cpp fsk_fft_bound)); unflagged compares are then bit-exact only if the fast path's
     envelopes are within tau peak|x| of the reference's.  F1 computes scipy's
     filtfilt bit for bit, so the difference is the FFTs' rounding alone --
     two-pass (96000, 30000), Bluestein over a two-pass M (24001, 77880),
@@ -235,7 +235,12 @@ def test_envelope_error_is_far_below_the_margin(n, baud, mark, space):
         peak = np.abs(xi).max()
         worst = max(worst, np.abs(gm[i] - env(mark)).max() / peak, np.abs(gs[i] - env(space)).max() / peak)
     tau = 2.0 ** -36
-    print(f"n={n}: max |env_gpu - env_ref| / peak|x| = {worst:.3e} (tau = {tau:.3e}, ratio {tau / worst:.0f})")
+    # the plan's own scale: max(2^-36, the standard FFT bound, fsk_api.cpp
+    # fsk_fft_bound; tests/test_fsk_fft_bound.py)
+    tp = pl.margin()["tau"]
+    assert tp >= tau and abs(tp - _fsk.fft_margin(n, baud, mark, space)["tau"]) <= 1e-15 * tp
+    print(f"n={n}: max |env_gpu - env_ref| / peak|x| = {worst:.3e} (2^-36 = {tau:.3e}, ratio {tau / worst:.0f}; "
+          f"the plan's tau {tp:.3e}, ratio {tp / worst:.0f}; exact streams {pl.exact_streams()} of {len(rows)})")
     assert worst < tau / 100
 
 
