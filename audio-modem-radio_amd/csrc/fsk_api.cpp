@@ -993,9 +993,16 @@ bool fsk_split_design(const FskIir& f, int nt, int64_t n, int64_t* w_out, double
 //     gamma_{p+4} / log2 p) + 2u (a radix-p pass's 2-norm error per binary
 //     level -- Higham's radix-2 eta = mu + gamma_4 (sqrt2 + mu) generalised --
 //     plus twiddles within 2u);
-//   Bluestein (n, M): (2n - 1) / sqrt(n) (3 eps_M + 2 gc) + gc, gc = sqrt2
-//     gamma_2 + 2u (the chirp products; 2n - 1 = ||chirp||_1 bounds its
-//     spectrum's peak);
+//   Bluestein (n, M): (Bmax / sqrt n) (2 eps_M + 2 gc) + sqrt(2n - 1) eps_M +
+//     gc, gc = sqrt2 gamma_2 + 2u (a complex product with a rounded chirp):
+//     the chirp product, FFT_M, the product with the kernel's spectrum (whose
+//     own FFT-computed table is off by <= eps_M ||B||_2 = eps_M sqrt(M (2n -
+//     1)) -- the sqrt(2n - 1) term), IFFT_M, the chirp product.  Bmax =
+//     max |FFT_M(kernel)| <= sqrt(n) (6 + 2 ln n): the chirp exp(i pi m^2 / n)
+//     is periodic (n or 2n) with Fourier coefficients of modulus 1 / sqrt(n)
+//     (a quadratic Gauss sum), so the windowed kernel's spectrum is a sum of
+//     Dirichlet kernels D_{2n-1}, whose values on a grid sum to <= 2 (2n - 1)
+//     + P (ln(P / 2) + 1) (measured max |B| = 2.0-2.2 sqrt(n));
 // and ||z||_2 <= (G^2 sqrt(m1) + 2 G R + R^2) peak|ext x| per tone (G the
 // band-pass's L1 gain, R the L2 norm of its zi-start transient: both
 // filtfilt passes).  tau = max(2^-36, (4 eps_fast + 4 eps_ref + 8u) max
@@ -1028,8 +1035,10 @@ bool fsk_fft_bound(const FskIir& f, int nt, int64_t n, int pad, FskFftBound& o) 
     return e / (1.0 - e);
   };
   const double gc = std::sqrt(2.0) * gam(2.0) + 2.0 * u;
+  const double bq = 6.0 + 2.0 * std::log((double)n);   // Bmax / sqrt(n)
   auto eps_blue = [&](int64_t M) {
-    return (2.0 * (double)n - 1.0) / std::sqrt((double)n) * (3.0 * eps_direct(M, lpf_of(M)) + 2.0 * gc) + gc;
+    const double em = eps_direct(M, lpf_of(M));
+    return bq * (2.0 * em + 2.0 * gc) + std::sqrt(2.0 * (double)n - 1.0) * em + gc;
   };
   FftShape sh;
   if (!fft_shape(n, sh)) return false;

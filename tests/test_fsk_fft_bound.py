@@ -49,7 +49,8 @@ def _restated(n, d, G, R, pad=21):
     gc = math.sqrt(2) * gam(2.0) + 2 * U
 
     def eps_blue(M):
-        return (2.0 * n - 1) / math.sqrt(n) * (3 * eps_direct(M, _lpf(M)) + 2 * gc) + gc
+        em = eps_direct(M, _lpf(M))
+        return (6 + 2 * math.log(n)) * (2 * em + 2 * gc) + math.sqrt(2.0 * n - 1) * em + gc
 
     ef = eps_blue(d["fast_M"]) if d["fast_blue"] else eps_direct(n, _lpf(n))
     er = eps_blue(d["ref_M"]) if d["ref_blue"] else eps_direct(n, _lpf(d["ref_M"]))
@@ -84,6 +85,22 @@ def test_tau_is_the_standard_bound(n, baud, mark, space, built_lib):
     assert math.isclose(d["tau"], tau, rel_tol=1e-6), (d["tau"], tau)
     print(f"n={n}: tau {d['tau']:.3e} = {d['tau'] / 2.0 ** -36:.1f} x 2^-36 (fast {'Bluestein M=' + str(d['fast_M']) if d['fast_blue'] else 'direct'}, "
           f"pocketfft {'Bluestein M=' + str(d['ref_M']) if d['ref_blue'] else 'direct'})")
+
+
+@pytest.mark.parametrize("n", [77, 1000, 1001, 24001, 96001])
+def test_chirp_spectrum_bound(n):
+    """Bluestein's kernel (the chirp exp(i pi m^2 / n), |m| < n, wrapped into
+    a length-M >= 2n - 1 transform) has max |FFT_M| <= sqrt(n) (6 + 2 ln n),
+    the constant fsk_fft_bound takes (measured: ~2.2 sqrt(n))."""
+    M = 1
+    while M < 2 * n - 1:
+        M *= 2
+    for MM in (M, 2 * n - 1 + (n % 7)):
+        b = np.zeros(MM, complex)
+        k = np.arange(n, dtype=np.float64)
+        b[:n] = np.exp(1j * np.pi * ((k * k) % (2 * n)) / n)
+        b[MM - n + 1:] = b[1:n][::-1]
+        assert np.abs(np.fft.fft(b)).max() <= math.sqrt(n) * (6 + 2 * math.log(n))
 
 
 @pytest.mark.parametrize("n,baud,mark,space", [CASES[0], CASES[1], CASES[3], CASES[4], CASES[6]],
