@@ -57,7 +57,8 @@ EXPORTS = [
     "amr_psk_split_symbols_host", "amr_psk_f32_margin", "amr_psk_plan_last_f32f", "amr_split_state_tables",
     "amr_psk_plan_split_conv",
     "amr_fsk_plan_set_layout", "amr_fsk_plan_split_info", "amr_fsk_split_design", "amr_fsk_split_bandpass_host",
-    "amr_fsk_fft_margin", "amr_fsk_plan_margin",
+    "amr_fsk_fft_margin", "amr_fsk_plan_margin", "amr_fsk_plan_set_split_strict", "amr_fsk_plan_split_strict",
+    "amr_fsk_plan_last_strict", "amr_fsk_split_strict_design", "amr_fsk_split_bounds_host",
     "amr_fsk_plan_split_conv",
     "amr_psk_demod_host_edges", "amr_psk_demod_device_edges", "amr_fsk_demod_host_edges", "amr_fsk_demod_device_edges",
     "amr_psk_split_bounds_host", "amr_psk_plan_set_split_strict", "amr_psk_plan_split_strict",
@@ -277,6 +278,11 @@ def lib():
             "amr_fsk_split_design": (I32, [I64, P, P, P, P, I32, P, P, P]),
             "amr_fsk_fft_margin": (I32, [I64, P, P, P, P, P, P, I32, P]),
             "amr_fsk_plan_margin": (I32, [P, P, P]),
+            "amr_fsk_plan_set_split_strict": (I32, [P, I32]),
+            "amr_fsk_plan_split_strict": (I32, [P]),
+            "amr_fsk_plan_last_strict": (I32, [P]),
+            "amr_fsk_split_strict_design": (I32, [P, P, P, I32, I64, P, P]),
+            "amr_fsk_split_bounds_host": (I32, [P, P, I32, I64, I64, P, P, P]),
             "amr_fsk_split_bandpass_host": (I32, [P, P, I32, I64, I64, I64, P]),
             "amr_fsk_plan_split_conv": (I32, [P]),
             "amr_tx_work_bytes": (I64, [I32, D, D, I64, I64]),

@@ -64,6 +64,34 @@ def split_design(n: int, baud, mark_freq, space_freq, samp_rate=96000):
     return {"warmup": w.value, "kappa": k.value, "hilbert_l1": h.value, "tau": m["tau"] + k.value * h.value}
 
 
+def split_strict_design(n: int, baud, mark_freq, space_freq, samp_rate=96000):
+    """The split F1's strict band-pass design per tone (libamr.so host
+    arithmetic, amr_fsk_split_strict_design): [mark, space] dicts of the
+    constants (_amr.STRICT_CONSTS) and the tables kabs, z0abs, W, K12, HS, GS,
+    TZ; None when there is no split design or no strict bound."""
+    sd = split_design(n, baud, mark_freq, space_freq, samp_rate)
+    if sd is None:
+        return None
+    _, tones = design_fsk(n, baud, mark_freq, space_freq, samp_rate)
+    out = []
+    for b, a, zi in tones:
+        c = np.zeros(32)
+        if lib().amr_fsk_split_strict_design(ptr(b), ptr(a), ptr(zi), len(b), int(sd["warmup"]), ptr(c), None) != 0:
+            return None
+        d = dict(zip(_amr.STRICT_CONSTS, c[:len(_amr.STRICT_CONSTS)].tolist()))
+        w = int(d["w1"])
+        sizes = [("kabs", w), ("z0abs", w + 1), ("W", int(d["nw"])), ("K12", int(d["nk"])), ("HS", int(d["nh"])),
+                 ("GS", int(d["ng"])), ("TZ", int(d["nz"]))]
+        tabs = np.zeros(sum(k for _, k in sizes))
+        check(lib().amr_fsk_split_strict_design(ptr(b), ptr(a), ptr(zi), len(b), w, ptr(c), ptr(tabs)))
+        o = 0
+        for name, k in sizes:
+            d[name] = tabs[o:o + k]
+            o += k
+        out.append(d)
+    return out
+
+
 def fft_margin(n: int, baud, mark_freq, space_freq, samp_rate=96000):
     """F2's margin scale from a standard FFT rounding bound (host arithmetic
     in libamr.so, no device; include/amr.h amr_fsk_fft_margin): dict of tau,
@@ -198,6 +226,33 @@ class FskPlan:
         check(lib().amr_fsk_plan_split_info(self.handle, ctypes.byref(ls), ctypes.byref(w), ctypes.byref(L),
                                             ctypes.byref(k), ctypes.byref(t)))
         return {"last_split": bool(ls.value), "warmup": w.value, "chunk": L.value, "kappa": k.value, "tau": t.value}
+
+    def set_split_strict(self, on):
+        """The split F1's strict margin for this plan: True / False, None = the
+        process default (AMR_FSK_SPLIT_STRICT)."""
+        check(lib().amr_fsk_plan_set_split_strict(self.handle, -1 if on is None else (1 if on else 0)))
+
+    def split_strict(self) -> bool:
+        return int(lib().amr_fsk_plan_split_strict(self.handle)) == 1
+
+    def last_strict(self) -> bool:
+        return int(lib().amr_fsk_plan_last_strict(self.handle)) == 1
+
+    def split_bounds(self, x: np.ndarray):
+        """Diagnostic: the strict split F1 over x [B][n] -> (z [B][n][2] (mark,
+        space), per-tone maxima [B][2][8] (D1max, E1max, max|y1|, D2max, S1max,
+        -, F, -), peak [B] = max |ext x|)."""
+        x = np.ascontiguousarray(np.atleast_2d(x))
+        if x.dtype not in _amr.DTYPES:
+            x = np.ascontiguousarray(x, np.float64)
+        B = x.shape[0]
+        z = np.zeros((B, self.n, 2))
+        bnd = np.zeros((B, 2, 8))
+        pk = np.zeros(B)
+        with self.lock:
+            check(lib().amr_fsk_split_bounds_host(self.handle, ptr(x), _amr.DTYPES[x.dtype], B, x.shape[1], ptr(z),
+                                                  ptr(bnd), ptr(pk)))
+        return z, bnd, pk
 
     def margin(self) -> dict:
         """F2's margin scales of this plan: tau (serial F1) and tau_split."""

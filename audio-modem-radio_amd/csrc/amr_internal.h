@@ -239,6 +239,19 @@ __host__ __device__ inline double amb_scale(double peak, double tau = kAmbTau) {
   return 8.0 * d * d;
 }
 
+// One filter's strict band-pass design as the kernels read it (split_strict.h
+// strict_design_bp; the FSK split's strict mode holds one per tone): the
+// convolution-start bound tables, the block kernels and their cut remainders,
+// and the per-step / per-pass constants
+struct StrictBp {
+  const double* kabs;         // [w]
+  const double* z0abs;        // [w + 1]
+  const double *W, *K12, *HS, *GS, *TZ;
+  int nw, nk, nh, nz, k12_off;
+  double w_tail, k12_tail, hs_tail, tz_tail;
+  double gam, kx, ky, g1x, gmax, hz, tk, zi_sum, zb;
+};
+
 // FSK time-split F1 (fsk_kernels.hip FS1-FS3):
 // each filtfilt pass of both tones cut into chunks of L outputs, one lane per
 // (chunk, tone), every chunk started w samples early from a zero state.  Its
@@ -258,7 +271,23 @@ struct FskSplit {
   const double* ktab;         // [2 tones][w][6] (iir_design.h split_state_tables)
   const double* z0tab;        // [2 tones][w + 1][6]
   double* zs;                 // [B][2][c][6] start states, FS0 -> FS1 (then reused for FS2)
+  // STRICT (round 6; split_strict.h strict_design_bp per tone, fsk_kernels.hip
+  // FS0-FS2 with ST, KF1-KF2, FS3): F2's margin from a bound on |z_split -
+  // z_serial| that holds for every input, in place of kappa * peak
+  int strict;
+  StrictBp sb[2];             // the per-tone design (device tables + constants)
+  double u2;
+  double hl1;                 // ||ifft(h)||_1 of scipy.signal.hilbert's kernel at n
+  unsigned long long* bnd;    // [B][2][8] bits: D1max, E1max, max|y1|, D2max, S1max, -, Fmax, -
+  double* sc;                 // [B][2][sstride]: d1 nb1 | d2 nb1 | ds1 c | ds2 c | e1 nb1 | s1 nb1 | e2 nb1
+  int64_t sstride, nb1;
 };
+__host__ __device__ inline int64_t fsk_strict_off_d2(const FskSplit& s) { return s.nb1; }
+__host__ __device__ inline int64_t fsk_strict_off_ds1(const FskSplit& s) { return 2 * s.nb1; }
+__host__ __device__ inline int64_t fsk_strict_off_ds2(const FskSplit& s) { return 2 * s.nb1 + s.c; }
+__host__ __device__ inline int64_t fsk_strict_off_e1(const FskSplit& s) { return 2 * s.nb1 + 2 * s.c; }
+__host__ __device__ inline int64_t fsk_strict_off_s1(const FskSplit& s) { return 3 * s.nb1 + 2 * s.c; }
+__host__ __device__ inline int64_t fsk_strict_off_e2(const FskSplit& s) { return 4 * s.nb1 + 2 * s.c; }
 
 struct FskIir {            // [tone][tap], tone 0 = mark
   double b[2][8];

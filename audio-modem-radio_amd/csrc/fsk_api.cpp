@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -23,6 +24,7 @@
 #include "fsk_exact.h"
 #include "fft.h"
 #include "iir_design.h"
+#include "split_strict.h"
 
 namespace amr {
 hipError_t launch_fsk_bandpass(int, const void*, int64_t, int64_t, double*, double2*, const FskParams&,
@@ -415,6 +417,17 @@ struct amr_fsk_plan {
   std::vector<double> split_tab_host;
   double* split_cz = nullptr;
   int64_t split_cz_bytes = 0;
+  // the split F1's STRICT mode (round 6; split_strict.h strict_design_bp per
+  // tone, fsk_kernels.hip FS0-FS2 with ST, KF1-KF2, FS3): designed on the
+  // first strict call; its tables, per-stream maxima and scratch in
+  // strict_tab / strict_bnd / strict_sc (strict_bytes, not in split_alloc)
+  int strict_mode = -1;        // amr_fsk_plan_set_split_strict: 1 on, 0 off, -1 the default
+  bool strict_designed = false, strict_ok = false, last_strict = false;
+  StrictDesign sdes[2];
+  double* strict_tab = nullptr;
+  unsigned long long* strict_bnd = nullptr;
+  double* strict_sc = nullptr;
+  int64_t strict_tab_n = 0, strict_bnd_cap = 0, strict_sc_bytes = 0, strict_bytes = 0;
   GatherGate gate;             // an all-gather still reading this plan's outputs
   // staging for the host API
   void* d_x = nullptr;
@@ -439,7 +452,8 @@ void fsk_plan_free(amr_fsk_plan* pl) {
   for (void* p : {(void*)pl->z, (void*)pl->u, (void*)pl->v, (void*)pl->dd, (void*)pl->cmp, (void*)pl->words, pl->d_x,
                   (void*)pl->d_out, (void*)pl->d_len, (void*)pl->d_sync, (void*)pl->xflags, (void*)pl->amb,
                   (void*)pl->xlist, (void*)pl->xslots, (void*)pl->xbits, (void*)pl->xpool, (void*)pl->xL,
-                  (void*)pl->split_y1, (void*)pl->split_peak, (void*)pl->split_cz, (void*)pl->d_edge})
+                  (void*)pl->split_y1, (void*)pl->split_peak, (void*)pl->split_cz, (void*)pl->d_edge,
+                  (void*)pl->strict_tab, (void*)pl->strict_bnd, (void*)pl->strict_sc})
     if (p) (void)hipFree(p);
   fft_plan_free(pl->fft);
   for (auto& e : pl->ev)
@@ -478,9 +492,21 @@ constexpr int64_t kFskSplitLanes = 65536;
 constexpr int64_t kFskSplitConvMinL = 128;
 constexpr int64_t kFskSplitConvMaxL = 1024;
 constexpr int64_t kFskSplitConvChunks = 3072;
+// the split F1's strict margin by default (AMR_FSK_SPLIT_STRICT=0 / 1 overrides)
+constexpr int kFskStrictDefault = 1;
 bool fsk_split_conv_on(const amr_fsk_plan* pl) {
   static const bool env = [] { const char* e = std::getenv("AMR_FSK_SPLIT_CONV"); return !(e && e[0] == '0'); }();
   return env && pl->split_ok && !pl->split_tab_host.empty();
+}
+// STRICT: AMR_FSK_SPLIT_STRICT=0 / 1 sets the default, amr_fsk_plan_set_split_strict
+// a plan's; the bound covers the convolution starts only
+bool fsk_split_strict_on(const amr_fsk_plan* pl) {
+  static const int env = [] {
+    const char* e = std::getenv("AMR_FSK_SPLIT_STRICT");
+    return e ? (e[0] == '1' ? 1 : 0) : kFskStrictDefault;
+  }();
+  const bool want = pl->strict_mode >= 0 ? pl->strict_mode == 1 : env == 1;
+  return want && fsk_split_conv_on(pl);
 }
 FskSplit fsk_split_params(amr_fsk_plan* pl, int64_t B, int64_t L) {
   FskSplit sp{};
@@ -494,12 +520,122 @@ FskSplit fsk_split_params(amr_fsk_plan* pl, int64_t B, int64_t L) {
                                                                       kFskSplitConvChunks)));
   else sp.L = std::max({kFskSplitMinL, pl->split_w / 4, lanes});
   sp.w = pl->split_w;
+  if (L <= 0 && sp.conv && fsk_split_strict_on(pl) && pl->strict_ok)   // chunks on block boundaries
+    sp.L = (sp.L + kStrictBlk - 1) / kStrictBlk * kStrictBlk;
   sp.c = (m1 + sp.L - 1) / sp.L;
   sp.tau = pl->split_tau;
   sp.y1 = pl->split_y1;
   sp.peak = pl->split_peak;
   pl->split_L = sp.L;
   return sp;
+}
+
+// STRICT: the per-tone designs from FS0's tables (host arithmetic, once) and
+// their device copy: per tone kabs [w] | z0abs [w + 1] | W | K12 | HS | GS | TZ
+int fsk_strict_prepare(amr_fsk_plan* pl) {
+  if (pl->strict_designed) return AMR_OK;
+  pl->strict_designed = true;
+  pl->strict_ok = false;
+  if (!pl->split_ok || pl->split_tab_host.empty()) return AMR_OK;
+  const int nt = pl->p.nt;
+  const int64_t w = pl->split_w;
+  bool ok = true;
+  for (int t = 0; t < 2 && ok; ++t) {
+    Iir fi{};
+    fi.nt = nt;
+    for (int i = 0; i < nt; ++i) { fi.b[i] = pl->f.b[t][i]; fi.a[i] = pl->f.a[t][i]; }
+    for (int i = 0; i < nt - 1; ++i) fi.zi[i] = pl->f.zi[t][i];
+    StrictDesign& d = pl->sdes[t];
+    ok = strict_design_bp(fi, pl->split_tab_host.data() + (size_t)t * w * 6,
+                          pl->split_tab_host.data() + (size_t)(2 * w + t * (w + 1)) * 6, w, d,
+                          strict_detail::responses(fi)) &&
+         d.g1x * (d.kx + 2.0 * d.ky) < 0.125;
+    d.ok = ok;
+  }
+  if (!ok) return AMR_OK;
+  std::vector<double> tab;
+  for (int t = 0; t < 2; ++t)
+    for (const std::vector<double>* v : {&pl->sdes[t].kabs, &pl->sdes[t].z0abs, &pl->sdes[t].W, &pl->sdes[t].K12,
+                                         &pl->sdes[t].HS, &pl->sdes[t].GS, &pl->sdes[t].TZ})
+      tab.insert(tab.end(), v->begin(), v->end());
+  HIP_TRY(hipMalloc((void**)&pl->strict_tab, tab.size() * 8));
+  HIP_TRY(hipMemcpy(pl->strict_tab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+  pl->strict_tab_n = (int64_t)tab.size();
+  pl->strict_bytes += (int64_t)tab.size() * 8;
+  pl->strict_ok = true;
+  return AMR_OK;
+}
+// STRICT: this call's scratch and maxima for B streams, and sp's strict fields
+int ensure_fsk_strict(amr_fsk_plan* pl, FskSplit& sp, int64_t B) {
+  // (a diagnostic's forced chunk off block boundaries runs without it)
+  if (!sp.conv || !fsk_split_strict_on(pl) || !pl->strict_ok || sp.L % kStrictBlk != 0) return AMR_OK;
+  const int64_t m1 = pl->p.n + 2 * (int64_t)pl->p.pad;
+  sp.nb1 = (m1 + kStrictBlk - 1) / kStrictBlk;
+  sp.sstride = 5 * sp.nb1 + 2 * sp.c;
+  const int64_t need = B * 2 * sp.sstride * 8;
+  if (pl->strict_sc_bytes < need || !pl->strict_sc) {
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    if (pl->strict_sc) (void)hipFree(pl->strict_sc);
+    pl->strict_bytes -= pl->strict_sc_bytes;
+    pl->strict_sc = nullptr;
+    pl->strict_sc_bytes = 0;
+    HIP_TRY(hipMalloc((void**)&pl->strict_sc, (size_t)need));
+    pl->strict_sc_bytes = need;
+    pl->strict_bytes += need;
+  }
+  if (pl->strict_bnd_cap < B || !pl->strict_bnd) {
+    HIP_TRY(hipStreamSynchronize(pl->stream));
+    if (pl->strict_bnd) (void)hipFree(pl->strict_bnd);
+    pl->strict_bytes -= pl->strict_bnd_cap * 2 * 64;
+    pl->strict_bnd = nullptr;
+    pl->strict_bnd_cap = 0;
+    HIP_TRY(hipMalloc((void**)&pl->strict_bnd, (size_t)(B * 2 * 64)));
+    pl->strict_bnd_cap = B;
+    pl->strict_bytes += B * 2 * 64;
+  }
+  sp.strict = 1;
+  sp.u2 = 2.0 * 0x1p-53 * (1.0 + 0x1p-50);
+  sp.hl1 = pl->split_hl1;
+  sp.sc = pl->strict_sc;
+  sp.bnd = pl->strict_bnd;
+  const double* o = pl->strict_tab;
+  for (int t = 0; t < 2; ++t) {
+    const StrictDesign& d = pl->sdes[t];
+    StrictBp& b = sp.sb[t];
+    b.kabs = o;
+    o += d.kabs.size();
+    b.z0abs = o;
+    o += d.z0abs.size();
+    b.W = o;
+    o += d.W.size();
+    b.K12 = o;
+    o += d.K12.size();
+    b.HS = o;
+    o += d.HS.size();
+    b.GS = o;
+    o += d.GS.size();
+    b.TZ = o;
+    o += d.TZ.size();
+    b.nw = (int)d.W.size();
+    b.nk = (int)d.K12.size();
+    b.nh = (int)d.HS.size();
+    b.nz = (int)d.TZ.size();
+    b.k12_off = d.k12_off;
+    b.w_tail = d.w_tail;
+    b.k12_tail = d.k12_tail;
+    b.hs_tail = d.hs_tail;
+    b.tz_tail = d.tz_tail;
+    b.gam = d.gam;
+    b.kx = d.kx;
+    b.ky = d.ky;
+    b.g1x = d.g1x;
+    b.gmax = d.gmax;
+    b.hz = d.hz;
+    b.tk = d.tk;
+    b.zi_sum = d.zi_sum;
+    b.zb = d.zb;
+  }
+  return AMR_OK;
 }
 // the tables and this call's zs in split_cz (grown as needed; counted in
 // split_alloc), then sp's pointers into it
@@ -558,8 +694,12 @@ int run_fsk_f1(amr_fsk_plan* pl, const void* d_x, int dtype, int64_t B, int64_t 
   p.force_exact = pl->exact_mode == 2 ? 1 : 0;
   if (pl->split_now) {
     if (int rc = ensure_split_buffers(pl, B)) return rc;
+    if (fsk_split_strict_on(pl))
+      if (int rc = fsk_strict_prepare(pl)) return rc;
     FskSplit sp = fsk_split_params(pl, B, 0);
     if (int rc = ensure_split_conv(pl, sp, B)) return rc;
+    if (int rc = ensure_fsk_strict(pl, sp, B)) return rc;
+    pl->last_strict = sp.strict != 0;
     HIP_TRY(launch_fsk_split(dtype, d_x, x_stride, B, pl->z, p, pl->f, sp, pl->stream));
     return AMR_OK;
   }
@@ -1318,7 +1458,7 @@ int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
   // no staging (no d_x, no dd, no output staging)
   return plan->scratch_bytes + (plan->d_x ? plan->staging_bytes : 0) +
          (plan->d_out ? plan->max_streams * (plan->out_cap + 16 + 2 * (int64_t)plan->p.pad * 8) : 0) +
-         plan->split_alloc;
+         plan->split_alloc + plan->strict_bytes;
 }
 int64_t amr_fsk_plan_fft_length(const amr_fsk_plan* plan) { return plan ? plan->fft.M : -1; }
 int amr_fsk_plan_live_columns(const amr_fsk_plan* plan) { return plan ? plan->p.lc.on : -1; }
@@ -1346,6 +1486,96 @@ int amr_fsk_plan_split_info(amr_fsk_plan* plan, int* last_split, int64_t* warmup
   if (chunk) *chunk = plan->split_L;
   if (kappa) *kappa = plan->split_kappa;
   if (tau) *tau = plan->split_tau;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_set_split_strict(amr_fsk_plan* plan, int mode) {
+  if (!plan || mode < -1 || mode > 1) return fail(AMR_E_INVALID, "amr_fsk_plan_set_split_strict: bad argument");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  plan->strict_mode = mode;
+  return AMR_OK;
+}
+
+int amr_fsk_plan_split_strict(amr_fsk_plan* plan) {
+  if (!plan) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return fsk_split_strict_on(plan) ? 1 : 0;
+}
+
+int amr_fsk_plan_last_strict(amr_fsk_plan* plan) {
+  if (!plan) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return plan->last_strict ? 1 : 0;
+}
+
+int amr_fsk_split_strict_design(const double* b, const double* a, const double* zi, int nt, int64_t w, double* consts,
+                                double* tabs) {
+  if (!b || !a || !zi || !consts || nt < 2 || nt > kMaxTaps || w < 1)
+    return fail(AMR_E_INVALID, "amr_fsk_split_strict_design: bad argument");
+  Iir f{};
+  f.nt = nt;
+  for (int i = 0; i < nt; ++i) { f.b[i] = b[i]; f.a[i] = a[i]; }
+  for (int i = 0; i < nt - 1; ++i) f.zi[i] = zi[i];
+  const int N = nt - 1;
+  std::vector<double> tab((size_t)(2 * w + 1) * N);
+  split_state_tables(f, w, tab.data(), tab.data() + (size_t)w * N);
+  StrictDesign d;
+  const bool ok = strict_design_bp(f, tab.data(), tab.data() + (size_t)w * N, w, d, strict_detail::responses(f)) &&
+                  d.g1x * (d.kx + 2.0 * d.ky) < 0.125;
+  // the PSK entry's layout (amr_psk_split_strict_design) without the low-pass
+  const double v[32] = {d.g1x, d.gmax, d.hz, d.tk, d.zi_sum, d.zb, d.kx, d.ky, 2.0 * 0x1p-53 * (1.0 + 0x1p-50),
+                        d.gam, 0.0, (double)w, 0.0, 0.0, (double)d.W.size(), (double)d.K12.size(),
+                        (double)d.HS.size(), (double)d.GS.size(), (double)d.TZ.size(), (double)d.k12_off, d.w_tail,
+                        d.k12_tail, d.hs_tail, d.tz_tail, 0.0, 0.0, ok ? 1.0 : 0.0, 0.0};
+  for (int i = 0; i < 32; ++i) consts[i] = v[i];
+  if (!ok) return fail(AMR_E_INVALID, "no strict bound for this filter");
+  if (tabs) {
+    double* o = tabs;
+    for (const std::vector<double>* t : {&d.kabs, &d.z0abs, &d.W, &d.K12, &d.HS, &d.GS, &d.TZ}) {
+      std::memcpy(o, t->data(), t->size() * 8);
+      o += t->size();
+    }
+  }
+  return AMR_OK;
+}
+
+int amr_fsk_split_bounds_host(amr_fsk_plan* plan, const void* x, int dtype, int64_t B, int64_t x_stride,
+                              double* z_out, double* bnd_out, double* peak_out) {
+  if (!plan || !x || !z_out || !bnd_out || !peak_out || B < 1)
+    return fail(AMR_E_INVALID, "amr_fsk_split_bounds_host: bad argument");
+  if (!dtype_size(dtype)) return fail(AMR_E_INVALID, "unknown dtype");
+  std::lock_guard<std::mutex> lk(plan->mu);
+  HIP_TRY(hipSetDevice(plan->device));
+  if (!plan->split_ok || !fsk_split_conv_on(plan)) return fail(AMR_E_INVALID, "no convolution-start split F1 for this plan");
+  if (B > plan->max_streams || B > 65535) return fail(AMR_E_CAPACITY, "batch exceeds plan max_streams");
+  if (x_stride < plan->p.n) return fail(AMR_E_INVALID, "x_stride < n_samples");
+  const int saved = plan->strict_mode;
+  plan->strict_mode = 1;
+  int rc = fsk_strict_prepare(plan);
+  if (!rc && !plan->strict_ok) rc = fail(AMR_E_INVALID, "no strict bound for this plan's filters");
+  const int64_t n = plan->p.n;
+  void* xs = nullptr;
+  if (!rc) rc = stage_input(plan, x, dtype, B, x_stride, &xs);
+  if (!rc) rc = ensure_split_buffers(plan, B);
+  FskParams p = plan->p;
+  p.lc = LiveCols{};                         // natural order for the caller
+  p.amb = nullptr;
+  FskSplit sp{};
+  if (!rc) {
+    sp = fsk_split_params(plan, B, 0);
+    rc = ensure_split_conv(plan, sp, B);
+  }
+  if (!rc) rc = ensure_fsk_strict(plan, sp, B);
+  plan->strict_mode = saved;
+  if (rc) return rc;
+  HIP_TRY(launch_fsk_split(dtype, xs, n, B, plan->z, p, plan->f, sp, plan->stream));
+  HIP_TRY(hipMemcpyAsync(z_out, plan->z, (size_t)(B * n * 16), hipMemcpyDeviceToHost, plan->stream));
+  std::vector<unsigned long long> hb((size_t)B * 16), hp((size_t)B);
+  HIP_TRY(hipMemcpyAsync(hb.data(), sp.bnd, hb.size() * 8, hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipMemcpyAsync(hp.data(), sp.peak, hp.size() * 8, hipMemcpyDeviceToHost, plan->stream));
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  std::memcpy(bnd_out, hb.data(), hb.size() * 8);
+  std::memcpy(peak_out, hp.data(), hp.size() * 8);
   return AMR_OK;
 }
 

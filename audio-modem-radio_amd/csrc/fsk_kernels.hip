@@ -652,7 +652,24 @@ __device__ __forceinline__ void fsk_split_warm(double (&z)[6], const double (&b)
 // warm-up (split_chain.h split_conv_state; the PSK split's KS0): one wave
 // per (chunk, tone), four per workgroup, -> zs; before FS1 over ext(x) and
 // again before FS2 over y1 reversed
-template <typename T>
+// STRICT (FskSplit::strict): the (stream, tone) scratch row and its bounds
+__device__ __forceinline__ double* fsk_strict_row(const FskSplit& sp, int64_t s, int tone) {
+  return sp.sc + ((size_t)s * 2 + tone) * sp.sstride;
+}
+__device__ __forceinline__ ConvBound fsk_conv_bound(const FskSplit& sp, int64_t s, int tone, int64_t off) {
+  const StrictBp& d = sp.sb[tone];
+  return ConvBound{d.kabs, d.z0abs, d.gam, fsk_strict_row(sp, s, tone) + off};
+}
+// the rounding one step of scipy's order commits, summed over states (split_strict.h):
+// u2 sum_{i>=1} |z_i| + kx |x| + ky |y|, the pre-step |z1..z5| in this pairing
+__device__ __forceinline__ double fsk_step_sz(const double (&z)[6]) {
+  return ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) + fabs(z[5]);
+}
+__device__ __forceinline__ unsigned long long fsk_abs_bits(double v) {
+  return (unsigned long long)__double_as_longlong(v) & 0x7fffffffffffffffULL;
+}
+
+template <typename T, bool ST>
 __global__ __launch_bounds__(256) void k_fsk_split_state_fwd(const void* xv, int64_t x_stride, FskParams p,
                                                              FskSplit sp) {
   const int64_t s = blockIdx.y;
@@ -664,15 +681,17 @@ __global__ __launch_bounds__(256) void k_fsk_split_state_fwd(const void* xv, int
   const int64_t n = p.n;
   const int pad = p.pad;
   const OddExt<T> ox(x, p.edge, s, n, pad);
-  split_conv_state<6>(
+  split_conv_state<6, ST>(
       sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L, ox.left(0),
       [&](int64_t j) -> double {
         if (j < pad) return ox.left(j);
         if (j < pad + n) return In<T>::cvt(x[j - pad]);
         return ox.right(j - pad - n);
       },
-      sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6);
+      sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6,
+      ST ? fsk_conv_bound(sp, s, tone, fsk_strict_off_ds1(sp) + c) : ConvBound{});
 }
+template <bool ST>
 __global__ __launch_bounds__(256) void k_fsk_split_state_bwd(FskParams p, FskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -681,15 +700,16 @@ __global__ __launch_bounds__(256) void k_fsk_split_state_bwd(FskParams p, FskSpl
   const int64_t c = q >> 1;
   const int64_t m1 = p.n + 2 * (int64_t)p.pad;
   const double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
-  split_conv_state<6>(
+  split_conv_state<6, ST>(
       sp.ktab + (size_t)tone * sp.w * 6, sp.z0tab + (size_t)tone * (sp.w + 1) * 6, sp.w, c * sp.L, y1[m1 - 1],
-      [&](int64_t k) { return y1[m1 - 1 - k]; }, sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6);
+      [&](int64_t k) { return y1[m1 - 1 - k]; }, sp.zs + (((size_t)s * 2 + tone) * sp.c + c) * 6,
+      ST ? fsk_conv_bound(sp, s, tone, fsk_strict_off_ds2(sp) + c) : ConvBound{});
 }
 
 // FS1: forward pass over ext(x) (odd extension in the input's precision, as
 // F1), outputs [o0, o1) of chunk c for tone q & 1 -> y1; tone-0 lanes keep
 // the stream's max |ext x|
-template <typename T, int MODE>
+template <typename T, int MODE, bool ST>
 __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_stride, FskParams p, FskIir f,
                                                       FskSplit sp) {
   const int64_t s = blockIdx.y;
@@ -723,14 +743,35 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
   }
   double* __restrict__ y1 = sp.y1 + ((size_t)s * 2 + tone) * m1;
   unsigned long long pk = 0;
-  auto body = [&](int64_t jj, double e) {
-    if (jj < o0) {
-      fsk_split_warm(z, b, a, e);
+  // ST: this chunk's largest step bound and |y1|, and the step bounds summed
+  // per block of kStrictBlk outputs (chunks start on block boundaries)
+  [[maybe_unused]] double dmax = 0.0, ymax = 0.0, dsum = 0.0;
+  [[maybe_unused]] int dcnt = 0;
+  [[maybe_unused]] double* dblk = ST ? fsk_strict_row(sp, s, tone) : nullptr;
+  [[maybe_unused]] const double kx = ST ? sp.sb[tone].kx : 0.0, ky = ST ? sp.sb[tone].ky : 0.0;
+  auto out = [&](int64_t jj, double e) {
+    if constexpr (ST) {
+      const double sz = fsk_step_sz(z);
+      const double y = fsk_step<MODE>(z, b, a, e);
+      y1[jj] = y;
+      const double dd = __builtin_fma(sp.u2, sz, __builtin_fma(kx, fabs(e), ky * fabs(y)));
+      dmax = fmax(dmax, dd);
+      dsum += dd;
+      if (++dcnt == kStrictBlk) {
+        dblk[jj / kStrictBlk] = dsum;
+        dsum = 0.0;
+        dcnt = 0;
+      }
+      ymax = fmax(ymax, fabs(y));                 // (NaN / inf input: the peak test flags the stream)
     } else {
       y1[jj] = fsk_step<MODE>(z, b, a, e);
-      const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
-      pk = bits > pk ? bits : pk;
     }
+    const unsigned long long bits = fsk_abs_bits(e);
+    pk = bits > pk ? bits : pk;
+  };
+  auto body = [&](int64_t jj, double e) {
+    if (jj < o0) fsk_split_warm(z, b, a, e);
+    else out(jj, e);
   };
   for (; j < o1 && j < pad; ++j) body(j, ox.left(j));
   const int64_t jm = o1 < pad + n ? o1 : pad + n;
@@ -738,22 +779,22 @@ __global__ __launch_bounds__(64) void k_fsk_split_fwd(const void* xv, int64_t x_
     split_chain_2(
         j, o0, jm, fwd_blocks(x - pad, [](T v) { return In<T>::cvt(v); }),
         [&](int64_t jj) { return In<T>::cvt(x[jj - pad]); },
-        [&](int64_t, double e) { fsk_split_warm(z, b, a, e); },
-        [&](int64_t jj, double e) {
-          y1[jj] = fsk_step<MODE>(z, b, a, e);
-          const unsigned long long bits = (unsigned long long)__double_as_longlong(e) & 0x7fffffffffffffffULL;
-          pk = bits > pk ? bits : pk;
-        });
+        [&](int64_t, double e) { fsk_split_warm(z, b, a, e); }, out);
     j = jm;
   }
   for (; j < o1; ++j) body(j, ox.right(j - pad - n));
   if (tone == 0) atomicMax(&sp.peak[s], pk);
+  if constexpr (ST) {
+    if (dcnt > 0) dblk[(o1 - 1) / kStrictBlk] = dsum;   // the pass's last, partial block
+    atomicMax(sp.bnd + ((size_t)s * 2 + tone) * 8 + 0, fsk_abs_bits(dmax));
+    atomicMax(sp.bnd + ((size_t)s * 2 + tone) * 8 + 2, fsk_abs_bits(ymax));
+  }
 }
 
 // FS2: backward pass (scipy: lfilter over y1 reversed from zi * y1[-1]);
 // chunk c covers reversed positions [o0, o1): f[i], i = m1 - 1 - k - pad, into
 // z at F1's offsets (the live-column layout when the plan has it)
-template <int MODE, bool LIVE>
+template <int MODE, bool LIVE, bool ST>
 __global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, FskParams p, FskIir f, FskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -783,27 +824,176 @@ __global__ __launch_bounds__(64) void k_fsk_split_bwd(double* __restrict__ zd, F
 #pragma unroll
     for (int i = 0; i < 6; ++i) z[i] = 0.0;
   }
+  [[maybe_unused]] double dmax = 0.0, dsum = 0.0;   // ST: the largest step bound, block sums
+  [[maybe_unused]] int dcnt = 0;
+  [[maybe_unused]] double* dblk = ST ? fsk_strict_row(sp, s, tone) + fsk_strict_off_d2(sp) : nullptr;
+  [[maybe_unused]] const double kx = ST ? sp.sb[tone].kx : 0.0, ky = ST ? sp.sb[tone].ky : 0.0;
   split_chain_2(
       k, o0, o1, bwd_blocks(y1, m1 - 1), [&](int64_t kk) { return y1[m1 - 1 - kk]; },
       [&](int64_t, double v) { fsk_split_warm(z, b, a, v); },
       [&](int64_t kk, double v) {
+        [[maybe_unused]] double sz = 0.0;
+        if constexpr (ST) sz = fsk_step_sz(z);
         const double y = fsk_step<MODE>(z, b, a, v);
         const int64_t i = m1 - 1 - kk - pad;
         if (i >= 0 && i < n) zd[((size_t)s * n + fsk_zoff<LIVE>(p, i)) * 2 + tone] = y;
+        if constexpr (ST) {
+          const double dd = __builtin_fma(sp.u2, sz, __builtin_fma(kx, fabs(v), ky * fabs(y)));
+          dmax = fmax(dmax, dd);
+          dsum += dd;
+          if (++dcnt == kStrictBlk) {
+            dblk[kk / kStrictBlk] = dsum;
+            dsum = 0.0;
+            dcnt = 0;
+          }
+        }
       });
+  if constexpr (ST) {
+    if (dcnt > 0) dblk[(o1 - 1) / kStrictBlk] = dsum;
+    atomicMax(sp.bnd + ((size_t)s * 2 + tone) * 8 + 3, fsk_abs_bits(dmax));
+  }
+}
+
+// KF1 / KF2 (STRICT; split_strict.h, as the PSK split's KB1 / KB2 per tone):
+// thread = (forward block J, stream, tone) -- grid.y = 2 s + tone.
+//   E1[J]  the forward pass's error at output block J: both paths' rounding
+//          (block sums of D through W, the cut remainder at max D), the chunk
+//          starts' errors (+ truncation tk * peak) through GS;
+//   E2[J]  the backward pass's at forward block J: pass 1's rounding through
+//          pass 2 (K12), the start errors through |h| (HS), the last input's
+//          error through the zi start (TZ), its own rounding and starts.
+// max E2 = F bounds |z_split - z_serial| on every sample of the tone while the
+// a-posteriori caps hold (each pass's difference <= 2^-10 of its input peak).
+constexpr int kKfThreads = 256;
+constexpr double kKfTwo = 2.0 + 0x1p-20;
+struct KfRow {
+  double* row;
+  unsigned long long* bw;
+  double D1m, y1m, D2m, peak1, cap1, p2, cap2, c1;
+};
+__device__ __forceinline__ KfRow kf_row(const FskSplit& sp, int64_t s, int tone) {
+  const StrictBp& d = sp.sb[tone];
+  KfRow k;
+  k.row = fsk_strict_row(sp, s, tone);
+  k.bw = sp.bnd + ((size_t)s * 2 + tone) * 8;
+  k.D1m = __longlong_as_double((long long)k.bw[0]);
+  k.y1m = __longlong_as_double((long long)k.bw[2]);
+  k.D2m = __longlong_as_double((long long)k.bw[3]);
+  k.peak1 = __longlong_as_double((long long)sp.peak[s]);
+  k.cap1 = 0x1p-10 * k.peak1;
+  k.p2 = k.y1m + k.cap1;
+  k.cap2 = 0x1p-10 * k.p2;
+  const double sec1 = sp.u2 * d.zb * k.cap1 + d.ky * k.cap1;
+  k.c1 = d.g1x * (sec1 + 2 * 0x1p-1060) + d.gmax * 0x1p-53 * d.zi_sum * k.peak1;
+  return k;
+}
+__device__ __forceinline__ void kf_wave_max(unsigned long long* m, double v, bool live) {
+  unsigned long long x = live ? fsk_abs_bits(v) : 0ull;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(x, o);
+    x = y > x ? y : x;
+  }
+  if ((threadIdx.x & 63) == 0 && x != 0ull) atomicMax(m, x);
+}
+__global__ __launch_bounds__(kKfThreads) void k_fsk_strict_e1(FskSplit sp) {
+  const int64_t s = blockIdx.y >> 1;
+  const int tone = (int)(blockIdx.y & 1);
+  const int64_t J = (int64_t)blockIdx.x * kKfThreads + threadIdx.x;
+  const StrictBp& d = sp.sb[tone];
+  const KfRow k = kf_row(sp, s, tone);
+  const int64_t LB = sp.L / kStrictBlk;
+  const double* d1 = k.row;
+  const double* ds1 = k.row + fsk_strict_off_ds1(sp);
+  double e = 0.0, st = 0.0;
+  const bool live = J < sp.nb1;
+  if (live) {
+    double r = d.w_tail * k.D1m;
+    const int64_t dn = J + 1 < d.nw ? J + 1 : d.nw;
+    for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(d.W[dl], d1[J - dl], r);
+    const int64_t c = J / LB;
+    const int64_t q = J - c * LB;
+    st = c > 0 ? (q < 64 ? d.GS[q] : d.gmax) * (ds1[c] + d.tk * k.peak1) : 0.0;
+    e = kKfTwo * r + k.c1 + st;
+    k.row[fsk_strict_off_s1(sp) + J] = st;
+    k.row[fsk_strict_off_e1(sp) + J] = e;
+  }
+  kf_wave_max(k.bw + 1, e, live);
+  kf_wave_max(k.bw + 4, st, live);
+}
+__global__ __launch_bounds__(kKfThreads) void k_fsk_strict_e2(FskParams p, FskSplit sp) {
+  const int64_t s = blockIdx.y >> 1;
+  const int tone = (int)(blockIdx.y & 1);
+  const int64_t J = (int64_t)blockIdx.x * kKfThreads + threadIdx.x;
+  const StrictBp& d = sp.sb[tone];
+  const KfRow k = kf_row(sp, s, tone);
+  const int64_t nb1 = sp.nb1, m1 = p.n + 2 * (int64_t)p.pad, LB = sp.L / kStrictBlk;
+  const double* d1 = k.row;
+  const double* d2 = k.row + fsk_strict_off_d2(sp);
+  const double* ds2 = k.row + fsk_strict_off_ds2(sp);
+  const double* e1 = k.row + fsk_strict_off_e1(sp);
+  const double* s1 = k.row + fsk_strict_off_s1(sp);
+  const double E1max = __longlong_as_double((long long)k.bw[1]), S1max = __longlong_as_double((long long)k.bw[4]);
+  const double E1last = fmax(e1[nb1 - 1], nb1 > 1 ? e1[nb1 - 2] : 0.0);
+  const double sec2 = sp.u2 * d.zb * k.cap2 + d.kx * E1max + d.ky * k.cap2;
+  const double c2 = d.hz * k.c1 + d.g1x * (sec2 + 2 * 0x1p-1060) + 2.0 * d.gmax * 0x1p-53 * d.zi_sum * k.p2;
+  auto own2 = [&](int64_t K) {
+    if (K < 0 || K >= nb1) return 0.0;
+    double r = d.w_tail * k.D2m;
+    const int64_t dn = K + 1 < d.nw ? K + 1 : d.nw;
+    for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(d.W[dl], d2[K - dl], r);
+    const int64_t c = K / LB;
+    const int64_t q = K - c * LB;
+    const double st = c > 0 ? (q < 64 ? d.GS[q] : d.gmax) * (ds2[c] + d.tk * k.p2) : 0.0;
+    return kKfTwo * r + st;
+  };
+  auto tzw = [&](int64_t q) { return q < d.nz ? d.TZ[q] : d.tz_tail; };
+  double e = 0.0;
+  const bool live = J < nb1;
+  if (live) {
+    double a = d.k12_tail * k.D1m;
+    for (int64_t kq = 0; kq < d.nk; ++kq) {
+      const int64_t bb = J + kq - d.k12_off;
+      if (bb >= 0 && bb < nb1) a = __builtin_fma(d.K12[kq], d1[bb], a);
+    }
+    double h = d.hs_tail * S1max;
+    for (int64_t db = 0; db < d.nh && J + db < nb1; ++db) h = __builtin_fma(d.HS[db], s1[J + db], h);
+    const int64_t jhi = 16 * J + 15 < m1 - 1 ? 16 * J + 15 : m1 - 1;
+    const int64_t k2lo = m1 - 1 - jhi, k2hi = m1 - 1 - 16 * J;
+    const int64_t Ka = k2lo / kStrictBlk, Kb = k2hi / kStrictBlk;
+    const double tz = fmax(tzw(Ka), tzw(Kb)) * E1last;
+    const double o2 = fmax(own2(Ka), own2(Kb));
+    e = kKfTwo * a + h + tz + o2 + c2;
+    k.row[fsk_strict_off_e2(sp) + J] = e;
+  }
+  kf_wave_max(k.bw + 6, e, live);
 }
 
 // FS3: per stream, F2's margin scale from the input peak with the split's
-// tau (exact mode 2: +inf, every stream exact), and its flag word cleared
+// tau (exact mode 2: +inf, every stream exact), and its flag word cleared.
+// STRICT: tau = the plan's + max over the tones of F * ||ifft(h)||_1 / peak
+// (F from KF2), +inf when a tone's caps failed
 __global__ __launch_bounds__(64) void k_fsk_split_amb(int64_t n_streams, FskParams p, FskSplit sp) {
   const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (s >= n_streams) return;
   const double peak = __longlong_as_double((long long)sp.peak[s]);
-  p.amb[s] = p.force_exact ? __builtin_inf() : amb_scale(peak, sp.tau);
+  double tau = sp.tau;
+  bool ok = true;
+  if (sp.strict) {
+    double F = 0.0;
+    for (int t = 0; t < 2; ++t) {
+      const KfRow k = kf_row(sp, s, t);
+      const double E1max = __longlong_as_double((long long)k.bw[1]), Fm = __longlong_as_double((long long)k.bw[6]);
+      ok = ok && E1max <= k.cap1 && Fm <= k.cap2;   // false for NaN
+      F = fmax(F, Fm);
+    }
+    tau = p.tau + (peak > 0.0 ? F * sp.hl1 * (1.0 + 0x1p-40) / peak : 0.0);
+  }
+  p.amb[s] = p.force_exact || !ok ? __builtin_inf() : amb_scale(peak, tau);
   if ((s & 31) == 0) p.xflags[s >> 5] = 0u;
 }
 
-template <int MODE>
+template <int MODE, bool ST>
 static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride, int64_t B, double2* z,
                                      const FskParams& p, const FskIir& f, const FskSplit& sp, hipStream_t st) {
   const dim3 blk(64), g((unsigned)((2 * sp.c + 63) / 64), (unsigned)B);
@@ -811,22 +1001,27 @@ static hipError_t launch_fsk_split_t(int dtype, const void* x, int64_t x_stride,
   if (sp.conv && (!sp.ktab || !sp.z0tab || !sp.zs)) return hipErrorInvalidValue;
   if (sp.conv) {
     switch (dtype) {
-      case kF32: hipLaunchKernelGGL(k_fsk_split_state_fwd<float>, g0, blk0, 0, st, x, x_stride, p, sp); break;
-      case kF64: hipLaunchKernelGGL(k_fsk_split_state_fwd<double>, g0, blk0, 0, st, x, x_stride, p, sp); break;
-      case kI16: hipLaunchKernelGGL(k_fsk_split_state_fwd<int16_t>, g0, blk0, 0, st, x, x_stride, p, sp); break;
+      case kF32: hipLaunchKernelGGL((k_fsk_split_state_fwd<float, ST>), g0, blk0, 0, st, x, x_stride, p, sp); break;
+      case kF64: hipLaunchKernelGGL((k_fsk_split_state_fwd<double, ST>), g0, blk0, 0, st, x, x_stride, p, sp); break;
+      case kI16: hipLaunchKernelGGL((k_fsk_split_state_fwd<int16_t, ST>), g0, blk0, 0, st, x, x_stride, p, sp); break;
       default: return hipErrorInvalidValue;
     }
   }
   switch (dtype) {
-    case kF32: hipLaunchKernelGGL((k_fsk_split_fwd<float, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
-    case kF64: hipLaunchKernelGGL((k_fsk_split_fwd<double, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
-    case kI16: hipLaunchKernelGGL((k_fsk_split_fwd<int16_t, MODE>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    case kF32: hipLaunchKernelGGL((k_fsk_split_fwd<float, MODE, ST>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    case kF64: hipLaunchKernelGGL((k_fsk_split_fwd<double, MODE, ST>), g, blk, 0, st, x, x_stride, p, f, sp); break;
+    case kI16: hipLaunchKernelGGL((k_fsk_split_fwd<int16_t, MODE, ST>), g, blk, 0, st, x, x_stride, p, f, sp); break;
     default: return hipErrorInvalidValue;
   }
   double* zd = reinterpret_cast<double*>(z);
-  if (sp.conv) hipLaunchKernelGGL(k_fsk_split_state_bwd, g0, blk0, 0, st, p, sp);
-  if (p.lc.on) hipLaunchKernelGGL((k_fsk_split_bwd<MODE, true>), g, blk, 0, st, zd, p, f, sp);
-  else hipLaunchKernelGGL((k_fsk_split_bwd<MODE, false>), g, blk, 0, st, zd, p, f, sp);
+  if (sp.conv) hipLaunchKernelGGL((k_fsk_split_state_bwd<ST>), g0, blk0, 0, st, p, sp);
+  if (p.lc.on) hipLaunchKernelGGL((k_fsk_split_bwd<MODE, true, ST>), g, blk, 0, st, zd, p, f, sp);
+  else hipLaunchKernelGGL((k_fsk_split_bwd<MODE, false, ST>), g, blk, 0, st, zd, p, f, sp);
+  if constexpr (ST) {
+    const dim3 gk((unsigned)((sp.nb1 + kKfThreads - 1) / kKfThreads), (unsigned)(2 * B));
+    hipLaunchKernelGGL(k_fsk_strict_e1, gk, dim3(kKfThreads), 0, st, sp);
+    hipLaunchKernelGGL(k_fsk_strict_e2, gk, dim3(kKfThreads), 0, st, p, sp);
+  }
   if (p.amb) hipLaunchKernelGGL(k_fsk_split_amb, dim3((unsigned)((B + 63) / 64)), blk, 0, st, B, p, sp);
   return hipGetLastError();
 }
@@ -970,10 +1165,22 @@ hipError_t launch_fsk_split(int dtype, const void* x, int64_t x_stride, int64_t 
   if (B > 65535 || p.nt != 7 || sp.L < 1 || sp.c < 1) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(sp.peak, 0, (size_t)B * sizeof(unsigned long long), st);
   if (e != hipSuccess) return e;
+  if (sp.strict) {
+    e = hipMemsetAsync(sp.bnd, 0, (size_t)B * 2 * 8 * sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+  }
   const int mode = fsk_step_mode(f, false);
-  if (mode == 3) return launch_fsk_split_t<3>(dtype, x, x_stride, B, z, p, f, sp, st);
-  return mode == 1 ? launch_fsk_split_t<1>(dtype, x, x_stride, B, z, p, f, sp, st)
-                   : launch_fsk_split_t<0>(dtype, x, x_stride, B, z, p, f, sp, st);
+  if (sp.strict) {
+    // the strict bound covers the convolution starts and scipy's step order only
+    if (!sp.conv || !sp.sc || !sp.bnd || sp.L % kStrictBlk != 0 || !sp.sb[0].kabs || !sp.sb[1].kabs)
+      return hipErrorInvalidValue;
+    if (mode == 3) return launch_fsk_split_t<3, true>(dtype, x, x_stride, B, z, p, f, sp, st);
+    return mode == 1 ? launch_fsk_split_t<1, true>(dtype, x, x_stride, B, z, p, f, sp, st)
+                     : launch_fsk_split_t<0, true>(dtype, x, x_stride, B, z, p, f, sp, st);
+  }
+  if (mode == 3) return launch_fsk_split_t<3, false>(dtype, x, x_stride, B, z, p, f, sp, st);
+  return mode == 1 ? launch_fsk_split_t<1, false>(dtype, x, x_stride, B, z, p, f, sp, st)
+                   : launch_fsk_split_t<0, false>(dtype, x, x_stride, B, z, p, f, sp, st);
 }
 
 hipError_t launch_fsk_decide(const uint8_t* cmp, uint32_t* words, int64_t n_streams, const FskParams& p,

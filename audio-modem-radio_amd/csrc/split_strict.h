@@ -148,18 +148,17 @@ inline LD max_abs(const std::vector<LD>& v) {
 }
 }  // namespace strict_detail
 
-// bp, lp: the plan's filters; K [w1][8], Z0 [w1 + 1][8]: KS0's tables as the
-// device holds them; n, first, sps, n_sym: the plan's shape; w2: the low-pass
-// warm-up.  ok = false when a response does not decay (no strict mode).
-inline StrictDesign strict_design(const Iir& bp, const Iir& lp, const double* K, const double* Z0, int64_t w1,
-                                  int64_t w2, int64_t n, int64_t first, int64_t sps, int64_t n_sym) {
+// The band-pass half of the design (both filtfilt passes of one filter; the
+// FSK split's strict mode uses it per tone): bp the filter, K [w1][N], Z0
+// [w1 + 1][N] the convolution-start tables as the device holds them.  Fills
+// the band-pass fields and block kernels of d; false when a response does not
+// decay.
+inline bool strict_design_bp(const Iir& bp, const double* K, const double* Z0, int64_t w1, StrictDesign& d,
+                             const strict_detail::Responses& rb) {
   using namespace strict_detail;
-  StrictDesign d;
-  const Responses rb = responses(bp), rl = responses(lp);
-  if (!rb.ok || !rl.ok || w1 < 1 || n_sym < 2) return d;
-  const int N = bp.nt - 1, Nl = lp.nt - 1;
+  if (!rb.ok || w1 < 1) return false;
+  const int N = bp.nt - 1;
   const LD U = kU * std::pow(1.0L + kU, 4);
-  // ---- band-pass
   LD g1x = 1.0L, gmax = 0.0L;
   d.gm_pmax.resize(rb.gm.size());
   for (size_t m = 0; m < rb.gm.size(); ++m) {
@@ -223,60 +222,6 @@ inline StrictDesign strict_design(const Iir& bp, const Iir& lp, const double* K,
     LD s = 0.0L;
     for (int i = 0; i < N; ++i) s += std::fabs((LD)Z0[t * N + i]);
     d.z0abs[(size_t)t] = (double)up(s);
-  }
-  // ---- low-pass: the band-pass error X per sample reaches symbol k's sample
-  // t (ext index s = t + pad2) with at most lpc[k] X:
-  //   input weight w(s) = 3 on the odd extension (2 x[0] - x[k]), 1 inside;
-  //   A(s) = sum_{l <= s} |h(l)| w(s - l) + 3 |tz(s)|        (forward pass)
-  //   B(s) = sum_k |h(k)| A(s + k) + |tz(m2 - 1 - s)| A(m2 - 1)   (backward)
-  const int pad2 = 3 * lp.nt;
-  const int64_t m2 = n + 2 * (int64_t)pad2;
-  std::vector<LD> habs(rl.h.size());
-  for (size_t i = 0; i < habs.size(); ++i) habs[i] = std::fabs(rl.h[i]);
-  std::vector<LD> H(habs.size() + 1, 0.0L);   // H[i] = sum_{l < i} |h(l)|
-  for (size_t i = 0; i < habs.size(); ++i) H[i + 1] = H[i] + habs[i];
-  const LD h1 = H.back();
-  auto Hc = [&](int64_t s) -> LD {            // sum_{l <= s} |h(l)|
-    if (s < 0) return 0.0L;
-    return (size_t)(s + 1) < H.size() ? H[(size_t)s + 1] : h1;
-  };
-  auto tzs = [&](int64_t s) -> LD { return s >= 0 && (size_t)s < rl.tz.size() ? std::fabs(rl.tz[(size_t)s]) : 0.0L; };
-  auto A = [&](int64_t s) -> LD {
-    return Hc(s) + 2.0L * (Hc(s) - Hc(s - pad2)) + 2.0L * Hc(s - pad2 - n) + 3.0L * tzs(s);
-  };
-  const LD tail = 1e-30L * h1 * (3.0L * h1 + 3.0L);   // past the decayed responses
-  const LD Aend = A(m2 - 1);
-  d.lpc.resize((size_t)n_sym);
-  for (int64_t k = 0; k < n_sym; ++k) {
-    const int64_t s = first + k * sps + pad2;
-    LD B = 0.0L;
-    const int64_t kmax = std::min<int64_t>((int64_t)habs.size(), m2 - s);
-    for (int64_t q = 0; q < kmax; ++q) B += habs[(size_t)q] * A(s + q);
-    B += tzs(m2 - 1 - s) * Aend + tail;
-    d.lpc[(size_t)k] = (double)up(B);
-  }
-  // the low-pass's own rounding (split and serial, both passes), its warm-up
-  // truncation and the extension's rounding, per unit low-pass input peak P3
-  // (P3 = 3 (max|f| + X): the odd extension of f * lo)
-  {
-    LD cal = 0.0L, cbl = 0.0L;
-    for (int j = 1; j <= Nl; ++j) { cal += std::fabs((LD)lp.a[j]); cbl += std::fabs((LD)lp.b[j]); }
-    const LD kxl = 3.0L * cbl + std::fabs((LD)lp.b[0]) * cal, kyl = 3.0L * cal;
-    LD g1l = 1.0L;
-    for (LD g : rl.gm) g1l += g;
-    const LD hzl = h1 + max_abs(rl.tz);
-    // states <= zb P (incl. the zi start), outputs <= hzl P, for both paths:
-    // the split / serial difference is within the 2^-10 caps of P
-    const LD dstep = U * (2.0L * rl.zb + kxl + kyl * hzl) * (1.0L + 0x1p-8L);
-    const LD own3 = 2.0L * g1l * dstep;                 // pass 3 (input P3)
-    const LD own4 = 2.0L * g1l * dstep * hzl;           // pass 4 (input <= hzl P3)
-    LD tailg = 0.0L;                                    // sup_{m >= w2} max_j |g_j(m)|
-    for (size_t m = (size_t)std::max<int64_t>(w2, 0); m < rl.gm.size(); ++m) tailg = std::max(tailg, rl.gm[m]);
-    const LD trunc = 2.0L * tailg * rl.zb * hzl;        // both passes' dropped start states
-    const LD ext = 2.1L * kU * hzl * hzl;               // fl(2 x0 - x) of both paths, weight 1 (P3 already x3)
-    d.c3 = (double)up(own3 * hzl + own4 + trunc + ext + 1e-30L);
-    d.lp_kx = (double)kxl;
-    d.lp_ky = (double)kyl;
   }
   // ---- block kernels (long double, rounded up)
   {
@@ -368,6 +313,76 @@ inline StrictDesign strict_design(const Iir& bp, const Iir& lp, const double* K,
       for (int64_t m = (int64_t)q * BS; m < (int64_t)q * BS + BS && m < Mz; ++m) mx = std::max(mx, std::fabs(rb.tz[(size_t)m]));
       d.TZ[q] = (double)up(mx);
     }
+  }
+  return std::isfinite(d.g1x) && std::isfinite(d.hz) && std::isfinite(d.tk);
+}
+
+// bp, lp: the plan's filters; K [w1][8], Z0 [w1 + 1][8]: KS0's tables as the
+// device holds them; n, first, sps, n_sym: the plan's shape; w2: the low-pass
+// warm-up.  ok = false when a response does not decay (no strict mode).
+inline StrictDesign strict_design(const Iir& bp, const Iir& lp, const double* K, const double* Z0, int64_t w1,
+                                  int64_t w2, int64_t n, int64_t first, int64_t sps, int64_t n_sym) {
+  using namespace strict_detail;
+  StrictDesign d;
+  const Responses rb = responses(bp), rl = responses(lp);
+  if (!rl.ok || n_sym < 2 || !strict_design_bp(bp, K, Z0, w1, d, rb)) return d;
+  const int Nl = lp.nt - 1;
+  const LD U = kU * std::pow(1.0L + kU, 4);
+  // ---- low-pass: the band-pass error X per sample reaches symbol k's sample
+  // t (ext index s = t + pad2) with at most lpc[k] X:
+  //   input weight w(s) = 3 on the odd extension (2 x[0] - x[k]), 1 inside;
+  //   A(s) = sum_{l <= s} |h(l)| w(s - l) + 3 |tz(s)|        (forward pass)
+  //   B(s) = sum_k |h(k)| A(s + k) + |tz(m2 - 1 - s)| A(m2 - 1)   (backward)
+  const int pad2 = 3 * lp.nt;
+  const int64_t m2 = n + 2 * (int64_t)pad2;
+  std::vector<LD> habs(rl.h.size());
+  for (size_t i = 0; i < habs.size(); ++i) habs[i] = std::fabs(rl.h[i]);
+  std::vector<LD> H(habs.size() + 1, 0.0L);   // H[i] = sum_{l < i} |h(l)|
+  for (size_t i = 0; i < habs.size(); ++i) H[i + 1] = H[i] + habs[i];
+  const LD h1 = H.back();
+  auto Hc = [&](int64_t s) -> LD {            // sum_{l <= s} |h(l)|
+    if (s < 0) return 0.0L;
+    return (size_t)(s + 1) < H.size() ? H[(size_t)s + 1] : h1;
+  };
+  auto tzs = [&](int64_t s) -> LD { return s >= 0 && (size_t)s < rl.tz.size() ? std::fabs(rl.tz[(size_t)s]) : 0.0L; };
+  auto A = [&](int64_t s) -> LD {
+    return Hc(s) + 2.0L * (Hc(s) - Hc(s - pad2)) + 2.0L * Hc(s - pad2 - n) + 3.0L * tzs(s);
+  };
+  const LD tail = 1e-30L * h1 * (3.0L * h1 + 3.0L);   // past the decayed responses
+  const LD Aend = A(m2 - 1);
+  d.lpc.resize((size_t)n_sym);
+  for (int64_t k = 0; k < n_sym; ++k) {
+    const int64_t s = first + k * sps + pad2;
+    LD B = 0.0L;
+    const int64_t kmax = std::min<int64_t>((int64_t)habs.size(), m2 - s);
+    for (int64_t q = 0; q < kmax; ++q) B += habs[(size_t)q] * A(s + q);
+    B += tzs(m2 - 1 - s) * Aend + tail;
+    d.lpc[(size_t)k] = (double)up(B);
+  }
+  // the low-pass's own rounding (split and serial, both passes), its warm-up
+  // truncation and the extension's rounding, per unit low-pass input peak P3
+  // (P3 = 3 (max|f| + X): the odd extension of f * lo)
+  {
+    LD cal = 0.0L, cbl = 0.0L;
+    for (int j = 1; j <= Nl; ++j) { cal += std::fabs((LD)lp.a[j]); cbl += std::fabs((LD)lp.b[j]); }
+    const LD kxl = 3.0L * cbl + std::fabs((LD)lp.b[0]) * cal, kyl = 3.0L * cal;
+    LD g1l = 1.0L;
+    for (LD g : rl.gm) g1l += g;
+    const LD hzl = h1 + max_abs(rl.tz);
+    // states <= zb P (incl. the zi start), outputs <= hzl P, for both paths:
+    // the split / serial difference is within the 2^-10 caps of P
+    const LD dstep = U * (2.0L * rl.zb + kxl + kyl * hzl) * (1.0L + 0x1p-8L);
+    const LD own3 = 2.0L * g1l * dstep;                 // pass 3 (input P3)
+    const LD own4 = 2.0L * g1l * dstep * hzl;           // pass 4 (input <= hzl P3)
+    LD tailg = 0.0L;                                    // sup_{m >= w2} max_j |g_j(m)|
+    for (size_t m = (size_t)std::max<int64_t>(w2, 0); m < rl.gm.size(); ++m) tailg = std::max(tailg, rl.gm[m]);
+    const LD trunc = 2.0L * tailg * rl.zb * hzl;        // both passes' dropped start states
+    const LD ext = 2.1L * kU * hzl * hzl;               // fl(2 x0 - x) of both paths, weight 1 (P3 already x3)
+    d.c3 = (double)up(own3 * hzl + own4 + trunc + ext + 1e-30L);
+    d.lp_kx = (double)kxl;
+    d.lp_ky = (double)kyl;
+  }
+  {
     // low-pass radius: |h_lp| mass beyond R / 2 below kStrictCut h1 -> pairs (k, l) with |k - l| > R
     // carry at most 2 h1 rem (x 3: the extension's weight)
     LD rem = 0.0L;

@@ -72,7 +72,8 @@ extern "C" {
                                   amr_fsk_demod_host_edges / _device_edges (the odd extension as the
                                   caller's dtype forms it); the PSK split's strict mode
                                   (amr_psk_plan_set_split_strict ...); F2's margin from a standard
-                                  FFT rounding bound (amr_fsk_fft_margin, amr_fsk_plan_margin) */
+                                  FFT rounding bound (amr_fsk_fft_margin, amr_fsk_plan_margin); the FSK
+                                  split's strict mode (amr_fsk_plan_set_split_strict ...) */
 
 #define AMR_OK 0
 #define AMR_E_INVALID -1      /* bad argument */
@@ -429,6 +430,28 @@ int amr_fsk_plan_margin(amr_fsk_plan *plan, double *tau, double *tau_split);
  * length n.  Returns AMR_E_INVALID when the filters cannot be split at n. */
 int amr_fsk_split_design(int64_t n_samples, const double *mark_b, const double *mark_a, const double *space_b,
                          const double *space_a, int ntaps, int64_t *warmup, double *kappa, double *hilbert_l1);
+/* The FSK split F1's STRICT mode (fsk_kernels.hip FS0-FS2 with
+ * their step bounds, KF1-KF2): F2's margin for a split call becomes tau +
+ * F ||ifft(h)||_1 / peak with F a bound on |z_split - z_serial| per tone that
+ * holds for every input (the PSK strict mode's band-pass analysis per tone),
+ * instead of tau + kappa ||ifft(h)||_1 (a measured premise).  Set: 1 on, 0
+ * off, -1 the process default (AMR_FSK_SPLIT_STRICT=0 / 1).  split_strict:
+ * whether this plan's split calls use it; last_strict: whether the last did. */
+int amr_fsk_plan_set_split_strict(amr_fsk_plan *plan, int mode);
+int amr_fsk_plan_split_strict(amr_fsk_plan *plan);
+int amr_fsk_plan_last_strict(amr_fsk_plan *plan);
+/* The strict band-pass design of ONE filter (host arithmetic; the tests'
+ * restatement reads it): w the plan's warm-up (amr_fsk_split_design), consts
+ * [32] in amr_psk_split_strict_design's layout (the low-pass fields 0), tabs
+ * (NULL: not written) = kabs [w] | z0abs [w + 1] | W | K12 | HS | GS | TZ. */
+int amr_fsk_split_strict_design(const double *b, const double *a, const double *zi, int ntaps, int64_t w,
+                                double *consts, double *tabs);
+/* Diagnostic (tests): the strict split F1 over a host batch: z_out
+ * [n_streams][n_samples][2] (mark, space), bnd_out [n_streams][2][8] the
+ * per-tone maxima as doubles (D1max, E1max, max|y1|, D2max, S1max, -, F, -),
+ * peak_out [n_streams] max |ext x|.  Synchronous. */
+int amr_fsk_split_bounds_host(amr_fsk_plan *plan, const void *x, int dtype, int64_t n_streams, int64_t x_stride,
+                              double *z_out, double *bnd_out, double *peak_out);
 /* the split F1's band-pass output itself (a diagnostic the tests compare with
  * the oracle's restatement): out [n_streams][n_samples][2] (mark, space);
  * chunk 0 = the plan's rule (1..127 refused with the convolution starts on,

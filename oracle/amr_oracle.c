@@ -509,8 +509,11 @@ static void chunked_pass_conv_stats(const double *b, const double *a, int nt, co
         double dsum = 0.0;
         int cnt = 0;
         for (int64_t j = o0; j < o1; ++j) {
-            const double sz = ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) +
-                              ((fabs(z[5]) + fabs(z[6])) + fabs(z[7]));
+            /* the kernels' pairing: 8 states (psk_split_kernels.hip step_bound_pre),
+             * 6 states (fsk_kernels.hip fsk_step_sz) */
+            const double sz = nt == 9 ? ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) +
+                                            ((fabs(z[5]) + fabs(z[6])) + fabs(z[7]))
+                                      : ((fabs(z[1]) + fabs(z[2])) + (fabs(z[3]) + fabs(z[4]))) + fabs(z[5]);
             df2t(b, a, nt, z, in + j, &out[j], 1, 1);
             const double dd = fma(cst[0], sz, fma(cst[1], fabs(in[j]), cst[2] * fabs(out[j])));
             if (dd > *dmax) *dmax = dd;
@@ -608,15 +611,16 @@ int64_t oracle_psk_split_symbols(const void *x, int dtype, int64_t n, int64_t sp
  * (restating the device's; tests compute the bound from them): d1, d2 [nb1]
  * the passes' per-block step bound sums (nb1 = ceil(m1 / 16)), ds1, ds2 [c1]
  * their chunk-start bounds (c1 = ceil(m1 / L)), stats[4] = D1max, max|y1|,
- * D2max, max|f|.  Returns 0, or -1 for bad arguments (bp_nt must be 9: the
- * kernels' 8 states; L a multiple of 16). */
+ * D2max, max|f|.  Returns 0, or -1 for bad arguments (bp_nt 9: the PSK
+ * kernels' 8 states, or 7: the FSK split F1's 6 (fsk_kernels.hip FS0-FS2 with
+ * the strict step bounds, one tone); L a multiple of 16). */
 int oracle_psk_split_stats(const void *x, int dtype, int64_t n, const double *bp_b, const double *bp_a, int bp_nt,
                            int64_t L, int64_t w1, const double *K, const double *Z0, const double *kabs,
                            const double *z0abs, const double *cst, double *d1, double *d2, double *ds1, double *ds2,
                            double *stats)
 {
     const int pad1 = 3 * bp_nt;
-    if (bp_nt != 9 || n <= pad1 || L < 16 || L % 16 || !K || !Z0) return -1;
+    if ((bp_nt != 9 && bp_nt != 7) || n <= pad1 || L < 16 || L % 16 || !K || !Z0) return -1;
     const int64_t m1 = n + 2 * (int64_t)pad1;
     double *e = (double *)malloc(sizeof(double) * (size_t)m1);
     double *y = (double *)malloc(sizeof(double) * (size_t)m1);

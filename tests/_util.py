@@ -79,17 +79,16 @@ def pass1_peak(x, pad1=27) -> float:
     return float(max(np.abs(np.asarray(x, dtype=np.float64)).max(), np.abs(oracle.odd_edges(x, pad1)).max()))
 
 
-def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
-    """The strict mode's per-symbol bound e(k) on each symbol component's
-    |split - reference| (psk_split_kernels.hip KB, restated in numpy) from a
-    stream's split statistics st (oracle.psk_split_stats / the device's) and
-    the design d (_amr.split_strict_design); peak1 = pass1_peak(x).  Returns (e [S], (E1max, Fmax,
-    Xmax, P3, ok))."""
+def strict_pass_bounds(st, d, peak1, n, L, pad1):
+    """The strict bound of a split filtfilt band-pass (psk_split_kernels.hip
+    KB1-KB2 / fsk_kernels.hip KF1-KF2, restated in numpy) from its statistics
+    st (oracle.psk_split_stats / fsk_split_stats) and design d: E1 / E2 per
+    forward block, their maxima, the caps and whether they hold."""
     import numpy as np
     u, eta, two = 2.0 ** -53, 2.0 ** -1060, 2.0 + 2.0 ** -20
     BS = 16
     m1 = n + 2 * pad1
-    nb1, nbs, LB = -(-m1 // BS), -(-n // BS), L // BS
+    nb1, LB = -(-m1 // BS), L // BS
     d1, d2, ds1, ds2 = st["d1"], st["d2"], st["ds1"], st["ds2"]
     D1m, y1m, D2m, fm0 = st["D1max"], st["y1max"], st["D2max"], st["fmax"]
     cap1 = 2.0 ** -10 * peak1
@@ -133,14 +132,29 @@ def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
     o2 = np.maximum(own2[np.clip(Ka, 0, nb1 - 1)], own2[np.clip(Kb, 0, nb1 - 1)])
     E2 = two * A + H + tz + o2 + c2
     Fmax = E2.max()
-    fm = fm0 + Fmax
+    return dict(E1=E1, E2=E2, E1max=E1max, Fmax=Fmax, cap1=cap1, cap2=cap2, fm0=st["fmax"],
+                ok=bool(E1max <= cap1 and Fmax <= cap2))
+
+
+def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
+    """The strict mode's per-symbol bound e(k) on each symbol component's
+    |split - reference| (psk_split_kernels.hip KB, restated in numpy) from a
+    stream's split statistics st (oracle.psk_split_stats / the device's) and
+    the design d (_amr.split_strict_design); peak1 = pass1_peak(x).  Returns (e [S], (E1max, Fmax,
+    Xmax, P3, ok))."""
+    import numpy as np
+    BS = 16
+    pb = strict_pass_bounds(st, d, peak1, n, L, pad1)
+    E2, E1max, Fmax = pb["E2"], pb["E1max"], pb["Fmax"]
+    nbs = -(-n // BS)
+    fm = pb["fm0"] + Fmax
     fb = np.arange(nbs)
     ilo, ihi = 16 * fb, np.minimum(16 * fb + 15, n - 1)
     Fb = np.maximum(E2[(ilo + pad1) // BS], E2[(ihi + pad1) // BS])
     X = Fb * (1 + 2.0 ** -50) + 2.0 ** -52 * 1.0078125 * fm
     Xmax = X.max()
     P3 = 3.0 * (fm + Xmax)
-    ok = bool(E1max <= cap1 and Fmax <= cap2)
+    ok = pb["ok"]
     S = d["lpc"].size
     t = first + np.arange(S) * sps
     lo = t - int(d["lp_rad"]) - pad2

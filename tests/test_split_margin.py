@@ -282,3 +282,88 @@ def test_strict_bound_holds(kind, baud, fc, fs, built_lib):
           f"(kappa / worst = {sd['kappa'] / max(adv_worst, 1e-300):.1f})")
     assert not bad, bad
     assert adv_worst <= sd["kappa"] / 16
+
+
+# ---- the FSK split F1's strict bound (fsk_kernels.hip KF1-KF2, round 6) -----
+def _fsk_adversarial(baud, mark, space, fs, n, rng):
+    """The PSK adversarial set (above) aimed at the FSK tones' band-passes:
+    square waves at every pole frequency of both filters, the sign pattern of
+    each filter's slowest state response, a clipped full-scale FSK frame, a
+    frame with full-scale edge clicks, a chirp across both bands."""
+    import _fsk
+    import synth
+    _, tones = _fsk.design_fsk(n, baud, mark, space, fs)
+    ins = {}
+    for tn, (b, a, _) in zip("ms", tones):
+        poles = np.roots(a)
+        for i, p in enumerate(sorted({round(abs(float(np.angle(q))), 9) for q in poles if np.angle(q) > 0})):
+            ins[f"pole_sq_{tn}{i}"] = np.sign(np.sin(p * np.arange(n) + 0.3))
+        z = np.zeros(len(a) - 1)
+        z[0] = 1.0
+        g = []
+        for _ in range(4096):
+            y = z[0]
+            g.append(y)
+            z = np.append(z[1:], 0.0) - a[1:] * y
+        pat = np.sign(np.array(g[::-1]))
+        pat[pat == 0] = 1.0
+        ins[f"g_sign_{tn}"] = np.resize(pat, n)
+    w = synth.fsk_waveform(synth.random_frame(rng, 200), baud, mark, space, float(fs))
+    x = np.zeros(n)
+    x[:min(n, w.size)] = w[:n]
+    ins["clipped"] = np.clip(4.0 * x + rng.normal(0, 0.05, n), -1, 1)
+    xc = x.copy()
+    xc[0], xc[-1] = 1.0, -1.0
+    ins["edge_clicks"] = xc
+    t = np.arange(n) / fs
+    lo, hi = max(10.0, 0.7 * (mark - baud)), min(0.49 * fs, 1.3 * (space + baud))
+    ins["chirp"] = np.sin(2 * np.pi * (lo * t + (hi - lo) * t * t / (2 * t[-1])))
+    return ins
+
+
+@pytest.mark.parametrize("baud,mark,space,fs", FSK_CONFIGS, ids=lambda v: str(v))
+def test_fsk_strict_bound_holds(baud, mark, space, fs, built_lib):
+    """The FSK split F1's strict bound per tone (KF1-KF2 restated:
+    tests/_util.py strict_pass_bounds over the oracle's FS0-FS2 statistics and
+    libamr.so's per-tone design) is at least the measured max |split - serial|
+    of the tone's band-pass output, over the signal classes and the
+    adversarial set, at two chunk lengths; its size against kappa peak is
+    printed.  The adversarial set's measured error is also held against the
+    default kappa: kappa / worst >= 16."""
+    import _amr
+    import _fsk
+    from oracle import oracle
+    from _util import pass1_peak, strict_pass_bounds
+    n = 48000
+    sd = _fsk.split_design(n, baud, mark, space, fs)
+    D = _fsk.split_strict_design(n, baud, mark, space, fs)
+    assert sd is not None and D is not None and all(d["ok"] == 1.0 for d in D)
+    _, tones = _fsk.design_fsk(n, baud, mark, space, fs)
+    T = [_amr.state_tables(b, a, zi, sd["warmup"]) for b, a, zi in tones]
+    rng = np.random.default_rng(7 * baud + int(space))
+    ins = _fsk_inputs(baud, mark, space, fs, n, rng)
+    adv = _fsk_adversarial(baud, mark, space, fs, n, rng)
+    ins.update(adv)
+    worst_ratio, size, adv_worst, bad = np.inf, [], 0.0, []
+    for name, x in ins.items():
+        p1 = pass1_peak(x, 21)
+        peak = np.abs(x).max()
+        for t, (b, a, zi) in enumerate(tones):
+            ref = oracle.filtfilt(b, a, x)
+            for L in (128, 1024):
+                st = oracle.fsk_split_stats(x, b, a, L, sd["warmup"], T[t], D[t])
+                pb = strict_pass_bounds(st, D[t], p1, n, L, 21)
+                sp = oracle.split_filtfilt(b, a, x, L, sd["warmup"], tables=T[t])
+                act = float(np.abs(sp - ref).max())
+                if pb["ok"]:
+                    if act > pb["Fmax"]:
+                        bad.append((name, t, L, act, pb["Fmax"]))
+                    worst_ratio = min(worst_ratio, pb["Fmax"] / max(act, 1e-300))
+                    size.append(pb["Fmax"] / (sd["kappa"] * peak))
+                if name in adv:
+                    adv_worst = max(adv_worst, act / peak)
+    print(f"fsk@{baud} {mark:g}/{space:g} fs {fs}: strict F / measured >= {worst_ratio:.1f}; median F "
+          f"{np.median(size):.2f}x kappa peak; adversarial worst |split - serial| / peak {adv_worst:.3e} "
+          f"(kappa / worst = {sd['kappa'] / max(adv_worst, 1e-300):.1f})")
+    assert not bad, bad
+    assert adv_worst <= sd["kappa"] / 16
