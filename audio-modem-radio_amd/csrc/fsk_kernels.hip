@@ -979,7 +979,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_amb(int64_t n_streams, FskPara
   const double peak = __longlong_as_double((long long)sp.peak[s]);
   double tau = sp.tau;
   bool ok = true;
-  if (sp.strict) {
+  if (sp.strict && peak != 0.0) {   // (an all-zero stream: exact zeros on both paths, never flagged)
     double F = 0.0;
     for (int t = 0; t < 2; ++t) {
       const KfRow k = kf_row(sp, s, t);
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(64) void k_fsk_split_amb(int64_t n_streams, FskPara
       ok = ok && E1max <= k.cap1 && Fm <= k.cap2;   // false for NaN
       F = fmax(F, Fm);
     }
-    tau = p.tau + (peak > 0.0 ? F * sp.hl1 * (1.0 + 0x1p-40) / peak : 0.0);
+    tau = p.tau + F * sp.hl1 * (1.0 + 0x1p-40) / peak;
   }
   p.amb[s] = p.force_exact || !ok ? __builtin_inf() : amb_scale(peak, tau);
   if ((s & 31) == 0) p.xflags[s >> 5] = 0u;

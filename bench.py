@@ -708,6 +708,19 @@ def fsk_dropin_path(xh, out_dev, len_dev, baud, mark, space):
         oracle.fsk_demodulate(xh[i], **args)
         tc.append(time.perf_counter() - t1)
     info = plan1.split_info()
+    info["strict"] = plan1.last_strict()
+    info["margin"] = plan1.margin()
+    # round 5's kappa margin on the same captures (AMR_FSK_SPLIT_STRICT=0): latency and exact-path count
+    plan1.set_split_strict(False)
+    tk, fk = [], 0
+    for i in range(n1):
+        t1 = time.perf_counter()
+        r = modem.fsk_demodulate(xh[i], **args)
+        tk.append(time.perf_counter() - t1)
+        same &= r == out_dev[i, :len_dev[i]].tobytes()
+        fk += plan1.exact_streams()
+    plan1.set_split_strict(None)
+    info["kappa_margin"] = {"ms": round(float(np.median(tk)) * 1e3, 3), "flagged_of": f"{fk}/{n1}"}
     # a capture that opens with digital silence (as a padded WAV does): its
     # compares there sit inside the margin, so the call also runs the exact
     # path (the serial F1 again, then pocketfft's envelopes)
