@@ -1038,9 +1038,13 @@ bool fsk_geometry(int64_t n, int64_t sps, int nt, int64_t max_streams, FskGeom& 
   g.six = g.sh.six ? 2 * max_streams * M * 16 : 0;
   g.out = max_streams * (g.out_cap + 16 + 2 * (int64_t)p.pad * 8);   // host-API output staging + edge table
   // (+ FS0's tables, w <= n / 4, and start states at L >= kFskSplitConvMinL)
+  // (+ the strict margin's per-tone scratch: 5 blocks rows of ceil(m1 / 16) and
+  // two chunk rows, the maxima, and the tables -- W, K12, HS, TZ <= 4 w / 16 + 64 each)
+  const int64_t m1g = n + 2 * (int64_t)p.pad;
+  const int64_t strict_row = 5 * ((m1g + kStrictBlk - 1) / kStrictBlk) + 2 * (m1g / kFskSplitConvMinL + 2);
   g.split = std::min<int64_t>(max_streams, kFskSplitMaxStreams) *
-                (2 * (n + 2 * (int64_t)p.pad) * 8 + 8 + 96 * ((n + 2 * (int64_t)p.pad) / kFskSplitConvMinL + 2)) +
-            2 * (2 * (n / 4) + 1) * 48;
+                (2 * m1g * 8 + 8 + 96 * (m1g / kFskSplitConvMinL + 2) + 2 * (strict_row * 8 + 64)) +
+            2 * (2 * (n / 4) + 1) * 48 + 2 * (2 * (n / 4) + 1 + 4 * (2 * (n / 4) / 16 + 64) + 64) * 8;
   // the exact path (AMR_FSK_EXACT=0: off), at every length with decisions to make
   static const bool exact_env = [] { const char* e = std::getenv("AMR_FSK_EXACT"); return !(e && e[0] == '0'); }();
   g.exact = exact_env && p.n_bits > 0;
@@ -1450,7 +1454,7 @@ int64_t amr_fsk_plan_scratch_bytes(const amr_fsk_plan* plan) {
   // d_x, or dd on a plan that keeps z)
   return plan->scratch_bytes + plan->staging_bytes + (plan->dd ? 0 : plan->dd_bytes) +
          plan->max_streams * (plan->out_cap + 16 + 2 * (int64_t)plan->p.pad * 8) +
-         std::max(plan->split_reserved, plan->split_alloc);   // == fsk_geometry().total() (split calls <= 1024 streams)
+         std::max(plan->split_reserved, plan->split_alloc + plan->strict_bytes);   // == fsk_geometry().total() (split calls <= 1024 streams)
 }
 int64_t amr_fsk_plan_resident_bytes(const amr_fsk_plan* plan) {
   if (!plan) return -1;

@@ -357,9 +357,12 @@ def test_fsk_device_entry_lean_plan():
     total = pl.scratch_bytes()
     lean = pl.resident_bytes()
     # counted, allocated by the first split call: the forward outputs, peaks,
-    # FS0's start states (chunks >= 128) and tables (w <= n / 4)
+    # FS0's start states (chunks >= 128) and tables (w <= n / 4), and the
+    # strict margin's per-tone scratch, maxima and tables
     m1 = n + 42
-    split_reserved = min(B, 1024) * (2 * m1 * 8 + 8 + 96 * (m1 // 128 + 2)) + 2 * (2 * (n // 4) + 1) * 48
+    strict_row = 5 * (-(-m1 // 16)) + 2 * (m1 // 128 + 2)
+    split_reserved = (min(B, 1024) * (2 * m1 * 8 + 8 + 96 * (m1 // 128 + 2) + 2 * (strict_row * 8 + 64)) +
+                      2 * (2 * (n // 4) + 1) * 48 + 2 * (2 * (n // 4) + 1 + 4 * (2 * (n // 4) // 16 + 64) + 64) * 8)
     dd = B * n * 6 // 10 * 16            # the dead columns' transform: nd / n1 = 6 / 10 at sps 10
     assert total - lean >= dd, (total, lean, dd)
     got, _ = fsk_device_demod(pl, x)
