@@ -567,10 +567,19 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e(PskParams p, PskS
 
 // KS5: one thread per (stream, 32-bit word): the differential products of the
 // word's symbols in numpy's fma form, the reference's decision (qpsk_dibit /
-// real < 0, as K4a), and the margin: |s| <= |s|_1, a symbol's error <= E, so
-// |d error|_1 <= sqrt2 E (|s0|_1 + |s1|_1 + E) (+ forming d's own rounding);
+// real < 0, as K4a), and the margin: a symbol's error <= E, so |d error|_1
+// <= sqrt2 E (|s0|_2 + |s1|_2 + E) (+ forming d's own rounding; |s|_2 from
+// above, norm2_up -- round 6; |s|_1 before, up to sqrt2 wider at QPSK's angles);
 // a decision closer than that to its boundary -- QPSK's diagonals
 // ||di| - |dr|| (K4a's 2^-29 sliver on top), BPSK's dr = 0 -- flags the stream
+// an upper bound on |s|_2 = hypot(re, im): the rounded sqrt of the rounded
+// sum of squares is within 4u of it, so x (1 + 2^-50) covers it; |s|_1 (a1,
+// always an upper bound) where the squares could underflow or it is smaller
+__device__ __forceinline__ double norm2_up(double re, double im, double a1) {
+  if (!(a1 >= 0x1p-500 && a1 <= 0x1p500)) return a1;
+  const double r = sqrt(__builtin_fma(re, re, im * im)) * (1.0 + 0x1p-50);
+  return r < a1 ? r : a1;
+}
 __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t w = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -598,10 +607,11 @@ __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p,
     const double bi = -bi0;
     const double dr = __builtin_fma(pr, br, -(pim * bi));
     const double a0 = fabs(br) + fabs(bi), a1 = fabs(pr) + fabs(pim);
+    const double r0 = norm2_up(br, bi, a0), r1 = norm2_up(pr, pim, a1);
     const double e1 = sp.strict ? esym(k + 1) : E;
-    // |d error|_1 <= sqrt2 (e1 |s0|_2 + e0 |s1|_2 + e0 e1), |s|_2 <= |s|_1
-    const double md = sp.strict ? sq2 * ((e1 * a0 + e0 * a1) + e0 * e1) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1)
-                                : sq2 * E * (a0 + a1 + E) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
+    // |d error|_1 <= sqrt2 (e1 |s0|_2 + e0 |s1|_2 + e0 e1) (r: upper bounds on |s|_2)
+    const double md = sp.strict ? sq2 * ((e1 * r0 + e0 * r1) + e0 * e1) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1)
+                                : sq2 * E * (r0 + r1 + E) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
     e0 = e1;
     if (qpsk) {
       const double di = __builtin_fma(pr, bi, pim * br);
