@@ -567,9 +567,10 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e(PskParams p, PskS
 
 // KS5: one thread per (stream, 32-bit word): the differential products of the
 // word's symbols in numpy's fma form, the reference's decision (qpsk_dibit /
-// real < 0, as K4a), and the margin: a symbol's error <= E, so |d error|_1
-// <= sqrt2 E (|s0|_2 + |s1|_2 + E) (+ forming d's own rounding; |s|_2 from
-// above, norm2_up -- round 6; |s|_1 before, up to sqrt2 wider at QPSK's angles);
+// real < 0, as K4a), and the margin: a symbol's error <= E, so |d error|_2
+// <= E (|s0|_2 + |s1|_2 + E), times sqrt2 for QPSK's L1 use (+ forming d's own
+// rounding; |s|_2 from above, norm2_up -- round 6; before it |s|_1 and the
+// sqrt2 for BPSK too, up to 2x wider);
 // a decision closer than that to its boundary -- QPSK's diagonals
 // ||di| - |dr|| (K4a's 2^-29 sliver on top), BPSK's dr = 0 -- flags the stream
 // an upper bound on |s|_2 = hypot(re, im): the rounded sqrt of the rounded
@@ -609,9 +610,10 @@ __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p,
     const double a0 = fabs(br) + fabs(bi), a1 = fabs(pr) + fabs(pim);
     const double r0 = norm2_up(br, bi, a0), r1 = norm2_up(pr, pim, a1);
     const double e1 = sp.strict ? esym(k + 1) : E;
-    // |d error|_1 <= sqrt2 (e1 |s0|_2 + e0 |s1|_2 + e0 e1) (r: upper bounds on |s|_2)
-    const double md = sp.strict ? sq2 * ((e1 * r0 + e0 * r1) + e0 * e1) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1)
-                                : sq2 * E * (r0 + r1 + E) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
+    // |d error|_2 <= e1 |s0|_2 + e0 |s1|_2 + e0 e1 (r: upper bounds on |s|_2); QPSK's
+    // |di| - |dr| moves by at most its L1 norm (x sqrt2), BPSK's dr by the L2 norm itself
+    const double dx = sp.strict ? (e1 * r0 + e0 * r1) + e0 * e1 : E * (r0 + r1 + E);
+    const double md = (qpsk ? sq2 * dx : dx) * (1.0 + 0x1p-40) + 0x1p-48 * (a0 * a1);
     e0 = e1;
     if (qpsk) {
       const double di = __builtin_fma(pr, bi, pim * br);
