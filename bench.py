@@ -888,6 +888,7 @@ def dropin_path(xh, baud, sym_per_stream, out_dev, len_dev):
     # one capture at a time with the strict margin: latency and how many of
     # the captures went to the serial kernels
     plan1.set_split_strict(True)
+    modem.qpsk_demodulate(np.ascontiguousarray(xh[n1 % B]), baud=baud)   # the strict design and scratch, once
     ts, flagged, same = [], 0, True
     for i in range(n1):
         xi = np.ascontiguousarray(xh[i])
