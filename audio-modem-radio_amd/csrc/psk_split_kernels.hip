@@ -32,9 +32,11 @@
 //     csrc/split_strict.h; a pass whose error exceeds 2^-10 of its input's
 //     peak flags the stream instead).  E = e(k) then, and the margin below is
 //     a proof.
-//   * either way a differential product whose decision could move by E --
-//     QPSK ||di| - |dr|| or BPSK |dr| within sqrt2 E (|s0| + |s1| + E) --
-//     flags its stream (so does exact silence: every zero product is flagged);
+//   * either way a differential product whose decision could move by its
+//     error -- |d error|_2 <= E (|s0|_2 + |s1|_2 + E) (strict: e1 |s0|_2 +
+//     e0 |s1|_2 + e0 e1, e = a bound on the symbol's complex error), times
+//     sqrt2 for QPSK's ||di| - |dr||, not for BPSK's |dr| -- flags its stream
+//     (so does exact silence: every zero product is flagged);
 //   * a flagged stream's batch is recomputed by the serial row-layout kernels
 //     (psk_kernels.hip: bit-exact), launched behind these ones and gated on
 //     the flag count on the device (they exit at once when it is zero).
@@ -395,8 +397,10 @@ __global__ __launch_bounds__(64) void k_split_lp_bwd(PskBuffers buf, PskParams p
 //              start errors through |h| (HS), the last input's error through the
 //              zi start (TZ), its own rounding and starts (in its own block index)
 //   KB3 X[fb]  the mixer's output error over sample block fb
-//   KB4 e(k)   lpc[k] x the largest X within the low-pass's reach of symbol k
-//              (and the extension's source blocks), + the cut remainder, + c3 P3
+//   KB4 e(k)   the symbol's complex error: lpc[k] x the largest X within the
+//              low-pass's reach of symbol k (and the extension's source blocks)
+//              + the cut remainder (one complex sum through the unit-modulus
+//              mixer), + sqrt2 x the per-component roundings (mixer, c3 P3)
 // The serial's rounding is the split's within the a-posteriori caps (each
 // pass's difference <= 2^-10 of its input peak; a stream past them gets e =
 // inf: flagged).  Every sum is of non-negative terms; the final factor
@@ -547,13 +551,19 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e(PskParams p, PskS
   const double P3 = 3.0 * (fm + Xmax);
   const bool ok = E1max <= k.cap1 && Fmax <= k.cap2;      // false for NaN
   if (kk < S) {
-    const double tailc = sp.lp_tail * Xmax + sp.c3 * P3;
+    // the symbol's complex error: the band-pass error f reaches it through the
+    // mixer's unit-modulus lo (|lo| <= 1 + 2u) and the real low-pass kernel, so
+    // as one complex sum, |.|_2 <= (lpc xw + lp_tail Xmax)(1 + 2^-50); the
+    // per-component roundings (the mixer's rho, the low-pass's own c3 P3) are
+    // independent per component: sqrt2 on those alone
+    const double rho = 0x1.02p-52 * fm;
+    const double t0 = sp.lp_tail * Xmax, t1 = 0x1.6a09e667f3bcdp+0 * ((sp.lpc[kk] + sp.lp_tail) * rho + sp.c3 * P3);
     const int64_t t = p.first + kk * p.sps;
     const int64_t lo = t - sp.lp_rad - p.pad2, hi = t + sp.lp_rad + p.pad2;
     const int64_t flo = lo > 0 ? lo / kStrictBlk : 0, fhi = (hi < n - 1 ? hi : n - 1) / kStrictBlk;
     double xw = fmax(xb[0], xb[nbs - 1]);
     for (int64_t fb = flo; fb <= fhi; ++fb) xw = fmax(xw, xb[fb]);
-    const double e = (1.0 + 0x1p-30) * __builtin_fma(sp.lpc[kk], xw, tailc);
+    const double e = (1.0 + 0x1p-30) * (__builtin_fma(sp.lpc[kk], xw, t0) * (1.0 + 0x1p-50) + t1);
     eo[kk] = ok ? e : __builtin_inf();
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -565,14 +575,6 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e(PskParams p, PskS
   }
 }
 
-// KS5: one thread per (stream, 32-bit word): the differential products of the
-// word's symbols in numpy's fma form, the reference's decision (qpsk_dibit /
-// real < 0, as K4a), and the margin: a symbol's error <= E, so |d error|_2
-// <= E (|s0|_2 + |s1|_2 + E), times sqrt2 for QPSK's L1 use (+ forming d's own
-// rounding; |s|_2 from above, norm2_up -- round 6; before it |s|_1 and the
-// sqrt2 for BPSK too, up to 2x wider);
-// a decision closer than that to its boundary -- QPSK's diagonals
-// ||di| - |dr|| (K4a's 2^-29 sliver on top), BPSK's dr = 0 -- flags the stream
 // an upper bound on |s|_2 = hypot(re, im): the rounded sqrt of the rounded
 // sum of squares is within 4u of it, so x (1 + 2^-50) covers it; |s|_1 (a1,
 // always an upper bound) where the squares could underflow or it is smaller
@@ -581,6 +583,15 @@ __device__ __forceinline__ double norm2_up(double re, double im, double a1) {
   const double r = sqrt(__builtin_fma(re, re, im * im)) * (1.0 + 0x1p-50);
   return r < a1 ? r : a1;
 }
+
+// KS5: one thread per (stream, 32-bit word): the differential products of the
+// word's symbols in numpy's fma form, the reference's decision (qpsk_dibit /
+// real < 0, as K4a), and the margin: a symbol's error <= E, so |d error|_2
+// <= E (|s0|_2 + |s1|_2 + E), times sqrt2 for QPSK's L1 use (+ forming d's own
+// rounding; |s|_2 from above, norm2_up -- round 6; before it |s|_1 and the
+// sqrt2 for BPSK too, up to 2x wider);
+// a decision closer than that to its boundary -- QPSK's diagonals
+// ||di| - |dr|| (K4a's 2^-29 sliver on top), BPSK's dr = 0 -- flags the stream
 __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p, PskSplit sp) {
   const int64_t s = blockIdx.y;
   const int64_t w = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -594,11 +605,11 @@ __global__ __launch_bounds__(64) void k_split_slice(PskBuffers buf, PskParams p,
   const double E = sp.kappa * peak;
   // tiny / huge / non-finite input: every decision goes the serial way
   bool flag = !(peak >= 0x1p-400 && peak <= 0x1p400);
-  // STRICT: |symbol error|_2 <= sqrt2 e(k), both components within e(k) (KB;
-  // inf when the stream's caps failed); else kappa * peak for every symbol
+  // STRICT: |symbol error|_2 <= e(k) (KB4; inf when the stream's caps failed);
+  // else kappa * peak for every symbol
   const double sq2 = 0x1.6a09e667f3bcdp+0;
   const double* eo = sp.strict ? sp.sc + s * sp.sstride + strict_off_e(sp) : nullptr;
-  auto esym = [&](int64_t k) { return sq2 * eo[k]; };
+  auto esym = [&](int64_t k) { return eo[k]; };
   const double* __restrict__ sy = sp.sym + (size_t)s * S * 2;
   uint32_t word = 0;
   double br = sy[2 * k0], bi0 = sy[2 * k0 + 1];

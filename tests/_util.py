@@ -137,8 +137,8 @@ def strict_pass_bounds(st, d, peak1, n, L, pad1):
 
 
 def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
-    """The strict mode's per-symbol bound e(k) on each symbol component's
-    |split - reference| (psk_split_kernels.hip KB, restated in numpy) from a
+    """The strict mode's per-symbol bound e(k) on |split - reference| of the
+    complex symbol (psk_split_kernels.hip KB, restated in numpy) from a
     stream's split statistics st (oracle.psk_split_stats / the device's) and
     the design d (_amr.split_strict_design); peak1 = pass1_peak(x).  Returns (e [S], (E1max, Fmax,
     Xmax, P3, ok))."""
@@ -162,5 +162,10 @@ def strict_symbol_bounds(st, d, peak1, n, first, sps, L, pad1=27, pad2=15):
     flo = np.where(lo > 0, lo // BS, 0)
     fhi = np.minimum(hi, n - 1) // BS
     xw = np.array([max(X[0], X[-1], X[a:b + 1].max()) for a, b in zip(flo, fhi)])
-    e = (1 + 2.0 ** -30) * (d["lpc"] * xw + (d["lp_tail"] * Xmax + d["c3"] * P3))
+    # the symbol's complex error: the band-pass error through the unit-modulus
+    # mixer and the real low-pass as one complex sum, sqrt2 on the
+    # per-component roundings (the mixer's rho, the low-pass's c3 P3)
+    rho = 2.0 ** -52 * 1.0078125 * fm
+    t1 = np.sqrt(2.0) * ((d["lpc"] + d["lp_tail"]) * rho + d["c3"] * P3)
+    e = (1 + 2.0 ** -30) * ((d["lpc"] * xw + d["lp_tail"] * Xmax) * (1 + 2.0 ** -50) + t1)
     return e, (E1max, Fmax, Xmax, P3, ok)
