@@ -1570,6 +1570,7 @@ int amr_fsk_split_bounds_host(amr_fsk_plan* plan, const void* x, int dtype, int6
     rc = ensure_split_conv(plan, sp, B);
   }
   if (!rc) rc = ensure_fsk_strict(plan, sp, B);
+  if (!rc && !sp.strict) rc = fail(AMR_E_INVALID, "no strict bound for this call's chunk (not a multiple of 16)");
   plan->strict_mode = saved;
   if (rc) return rc;
   HIP_TRY(launch_fsk_split(dtype, xs, n, B, plan->z, p, plan->f, sp, plan->stream));
