@@ -910,6 +910,7 @@ __global__ __launch_bounds__(kKfThreads) void k_fsk_strict_e1(FskSplit sp) {
   if (live) {
     double r = d.w_tail * k.D1m;
     const int64_t dn = J + 1 < d.nw ? J + 1 : d.nw;
+#pragma unroll 8
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(d.W[dl], d1[J - dl], r);
     const int64_t c = J / LB;
     const int64_t q = J - c * LB;
@@ -941,6 +942,7 @@ __global__ __launch_bounds__(kKfThreads) void k_fsk_strict_e2(FskParams p, FskSp
     if (K < 0 || K >= nb1) return 0.0;
     double r = d.w_tail * k.D2m;
     const int64_t dn = K + 1 < d.nw ? K + 1 : d.nw;
+#pragma unroll 8
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(d.W[dl], d2[K - dl], r);
     const int64_t c = K / LB;
     const int64_t q = K - c * LB;
@@ -952,12 +954,15 @@ __global__ __launch_bounds__(kKfThreads) void k_fsk_strict_e2(FskParams p, FskSp
   const bool live = J < nb1;
   if (live) {
     double a = d.k12_tail * k.D1m;
-    for (int64_t kq = 0; kq < d.nk; ++kq) {
-      const int64_t bb = J + kq - d.k12_off;
-      if (bb >= 0 && bb < nb1) a = __builtin_fma(d.K12[kq], d1[bb], a);
-    }
+    // the taps whose block lies inside the pass, in the same (ascending) order
+    const int64_t klo = d.k12_off - J > 0 ? d.k12_off - J : 0;
+    const int64_t khi = nb1 - J + d.k12_off < d.nk ? nb1 - J + d.k12_off : d.nk;
+#pragma unroll 8
+    for (int64_t kq = klo; kq < khi; ++kq) a = __builtin_fma(d.K12[kq], d1[J + kq - d.k12_off], a);
     double h = d.hs_tail * S1max;
-    for (int64_t db = 0; db < d.nh && J + db < nb1; ++db) h = __builtin_fma(d.HS[db], s1[J + db], h);
+    const int64_t hhi = nb1 - J < d.nh ? nb1 - J : d.nh;
+#pragma unroll 8
+    for (int64_t db = 0; db < hhi; ++db) h = __builtin_fma(d.HS[db], s1[J + db], h);
     const int64_t jhi = 16 * J + 15 < m1 - 1 ? 16 * J + 15 : m1 - 1;
     const int64_t k2lo = m1 - 1 - jhi, k2hi = m1 - 1 - 16 * J;
     const int64_t Ka = k2lo / kStrictBlk, Kb = k2hi / kStrictBlk;

@@ -460,6 +460,7 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e1(PskParams p, Psk
   if (live) {
     double r = sp.w_tail * k.D1m;
     const int64_t dn = J + 1 < sp.nw ? J + 1 : sp.nw;
+#pragma unroll 8
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d1[J - dl], r);
     const int64_t c = J / LB;
     const int64_t q = J - c * LB;
@@ -492,6 +493,7 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e2(PskParams p, Psk
     if (K < 0 || K >= nb1) return 0.0;
     double r = sp.w_tail * k.D2m;
     const int64_t dn = K + 1 < sp.nw ? K + 1 : sp.nw;
+#pragma unroll 8
     for (int64_t dl = 0; dl < dn; ++dl) r = __builtin_fma(sp.kW[dl], d2[K - dl], r);
     const int64_t c = K / LB;
     const int64_t q = K - c * LB;
@@ -504,12 +506,15 @@ __global__ __launch_bounds__(kKbThreads) void k_split_strict_e2(PskParams p, Psk
   if (live) {
     // forward block J: j in [16 J, 16 J + 15] <-> backward index k2 = m1 - 1 - j
     double a = sp.k12_tail * k.D1m;
-    for (int64_t kq = 0; kq < sp.nk; ++kq) {
-      const int64_t bb = J + kq - sp.k12_off;
-      if (bb >= 0 && bb < nb1) a = __builtin_fma(sp.kK12[kq], d1[bb], a);
-    }
+    // the taps whose block lies inside the pass, in the same (ascending) order
+    const int64_t klo = sp.k12_off - J > 0 ? sp.k12_off - J : 0;
+    const int64_t khi = nb1 - J + sp.k12_off < sp.nk ? nb1 - J + sp.k12_off : sp.nk;
+#pragma unroll 8
+    for (int64_t kq = klo; kq < khi; ++kq) a = __builtin_fma(sp.kK12[kq], d1[J + kq - sp.k12_off], a);
     double h = sp.hs_tail * S1max;
-    for (int64_t db = 0; db < sp.nh && J + db < nb1; ++db) h = __builtin_fma(sp.kHS[db], s1[J + db], h);
+    const int64_t hhi = nb1 - J < sp.nh ? nb1 - J : sp.nh;
+#pragma unroll 8
+    for (int64_t db = 0; db < hhi; ++db) h = __builtin_fma(sp.kHS[db], s1[J + db], h);
     const int64_t jhi = 16 * J + 15 < m1 - 1 ? 16 * J + 15 : m1 - 1;
     const int64_t k2lo = m1 - 1 - jhi, k2hi = m1 - 1 - 16 * J;
     const int64_t Ka = k2lo / kStrictBlk, Kb = k2hi / kStrictBlk;
