@@ -121,6 +121,7 @@ __device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab
   for (int64_t m0 = lane; m0 < M; m0 += 64 * U) {
     double v[U];
     V2 k[U][NS / 2];
+    [[maybe_unused]] double ka[U];      // ST: kabs, loaded with the rest (not behind the FMAs)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t m = m0 + 64 * u < M ? m0 + 64 * u : M - 1;   // clamped: loaded, not used
@@ -128,6 +129,7 @@ __device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab
       const V2* kp = reinterpret_cast<const V2*>(ktab + m * NS);
 #pragma unroll
       for (int h = 0; h < NS / 2; ++h) k[u][h] = kp[h];
+      if constexpr (ST) ka[u] = cb.kabs[m];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -137,7 +139,7 @@ __device__ __forceinline__ void split_conv_state(const double* __restrict__ ktab
           acc[2 * h] = __builtin_fma(k[u][h][0], v[u], acc[2 * h]);
           acc[2 * h + 1] = __builtin_fma(k[u][h][1], v[u], acc[2 * h + 1]);
         }
-        if constexpr (ST) sa = __builtin_fma(cb.kabs[m0 + 64 * u], fabs(v[u]), sa);
+        if constexpr (ST) sa = __builtin_fma(ka[u], fabs(v[u]), sa);
       }
     }
   }
